@@ -1,0 +1,170 @@
+/*
+ * zarrhip.h — C ABI of the MI355X-native zarr v3 codec-pipeline kernels.
+ *
+ * This is the drop-in boundary below zarr-python's CodecPipeline interface
+ * (src/zarr/abc/codec.py:315-508 in the reference).  A host planner (the
+ * Python package zarr_hip, mirroring CodecPipeline.read/write) turns a batch of
+ * (ByteGetter, ArraySpec, chunk_selection, out_selection, is_complete) tuples
+ * into the flat tables below and calls these entry points through ctypes.  No
+ * torch or C++ types cross the boundary: plain pointers, sizes, POD structs.
+ *
+ * Entry points and the reference interface each one replaces:
+ *
+ *   zhip_decode       FusedCodecPipeline.read_sync's per-chunk body
+ *                     (src/zarr/core/codec_pipeline.py:1095-1172):
+ *                       Crc32cCodec._decode_sync   (src/zarr/codecs/crc32c_.py:34-50)
+ *                       BytesCodec._decode_sync    (src/zarr/codecs/bytes.py:97-131)
+ *                       TransposeCodec._decode_sync(src/zarr/codecs/transpose.py:98-104)
+ *                       decode_and_scatter_chunk / scatter_chunk
+ *                                                  (src/zarr/core/chunk_utils.py:88-214)
+ *                     and, for sharded batches, the sub-chunk extraction of
+ *                       ShardingCodec._decode_partial_sync (src/zarr/codecs/sharding.py:1222-1309)
+ *                       _ShardIndex.get_chunk_slice        (sharding.py:248-254)
+ *                     With ZHIP_LF_NO_WRITE the same entry point is the
+ *                     shard-index CRC check of _decode_shard_index_sync
+ *                     (sharding.py:624-631) run over many shards at once.
+ *   zhip_encode       ChunkTransform.encode_chunk for fixed-size chains
+ *                     (chunk_utils.py:335-363): transpose/bytes/crc32c _encode_sync
+ *                     (transpose.py:113-118, bytes.py:140-158, crc32c_.py:59-68) plus
+ *                     chunk_is_empty (chunk_utils.py:74-85, buffer/core.py:534-558).
+ *   zhip_shard_pack   ShardingCodec._build_shard_layout / _assemble_shard /
+ *                     _encode_shard_index_sync (sharding.py:887-950, 633-640).
+ *   zhip_plan_*       host-side constant tables (no reference counterpart:
+ *                     the CRC-combine operators the GPU kernels need).
+ *
+ * Error model: every function returns 0 on success or a negative ZHIP_E_*
+ * code; zhip_last_error() gives a message.  Per-chunk outcomes are written to
+ * device-resident zhip_status records; the host raises the reference's
+ * exceptions (ValueError "Stored and computed checksum do not match ...") after
+ * the batch completes.  No exception crosses the ABI.
+ */
+#ifndef ZARRHIP_H
+#define ZARRHIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ZHIP_ABI_VERSION 1
+#define ZHIP_MAX_DIMS 8
+
+/* return codes */
+#define ZHIP_OK 0
+#define ZHIP_E_INVALID -1
+#define ZHIP_E_HIP -2
+#define ZHIP_E_UNSUPPORTED -3
+
+/* per-chunk status codes (zhip_status.code) */
+#define ZHIP_ST_OK 0u
+#define ZHIP_ST_MISSING 1u            /* chunk absent: fill value scattered  */
+#define ZHIP_ST_CRC_MISMATCH 2u       /* Crc32cCodec._decode_sync ValueError */
+#define ZHIP_ST_INDEX_OOB 3u          /* shard index entry outside the blob  */
+#define ZHIP_ST_LENGTH_MISMATCH 4u    /* encoded length != fixed-size chain  */
+
+/* layout flags (zhip_layout.flags) */
+#define ZHIP_LF_CRC 1u            /* chain ends in crc32c (4-byte LE trailer)        */
+#define ZHIP_LF_SWAP 2u           /* stored endian != native: byteswap items        */
+#define ZHIP_LF_SHARDED 4u        /* chunk source = inner chunk of a shard blob     */
+#define ZHIP_LF_INDEX_START 8u    /* sharding index_location == "start"             */
+#define ZHIP_LF_NO_WRITE 16u      /* verify only (shard index CRC)                  */
+
+/* chunk flags (zhip_chunk.flags) */
+#define ZHIP_CF_MISSING 1u        /* store returned None: scatter fill value        */
+
+typedef struct zhip_fdiv {  /* n / d == (n * m) >> s  for 0 <= n < 2^31 */
+    uint32_t m;
+    uint32_t s;
+} zhip_fdiv;
+
+/* Geometry shared by every chunk of one launch (one array, one codec chain).
+ * All per-dimension arrays are in STORED (encoded) dimension order: stored
+ * dim i is decoded dim order[i] of the transpose codec (transpose.py:89-96),
+ * so out_stride[i] is the out byte-stride of decoded dim order[i]. */
+typedef struct zhip_layout {
+    int32_t ndim;
+    int32_t itemsize;                  /* 1, 2, 4 or 8 */
+    int32_t shape[ZHIP_MAX_DIMS];      /* stored chunk shape (inner chunk if sharded) */
+    int64_t out_stride[ZHIP_MAX_DIMS]; /* bytes; arbitrary (F order, views, drops)   */
+    uint64_t nbytes;                   /* decoded bytes per chunk = prod(shape)*item */
+    uint32_t flags;                    /* ZHIP_LF_*                                   */
+    uint32_t n_inner;                  /* sharded: inner chunks per shard             */
+    uint32_t index_size;               /* sharded: encoded index bytes (16n [+4])     */
+    uint32_t _pad;
+    uint8_t fill[16];                  /* fill value bytes, native order              */
+} zhip_layout;
+
+/* One chunk (decode unit) of a batch. */
+typedef struct zhip_chunk {
+    uint64_t src;      /* byte offset in src: encoded chunk | shard blob (SHARDED) */
+    uint64_t src_len;  /* encoded chunk length | shard blob length                 */
+    int64_t out_off;   /* byte offset in out of the selection's first element      */
+    uint32_t flags;    /* ZHIP_CF_*                                                */
+    uint32_t slot;     /* SHARDED: C-order index of the inner chunk in its shard   */
+    uint32_t sel;      /* index into the selection table                           */
+    uint32_t _pad[3];
+} zhip_chunk;
+
+/* Per-chunk selection (chunk_selection of a ChunkProjection), stored dim order:
+ * element s of dim i is selected iff s = start + k*step, 0 <= k < count; it
+ * lands at out_off + sum_i k_i * out_stride[i]. */
+typedef struct zhip_sel {
+    int32_t start[ZHIP_MAX_DIMS];
+    int32_t count[ZHIP_MAX_DIMS];
+    int32_t step[ZHIP_MAX_DIMS];
+    zhip_fdiv div_step[ZHIP_MAX_DIMS];
+} zhip_sel;
+
+/* Per-chunk outcome, written by the device. */
+typedef struct zhip_status {
+    uint32_t code;     /* ZHIP_ST_* */
+    uint32_t stored;   /* stored CRC (LE trailer), when ZHIP_LF_CRC              */
+    uint32_t computed; /* CRC-32C computed on the device, when ZHIP_LF_CRC       */
+    uint32_t aux;
+} zhip_status;
+
+typedef struct zhip_plan zhip_plan;
+
+int zhip_abi_version(void);
+const char *zhip_last_error(void);
+int zhip_device_count(void);
+
+/* Build the constant tables for one layout (host math + one upload to the
+ * current device).  Not for the timed path: cache the plan per array. */
+int zhip_plan_create(const zhip_layout *layout, zhip_plan **plan);
+int zhip_plan_destroy(zhip_plan *plan);
+/* Units (workgroup work items) per chunk and workspace words per chunk. */
+int zhip_plan_info(const zhip_plan *plan, uint32_t *units_per_chunk, uint32_t *workspace_words);
+
+/* decode flags (zhip_decode decode_flags) */
+#define ZHIP_DF_FAST_ROWS 1u  /* every chunk selects whole innermost rows that are
+                                 contiguous in out, 16-byte multiples and 16-byte
+                                 aligned: one 16-byte store per 16 input bytes */
+
+/* Upload the plan's constant tables to the current HIP device (once). */
+int zhip_plan_upload(zhip_plan *plan);
+
+/* Decode `n_chunks` chunks of `src` (device) into `out` (device).
+ * src must stay readable for 64 bytes past src_size (loads are 16-byte wide).
+ * d_chunks/d_sels/d_status/d_workspace/d_errflag are device pointers;
+ * d_workspace holds 2*n_chunks zeroed uint32 words (self-resetting: keep it
+ * for the next call).  *d_errflag gets the OR of (1 << status code) over all
+ * chunks whose status is an error (not OK, not MISSING).  `stream` is a
+ * hipStream_t (NULL = default stream).  Asynchronous.  With ZHIP_LF_NO_WRITE
+ * (shard-index CRC verification, itemsize 1) `out` may be NULL. */
+int zhip_decode(const zhip_plan *plan, const void *src, uint64_t src_size, void *out,
+                const zhip_chunk *d_chunks, uint32_t n_chunks, const zhip_sel *d_sels,
+                zhip_status *d_status, uint32_t *d_workspace, uint32_t *d_errflag,
+                uint32_t decode_flags, void *stream);
+
+/* CPU-only test hooks (no GPU needed). */
+int zhip_selftest(void);                                  /* 0 = all identities hold */
+uint32_t zhip_emulate_chunk_crc(const zhip_plan *plan, const uint8_t *data);
+uint32_t zhip_fdiv_eval(uint32_t n, uint32_t d);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ZARRHIP_H */

@@ -1,0 +1,24 @@
+#!/bin/bash
+# One GPU-box session: tests, smoke, short bench, rocprof kernel stats.
+# Stops at the first crash/timeout (exit codes other than 0/1 from pytest).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+STEPS=${STEPS:-50}
+timeout -k 10 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
+rc=$?
+echo "pytest_gpu rc=$rc"; tail -5 gpurun_out/pytest_gpu.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after pytest rc=$rc"; exit $rc; fi
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+rc=$?; echo "smoke rc=$rc"; tail -3 gpurun_out/smoke.log
+if [ $rc -ne 0 ]; then exit $rc; fi
+timeout -k 10 600 python bench.py --steps "$STEPS" --warmup 10 > gpurun_out/bench.json 2> gpurun_out/bench.err
+rc=$?; echo "bench rc=$rc"; cat gpurun_out/bench.json; tail -3 gpurun_out/bench.err
+if [ $rc -ne 0 ]; then exit $rc; fi
+if [ "${PROFILE:-1}" = "1" ]; then
+  cd /tmp && export TMPDIR=/tmp
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run --output-format csv -- python "$GRAFT_REPO_ROOT/bench.py" --steps "$STEPS" --warmup 10 --no-cpu-baseline > "$GRAFT_REPO_ROOT/gpurun_out/bench_prof.json" 2> "$GRAFT_REPO_ROOT/gpurun_out/bench_prof.err"
+  rc=$?; echo "rocprof rc=$rc"
+  find "$GRAFT_REPO_ROOT/gpurun_out/prof" -name "*stats*" | head
+fi
+exit $rc

@@ -1,0 +1,193 @@
+"""GPU parity: zarr_hip decode (HIP kernels through the C ABI) vs the CPU oracle,
+bit-exact (compared as raw bytes so NaN payloads and -0.0 count).
+
+Encoded inputs are produced by the oracle (oracle/oracle.py, test infrastructure)
+from seeded data; the decode under test runs only on the GPU."""
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+LE = {"name": "bytes", "configuration": {"endian": "little"}}
+BE = {"name": "bytes", "configuration": {"endian": "big"}}
+CRC = {"name": "crc32c"}
+
+
+def T(order):
+    return {"name": "transpose", "configuration": {"order": list(order)}}
+
+
+def SHARD(inner_shape, codecs, loc="end", index=(LE, CRC)):
+    return {"name": "sharding_indexed", "configuration": {
+        "chunk_shape": list(inner_shape), "codecs": list(codecs), "index_codecs": list(index),
+        "index_location": loc}}
+
+
+def _data(shape, dtype, seed=0):
+    rng = np.random.default_rng(seed)
+    dt = np.dtype(dtype)
+    if dt.kind == "f":
+        a = rng.standard_normal(shape).astype(dt)
+        flat = a.reshape(-1)
+        if flat.size > 8:
+            flat[3] = -0.0
+            if dt.itemsize == 4:
+                flat[5:6].view(np.uint32)[0] = 0x7FC00001  # NaN payload
+            else:
+                flat[5] = np.nan
+        return a
+    info = np.iinfo(dt)
+    return rng.integers(info.min, info.max, size=shape, dtype=dt, endpoint=True)
+
+
+def _roundtrip(device, shape, chunks, dtype, codecs, fill=0, selection=(Ellipsis,), drop=None,
+               order="C", seed=0, host_store=False):
+    import zarr_hip
+    from zarr_hip.spec import ArrayConfig
+
+    meta = O.ArrayMeta(tuple(shape), tuple(chunks), np.dtype(dtype), fill, codecs=codecs)
+    host = {}
+    data = _data(shape, dtype, seed)
+    O.write(host, meta, (Ellipsis,), data)
+    for k in drop or []:
+        host.pop(k, None)
+    store = zarr_hip.MemoryStore(dict(host)) if host_store else zarr_hip.DeviceStore.from_host(
+        host, device)
+    arr = zarr_hip.Array.create(store, shape, chunks, dtype, fill, codecs=codecs,
+                                config=ArrayConfig(order=order))
+    got = arr[selection]
+    want = O.read(host, meta, selection)
+    assert got.shape == want.shape
+    assert got.tobytes() == np.ascontiguousarray(want).tobytes()
+    return arr, host, meta
+
+
+@pytest.mark.parametrize("dtype", ["float32", "int16", "uint8", "float64", "int32"])
+def test_bytes_crc_full(device, dtype):
+    _roundtrip(device, (40, 33, 20), (16, 16, 8), dtype, [LE, CRC])
+
+
+def test_c2_shape(device):
+    _roundtrip(device, (128, 128, 128), (64, 64, 64), "float32", [LE, CRC])
+
+
+@pytest.mark.parametrize("dtype", ["float32", "int16", "float64", "uint16"])
+def test_big_endian(device, dtype):
+    _roundtrip(device, (21, 34), (8, 16), dtype, [BE, CRC])
+
+
+def test_bytes_only_no_crc(device):
+    _roundtrip(device, (1000,), (128,), "float32", [LE])
+
+
+@pytest.mark.parametrize("order", [(2, 1, 0), (1, 2, 0), (0, 2, 1), (2, 0, 1)])
+def test_transpose(device, order):
+    _roundtrip(device, (10, 20, 30), (5, 10, 15), "float32", [T(order), LE, CRC], fill=np.nan)
+
+
+def test_transpose_c3_shape(device):
+    _roundtrip(device, (128, 64, 64), (64, 64, 64), "float32", [T((2, 1, 0)), LE, CRC])
+
+
+@pytest.mark.parametrize("sel", [(slice(3, 17), slice(None, None, 3)), (5, slice(2, 30, 7)),
+                                 (slice(1, 40, 13), 0), (-1, -2), (slice(None), slice(9, 10)),
+                                 (slice(7, 8), slice(0, 29))])
+def test_partial_selections(device, sel):
+    _roundtrip(device, (37, 29), (8, 10), "float32", [LE, CRC], selection=sel)
+
+
+def test_missing_chunks_fill(device):
+    _roundtrip(device, (32, 32), (8, 8), "float32", [LE, CRC], fill=-7.5,
+               drop=["c/0/0", "c/2/3", "c/3/3"])
+
+
+def test_f_order_out(device):
+    _roundtrip(device, (24, 20, 12), (8, 8, 8), "float32", [LE, CRC], order="F")
+
+
+def test_host_store_staging(device):
+    _roundtrip(device, (40, 40), (16, 16), "int16", [LE, CRC], host_store=True)
+
+
+def test_crc_mismatch_raises_reference_message(device):
+    import zarr_hip
+
+    meta = O.ArrayMeta((16, 16), (8, 8), np.dtype("float32"), 0.0, codecs=[LE, CRC])
+    host = {}
+    O.write(host, meta, (Ellipsis,), _data((16, 16), "float32"))
+    bad = bytearray(host["c/1/0"])
+    bad[10] ^= 0x40
+    host["c/1/0"] = bytes(bad)
+    with pytest.raises(ValueError) as want:
+        O.read(host, meta)
+    store = zarr_hip.DeviceStore.from_host(host, device)
+    arr = zarr_hip.Array.create(store, (16, 16), (8, 8), "float32", 0.0, codecs=[LE, CRC])
+    with pytest.raises(ValueError) as got:
+        arr[...]
+    assert str(got.value) == str(want.value)
+
+
+# ------------------------------------------------------------------ sharding
+
+@pytest.mark.parametrize("loc", ["end", "start"])
+@pytest.mark.parametrize("inner", [[LE, CRC], [LE], [T((1, 0, 2)), LE, CRC]])
+def test_sharded(device, loc, inner):
+    _roundtrip(device, (32, 32, 32), (16, 16, 16), "float32", [SHARD((8, 8, 8), inner, loc)])
+
+
+def test_sharded_partial_and_missing_inner(device):
+    # fill-valued inner chunks are elided at write time -> missing inner -> fill
+    import zarr_hip
+
+    codecs = [SHARD((4, 4), [LE, CRC])]
+    meta = O.ArrayMeta((16, 24), (8, 8), np.dtype("int16"), -1, codecs=codecs)
+    data = _data((16, 24), "int16")
+    data[0:4, 4:8] = -1
+    data[8:16, 16:24] = -1  # a whole shard of fill -> shard key absent
+    host = {}
+    O.write(host, meta, (Ellipsis,), data)
+    assert "c/1/2" not in host
+    store = zarr_hip.DeviceStore.from_host(host, device)
+    arr = zarr_hip.Array.create(store, (16, 24), (8, 8), "int16", -1, codecs=codecs)
+    for sel in [(Ellipsis,), (slice(3, 13), slice(2, 23, 3)), (7, slice(None)), (slice(9, 10), 20)]:
+        got = arr[sel]
+        want = O.read(host, meta, sel)
+        assert got.tobytes() == np.ascontiguousarray(want).tobytes()
+
+
+def test_sharded_index_crc_mismatch(device):
+    import zarr_hip
+
+    codecs = [SHARD((4, 4), [LE])]
+    meta = O.ArrayMeta((8, 8), (8, 8), np.dtype("float32"), 0.0, codecs=codecs)
+    host = {}
+    O.write(host, meta, (Ellipsis,), _data((8, 8), "float32"))
+    bad = bytearray(host["c/0/0"])
+    bad[-10] ^= 1  # inside the index
+    host["c/0/0"] = bytes(bad)
+    with pytest.raises(ValueError) as want:
+        O.read(host, meta)
+    store = zarr_hip.DeviceStore.from_host(host, device)
+    arr = zarr_hip.Array.create(store, (8, 8), (8, 8), "float32", 0.0, codecs=codecs)
+    with pytest.raises(ValueError) as got:
+        arr[...]
+    assert str(got.value) == str(want.value)
+
+
+def test_sharded_c4_like(device):
+    # C4 geometry scaled down: 128^3 f32, 64^3 shards of 16^3 inner, crc
+    _roundtrip(device, (128, 128, 128), (64, 64, 64), "float32", [SHARD((16, 16, 16), [LE, CRC])])
+
+
+def test_program_relaunch_is_idempotent(device):
+    arr, host, meta = _roundtrip(device, (64, 64, 64), (32, 32, 32), "float32", [LE, CRC])
+    prog, out = arr.prepare_read((Ellipsis,))
+    for _ in range(3):
+        prog.launch()
+    prog.results()
+    from zarr_hip.buffer import to_numpy
+
+    assert to_numpy(out, "float32").tobytes() == O.read(host, meta).tobytes()

@@ -1,0 +1,328 @@
+// C ABI of zarr_hip (include/zarrhip.h): plan building (host GF(2) math, one
+// upload), launches, error reporting, and CPU self-tests of the CRC-combine
+// algebra the kernels rely on.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/zarrhip.h"
+#include "zhip_gf2.h"
+#include "zhip_internal.h"
+
+using namespace zhip;
+
+namespace {
+
+thread_local std::string g_err;
+
+int set_err(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                     \
+    do {                                                                                  \
+        hipError_t e_ = (expr);                                                           \
+        if (e_ != hipSuccess)                                                             \
+            return set_err(ZHIP_E_HIP, std::string(#expr ": ") + hipGetErrorString(e_));  \
+    } while (0)
+
+uint32_t g_T[256];      // standard byte table: A_1(v) = (v >> 8) ^ T[v & 255]
+uint8_t g_invtop[256];  // top byte of T[i] -> i
+std::once_flag g_once;
+
+void init_tables() {
+    for (uint32_t i = 0; i < 256; ++i) {
+        uint32_t c = i;
+        for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (kPoly & (0u - (c & 1u)));
+        g_T[i] = c;
+    }
+    for (uint32_t i = 0; i < 256; ++i) g_invtop[g_T[i] >> 24] = (uint8_t)i;
+}
+
+// x^(8n) mod P
+uint32_t xpow8(uint64_t n) {
+    uint32_t p = kOne;
+    uint32_t b = kOne >> 8;  // x^8
+    while (n) {
+        if (n & 1) p = gf_mul(p, b);
+        b = gf_mul(b, b);
+        n >>= 1;
+    }
+    return p;
+}
+
+// x^(-8n) mod P: n inverse byte-steps applied to 1.
+uint32_t xpow8_inv(uint64_t n) {
+    uint32_t s = kOne;
+    for (uint64_t k = 0; k < n; ++k) {
+        const uint32_t i = g_invtop[s >> 24];
+        s = (((s ^ g_T[i]) & 0x00FFFFFFu) << 8) | i;
+    }
+    return s;
+}
+
+zhip_fdiv make_fdiv(uint32_t d) {
+    zhip_fdiv f;
+    uint32_t l = 0;
+    while ((1ull << l) < d) ++l;
+    f.s = 31 + l;
+    f.m = (uint32_t)(((1ull << (31 + l)) + d - 1) / d);  // ceil(2^(31+l)/d) <= 2^32-1 for d>=1... (d=1 -> 2^31)
+    return f;
+}
+
+uint32_t crc_bytewise(const uint8_t* p, size_t n) {
+    uint32_t c = 0xFFFFFFFFu;
+    for (size_t i = 0; i < n; ++i) c = (c >> 8) ^ g_T[(c ^ p[i]) & 255u];
+    return ~c;
+}
+
+void build_horner(uint32_t* tab) {  // [op][slice][256], op k = A_(4096 - 4k)
+    for (int op = 0; op < 4; ++op) {
+        const uint32_t x = xpow8((uint64_t)kWgStride - 4u * op);
+        for (int sl = 0; sl < 4; ++sl)
+            for (uint32_t b = 0; b < 256; ++b) tab[op * 1024 + sl * 256 + b] = gf_mul(x, b << (8 * sl));
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int zhip_abi_version(void) { return ZHIP_ABI_VERSION; }
+
+const char* zhip_last_error(void) { return g_err.c_str(); }
+
+int zhip_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int zhip_plan_create(const zhip_layout* layout, zhip_plan** out) {
+    std::call_once(g_once, init_tables);
+    if (!layout || !out) return set_err(ZHIP_E_INVALID, "null argument");
+    const zhip_layout& L = *layout;
+    if (L.ndim < 1 || L.ndim > ZHIP_MAX_DIMS) return set_err(ZHIP_E_UNSUPPORTED, "ndim must be 1..8");
+    if (!(L.itemsize == 1 || L.itemsize == 2 || L.itemsize == 4 || L.itemsize == 8))
+        return set_err(ZHIP_E_UNSUPPORTED, "itemsize must be 1, 2, 4 or 8");
+    uint64_t n = (uint64_t)L.itemsize;
+    for (int d = 0; d < L.ndim; ++d) {
+        if (L.shape[d] < 0) return set_err(ZHIP_E_INVALID, "negative shape");
+        n *= (uint64_t)L.shape[d];
+    }
+    if (n != L.nbytes) return set_err(ZHIP_E_INVALID, "nbytes != prod(shape)*itemsize");
+    if (n >= (1ull << 31) - 8192) return set_err(ZHIP_E_UNSUPPORTED, "chunk payload must be < 2 GiB");
+    zhip_plan* p = new (std::nothrow) zhip_plan();
+    if (!p) return set_err(ZHIP_E_INVALID, "out of memory");
+    p->layout = L;
+    p->E = (uint32_t)((n + 15) & ~15ull);
+    p->nseg = p->E == 0 ? 1u : (p->E + kSeg - 1) / kSeg;
+    p->R = (uint64_t)p->E + kWgStride;
+    p->c_inv = xpow8_inv(p->R - n);
+    p->c3 = gf_mul(xpow8(n), 0xFFFFFFFFu);
+    for (int d = 0; d < ZHIP_MAX_DIMS; ++d) p->dshape[d] = make_fdiv(d < L.ndim && L.shape[d] > 0 ? (uint32_t)L.shape[d] : 1u);
+    p->row_bytes = (uint32_t)L.shape[L.ndim - 1] * (uint32_t)L.itemsize;
+    p->drow = make_fdiv(p->row_bytes ? p->row_bytes : 1u);
+    // fill pattern replicated to 16 bytes
+    uint8_t f16[16];
+    for (int i = 0; i < 16; ++i) f16[i] = L.fill[i % L.itemsize];
+    std::memcpy(p->fill, f16, 16);
+    p->device = -1;
+    p->max_grid = 2048;
+    p->d_tables = nullptr;
+    *out = p;
+    return ZHIP_OK;
+}
+
+// Upload the constant tables to the current device (done once per plan).
+int zhip_plan_upload(zhip_plan* p) {
+    if (!p) return set_err(ZHIP_E_INVALID, "null plan");
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    if (p->d_tables && p->device == dev) return ZHIP_OK;
+    std::vector<uint32_t> h(4096 + kThreads + p->nseg);
+    build_horner(h.data());
+    for (int t = 0; t < kThreads; ++t) h[4096 + t] = xpow8((uint64_t)kWgStride - 16u * t);
+    for (uint32_t s = 0; s < p->nseg; ++s) h[4096 + kThreads + s] = xpow8((uint64_t)s * kSeg);
+    if (p->d_tables) (void)hipFree(p->d_tables);
+    p->d_tables = nullptr;
+    HIP_TRY(hipMalloc(&p->d_tables, h.size() * sizeof(uint32_t)));
+    HIP_TRY(hipMemcpy(p->d_tables, h.data(), h.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0)
+        p->max_grid = prop.multiProcessorCount * 8;
+    p->device = dev;
+    return ZHIP_OK;
+}
+
+int zhip_plan_destroy(zhip_plan* p) {
+    if (!p) return ZHIP_OK;
+    if (p->d_tables) (void)hipFree(p->d_tables);
+    delete p;
+    return ZHIP_OK;
+}
+
+int zhip_plan_info(const zhip_plan* p, uint32_t* units_per_chunk, uint32_t* workspace_words) {
+    if (!p) return set_err(ZHIP_E_INVALID, "null plan");
+    if (units_per_chunk) *units_per_chunk = p->nseg;
+    if (workspace_words) *workspace_words = 2;
+    return ZHIP_OK;
+}
+
+int zhip_decode(const zhip_plan* plan, const void* src, uint64_t src_size, void* out,
+                const zhip_chunk* d_chunks, uint32_t n_chunks, const zhip_sel* d_sels,
+                zhip_status* d_status, uint32_t* d_workspace, uint32_t* d_errflag, uint32_t decode_flags,
+                void* stream) {
+    if (!plan) return set_err(ZHIP_E_INVALID, "null plan");
+    if (!plan->d_tables) return set_err(ZHIP_E_INVALID, "plan not uploaded (zhip_plan_upload)");
+    if (n_chunks == 0) return ZHIP_OK;
+    if (!src || !d_chunks || !d_sels || !d_status || !d_workspace || !d_errflag)
+        return set_err(ZHIP_E_INVALID, "null device pointer");
+    const zhip_layout& L = plan->layout;
+    if (!(L.flags & ZHIP_LF_NO_WRITE) && !out) return set_err(ZHIP_E_INVALID, "null out");
+    const uint64_t units = (uint64_t)n_chunks * plan->nseg;
+    if (units >= (1ull << 32)) return set_err(ZHIP_E_UNSUPPORTED, "too many units in one batch");
+    DecodeParams p{};
+    p.src = static_cast<const uint8_t*>(src);
+    p.src_size = src_size;
+    p.out = static_cast<uint8_t*>(out);
+    p.chunks = d_chunks;
+    p.sels = d_sels;
+    p.status = d_status;
+    p.ws = d_workspace;
+    p.errflag = d_errflag;
+    p.horner = plan->d_tables;
+    p.kthread = plan->d_tables + 4096;
+    p.kunit = plan->d_tables + 4096 + kThreads;
+    p.n_chunks = n_chunks;
+    p.nseg = plan->nseg;
+    p.n_units = (uint32_t)units;
+    p.c_inv = plan->c_inv;
+    p.c3 = plan->c3;
+    p.lflags = L.flags;
+    p.ndim = L.ndim;
+    p.itemsize = L.itemsize;
+    for (int d = 0; d < ZHIP_MAX_DIMS; ++d) {
+        p.shape[d] = d < L.ndim ? L.shape[d] : 1;
+        p.ostride[d] = d < L.ndim ? L.out_stride[d] : 0;
+        p.dshape[d] = plan->dshape[d];
+    }
+    p.nbytes = (uint32_t)L.nbytes;
+    p.E = plan->E;
+    p.row_bytes = plan->row_bytes;
+    p.drow = plan->drow;
+    p.index_size = L.index_size;
+    p.n_inner = L.n_inner;
+    std::memcpy(p.fill, plan->fill, sizeof(p.fill));
+    p.fast = (decode_flags & ZHIP_DF_FAST_ROWS) ? 1u : 0u;
+    int rc = launch_decode(p, static_cast<hipStream_t>(stream), plan->max_grid);
+    if (rc == ZHIP_E_UNSUPPORTED) return set_err(rc, "no kernel for this layout");
+    if (rc != ZHIP_OK) return set_err(rc, std::string("launch failed: ") + hipGetErrorString(hipGetLastError()));
+    return ZHIP_OK;
+}
+
+uint32_t zhip_fdiv_eval(uint32_t n, uint32_t d) {
+    const zhip_fdiv f = make_fdiv(d);
+    return fdiv_apply(n, f.m, f.s);
+}
+
+// CPU emulation of the device CRC combine for one chunk of a plan (the exact
+// decomposition, tables and constants the kernel uses).  Test hook: lets the
+// CPU suite prove the algebra without a GPU.
+uint32_t zhip_emulate_chunk_crc(const zhip_plan* plan, const uint8_t* data) {
+    std::call_once(g_once, init_tables);
+    std::vector<uint32_t> tab(4096);
+    build_horner(tab.data());
+    const uint32_t N = (uint32_t)plan->layout.nbytes;
+    uint32_t V = 0;
+    for (uint32_t s = 0; s < plan->nseg; ++s) {
+        const int32_t hi = (int32_t)plan->E - (int32_t)(s * (uint32_t)kSeg);
+        const int32_t lo = hi - kSeg;
+        uint32_t unit = 0;
+        for (int t = 0; t < kThreads; ++t) {
+            uint32_t acc = 0;
+            for (int k = 0; k < kBlocksPerThread; ++k) {
+                const int32_t o = lo + kWgStride * k + 16 * t;
+                uint8_t b[16] = {0};
+                for (int i = 0; i < 16; ++i) {
+                    const int64_t q = (int64_t)o + i;
+                    if (q >= 0 && q < (int64_t)N) b[i] = data[q];
+                }
+                uint32_t w[4];
+                std::memcpy(w, b, 16);
+                auto ap = [&](int op, uint32_t x) {
+                    const uint32_t* tb = tab.data() + op * 1024;
+                    return tb[x & 255u] ^ tb[256 + ((x >> 8) & 255u)] ^ tb[512 + ((x >> 16) & 255u)] ^
+                           tb[768 + (x >> 24)];
+                };
+                acc = ap(0, acc ^ w[0]) ^ ap(1, w[1]) ^ ap(2, w[2]) ^ ap(3, w[3]);
+            }
+            unit ^= gf_mul(acc, xpow8((uint64_t)kWgStride - 16u * t));
+        }
+        V ^= gf_mul(unit, xpow8((uint64_t)s * kSeg));
+    }
+    return ~(gf_mul(V, plan->c_inv) ^ plan->c3);
+}
+
+// CPU self-test of the identities the kernels rely on.  Returns 0 when all hold.
+int zhip_selftest(void) {
+    std::call_once(g_once, init_tables);
+    // 1. top byte of T[i] is a bijection (needed for the inverse byte step)
+    bool seen[256] = {false};
+    for (int i = 0; i < 256; ++i) seen[g_T[i] >> 24] = true;
+    for (int i = 0; i < 256; ++i)
+        if (!seen[i]) return set_err(1, "T top-byte map is not a bijection");
+    // 2. A_1(v) == gf_mul(v, x^8) and inverse round trip
+    uint32_t v = 0x12345678u;
+    for (int it = 0; it < 1000; ++it) {
+        v = v * 1664525u + 1013904223u;
+        const uint32_t a = (v >> 8) ^ g_T[v & 255u];
+        if (a != gf_mul(v, xpow8(1))) return set_err(2, "A_1 != multiply by x^8");
+        if (gf_mul(gf_mul(v, xpow8(777)), xpow8_inv(777)) != v) return set_err(3, "x^-8n inverse wrong");
+    }
+    // 3. crc of "123456789"
+    if (crc_bytewise((const uint8_t*)"123456789", 9) != 0xE3069283u) return set_err(4, "check value");
+    // 4. fast division
+    const uint32_t ds[] = {1, 2, 3, 5, 7, 10, 15, 60, 64, 100, 255, 256, 1000, 4096, 65537, 1000003u};
+    for (uint32_t d : ds) {
+        const zhip_fdiv f = make_fdiv(d);
+        uint32_t x = 1;
+        for (int it = 0; it < 20000; ++it) {
+            x = x * 1103515245u + 12345u;
+            const uint32_t n = (it < 1000) ? (uint32_t)it : (x & 0x7FFFFFFFu);
+            if (fdiv_apply(n, f.m, f.s) != n / d) return set_err(5, "fdiv wrong");
+        }
+        const uint32_t nmax = 0x7FFFFFFFu;
+        if (fdiv_apply(nmax, f.m, f.s) != nmax / d) return set_err(5, "fdiv wrong at 2^31-1");
+    }
+    // 5. kernel decomposition == bytewise CRC for several sizes
+    const uint64_t sizes[] = {0, 1, 3, 4, 15, 16, 17, 100, 4095, 4096, 4097, 32768, 32769, 100000, 262148};
+    std::vector<uint8_t> buf(262148);
+    uint32_t r = 7;
+    for (auto& b : buf) {
+        r = r * 1664525u + 1013904223u;
+        b = (uint8_t)(r >> 24);
+    }
+    for (uint64_t n : sizes) {
+        zhip_layout L{};
+        L.ndim = 1;
+        L.itemsize = 1;
+        L.shape[0] = (int32_t)n;
+        L.nbytes = n;
+        zhip_plan* p = nullptr;
+        if (zhip_plan_create(&L, &p) != ZHIP_OK) return 6;
+        const uint32_t got = zhip_emulate_chunk_crc(p, buf.data());
+        zhip_plan_destroy(p);
+        if (got != crc_bytewise(buf.data(), n)) return set_err(7, "emulated kernel CRC wrong at n=" + std::to_string(n));
+    }
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,62 @@
+// Internal (non-ABI) structures shared by the plan builder and the kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/zarrhip.h"
+
+namespace zhip {
+
+constexpr int kThreads = 256;                            // one workgroup = 4 waves
+constexpr int kBlocksPerThread = 8;                      // 16-byte blocks per thread per unit
+constexpr int kWgStride = kThreads * 16;                 // 4 KiB per workgroup step
+constexpr int kSeg = kWgStride * kBlocksPerThread;       // 32 KiB per unit
+
+// Kernel argument block (passed by value; indexed only with compile-time
+// subscripts inside the kernels so it stays in SGPRs / kernarg memory).
+struct DecodeParams {
+    const uint8_t* src;
+    uint64_t src_size;
+    uint8_t* out;
+    const zhip_chunk* chunks;
+    const zhip_sel* sels;
+    zhip_status* status;
+    uint32_t* ws;
+    uint32_t* errflag;
+    const uint32_t* horner;   // [4 operators][4 byte slices][256]
+    const uint32_t* kthread;  // [kThreads]
+    const uint32_t* kunit;    // [nseg]
+    uint32_t n_chunks, nseg, n_units;
+    uint32_t c_inv, c3;
+    uint32_t lflags;
+    int32_t ndim, itemsize;
+    int32_t shape[ZHIP_MAX_DIMS];
+    int64_t ostride[ZHIP_MAX_DIMS];
+    zhip_fdiv dshape[ZHIP_MAX_DIMS];
+    uint32_t nbytes;  // N (< 2^31)
+    uint32_t E;       // align16(N)
+    uint32_t row_bytes;
+    zhip_fdiv drow;
+    uint32_t index_size, n_inner;
+    uint32_t fill[4];
+    uint32_t fast;
+};
+
+int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid);
+
+}  // namespace zhip
+
+struct zhip_plan {
+    zhip_layout layout;
+    uint32_t nseg;
+    uint32_t E;
+    uint64_t R;
+    uint32_t c_inv, c3;
+    zhip_fdiv dshape[ZHIP_MAX_DIMS];
+    uint32_t row_bytes;
+    zhip_fdiv drow;
+    uint32_t fill[4];
+    int device;
+    int max_grid;
+    uint32_t* d_tables;  // horner (4096) | kthread (256) | kunit (nseg)
+};

@@ -1,0 +1,20 @@
+"""zarr_hip — MI355X-native zarr v3 codec pipeline (fixed-size chain on the GPU).
+
+Drop-in for zarr-python's CodecPipeline (src/zarr/abc/codec.py:315-508): see
+``HipCodecPipeline``.  Select it in a zarr >= 3.3 environment with
+``zarr.config.set({"codec_pipeline.path": "zarr_hip.HipCodecPipeline"})``
+(INTEGRATION.md).  Kernels live in ``csrc/`` behind the C ABI in
+``include/zarrhip.h``; there is no CPU fallback.
+"""
+
+from .array import Array, ArrayMetadata, ChunkNotFoundError
+from .codecs import BytesCodec, Crc32cCodec, ShardingCodec, TransposeCodec
+from .pipeline import DecodeProgram, HipCodecPipeline
+from .spec import ArrayConfig, ArraySpec, GetResult
+from .store import DeviceStore, LocalStore, MemoryStore, StorePath
+
+__all__ = [
+    "Array", "ArrayMetadata", "ArrayConfig", "ArraySpec", "BytesCodec", "ChunkNotFoundError",
+    "Crc32cCodec", "DecodeProgram", "DeviceStore", "GetResult", "HipCodecPipeline", "LocalStore",
+    "MemoryStore", "ShardingCodec", "StorePath", "TransposeCodec",
+]

@@ -1,0 +1,183 @@
+"""ctypes binding of the HIP C-ABI library (include/zarrhip.h).
+
+The product path has no CPU fallback: if ``libzarrhip.so`` is missing or a
+call fails, this module raises.  The library is built in-tree by
+``__graft_entry__.build()`` / ``make -C zarr-python_amd``.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+
+MAX_DIMS = 8
+
+ST_OK = 0
+ST_MISSING = 1
+ST_CRC_MISMATCH = 2
+ST_INDEX_OOB = 3
+ST_LENGTH_MISMATCH = 4
+
+LF_CRC = 1
+LF_SWAP = 2
+LF_SHARDED = 4
+LF_INDEX_START = 8
+LF_NO_WRITE = 16
+
+CF_MISSING = 1
+
+DF_FAST_ROWS = 1
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "libzarrhip.so")
+
+
+class FDiv(ctypes.Structure):
+    _fields_ = [("m", ctypes.c_uint32), ("s", ctypes.c_uint32)]
+
+
+class Layout(ctypes.Structure):
+    _fields_ = [
+        ("ndim", ctypes.c_int32),
+        ("itemsize", ctypes.c_int32),
+        ("shape", ctypes.c_int32 * MAX_DIMS),
+        ("out_stride", ctypes.c_int64 * MAX_DIMS),
+        ("nbytes", ctypes.c_uint64),
+        ("flags", ctypes.c_uint32),
+        ("n_inner", ctypes.c_uint32),
+        ("index_size", ctypes.c_uint32),
+        ("_pad", ctypes.c_uint32),
+        ("fill", ctypes.c_uint8 * 16),
+    ]
+
+
+class Chunk(ctypes.Structure):
+    _fields_ = [
+        ("src", ctypes.c_uint64),
+        ("src_len", ctypes.c_uint64),
+        ("out_off", ctypes.c_int64),
+        ("flags", ctypes.c_uint32),
+        ("slot", ctypes.c_uint32),
+        ("sel", ctypes.c_uint32),
+        ("_pad", ctypes.c_uint32 * 3),
+    ]
+
+
+class Sel(ctypes.Structure):
+    _fields_ = [
+        ("start", ctypes.c_int32 * MAX_DIMS),
+        ("count", ctypes.c_int32 * MAX_DIMS),
+        ("step", ctypes.c_int32 * MAX_DIMS),
+        ("div_step", FDiv * MAX_DIMS),
+    ]
+
+
+class Status(ctypes.Structure):
+    _fields_ = [
+        ("code", ctypes.c_uint32),
+        ("stored", ctypes.c_uint32),
+        ("computed", ctypes.c_uint32),
+        ("aux", ctypes.c_uint32),
+    ]
+
+
+# numpy structured dtypes with the same byte layout (tables are built with numpy
+# and uploaded as raw bytes)
+def _np_dtypes():
+    import numpy as np
+
+    chunk = np.dtype([("src", "<u8"), ("src_len", "<u8"), ("out_off", "<i8"), ("flags", "<u4"),
+                      ("slot", "<u4"), ("sel", "<u4"), ("_pad", "<u4", (3,))])
+    sel = np.dtype([("start", "<i4", (MAX_DIMS,)), ("count", "<i4", (MAX_DIMS,)),
+                    ("step", "<i4", (MAX_DIMS,)), ("div", "<u4", (MAX_DIMS, 2))])
+    status = np.dtype([("code", "<u4"), ("stored", "<u4"), ("computed", "<u4"), ("aux", "<u4")])
+    return chunk, sel, status
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeError(
+            f"zarr_hip native library not built: {LIB_PATH} is missing "
+            "(run __graft_entry__.build() or `make -C zarr-python_amd`)")
+    L = ctypes.CDLL(LIB_PATH)
+    L.zhip_abi_version.restype = ctypes.c_int
+    L.zhip_last_error.restype = ctypes.c_char_p
+    L.zhip_device_count.restype = ctypes.c_int
+    L.zhip_plan_create.argtypes = [ctypes.POINTER(Layout), ctypes.POINTER(ctypes.c_void_p)]
+    L.zhip_plan_create.restype = ctypes.c_int
+    L.zhip_plan_destroy.argtypes = [ctypes.c_void_p]
+    L.zhip_plan_destroy.restype = ctypes.c_int
+    L.zhip_plan_upload.argtypes = [ctypes.c_void_p]
+    L.zhip_plan_upload.restype = ctypes.c_int
+    L.zhip_plan_info.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32),
+                                 ctypes.POINTER(ctypes.c_uint32)]
+    L.zhip_plan_info.restype = ctypes.c_int
+    L.zhip_decode.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                              ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
+    L.zhip_decode.restype = ctypes.c_int
+    L.zhip_selftest.restype = ctypes.c_int
+    L.zhip_emulate_chunk_crc.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    L.zhip_emulate_chunk_crc.restype = ctypes.c_uint32
+    L.zhip_fdiv_eval.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
+    L.zhip_fdiv_eval.restype = ctypes.c_uint32
+    if L.zhip_abi_version() != 1:
+        raise NativeError("libzarrhip ABI version mismatch")
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib().zhip_last_error().decode(errors="replace")
+        raise NativeError(f"{what} failed ({rc}): {msg}")
+
+
+def fdiv(d: int) -> tuple[int, int]:
+    """Magic numbers for n // d with 0 <= n < 2**31 (mirrors make_fdiv in capi.cpp)."""
+    d = max(int(d), 1)
+    l = (d - 1).bit_length()
+    s = 31 + l
+    m = ((1 << s) + d - 1) // d
+    return m, s
+
+
+class Plan:
+    """Owns a zhip_plan (constant tables for one layout) on the current device."""
+
+    def __init__(self, layout: Layout, upload: bool = True):
+        self.layout = layout
+        h = ctypes.c_void_p()
+        check(lib().zhip_plan_create(ctypes.byref(layout), ctypes.byref(h)), "zhip_plan_create")
+        self._h = h
+        upc = ctypes.c_uint32()
+        wsw = ctypes.c_uint32()
+        check(lib().zhip_plan_info(h, ctypes.byref(upc), ctypes.byref(wsw)), "zhip_plan_info")
+        self.units_per_chunk = upc.value
+        self.workspace_words = wsw.value
+        if upload:
+            check(lib().zhip_plan_upload(h), "zhip_plan_upload")
+
+    @property
+    def handle(self):
+        return self._h
+
+    def emulate_chunk_crc(self, data: bytes) -> int:
+        buf = ctypes.create_string_buffer(bytes(data) + b"\0" * 16)
+        return int(lib().zhip_emulate_chunk_crc(self._h, buf))
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h and _lib is not None:
+            _lib.zhip_plan_destroy(h)
+            self._h = None

@@ -1,0 +1,289 @@
+"""Codec configuration objects for the fixed-size chain the GPU pipeline runs.
+
+These mirror the reference codecs' *metadata* surface (from_dict / to_dict /
+evolve_from_array_spec / resolve_metadata / compute_encoded_size / validate);
+their compute lives in the HIP kernels, driven by ``pipeline.HipCodecPipeline``.
+
+  BytesCodec      src/zarr/codecs/bytes.py:42-168
+  Crc32cCodec     src/zarr/codecs/crc32c_.py:20-78
+  TransposeCodec  src/zarr/codecs/transpose.py:29-128
+  ShardingCodec   src/zarr/codecs/sharding.py:402-1756 (configuration + layout rules)
+"""
+
+from __future__ import annotations
+
+import sys
+from dataclasses import dataclass, field, replace
+from typing import Any
+
+import numpy as np
+
+from .spec import ArraySpec
+
+MAX_UINT_64 = 2**64 - 1
+SUBCHUNK_WRITE_ORDER = ("morton", "unordered", "lexicographic", "colexicographic")
+
+
+def _named(data: Any, name: str) -> dict:
+    if isinstance(data, str):
+        if data != name:
+            raise ValueError(f"Expected '{name}'. Got {data} instead.")
+        return {}
+    if data.get("name") != name:
+        raise ValueError(f"Expected '{name}'. Got {data.get('name')} instead.")
+    return dict(data.get("configuration") or {})
+
+
+@dataclass(frozen=True)
+class BytesCodec:
+    """bytes.py:42-168.  ``endian`` None is legal only for single-byte types."""
+
+    endian: str | None = sys.byteorder
+    is_fixed_size = True
+
+    def __post_init__(self):
+        if self.endian is not None and self.endian not in ("little", "big"):
+            raise ValueError(f"endian must be one of ['little', 'big']. Got {self.endian!r}.")
+
+    @classmethod
+    def from_dict(cls, data: Any) -> "BytesCodec":
+        conf = _named(data, "bytes")
+        return cls(endian=conf.get("endian"))
+
+    def to_dict(self) -> dict:
+        if self.endian is None:
+            return {"name": "bytes"}
+        return {"name": "bytes", "configuration": {"endian": self.endian}}
+
+    def evolve_from_array_spec(self, spec: ArraySpec) -> "BytesCodec":
+        """bytes.py:74-95 (structured dtypes are outside the GPU path)."""
+        if spec.dtype.itemsize == 1:
+            return replace(self, endian=None) if self.endian is not None else self
+        if self.endian is None:
+            raise ValueError(
+                "The `endian` configuration needs to be specified for multi-byte data types.")
+        return self
+
+    def resolve_metadata(self, spec: ArraySpec) -> ArraySpec:
+        return spec
+
+    def compute_encoded_size(self, n: int, spec: ArraySpec | None = None) -> int:
+        return n
+
+    def validate(self, **kw) -> None:
+        return None
+
+    def needs_swap(self, dtype: np.dtype) -> bool:
+        """Decoded arrays are native (little-endian on MI355X and its host), so the
+        stored bytes need a swap exactly when they are big-endian multi-byte items
+        (bytes.py:118-127)."""
+        return dtype.itemsize > 1 and self.endian == "big"
+
+
+@dataclass(frozen=True)
+class Crc32cCodec:
+    """crc32c_.py:20-78: 4-byte little-endian CRC-32C trailer."""
+
+    is_fixed_size = True
+
+    @classmethod
+    def from_dict(cls, data: Any) -> "Crc32cCodec":
+        _named(data, "crc32c")
+        return cls()
+
+    def to_dict(self) -> dict:
+        return {"name": "crc32c"}
+
+    def evolve_from_array_spec(self, spec: ArraySpec) -> "Crc32cCodec":
+        return self
+
+    def resolve_metadata(self, spec: ArraySpec) -> ArraySpec:
+        return spec
+
+    def compute_encoded_size(self, n: int, spec: ArraySpec | None = None) -> int:
+        return n + 4
+
+    def validate(self, **kw) -> None:
+        return None
+
+
+@dataclass(frozen=True)
+class TransposeCodec:
+    """transpose.py:29-128."""
+
+    order: tuple[int, ...]
+    is_fixed_size = True
+
+    def __post_init__(self):
+        object.__setattr__(self, "order", tuple(int(i) for i in self.order))
+
+    @classmethod
+    def from_dict(cls, data: Any) -> "TransposeCodec":
+        conf = _named(data, "transpose")
+        return cls(order=tuple(conf["order"]))
+
+    def to_dict(self) -> dict:
+        return {"name": "transpose", "configuration": {"order": tuple(self.order)}}
+
+    def _check(self, ndim: int) -> None:
+        if len(self.order) != ndim:
+            raise ValueError(
+                "The `order` tuple must have as many entries as there are dimensions in the "
+                f"array. Got {self.order}.")
+        if len(self.order) != len(set(self.order)):
+            raise ValueError(f"There must not be duplicates in the `order` tuple. Got {self.order}.")
+        if not all(0 <= x < ndim for x in self.order):
+            raise ValueError(
+                "All entries in the `order` tuple must be between 0 and the number of dimensions "
+                f"in the array. Got {self.order}.")
+
+    def validate(self, *, shape, **kw) -> None:
+        self._check(len(shape))
+
+    def evolve_from_array_spec(self, spec: ArraySpec) -> "TransposeCodec":
+        self._check(spec.ndim)
+        return self
+
+    def resolve_metadata(self, spec: ArraySpec) -> ArraySpec:
+        """transpose.py:89-96."""
+        return replace(spec, shape=tuple(spec.shape[self.order[i]] for i in range(spec.ndim)))
+
+    def compute_encoded_size(self, n: int, spec: ArraySpec | None = None) -> int:
+        return n
+
+
+@dataclass(frozen=True)
+class ShardingCodec:
+    """sharding.py:402-1756: configuration, index layout and size rules."""
+
+    chunk_shape: tuple[int, ...]
+    codecs: tuple = field(default_factory=lambda: (BytesCodec(),))
+    index_codecs: tuple = field(default_factory=lambda: (BytesCodec(endian="little"), Crc32cCodec()))
+    index_location: str = "end"
+    subchunk_write_order: str = "morton"
+    is_fixed_size = False
+
+    def __post_init__(self):
+        object.__setattr__(self, "chunk_shape", tuple(int(c) for c in self.chunk_shape))
+        object.__setattr__(self, "codecs", tuple(parse_codecs(self.codecs)))
+        object.__setattr__(self, "index_codecs", tuple(parse_codecs(self.index_codecs)))
+        if self.index_location not in ("start", "end"):
+            raise ValueError(
+                f"index_location must be one of ['start', 'end']. Got {self.index_location!r}.")
+        if self.subchunk_write_order not in SUBCHUNK_WRITE_ORDER:
+            raise ValueError(
+                f"Unrecognized subchunk write order: {self.subchunk_write_order}. "
+                f"Only {SUBCHUNK_WRITE_ORDER} are allowed.")
+
+    @classmethod
+    def from_dict(cls, data: Any) -> "ShardingCodec":
+        conf = _named(data, "sharding_indexed")
+        return cls(chunk_shape=tuple(conf["chunk_shape"]),
+                   codecs=tuple(conf.get("codecs", ({"name": "bytes"},))),
+                   index_codecs=tuple(conf.get("index_codecs", (
+                       {"name": "bytes", "configuration": {"endian": "little"}},
+                       {"name": "crc32c"}))),
+                   index_location=conf.get("index_location", "end"))
+
+    def to_dict(self) -> dict:
+        return {"name": "sharding_indexed", "configuration": {
+            "chunk_shape": self.chunk_shape,
+            "codecs": tuple(c.to_dict() for c in self.codecs),
+            "index_codecs": tuple(c.to_dict() for c in self.index_codecs),
+            "index_location": self.index_location}}
+
+    def validate(self, *, shape, chunk_shape=None, **kw) -> None:
+        """sharding.py:558-590 (regular grid)."""
+        if len(self.chunk_shape) != len(shape):
+            raise ValueError("The shard's `chunk_shape` and array's `shape` need to have the same "
+                             "number of dimensions.")
+        if chunk_shape is not None:
+            for i, (edge, inner) in enumerate(zip(chunk_shape, self.chunk_shape)):
+                if edge % inner != 0:
+                    raise ValueError(f"Chunk edge length {edge} in dimension {i} is not divisible "
+                                     f"by the shard's inner chunk size {inner}.")
+
+    def chunks_per_shard(self, shard_shape: tuple[int, ...]) -> tuple[int, ...]:
+        """_get_chunks_per_shard (sharding.py:1544-1552)."""
+        return tuple(s // c for s, c in zip(shard_shape, self.chunk_shape))
+
+    def inner_spec(self, shard_spec: ArraySpec) -> ArraySpec:
+        """_get_chunk_spec (sharding.py:1535-1542)."""
+        return replace(shard_spec, shape=self.chunk_shape)
+
+    def shard_index_size(self, n_inner: int) -> int:
+        """_shard_index_size (sharding.py:1515-1522)."""
+        n = 16 * n_inner
+        for c in self.index_codecs:
+            n = c.compute_encoded_size(n)
+        return n
+
+    @property
+    def index_has_crc(self) -> bool:
+        return any(isinstance(c, Crc32cCodec) for c in self.index_codecs)
+
+    def evolve_from_array_spec(self, spec: ArraySpec) -> "ShardingCodec":
+        inner = self.inner_spec(spec)
+        ev = evolve_codecs(self.codecs, inner)
+        return replace(self, codecs=ev) if ev != self.codecs else self
+
+    def resolve_metadata(self, spec: ArraySpec) -> ArraySpec:
+        return spec
+
+    def compute_encoded_size(self, n: int, spec: ArraySpec | None = None) -> int:
+        raise NotImplementedError("sharding_indexed output is not fixed-size")
+
+
+_REGISTRY = {
+    "bytes": BytesCodec,
+    "crc32c": Crc32cCodec,
+    "transpose": TransposeCodec,
+    "sharding_indexed": ShardingCodec,
+}
+
+
+def parse_codecs(codecs) -> list:
+    out = []
+    for c in codecs:
+        if isinstance(c, (BytesCodec, Crc32cCodec, TransposeCodec, ShardingCodec)):
+            out.append(c)
+            continue
+        name = c if isinstance(c, str) else c["name"]
+        if name not in _REGISTRY:
+            raise NotImplementedError(
+                f"codec {name!r} is not on the GPU fixed-size path (compression stays on the host)")
+        out.append(_REGISTRY[name].from_dict(c))
+    return out
+
+
+def evolve_codecs(codecs, spec: ArraySpec) -> tuple:
+    """chunk_utils.py:18-40: evolve each codec against the spec threaded forward."""
+    out = []
+    for c in codecs:
+        e = c.evolve_from_array_spec(spec)
+        out.append(e)
+        spec = e.resolve_metadata(spec)
+    return tuple(out)
+
+
+def split_codecs(codecs) -> tuple[tuple, Any, tuple]:
+    """codecs_from_list (codec_pipeline.py:859-944): AA*, exactly one AB, BB*."""
+    aa, ab, bb = [], None, []
+    for c in codecs:
+        if isinstance(c, TransposeCodec):
+            if ab is not None:
+                raise TypeError("ArrayArrayCodec must come before the ArrayBytesCodec")
+            aa.append(c)
+        elif isinstance(c, (BytesCodec, ShardingCodec)):
+            if ab is not None:
+                raise ValueError("Only one ArrayBytesCodec is allowed.")
+            ab = c
+        elif isinstance(c, Crc32cCodec):
+            if ab is None:
+                raise TypeError("BytesBytesCodec must come after the ArrayBytesCodec")
+            bb.append(c)
+        else:
+            raise NotImplementedError(type(c).__name__)
+    if ab is None:
+        raise ValueError("Required ArrayBytesCodec was not found.")
+    return tuple(aa), ab, tuple(bb)

@@ -1,0 +1,265 @@
+"""Host planner: a batch of (source, chunk_selection, out_selection) items plus an
+evolved codec chain  ->  one zhip_layout and flat chunk / selection tables.
+
+This is where zarr semantics stay on the host: the codec chain
+is reduced to (stored-dim permutation, byteswap, crc, sharding geometry); the
+transpose codec (transpose.py:89-104) disappears into a permutation of the
+out strides, so the kernels only ever walk the *stored* byte order.
+"""
+
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _native as N
+from .codecs import BytesCodec, Crc32cCodec, ShardingCodec, TransposeCodec, split_codecs
+from .indexing import basic_projections
+from .spec import ArraySpec
+
+CHUNK_DT, SEL_DT, STATUS_DT = N._np_dtypes()
+
+
+@dataclass(frozen=True)
+class ChainInfo:
+    """The GPU-relevant content of an evolved fixed-size codec chain."""
+
+    perm: tuple[int, ...]         # stored dim i is decoded dim perm[i]
+    swap: bool                    # bytes codec endian != native
+    crc: bool                     # trailing crc32c
+    endian: str | None
+    shard: ShardingCodec | None = None
+    inner: "ChainInfo | None" = None
+
+
+def analyze_chain(codecs, spec: ArraySpec) -> ChainInfo:
+    aa, ab, bb = split_codecs(codecs)
+    if len(bb) > 1 or any(not isinstance(c, Crc32cCodec) for c in bb):
+        raise NotImplementedError("only a single trailing crc32c bytes->bytes codec is supported")
+    perm = tuple(range(spec.ndim))
+    for t in aa:
+        assert isinstance(t, TransposeCodec)
+        t.evolve_from_array_spec(ArraySpec(tuple(spec.shape[p] for p in perm), spec.dtype,
+                                           spec.fill_value))
+        perm = tuple(perm[t.order[i]] for i in range(len(perm)))
+    if isinstance(ab, ShardingCodec):
+        if aa or bb:
+            raise NotImplementedError(
+                "array->array / bytes->bytes codecs around sharding_indexed are not on the GPU path")
+        inner_spec = ab.inner_spec(spec)
+        inner = analyze_chain(ab.codecs, inner_spec)
+        if inner.shard is not None:
+            raise NotImplementedError("nested sharding is not on the GPU path yet")
+        ia, iab, ibb = split_codecs(ab.index_codecs)
+        if ia or not isinstance(iab, BytesCodec) or iab.endian not in (None, "little") or \
+                len(ibb) > 1:
+            raise NotImplementedError("shard index codecs must be [bytes(little)] + optional crc32c")
+        return ChainInfo(perm, False, False, None, ab, inner)
+    assert isinstance(ab, BytesCodec)
+    ab = ab.evolve_from_array_spec(spec)
+    return ChainInfo(perm, ab.needs_swap(spec.dtype), len(bb) == 1, ab.endian)
+
+
+def _sel_fields(csel, ndim):
+    start = np.zeros(ndim, np.int64)
+    count = np.ones(ndim, np.int64)
+    step = np.ones(ndim, np.int64)
+    is_int = np.zeros(ndim, bool)
+    for d, s in enumerate(csel):
+        if isinstance(s, (int, np.integer)):
+            start[d] = int(s)
+            is_int[d] = True
+        else:
+            a, b, st = s.start or 0, s.stop, s.step or 1
+            start[d] = a
+            step[d] = st
+            count[d] = max(0, -((a - b) // st))
+    return start, count, step, is_int
+
+
+def out_dim_strides(ndim: int, is_int: np.ndarray, drop_axes, out_strides_bytes) -> np.ndarray:
+    """Per decoded dim: the out byte stride (0 for dims absent from out)."""
+    kept = [d for d in range(ndim) if not is_int[d]]
+    drop = set(int(a) for a in drop_axes)
+    kept = [d for k, d in enumerate(kept) if k not in drop]
+    st = np.zeros(ndim, np.int64)
+    if len(kept) != len(out_strides_bytes):
+        raise ValueError(f"selection has {len(kept)} output dims, out has {len(out_strides_bytes)}")
+    for j, d in enumerate(kept):
+        st[d] = out_strides_bytes[j]
+    return st
+
+
+def _out_offset(osel, out_strides_bytes) -> int:
+    off = 0
+    for j, s in enumerate(osel):
+        a = s if isinstance(s, (int, np.integer)) else (s.start or 0)
+        off += int(a) * int(out_strides_bytes[j])
+    return off
+
+
+@dataclass
+class Tables:
+    layout: N.Layout
+    chunks: np.ndarray            # CHUNK_DT[n]
+    sels: np.ndarray              # SEL_DT[m]
+    fast: bool
+    item_of_chunk: np.ndarray     # int64[n]: batch item of each chunk entry
+    index_layout: N.Layout | None = None
+    index_chunks: np.ndarray | None = None
+    index_item: np.ndarray | None = None
+    extra: dict = field(default_factory=dict)
+
+
+def _make_layout(shape_stored, itemsize, ostride_stored, flags, fill: bytes, n_inner=0,
+                 index_size=0) -> N.Layout:
+    L = N.Layout()
+    nd = len(shape_stored)
+    L.ndim = nd
+    L.itemsize = itemsize
+    for i in range(N.MAX_DIMS):
+        L.shape[i] = int(shape_stored[i]) if i < nd else 1
+        L.out_stride[i] = int(ostride_stored[i]) if i < nd else 0
+    L.nbytes = int(np.prod(shape_stored, dtype=np.int64)) * itemsize if nd else itemsize
+    L.flags = flags
+    L.n_inner = n_inner
+    L.index_size = index_size
+    fb = (fill * (16 // max(len(fill), 1) + 1))[:16]
+    ctypes.memmove(L.fill, fb, 16)
+    return L
+
+
+def _pack_sels(start, count, step) -> tuple[np.ndarray, np.ndarray]:
+    """Dedup selection rows; returns (SEL_DT table, row index per entry)."""
+    n, nd = start.shape
+    key = np.concatenate([start, count, step], axis=1)
+    uniq, inv = np.unique(key, axis=0, return_inverse=True)
+    sels = np.zeros(len(uniq), SEL_DT)
+    for r, row in enumerate(uniq):
+        st, ct, sp = row[:nd], row[nd:2 * nd], row[2 * nd:]
+        sels["start"][r, :nd] = st
+        sels["count"][r, :nd] = ct
+        sels["step"][r, :nd] = sp
+        sels["step"][r, nd:] = 1
+        sels["count"][r, nd:] = 1
+        for d in range(N.MAX_DIMS):
+            m, s = N.fdiv(int(sp[d]) if d < nd else 1)
+            sels["div"][r, d, 0] = m
+            sels["div"][r, d, 1] = s
+    return sels, inv.reshape(-1).astype(np.uint32)
+
+
+def _fast_ok(layout: N.Layout, start, count, step, out_offs, out_base_ptr: int) -> bool:
+    nd = layout.ndim
+    it = layout.itemsize
+    last = nd - 1
+    row_bytes = layout.shape[last] * it
+    if layout.out_stride[last] != it or row_bytes % 16 != 0:
+        return False
+    if out_base_ptr % 16 != 0 or np.any(out_offs % 16 != 0):
+        return False
+    for d in range(last):
+        if layout.out_stride[d] % 16 != 0:
+            return False
+    return bool(np.all(start[:, last] == 0) and np.all(count[:, last] == layout.shape[last])
+                and np.all(step[:, last] == 1))
+
+
+def plan_decode(chain: ChainInfo, spec: ArraySpec, items: list, out_strides_bytes,
+                out_base_ptr: int, drop_axes=()) -> Tables:
+    """items: list of (src_off, src_len, missing, chunk_selection, out_selection)."""
+    ndim = spec.ndim
+    itemsize = spec.dtype.itemsize
+    fill = spec.fill_bytes()
+    if not items:
+        raise ValueError("empty batch")
+    _, _, _, is_int0 = _sel_fields(items[0][3], ndim)
+    ost_dec = out_dim_strides(ndim, is_int0, drop_axes, out_strides_bytes)
+
+    if chain.shard is None:
+        perm = chain.perm
+        shape_st = [spec.shape[p] for p in perm]
+        ost_st = [ost_dec[p] for p in perm]
+        flags = (N.LF_CRC if chain.crc else 0) | (N.LF_SWAP if chain.swap else 0)
+        layout = _make_layout(shape_st, itemsize, ost_st, flags, fill)
+        n = len(items)
+        chunks = np.zeros(n, CHUNK_DT)
+        start = np.zeros((n, ndim), np.int64)
+        count = np.zeros((n, ndim), np.int64)
+        step = np.zeros((n, ndim), np.int64)
+        for i, (so, sl, miss, csel, osel) in enumerate(items):
+            st, ct, sp, _ = _sel_fields(csel, ndim)
+            start[i], count[i], step[i] = st[list(perm)], ct[list(perm)], sp[list(perm)]
+            chunks["src"][i] = so
+            chunks["src_len"][i] = sl
+            chunks["flags"][i] = N.CF_MISSING if miss else 0
+            chunks["out_off"][i] = _out_offset(osel, out_strides_bytes)
+        sels, inv = _pack_sels(start, count, step)
+        chunks["sel"] = inv
+        fast = _fast_ok(layout, start, count, step, chunks["out_off"], out_base_ptr)
+        return Tables(layout, chunks, sels, fast, np.arange(n))
+
+    # ---- sharded: expand every shard item into its inner chunks ----
+    sh = chain.shard
+    inner = chain.inner
+    cps = sh.chunks_per_shard(spec.shape)
+    n_inner = int(np.prod(cps))
+    inner_shape = sh.chunk_shape
+    perm = inner.perm
+    shape_st = [inner_shape[p] for p in perm]
+    ost_st = [ost_dec[p] for p in perm]
+    index_size = sh.shard_index_size(n_inner)
+    flags = N.LF_SHARDED | (N.LF_CRC if inner.crc else 0) | (N.LF_SWAP if inner.swap else 0) | \
+        (N.LF_INDEX_START if sh.index_location == "start" else 0)
+    layout = _make_layout(shape_st, itemsize, ost_st, flags, fill, n_inner, index_size)
+    cps_strides = np.array([int(np.prod(cps[d + 1:])) for d in range(ndim)], np.int64)
+    proj_cache: dict = {}
+    parts = []
+    for i, (so, sl, miss, csel, osel) in enumerate(items):
+        key = tuple((s.start, s.stop, s.step) if isinstance(s, slice) else int(s) for s in csel)
+        pr = proj_cache.get(key)
+        if pr is None:
+            pr = basic_projections(tuple(csel), spec.shape, inner_shape)
+            proj_cache[key] = pr
+        base = _out_offset(osel, out_strides_bytes)
+        m = len(pr.coords)
+        oo = base + (pr.out_start * ost_dec[None, :]).sum(axis=1)
+        parts.append((i, so, sl, miss, pr, oo, m))
+    total = sum(p[-1] for p in parts)
+    chunks = np.zeros(total, CHUNK_DT)
+    start = np.zeros((total, ndim), np.int64)
+    count = np.zeros((total, ndim), np.int64)
+    step = np.zeros((total, ndim), np.int64)
+    item_of = np.zeros(total, np.int64)
+    pos = 0
+    idx_rows = []
+    for i, so, sl, miss, pr, oo, m in parts:
+        sl_ = slice(pos, pos + m)
+        chunks["src"][sl_] = so
+        chunks["src_len"][sl_] = sl
+        chunks["flags"][sl_] = N.CF_MISSING if miss else 0
+        chunks["slot"][sl_] = (pr.coords * cps_strides[None, :]).sum(axis=1)
+        chunks["out_off"][sl_] = oo
+        start[sl_] = pr.sel_start[:, list(perm)]
+        count[sl_] = pr.sel_count[:, list(perm)]
+        step[sl_] = np.broadcast_to(pr.step[list(perm)], (m, ndim))
+        item_of[sl_] = i
+        if not miss and sh.index_has_crc:
+            ipos = 0 if sh.index_location == "start" else sl - index_size
+            idx_rows.append((i, so + ipos, index_size))
+        pos += m
+    sels, inv = _pack_sels(start, count, step)
+    chunks["sel"] = inv
+    fast = _fast_ok(layout, start, count, step, chunks["out_off"], out_base_ptr)
+    t = Tables(layout, chunks, sels, fast, item_of)
+    if idx_rows:
+        L2 = _make_layout([16 * n_inner], 1, [0], N.LF_CRC | N.LF_NO_WRITE, b"\0")
+        ic = np.zeros(len(idx_rows), CHUNK_DT)
+        ic["src"] = [r[1] for r in idx_rows]
+        ic["src_len"] = [r[2] for r in idx_rows]
+        t.index_layout = L2
+        t.index_chunks = ic
+        t.index_item = np.array([r[0] for r in idx_rows], np.int64)
+    return t

@@ -1,0 +1,291 @@
+"""Stores: a host MemoryStore and a device-resident store whose chunk and shard
+blobs live in one HBM arena (the data layout the decode kernels read).
+
+  MemoryStore   src/zarr/storage/_memory.py:27-166 (dict of bytes; get_sync returns a view)
+  LocalStore    src/zarr/storage/_local.py (files; host side of the e2e path)
+  StorePath     src/zarr/storage/_common.py:247 (a store + key acting as ByteGetter/ByteSetter)
+
+DeviceStore has no direct reference counterpart (the reference's GpuMemoryStore,
+_memory.py:247-330, is CuPy-only and holds one device buffer per key); here all
+blobs share one arena so a whole batch decodes from a single base pointer with
+16-byte-aligned, 256-byte-padded placements.
+"""
+
+from __future__ import annotations
+
+import os
+import threading
+from dataclasses import dataclass
+from typing import Any
+
+import numpy as np
+
+ALIGN = 256
+TAIL_SLACK = 64  # kernels read up to 64 bytes past a blob (include/zarrhip.h)
+
+
+class MemoryStore:
+    """Host dict store (MemoryStore restated)."""
+
+    supports_sync_io = True
+
+    def __init__(self, data: dict | None = None):
+        self._d: dict[str, bytes] = {} if data is None else data
+
+    def get_sync(self, key: str, byte_range: tuple[int, int] | None = None):
+        v = self._d.get(key)
+        if v is None:
+            return None
+        if byte_range is None:
+            return memoryview(v)
+        a, b = byte_range
+        return memoryview(v)[a:b]
+
+    def set_sync(self, key: str, value) -> None:
+        self._d[key] = bytes(value)
+
+    def delete_sync(self, key: str) -> None:
+        self._d.pop(key, None)
+
+    def exists(self, key: str) -> bool:
+        return key in self._d
+
+    def keys(self):
+        return list(self._d.keys())
+
+    def __contains__(self, key):
+        return key in self._d
+
+    def to_dict(self) -> dict[str, bytes]:
+        return dict(self._d)
+
+
+class LocalStore(MemoryStore):
+    """Files under a root directory (LocalStore restated, host side only)."""
+
+    def __init__(self, root: str):
+        super().__init__()
+        self.root = root
+        os.makedirs(root, exist_ok=True)
+
+    def _path(self, key):
+        return os.path.join(self.root, *key.split("/"))
+
+    def get_sync(self, key, byte_range=None):
+        p = self._path(key)
+        if not os.path.exists(p):
+            return None
+        with open(p, "rb") as f:
+            if byte_range is None:
+                return memoryview(f.read())
+            a, b = byte_range
+            f.seek(a)
+            return memoryview(f.read(b - a))
+
+    def set_sync(self, key, value):
+        p = self._path(key)
+        os.makedirs(os.path.dirname(p), exist_ok=True)
+        with open(p, "wb") as f:
+            f.write(bytes(value))
+
+    def delete_sync(self, key):
+        p = self._path(key)
+        if os.path.exists(p):
+            os.remove(p)
+
+    def exists(self, key):
+        return os.path.exists(self._path(key))
+
+    def keys(self):
+        out = []
+        for dp, _, fs in os.walk(self.root):
+            for f in fs:
+                out.append(os.path.relpath(os.path.join(dp, f), self.root).replace(os.sep, "/"))
+        return out
+
+    def __contains__(self, key):
+        return self.exists(key)
+
+    def to_dict(self):
+        return {k: bytes(self.get_sync(k)) for k in self.keys()}
+
+
+class DeviceArena:
+    """A growable HBM byte arena (torch uint8 tensor) holding encoded blobs."""
+
+    def __init__(self, device, capacity: int = 1 << 24):
+        import torch
+
+        self.device = torch.device(device)
+        self.buf = torch.empty(int(capacity) + TAIL_SLACK, dtype=torch.uint8, device=self.device)
+        self.top = 0
+        self.version = 0
+        self._lock = threading.Lock()
+
+    @property
+    def capacity(self) -> int:
+        return self.buf.numel() - TAIL_SLACK
+
+    def _grow(self, need: int) -> None:
+        import torch
+
+        cap = max(need, 2 * self.capacity)
+        nb = torch.empty(cap + TAIL_SLACK, dtype=torch.uint8, device=self.device)
+        nb[: self.top].copy_(self.buf[: self.top])
+        self.buf = nb
+        self.version += 1
+
+    def reserve(self, nbytes: int) -> int:
+        """Reserve an aligned region; returns its offset."""
+        with self._lock:
+            off = (self.top + ALIGN - 1) // ALIGN * ALIGN
+            end = off + int(nbytes)
+            if end > self.capacity:
+                self._grow(end)
+            self.top = end
+            return off
+
+    def put(self, data) -> tuple[int, int]:
+        """Copy host bytes / numpy / device tensor into the arena."""
+        import torch
+
+        if isinstance(data, torch.Tensor):
+            t = data.reshape(-1).view(torch.uint8)
+            off = self.reserve(t.numel())
+            self.buf[off: off + t.numel()].copy_(t, non_blocking=True)
+            return off, t.numel()
+        arr = np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray) \
+            else np.ascontiguousarray(data).reshape(-1).view(np.uint8)
+        off = self.reserve(arr.size)
+        if arr.size:
+            self.buf[off: off + arr.size].copy_(torch.from_numpy(arr.copy()))
+        return off, int(arr.size)
+
+    def view(self, off: int, n: int):
+        return self.buf[off: off + n]
+
+
+@dataclass
+class DeviceRef:
+    """A ByteGetter result that stays on the device: (arena, offset, length)."""
+
+    arena: DeviceArena
+    offset: int
+    length: int
+
+    def __len__(self):
+        return self.length
+
+    def to_bytes(self) -> bytes:
+        return self.arena.view(self.offset, self.length).cpu().numpy().tobytes()
+
+
+class DeviceStore:
+    """Key -> blob placements in one DeviceArena (HBM-resident chunk store)."""
+
+    supports_sync_io = True
+
+    def __init__(self, device="cuda:0", capacity: int = 1 << 24):
+        self.arena = DeviceArena(device, capacity)
+        self._index: dict[str, tuple[int, int]] = {}
+        self._meta: dict[str, bytes] = {}  # zarr.json documents stay on the host
+
+    @property
+    def device(self):
+        return self.arena.device
+
+    def get_sync(self, key: str, byte_range=None) -> DeviceRef | None:
+        if key.endswith("zarr.json"):
+            m = self._meta.get(key)
+            return None if m is None else memoryview(m)
+        v = self._index.get(key)
+        if v is None:
+            return None
+        off, n = v
+        if byte_range is not None:
+            a, b = byte_range
+            return DeviceRef(self.arena, off + a, b - a)
+        return DeviceRef(self.arena, off, n)
+
+    def set_sync(self, key: str, value: Any) -> None:
+        if key.endswith("zarr.json"):
+            self._meta[key] = bytes(value)
+            return
+        if isinstance(value, DeviceRef):
+            value = value.arena.view(value.offset, value.length)
+        self._index[key] = self.arena.put(value)
+
+    def set_reserved(self, key: str, nbytes: int) -> int:
+        off = self.arena.reserve(nbytes)
+        self._index[key] = (off, nbytes)
+        return off
+
+    def delete_sync(self, key: str) -> None:
+        self._index.pop(key, None)
+
+    def exists(self, key: str) -> bool:
+        return key in self._index
+
+    def __contains__(self, key):
+        return key in self._index
+
+    def keys(self):
+        return list(self._index.keys())
+
+    def placement(self, key: str) -> tuple[int, int] | None:
+        return self._index.get(key)
+
+    def to_dict(self) -> dict[str, bytes]:
+        host = self.arena.buf[: self.arena.top].cpu().numpy()
+        return {k: host[o: o + n].tobytes() for k, (o, n) in self._index.items()}
+
+    @classmethod
+    def from_host(cls, data: dict, device="cuda:0") -> "DeviceStore":
+        total = sum((len(v) + ALIGN) for v in data.values()) + ALIGN
+        st = cls(device, capacity=max(total, 1 << 16))
+        host = np.zeros(total, dtype=np.uint8)
+        placements = {}
+        top = 0
+        for k, v in data.items():
+            if k.endswith("zarr.json"):
+                st._meta[k] = bytes(v)
+                continue
+            b = np.frombuffer(bytes(v), dtype=np.uint8)
+            placements[k] = (top, b.size)
+            host[top: top + b.size] = b
+            top = (top + b.size + ALIGN - 1) // ALIGN * ALIGN
+        import torch
+
+        st.arena.buf[:top].copy_(torch.from_numpy(host[:top]))
+        st.arena.top = top
+        st._index = placements
+        return st
+
+
+@dataclass(frozen=True)
+class StorePath:
+    """store + key: the reference's ByteGetter / ByteSetter (storage/_common.py)."""
+
+    store: Any
+    path: str
+
+    def get_sync(self, prototype=None, byte_range=None):
+        return self.store.get_sync(self.path, byte_range)
+
+    def set_sync(self, value) -> None:
+        self.store.set_sync(self.path, value)
+
+    def delete_sync(self) -> None:
+        self.store.delete_sync(self.path)
+
+    async def get(self, prototype=None, byte_range=None):
+        return self.get_sync(prototype, byte_range)
+
+    async def set(self, value, byte_range=None):
+        self.set_sync(value)
+
+    async def delete(self):
+        self.delete_sync()
+
+    def __truediv__(self, other: str) -> "StorePath":
+        return StorePath(self.store, f"{self.path}/{other}" if self.path else other)
