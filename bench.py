@@ -174,7 +174,7 @@ def main():
     if out0.view(torch.int32).cpu().numpy().tobytes() != data.view(np.int32).tobytes():
         raise SystemExit("bench: decoded output differs from the synthetic input")
     for p, _ in progs:
-        assert p.data.tables.fast, "C2 should take the whole-row fast path"
+        assert p.tables.fast, "C2 should take the whole-row fast path"
 
     stream = torch.cuda.current_stream(device)
     sh = int(stream.cuda_stream)

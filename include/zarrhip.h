@@ -148,7 +148,7 @@ int zhip_plan_upload(zhip_plan *plan);
 /* Decode `n_chunks` chunks of `src` (device) into `out` (device).
  * src must stay readable for 64 bytes past src_size (loads are 16-byte wide).
  * d_chunks/d_sels/d_status/d_workspace/d_errflag are device pointers;
- * d_workspace holds 2*n_chunks zeroed uint32 words (self-resetting: keep it
+ * d_workspace holds 4*n_chunks zeroed uint32 words (8-byte aligned) (self-resetting: keep it
  * for the next call).  *d_errflag gets the OR of (1 << status code) over all
  * chunks whose status is an error (not OK, not MISSING).  `stream` is a
  * hipStream_t (NULL = default stream).  Asynchronous.  With ZHIP_LF_NO_WRITE
@@ -157,6 +157,13 @@ int zhip_decode(const zhip_plan *plan, const void *src, uint64_t src_size, void 
                 const zhip_chunk *d_chunks, uint32_t n_chunks, const zhip_sel *d_sels,
                 zhip_status *d_status, uint32_t *d_workspace, uint32_t *d_errflag,
                 uint32_t decode_flags, void *stream);
+
+/* Process-wide tuning / ablation knobs for measurement (never needed for
+ * correct operation): ZHIP_TUNE_MAX_GRID = persistent-grid cap (0 = auto),
+ * ZHIP_TUNE_ABLATION = ablation bits (0 = production). */
+#define ZHIP_TUNE_MAX_GRID 1
+#define ZHIP_TUNE_ABLATION 2
+int zhip_set_tuning(int key, int value);
 
 /* CPU-only test hooks (no GPU needed). */
 int zhip_selftest(void);                                  /* 0 = all identities hold */

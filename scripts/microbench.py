@@ -1,0 +1,107 @@
+#!/usr/bin/env python
+"""Kernel ablation / tuning matrix for the C2 decode (interleaved rounds in ONE
+process, cdna_hip_programming.md §5.4 rule 24).  Prints one JSON line per arm:
+median / min kernel ms over rounds, algorithmic GB/s, plus a torch D2D copy of
+the same bytes as the practical ceiling."""
+
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "zarr-python_amd"))
+
+import bench  # noqa: E402
+
+
+def main():
+    import torch
+
+    from zarr_hip import _native as N
+
+    dev = torch.device("cuda:0")
+    shape, chunks = (256, 256, 256), (64, 64, 64)
+    data = bench.synthetic(shape)
+    progs = []
+    R = int(os.environ.get("REPLICAS", "4"))
+    for _ in range(R):
+        arr = bench.build_c2_replica(dev, data, shape, chunks)
+        progs.append(arr.prepare_read((Ellipsis,)))
+    stream = torch.cuda.current_stream(dev)
+    sh = int(stream.cuda_stream)
+    alg = 64 * (1048576 + 4) + data.nbytes
+
+    def time_arm(launch, n=20):
+        for i in range(5):
+            launch(i)
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(n)]
+        for i, (a, b) in enumerate(evs):
+            a.record(stream)
+            launch(i)
+            b.record(stream)
+        torch.cuda.synchronize(dev)
+        return [a.elapsed_time(b) for a, b in evs]
+
+    arms = []
+    grids = [int(g) for g in os.environ.get("GRIDS", "0,256,512,1024,4096").split(",")]
+    ablations = [int(a) for a in os.environ.get("ABLATIONS", "0,1,2,4").split(",")]
+    for g in grids:
+        for ab in ablations:
+            arms.append(("decode", g, ab))
+    srcs = [torch.empty(data.nbytes, dtype=torch.uint8, device=dev) for _ in range(R)]
+    dsts = [torch.empty(data.nbytes, dtype=torch.uint8, device=dev) for _ in range(R)]
+    # no-CRC twin of the same batch: same kernel structure, no tables / atomics
+    from zarr_hip.pipeline import DecodeLaunch
+    nocrc = []
+    for prog, out in progs:
+        t = prog.tables
+        L2 = type(t.layout).from_buffer_copy(bytes(t.layout))
+        L2.flags = L2.flags & ~N.LF_CRC
+        ch = t.chunks.copy()
+        ch["src_len"] -= 4
+        nocrc.append(DecodeLaunch(L2, ch, t.sels, prog.data.src, prog.data.src_size, out, True, dev))
+    for g in grids:
+        arms.append(("nocrc", g, 0))
+    arms.append(("torch_copy", 0, 0))
+    arms.append(("torch_read_sum", 0, 0))
+    results = {a: [] for a in arms}
+    rounds = int(os.environ.get("ROUNDS", "5"))
+    for _ in range(rounds):
+        for arm in arms:
+            kind, g, ab = arm
+            if kind == "decode":
+                N.lib().zhip_set_tuning(1, g)
+                N.lib().zhip_set_tuning(2, ab)
+                ms = time_arm(lambda i: progs[i % R][0].launch(sh))
+            elif kind == "nocrc":
+                N.lib().zhip_set_tuning(1, g)
+                N.lib().zhip_set_tuning(2, 0)
+                ms = time_arm(lambda i: nocrc[i % R].launch(sh))
+            elif kind == "torch_copy":
+                ms = time_arm(lambda i: dsts[i % R].copy_(srcs[i % R]))
+            else:
+                ms = time_arm(lambda i: srcs[i % R].view(torch.int32).sum())
+            results[arm].extend(ms)
+    N.lib().zhip_set_tuning(1, 0)
+    N.lib().zhip_set_tuning(2, 0)
+    for p, out in progs:
+        p.data.d_ws.zero_()
+        p.launch(sh)
+        p.results()
+    for arm, ms in results.items():
+        kind, g, ab = arm
+        med = float(np.median(ms))
+        byts = alg if kind != "torch_read_sum" else data.nbytes
+        if kind == "torch_copy":
+            byts = 2 * data.nbytes
+        print(json.dumps({"arm": kind, "grid": g, "ablation": ab, "ms_med": round(med, 4),
+                          "ms_min": round(float(np.min(ms)), 4),
+                          "GBps_med": round(byts / med / 1e6, 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

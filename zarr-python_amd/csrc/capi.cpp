@@ -93,7 +93,19 @@ void build_horner(uint32_t* tab) {  // [op][slice][256], op k = A_(4096 - 4k)
 
 }  // namespace
 
+namespace zhip {
+uint32_t g_tune_bits = 0;
+}
+
 extern "C" {
+
+int zhip_set_tuning(int key, int value) {
+    switch (key) {
+        case ZHIP_TUNE_MAX_GRID: g_tune_max_grid = value; return ZHIP_OK;
+        case ZHIP_TUNE_ABLATION: g_tune_bits = (uint32_t)value; return ZHIP_OK;
+        default: return set_err(ZHIP_E_INVALID, "unknown tuning key");
+    }
+}
 
 int zhip_abi_version(void) { return ZHIP_ABI_VERSION; }
 
@@ -172,7 +184,7 @@ int zhip_plan_destroy(zhip_plan* p) {
 int zhip_plan_info(const zhip_plan* p, uint32_t* units_per_chunk, uint32_t* workspace_words) {
     if (!p) return set_err(ZHIP_E_INVALID, "null plan");
     if (units_per_chunk) *units_per_chunk = p->nseg;
-    if (workspace_words) *workspace_words = 2;
+    if (workspace_words) *workspace_words = 4;
     return ZHIP_OK;
 }
 
@@ -222,6 +234,7 @@ int zhip_decode(const zhip_plan* plan, const void* src, uint64_t src_size, void*
     p.n_inner = L.n_inner;
     std::memcpy(p.fill, plan->fill, sizeof(p.fill));
     p.fast = (decode_flags & ZHIP_DF_FAST_ROWS) ? 1u : 0u;
+    p.tune = g_tune_bits;
     int rc = launch_decode(p, static_cast<hipStream_t>(stream), plan->max_grid);
     if (rc == ZHIP_E_UNSUPPORTED) return set_err(rc, "no kernel for this layout");
     if (rc != ZHIP_OK) return set_err(rc, std::string("launch failed: ") + hipGetErrorString(hipGetLastError()));

@@ -37,6 +37,8 @@
 
 namespace zhip {
 
+int g_tune_max_grid = 0;
+
 __device__ __forceinline__ uint32_t bswap_item(uint32_t x, int item) {
     if (item == 2) return ((x & 0x00FF00FFu) << 8) | ((x >> 8) & 0x00FF00FFu);
     if (item == 4) return __builtin_bswap32(x);
@@ -57,24 +59,9 @@ __device__ __forceinline__ uint4 swap_block(uint4 v) {
 }
 
 // Load the 16 chunk bytes [o, o+16) (o a multiple of 16, chunk-relative), zero
-// outside [0, n).  `cp` need only be byte-aligned; 4-aligned chunks use one
-// dwordx4 load, others funnel-shift five aligned dwords.
-__device__ __forceinline__ uint4 load_block(const uint8_t* cp, int32_t o, uint32_t n, bool al4) {
-    if (o < 0 || (uint32_t)o >= n) return make_uint4(0, 0, 0, 0);
-    uint4 v;
-    if (al4) {
-        v = *reinterpret_cast<const uint4*>(cp + o);
-    } else {
-        const uintptr_t a = reinterpret_cast<uintptr_t>(cp + o);
-        const uint32_t* b = reinterpret_cast<const uint32_t*>(a & ~uintptr_t(3));
-        const uint32_t sh = (uint32_t)(a & 3u) * 8u;
-        const uint4 lo = *reinterpret_cast<const uint4*>(b);
-        const uint32_t hi = b[4];
-        v.x = (uint32_t)((((uint64_t)lo.y << 32) | lo.x) >> sh);
-        v.y = (uint32_t)((((uint64_t)lo.z << 32) | lo.y) >> sh);
-        v.z = (uint32_t)((((uint64_t)lo.w << 32) | lo.z) >> sh);
-        v.w = (uint32_t)((((uint64_t)hi << 32) | lo.w) >> sh);
-    }
+// outside [0, n).  AL4: `cp` is 4-byte aligned -> one dwordx4 load; otherwise
+// five aligned dwords are funnel-shifted.
+__device__ __forceinline__ uint4 mask_tail(uint4 v, int32_t o, uint32_t n) {
     const uint32_t valid = n - (uint32_t)o;
     if (valid < 16u) {
         uint32_t w[4] = {v.x, v.y, v.z, v.w};
@@ -87,6 +74,26 @@ __device__ __forceinline__ uint4 load_block(const uint8_t* cp, int32_t o, uint32
         v = make_uint4(w[0], w[1], w[2], w[3]);
     }
     return v;
+}
+
+template <bool AL4>
+__device__ __forceinline__ uint4 load_block(const uint8_t* cp, int32_t o, uint32_t n) {
+    if (o < 0 || (uint32_t)o >= n) return make_uint4(0, 0, 0, 0);
+    uint4 v;
+    if constexpr (AL4) {
+        v = *reinterpret_cast<const uint4*>(cp + o);
+    } else {
+        const uintptr_t a = reinterpret_cast<uintptr_t>(cp + o);
+        const uint32_t* b = reinterpret_cast<const uint32_t*>(a & ~uintptr_t(3));
+        const uint32_t sh = (uint32_t)(a & 3u) * 8u;
+        const uint4 lo = *reinterpret_cast<const uint4*>(b);
+        const uint32_t hi = b[4];
+        v.x = (uint32_t)((((uint64_t)lo.y << 32) | lo.x) >> sh);
+        v.y = (uint32_t)((((uint64_t)lo.z << 32) | lo.y) >> sh);
+        v.z = (uint32_t)((((uint64_t)lo.w << 32) | lo.z) >> sh);
+        v.w = (uint32_t)((((uint64_t)hi << 32) | lo.w) >> sh);
+    }
+    return mask_tail(v, o, n);
 }
 
 __device__ __forceinline__ uint32_t tab_apply(const uint32_t* tab, uint32_t w) {
@@ -175,128 +182,264 @@ __device__ __forceinline__ void scatter_block_rows(const DecodeParams& p, const 
     *reinterpret_cast<uint4*>(p.out + dst) = swap_block<ITEM, SWAP>(v);
 }
 
+// Per-unit context (wave-uniform).
+struct Unit {
+    uint32_t c;       // chunk
+    uint32_t sidx;    // unit index inside the chunk (0 = the one ending at E)
+    uint32_t mode;    // ZHIP_ST_OK / MISSING / error code
+    const uint8_t* cp;
+    int32_t seg_lo;
+    uint32_t sel;
+    int64_t out_off;
+};
+
+__device__ __forceinline__ Unit resolve_unit(const DecodeParams& p, uint32_t u, uint32_t expected) {
+    Unit U;
+    U.c = u / p.nseg;
+    U.sidx = u - U.c * p.nseg;
+    const zhip_chunk ch = p.chunks[U.c];
+    U.mode = ZHIP_ST_OK;
+    uint64_t base = ch.src;
+    if (ch.flags & ZHIP_CF_MISSING) {
+        U.mode = ZHIP_ST_MISSING;
+    } else if (p.lflags & ZHIP_LF_SHARDED) {
+        // _ShardIndex.get_chunk_slice (sharding.py:248-254): LE u64 (offset, nbytes),
+        // (2^64-1, 2^64-1) = missing; offsets are absolute within the blob.
+        const uint64_t ipos = (p.lflags & ZHIP_LF_INDEX_START) ? 0ull : ch.src_len - p.index_size;
+        const uint8_t* e = p.src + ch.src + ipos + 16ull * ch.slot;
+        const uint64_t off = load_u64_le_bytes(e);
+        const uint64_t len = load_u64_le_bytes(e + 8);
+        if (off == ~0ull && len == ~0ull) U.mode = ZHIP_ST_MISSING;
+        else if (off > ch.src_len || len > ch.src_len - off) U.mode = ZHIP_ST_INDEX_OOB;
+        else if (len != expected) U.mode = ZHIP_ST_LENGTH_MISMATCH;
+        else base = ch.src + off;
+    } else if (ch.src_len != expected) {
+        U.mode = ZHIP_ST_LENGTH_MISMATCH;
+    }
+    U.cp = p.src + base;
+    U.seg_lo = (int32_t)p.E - (int32_t)(U.sidx * (uint32_t)kSeg) - kSeg;
+    U.sel = ch.sel;
+    U.out_off = ch.out_off;
+    return U;
+}
+
+__device__ __forceinline__ void load_unit(const DecodeParams& p, const Unit& U, int t,
+                                          uint4 (&blk)[kBlocksPerThread]) {
+    // uniform branches (SGPR conditions): never if-convert the two load forms
+    const uint32_t ok = __builtin_amdgcn_readfirstlane(U.mode == ZHIP_ST_OK ? 1u : 0u);
+    const uint32_t al4 = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(reinterpret_cast<uintptr_t>(U.cp) & 3u) == 0u ? 1u : 0u);
+    if (!ok) {
+#pragma unroll
+        for (int k = 0; k < kBlocksPerThread; ++k) blk[k] = make_uint4(0, 0, 0, 0);
+    } else if (al4) {
+#pragma unroll
+        for (int k = 0; k < kBlocksPerThread; ++k)
+            blk[k] = load_block<true>(U.cp, U.seg_lo + kWgStride * k + 16 * t, p.nbytes);
+    } else {
+#pragma unroll
+        for (int k = 0; k < kBlocksPerThread; ++k)
+            blk[k] = load_block<false>(U.cp, U.seg_lo + kWgStride * k + 16 * t, p.nbytes);
+    }
+}
+
+// Last unit of chunk c has arrived: turn the accumulator into the CRC-32C value
+// and compare with the stored little-endian trailer (crc32c_.py:41-49).
+__device__ __forceinline__ void finalize_chunk(const DecodeParams& p, uint32_t c, uint32_t stored,
+                                               uint32_t raw) {
+    const uint32_t computed = ~(gf_mul(raw, p.c_inv) ^ p.c3);
+    const uint32_t code = computed == stored ? ZHIP_ST_OK : ZHIP_ST_CRC_MISMATCH;
+    zhip_status st;
+    st.code = code;
+    st.stored = stored;
+    st.computed = computed;
+    st.aux = 0;
+    p.status[c] = st;
+    if (code != ZHIP_ST_OK) atomicOr(p.errflag, 1u << code);
+}
+
+__device__ __forceinline__ uint32_t load_trailer(const uint8_t* cp, uint32_t n) {
+    const uint8_t* tr = cp + n;
+    return (uint32_t)tr[0] | ((uint32_t)tr[1] << 8) | ((uint32_t)tr[2] << 16) | ((uint32_t)tr[3] << 24);
+}
+
+struct Pending {  // thread 0's outstanding arrival for one run, checked one run later
+    uint64_t prev;
+    uint32_t stored, c, bits, V, valid;
+};
+
+__device__ __forceinline__ void retire(const DecodeParams& p, Pending& q, uint64_t full) {
+    if (!q.valid) return;
+    q.valid = 0;
+    if (((q.prev >> 32) ^ q.bits) == full) {
+        uint64_t* w = reinterpret_cast<uint64_t*>(p.ws) + 2ull * q.c;
+        __hip_atomic_store(w, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        finalize_chunk(p, q.c, q.stored, (uint32_t)q.prev ^ q.V);
+    }
+}
+
+// Work assignment: unit "positions" q are numbered chunk-major in INCREASING
+// address order (q = c*nseg + nseg-1-sidx) and every workgroup takes one
+// contiguous, balanced range of them.  Consecutive units of one chunk then
+// continue the same per-thread Horner chain (stride 4096 B), so a workgroup
+// reduces, shifts and publishes once per (chunk, run), not once per unit.
 template <bool CRC, bool WRITE, bool FAST, int ITEM, bool SWAP>
 __global__ __launch_bounds__(kThreads) void k_decode(const DecodeParams p) {
     __shared__ uint32_t s_tab[CRC ? 16 * 256 : 1];
-    __shared__ uint32_t s_red[kThreads / 64];
+    __shared__ uint32_t s_red[2][kThreads / 64];
     const int t = threadIdx.x;
     uint32_t kth = 0;
+    const bool crc_on = CRC && !(p.tune & kTuneSkipCrc);
     if constexpr (CRC) {
         const uint4* g = reinterpret_cast<const uint4*>(p.horner);
         uint4* sv = reinterpret_cast<uint4*>(s_tab);
         for (int i = t; i < 1024; i += kThreads) sv[i] = g[i];
         kth = p.kthread[t];
-        __syncthreads();
     }
     const uint32_t expected = p.nbytes + (CRC ? 4u : 0u);
-    for (uint32_t u = blockIdx.x; u < p.n_units; u += gridDim.x) {
-        const uint32_t c = u / p.nseg;
-        const uint32_t sidx = u - c * p.nseg;
-        const zhip_chunk ch = p.chunks[c];
-        uint32_t mode = ZHIP_ST_OK;
-        uint64_t base = ch.src;
-        if (ch.flags & ZHIP_CF_MISSING) {
-            mode = ZHIP_ST_MISSING;
-        } else if (p.lflags & ZHIP_LF_SHARDED) {
-            const uint64_t ipos = (p.lflags & ZHIP_LF_INDEX_START) ? 0ull : ch.src_len - p.index_size;
-            const uint8_t* e = p.src + ch.src + ipos + 16ull * ch.slot;
-            const uint64_t off = load_u64_le_bytes(e);
-            const uint64_t len = load_u64_le_bytes(e + 8);
-            if (off == ~0ull && len == ~0ull) mode = ZHIP_ST_MISSING;
-            else if (off > ch.src_len || len > ch.src_len - off) mode = ZHIP_ST_INDEX_OOB;
-            else if (len != expected) mode = ZHIP_ST_LENGTH_MISMATCH;
-            else base = ch.src + off;
-        } else if (ch.src_len != expected) {
-            mode = ZHIP_ST_LENGTH_MISMATCH;
-        }
-        const int32_t seg_hi = (int32_t)p.E - (int32_t)(sidx * (uint32_t)kSeg);
-        const int32_t seg_lo = seg_hi - kSeg;
-        const zhip_sel& sel = p.sels[ch.sel];
+    // one 64-bit arrival word per chunk: high half = bitmask of arrived units, low = xor
+    const bool one_atomic = p.nseg <= 32 && !(p.tune & (kTuneAcqRel | kTuneNoTicket));
+    const uint64_t full = p.nseg >= 32 ? 0xFFFFFFFFull : ((1ull << p.nseg) - 1ull);
+    Pending pend;
+    pend.valid = 0;
 
-        if (mode == ZHIP_ST_OK) {
-            const uint8_t* cp = p.src + base;
-            const bool al4 = (reinterpret_cast<uintptr_t>(cp) & 3u) == 0;
-            uint4 blk[kBlocksPerThread];
-#pragma unroll
-            for (int k = 0; k < kBlocksPerThread; ++k)
-                blk[k] = load_block(cp, seg_lo + kWgStride * k + 16 * t, p.nbytes, al4);
-            uint32_t acc = 0;
-            if constexpr (CRC) {
-#pragma unroll
-                for (int k = 0; k < kBlocksPerThread; ++k) {
-                    const uint4 v = blk[k];
-                    acc = tab_apply(s_tab, acc ^ v.x) ^ tab_apply(s_tab + 1024, v.y) ^
-                          tab_apply(s_tab + 2048, v.z) ^ tab_apply(s_tab + 3072, v.w);
-                }
-            }
+    const uint32_t G = gridDim.x, g = blockIdx.x;
+    const uint32_t per = p.n_units / G, rem = p.n_units % G;
+    const uint32_t q0 = g * per + (g < rem ? g : rem);
+    const uint32_t q1 = q0 + per + (g < rem ? 1u : 0u);
+    if (q0 >= q1) return;
+    uint4 A[kBlocksPerThread], B[kBlocksPerThread];
+    auto unit_of = [&](uint32_t q) {
+        const uint32_t c = q / p.nseg;
+        return c * p.nseg + (p.nseg - 1u - (q - c * p.nseg));
+    };
+    Unit ua = resolve_unit(p, unit_of(q0), expected);
+    load_unit(p, ua, t, A);
+    uint32_t stored = 0;
+    if (CRC && t == 0 && ua.mode == ZHIP_ST_OK) stored = load_trailer(ua.cp, p.nbytes);
+    if constexpr (CRC) __syncthreads();  // tables in LDS
+    uint32_t acc = 0, run_bits = 0, run_len = 0, parity = 0;
+    for (uint32_t q = q0;;) {
+        // software pipeline: issue the next unit's loads before working on this one
+        const uint32_t qn = q + 1;
+        const bool more = qn < q1;
+        Unit ub;
+        if (more) {
+            ub = resolve_unit(p, unit_of(qn), expected);
+            load_unit(p, ub, t, B);
+        }
+        const bool run_end = !more || ub.c != ua.c;
+        const zhip_sel& sel = p.sels[ua.sel];
+        if (ua.mode == ZHIP_ST_OK) {
+            // stores first: they do not depend on the CRC, and starting the write
+            // stream early interleaves it with the read stream of later units
             if constexpr (WRITE) {
 #pragma unroll
                 for (int k = 0; k < kBlocksPerThread; ++k) {
-                    const int32_t o = seg_lo + kWgStride * k + 16 * t;
+                    const int32_t o = ua.seg_lo + kWgStride * k + 16 * t;
                     if (o < 0 || (uint32_t)o >= p.nbytes) continue;
-                    if constexpr (FAST) scatter_block_rows<ITEM, SWAP>(p, sel, ch.out_off, o, blk[k]);
-                    else scatter_block_generic<ITEM, SWAP>(p, sel, ch.out_off, o, blk[k]);
+                    if constexpr (FAST) scatter_block_rows<ITEM, SWAP>(p, sel, ua.out_off, o, A[k]);
+                    else scatter_block_generic<ITEM, SWAP>(p, sel, ua.out_off, o, A[k]);
                 }
             }
-            if constexpr (CRC) {
-                uint32_t v = gf_mul(acc, kth);
+            if (crc_on) {
 #pragma unroll
-                for (int off = 32; off > 0; off >>= 1) v ^= __shfl_xor(v, off, 64);
-                if ((t & 63) == 0) s_red[t >> 6] = v;
-                __syncthreads();
-                if (t == 0) {
-                    uint32_t V = s_red[0] ^ s_red[1] ^ s_red[2] ^ s_red[3];
-                    V = gf_mul(V, p.kunit[sidx]);
-                    uint32_t* accw = p.ws + 2ull * c;
-                    __hip_atomic_fetch_xor(accw, V, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    const uint32_t tk = __hip_atomic_fetch_add(accw + 1, 1u, __ATOMIC_ACQ_REL,
-                                                               __HIP_MEMORY_SCOPE_AGENT);
-                    if (tk == p.nseg - 1) {
-                        // last unit of this chunk: every other unit's xor is visible
-                        const uint32_t raw =
-                            __hip_atomic_exchange(accw, 0u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-                        __hip_atomic_store(accw + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        const uint32_t computed = ~(gf_mul(raw, p.c_inv) ^ p.c3);
-                        const uint8_t* tr = cp + p.nbytes;
-                        const uint32_t stored = (uint32_t)tr[0] | ((uint32_t)tr[1] << 8) |
-                                                ((uint32_t)tr[2] << 16) | ((uint32_t)tr[3] << 24);
-                        const uint32_t code = computed == stored ? ZHIP_ST_OK : ZHIP_ST_CRC_MISMATCH;
-                        zhip_status st;
-                        st.code = code;
-                        st.stored = stored;
-                        st.computed = computed;
-                        st.aux = 0;
-                        p.status[c] = st;
-                        if (code != ZHIP_ST_OK) atomicOr(p.errflag, 1u << code);
-                    }
+                for (int k = 0; k < kBlocksPerThread; ++k) {
+                    const uint4 v = A[k];
+                    acc = tab_apply(s_tab, acc ^ v.x) ^ tab_apply(s_tab + 1024, v.y) ^
+                          tab_apply(s_tab + 2048, v.z) ^ tab_apply(s_tab + 3072, v.w);
                 }
-                __syncthreads();
+            } else if constexpr (CRC) {
+#pragma unroll
+                for (int k = 0; k < kBlocksPerThread; ++k) acc ^= A[k].x ^ A[k].y ^ A[k].z ^ A[k].w;
+            }
+            run_bits |= 1u << (ua.sidx & 31u);
+            ++run_len;
+            if constexpr (CRC) {
+                if (run_end) {
+                    uint32_t v = crc_on ? gf_mul(acc, kth) : acc;
+#pragma unroll
+                    for (int off = 32; off > 0; off >>= 1) v ^= __shfl_xor(v, off, 64);
+                    if ((t & 63) == 0) s_red[parity][t >> 6] = v;
+                    __syncthreads();
+                    if (t == 0) {
+                        uint32_t V = s_red[parity][0] ^ s_red[parity][1] ^ s_red[parity][2] ^
+                                     s_red[parity][3];
+                        V = gf_mul(V, p.kunit[ua.sidx]);
+                        if (one_atomic) {
+                            retire(p, pend, full);  // the previous run's arrival has returned by now
+                            uint64_t* w = reinterpret_cast<uint64_t*>(p.ws) + 2ull * ua.c;
+                            pend.prev = __hip_atomic_fetch_xor(w, ((uint64_t)run_bits << 32) | V,
+                                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            pend.stored = stored;
+                            pend.c = ua.c;
+                            pend.bits = run_bits;
+                            pend.V = V;
+                            pend.valid = 1;
+                        } else {
+                            uint32_t* accw = p.ws + 4ull * ua.c;
+                            uint32_t tk;
+                            if (p.tune & kTuneAcqRel) {
+                                __hip_atomic_fetch_xor(accw, V, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                tk = __hip_atomic_fetch_add(accw + 2, run_len, __ATOMIC_ACQ_REL,
+                                                            __HIP_MEMORY_SCOPE_AGENT);
+                            } else {
+                                // the xor must be performed at the device-coherent point
+                                // before the count is drawn: wait for its return first
+                                const uint32_t prev = __hip_atomic_fetch_xor(accw, V, __ATOMIC_RELAXED,
+                                                                             __HIP_MEMORY_SCOPE_AGENT);
+                                asm volatile("s_waitcnt vmcnt(0)" ::"v"(prev) : "memory");
+                                tk = (p.tune & kTuneNoTicket)
+                                         ? 0u
+                                         : __hip_atomic_fetch_add(accw + 2, run_len, __ATOMIC_RELAXED,
+                                                                  __HIP_MEMORY_SCOPE_AGENT);
+                            }
+                            if (tk + run_len == p.nseg && !(p.tune & kTuneNoTicket)) {
+                                const uint32_t raw =
+                                    __hip_atomic_exchange(accw, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                __hip_atomic_store(accw + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                finalize_chunk(p, ua.c, stored, raw);
+                            }
+                        }
+                    }
+                    parity ^= 1u;
+                    acc = 0;
+                    run_bits = 0;
+                    run_len = 0;
+                }
             } else {
-                if (sidx == 0 && t == 0) {
+                if (ua.sidx == 0 && t == 0) {
                     zhip_status st = {ZHIP_ST_OK, 0u, 0u, 0u};
-                    p.status[c] = st;
+                    p.status[ua.c] = st;
                 }
             }
         } else {
             if constexpr (WRITE) {
-                if (mode == ZHIP_ST_MISSING) {
+                if (ua.mode == ZHIP_ST_MISSING) {
                     const uint4 f = make_uint4(p.fill[0], p.fill[1], p.fill[2], p.fill[3]);
 #pragma unroll
                     for (int k = 0; k < kBlocksPerThread; ++k) {
-                        const int32_t o = seg_lo + kWgStride * k + 16 * t;
+                        const int32_t o = ua.seg_lo + kWgStride * k + 16 * t;
                         if (o < 0 || (uint32_t)o >= p.nbytes) continue;
-                        if constexpr (FAST) scatter_block_rows<ITEM, false>(p, sel, ch.out_off, o, f);
-                        else scatter_block_generic<ITEM, false>(p, sel, ch.out_off, o, f);
+                        if constexpr (FAST) scatter_block_rows<ITEM, false>(p, sel, ua.out_off, o, f);
+                        else scatter_block_generic<ITEM, false>(p, sel, ua.out_off, o, f);
                     }
                 }
             }
-            if (sidx == 0 && t == 0) {
-                zhip_status st = {mode, 0u, 0u, 0u};
-                p.status[c] = st;
-                if (mode != ZHIP_ST_MISSING) atomicOr(p.errflag, 1u << mode);
+            if (ua.sidx == 0 && t == 0) {
+                zhip_status st = {ua.mode, 0u, 0u, 0u};
+                p.status[ua.c] = st;
+                if (ua.mode != ZHIP_ST_MISSING) atomicOr(p.errflag, 1u << ua.mode);
             }
         }
+        if (!more) break;
+        if (CRC && t == 0 && ub.c != ua.c && ub.mode == ZHIP_ST_OK) stored = load_trailer(ub.cp, p.nbytes);
+        q = qn;
+        ua = ub;
+#pragma unroll
+        for (int k = 0; k < kBlocksPerThread; ++k) A[k] = B[k];
     }
+    if (t == 0) retire(p, pend, full);
 }
 
 using KernelFn = void (*)(const DecodeParams);
@@ -319,10 +462,18 @@ KernelFn select_decode_kernel(bool crc, bool write, bool fast, int item, bool sw
 }
 
 int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
+    if (g_tune_max_grid > 0) max_grid = g_tune_max_grid;
     KernelFn fn = select_decode_kernel((p.lflags & ZHIP_LF_CRC) != 0, (p.lflags & ZHIP_LF_NO_WRITE) == 0,
                                        p.fast != 0, p.itemsize, (p.lflags & ZHIP_LF_SWAP) != 0);
     if (!fn) return ZHIP_E_UNSUPPORTED;
     if (p.n_units == 0) return ZHIP_OK;
+    if (g_tune_max_grid <= 0) {
+        // persistent grid = resident workgroups (units are software-pipelined per WG)
+        int per_cu = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(fn),
+                                                         kThreads, 0) == hipSuccess && per_cu > 0)
+            max_grid = (max_grid / 8) * per_cu;  // max_grid arrives as CUs * 8
+    }
     const uint32_t grid = p.n_units < (uint32_t)max_grid ? p.n_units : (uint32_t)max_grid;
     hipLaunchKernelGGL(fn, dim3(grid), dim3(kThreads), 0, stream, p);
     return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;

@@ -24,9 +24,12 @@ constexpr uint32_t kPoly = 0x82F63B78u;
 constexpr uint32_t kOne = 0x80000000u;  // the polynomial "1"
 
 // a(x) * b(x) mod P, branch-free (32 steps of shift/xor).
+// Rolled by 4 on purpose: fully unrolled, the compiler materialises all 32
+// shifted copies of a uniform operand in SGPRs and 32 bit-masks in VGPRs at
+// once (80+ spilled SGPRs, +60 VGPRs); it runs a few times per 32 KiB unit.
 ZHIP_HD uint32_t gf_mul(uint32_t a, uint32_t b) {
     uint32_t p = 0;
-#pragma unroll
+#pragma unroll 4
     for (int i = 31; i >= 0; --i) {
         p ^= b & (0u - ((a >> i) & 1u));
         b = (b >> 1) ^ (kPoly & (0u - (b & 1u)));

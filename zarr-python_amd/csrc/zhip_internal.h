@@ -40,7 +40,15 @@ struct DecodeParams {
     uint32_t index_size, n_inner;
     uint32_t fill[4];
     uint32_t fast;
+    uint32_t tune;  // kTune* ablation bits (0 in production)
 };
+
+// Ablation / tuning knobs (zhip_set_tuning): never set on the product path.
+constexpr uint32_t kTuneSkipCrc = 1u;   // replace the CRC lookups by a plain xor
+constexpr uint32_t kTuneAcqRel = 2u;    // acq_rel ticket (the round-1 first version)
+constexpr uint32_t kTuneNoTicket = 4u;  // xor only, no last-arriver finalize
+extern int g_tune_max_grid;
+extern uint32_t g_tune_bits;
 
 int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid);
 

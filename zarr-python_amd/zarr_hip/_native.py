@@ -126,6 +126,8 @@ def lib():
                               ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
                               ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
     L.zhip_decode.restype = ctypes.c_int
+    L.zhip_set_tuning.argtypes = [ctypes.c_int, ctypes.c_int]
+    L.zhip_set_tuning.restype = ctypes.c_int
     L.zhip_selftest.restype = ctypes.c_int
     L.zhip_emulate_chunk_crc.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
     L.zhip_emulate_chunk_crc.restype = ctypes.c_uint32

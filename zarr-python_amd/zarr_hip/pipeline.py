@@ -82,7 +82,7 @@ class DecodeLaunch:
         self.d_chunks = _upload(chunks, device)
         self.d_sels = _upload(sels if len(sels) else np.zeros(1, SEL_DT), device)
         self.d_status = torch.zeros(max(self.n, 1) * 4, dtype=torch.int32, device=device)
-        self.d_ws = torch.zeros(max(self.n, 1) * 2, dtype=torch.int32, device=device)
+        self.d_ws = torch.zeros(max(self.n, 1) * 4, dtype=torch.int32, device=device)
         self.d_err = torch.zeros(4, dtype=torch.int32, device=device)
         self.src = src
         self.src_size = src_size
