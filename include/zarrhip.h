@@ -163,6 +163,7 @@ int zhip_decode(const zhip_plan *plan, const void *src, uint64_t src_size, void 
  * ZHIP_TUNE_ABLATION = ablation bits (0 = production). */
 #define ZHIP_TUNE_MAX_GRID 1
 #define ZHIP_TUNE_ABLATION 2
+#define ZHIP_TUNE_BLOCKS 3   /* blocks/thread per unit for plans created afterwards (4, 8, 16) */
 int zhip_set_tuning(int key, int value);
 
 /* CPU-only test hooks (no GPU needed). */

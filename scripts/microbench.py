@@ -52,6 +52,20 @@ def main():
     for g in grids:
         for ab in ablations:
             arms.append(("decode", g, ab))
+    # K (blocks per thread per unit) variants: separate plans of the same tables
+    from zarr_hip import pipeline as PL
+    kvar = {}
+    for kb in [int(k) for k in os.environ.get("BLOCKS", "").split(",") if k]:
+        N.lib().zhip_set_tuning(3, kb)
+        PL._PLAN_CACHE.clear()
+        kvar[kb] = []
+        for prog, out in progs:
+            t = prog.tables
+            kvar[kb].append(PL.DecodeLaunch(t.layout, t.chunks, t.sels, prog.data.src,
+                                            prog.data.src_size, out, True, dev))
+        arms.append(("decodeK%d" % kb, 0, 0))
+    N.lib().zhip_set_tuning(3, 0)
+    PL._PLAN_CACHE.clear()
     srcs = [torch.empty(data.nbytes, dtype=torch.uint8, device=dev) for _ in range(R)]
     dsts = [torch.empty(data.nbytes, dtype=torch.uint8, device=dev) for _ in range(R)]
     # no-CRC twin of the same batch: same kernel structure, no tables / atomics
@@ -77,6 +91,11 @@ def main():
                 N.lib().zhip_set_tuning(1, g)
                 N.lib().zhip_set_tuning(2, ab)
                 ms = time_arm(lambda i: progs[i % R][0].launch(sh))
+            elif kind.startswith("decodeK"):
+                N.lib().zhip_set_tuning(1, g)
+                N.lib().zhip_set_tuning(2, 0)
+                kl = kvar[int(kind[7:])]
+                ms = time_arm(lambda i: kl[i % R].launch(sh))
             elif kind == "nocrc":
                 N.lib().zhip_set_tuning(1, g)
                 N.lib().zhip_set_tuning(2, 0)
@@ -92,6 +111,12 @@ def main():
         p.data.d_ws.zero_()
         p.launch(sh)
         p.results()
+    for kb, kl in kvar.items():
+        for i, l in enumerate(kl):
+            l.launch(sh)
+            st = l.statuses()
+            assert (st["code"] == 0).all(), f"K={kb}: bad statuses"
+            assert progs[i][1].view(torch.int32).cpu().numpy().tobytes() == data.view(np.int32).tobytes()
     for arm, ms in results.items():
         kind, g, ab = arm
         med = float(np.median(ms))

@@ -95,6 +95,7 @@ void build_horner(uint32_t* tab) {  // [op][slice][256], op k = A_(4096 - 4k)
 
 namespace zhip {
 uint32_t g_tune_bits = 0;
+int g_tune_blocks = 0;
 }
 
 extern "C" {
@@ -103,6 +104,7 @@ int zhip_set_tuning(int key, int value) {
     switch (key) {
         case ZHIP_TUNE_MAX_GRID: g_tune_max_grid = value; return ZHIP_OK;
         case ZHIP_TUNE_ABLATION: g_tune_bits = (uint32_t)value; return ZHIP_OK;
+        case ZHIP_TUNE_BLOCKS: g_tune_blocks = value; return ZHIP_OK;
         default: return set_err(ZHIP_E_INVALID, "unknown tuning key");
     }
 }
@@ -135,7 +137,10 @@ int zhip_plan_create(const zhip_layout* layout, zhip_plan** out) {
     if (!p) return set_err(ZHIP_E_INVALID, "out of memory");
     p->layout = L;
     p->E = (uint32_t)((n + 15) & ~15ull);
-    p->nseg = p->E == 0 ? 1u : (p->E + kSeg - 1) / kSeg;
+    p->kblocks = (g_tune_blocks == 4 || g_tune_blocks == 16) ? (uint32_t)g_tune_blocks : (uint32_t)kDefaultBlocks;
+    if (L.flags & ZHIP_LF_NO_WRITE || !(L.flags & ZHIP_LF_CRC)) p->kblocks = kDefaultBlocks;
+    p->seg = (uint32_t)kWgStride * p->kblocks;
+    p->nseg = p->E == 0 ? 1u : (p->E + p->seg - 1) / p->seg;
     p->R = (uint64_t)p->E + kWgStride;
     p->c_inv = xpow8_inv(p->R - n);
     p->c3 = gf_mul(xpow8(n), 0xFFFFFFFFu);
@@ -162,7 +167,7 @@ int zhip_plan_upload(zhip_plan* p) {
     std::vector<uint32_t> h(4096 + kThreads + p->nseg);
     build_horner(h.data());
     for (int t = 0; t < kThreads; ++t) h[4096 + t] = xpow8((uint64_t)kWgStride - 16u * t);
-    for (uint32_t s = 0; s < p->nseg; ++s) h[4096 + kThreads + s] = xpow8((uint64_t)s * kSeg);
+    for (uint32_t s = 0; s < p->nseg; ++s) h[4096 + kThreads + s] = xpow8((uint64_t)s * p->seg);
     if (p->d_tables) (void)hipFree(p->d_tables);
     p->d_tables = nullptr;
     HIP_TRY(hipMalloc(&p->d_tables, h.size() * sizeof(uint32_t)));
@@ -227,6 +232,7 @@ int zhip_decode(const zhip_plan* plan, const void* src, uint64_t src_size, void*
         p.dshape[d] = plan->dshape[d];
     }
     p.nbytes = (uint32_t)L.nbytes;
+    p.seg = plan->seg;
     p.E = plan->E;
     p.row_bytes = plan->row_bytes;
     p.drow = plan->drow;
@@ -256,12 +262,12 @@ uint32_t zhip_emulate_chunk_crc(const zhip_plan* plan, const uint8_t* data) {
     const uint32_t N = (uint32_t)plan->layout.nbytes;
     uint32_t V = 0;
     for (uint32_t s = 0; s < plan->nseg; ++s) {
-        const int32_t hi = (int32_t)plan->E - (int32_t)(s * (uint32_t)kSeg);
-        const int32_t lo = hi - kSeg;
+        const int32_t hi = (int32_t)plan->E - (int32_t)(s * plan->seg);
+        const int32_t lo = hi - (int32_t)plan->seg;
         uint32_t unit = 0;
         for (int t = 0; t < kThreads; ++t) {
             uint32_t acc = 0;
-            for (int k = 0; k < kBlocksPerThread; ++k) {
+            for (int k = 0; k < (int)plan->kblocks; ++k) {
                 const int32_t o = lo + kWgStride * k + 16 * t;
                 uint8_t b[16] = {0};
                 for (int i = 0; i < 16; ++i) {
@@ -279,7 +285,7 @@ uint32_t zhip_emulate_chunk_crc(const zhip_plan* plan, const uint8_t* data) {
             }
             unit ^= gf_mul(acc, xpow8((uint64_t)kWgStride - 16u * t));
         }
-        V ^= gf_mul(unit, xpow8((uint64_t)s * kSeg));
+        V ^= gf_mul(unit, xpow8((uint64_t)s * plan->seg));
     }
     return ~(gf_mul(V, plan->c_inv) ^ plan->c3);
 }

@@ -13,8 +13,8 @@
 //   _ShardIndex.get_chunk_slice     src/zarr/codecs/sharding.py:248-254 (MAX_UINT_64 -> missing)
 //
 // Work decomposition.  A chunk's decoded payload [0, N) is cut into "units" of
-// kSeg = 32 KiB, aligned to E = align16(N) from the END (unit s covers
-// [E-(s+1)kSeg, E-s*kSeg)); bytes outside [0, N) are zero.  One 256-thread
+// seg = 4 KiB * K (K = 8 by default: 32 KiB), aligned to E = align16(N) from the END
+// (unit s covers [E-(s+1)seg, E-s*seg)); bytes outside [0, N) are zero.  One 256-thread
 // workgroup handles one unit: thread t owns the 16-byte blocks at
 // lo + 16t + 4096k, k < 8 (each wave instruction reads 1 KiB contiguous).
 //
@@ -217,28 +217,28 @@ __device__ __forceinline__ Unit resolve_unit(const DecodeParams& p, uint32_t u, 
         U.mode = ZHIP_ST_LENGTH_MISMATCH;
     }
     U.cp = p.src + base;
-    U.seg_lo = (int32_t)p.E - (int32_t)(U.sidx * (uint32_t)kSeg) - kSeg;
+    U.seg_lo = (int32_t)p.E - (int32_t)((U.sidx + 1u) * p.seg);
     U.sel = ch.sel;
     U.out_off = ch.out_off;
     return U;
 }
 
-__device__ __forceinline__ void load_unit(const DecodeParams& p, const Unit& U, int t,
-                                          uint4 (&blk)[kBlocksPerThread]) {
+template <int K>
+__device__ __forceinline__ void load_unit(const DecodeParams& p, const Unit& U, int t, uint4 (&blk)[K]) {
     // uniform branches (SGPR conditions): never if-convert the two load forms
     const uint32_t ok = __builtin_amdgcn_readfirstlane(U.mode == ZHIP_ST_OK ? 1u : 0u);
     const uint32_t al4 = __builtin_amdgcn_readfirstlane(
         (uint32_t)(reinterpret_cast<uintptr_t>(U.cp) & 3u) == 0u ? 1u : 0u);
     if (!ok) {
 #pragma unroll
-        for (int k = 0; k < kBlocksPerThread; ++k) blk[k] = make_uint4(0, 0, 0, 0);
+        for (int k = 0; k < K; ++k) blk[k] = make_uint4(0, 0, 0, 0);
     } else if (al4) {
 #pragma unroll
-        for (int k = 0; k < kBlocksPerThread; ++k)
+        for (int k = 0; k < K; ++k)
             blk[k] = load_block<true>(U.cp, U.seg_lo + kWgStride * k + 16 * t, p.nbytes);
     } else {
 #pragma unroll
-        for (int k = 0; k < kBlocksPerThread; ++k)
+        for (int k = 0; k < K; ++k)
             blk[k] = load_block<false>(U.cp, U.seg_lo + kWgStride * k + 16 * t, p.nbytes);
     }
 }
@@ -283,7 +283,7 @@ __device__ __forceinline__ void retire(const DecodeParams& p, Pending& q, uint64
 // contiguous, balanced range of them.  Consecutive units of one chunk then
 // continue the same per-thread Horner chain (stride 4096 B), so a workgroup
 // reduces, shifts and publishes once per (chunk, run), not once per unit.
-template <bool CRC, bool WRITE, bool FAST, int ITEM, bool SWAP>
+template <bool CRC, bool WRITE, bool FAST, int ITEM, bool SWAP, int K = 8>
 __global__ __launch_bounds__(kThreads) void k_decode(const DecodeParams p) {
     __shared__ uint32_t s_tab[CRC ? 16 * 256 : 1];
     __shared__ uint32_t s_red[2][kThreads / 64];
@@ -308,13 +308,13 @@ __global__ __launch_bounds__(kThreads) void k_decode(const DecodeParams p) {
     const uint32_t q0 = g * per + (g < rem ? g : rem);
     const uint32_t q1 = q0 + per + (g < rem ? 1u : 0u);
     if (q0 >= q1) return;
-    uint4 A[kBlocksPerThread], B[kBlocksPerThread];
+    uint4 A[K], B[K];
     auto unit_of = [&](uint32_t q) {
         const uint32_t c = q / p.nseg;
         return c * p.nseg + (p.nseg - 1u - (q - c * p.nseg));
     };
     Unit ua = resolve_unit(p, unit_of(q0), expected);
-    load_unit(p, ua, t, A);
+    load_unit<K>(p, ua, t, A);
     uint32_t stored = 0;
     if (CRC && t == 0 && ua.mode == ZHIP_ST_OK) stored = load_trailer(ua.cp, p.nbytes);
     if constexpr (CRC) __syncthreads();  // tables in LDS
@@ -326,7 +326,7 @@ __global__ __launch_bounds__(kThreads) void k_decode(const DecodeParams p) {
         Unit ub;
         if (more) {
             ub = resolve_unit(p, unit_of(qn), expected);
-            load_unit(p, ub, t, B);
+            load_unit<K>(p, ub, t, B);
         }
         const bool run_end = !more || ub.c != ua.c;
         const zhip_sel& sel = p.sels[ua.sel];
@@ -335,7 +335,7 @@ __global__ __launch_bounds__(kThreads) void k_decode(const DecodeParams p) {
             // stream early interleaves it with the read stream of later units
             if constexpr (WRITE) {
 #pragma unroll
-                for (int k = 0; k < kBlocksPerThread; ++k) {
+                for (int k = 0; k < K; ++k) {
                     const int32_t o = ua.seg_lo + kWgStride * k + 16 * t;
                     if (o < 0 || (uint32_t)o >= p.nbytes) continue;
                     if constexpr (FAST) scatter_block_rows<ITEM, SWAP>(p, sel, ua.out_off, o, A[k]);
@@ -344,14 +344,14 @@ __global__ __launch_bounds__(kThreads) void k_decode(const DecodeParams p) {
             }
             if (crc_on) {
 #pragma unroll
-                for (int k = 0; k < kBlocksPerThread; ++k) {
+                for (int k = 0; k < K; ++k) {
                     const uint4 v = A[k];
                     acc = tab_apply(s_tab, acc ^ v.x) ^ tab_apply(s_tab + 1024, v.y) ^
                           tab_apply(s_tab + 2048, v.z) ^ tab_apply(s_tab + 3072, v.w);
                 }
             } else if constexpr (CRC) {
 #pragma unroll
-                for (int k = 0; k < kBlocksPerThread; ++k) acc ^= A[k].x ^ A[k].y ^ A[k].z ^ A[k].w;
+                for (int k = 0; k < K; ++k) acc ^= A[k].x ^ A[k].y ^ A[k].z ^ A[k].w;
             }
             run_bits |= 1u << (ua.sidx & 31u);
             ++run_len;
@@ -418,7 +418,7 @@ __global__ __launch_bounds__(kThreads) void k_decode(const DecodeParams p) {
                 if (ua.mode == ZHIP_ST_MISSING) {
                     const uint4 f = make_uint4(p.fill[0], p.fill[1], p.fill[2], p.fill[3]);
 #pragma unroll
-                    for (int k = 0; k < kBlocksPerThread; ++k) {
+                    for (int k = 0; k < K; ++k) {
                         const int32_t o = ua.seg_lo + kWgStride * k + 16 * t;
                         if (o < 0 || (uint32_t)o >= p.nbytes) continue;
                         if constexpr (FAST) scatter_block_rows<ITEM, false>(p, sel, ua.out_off, o, f);
@@ -437,34 +437,44 @@ __global__ __launch_bounds__(kThreads) void k_decode(const DecodeParams p) {
         q = qn;
         ua = ub;
 #pragma unroll
-        for (int k = 0; k < kBlocksPerThread; ++k) A[k] = B[k];
+        for (int k = 0; k < K; ++k) A[k] = B[k];
     }
     if (t == 0) retire(p, pend, full);
 }
 
 using KernelFn = void (*)(const DecodeParams);
 
-template <bool CRC, bool WRITE, bool FAST>
+template <bool CRC, bool WRITE, bool FAST, int K>
 static KernelFn pick_item(int item, bool swap) {
     switch (item) {
-        case 1: return k_decode<CRC, WRITE, FAST, 1, false>;
-        case 2: return swap ? k_decode<CRC, WRITE, FAST, 2, true> : k_decode<CRC, WRITE, FAST, 2, false>;
-        case 4: return swap ? k_decode<CRC, WRITE, FAST, 4, true> : k_decode<CRC, WRITE, FAST, 4, false>;
-        case 8: return swap ? k_decode<CRC, WRITE, FAST, 8, true> : k_decode<CRC, WRITE, FAST, 8, false>;
+        case 1: return k_decode<CRC, WRITE, FAST, 1, false, K>;
+        case 2: return swap ? k_decode<CRC, WRITE, FAST, 2, true, K> : k_decode<CRC, WRITE, FAST, 2, false, K>;
+        case 4: return swap ? k_decode<CRC, WRITE, FAST, 4, true, K> : k_decode<CRC, WRITE, FAST, 4, false, K>;
+        case 8: return swap ? k_decode<CRC, WRITE, FAST, 8, true, K> : k_decode<CRC, WRITE, FAST, 8, false, K>;
         default: return nullptr;
     }
 }
 
-KernelFn select_decode_kernel(bool crc, bool write, bool fast, int item, bool swap) {
-    if (!write) return crc ? k_decode<true, false, false, 1, false> : nullptr;
-    if (crc) return fast ? pick_item<true, true, true>(item, swap) : pick_item<true, true, false>(item, swap);
-    return fast ? pick_item<false, true, true>(item, swap) : pick_item<false, true, false>(item, swap);
+KernelFn select_decode_kernel(bool crc, bool write, bool fast, int item, bool swap, int k) {
+    if (!write) {
+        if (!crc) return nullptr;
+        return k == 4 ? k_decode<true, false, false, 1, false, 4>
+             : k == 16 ? k_decode<true, false, false, 1, false, 16> : k_decode<true, false, false, 1, false, 8>;
+    }
+    if (crc && fast) {
+        return k == 4 ? pick_item<true, true, true, 4>(item, swap)
+             : k == 16 ? pick_item<true, true, true, 16>(item, swap) : pick_item<true, true, true, 8>(item, swap);
+    }
+    if (k != 8) return nullptr;
+    if (crc) return pick_item<true, true, false, 8>(item, swap);
+    return fast ? pick_item<false, true, true, 8>(item, swap) : pick_item<false, true, false, 8>(item, swap);
 }
 
 int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
     if (g_tune_max_grid > 0) max_grid = g_tune_max_grid;
     KernelFn fn = select_decode_kernel((p.lflags & ZHIP_LF_CRC) != 0, (p.lflags & ZHIP_LF_NO_WRITE) == 0,
-                                       p.fast != 0, p.itemsize, (p.lflags & ZHIP_LF_SWAP) != 0);
+                                       p.fast != 0, p.itemsize, (p.lflags & ZHIP_LF_SWAP) != 0,
+                                       (int)(p.seg / kWgStride));
     if (!fn) return ZHIP_E_UNSUPPORTED;
     if (p.n_units == 0) return ZHIP_OK;
     if (g_tune_max_grid <= 0) {

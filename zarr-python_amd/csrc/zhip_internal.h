@@ -8,9 +8,8 @@
 namespace zhip {
 
 constexpr int kThreads = 256;                            // one workgroup = 4 waves
-constexpr int kBlocksPerThread = 8;                      // 16-byte blocks per thread per unit
 constexpr int kWgStride = kThreads * 16;                 // 4 KiB per workgroup step
-constexpr int kSeg = kWgStride * kBlocksPerThread;       // 32 KiB per unit
+constexpr int kDefaultBlocks = 8;                        // 16-byte blocks per thread per unit
 
 // Kernel argument block (passed by value; indexed only with compile-time
 // subscripts inside the kernels so it stays in SGPRs / kernarg memory).
@@ -33,6 +32,7 @@ struct DecodeParams {
     int32_t shape[ZHIP_MAX_DIMS];
     int64_t ostride[ZHIP_MAX_DIMS];
     zhip_fdiv dshape[ZHIP_MAX_DIMS];
+    uint32_t seg;     // bytes per unit = kWgStride * K
     uint32_t nbytes;  // N (< 2^31)
     uint32_t E;       // align16(N)
     uint32_t row_bytes;
@@ -48,6 +48,7 @@ constexpr uint32_t kTuneSkipCrc = 1u;   // replace the CRC lookups by a plain xo
 constexpr uint32_t kTuneAcqRel = 2u;    // acq_rel ticket (the round-1 first version)
 constexpr uint32_t kTuneNoTicket = 4u;  // xor only, no last-arriver finalize
 extern int g_tune_max_grid;
+extern int g_tune_blocks;
 extern uint32_t g_tune_bits;
 
 int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid);
@@ -56,6 +57,8 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid);
 
 struct zhip_plan {
     zhip_layout layout;
+    uint32_t kblocks;  // K: blocks per thread per unit (4, 8 or 16)
+    uint32_t seg;      // kWgStride * K
     uint32_t nseg;
     uint32_t E;
     uint64_t R;
