@@ -69,6 +69,7 @@ extern "C" {
 #define ZHIP_LF_SHARDED 4u        /* chunk source = inner chunk of a shard blob     */
 #define ZHIP_LF_INDEX_START 8u    /* sharding index_location == "start"             */
 #define ZHIP_LF_NO_WRITE 16u      /* verify only (shard index CRC)                  */
+#define ZHIP_LF_FLOAT 32u         /* items are IEEE floats (NaN-aware fill equality) */
 
 /* chunk flags (zhip_chunk.flags) */
 #define ZHIP_CF_MISSING 1u        /* store returned None: scatter fill value        */
@@ -124,6 +125,13 @@ typedef struct zhip_status {
     uint32_t aux;
 } zhip_status;
 
+/* One shard of an encode batch (zhip_shard_pack). */
+typedef struct zhip_shard {
+    uint64_t blob;         /* byte offset of the shard blob in dst                */
+    uint32_t first_chunk;  /* id of its Morton-rank-0 inner chunk in the batch    */
+    uint32_t _pad;
+} zhip_shard;
+
 typedef struct zhip_plan zhip_plan;
 
 int zhip_abi_version(void);
@@ -165,6 +173,37 @@ int zhip_decode(const zhip_plan *plan, const void *src, uint64_t src_size, void 
 #define ZHIP_TUNE_ABLATION 2
 #define ZHIP_TUNE_BLOCKS 3   /* blocks/thread per unit for plans created afterwards (4, 8, 16) */
 int zhip_set_tuning(int key, int value);
+
+/* Encode `n_chunks` chunks gathered from the device array `arr` into `dst`.
+ * Per chunk: zhip_chunk.src = byte offset of the encoded chunk in dst (its
+ * N [+4] bytes are written there), out_off = byte offset in arr of the chunk's
+ * selection origin, sel = selection (stored dims) — elements outside it are
+ * written as the fill value (edge chunks, _merge_chunk_array).  With
+ * ZHIP_LF_CRC the CRC-32C trailer is appended and also reported in
+ * d_status[i].computed.  d_nonempty[i] (zeroed by the caller) is set to 1 if
+ * any element differs from the fill value under NDBuffer.all_equal rules.
+ * ZHIP_DF_FAST_ROWS: every chunk selects whole rows that are contiguous and
+ * 16-byte aligned in arr.  Asynchronous. */
+int zhip_encode(const zhip_plan *plan, const void *arr, void *dst, const zhip_chunk *d_chunks,
+                uint32_t n_chunks, const zhip_sel *d_sels, zhip_status *d_status,
+                uint32_t *d_workspace, uint32_t *d_nonempty, uint32_t encode_flags, void *stream);
+
+/* shard pack flags */
+#define ZHIP_PF_INDEX_START 1u   /* index_location == "start" */
+#define ZHIP_PF_INDEX_CRC 2u     /* index codecs end in crc32c */
+#define ZHIP_PF_KEEP_EMPTY 4u    /* write_empty_chunks: no elision */
+
+/* Pack shards whose inner chunks zhip_encode wrote densely in Morton-rank order
+ * at blob + data_start + rank*elen (data_start = index_size if the index is at
+ * the start, else 0): elide empty inner chunks (compacting the rest), write the
+ * index (LE u64 offset/length, 2^64-1 pairs for absent chunks) and its CRC.
+ * d_rank_of_slot[i] = Morton rank of C-order slot i.  d_blob_len[s] receives
+ * the final blob length (0 = every inner chunk empty: delete the shard).
+ * `plan` is the inner-chunk plan (supplies the CRC tables).  Asynchronous. */
+int zhip_shard_pack(const zhip_plan *plan, void *dst, const zhip_shard *d_shards, uint32_t n_shards,
+                    uint32_t n_inner, uint32_t elen, uint32_t index_size, uint32_t pack_flags,
+                    const uint32_t *d_nonempty, uint32_t *d_newrank, const uint32_t *d_rank_of_slot,
+                    uint64_t *d_blob_len, void *stream);
 
 /* CPU-only test hooks (no GPU needed). */
 int zhip_selftest(void);                                  /* 0 = all identities hold */

@@ -94,6 +94,20 @@ void build_horner(uint32_t* tab) {  // [op][slice][256], op k = A_(4096 - 4k)
 }  // namespace
 
 namespace zhip {
+void fill_geom(Geom& g, const zhip_plan& plan) {
+    const zhip_layout& L = plan.layout;
+    g.ndim = L.ndim;
+    g.itemsize = L.itemsize;
+    for (int d = 0; d < ZHIP_MAX_DIMS; ++d) {
+        g.shape[d] = d < L.ndim ? L.shape[d] : 1;
+        g.ostride[d] = d < L.ndim ? L.out_stride[d] : 0;
+        g.dshape[d] = plan.dshape[d];
+    }
+    g.nbytes = (uint32_t)L.nbytes;
+    g.row_bytes = plan.row_bytes;
+    g.drow = plan.drow;
+}
+
 uint32_t g_tune_bits = 0;
 int g_tune_blocks = 0;
 }
@@ -224,18 +238,9 @@ int zhip_decode(const zhip_plan* plan, const void* src, uint64_t src_size, void*
     p.c_inv = plan->c_inv;
     p.c3 = plan->c3;
     p.lflags = L.flags;
-    p.ndim = L.ndim;
-    p.itemsize = L.itemsize;
-    for (int d = 0; d < ZHIP_MAX_DIMS; ++d) {
-        p.shape[d] = d < L.ndim ? L.shape[d] : 1;
-        p.ostride[d] = d < L.ndim ? L.out_stride[d] : 0;
-        p.dshape[d] = plan->dshape[d];
-    }
-    p.nbytes = (uint32_t)L.nbytes;
+    fill_geom(p.g, *plan);
     p.seg = plan->seg;
     p.E = plan->E;
-    p.row_bytes = plan->row_bytes;
-    p.drow = plan->drow;
     p.index_size = L.index_size;
     p.n_inner = L.n_inner;
     std::memcpy(p.fill, plan->fill, sizeof(p.fill));
@@ -243,6 +248,90 @@ int zhip_decode(const zhip_plan* plan, const void* src, uint64_t src_size, void*
     p.tune = g_tune_bits;
     int rc = launch_decode(p, static_cast<hipStream_t>(stream), plan->max_grid);
     if (rc == ZHIP_E_UNSUPPORTED) return set_err(rc, "no kernel for this layout");
+    if (rc != ZHIP_OK) return set_err(rc, std::string("launch failed: ") + hipGetErrorString(hipGetLastError()));
+    return ZHIP_OK;
+}
+
+int zhip_encode(const zhip_plan* plan, const void* arr, void* dst, const zhip_chunk* d_chunks, uint32_t n_chunks,
+                const zhip_sel* d_sels, zhip_status* d_status, uint32_t* d_workspace, uint32_t* d_nonempty,
+                uint32_t encode_flags, void* stream) {
+    if (!plan) return set_err(ZHIP_E_INVALID, "null plan");
+    if (!plan->d_tables) return set_err(ZHIP_E_INVALID, "plan not uploaded (zhip_plan_upload)");
+    if (n_chunks == 0) return ZHIP_OK;
+    if (!arr || !dst || !d_chunks || !d_sels || !d_status || !d_workspace || !d_nonempty)
+        return set_err(ZHIP_E_INVALID, "null device pointer");
+    if (plan->kblocks != (uint32_t)kDefaultBlocks) return set_err(ZHIP_E_UNSUPPORTED, "encode needs K=8 plans");
+    const zhip_layout& L = plan->layout;
+    const uint64_t units = (uint64_t)n_chunks * plan->nseg;
+    if (units >= (1ull << 32)) return set_err(ZHIP_E_UNSUPPORTED, "too many units in one batch");
+    EncodeParams p{};
+    p.arr = static_cast<const uint8_t*>(arr);
+    p.dst = static_cast<uint8_t*>(dst);
+    p.chunks = d_chunks;
+    p.sels = d_sels;
+    p.status = d_status;
+    p.ws = d_workspace;
+    p.nonempty = d_nonempty;
+    p.horner = plan->d_tables;
+    p.kthread = plan->d_tables + 4096;
+    p.kunit = plan->d_tables + 4096 + kThreads;
+    p.n_chunks = n_chunks;
+    p.nseg = plan->nseg;
+    p.n_units = (uint32_t)units;
+    p.c_inv = plan->c_inv;
+    p.c3 = plan->c3;
+    p.lflags = L.flags;
+    fill_geom(p.g, *plan);
+    p.seg = plan->seg;
+    p.E = plan->E;
+    std::memcpy(p.fill, plan->fill, sizeof(p.fill));
+    p.fill_nan = 0;
+    if (L.flags & ZHIP_LF_FLOAT) {
+        if (L.itemsize == 4) p.fill_nan = (p.fill[0] & 0x7FFFFFFFu) > 0x7F800000u;
+        else if (L.itemsize == 2) p.fill_nan = (p.fill[0] & 0x7FFFu) > 0x7C00u;
+        else if (L.itemsize == 8)
+            p.fill_nan = ((((uint64_t)p.fill[1] << 32) | p.fill[0]) & 0x7FFFFFFFFFFFFFFFull) > 0x7FF0000000000000ull;
+    }
+    p.fast = (encode_flags & ZHIP_DF_FAST_ROWS) ? 1u : 0u;
+    int rc = launch_encode(p, static_cast<hipStream_t>(stream), plan->max_grid);
+    if (rc == ZHIP_E_UNSUPPORTED) return set_err(rc, "no encode kernel for this layout");
+    if (rc != ZHIP_OK) return set_err(rc, std::string("launch failed: ") + hipGetErrorString(hipGetLastError()));
+    return ZHIP_OK;
+}
+
+int zhip_shard_pack(const zhip_plan* plan, void* dst, const zhip_shard* d_shards, uint32_t n_shards,
+                    uint32_t n_inner, uint32_t elen, uint32_t index_size, uint32_t pack_flags,
+                    const uint32_t* d_nonempty, uint32_t* d_newrank, const uint32_t* d_rank_of_slot,
+                    uint64_t* d_blob_len, void* stream) {
+    std::call_once(g_once, init_tables);
+    if (!plan || !plan->d_tables) return set_err(ZHIP_E_INVALID, "plan not uploaded");
+    if (n_shards == 0) return ZHIP_OK;
+    if (!dst || !d_shards || !d_nonempty || !d_newrank || !d_rank_of_slot || !d_blob_len)
+        return set_err(ZHIP_E_INVALID, "null device pointer");
+    if (n_inner == 0) return set_err(ZHIP_E_INVALID, "n_inner == 0");
+    PackParams p{};
+    p.dst = static_cast<uint8_t*>(dst);
+    p.shards = d_shards;
+    p.nonempty = d_nonempty;
+    p.newrank = d_newrank;
+    p.rank_of_slot = d_rank_of_slot;
+    p.blob_len = d_blob_len;
+    p.horner = plan->d_tables;
+    p.kthread = plan->d_tables + 4096;
+    p.n_inner = n_inner;
+    p.elen = elen;
+    p.index_size = index_size;
+    p.index_start = (pack_flags & ZHIP_PF_INDEX_START) ? 1u : 0u;
+    p.index_crc = (pack_flags & ZHIP_PF_INDEX_CRC) ? 1u : 0u;
+    p.keep_empty = (pack_flags & ZHIP_PF_KEEP_EMPTY) ? 1u : 0u;
+    // index CRC constants: thread t's Horner state lands at 16t + 4096*kiters,
+    // shifted by kthread[t] to R = 4096*(kiters+1); payload = 16*n_inner bytes
+    const uint64_t nidx = 16ull * n_inner;
+    const uint64_t kiters = (n_inner + kThreads - 1) / kThreads;
+    const uint64_t R = (uint64_t)kWgStride * (kiters + 1);
+    p.idx_c_inv = xpow8_inv(R - nidx);
+    p.idx_c3 = gf_mul(xpow8(nidx), 0xFFFFFFFFu);
+    int rc = launch_shard_pack(p, n_shards, static_cast<hipStream_t>(stream));
     if (rc != ZHIP_OK) return set_err(rc, std::string("launch failed: ") + hipGetErrorString(hipGetLastError()));
     return ZHIP_OK;
 }

@@ -34,153 +34,11 @@
 #include "../../include/zarrhip.h"
 #include "zhip_gf2.h"
 #include "zhip_internal.h"
+#include "zhip_device.h"
 
 namespace zhip {
 
 int g_tune_max_grid = 0;
-
-__device__ __forceinline__ uint32_t bswap_item(uint32_t x, int item) {
-    if (item == 2) return ((x & 0x00FF00FFu) << 8) | ((x >> 8) & 0x00FF00FFu);
-    if (item == 4) return __builtin_bswap32(x);
-    return x;
-}
-
-template <int ITEM, bool SWAP>
-__device__ __forceinline__ uint4 swap_block(uint4 v) {
-    if constexpr (!SWAP || ITEM == 1) {
-        return v;
-    } else if constexpr (ITEM == 8) {
-        return make_uint4(__builtin_bswap32(v.y), __builtin_bswap32(v.x), __builtin_bswap32(v.w),
-                          __builtin_bswap32(v.z));
-    } else {
-        return make_uint4(bswap_item(v.x, ITEM), bswap_item(v.y, ITEM), bswap_item(v.z, ITEM),
-                          bswap_item(v.w, ITEM));
-    }
-}
-
-// Load the 16 chunk bytes [o, o+16) (o a multiple of 16, chunk-relative), zero
-// outside [0, n).  AL4: `cp` is 4-byte aligned -> one dwordx4 load; otherwise
-// five aligned dwords are funnel-shifted.
-__device__ __forceinline__ uint4 mask_tail(uint4 v, int32_t o, uint32_t n) {
-    const uint32_t valid = n - (uint32_t)o;
-    if (valid < 16u) {
-        uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int32_t keep = (int32_t)valid - 4 * i;
-            if (keep <= 0) w[i] = 0;
-            else if (keep < 4) w[i] &= (1u << (8 * keep)) - 1u;
-        }
-        v = make_uint4(w[0], w[1], w[2], w[3]);
-    }
-    return v;
-}
-
-template <bool AL4>
-__device__ __forceinline__ uint4 load_block(const uint8_t* cp, int32_t o, uint32_t n) {
-    if (o < 0 || (uint32_t)o >= n) return make_uint4(0, 0, 0, 0);
-    uint4 v;
-    if constexpr (AL4) {
-        v = *reinterpret_cast<const uint4*>(cp + o);
-    } else {
-        const uintptr_t a = reinterpret_cast<uintptr_t>(cp + o);
-        const uint32_t* b = reinterpret_cast<const uint32_t*>(a & ~uintptr_t(3));
-        const uint32_t sh = (uint32_t)(a & 3u) * 8u;
-        const uint4 lo = *reinterpret_cast<const uint4*>(b);
-        const uint32_t hi = b[4];
-        v.x = (uint32_t)((((uint64_t)lo.y << 32) | lo.x) >> sh);
-        v.y = (uint32_t)((((uint64_t)lo.z << 32) | lo.y) >> sh);
-        v.z = (uint32_t)((((uint64_t)lo.w << 32) | lo.z) >> sh);
-        v.w = (uint32_t)((((uint64_t)hi << 32) | lo.w) >> sh);
-    }
-    return mask_tail(v, o, n);
-}
-
-__device__ __forceinline__ uint32_t tab_apply(const uint32_t* tab, uint32_t w) {
-    return tab[w & 255u] ^ tab[256 + ((w >> 8) & 255u)] ^ tab[512 + ((w >> 16) & 255u)] ^
-           tab[768 + (w >> 24)];
-}
-
-__device__ __forceinline__ uint64_t load_u64_le_bytes(const uint8_t* p) {
-    uint64_t v = 0;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) v |= (uint64_t)p[i] << (8 * i);
-    return v;
-}
-
-// Output byte offset of selected stored-dims coordinates; `rem` is the
-// (flattened, C-order) index over dims [0, last] where `last` = ndim-1 for an
-// element index or ndim-2 for a row index.  Returns false if not selected.
-__device__ __forceinline__ bool sel_offset(const DecodeParams& p, const zhip_sel& s, uint32_t rem,
-                                           int last, int64_t& dst) {
-    bool ok = true;
-#pragma unroll
-    for (int d = ZHIP_MAX_DIMS - 1; d >= 0; --d) {
-        if (d > last) continue;
-        uint32_t q = d > 0 ? fdiv_apply(rem, p.dshape[d].m, p.dshape[d].s) : 0u;
-        const int32_t sd = (int32_t)(rem - q * (uint32_t)p.shape[d]);
-        if (d == 0) { /* rem < shape[0] for in-range indices */
-            q = 0;
-        }
-        rem = q;
-        const int32_t rel = sd - s.start[d];
-        const uint32_t kq = fdiv_apply((uint32_t)max(rel, 0), s.div_step[d].m, s.div_step[d].s);
-        ok = ok && rel >= 0 && (int32_t)(kq * (uint32_t)s.step[d]) == rel && (int32_t)kq < s.count[d];
-        dst += (int64_t)kq * p.ostride[d];
-    }
-    return ok;
-}
-
-template <int ITEM, bool SWAP>
-__device__ __forceinline__ void store_item(uint8_t* dst, uint32_t lo, uint32_t hi) {
-    if constexpr (ITEM == 1) {
-        *dst = (uint8_t)lo;
-    } else if constexpr (ITEM == 2) {
-        uint16_t v = (uint16_t)lo;
-        if constexpr (SWAP) v = (uint16_t)((v >> 8) | (v << 8));
-        *reinterpret_cast<uint16_t*>(dst) = v;
-    } else if constexpr (ITEM == 4) {
-        *reinterpret_cast<uint32_t*>(dst) = SWAP ? __builtin_bswap32(lo) : lo;
-    } else {
-        uint2 v = SWAP ? make_uint2(__builtin_bswap32(hi), __builtin_bswap32(lo)) : make_uint2(lo, hi);
-        *reinterpret_cast<uint2*>(dst) = v;
-    }
-}
-
-// Scatter one 16-byte block (chunk bytes [o, o+16), whole items) element by element.
-template <int ITEM, bool SWAP>
-__device__ __forceinline__ void scatter_block_generic(const DecodeParams& p, const zhip_sel& s,
-                                                      int64_t out_off, int32_t o, uint4 v) {
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-    constexpr int kItems = 16 / ITEM;
-    const uint32_t e0 = (uint32_t)o / ITEM;
-#pragma unroll
-    for (int j = 0; j < kItems; ++j) {
-        if ((uint32_t)o + (uint32_t)(j * ITEM) >= p.nbytes) break;
-        int64_t dst = out_off;
-        if (!sel_offset(p, s, e0 + j, p.ndim - 1, dst)) continue;
-        uint32_t lo, hi = 0;
-        if constexpr (ITEM == 8) {
-            lo = w[2 * j];
-            hi = w[2 * j + 1];
-        } else {
-            lo = (w[(j * ITEM) / 4] >> (8 * ((j * ITEM) % 4))) & (ITEM == 4 ? 0xFFFFFFFFu : ((1u << (8 * ITEM)) - 1u));
-        }
-        store_item<ITEM, SWAP>(p.out + dst, lo, hi);
-    }
-}
-
-// Whole-row fast path: rows of the innermost stored dim are fully selected,
-// contiguous in out and a multiple of 16 bytes, out rows 16-byte aligned.
-template <int ITEM, bool SWAP>
-__device__ __forceinline__ void scatter_block_rows(const DecodeParams& p, const zhip_sel& s,
-                                                   int64_t out_off, int32_t o, uint4 v) {
-    const uint32_t r = fdiv_apply((uint32_t)o, p.drow.m, p.drow.s);
-    const uint32_t col = (uint32_t)o - r * p.row_bytes;
-    int64_t dst = out_off + col;
-    if (!sel_offset(p, s, r, p.ndim - 2, dst)) return;
-    *reinterpret_cast<uint4*>(p.out + dst) = swap_block<ITEM, SWAP>(v);
-}
 
 // Per-unit context (wave-uniform).
 struct Unit {
@@ -235,11 +93,11 @@ __device__ __forceinline__ void load_unit(const DecodeParams& p, const Unit& U, 
     } else if (al4) {
 #pragma unroll
         for (int k = 0; k < K; ++k)
-            blk[k] = load_block<true>(U.cp, U.seg_lo + kWgStride * k + 16 * t, p.nbytes);
+            blk[k] = load_block<true>(U.cp, U.seg_lo + kWgStride * k + 16 * t, p.g.nbytes);
     } else {
 #pragma unroll
         for (int k = 0; k < K; ++k)
-            blk[k] = load_block<false>(U.cp, U.seg_lo + kWgStride * k + 16 * t, p.nbytes);
+            blk[k] = load_block<false>(U.cp, U.seg_lo + kWgStride * k + 16 * t, p.g.nbytes);
     }
 }
 
@@ -296,7 +154,7 @@ __global__ __launch_bounds__(kThreads) void k_decode(const DecodeParams p) {
         for (int i = t; i < 1024; i += kThreads) sv[i] = g[i];
         kth = p.kthread[t];
     }
-    const uint32_t expected = p.nbytes + (CRC ? 4u : 0u);
+    const uint32_t expected = p.g.nbytes + (CRC ? 4u : 0u);
     // one 64-bit arrival word per chunk: high half = bitmask of arrived units, low = xor
     const bool one_atomic = p.nseg <= 32 && !(p.tune & (kTuneAcqRel | kTuneNoTicket));
     const uint64_t full = p.nseg >= 32 ? 0xFFFFFFFFull : ((1ull << p.nseg) - 1ull);
@@ -316,7 +174,7 @@ __global__ __launch_bounds__(kThreads) void k_decode(const DecodeParams p) {
     Unit ua = resolve_unit(p, unit_of(q0), expected);
     load_unit<K>(p, ua, t, A);
     uint32_t stored = 0;
-    if (CRC && t == 0 && ua.mode == ZHIP_ST_OK) stored = load_trailer(ua.cp, p.nbytes);
+    if (CRC && t == 0 && ua.mode == ZHIP_ST_OK) stored = load_trailer(ua.cp, p.g.nbytes);
     if constexpr (CRC) __syncthreads();  // tables in LDS
     uint32_t acc = 0, run_bits = 0, run_len = 0, parity = 0;
     for (uint32_t q = q0;;) {
@@ -337,9 +195,9 @@ __global__ __launch_bounds__(kThreads) void k_decode(const DecodeParams p) {
 #pragma unroll
                 for (int k = 0; k < K; ++k) {
                     const int32_t o = ua.seg_lo + kWgStride * k + 16 * t;
-                    if (o < 0 || (uint32_t)o >= p.nbytes) continue;
-                    if constexpr (FAST) scatter_block_rows<ITEM, SWAP>(p, sel, ua.out_off, o, A[k]);
-                    else scatter_block_generic<ITEM, SWAP>(p, sel, ua.out_off, o, A[k]);
+                    if (o < 0 || (uint32_t)o >= p.g.nbytes) continue;
+                    if constexpr (FAST) scatter_block_rows<ITEM, SWAP>(p.g, p.out, sel, ua.out_off, o, A[k]);
+                    else scatter_block_generic<ITEM, SWAP>(p.g, p.out, sel, ua.out_off, o, A[k]);
                 }
             }
             if (crc_on) {
@@ -420,9 +278,9 @@ __global__ __launch_bounds__(kThreads) void k_decode(const DecodeParams p) {
 #pragma unroll
                     for (int k = 0; k < K; ++k) {
                         const int32_t o = ua.seg_lo + kWgStride * k + 16 * t;
-                        if (o < 0 || (uint32_t)o >= p.nbytes) continue;
-                        if constexpr (FAST) scatter_block_rows<ITEM, false>(p, sel, ua.out_off, o, f);
-                        else scatter_block_generic<ITEM, false>(p, sel, ua.out_off, o, f);
+                        if (o < 0 || (uint32_t)o >= p.g.nbytes) continue;
+                        if constexpr (FAST) scatter_block_rows<ITEM, false>(p.g, p.out, sel, ua.out_off, o, f);
+                        else scatter_block_generic<ITEM, false>(p.g, p.out, sel, ua.out_off, o, f);
                     }
                 }
             }
@@ -433,7 +291,7 @@ __global__ __launch_bounds__(kThreads) void k_decode(const DecodeParams p) {
             }
         }
         if (!more) break;
-        if (CRC && t == 0 && ub.c != ua.c && ub.mode == ZHIP_ST_OK) stored = load_trailer(ub.cp, p.nbytes);
+        if (CRC && t == 0 && ub.c != ua.c && ub.mode == ZHIP_ST_OK) stored = load_trailer(ub.cp, p.g.nbytes);
         q = qn;
         ua = ub;
 #pragma unroll
@@ -473,7 +331,7 @@ KernelFn select_decode_kernel(bool crc, bool write, bool fast, int item, bool sw
 int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
     if (g_tune_max_grid > 0) max_grid = g_tune_max_grid;
     KernelFn fn = select_decode_kernel((p.lflags & ZHIP_LF_CRC) != 0, (p.lflags & ZHIP_LF_NO_WRITE) == 0,
-                                       p.fast != 0, p.itemsize, (p.lflags & ZHIP_LF_SWAP) != 0,
+                                       p.fast != 0, p.g.itemsize, (p.lflags & ZHIP_LF_SWAP) != 0,
                                        (int)(p.seg / kWgStride));
     if (!fn) return ZHIP_E_UNSUPPORTED;
     if (p.n_units == 0) return ZHIP_OK;

@@ -1,0 +1,383 @@
+// Fused zarr v3 encode for MI355X (gfx950): gather each chunk from a device
+// array (transpose folded into the stored-dim strides), byteswap to the stored
+// endian, write the encoded bytes, append the CRC-32C trailer and flag chunks
+// that equal the fill value; plus the shard packer (Morton-ordered layout,
+// empty-chunk elision, index + index CRC).
+//
+// Reference behaviour restated (file:line under /root/reference):
+//   _merge_chunk_array (edge chunks: outside the selection = fill)
+//                                   src/zarr/core/chunk_utils.py:115-162
+//   chunk_is_empty / all_equal      chunk_utils.py:74-85, src/zarr/core/buffer/core.py:534-558
+//   TransposeCodec._encode_sync     src/zarr/codecs/transpose.py:113-118
+//   BytesCodec._encode_sync         src/zarr/codecs/bytes.py:140-158
+//   Crc32cCodec._encode_sync        src/zarr/codecs/crc32c_.py:59-68
+//   ShardingCodec._build_shard_layout / _assemble_shard / _encode_shard_index_sync
+//                                   src/zarr/codecs/sharding.py:887-950, 633-640
+//   Morton order                    src/zarr/core/indexing.py:1578-1643 (rank table from host)
+//
+// The unit decomposition and CRC combine are those of decode.hip (see there):
+// the stored byte stream [0, N) is cut into end-aligned units of 4 KiB * K,
+// thread t of a unit owns the 16-byte blocks at lo + 16t + 4096k.
+#include <hip/hip_runtime.h>
+
+#include "../../include/zarrhip.h"
+#include "zhip_device.h"
+#include "zhip_gf2.h"
+#include "zhip_internal.h"
+
+namespace zhip {
+
+// Element equality with the fill value as NDBuffer.all_equal defines it:
+// bitwise, except that any NaN equals a NaN fill (equal_nan=True); a 0.0 fill
+// compares bit patterns (so -0.0 != 0.0), which bitwise equality gives.
+template <int ITEM>
+__device__ __forceinline__ bool item_eq_fill(uint32_t lo, uint32_t hi, const EncodeParams& p) {
+    if constexpr (ITEM == 8) {
+        const bool eq = lo == p.fill[0] && hi == p.fill[1];
+        if (!p.fill_nan) return eq;
+        const uint64_t v = ((uint64_t)hi << 32) | lo;
+        return eq || (v & 0x7FFFFFFFFFFFFFFFull) > 0x7FF0000000000000ull;
+    } else {
+        constexpr uint32_t mask = ITEM == 4 ? 0xFFFFFFFFu : ((1u << (8 * ITEM)) - 1u);
+        const bool eq = (lo & mask) == (p.fill[0] & mask);
+        if (!p.fill_nan) return eq;
+        if constexpr (ITEM == 4) return eq || (lo & 0x7FFFFFFFu) > 0x7F800000u;
+        if constexpr (ITEM == 2) return eq || (lo & 0x7FFFu) > 0x7C00u;
+        return eq;
+    }
+}
+
+template <int ITEM>
+__device__ __forceinline__ bool block_eq_fill(uint4 v, uint32_t valid, const EncodeParams& p) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    bool all = true;
+    constexpr int kItems = 16 / ITEM;
+#pragma unroll
+    for (int j = 0; j < kItems; ++j) {
+        if ((uint32_t)(j * ITEM) >= valid) break;
+        uint32_t lo, hi = 0;
+        if constexpr (ITEM == 8) {
+            lo = w[2 * j];
+            hi = w[2 * j + 1];
+        } else {
+            lo = w[(j * ITEM) / 4] >> (8 * ((j * ITEM) % 4));
+        }
+        all = all && item_eq_fill<ITEM>(lo, hi, p);
+    }
+    return all;
+}
+
+template <int ITEM>
+__device__ __forceinline__ void load_item(const uint8_t* src, uint32_t& lo, uint32_t& hi) {
+    if constexpr (ITEM == 1) lo = *src;
+    else if constexpr (ITEM == 2) lo = *reinterpret_cast<const uint16_t*>(src);
+    else if constexpr (ITEM == 4) lo = *reinterpret_cast<const uint32_t*>(src);
+    else {
+        const uint2 v = *reinterpret_cast<const uint2*>(src);
+        lo = v.x;
+        hi = v.y;
+    }
+}
+
+// Gather the 16 stored bytes [o, o+16) of a chunk from the array (native
+// order): selected elements from `arr`, the rest = fill.
+template <int ITEM, bool FAST>
+__device__ __forceinline__ uint4 gather_block(const EncodeParams& p, const zhip_sel& s, int64_t arr_off,
+                                              int32_t o) {
+    if constexpr (FAST) {
+        const uint32_t r = fdiv_apply((uint32_t)o, p.g.drow.m, p.g.drow.s);
+        const uint32_t col = (uint32_t)o - r * p.g.row_bytes;
+        int64_t src = arr_off + col;
+        if (!sel_offset(p.g, s, r, p.g.ndim - 2, src)) return make_uint4(p.fill[0], p.fill[1], p.fill[2], p.fill[3]);
+        return *reinterpret_cast<const uint4*>(p.arr + src);
+    } else {
+        uint32_t w[4] = {p.fill[0], p.fill[1], p.fill[2], p.fill[3]};
+        constexpr int kItems = 16 / ITEM;
+        const uint32_t e0 = (uint32_t)o / ITEM;
+#pragma unroll
+        for (int j = 0; j < kItems; ++j) {
+            if ((uint32_t)o + (uint32_t)(j * ITEM) >= p.g.nbytes) break;
+            int64_t src = arr_off;
+            if (!sel_offset(p.g, s, e0 + j, p.g.ndim - 1, src)) continue;
+            uint32_t lo = 0, hi = 0;
+            load_item<ITEM>(p.arr + src, lo, hi);
+            if constexpr (ITEM == 8) {
+                w[2 * j] = lo;
+                w[2 * j + 1] = hi;
+            } else if constexpr (ITEM == 4) {
+                w[j] = lo;
+            } else {
+                constexpr uint32_t m = (1u << (8 * ITEM)) - 1u;
+                const int sh = 8 * ((j * ITEM) % 4);
+                w[(j * ITEM) / 4] = (w[(j * ITEM) / 4] & ~(m << sh)) | ((lo & m) << sh);
+            }
+        }
+        return make_uint4(w[0], w[1], w[2], w[3]);
+    }
+}
+
+// Store the 16 encoded bytes at dst (chunk-relative block o), only [0, valid).
+__device__ __forceinline__ void store_block(uint8_t* cp, int32_t o, uint4 v, uint32_t valid, bool al4) {
+    if (valid >= 16u && al4) {
+        *reinterpret_cast<uint4*>(cp + o) = v;
+        return;
+    }
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    const uint32_t n = valid < 16u ? valid : 16u;
+    for (uint32_t i = 0; i < n; ++i) cp[o + i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3u)));
+}
+
+template <bool CRC, bool FAST, int ITEM, bool SWAP>
+__global__ __launch_bounds__(kThreads) void k_encode(const EncodeParams p) {
+    constexpr int K = kDefaultBlocks;
+    __shared__ uint32_t s_tab[CRC ? 16 * 256 : 1];
+    __shared__ uint32_t s_red[2][kThreads / 64];
+    const int t = threadIdx.x;
+    uint32_t kth = 0;
+    if constexpr (CRC) {
+        const uint4* g = reinterpret_cast<const uint4*>(p.horner);
+        uint4* sv = reinterpret_cast<uint4*>(s_tab);
+        for (int i = t; i < 1024; i += kThreads) sv[i] = g[i];
+        kth = p.kthread[t];
+        __syncthreads();
+    }
+    const uint32_t G = gridDim.x, gi = blockIdx.x;
+    const uint32_t per = p.n_units / G, rem = p.n_units % G;
+    const uint32_t q0 = gi * per + (gi < rem ? gi : rem);
+    const uint32_t q1 = q0 + per + (gi < rem ? 1u : 0u);
+    uint32_t acc = 0, parity = 0;
+    bool alleq = true;
+    for (uint32_t q = q0; q < q1; ++q) {
+        const uint32_t c = q / p.nseg;
+        const uint32_t sidx = p.nseg - 1u - (q - c * p.nseg);
+        const zhip_chunk ch = p.chunks[c];
+        const zhip_sel& sel = p.sels[ch.sel];
+        uint8_t* cp = p.dst + ch.src;
+        const bool al4 = __builtin_amdgcn_readfirstlane((uint32_t)(reinterpret_cast<uintptr_t>(cp) & 3u)) == 0u;
+        const int32_t seg_lo = (int32_t)p.E - (int32_t)((sidx + 1u) * p.seg);
+        uint4 blk[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int32_t o = seg_lo + kWgStride * k + 16 * t;
+            blk[k] = (o < 0 || (uint32_t)o >= p.g.nbytes) ? make_uint4(0, 0, 0, 0)
+                                                          : gather_block<ITEM, FAST>(p, sel, ch.out_off, o);
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int32_t o = seg_lo + kWgStride * k + 16 * t;
+            if (o < 0 || (uint32_t)o >= p.g.nbytes) continue;
+            const uint32_t valid = p.g.nbytes - (uint32_t)o;
+            alleq = alleq && block_eq_fill<ITEM>(blk[k], valid, p);
+            blk[k] = mask_tail(swap_block<ITEM, SWAP>(blk[k]), o, p.g.nbytes);
+            store_block(cp, o, blk[k], valid, al4);
+        }
+        if constexpr (CRC) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const uint4 v = blk[k];
+                acc = tab_apply(s_tab, acc ^ v.x) ^ tab_apply(s_tab + 1024, v.y) ^ tab_apply(s_tab + 2048, v.z) ^
+                      tab_apply(s_tab + 3072, v.w);
+            }
+        }
+        const bool run_end = (q + 1 >= q1) || ((q + 1) / p.nseg != c);
+        if (run_end) {
+            // chunk_is_empty: any element != fill anywhere in the chunk -> non-empty
+            if (__any(!alleq) && (t & 63) == 0) atomicOr(p.nonempty + c, 1u);
+            alleq = true;
+            if constexpr (CRC) {
+                uint32_t v = gf_mul(acc, kth);
+#pragma unroll
+                for (int off = 32; off > 0; off >>= 1) v ^= __shfl_xor(v, off, 64);
+                if ((t & 63) == 0) s_red[parity][t >> 6] = v;
+                __syncthreads();
+                if (t == 0) {
+                    uint32_t V = s_red[parity][0] ^ s_red[parity][1] ^ s_red[parity][2] ^ s_red[parity][3];
+                    V = gf_mul(V, p.kunit[sidx]);
+                    uint32_t* accw = p.ws + 4ull * c;
+                    const uint32_t prev = __hip_atomic_fetch_xor(accw, V, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    asm volatile("s_waitcnt vmcnt(0)" ::"v"(prev) : "memory");
+                    const uint32_t run_len = q + 1u - (q0 > c * p.nseg ? q0 : c * p.nseg);
+                    const uint32_t tk =
+                        __hip_atomic_fetch_add(accw + 2, run_len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (tk + run_len == p.nseg) {
+                        const uint32_t raw = __hip_atomic_exchange(accw, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store(accw + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        const uint32_t crc = ~(gf_mul(raw, p.c_inv) ^ p.c3);
+                        uint8_t* tr = cp + p.g.nbytes;  // LE trailer (crc32c_.py:64-68)
+                        tr[0] = (uint8_t)crc;
+                        tr[1] = (uint8_t)(crc >> 8);
+                        tr[2] = (uint8_t)(crc >> 16);
+                        tr[3] = (uint8_t)(crc >> 24);
+                        zhip_status st = {ZHIP_ST_OK, crc, crc, 0u};
+                        p.status[c] = st;
+                    }
+                }
+                parity ^= 1u;
+                acc = 0;
+            } else if (t == 0 && sidx == 0) {
+                zhip_status st = {ZHIP_ST_OK, 0u, 0u, 0u};
+                p.status[c] = st;
+            }
+        }
+    }
+}
+
+using EncodeFn = void (*)(const EncodeParams);
+
+template <bool CRC, bool FAST>
+static EncodeFn pick_encode(int item, bool swap) {
+    switch (item) {
+        case 1: return k_encode<CRC, FAST, 1, false>;
+        case 2: return swap ? k_encode<CRC, FAST, 2, true> : k_encode<CRC, FAST, 2, false>;
+        case 4: return swap ? k_encode<CRC, FAST, 4, true> : k_encode<CRC, FAST, 4, false>;
+        case 8: return swap ? k_encode<CRC, FAST, 8, true> : k_encode<CRC, FAST, 8, false>;
+        default: return nullptr;
+    }
+}
+
+int launch_encode(const EncodeParams& p, hipStream_t stream, int max_grid) {
+    const bool crc = (p.lflags & ZHIP_LF_CRC) != 0;
+    const bool swap = (p.lflags & ZHIP_LF_SWAP) != 0;
+    EncodeFn fn = crc ? (p.fast ? pick_encode<true, true>(p.g.itemsize, swap) : pick_encode<true, false>(p.g.itemsize, swap))
+                      : (p.fast ? pick_encode<false, true>(p.g.itemsize, swap) : pick_encode<false, false>(p.g.itemsize, swap));
+    if (!fn) return ZHIP_E_UNSUPPORTED;
+    if (p.n_units == 0) return ZHIP_OK;
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(fn), kThreads, 0) ==
+            hipSuccess && per_cu > 0)
+        max_grid = (max_grid / 8) * per_cu;
+    if (g_tune_max_grid > 0) max_grid = g_tune_max_grid;
+    const uint32_t grid = p.n_units < (uint32_t)max_grid ? p.n_units : (uint32_t)max_grid;
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(kThreads), 0, stream, p);
+    return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
+}
+
+// ---------------------------------------------------------------------------
+// Shard packing: one workgroup per shard.
+//   in : inner chunks already encoded densely in Morton-rank order at
+//        blob + data_start + rank * elen; nonempty flags per inner chunk
+//   out: present chunks compacted (rare path: only when some inner chunk is
+//        empty), index (LE u64 offset/length, MAX_UINT_64 for absent) + CRC
+//        written, blob length reported (0 = all empty: delete the shard key).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void put_u32_bytes(uint8_t* d, uint32_t v) {
+    d[0] = (uint8_t)v;
+    d[1] = (uint8_t)(v >> 8);
+    d[2] = (uint8_t)(v >> 16);
+    d[3] = (uint8_t)(v >> 24);
+}
+
+__global__ __launch_bounds__(kThreads) void k_shard_pack(const PackParams p) {
+    __shared__ uint32_t s_tab[16 * 256];
+    __shared__ uint32_t s_scan[kThreads];
+    __shared__ uint32_t s_red[kThreads / 64];
+    __shared__ uint32_t s_total;
+    const int t = threadIdx.x;
+    const uint32_t sh = blockIdx.x;
+    const zhip_shard ps = p.shards[sh];
+    uint8_t* blob = p.dst + ps.blob;
+    const uint32_t n = p.n_inner;
+    const uint32_t data_start = p.index_start ? p.index_size : 0u;
+    if (p.index_crc) {
+        const uint4* g = reinterpret_cast<const uint4*>(p.horner);
+        uint4* sv = reinterpret_cast<uint4*>(s_tab);
+        for (int i = t; i < 1024; i += kThreads) sv[i] = g[i];
+    }
+    // 1. present flags in rank order -> exclusive scan (chunks of 256 ranks)
+    const uint32_t* ne = p.nonempty + ps.first_chunk;  // indexed by rank
+    uint32_t carry = 0;
+    for (uint32_t base = 0; base < n; base += kThreads) {
+        const uint32_t r = base + t;
+        const uint32_t pr = (r < n) ? ((p.keep_empty || ne[r]) ? 1u : 0u) : 0u;
+        s_scan[t] = pr;
+        __syncthreads();
+        for (int off = 1; off < kThreads; off <<= 1) {
+            const uint32_t v = t >= off ? s_scan[t - off] : 0u;
+            __syncthreads();
+            s_scan[t] += v;
+            __syncthreads();
+        }
+        const uint32_t incl = s_scan[t];
+        const uint32_t tot = s_scan[kThreads - 1];
+        __syncthreads();
+        if (r < n) {
+            const uint32_t newrank = carry + incl - pr;
+            p.newrank[ps.first_chunk + r] = pr ? newrank : 0xFFFFFFFFu;
+        }
+        carry += tot;
+    }
+    if (t == 0) s_total = carry;
+    __syncthreads();
+    const uint32_t n_present = s_total;
+    const bool dense = n_present == n;
+    // 2. compaction (only when some inner chunk is empty), in increasing rank
+    //    order so a move never overwrites a chunk that has not moved yet
+    if (!dense) {
+        for (uint32_t r = 0; r < n; ++r) {
+            const uint32_t nr = p.newrank[ps.first_chunk + r];
+            __syncthreads();
+            if (nr == 0xFFFFFFFFu || nr == r) continue;
+            uint8_t* from = blob + data_start + (uint64_t)r * p.elen;
+            uint8_t* to = blob + data_start + (uint64_t)nr * p.elen;
+            for (uint32_t i = t; i < p.elen; i += kThreads) to[i] = from[i];
+        }
+        __syncthreads();
+    }
+    if (n_present == 0) {
+        if (t == 0) p.blob_len[sh] = 0;
+        return;
+    }
+    const uint64_t blen = (uint64_t)n_present * p.elen + p.index_size;
+    uint8_t* ix = blob + (p.index_start ? 0ull : (uint64_t)n_present * p.elen);
+    // 3. index entries in C order: entry i at ix + 16 i; Horner CRC over them
+    //    with the 4096-byte-stride tables (thread t owns entries t + 256 k)
+    __syncthreads();
+    uint32_t acc = 0;
+    const uint32_t kiters = (n + kThreads - 1) / kThreads;
+    for (uint32_t k = 0; k < kiters; ++k) {
+        const uint32_t i = k * kThreads + t;
+        uint32_t w[4] = {0u, 0u, 0u, 0u};
+        if (i < n) {
+            const uint32_t r = p.rank_of_slot[i];
+            const uint32_t nr = p.newrank[ps.first_chunk + r];
+            if (nr == 0xFFFFFFFFu) {
+                w[0] = w[1] = w[2] = w[3] = 0xFFFFFFFFu;
+            } else {
+                const uint64_t off = (uint64_t)data_start + (uint64_t)nr * p.elen;
+                w[0] = (uint32_t)off;
+                w[1] = (uint32_t)(off >> 32);
+                w[2] = p.elen;
+                w[3] = 0u;
+            }
+            uint8_t* e = ix + 16ull * i;
+            put_u32_bytes(e, w[0]);
+            put_u32_bytes(e + 4, w[1]);
+            put_u32_bytes(e + 8, w[2]);
+            put_u32_bytes(e + 12, w[3]);
+        }
+        if (p.index_crc)
+            acc = tab_apply(s_tab, acc ^ w[0]) ^ tab_apply(s_tab + 1024, w[1]) ^ tab_apply(s_tab + 2048, w[2]) ^
+                  tab_apply(s_tab + 3072, w[3]);
+    }
+    if (p.index_crc) {
+        uint32_t v = gf_mul(acc, p.kthread[t]);
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v ^= __shfl_xor(v, off, 64);
+        if ((t & 63) == 0) s_red[t >> 6] = v;
+        __syncthreads();
+        if (t == 0) {
+            const uint32_t V = s_red[0] ^ s_red[1] ^ s_red[2] ^ s_red[3];
+            const uint32_t crc = ~(gf_mul(V, p.idx_c_inv) ^ p.idx_c3);
+            put_u32_bytes(ix + 16ull * n, crc);
+        }
+    }
+    if (t == 0) p.blob_len[sh] = blen;
+}
+
+int launch_shard_pack(const PackParams& p, uint32_t n_shards, hipStream_t stream) {
+    if (n_shards == 0) return ZHIP_OK;
+    hipLaunchKernelGGL(k_shard_pack, dim3(n_shards), dim3(kThreads), 0, stream, p);
+    return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
+}
+
+}  // namespace zhip

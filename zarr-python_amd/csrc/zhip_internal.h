@@ -11,6 +11,17 @@ constexpr int kThreads = 256;                            // one workgroup = 4 wa
 constexpr int kWgStride = kThreads * 16;                 // 4 KiB per workgroup step
 constexpr int kDefaultBlocks = 8;                        // 16-byte blocks per thread per unit
 
+// Stored-chunk geometry + out mapping (shared by decode and encode).
+struct Geom {
+    int32_t ndim, itemsize;
+    int32_t shape[ZHIP_MAX_DIMS];
+    int64_t ostride[ZHIP_MAX_DIMS];
+    zhip_fdiv dshape[ZHIP_MAX_DIMS];
+    uint32_t nbytes;  // N (< 2^31)
+    uint32_t row_bytes;
+    zhip_fdiv drow;
+};
+
 // Kernel argument block (passed by value; indexed only with compile-time
 // subscripts inside the kernels so it stays in SGPRs / kernarg memory).
 struct DecodeParams {
@@ -28,15 +39,9 @@ struct DecodeParams {
     uint32_t n_chunks, nseg, n_units;
     uint32_t c_inv, c3;
     uint32_t lflags;
-    int32_t ndim, itemsize;
-    int32_t shape[ZHIP_MAX_DIMS];
-    int64_t ostride[ZHIP_MAX_DIMS];
-    zhip_fdiv dshape[ZHIP_MAX_DIMS];
+    Geom g;
     uint32_t seg;     // bytes per unit = kWgStride * K
-    uint32_t nbytes;  // N (< 2^31)
     uint32_t E;       // align16(N)
-    uint32_t row_bytes;
-    zhip_fdiv drow;
     uint32_t index_size, n_inner;
     uint32_t fill[4];
     uint32_t fast;
@@ -51,9 +56,50 @@ extern int g_tune_max_grid;
 extern int g_tune_blocks;
 extern uint32_t g_tune_bits;
 
+struct EncodeParams {
+    const uint8_t* arr;   // source array base (device)
+    uint8_t* dst;         // encoded destination buffer
+    const zhip_chunk* chunks;  // src = dst offset of the encoded chunk, out_off = arr offset
+    const zhip_sel* sels;
+    zhip_status* status;
+    uint32_t* ws;
+    uint32_t* nonempty;
+    const uint32_t* horner;
+    const uint32_t* kthread;
+    const uint32_t* kunit;
+    uint32_t n_chunks, nseg, n_units;
+    uint32_t c_inv, c3;
+    uint32_t lflags;
+    Geom g;
+    uint32_t seg, E;
+    uint32_t fill[4];
+    uint32_t fill_nan;
+    uint32_t fast;
+};
+
+struct PackParams {
+    uint8_t* dst;
+    const zhip_shard* shards;
+    const uint32_t* nonempty;      // per inner chunk, chunk id = first_chunk + Morton rank
+    uint32_t* newrank;             // scratch per inner chunk
+    const uint32_t* rank_of_slot;  // C-order slot -> Morton rank
+    uint64_t* blob_len;            // out, per shard
+    const uint32_t* horner;
+    const uint32_t* kthread;
+    uint32_t n_inner, elen, index_size, index_start, index_crc, keep_empty;
+    uint32_t idx_c_inv, idx_c3;
+};
+
 int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid);
+int launch_encode(const EncodeParams& p, hipStream_t stream, int max_grid);
+int launch_shard_pack(const PackParams& p, uint32_t n_shards, hipStream_t stream);
 
 }  // namespace zhip
+
+struct zhip_plan;
+namespace zhip {
+void fill_geom(Geom& g, const zhip_plan& plan);
+}
 
 struct zhip_plan {
     zhip_layout layout;

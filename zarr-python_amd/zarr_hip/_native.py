@@ -23,10 +23,15 @@ LF_SWAP = 2
 LF_SHARDED = 4
 LF_INDEX_START = 8
 LF_NO_WRITE = 16
+LF_FLOAT = 32
 
 CF_MISSING = 1
 
 DF_FAST_ROWS = 1
+
+PF_INDEX_START = 1
+PF_INDEX_CRC = 2
+PF_KEEP_EMPTY = 4
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "_lib", "libzarrhip.so")
@@ -126,6 +131,15 @@ def lib():
                               ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
                               ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
     L.zhip_decode.restype = ctypes.c_int
+    L.zhip_encode.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                              ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                              ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
+    L.zhip_encode.restype = ctypes.c_int
+    L.zhip_shard_pack.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                  ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                  ctypes.c_void_p]
+    L.zhip_shard_pack.restype = ctypes.c_int
     L.zhip_set_tuning.argtypes = [ctypes.c_int, ctypes.c_int]
     L.zhip_set_tuning.restype = ctypes.c_int
     L.zhip_selftest.restype = ctypes.c_int

@@ -191,6 +191,25 @@ class Array:
     def __getitem__(self, selection) -> np.ndarray:
         return buffer.to_numpy(self.get(selection), self.metadata.dtype)
 
+    # ------------------------------------------------------------------ write
+    def set(self, selection, value) -> None:
+        """Array._set_selection (array.py:5563-5675): value may be a device
+        tensor, a numpy array or a scalar."""
+        batch, out_shape = self.batch_info(selection)
+        if not batch:
+            return
+        import torch
+
+        if not isinstance(value, torch.Tensor):
+            a = np.asarray(value, dtype=self.metadata.dtype)
+            if a.shape not in ((), tuple(out_shape)):
+                a = np.broadcast_to(a, out_shape)
+            value = a
+        self.codec_pipeline.write_sync(batch, value)
+
+    def __setitem__(self, selection, value) -> None:
+        self.set(selection, value)
+
 
 class ChunkNotFoundError(KeyError):
     """array.py:5496-5511 (read_missing_chunks=False)."""

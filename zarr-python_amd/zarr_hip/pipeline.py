@@ -280,6 +280,28 @@ class HipCodecPipeline:
         # one thread hop per batch, as FusedCodecPipeline.read (codec_pipeline.py:1287-1289)
         return await asyncio.to_thread(self.read_sync, list(batch_info), out, drop_axes)
 
+    # --------------------------------------------------------------- write
+    def write_sync(self, batch_info: Iterable, value, drop_axes: tuple = (),
+                   max_workers: int = 1) -> None:
+        """FusedCodecPipeline.write_sync (codec_pipeline.py:1174-1253) on the GPU."""
+        from .writer import ChunkWriter
+
+        torch = _torch()
+        batch = list(batch_info)
+        if not batch:
+            return
+        spec: ArraySpec = batch[0][1]
+        device = value.device if isinstance(value, torch.Tensor) and value.is_cuda else None
+        if device is None:
+            st = getattr(batch[0][0], "store", None)
+            device = getattr(st, "device", None) or torch.device("cuda", torch.cuda.current_device())
+        with torch.cuda.device(device):
+            w = ChunkWriter(self.codecs, spec, None or spec.shape, device)
+            w.write(batch, value, self.codecs, drop_axes)
+
+    async def write(self, batch_info: Iterable, value, drop_axes: tuple = ()) -> None:
+        await asyncio.to_thread(self.write_sync, list(batch_info), value, drop_axes)
+
     async def decode(self, chunk_bytes_and_specs: Iterable) -> list:
         """Decode standalone chunks (Buffer | None, ArraySpec) -> device arrays."""
         torch = _torch()

@@ -167,6 +167,36 @@ def _fast_ok(layout: N.Layout, start, count, step, out_offs, out_base_ptr: int) 
                 and np.all(step[:, last] == 1))
 
 
+def plan_encode(chain: ChainInfo, spec: ArraySpec, items: list, arr_strides_bytes,
+                arr_base_ptr: int) -> Tables:
+    """items: list of (dst_off, chunk_selection, arr_selection_start) for whole
+    chunks (unsharded chain).  chunk_selection is over decoded dims; elements
+    outside it are encoded as the fill value."""
+    ndim = spec.ndim
+    itemsize = spec.dtype.itemsize
+    perm = chain.perm
+    shape_st = [spec.shape[p] for p in perm]
+    ost = np.asarray(arr_strides_bytes, np.int64)
+    ost_st = [int(ost[p]) for p in perm]
+    flags = (N.LF_CRC if chain.crc else 0) | (N.LF_SWAP if chain.swap else 0) | \
+        (N.LF_FLOAT if spec.dtype.kind == "f" else 0)
+    layout = _make_layout(shape_st, itemsize, ost_st, flags, spec.fill_bytes())
+    n = len(items)
+    chunks = np.zeros(n, CHUNK_DT)
+    start = np.zeros((n, ndim), np.int64)
+    count = np.zeros((n, ndim), np.int64)
+    step = np.ones((n, ndim), np.int64)
+    for i, (dst, csel, astart) in enumerate(items):
+        st, ct, sp, _ = _sel_fields(csel, ndim)
+        start[i], count[i], step[i] = st[list(perm)], ct[list(perm)], sp[list(perm)]
+        chunks["src"][i] = dst
+        chunks["out_off"][i] = int(sum(int(a) * int(o) for a, o in zip(astart, ost)))
+    sels, inv = _pack_sels(start, count, step)
+    chunks["sel"] = inv
+    fast = _fast_ok(layout, start, count, step, chunks["out_off"], arr_base_ptr)
+    return Tables(layout, chunks, sels, fast, np.arange(n))
+
+
 def plan_decode(chain: ChainInfo, spec: ArraySpec, items: list, out_strides_bytes,
                 out_base_ptr: int, drop_axes=()) -> Tables:
     """items: list of (src_off, src_len, missing, chunk_selection, out_selection)."""

@@ -220,6 +220,10 @@ class DeviceStore:
         self._index[key] = (off, nbytes)
         return off
 
+    def register(self, key: str, off: int, nbytes: int) -> None:
+        """Bind a key to bytes already written in the arena (device encode output)."""
+        self._index[key] = (int(off), int(nbytes))
+
     def delete_sync(self, key: str) -> None:
         self._index.pop(key, None)
 
