@@ -54,35 +54,100 @@ def synthetic(shape, seed=0):
     return a
 
 
-def build_c2_replica(device, data_np, shape, chunks):
-    """Encode `data_np` into a DeviceStore: chunk bytes gathered on the device
-    (setup only, not timed), CRC-32C trailers computed by the zarr_hip kernel."""
+LE = {"name": "bytes", "configuration": {"endian": "little"}}
+CRC = {"name": "crc32c"}
+
+
+def build_replica(device, data_dev, shape, chunks, codecs, shards=None):
+    """Encode a device array into a fresh DeviceStore with zarr_hip's own GPU
+    encode path (setup, not timed)."""
     import torch
 
     import zarr_hip
-    from zarr_hip.crc import crc32c_regions
 
-    grid = tuple(s // c for s, c in zip(shape, chunks))
-    nbytes = int(np.prod(chunks)) * 4
-    store = zarr_hip.DeviceStore(device, capacity=int(np.prod(grid)) * (nbytes + 512) + 4096)
-    dev = torch.from_numpy(data_np).to(device)
-    keys, offs = [], []
-    for c in np.ndindex(*grid):
-        sl = tuple(slice(ci * k, (ci + 1) * k) for ci, k in zip(c, chunks))
-        key = "c/" + "/".join(map(str, c))
-        off = store.set_reserved(key, nbytes + 4)
-        store.arena.view(off, nbytes).copy_(dev[sl].contiguous().view(torch.uint8).reshape(-1))
-        keys.append(key)
-        offs.append(off)
-    crcs = crc32c_regions(store.arena.buf, offs, nbytes)
-    for off, crc in zip(offs, crcs):
-        store.arena.view(off + nbytes, 4).copy_(
-            torch.from_numpy(np.array([crc], "<u4").view(np.uint8)))
-    arr = zarr_hip.Array.create(store, shape, chunks, "float32", 0.0,
-                                codecs=[{"name": "bytes", "configuration": {"endian": "little"}},
-                                        {"name": "crc32c"}])
+    n_enc = int(np.prod(shape)) * data_dev.element_size() * 1.02 + (1 << 24)
+    store = zarr_hip.DeviceStore(device, capacity=int(n_enc))
+    if shards is None:
+        arr = zarr_hip.Array.create(store, shape, chunks, "float32", 0.0, codecs=codecs)
+    else:
+        arr = zarr_hip.Array.create(store, shape, chunks, "float32", 0.0, shards=shards,
+                                    inner_codecs=codecs)
+    arr.set((Ellipsis,), data_dev)
     torch.cuda.synchronize(device)
     return arr
+
+
+def build_c2_replica(device, data_np, shape, chunks):
+    import torch
+
+    return build_replica(device, torch.from_numpy(data_np).to(device), shape, chunks, [LE, CRC])
+
+
+def time_programs(progs, steps, warmup, device):
+    """Average kernel time (HIP events on the launch stream) over rotating programs."""
+    import torch
+
+    stream = torch.cuda.current_stream(device)
+    sh = int(stream.cuda_stream)
+    for i in range(warmup):
+        progs[i % len(progs)].launch(sh)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(steps)]
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for i, (a, b) in enumerate(ev):
+        a.record(stream)
+        progs[i % len(progs)].launch(sh)
+        b.record(stream)
+    torch.cuda.synchronize(device)
+    wall = time.perf_counter() - t0
+    for p in progs:
+        p.results()
+    return wall / steps, float(np.median([a.elapsed_time(b) for a, b in ev])) / 1e3
+
+
+def extra_configs(device, args):
+    """C3 (transpose) and C4 (sharded) measured beside the headline C2."""
+    import torch
+
+    out = {}
+    if "c3" in args.extra:
+        shape, chunks = (256, 256, 256), (64, 64, 64)
+        data = torch.from_numpy(synthetic(shape, seed=0)).to(device)
+        progs = []
+        for _ in range(args.replicas):
+            arr = build_replica(device, data, shape, chunks,
+                                [{"name": "transpose", "configuration": {"order": [2, 1, 0]}}, LE, CRC])
+            progs.append(arr.prepare_read((Ellipsis,))[0])
+        prog, outt = progs[0], None
+        wall, kern = time_programs(progs, max(10, args.steps // 2), 3, device)
+        dec = data.numel() * 4
+        enc = 64 * (1048576 + 4)
+        out["c3_transpose_210"] = {"decoded_GiBps": round(dec / wall / GIB, 1),
+                                   "kernel_ms": round(kern * 1e3, 4),
+                                   "hbm_frac": round((dec + enc) / kern / 1e9 / HBM_PEAK_GBS, 4)}
+        del progs, data
+    if "c4" in args.extra:
+        shape, shards, inner = (1024, 1024, 1024), (128, 128, 128), (32, 32, 32)
+        g = torch.Generator(device=device).manual_seed(0)
+        data = torch.randn(shape, generator=g, device=device, dtype=torch.float32)
+        progs = []
+        for _ in range(2):
+            arr = build_replica(device, data, shape, inner, [LE, CRC], shards=shards)
+            progs.append(arr.prepare_read((Ellipsis,))[0])
+        chk = progs[0]
+        chk.launch()
+        chk.results()
+        wall, kern = time_programs(progs, 6, 2, device)
+        dec = data.numel() * 4
+        enc = 512 * (64 * (131072 + 4) + 64 * 16 + 4)
+        out["c4_sharded_1024"] = {"decoded_GiBps": round(dec / wall / GIB, 1),
+                                  "step_ms": round(wall * 1e3, 3),
+                                  "kernel_ms": round(kern * 1e3, 3),
+                                  "hbm_frac": round((dec + enc) / kern / 1e9 / HBM_PEAK_GBS, 4)}
+        del progs, data
+    torch.cuda.empty_cache()
+    return out
 
 
 def cpu_baseline(data_np, shape, chunks, budget_s=12.0):
@@ -145,6 +210,7 @@ def main():
     ap.add_argument("--replicas", type=int, default=4)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--extra", default="c3,c4", help="extra configs measured at N=1 (c3,c4 or '')")
     args = ap.parse_args()
 
     import torch
@@ -235,6 +301,9 @@ def main():
             "algorithmic_bytes_per_launch": encoded + decoded,
         },
     }
+    if world == 1 and args.extra:
+        log("[bench] extra configs " + args.extra)
+        res["extra"] = extra_configs(device, args)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("[bench] cpu baseline")
         res["cpu_baseline"] = cpu_baseline(data, shape, chunks, args.cpu_budget)
