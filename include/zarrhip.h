@@ -149,6 +149,9 @@ int zhip_plan_info(const zhip_plan *plan, uint32_t *units_per_chunk, uint32_t *w
 #define ZHIP_DF_FAST_ROWS 1u  /* every chunk selects whole innermost rows that are
                                  contiguous in out, 16-byte multiples and 16-byte
                                  aligned: one 16-byte store per 16 input bytes */
+#define ZHIP_DF_TILE 2u       /* transposed layout: every chunk fully selected, the
+                                 out-contiguous stored dim is tiled through LDS;
+                                 out offsets/strides 16-byte aligned */
 
 /* Upload the plan's constant tables to the current HIP device (once). */
 int zhip_plan_upload(zhip_plan *plan);

@@ -191,3 +191,39 @@ def test_program_relaunch_is_idempotent(device):
     from zarr_hip.buffer import to_numpy
 
     assert to_numpy(out, "float32").tobytes() == O.read(host, meta).tobytes()
+
+
+# ------------------------------------------------- tiled transpose (ZHIP_DF_TILE)
+
+@pytest.mark.parametrize("order", [(2, 1, 0), (1, 2, 0), (2, 0, 1), (0, 2, 1)])
+@pytest.mark.parametrize("shape,chunks", [((64, 96, 128), (32, 48, 64)),   # partial tiles, 2 col blocks
+                                          ((128, 128, 64), (128, 64, 64)),  # full 64-row tiles
+                                          ((40, 24, 80), (20, 8, 80))])     # rows < 64, cols > 256 B
+def test_transpose_tiled(device, order, shape, chunks):
+    _roundtrip(device, shape, chunks, "float32", [T(order), LE, CRC], fill=np.nan)
+
+
+@pytest.mark.parametrize("dtype,endian", [("int16", LE), ("uint8", LE), ("float64", LE),
+                                          ("float32", BE), ("int16", BE), ("float64", BE)])
+def test_transpose_tiled_dtypes(device, dtype, endian):
+    _roundtrip(device, (64, 64, 64), (32, 32, 32), dtype, [T((2, 1, 0)), endian, CRC])
+
+
+def test_transpose_tiled_missing_and_sharded(device):
+    _roundtrip(device, (64, 64, 64), (32, 32, 32), "float32", [T((2, 1, 0)), LE, CRC], fill=-3.0,
+               drop=["c/0/1/0", "c/1/1/1"])
+    _roundtrip(device, (64, 64, 64), (32, 32, 32), "float32",
+               [SHARD((16, 16, 16), [T((2, 1, 0)), LE, CRC])])
+
+
+def test_tile_mode_engaged(device):
+    import zarr_hip
+
+    meta = O.ArrayMeta((64, 64, 64), (32, 32, 32), np.dtype("float32"), 0.0,
+                       codecs=[T((2, 1, 0)), LE, CRC])
+    host = {}
+    O.write(host, meta, (Ellipsis,), _data((64, 64, 64), "float32"))
+    store = zarr_hip.DeviceStore.from_host(host, device)
+    arr = zarr_hip.Array.create(store, meta.shape, meta.chunk_shape, "float32", 0.0, codecs=meta.codecs)
+    prog, _ = arr.prepare_read((Ellipsis,))
+    assert prog.tables.tile and not prog.tables.fast

@@ -58,14 +58,31 @@ uint32_t xpow8(uint64_t n) {
     return p;
 }
 
-// x^(-8n) mod P: n inverse byte-steps applied to 1.
+// x^-8 mod P: one inverse byte step applied to 1.
+uint32_t xinv8() {
+    const uint32_t s = kOne;
+    const uint32_t i = g_invtop[s >> 24];
+    return (((s ^ g_T[i]) & 0x00FFFFFFu) << 8) | i;
+}
+
+// x^(-8n) mod P = (x^-8)^n by square-and-multiply.
 uint32_t xpow8_inv(uint64_t n) {
-    uint32_t s = kOne;
-    for (uint64_t k = 0; k < n; ++k) {
-        const uint32_t i = g_invtop[s >> 24];
-        s = (((s ^ g_T[i]) & 0x00FFFFFFu) << 8) | i;
+    uint32_t p = kOne;
+    uint32_t b = xinv8();
+    while (n) {
+        if (n & 1) p = gf_mul(p, b);
+        b = gf_mul(b, b);
+        n >>= 1;
     }
-    return s;
+    return p;
+}
+
+void build_horner_stride(uint32_t* tab, uint64_t stride) {  // [op][slice][256], op k = A_(stride - 4k)
+    for (int op = 0; op < 4; ++op) {
+        const uint32_t x = xpow8(stride - 4u * op);
+        for (int sl = 0; sl < 4; ++sl)
+            for (uint32_t b = 0; b < 256; ++b) tab[op * 1024 + sl * 256 + b] = gf_mul(x, b << (8 * sl));
+    }
 }
 
 zhip_fdiv make_fdiv(uint32_t d) {
@@ -168,6 +185,28 @@ int zhip_plan_create(const zhip_layout* layout, zhip_plan** out) {
     p->device = -1;
     p->max_grid = 2048;
     p->d_tables = nullptr;
+    p->d_tile_tables = nullptr;
+    // tile mode: a stored dim (not the innermost) that is contiguous in out
+    p->tq = -1;
+    {
+        uint64_t st = (uint64_t)L.itemsize;
+        for (int d = L.ndim - 1; d >= 0; --d) {
+            p->sstride[d] = (uint32_t)st;
+            st *= (uint64_t)L.shape[d];
+        }
+        for (int d = L.ndim; d < ZHIP_MAX_DIMS; ++d) p->sstride[d] = 0;
+        if (!(L.flags & ZHIP_LF_NO_WRITE) && L.ndim >= 2 && p->row_bytes % 16 == 0 && p->row_bytes > 0)
+            for (int d = 0; d < L.ndim - 1; ++d)
+                if (L.out_stride[d] == L.itemsize && L.shape[d] > 1) { p->tq = d; break; }
+        if (p->tq >= 0) {
+            p->n_qb = (uint32_t)((L.shape[p->tq] + kTileRows - 1) / kTileRows);
+            p->n_cb = (p->row_bytes + kTileCols - 1) / kTileCols;
+            uint64_t other = 1;
+            for (int d = 0; d < L.ndim - 1; ++d)
+                if (d != p->tq) other *= (uint64_t)L.shape[d];
+            p->t_per_chunk = (uint32_t)(other * p->n_qb * p->n_cb);
+        }
+    }
     *out = p;
     return ZHIP_OK;
 }
@@ -186,6 +225,44 @@ int zhip_plan_upload(zhip_plan* p) {
     p->d_tables = nullptr;
     HIP_TRY(hipMalloc(&p->d_tables, h.size() * sizeof(uint32_t)));
     HIP_TRY(hipMemcpy(p->d_tables, h.data(), h.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    if (p->tq >= 0) {
+        // thread t's Horner state lands at rel_t = (64 + t/16)*sq + 16*(t%16) from the
+        // tile base; shift every thread to REF, every tile from base+REF to R_c
+        const uint64_t sq = p->sstride[p->tq];
+        const uint64_t REF = (uint64_t)(kTileRows + 16) * sq + kTileCols;
+        const uint32_t T = p->t_per_chunk;
+        std::vector<uint64_t> base(T);
+        const zhip_layout& L = p->layout;
+        uint64_t maxb = 0;
+        for (uint32_t ti = 0; ti < T; ++ti) {
+            uint32_t r = ti;
+            const uint32_t cb = r % p->n_cb;
+            r /= p->n_cb;
+            const uint32_t qb = r % p->n_qb;
+            r /= p->n_qb;
+            uint64_t b = (uint64_t)qb * kTileRows * sq + (uint64_t)cb * kTileCols;
+            for (int d = L.ndim - 2; d >= 0; --d) {
+                if (d == p->tq) continue;
+                b += (uint64_t)(r % (uint32_t)L.shape[d]) * p->sstride[d];
+                r /= (uint32_t)L.shape[d];
+            }
+            base[ti] = b;
+            if (b > maxb) maxb = b;
+        }
+        const uint64_t Rc = maxb + REF;
+        std::vector<uint32_t> ht(4096 + kThreads + T);
+        build_horner_stride(ht.data(), 16ull * sq);
+        for (int t = 0; t < kThreads; ++t) {
+            const uint64_t rel = (uint64_t)(kTileRows + t / 16) * sq + 16u * (t % 16);
+            ht[4096 + t] = xpow8(REF - rel);
+        }
+        for (uint32_t ti = 0; ti < T; ++ti) ht[4096 + kThreads + ti] = xpow8(Rc - base[ti] - REF);
+        p->t_c_inv = xpow8_inv(Rc - L.nbytes);
+        if (p->d_tile_tables) (void)hipFree(p->d_tile_tables);
+        p->d_tile_tables = nullptr;
+        HIP_TRY(hipMalloc(&p->d_tile_tables, ht.size() * sizeof(uint32_t)));
+        HIP_TRY(hipMemcpy(p->d_tile_tables, ht.data(), ht.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    }
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0)
         p->max_grid = prop.multiProcessorCount * 8;
@@ -196,6 +273,7 @@ int zhip_plan_upload(zhip_plan* p) {
 int zhip_plan_destroy(zhip_plan* p) {
     if (!p) return ZHIP_OK;
     if (p->d_tables) (void)hipFree(p->d_tables);
+    if (p->d_tile_tables) (void)hipFree(p->d_tile_tables);
     delete p;
     return ZHIP_OK;
 }
@@ -246,6 +324,24 @@ int zhip_decode(const zhip_plan* plan, const void* src, uint64_t src_size, void*
     std::memcpy(p.fill, plan->fill, sizeof(p.fill));
     p.fast = (decode_flags & ZHIP_DF_FAST_ROWS) ? 1u : 0u;
     p.tune = g_tune_bits;
+    p.tq = -1;
+    if ((decode_flags & ZHIP_DF_TILE) && plan->tq >= 0 && plan->d_tile_tables) {
+        p.tq = plan->tq;
+        p.t_per_chunk = plan->t_per_chunk;
+        p.n_qb = plan->n_qb;
+        p.n_cb = plan->n_cb;
+        for (int d = 0; d < ZHIP_MAX_DIMS; ++d) p.sstride[d] = plan->sstride[d];
+        p.d_qb = make_fdiv(plan->n_qb);
+        p.d_cb = make_fdiv(plan->n_cb);
+        p.horner = plan->d_tile_tables;
+        p.kthread = plan->d_tile_tables + 4096;
+        p.kunit = plan->d_tile_tables + 4096 + kThreads;
+        p.c_inv = plan->t_c_inv;
+        const uint64_t tunits = (uint64_t)n_chunks * plan->t_per_chunk;
+        if (tunits >= (1ull << 32)) return set_err(ZHIP_E_UNSUPPORTED, "too many tiles in one batch");
+        p.n_units = (uint32_t)tunits;
+        p.fast = 0;
+    }
     int rc = launch_decode(p, static_cast<hipStream_t>(stream), plan->max_grid);
     if (rc == ZHIP_E_UNSUPPORTED) return set_err(rc, "no kernel for this layout");
     if (rc != ZHIP_OK) return set_err(rc, std::string("launch failed: ") + hipGetErrorString(hipGetLastError()));

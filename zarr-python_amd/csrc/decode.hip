@@ -300,6 +300,232 @@ __global__ __launch_bounds__(kThreads) void k_decode(const DecodeParams p) {
     if (t == 0) retire(p, pend, full);
 }
 
+
+// ---------------------------------------------------------------------------
+// Tiled transpose decode (TransposeCodec._decode_sync, transpose.py:98-104, for
+// orders whose out-contiguous dim is not the innermost stored dim).  A tile =
+// kTileRows rows of the stored dim tq (contiguous in out) x kTileCols bytes of
+// the innermost stored row, other dims fixed.  Loads: 16 rows x 256 B per pass
+// (every wave reads whole 256-byte row pieces); the tile is transposed through
+// LDS and stored as whole out rows (256 B contiguous per column element).
+// CRC: thread t's blocks sit at a constant stride 16*sstride[tq], so it keeps
+// a Horner chain with stride-specific tables; per-thread / per-tile shift
+// constants (host-built) bring every tile's contribution to the chunk reference.
+// ---------------------------------------------------------------------------
+template <bool CRC, int ITEM, bool SWAP>
+__global__ __launch_bounds__(kThreads) void k_decode_tile(const DecodeParams p) {
+    constexpr int kPitch = ITEM == 8 ? 264 : 260;  // bytes per LDS tile row (2-way read conflicts)
+    constexpr int kPasses = kTileRows / 16;
+    __shared__ uint32_t s_tab[CRC ? 16 * 256 : 1];
+    __shared__ __attribute__((aligned(16))) uint8_t s_tile[kTileRows * kPitch];
+    __shared__ uint32_t s_red[kThreads / 64];
+    const int t = threadIdx.x;
+    uint32_t kth = 0;
+    if constexpr (CRC) {
+        const uint4* g = reinterpret_cast<const uint4*>(p.horner);
+        uint4* sv = reinterpret_cast<uint4*>(s_tab);
+        for (int i = t; i < 1024; i += kThreads) sv[i] = g[i];
+        kth = p.kthread[t];
+        __syncthreads();
+    }
+    const uint32_t expected = p.g.nbytes + (CRC ? 4u : 0u);
+    const int32_t last = p.g.ndim - 1;
+    const uint32_t rows_q = (uint32_t)p.g.shape[p.tq];
+    const uint32_t sq = p.sstride[p.tq];
+    const int64_t oq = p.g.ostride[p.tq];      // == ITEM
+    const int64_t ocol = p.g.ostride[last];    // out stride of the innermost stored dim
+    const uint32_t G = gridDim.x, gi = blockIdx.x;
+    const uint32_t per = p.n_units / G, rem = p.n_units % G;
+    const uint32_t q0 = gi * per + (gi < rem ? gi : rem);
+    const uint32_t q1 = q0 + per + (gi < rem ? 1u : 0u);
+    uint32_t runV = 0, run_len = 0;
+    for (uint32_t q = q0; q < q1; ++q) {
+        const uint32_t c = q / p.t_per_chunk;
+        const uint32_t ti = q - c * p.t_per_chunk;
+        // chunk source (as resolve_unit)
+        const zhip_chunk ch = p.chunks[c];
+        uint32_t mode = ZHIP_ST_OK;
+        uint64_t base = ch.src;
+        if (ch.flags & ZHIP_CF_MISSING) {
+            mode = ZHIP_ST_MISSING;
+        } else if (p.lflags & ZHIP_LF_SHARDED) {
+            const uint64_t ipos = (p.lflags & ZHIP_LF_INDEX_START) ? 0ull : ch.src_len - p.index_size;
+            const uint8_t* e = p.src + ch.src + ipos + 16ull * ch.slot;
+            const uint64_t off = load_u64_le_bytes(e);
+            const uint64_t len = load_u64_le_bytes(e + 8);
+            if (off == ~0ull && len == ~0ull) mode = ZHIP_ST_MISSING;
+            else if (off > ch.src_len || len > ch.src_len - off) mode = ZHIP_ST_INDEX_OOB;
+            else if (len != expected) mode = ZHIP_ST_LENGTH_MISMATCH;
+            else base = ch.src + off;
+        } else if (ch.src_len != expected) {
+            mode = ZHIP_ST_LENGTH_MISMATCH;
+        }
+        mode = __builtin_amdgcn_readfirstlane(mode);
+        const uint8_t* cp = p.src + base;
+        // tile coordinates
+        uint32_t r = ti;
+        const uint32_t rq = fdiv_apply(r, p.d_cb.m, p.d_cb.s);
+        const uint32_t cb = r - rq * p.n_cb;
+        r = rq;
+        const uint32_t rr = fdiv_apply(r, p.d_qb.m, p.d_qb.s);
+        const uint32_t qb = r - rr * p.n_qb;
+        r = rr;
+        uint32_t tbase = qb * (uint32_t)kTileRows * sq + cb * (uint32_t)kTileCols;
+        int64_t obase = ch.out_off + (int64_t)qb * kTileRows * oq + (int64_t)(cb * (kTileCols / ITEM)) * ocol;
+#pragma unroll
+        for (int d = ZHIP_MAX_DIMS - 1; d >= 0; --d) {
+            if (d >= last || d == p.tq) continue;
+            const uint32_t qd = fdiv_apply(r, p.g.dshape[d].m, p.g.dshape[d].s);
+            const uint32_t sd = r - qd * (uint32_t)p.g.shape[d];
+            r = qd;
+            tbase += sd * p.sstride[d];
+            obase += (int64_t)sd * p.g.ostride[d];
+        }
+        const uint32_t rows_here = min((uint32_t)kTileRows, rows_q - qb * kTileRows);
+        const uint32_t cols_here = min((uint32_t)kTileCols, p.g.row_bytes - cb * kTileCols);
+        if (mode == ZHIP_ST_OK) {
+            const int row0 = t >> 4;
+            const uint32_t col = 16u * (uint32_t)(t & 15);
+            uint4 blk[kPasses];
+            const uint32_t al4 =
+                __builtin_amdgcn_readfirstlane((uint32_t)(reinterpret_cast<uintptr_t>(cp) & 3u) == 0u ? 1u : 0u);
+            if (al4) {
+#pragma unroll
+                for (int k = 0; k < kPasses; ++k) {
+                    const uint32_t row = 16u * k + row0;
+                    blk[k] = (row < rows_here && col < cols_here)
+                                 ? *reinterpret_cast<const uint4*>(cp + tbase + row * sq + col)
+                                 : make_uint4(0, 0, 0, 0);
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < kPasses; ++k) {
+                    const uint32_t row = 16u * k + row0;
+                    blk[k] = (row < rows_here && col < cols_here)
+                                 ? load_block<false>(cp, (int32_t)(tbase + row * sq + col), p.g.nbytes)
+                                 : make_uint4(0, 0, 0, 0);
+                }
+            }
+            uint32_t acc = 0;
+            if constexpr (CRC) {
+#pragma unroll
+                for (int k = 0; k < kPasses; ++k) {
+                    const uint4 v = blk[k];
+                    acc = tab_apply(s_tab, acc ^ v.x) ^ tab_apply(s_tab + 1024, v.y) ^
+                          tab_apply(s_tab + 2048, v.z) ^ tab_apply(s_tab + 3072, v.w);
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < kPasses; ++k) {
+                const uint4 v = swap_block<ITEM, SWAP>(blk[k]);
+                uint32_t* d = reinterpret_cast<uint32_t*>(s_tile + (16 * k + row0) * kPitch + col);
+                d[0] = v.x;
+                d[1] = v.y;
+                d[2] = v.z;
+                d[3] = v.w;
+            }
+            __syncthreads();
+            // out pieces: column element j, 16/ITEM consecutive rows from q0
+            constexpr int kPer = 16 / ITEM;                  // rows per 16-byte piece
+            constexpr int kPiecesPerCol = kTileRows / kPer;  // pieces per out row
+#pragma unroll
+            for (int k = 0; k < kPasses; ++k) {
+                const uint32_t pc = (uint32_t)(k * kThreads + t);
+                const uint32_t j = pc / kPiecesPerCol;
+                const uint32_t r0 = (pc % kPiecesPerCol) * kPer;
+                if (j * ITEM >= cols_here || r0 >= rows_here) continue;
+                uint32_t w[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) w[e] = 0;
+#pragma unroll
+                for (int e = 0; e < kPer; ++e) {
+                    const uint8_t* src = s_tile + (r0 + e) * kPitch + j * ITEM;
+                    if constexpr (ITEM == 8) {
+                        const uint2 v = *reinterpret_cast<const uint2*>(src);
+                        w[2 * e] = v.x;
+                        w[2 * e + 1] = v.y;
+                    } else if constexpr (ITEM == 4) {
+                        w[e] = *reinterpret_cast<const uint32_t*>(src);
+                    } else if constexpr (ITEM == 2) {
+                        w[e / 2] |= (uint32_t)(*reinterpret_cast<const uint16_t*>(src)) << (16 * (e & 1));
+                    } else {
+                        w[e / 4] |= (uint32_t)(*src) << (8 * (e & 3));
+                    }
+                }
+                uint8_t* dst = p.out + obase + (int64_t)j * ocol + (int64_t)r0 * oq;
+                if (r0 + kPer <= rows_here) {
+                    *reinterpret_cast<uint4*>(dst) = make_uint4(w[0], w[1], w[2], w[3]);
+                } else {
+                    for (uint32_t e = 0; e < rows_here - r0; ++e)
+                        for (int b = 0; b < ITEM; ++b)
+                            dst[e * ITEM + b] = (uint8_t)(w[(e * ITEM + b) / 4] >> (8 * ((e * ITEM + b) % 4)));
+                }
+            }
+            if constexpr (CRC) {
+                uint32_t v = gf_mul(acc, kth);
+#pragma unroll
+                for (int off = 32; off > 0; off >>= 1) v ^= __shfl_xor(v, off, 64);
+                if ((t & 63) == 0) s_red[t >> 6] = v;
+            }
+            __syncthreads();  // LDS tile and s_red reads done before the next tile
+            if constexpr (CRC) {
+                if (t == 0) {
+                    const uint32_t V = s_red[0] ^ s_red[1] ^ s_red[2] ^ s_red[3];
+                    runV ^= gf_mul(V, p.kunit[ti]);
+                    ++run_len;
+                    const bool run_end = (q + 1 >= q1) || ((q + 1) / p.t_per_chunk != c);
+                    if (run_end) {
+                        uint32_t* accw = p.ws + 4ull * c;
+                        const uint32_t prev =
+                            __hip_atomic_fetch_xor(accw, runV, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        asm volatile("s_waitcnt vmcnt(0)" ::"v"(prev) : "memory");
+                        const uint32_t tk =
+                            __hip_atomic_fetch_add(accw + 2, run_len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if (tk + run_len == p.t_per_chunk) {
+                            const uint32_t raw =
+                                __hip_atomic_exchange(accw, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            __hip_atomic_store(accw + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            finalize_chunk(p, c, load_trailer(cp, p.g.nbytes), raw);
+                        }
+                        runV = 0;
+                        run_len = 0;
+                    }
+                }
+            } else if (t == 0 && ti == 0) {
+                zhip_status st = {ZHIP_ST_OK, 0u, 0u, 0u};
+                p.status[c] = st;
+            }
+        } else {
+            // missing chunk: fill this tile's region of out
+            const uint4 f = make_uint4(p.fill[0], p.fill[1], p.fill[2], p.fill[3]);
+            constexpr int kPer = 16 / ITEM;
+            constexpr int kPiecesPerCol = kTileRows / kPer;
+            if (mode == ZHIP_ST_MISSING) {
+#pragma unroll
+                for (int k = 0; k < kPasses; ++k) {
+                    const uint32_t pc = (uint32_t)(k * kThreads + t);
+                    const uint32_t j = pc / kPiecesPerCol;
+                    const uint32_t r0 = (pc % kPiecesPerCol) * kPer;
+                    if (j * ITEM >= cols_here || r0 >= rows_here) continue;
+                    uint8_t* dst = p.out + obase + (int64_t)j * ocol + (int64_t)r0 * oq;
+                    if (r0 + kPer <= rows_here) {
+                        *reinterpret_cast<uint4*>(dst) = f;
+                    } else {
+                        const uint32_t fw[4] = {f.x, f.y, f.z, f.w};
+                        for (uint32_t e = 0; e < (rows_here - r0) * ITEM; ++e)
+                            dst[e] = (uint8_t)(fw[e / 4] >> (8 * (e % 4)));
+                    }
+                }
+            }
+            if (t == 0 && ti == 0) {
+                zhip_status st = {mode, 0u, 0u, 0u};
+                p.status[c] = st;
+                if (mode != ZHIP_ST_MISSING) atomicOr(p.errflag, 1u << mode);
+            }
+        }
+    }
+}
+
 using KernelFn = void (*)(const DecodeParams);
 
 template <bool CRC, bool WRITE, bool FAST, int K>
@@ -328,8 +554,35 @@ KernelFn select_decode_kernel(bool crc, bool write, bool fast, int item, bool sw
     return fast ? pick_item<false, true, true, 8>(item, swap) : pick_item<false, true, false, 8>(item, swap);
 }
 
+static KernelFn select_tile_kernel(bool crc, int item, bool swap) {
+    switch (item) {
+        case 1: return crc ? k_decode_tile<true, 1, false> : k_decode_tile<false, 1, false>;
+        case 2: return crc ? (swap ? k_decode_tile<true, 2, true> : k_decode_tile<true, 2, false>)
+                           : (swap ? k_decode_tile<false, 2, true> : k_decode_tile<false, 2, false>);
+        case 4: return crc ? (swap ? k_decode_tile<true, 4, true> : k_decode_tile<true, 4, false>)
+                           : (swap ? k_decode_tile<false, 4, true> : k_decode_tile<false, 4, false>);
+        case 8: return crc ? (swap ? k_decode_tile<true, 8, true> : k_decode_tile<true, 8, false>)
+                           : (swap ? k_decode_tile<false, 8, true> : k_decode_tile<false, 8, false>);
+        default: return nullptr;
+    }
+}
+
 int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
     if (g_tune_max_grid > 0) max_grid = g_tune_max_grid;
+    if (p.tq >= 0) {
+        KernelFn fn = select_tile_kernel((p.lflags & ZHIP_LF_CRC) != 0, p.g.itemsize, (p.lflags & ZHIP_LF_SWAP) != 0);
+        if (!fn) return ZHIP_E_UNSUPPORTED;
+        if (p.n_units == 0) return ZHIP_OK;
+        if (g_tune_max_grid <= 0) {
+            int per_cu = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(fn), kThreads,
+                                                             0) == hipSuccess && per_cu > 0)
+                max_grid = (max_grid / 8) * per_cu;
+        }
+        const uint32_t grid = p.n_units < (uint32_t)max_grid ? p.n_units : (uint32_t)max_grid;
+        hipLaunchKernelGGL(fn, dim3(grid), dim3(kThreads), 0, stream, p);
+        return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
+    }
     KernelFn fn = select_decode_kernel((p.lflags & ZHIP_LF_CRC) != 0, (p.lflags & ZHIP_LF_NO_WRITE) == 0,
                                        p.fast != 0, p.g.itemsize, (p.lflags & ZHIP_LF_SWAP) != 0,
                                        (int)(p.seg / kWgStride));

@@ -46,7 +46,15 @@ struct DecodeParams {
     uint32_t fill[4];
     uint32_t fast;
     uint32_t tune;  // kTune* ablation bits (0 in production)
+    // tile mode (transposed chunks: stored dim tq is contiguous in out)
+    int32_t tq;
+    uint32_t t_per_chunk, n_qb, n_cb;
+    uint32_t sstride[ZHIP_MAX_DIMS];  // stored-stream byte stride of each dim
+    zhip_fdiv d_qb, d_cb;
 };
+
+constexpr int kTileRows = 64;    // rows of the contiguous-in-out dim per tile
+constexpr int kTileCols = 256;   // bytes of the innermost stored row per tile
 
 // Ablation / tuning knobs (zhip_set_tuning): never set on the product path.
 constexpr uint32_t kTuneSkipCrc = 1u;   // replace the CRC lookups by a plain xor
@@ -116,4 +124,10 @@ struct zhip_plan {
     int device;
     int max_grid;
     uint32_t* d_tables;  // horner (4096) | kthread (256) | kunit (nseg)
+    // tile mode (layouts with a transposed dim that is contiguous in out)
+    int32_t tq;          // -1: no tile mode
+    uint32_t t_per_chunk, n_qb, n_cb;
+    uint32_t sstride[ZHIP_MAX_DIMS];
+    uint32_t t_c_inv;
+    uint32_t* d_tile_tables;  // horner (stride 16*sstride[tq]) | kthread (256) | kunit (t_per_chunk)
 };

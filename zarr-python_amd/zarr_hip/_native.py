@@ -28,6 +28,7 @@ LF_FLOAT = 32
 CF_MISSING = 1
 
 DF_FAST_ROWS = 1
+DF_TILE = 2
 
 PF_INDEX_START = 1
 PF_INDEX_CRC = 2

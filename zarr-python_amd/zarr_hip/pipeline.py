@@ -74,7 +74,7 @@ class DecodeLaunch:
     """One zhip_decode launch with its device-resident tables."""
 
     def __init__(self, layout: N.Layout, chunks: np.ndarray, sels: np.ndarray, src, src_size: int,
-                 out, fast: bool, device):
+                 out, fast: bool, device, tile: bool = False):
         torch = _torch()
         self.plan = get_plan(layout)
         self.n = len(chunks)
@@ -87,7 +87,7 @@ class DecodeLaunch:
         self.src = src
         self.src_size = src_size
         self.out = out
-        self.flags = N.DF_FAST_ROWS if fast else 0
+        self.flags = (N.DF_FAST_ROWS if fast else 0) | (N.DF_TILE if tile else 0)
 
     def launch(self, stream: int | None = None) -> None:
         if self.n == 0:
@@ -259,7 +259,7 @@ class HipCodecPipeline:
         ostr = [int(s) * itemsize for s in out.stride()]
         with torch.cuda.device(device):
             t = plan_decode(chain, spec, items, ostr, out.data_ptr(), drop_axes)
-            data = DecodeLaunch(t.layout, t.chunks, t.sels, src, size, out, t.fast, device)
+            data = DecodeLaunch(t.layout, t.chunks, t.sels, src, size, out, t.fast, device, t.tile)
             index = None
             if t.index_layout is not None:
                 index = DecodeLaunch(t.index_layout, t.index_chunks, np.zeros(1, SEL_DT), src, size,

@@ -107,6 +107,7 @@ class Tables:
     sels: np.ndarray              # SEL_DT[m]
     fast: bool
     item_of_chunk: np.ndarray     # int64[n]: batch item of each chunk entry
+    tile: bool = False            # tiled-transpose decode (ZHIP_DF_TILE)
     index_layout: N.Layout | None = None
     index_chunks: np.ndarray | None = None
     index_item: np.ndarray | None = None
@@ -165,6 +166,25 @@ def _fast_ok(layout: N.Layout, start, count, step, out_offs, out_base_ptr: int) 
             return False
     return bool(np.all(start[:, last] == 0) and np.all(count[:, last] == layout.shape[last])
                 and np.all(step[:, last] == 1))
+
+
+def _tile_ok(layout: N.Layout, start, count, step, out_offs, out_base_ptr: int) -> bool:
+    """Transposed layouts: a stored dim other than the innermost is contiguous in
+    out, every chunk is fully selected and out is 16-byte aligned."""
+    nd = layout.ndim
+    it = layout.itemsize
+    last = nd - 1
+    if nd < 2 or layout.out_stride[last] == it or (layout.shape[last] * it) % 16:
+        return False
+    tq = [d for d in range(last) if layout.out_stride[d] == it and layout.shape[d] > 1]
+    if not tq:
+        return False
+    if out_base_ptr % 16 or np.any(out_offs % 16):
+        return False
+    if any(layout.out_stride[d] % 16 for d in range(nd) if d != tq[0]):
+        return False
+    shp = np.array([layout.shape[d] for d in range(nd)], np.int64)
+    return bool(np.all(start == 0) and np.all(step == 1) and np.all(count == shp[None, :]))
 
 
 def plan_encode(chain: ChainInfo, spec: ArraySpec, items: list, arr_strides_bytes,
@@ -229,7 +249,8 @@ def plan_decode(chain: ChainInfo, spec: ArraySpec, items: list, out_strides_byte
         sels, inv = _pack_sels(start, count, step)
         chunks["sel"] = inv
         fast = _fast_ok(layout, start, count, step, chunks["out_off"], out_base_ptr)
-        return Tables(layout, chunks, sels, fast, np.arange(n))
+        tile = not fast and _tile_ok(layout, start, count, step, chunks["out_off"], out_base_ptr)
+        return Tables(layout, chunks, sels, fast, np.arange(n), tile=tile)
 
     # ---- sharded: expand every shard item into its inner chunks ----
     sh = chain.shard
@@ -283,7 +304,8 @@ def plan_decode(chain: ChainInfo, spec: ArraySpec, items: list, out_strides_byte
     sels, inv = _pack_sels(start, count, step)
     chunks["sel"] = inv
     fast = _fast_ok(layout, start, count, step, chunks["out_off"], out_base_ptr)
-    t = Tables(layout, chunks, sels, fast, item_of)
+    tile = not fast and _tile_ok(layout, start, count, step, chunks["out_off"], out_base_ptr)
+    t = Tables(layout, chunks, sels, fast, item_of, tile=tile)
     if idx_rows:
         L2 = _make_layout([16 * n_inner], 1, [0], N.LF_CRC | N.LF_NO_WRITE, b"\0")
         ic = np.zeros(len(idx_rows), CHUNK_DT)
