@@ -23,6 +23,8 @@
  *                     With ZHIP_LF_NO_WRITE the same entry point is the
  *                     shard-index CRC check of _decode_shard_index_sync
  *                     (sharding.py:624-631) run over many shards at once.
+ *   zhip_decode_indexed  zhip_decode with that index check fused into the
+ *                     same launch.
  *   zhip_encode       ChunkTransform.encode_chunk for fixed-size chains
  *                     (chunk_utils.py:335-363): transpose/bytes/crc32c _encode_sync
  *                     (transpose.py:113-118, bytes.py:140-158, crc32c_.py:59-68) plus
@@ -168,6 +170,21 @@ int zhip_decode(const zhip_plan *plan, const void *src, uint64_t src_size, void 
                 const zhip_chunk *d_chunks, uint32_t n_chunks, const zhip_sel *d_sels,
                 zhip_status *d_status, uint32_t *d_workspace, uint32_t *d_errflag,
                 uint32_t decode_flags, void *stream);
+
+/* zhip_decode plus, in the same launch, the shard-index CRC check of
+ * _decode_shard_index_sync (sharding.py:624-631) for `n_index` indexes:
+ * d_index_chunks[j].src / src_len locate index j (16*n_inner payload bytes +
+ * the 4-byte CRC trailer) in src; its outcome goes to d_index_status[j].
+ * Workgroup g of the decode grid checks indexes g, g+G, ... while its first
+ * data unit loads (no second launch).  Needs a sharded plan (ZHIP_LF_SHARDED)
+ * with ZHIP_LF_CRC (the CRC tables) and no ZHIP_DF_TILE; otherwise returns
+ * ZHIP_E_UNSUPPORTED and the caller verifies the indexes with a separate
+ * ZHIP_LF_NO_WRITE zhip_decode. */
+int zhip_decode_indexed(const zhip_plan *plan, const void *src, uint64_t src_size, void *out,
+                        const zhip_chunk *d_chunks, uint32_t n_chunks, const zhip_sel *d_sels,
+                        zhip_status *d_status, uint32_t *d_workspace, uint32_t *d_errflag,
+                        const zhip_chunk *d_index_chunks, uint32_t n_index,
+                        zhip_status *d_index_status, uint32_t decode_flags, void *stream);
 
 /* Process-wide tuning / ablation knobs for measurement (never needed for
  * correct operation): ZHIP_TUNE_MAX_GRID = persistent-grid cap (0 = auto),

@@ -17,8 +17,13 @@ rc=$?; echo "bench rc=$rc"; cat gpurun_out/bench.json; tail -3 gpurun_out/bench.
 if [ $rc -ne 0 ]; then exit $rc; fi
 if [ "${PROFILE:-1}" = "1" ]; then
   cd /tmp && export TMPDIR=/tmp
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run --output-format csv -- python "$GRAFT_REPO_ROOT/bench.py" --steps "$STEPS" --warmup 10 --no-cpu-baseline > "$GRAFT_REPO_ROOT/gpurun_out/bench_prof.json" 2> "$GRAFT_REPO_ROOT/gpurun_out/bench_prof.err"
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run --output-format csv -- python "$GRAFT_REPO_ROOT/bench.py" --steps "$STEPS" --warmup 10 --no-cpu-baseline --extra "" > "$GRAFT_REPO_ROOT/gpurun_out/bench_prof.json" 2> "$GRAFT_REPO_ROOT/gpurun_out/bench_prof.err"
   rc=$?; echo "rocprof rc=$rc"
   find "$GRAFT_REPO_ROOT/gpurun_out/prof" -name "*stats*" | head
+  if [ $rc -ne 0 ]; then exit $rc; fi
+fi
+if [ "${PMC:-0}" = "1" ]; then
+  bash "$GRAFT_REPO_ROOT/scripts/gpu_pmc.sh"
+  rc=$?
 fi
 exit $rc

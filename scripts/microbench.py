@@ -47,8 +47,8 @@ def main():
         return [a.elapsed_time(b) for a, b in evs]
 
     arms = []
-    grids = [int(g) for g in os.environ.get("GRIDS", "0,256,512,1024,4096").split(",")]
-    ablations = [int(a) for a in os.environ.get("ABLATIONS", "0,1,2,4").split(",")]
+    grids = [int(g) for g in os.environ.get("GRIDS", "0,2048").split(",")]
+    ablations = [int(a) for a in os.environ.get("ABLATIONS", "0,1,8,9").split(",")]
     for g in grids:
         for ab in ablations:
             arms.append(("decode", g, ab))
@@ -79,7 +79,8 @@ def main():
         ch["src_len"] -= 4
         nocrc.append(DecodeLaunch(L2, ch, t.sels, prog.data.src, prog.data.src_size, out, True, dev))
     for g in grids:
-        arms.append(("nocrc", g, 0))
+        for ab in (0, 8):
+            arms.append(("nocrc", g, ab))
     arms.append(("torch_copy", 0, 0))
     arms.append(("torch_read_sum", 0, 0))
     results = {a: [] for a in arms}
@@ -98,7 +99,7 @@ def main():
                 ms = time_arm(lambda i: kl[i % R].launch(sh))
             elif kind == "nocrc":
                 N.lib().zhip_set_tuning(1, g)
-                N.lib().zhip_set_tuning(2, 0)
+                N.lib().zhip_set_tuning(2, ab)
                 ms = time_arm(lambda i: nocrc[i % R].launch(sh))
             elif kind == "torch_copy":
                 ms = time_arm(lambda i: dsts[i % R].copy_(srcs[i % R]))

@@ -227,3 +227,36 @@ def test_tile_mode_engaged(device):
     arr = zarr_hip.Array.create(store, meta.shape, meta.chunk_shape, "float32", 0.0, codecs=meta.codecs)
     prog, _ = arr.prepare_read((Ellipsis,))
     assert prog.tables.tile and not prog.tables.fast
+
+
+# ------------------------------------- shard-index CRC fused into the data launch
+
+@pytest.mark.parametrize("loc", ["end", "start"])
+def test_fused_index_check_engaged_and_correct(device, loc):
+    arr, host, meta = _roundtrip(device, (64, 64, 64), (32, 32, 32), "float32",
+                                 [SHARD((16, 16, 16), [LE, CRC], loc)])
+    prog, _ = arr.prepare_read((Ellipsis,))
+    assert prog.index is None and prog.data.n_idx == 8
+
+
+@pytest.mark.parametrize("loc", ["end", "start"])
+def test_fused_index_crc_mismatch(device, loc):
+    import zarr_hip
+
+    codecs = [SHARD((4, 4), [LE, CRC], loc)]
+    meta = O.ArrayMeta((8, 16), (8, 8), np.dtype("float32"), 0.0, codecs=codecs)
+    host = {}
+    O.write(host, meta, (Ellipsis,), _data((8, 16), "float32"))
+    bad = bytearray(host["c/0/1"])
+    pos = len(bad) - 3 if loc == "end" else 3 * 16 + 9  # the CRC trailer / an entry's high bytes
+    bad[pos] ^= 0x10
+    host["c/0/1"] = bytes(bad)
+    with pytest.raises(ValueError) as want:
+        O.read(host, meta)
+    store = zarr_hip.DeviceStore.from_host(host, device)
+    arr = zarr_hip.Array.create(store, (8, 16), (8, 8), "float32", 0.0, codecs=codecs)
+    prog, _ = arr.prepare_read((Ellipsis,))
+    assert prog.index is None and prog.data.n_idx == 2
+    with pytest.raises(ValueError) as got:
+        arr[...]
+    assert str(got.value) == str(want.value)

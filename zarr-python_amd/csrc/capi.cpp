@@ -182,6 +182,14 @@ int zhip_plan_create(const zhip_layout* layout, zhip_plan** out) {
     uint8_t f16[16];
     for (int i = 0; i < 16; ++i) f16[i] = L.fill[i % L.itemsize];
     std::memcpy(p->fill, f16, 16);
+    p->idx_nbytes = 0;
+    if (L.flags & ZHIP_LF_SHARDED) {
+        const uint64_t ni = 16ull * L.n_inner;
+        p->idx_nbytes = (uint32_t)ni;
+        p->idx_E = (uint32_t)((ni + 15) & ~15ull);
+        p->idx_c_inv = xpow8_inv((uint64_t)p->idx_E + kWgStride - ni);
+        p->idx_c3 = gf_mul(xpow8(ni), 0xFFFFFFFFu);
+    }
     p->device = -1;
     p->max_grid = 2048;
     p->d_tables = nullptr;
@@ -289,11 +297,26 @@ int zhip_decode(const zhip_plan* plan, const void* src, uint64_t src_size, void*
                 const zhip_chunk* d_chunks, uint32_t n_chunks, const zhip_sel* d_sels,
                 zhip_status* d_status, uint32_t* d_workspace, uint32_t* d_errflag, uint32_t decode_flags,
                 void* stream) {
+    return zhip_decode_indexed(plan, src, src_size, out, d_chunks, n_chunks, d_sels, d_status, d_workspace,
+                               d_errflag, nullptr, 0, nullptr, decode_flags, stream);
+}
+
+int zhip_decode_indexed(const zhip_plan* plan, const void* src, uint64_t src_size, void* out,
+                        const zhip_chunk* d_chunks, uint32_t n_chunks, const zhip_sel* d_sels,
+                        zhip_status* d_status, uint32_t* d_workspace, uint32_t* d_errflag,
+                        const zhip_chunk* d_index_chunks, uint32_t n_index, zhip_status* d_index_status,
+                        uint32_t decode_flags, void* stream) {
     if (!plan) return set_err(ZHIP_E_INVALID, "null plan");
     if (!plan->d_tables) return set_err(ZHIP_E_INVALID, "plan not uploaded (zhip_plan_upload)");
-    if (n_chunks == 0) return ZHIP_OK;
+    if (n_chunks == 0 && n_index == 0) return ZHIP_OK;
     if (!src || !d_chunks || !d_sels || !d_status || !d_workspace || !d_errflag)
         return set_err(ZHIP_E_INVALID, "null device pointer");
+    if (n_index) {
+        if (!d_index_chunks || !d_index_status) return set_err(ZHIP_E_INVALID, "null index pointer");
+        if (!(plan->layout.flags & ZHIP_LF_SHARDED) || !(plan->layout.flags & ZHIP_LF_CRC) ||
+            (decode_flags & ZHIP_DF_TILE) || plan->idx_nbytes == 0)
+            return set_err(ZHIP_E_UNSUPPORTED, "index check cannot be fused for this plan");
+    }
     const zhip_layout& L = plan->layout;
     if (!(L.flags & ZHIP_LF_NO_WRITE) && !out) return set_err(ZHIP_E_INVALID, "null out");
     const uint64_t units = (uint64_t)n_chunks * plan->nseg;
@@ -313,6 +336,13 @@ int zhip_decode(const zhip_plan* plan, const void* src, uint64_t src_size, void*
     p.n_chunks = n_chunks;
     p.nseg = plan->nseg;
     p.n_units = (uint32_t)units;
+    p.n_idx = n_index;
+    p.idx_chunks = d_index_chunks;
+    p.idx_status = d_index_status;
+    p.idx_nbytes = plan->idx_nbytes;
+    p.idx_E = plan->idx_E;
+    p.idx_c_inv = plan->idx_c_inv;
+    p.idx_c3 = plan->idx_c3;
     p.c_inv = plan->c_inv;
     p.c3 = plan->c3;
     p.lflags = L.flags;

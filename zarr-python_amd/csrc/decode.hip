@@ -87,9 +87,14 @@ __device__ __forceinline__ void load_unit(const DecodeParams& p, const Unit& U, 
     const uint32_t ok = __builtin_amdgcn_readfirstlane(U.mode == ZHIP_ST_OK ? 1u : 0u);
     const uint32_t al4 = __builtin_amdgcn_readfirstlane(
         (uint32_t)(reinterpret_cast<uintptr_t>(U.cp) & 3u) == 0u ? 1u : 0u);
+    const uint32_t nt = __builtin_amdgcn_readfirstlane((p.tune & kTuneNT) && ((reinterpret_cast<uintptr_t>(U.cp) & 15u) == 0u) ? 1u : 0u);
     if (!ok) {
 #pragma unroll
         for (int k = 0; k < K; ++k) blk[k] = make_uint4(0, 0, 0, 0);
+    } else if (nt) {
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            blk[k] = load_block_t<true, true>(U.cp, U.seg_lo + kWgStride * k + 16 * t, p.g.nbytes);
     } else if (al4) {
 #pragma unroll
         for (int k = 0; k < K; ++k)
@@ -119,6 +124,44 @@ __device__ __forceinline__ void finalize_chunk(const DecodeParams& p, uint32_t c
 __device__ __forceinline__ uint32_t load_trailer(const uint8_t* cp, uint32_t n) {
     const uint8_t* tr = cp + n;
     return (uint32_t)tr[0] | ((uint32_t)tr[1] << 8) | ((uint32_t)tr[2] << 16) | ((uint32_t)tr[3] << 24);
+}
+
+// CRC-32C check of one shard index (payload idx_nbytes + LE trailer) by one
+// workgroup: the same per-thread Horner chain as a data unit ending at idx_E
+// (reference point idx_E + 4096), reduced over the workgroup.  `red` is a
+// 4-word LDS scratch the caller does not use concurrently.
+__device__ __forceinline__ void verify_index(const DecodeParams& p, uint32_t j, int t, uint32_t kth,
+                                          const uint32_t* s_tab, uint32_t* red) {
+    const zhip_chunk ch = p.idx_chunks[j];
+    const uint32_t ok = ch.src_len == (uint64_t)p.idx_nbytes + 4u;
+    const uint8_t* cp = p.src + ch.src;
+    const uint32_t nk = (p.idx_E + kWgStride - 1) / kWgStride;
+    const int32_t lo = (int32_t)p.idx_E - (int32_t)(nk * kWgStride);
+    uint32_t acc = 0;
+    if (ok) {
+        for (uint32_t k = 0; k < nk; ++k) {
+            const uint4 v = load_block<false>(cp, lo + kWgStride * (int32_t)k + 16 * t, p.idx_nbytes);
+            acc = tab_apply(s_tab, acc ^ v.x) ^ tab_apply(s_tab + 1024, v.y) ^
+                  tab_apply(s_tab + 2048, v.z) ^ tab_apply(s_tab + 3072, v.w);
+        }
+    }
+    uint32_t v = gf_mul(acc, kth);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v ^= __shfl_xor(v, off, 64);
+    __syncthreads();  // red may still be read from a previous index
+    if ((t & 63) == 0) red[t >> 6] = v;
+    __syncthreads();
+    if (t == 0) {
+        zhip_status st = {ZHIP_ST_LENGTH_MISMATCH, 0u, 0u, 0u};
+        if (ok) {
+            const uint32_t V = red[0] ^ red[1] ^ red[2] ^ red[3];
+            st.stored = load_trailer(cp, p.idx_nbytes);
+            st.computed = ~(gf_mul(V, p.idx_c_inv) ^ p.idx_c3);
+            st.code = st.computed == st.stored ? ZHIP_ST_OK : ZHIP_ST_CRC_MISMATCH;
+        }
+        p.idx_status[j] = st;
+        if (st.code != ZHIP_ST_OK) atomicOr(p.errflag, 1u << st.code);
+    }
 }
 
 struct Pending {  // thread 0's outstanding arrival for one run, checked one run later
@@ -165,17 +208,26 @@ __global__ __launch_bounds__(kThreads) void k_decode(const DecodeParams p) {
     const uint32_t per = p.n_units / G, rem = p.n_units % G;
     const uint32_t q0 = g * per + (g < rem ? g : rem);
     const uint32_t q1 = q0 + per + (g < rem ? 1u : 0u);
-    if (q0 >= q1) return;
+    if (q0 >= q1 && g >= p.n_idx) return;
     uint4 A[K], B[K];
     auto unit_of = [&](uint32_t q) {
         const uint32_t c = q / p.nseg;
         return c * p.nseg + (p.nseg - 1u - (q - c * p.nseg));
     };
-    Unit ua = resolve_unit(p, unit_of(q0), expected);
-    load_unit<K>(p, ua, t, A);
+    Unit ua;
     uint32_t stored = 0;
-    if (CRC && t == 0 && ua.mode == ZHIP_ST_OK) stored = load_trailer(ua.cp, p.g.nbytes);
-    if constexpr (CRC) __syncthreads();  // tables in LDS
+    if (q0 < q1) {
+        ua = resolve_unit(p, unit_of(q0), expected);
+        load_unit<K>(p, ua, t, A);
+        if (CRC && t == 0 && ua.mode == ZHIP_ST_OK) stored = load_trailer(ua.cp, p.g.nbytes);
+    }
+    if constexpr (CRC) {
+        __syncthreads();  // tables in LDS
+        // fused shard-index checks (_decode_shard_index_sync, sharding.py:624-631):
+        // workgroup g verifies indexes g, g+G, ... while its first unit's loads fly
+        for (uint32_t j = g; j < p.n_idx; j += G) verify_index(p, j, t, kth, s_tab, s_red[1]);
+    }
+    if (q0 >= q1) return;
     uint32_t acc = 0, run_bits = 0, run_len = 0, parity = 0;
     for (uint32_t q = q0;;) {
         // software pipeline: issue the next unit's loads before working on this one
@@ -192,12 +244,21 @@ __global__ __launch_bounds__(kThreads) void k_decode(const DecodeParams p) {
             // stores first: they do not depend on the CRC, and starting the write
             // stream early interleaves it with the read stream of later units
             if constexpr (WRITE) {
+                if (FAST && (p.tune & kTuneNT)) {
 #pragma unroll
-                for (int k = 0; k < K; ++k) {
-                    const int32_t o = ua.seg_lo + kWgStride * k + 16 * t;
-                    if (o < 0 || (uint32_t)o >= p.g.nbytes) continue;
-                    if constexpr (FAST) scatter_block_rows<ITEM, SWAP>(p.g, p.out, sel, ua.out_off, o, A[k]);
-                    else scatter_block_generic<ITEM, SWAP>(p.g, p.out, sel, ua.out_off, o, A[k]);
+                    for (int k = 0; k < K; ++k) {
+                        const int32_t o = ua.seg_lo + kWgStride * k + 16 * t;
+                        if (o < 0 || (uint32_t)o >= p.g.nbytes) continue;
+                        scatter_block_rows<ITEM, SWAP, true>(p.g, p.out, sel, ua.out_off, o, A[k]);
+                    }
+                } else {
+#pragma unroll
+                    for (int k = 0; k < K; ++k) {
+                        const int32_t o = ua.seg_lo + kWgStride * k + 16 * t;
+                        if (o < 0 || (uint32_t)o >= p.g.nbytes) continue;
+                        if constexpr (FAST) scatter_block_rows<ITEM, SWAP>(p.g, p.out, sel, ua.out_off, o, A[k]);
+                        else scatter_block_generic<ITEM, SWAP>(p.g, p.out, sel, ua.out_off, o, A[k]);
+                    }
                 }
             }
             if (crc_on) {

@@ -66,6 +66,30 @@ __device__ __forceinline__ uint4 load_block(const uint8_t* cp, int32_t o, uint32
     return mask_tail(v, o, n);
 }
 
+typedef unsigned int zhip_v4u __attribute__((ext_vector_type(4)));
+
+// Streaming (nontemporal) 16-byte load / store: the decode touches every
+// encoded and decoded byte exactly once.
+__device__ __forceinline__ uint4 load_nt16(const uint8_t* p) {
+    const zhip_v4u w = __builtin_nontemporal_load(reinterpret_cast<const zhip_v4u*>(p));
+    return make_uint4(w.x, w.y, w.z, w.w);
+}
+
+__device__ __forceinline__ void store_nt16(uint8_t* p, uint4 v) {
+    zhip_v4u w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, reinterpret_cast<zhip_v4u*>(p));
+}
+
+template <bool AL4, bool NT>
+__device__ __forceinline__ uint4 load_block_t(const uint8_t* cp, int32_t o, uint32_t n) {
+    if constexpr (AL4 && NT) {
+        if (o < 0 || (uint32_t)o >= n) return make_uint4(0, 0, 0, 0);
+        return mask_tail(load_nt16(cp + o), o, n);
+    } else {
+        return load_block<AL4>(cp, o, n);
+    }
+}
+
 __device__ __forceinline__ uint32_t tab_apply(const uint32_t* tab, uint32_t w) {
     return tab[w & 255u] ^ tab[256 + ((w >> 8) & 255u)] ^ tab[512 + ((w >> 16) & 255u)] ^
            tab[768 + (w >> 24)];
@@ -142,14 +166,15 @@ __device__ __forceinline__ void scatter_block_generic(const Geom& g, uint8_t* ou
 
 // Whole-row fast path: rows of the innermost stored dim are fully selected,
 // contiguous in out and a multiple of 16 bytes, out rows 16-byte aligned.
-template <int ITEM, bool SWAP>
+template <int ITEM, bool SWAP, bool NT = false>
 __device__ __forceinline__ void scatter_block_rows(const Geom& g, uint8_t* out, const zhip_sel& s,
                                                    int64_t out_off, int32_t o, uint4 v) {
     const uint32_t r = fdiv_apply((uint32_t)o, g.drow.m, g.drow.s);
     const uint32_t col = (uint32_t)o - r * g.row_bytes;
     int64_t dst = out_off + col;
     if (!sel_offset(g, s, r, g.ndim - 2, dst)) return;
-    *reinterpret_cast<uint4*>(out + dst) = swap_block<ITEM, SWAP>(v);
+    if constexpr (NT) store_nt16(out + dst, swap_block<ITEM, SWAP>(v));
+    else *reinterpret_cast<uint4*>(out + dst) = swap_block<ITEM, SWAP>(v);
 }
 
 

@@ -51,6 +51,10 @@ struct DecodeParams {
     uint32_t t_per_chunk, n_qb, n_cb;
     uint32_t sstride[ZHIP_MAX_DIMS];  // stored-stream byte stride of each dim
     zhip_fdiv d_qb, d_cb;
+    // fused shard-index CRC verification: workgroup g checks indexes g, g+G, ...
+    const zhip_chunk* idx_chunks;
+    zhip_status* idx_status;
+    uint32_t n_idx, idx_nbytes, idx_E, idx_c_inv, idx_c3;
 };
 
 constexpr int kTileRows = 64;    // rows of the contiguous-in-out dim per tile
@@ -60,6 +64,7 @@ constexpr int kTileCols = 256;   // bytes of the innermost stored row per tile
 constexpr uint32_t kTuneSkipCrc = 1u;   // replace the CRC lookups by a plain xor
 constexpr uint32_t kTuneAcqRel = 2u;    // acq_rel ticket (the round-1 first version)
 constexpr uint32_t kTuneNoTicket = 4u;  // xor only, no last-arriver finalize
+constexpr uint32_t kTuneNT = 8u;        // nontemporal loads / stores (fast rows path)
 extern int g_tune_max_grid;
 extern int g_tune_blocks;
 extern uint32_t g_tune_bits;
@@ -129,5 +134,7 @@ struct zhip_plan {
     uint32_t t_per_chunk, n_qb, n_cb;
     uint32_t sstride[ZHIP_MAX_DIMS];
     uint32_t t_c_inv;
-    uint32_t* d_tile_tables;  // horner (stride 16*sstride[tq]) | kthread (256) | kunit (t_per_chunk)
+    uint32_t* d_tile_tables;
+    // shard index (sharded layouts): payload 16*n_inner, E, CRC constants
+    uint32_t idx_nbytes, idx_E, idx_c_inv, idx_c3;  // horner (stride 16*sstride[tq]) | kthread (256) | kunit (t_per_chunk)
 };

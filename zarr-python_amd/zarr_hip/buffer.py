@@ -42,10 +42,18 @@ def empty(shape, dtype, device, order: str = "C"):
 
 
 def to_numpy(t, dtype) -> np.ndarray:
-    """Device tensor -> numpy with the array's dtype (bit-exact: via raw bytes)."""
+    """Device tensor -> numpy with the array's dtype (bit-exact: via raw bytes).
+
+    One hipMemcpyAsync into pinned host memory (DMA at full PCIe rate, no
+    pageable bounce); the returned array keeps the pinned block alive."""
     import torch
 
     dt = np.dtype(dtype).newbyteorder("=")
     c = t.contiguous() if not t.is_contiguous() else t
-    raw = c.reshape(-1).view(torch.uint8).cpu().numpy()
-    return raw.view(dt).reshape(tuple(t.shape))
+    flat = c.reshape(-1).view(torch.uint8)
+    if not flat.is_cuda:
+        return flat.numpy().view(dt).reshape(tuple(t.shape))
+    host = torch.empty(flat.numel(), dtype=torch.uint8, pin_memory=True)
+    host.copy_(flat, non_blocking=True)
+    torch.cuda.current_stream(flat.device).synchronize()
+    return host.numpy().view(dt).reshape(tuple(t.shape))

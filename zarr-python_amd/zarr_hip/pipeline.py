@@ -22,10 +22,11 @@ from typing import Any, Iterable
 import numpy as np
 
 from . import _native as N
+from . import staging
 from .codecs import ShardingCodec, evolve_codecs, parse_codecs, split_codecs
 from .planner import CHUNK_DT, SEL_DT, STATUS_DT, ChainInfo, Tables, analyze_chain, plan_decode
 from .spec import ArraySpec, GetResult
-from .store import DeviceArena, DeviceRef, TAIL_SLACK
+from .store import DeviceRef, DeviceStore, _resolve_range
 
 
 def _torch():
@@ -74,11 +75,16 @@ class DecodeLaunch:
     """One zhip_decode launch with its device-resident tables."""
 
     def __init__(self, layout: N.Layout, chunks: np.ndarray, sels: np.ndarray, src, src_size: int,
-                 out, fast: bool, device, tile: bool = False):
+                 out, fast: bool, device, tile: bool = False, index_chunks: np.ndarray | None = None):
         torch = _torch()
         self.plan = get_plan(layout)
         self.n = len(chunks)
         self.device = device
+        # shard-index CRC checks fused into this launch (zhip_decode_indexed)
+        self.n_idx = 0 if index_chunks is None else len(index_chunks)
+        if self.n_idx:
+            self.d_idx_chunks = _upload(index_chunks, device)
+            self.d_idx_status = torch.zeros(self.n_idx * 4, dtype=torch.int32, device=device)
         self.d_chunks = _upload(chunks, device)
         self.d_sels = _upload(sels if len(sels) else np.zeros(1, SEL_DT), device)
         self.d_status = torch.zeros(max(self.n, 1) * 4, dtype=torch.int32, device=device)
@@ -94,6 +100,13 @@ class DecodeLaunch:
             return
         s = _stream_handle(self.device) if stream is None else stream
         out_ptr = self.out.data_ptr() if self.out is not None else None
+        if self.n_idx:
+            N.check(N.lib().zhip_decode_indexed(
+                self.plan.handle, self.src.data_ptr(), self.src_size, out_ptr, self.d_chunks.data_ptr(),
+                self.n, self.d_sels.data_ptr(), self.d_status.data_ptr(), self.d_ws.data_ptr(),
+                self.d_err.data_ptr(), self.d_idx_chunks.data_ptr(), self.n_idx,
+                self.d_idx_status.data_ptr(), self.flags, s), "zhip_decode_indexed")
+            return
         N.check(N.lib().zhip_decode(self.plan.handle, self.src.data_ptr(), self.src_size, out_ptr,
                                     self.d_chunks.data_ptr(), self.n, self.d_sels.data_ptr(),
                                     self.d_status.data_ptr(), self.d_ws.data_ptr(),
@@ -101,6 +114,9 @@ class DecodeLaunch:
 
     def statuses(self) -> np.ndarray:
         return self.d_status[: self.n * 4].cpu().numpy().view(STATUS_DT)
+
+    def index_statuses(self) -> np.ndarray:
+        return self.d_idx_status[: self.n_idx * 4].cpu().numpy().view(STATUS_DT)
 
     def errflag(self) -> int:
         return int(self.d_err[0].item())
@@ -128,8 +144,12 @@ class DecodeProgram:
 
     def results(self) -> tuple[GetResult, ...]:
         """Synchronise, then raise like the reference or return per-item statuses."""
+        st = None
         if self.index is not None:
             st = self.index.statuses()
+        elif self.data.n_idx:
+            st = self.data.index_statuses()
+        if st is not None:
             bad = np.nonzero(st["code"] != N.ST_OK)[0]
             if len(bad):
                 r = st[bad[0]]
@@ -156,45 +176,10 @@ class DecodeProgram:
         return tuple(out)
 
 
-def _gather_sources(batch: list, device) -> tuple[Any, int, list, list]:
-    """Resolve every ByteGetter to (offset, length, missing) inside ONE device
-    buffer: the shared arena for DeviceStore batches, else a staged copy."""
-    torch = _torch()
-    raws = []
-    for item in batch:
-        bg = item[0]
-        raws.append(bg.get_sync(prototype=None) if hasattr(bg, "get_sync") else bg)
-    arenas = {id(r.arena): r.arena for r in raws if isinstance(r, DeviceRef)}
-    all_dev = all(r is None or isinstance(r, DeviceRef) for r in raws)
-    if all_dev and len(arenas) <= 1:
-        if arenas:
-            arena = next(iter(arenas.values()))
-            src = arena.buf
-            size = arena.top
-        else:
-            src = torch.zeros(TAIL_SLACK + 16, dtype=torch.uint8, device=device)
-            size = 0
-        srcs = [(0, 0, True) if r is None else (r.offset, r.length, False) for r in raws]
-        return src, size, srcs, [src]
-    # stage host (and foreign device) bytes into one pinned buffer -> one H2D copy
-    sizes = [0 if r is None else len(r) for r in raws]
-    offs = []
-    top = 0
-    for n in sizes:
-        offs.append(top)
-        top = (top + n + 255) // 256 * 256
-    host = torch.zeros(top + TAIL_SLACK, dtype=torch.uint8, pin_memory=True)
-    hv = host.numpy()
-    dev = torch.empty(top + TAIL_SLACK, dtype=torch.uint8, device=device)
-    for r, o, n in zip(raws, offs, sizes):
-        if r is not None and n and not isinstance(r, DeviceRef):
-            hv[o: o + n] = np.frombuffer(r, dtype=np.uint8, count=n)
-    dev.copy_(host, non_blocking=True)
-    for r, o, n in zip(raws, offs, sizes):
-        if isinstance(r, DeviceRef) and n:
-            dev[o: o + n].copy_(r.arena.view(r.offset, r.length))
-    srcs = [(0, 0, True) if r is None else (o, n, False) for r, o, n in zip(raws, offs, sizes)]
-    return dev, top, srcs, [dev, host]
+def _device_resident(batch: list) -> bool:
+    """True when every ByteGetter reads from a DeviceStore (bytes already in HBM)."""
+    return all(isinstance(getattr(it[0], "store", None), DeviceStore)
+               or isinstance(getattr(it[0], "value", None), DeviceRef) for it in batch)
 
 
 @dataclass(frozen=True)
@@ -251,17 +236,31 @@ class HipCodecPipeline:
         spec: ArraySpec = batch[0][1]
         device = out.device
         chain: ChainInfo = analyze_chain(self.codecs, spec)
-        src, size, srcs, keep = _gather_sources(batch, device)
+        resolved = None
+        if chain.shard is not None and not _device_resident(batch):
+            sh = chain.shard
+            cps = sh.chunks_per_shard(spec.shape)
+            src, size, item_missing, resolved, keep = staging.gather_sharded_partial(
+                batch, sh, cps, int(np.prod(cps)), sh.chunk_shape, spec, device)
+            srcs = [(0, 0, bool(m)) for m in item_missing]
+        else:
+            src, size, srcs, keep = staging.gather_sources(batch, device)
         items = [(o, n, miss, it[2], it[3]) for (o, n, miss), it in zip(srcs, batch)]
         itemsize = out.element_size()
         if np.dtype(spec.dtype).itemsize != itemsize:
             raise TypeError("out dtype itemsize does not match the array dtype")
         ostr = [int(s) * itemsize for s in out.stride()]
         with torch.cuda.device(device):
-            t = plan_decode(chain, spec, items, ostr, out.data_ptr(), drop_axes)
-            data = DecodeLaunch(t.layout, t.chunks, t.sels, src, size, out, t.fast, device, t.tile)
+            t = plan_decode(chain, spec, items, ostr, out.data_ptr(), drop_axes, resolved)
+            # fuse the shard-index CRC checks into the data launch
+            # (zhip_decode_indexed: needs the CRC tables, i.e. an inner crc32c, and
+            # the non-tiled kernel); else a second NO_WRITE launch
+            fuse = (t.index_layout is not None and resolved is None and chain.inner.crc
+                    and not t.tile)
+            data = DecodeLaunch(t.layout, t.chunks, t.sels, src, size, out, t.fast, device, t.tile,
+                                t.index_chunks if fuse else None)
             index = None
-            if t.index_layout is not None:
+            if t.index_layout is not None and not fuse:
                 index = DecodeLaunch(t.index_layout, t.index_chunks, np.zeros(1, SEL_DT), src, size,
                                      None, False, device)
         return DecodeProgram(t, data, index, len(batch), chain.shard is not None,
@@ -327,4 +326,10 @@ class _Raw:
     value: Any
 
     def get_sync(self, prototype=None, byte_range=None):
-        return self.value
+        v = self.value
+        if byte_range is None or v is None:
+            return v
+        a, b = _resolve_range(byte_range, len(v))
+        if isinstance(v, DeviceRef):
+            return DeviceRef(v.arena, v.offset + a, b - a)
+        return memoryview(v)[a:b]

@@ -218,8 +218,16 @@ def plan_encode(chain: ChainInfo, spec: ArraySpec, items: list, arr_strides_byte
 
 
 def plan_decode(chain: ChainInfo, spec: ArraySpec, items: list, out_strides_bytes,
-                out_base_ptr: int, drop_axes=()) -> Tables:
-    """items: list of (src_off, src_len, missing, chunk_selection, out_selection)."""
+                out_base_ptr: int, drop_axes=(), resolved: list | None = None) -> Tables:
+    """items: list of (src_off, src_len, missing, chunk_selection, out_selection).
+
+    Sharded chains: by default every inner chunk is located by the kernel
+    through the shard index in HBM.  With `resolved` (host-staged partial
+    shard reads, staging.gather_sharded_partial) the host has already fetched
+    the touched inner chunks: resolved[i] = (src_by_slot, len_by_slot,
+    miss_by_slot, index_src) and the data launch is a plain (unsharded) one
+    over those inner chunks; the staged index bytes still get their CRC
+    verified by the index launch."""
     ndim = spec.ndim
     itemsize = spec.dtype.itemsize
     fill = spec.fill_bytes()
@@ -262,9 +270,12 @@ def plan_decode(chain: ChainInfo, spec: ArraySpec, items: list, out_strides_byte
     shape_st = [inner_shape[p] for p in perm]
     ost_st = [ost_dec[p] for p in perm]
     index_size = sh.shard_index_size(n_inner)
-    flags = N.LF_SHARDED | (N.LF_CRC if inner.crc else 0) | (N.LF_SWAP if inner.swap else 0) | \
-        (N.LF_INDEX_START if sh.index_location == "start" else 0)
-    layout = _make_layout(shape_st, itemsize, ost_st, flags, fill, n_inner, index_size)
+    flags = (N.LF_CRC if inner.crc else 0) | (N.LF_SWAP if inner.swap else 0)
+    if resolved is None:
+        flags |= N.LF_SHARDED | (N.LF_INDEX_START if sh.index_location == "start" else 0)
+        layout = _make_layout(shape_st, itemsize, ost_st, flags, fill, n_inner, index_size)
+    else:
+        layout = _make_layout(shape_st, itemsize, ost_st, flags, fill)
     cps_strides = np.array([int(np.prod(cps[d + 1:])) for d in range(ndim)], np.int64)
     proj_cache: dict = {}
     parts = []
@@ -286,18 +297,34 @@ def plan_decode(chain: ChainInfo, spec: ArraySpec, items: list, out_strides_byte
     item_of = np.zeros(total, np.int64)
     pos = 0
     idx_rows = []
+    idx_seen: set = set()
     for i, so, sl, miss, pr, oo, m in parts:
         sl_ = slice(pos, pos + m)
-        chunks["src"][sl_] = so
-        chunks["src_len"][sl_] = sl
-        chunks["flags"][sl_] = N.CF_MISSING if miss else 0
-        chunks["slot"][sl_] = (pr.coords * cps_strides[None, :]).sum(axis=1)
+        slots = (pr.coords * cps_strides[None, :]).sum(axis=1)
         chunks["out_off"][sl_] = oo
+        if resolved is not None:
+            r = resolved[i]
+            if r is None or miss:
+                chunks["flags"][sl_] = N.CF_MISSING
+            else:
+                src_by, len_by, miss_by, isrc = r
+                chunks["src"][sl_] = src_by[slots]
+                chunks["src_len"][sl_] = len_by[slots]
+                chunks["flags"][sl_] = np.where(miss_by[slots], N.CF_MISSING, 0)
+                if isrc >= 0 and isrc not in idx_seen:
+                    idx_seen.add(isrc)
+                    idx_rows.append((i, isrc, index_size))
+        else:
+            chunks["src"][sl_] = so
+            chunks["src_len"][sl_] = sl
+            chunks["flags"][sl_] = N.CF_MISSING if miss else 0
+            chunks["slot"][sl_] = slots
         start[sl_] = pr.sel_start[:, list(perm)]
         count[sl_] = pr.sel_count[:, list(perm)]
         step[sl_] = np.broadcast_to(pr.step[list(perm)], (m, ndim))
         item_of[sl_] = i
-        if not miss and sh.index_has_crc:
+        if resolved is None and not miss and sh.index_has_crc and so not in idx_seen:
+            idx_seen.add(so)
             ipos = 0 if sh.index_location == "start" else sl - index_size
             idx_rows.append((i, so + ipos, index_size))
         pos += m

@@ -15,9 +15,13 @@ class GetResult(TypedDict):
 
 @dataclass(frozen=True)
 class ArrayConfig:
+    """array_spec.py:40-105 (the fields this path reads)."""
+
     order: Literal["C", "F"] = "C"
     write_empty_chunks: bool = False
     read_missing_chunks: bool = True
+    sharding_coalesce_max_gap_bytes: int = 1 << 20
+    sharding_coalesce_max_bytes: int = 16 << 20
 
 
 @dataclass(frozen=True)

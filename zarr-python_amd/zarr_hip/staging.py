@@ -1,0 +1,226 @@
+"""Host -> HBM staging for batches whose bytes live in host memory.
+
+The reference reads chunk bytes into host buffers (``ByteGetter.get_sync``,
+``Store.get_ranges_sync`` with ``coalesce_ranges`` for partial shards:
+src/zarr/abc/store.py:474-539, src/zarr/core/_coalesce.py:61-135,
+src/zarr/codecs/sharding.py:1695-1752).  Here those bytes are packed into one
+pinned buffer (256-byte aligned placements) by a small thread pool, in
+windows of ``WINDOW`` bytes; each window's ``hipMemcpyAsync`` is issued on a
+dedicated copy stream as soon as the window is filled, so host packing
+overlaps PCIe transfer.  The compute stream waits on the copy stream once.
+
+Partial shard reads follow the reference's IO shape: the index is fetched
+by a suffix (or prefix) range request, the touched inner chunks' byte ranges
+are fetched with coalescing, and only those bytes cross PCIe.  The host reads
+the u64 (offset, length) pairs to know what to fetch; the index CRC itself is
+verified on the GPU (the staged index bytes go through the NO_WRITE decode
+launch), so errors surface with the reference's message.
+"""
+
+from __future__ import annotations
+
+import os
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+
+from .store import ALIGN, TAIL_SLACK, DeviceRef, RangeByteRequest, SuffixByteRequest
+
+WINDOW = 8 << 20
+MAX_U64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+_POOL: ThreadPoolExecutor | None = None
+_COPY_STREAMS: dict = {}
+
+
+def _workers() -> int:
+    n = os.cpu_count() or 1
+    cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return max(1, min(n, cap or 8, 16))
+
+
+def _pool() -> ThreadPoolExecutor:
+    global _POOL
+    if _POOL is None:
+        _POOL = ThreadPoolExecutor(max_workers=_workers(), thread_name_prefix="zhip-stage")
+    return _POOL
+
+
+def _copy_stream(device):
+    import torch
+
+    key = torch.device(device).index
+    s = _COPY_STREAMS.get(key)
+    if s is None:
+        s = torch.cuda.Stream(device=device)
+        _COPY_STREAMS[key] = s
+    return s
+
+
+class StagingLayout:
+    """Aligned placements of host byte pieces inside one staging buffer."""
+
+    def __init__(self):
+        self.pieces: list = []  # (buffer-like, dst_off, nbytes)
+        self.top = 0
+
+    def add(self, buf) -> tuple[int, int]:
+        n = len(buf) if buf is not None else 0
+        off = self.top
+        if n:
+            self.pieces.append((buf, off, n))
+        self.top = (off + n + ALIGN - 1) // ALIGN * ALIGN
+        return off, n
+
+    def reserve(self, n: int) -> int:
+        """Space filled later by a device-to-device copy."""
+        off = self.top
+        self.top = (off + n + ALIGN - 1) // ALIGN * ALIGN
+        return off
+
+
+def _fill_window(hv: np.ndarray, parts: list) -> None:
+    for buf, dst, a, b in parts:
+        hv[dst + a: dst + b] = np.frombuffer(buf, dtype=np.uint8)[a:b]
+
+
+def stage(layout: StagingLayout, device):
+    """Copy every piece to one new device buffer; returns (dev, keepalive)."""
+    import torch
+
+    total = max(layout.top, 16)
+    host = torch.empty(total + TAIL_SLACK, dtype=torch.uint8, pin_memory=True)
+    dev = torch.empty(total + TAIL_SLACK, dtype=torch.uint8, device=device)
+    hv = host.numpy()
+    by_window: dict = {}
+    for buf, off, n in layout.pieces:
+        a = 0
+        while a < n:
+            wi = (off + a) // WINDOW
+            b = min(n, (wi + 1) * WINDOW - off)
+            by_window.setdefault(wi, []).append((buf, off, a, b))
+            a = b
+    windows = [(wi * WINDOW, min((wi + 1) * WINDOW, total), by_window[wi])
+               for wi in sorted(by_window)]
+    pool = _pool()
+    futs = [pool.submit(_fill_window, hv, parts) for _, _, parts in windows]
+    compute = torch.cuda.current_stream(device)
+    cs = _copy_stream(device)
+    cs.wait_stream(compute)
+    with torch.cuda.stream(cs):
+        for (a, b, _), f in zip(windows, futs):
+            f.result()
+            dev[a:b].copy_(host[a:b], non_blocking=True)
+    dev.record_stream(cs)
+    compute.wait_stream(cs)
+    return dev, [dev, host]
+
+
+def gather_sources(batch: list, device):
+    """Resolve every ByteGetter to (offset, length, missing) inside ONE device
+    buffer: the shared arena for DeviceStore batches, else a staged copy.
+    Returns (src, size, [(off, len, missing)], keepalive)."""
+    import torch
+
+    raws = []
+    for item in batch:
+        bg = item[0]
+        raws.append(bg.get_sync(prototype=None) if hasattr(bg, "get_sync") else bg)
+    arenas = {id(r.arena): r.arena for r in raws if isinstance(r, DeviceRef)}
+    all_dev = all(r is None or isinstance(r, DeviceRef) for r in raws)
+    if all_dev and len(arenas) <= 1:
+        if arenas:
+            arena = next(iter(arenas.values()))
+            src, size = arena.buf, arena.top
+        else:
+            src = torch.zeros(TAIL_SLACK + 16, dtype=torch.uint8, device=device)
+            size = 0
+        srcs = [(0, 0, True) if r is None else (r.offset, r.length, False) for r in raws]
+        return src, size, srcs, [src]
+    lay = StagingLayout()
+    srcs = []
+    dev_refs = []
+    for r in raws:
+        if r is None:
+            srcs.append((0, 0, True))
+        elif isinstance(r, DeviceRef):  # a foreign arena: device-to-device copy below
+            off = lay.reserve(r.length)
+            dev_refs.append((r, off))
+            srcs.append((off, r.length, False))
+        else:
+            off, n = lay.add(r)
+            srcs.append((off, n, False))
+    dev, keep = stage(lay, device)
+    for r, off in dev_refs:
+        dev[off: off + r.length].copy_(r.arena.view(r.offset, r.length))
+    return dev, lay.top, srcs, keep
+
+
+def _shard_key(bg):
+    st = getattr(bg, "store", None)
+    return (id(st), getattr(bg, "path", id(bg)))
+
+
+def gather_sharded_partial(batch: list, sh, cps, n_inner: int, inner_shape, spec, device):
+    """Host-sourced sharded batch: index by range request, touched inner chunks
+    by coalesced range requests, staged into one device buffer.
+
+    Returns (src, size, item_missing[n_items], resolved, keepalive) where
+    resolved[i] = (src_by_slot, len_by_slot, miss_by_slot, index_src_or_-1)."""
+    from .indexing import basic_projections
+
+    isz = sh.shard_index_size(n_inner)
+    lay = StagingLayout()
+    cps_strides = np.array([int(np.prod(cps[d + 1:])) for d in range(len(cps))], np.int64)
+    shards: dict = {}
+    item_shard = []
+    for item in batch:
+        k = _shard_key(item[0])
+        if k not in shards:
+            shards[k] = {"bg": item[0], "slots": set()}
+        csel = item[2]
+        pr = basic_projections(tuple(csel), spec.shape, inner_shape)
+        shards[k]["slots"].update(int(s) for s in (pr.coords * cps_strides[None, :]).sum(axis=1))
+        item_shard.append(k)
+    out_of_shard = {}
+    for k, s in shards.items():
+        bg = s["bg"]
+        req = SuffixByteRequest(isz) if sh.index_location == "end" else RangeByteRequest(0, isz)
+        raw = bg.get_sync(prototype=None, byte_range=req)
+        if raw is None:
+            out_of_shard[k] = None  # whole shard missing -> fill (status "missing")
+            continue
+        if len(raw) < isz:
+            raise ValueError("shard blob is shorter than its index")
+        idx = np.frombuffer(raw, dtype="<u8", count=2 * n_inner).reshape(n_inner, 2)
+        idx_off, _ = lay.add(raw) if sh.index_has_crc else (-1, 0)
+        src_by = np.zeros(n_inner, np.int64)
+        len_by = np.zeros(n_inner, np.int64)
+        miss_by = np.ones(n_inner, bool)
+        slots = sorted(s["slots"])
+        reqs = []
+        want = []
+        for slot in slots:
+            o, n = idx[slot]
+            if o == MAX_U64 and n == MAX_U64:
+                continue  # missing inner chunk -> fill (sharding.py:700-712)
+            reqs.append(RangeByteRequest(int(o), int(o) + int(n)))
+            want.append(slot)
+        if reqs:
+            st = getattr(bg, "store", None)
+            if st is not None and hasattr(st, "get_ranges_sync"):
+                cfg = spec.config  # forwarded like sharding.py:1695-1752
+                got = st.get_ranges_sync(bg.path, reqs,
+                                         max_gap_bytes=cfg.sharding_coalesce_max_gap_bytes,
+                                         max_coalesced_bytes=cfg.sharding_coalesce_max_bytes)
+            else:
+                got = [(j, bg.get_sync(prototype=None, byte_range=r)) for j, r in enumerate(reqs)]
+            for j, buf in got:
+                slot = want[j]
+                off, n = lay.add(buf)
+                src_by[slot], len_by[slot], miss_by[slot] = off, n, False
+        out_of_shard[k] = (src_by, len_by, miss_by, idx_off)
+    dev, keep = stage(lay, device)
+    missing = np.array([out_of_shard[k] is None for k in item_shard], bool)
+    resolved = [out_of_shard[k] for k in item_shard]
+    return dev, lay.top, missing, resolved, keep

@@ -23,8 +23,98 @@ import numpy as np
 ALIGN = 256
 TAIL_SLACK = 64  # kernels read up to 64 bytes past a blob (include/zarrhip.h)
 
+# Store.get_ranges defaults (src/zarr/core/config.py:104-105: sharding_coalesce_*)
+MAX_GAP_BYTES = 1 << 20
+MAX_COALESCED_BYTES = 16 << 20
 
-class MemoryStore:
+
+@dataclass(frozen=True)
+class RangeByteRequest:
+    """src/zarr/abc/store.py RangeByteRequest: bytes [start, end)."""
+
+    start: int
+    end: int
+
+
+@dataclass(frozen=True)
+class SuffixByteRequest:
+    """The last `suffix` bytes."""
+
+    suffix: int
+
+
+@dataclass(frozen=True)
+class OffsetByteRequest:
+    """Bytes from `offset` to the end."""
+
+    offset: int
+
+
+def _resolve_range(req, n: int) -> tuple[int, int]:
+    """Byte request -> clamped [a, b) over a value of length n."""
+    if req is None:
+        return 0, n
+    if isinstance(req, RangeByteRequest):
+        a, b = req.start, req.end
+    elif isinstance(req, SuffixByteRequest):
+        a, b = max(n - req.suffix, 0), n
+    elif isinstance(req, OffsetByteRequest):
+        a, b = req.offset, n
+    else:
+        a, b = req
+    a = min(max(int(a), 0), n)
+    return a, min(max(int(b), a), n)
+
+
+def coalesce_ranges(byte_ranges, *, max_gap_bytes: int = MAX_GAP_BYTES,
+                    max_coalesced_bytes: int = MAX_COALESCED_BYTES):
+    """Plan merged fetches (src/zarr/core/_coalesce.py:61-135): ranges sorted by
+    start merge while the gap to the group's running end is <= max_gap_bytes
+    and the merged span stays <= max_coalesced_bytes.  Returns
+    (groups of [(input_index, RangeByteRequest)], uncoalescable [(i, req)])."""
+    indexed = list(enumerate(byte_ranges))
+    mergeable = [(i, r) for i, r in indexed if isinstance(r, RangeByteRequest)]
+    other = [(i, r) for i, r in indexed if not isinstance(r, RangeByteRequest)]
+    mergeable.sort(key=lambda pr: pr[1].start)
+    groups: list = []
+    g_start = g_end = 0
+    for pr in mergeable:
+        r = pr[1]
+        if groups and r.start - g_end <= max_gap_bytes:
+            new_end = max(g_end, r.end)
+            if new_end - g_start <= max_coalesced_bytes:
+                groups[-1].append(pr)
+                g_end = new_end
+                continue
+        groups.append([pr])
+        g_start, g_end = r.start, r.end
+    return groups, other
+
+
+class _RangesMixin:
+    def get_ranges_sync(self, key: str, byte_ranges, *, max_gap_bytes: int = MAX_GAP_BYTES,
+                        max_coalesced_bytes: int = MAX_COALESCED_BYTES):
+        """Store.get_ranges_sync (src/zarr/abc/store.py:474-539): one fetch per
+        coalesced group, sliced back per input; yields (input_index, buf)."""
+        groups, other = coalesce_ranges(byte_ranges, max_gap_bytes=max_gap_bytes,
+                                        max_coalesced_bytes=max_coalesced_bytes)
+        out = []
+        for g in groups:
+            a = g[0][1].start
+            b = max(r.end for _, r in g)
+            big = self.get_sync(key, RangeByteRequest(a, b))
+            if big is None:
+                raise FileNotFoundError(key)
+            out.extend((i, big[r.start - a: r.end - a]) for i, r in g)
+        for i, r in other:
+            v = self.get_sync(key, r)
+            if v is None:
+                raise FileNotFoundError(key)
+            out.append((i, v))
+        return out
+
+
+class MemoryStore(_RangesMixin):
     """Host dict store (MemoryStore restated)."""
 
     supports_sync_io = True
@@ -38,7 +128,7 @@ class MemoryStore:
             return None
         if byte_range is None:
             return memoryview(v)
-        a, b = byte_range
+        a, b = _resolve_range(byte_range, len(v))
         return memoryview(v)[a:b]
 
     def set_sync(self, key: str, value) -> None:
@@ -78,7 +168,7 @@ class LocalStore(MemoryStore):
         with open(p, "rb") as f:
             if byte_range is None:
                 return memoryview(f.read())
-            a, b = byte_range
+            a, b = _resolve_range(byte_range, os.fstat(f.fileno()).st_size)
             f.seek(a)
             return memoryview(f.read(b - a))
 
@@ -203,7 +293,7 @@ class DeviceStore:
             return None
         off, n = v
         if byte_range is not None:
-            a, b = byte_range
+            a, b = _resolve_range(byte_range, n)
             return DeviceRef(self.arena, off + a, b - a)
         return DeviceRef(self.arena, off, n)
 
@@ -241,7 +331,9 @@ class DeviceStore:
 
     def to_dict(self) -> dict[str, bytes]:
         host = self.arena.buf[: self.arena.top].cpu().numpy()
-        return {k: host[o: o + n].tobytes() for k, (o, n) in self._index.items()}
+        d = {k: host[o: o + n].tobytes() for k, (o, n) in self._index.items()}
+        d.update(self._meta)
+        return d
 
     @classmethod
     def from_host(cls, data: dict, device="cuda:0") -> "DeviceStore":
