@@ -154,6 +154,10 @@ int zhip_plan_info(const zhip_plan *plan, uint32_t *units_per_chunk, uint32_t *w
 #define ZHIP_DF_TILE 2u       /* transposed layout: every chunk fully selected, the
                                  out-contiguous stored dim is tiled through LDS;
                                  out offsets/strides 16-byte aligned */
+#define ZHIP_DF_ROWS 4u       /* with ZHIP_DF_FAST_ROWS: every selection has unit
+                                 steps, innermost rows are 2^k <= 4096 bytes and
+                                 shape[ndim-2] is a multiple of 4096/row_bytes
+                                 (ndim >= 2): affine per-step addressing */
 
 /* Upload the plan's constant tables to the current HIP device (once). */
 int zhip_plan_upload(zhip_plan *plan);

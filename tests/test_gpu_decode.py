@@ -260,3 +260,51 @@ def test_fused_index_crc_mismatch(device, loc):
     with pytest.raises(ValueError) as got:
         arr[...]
     assert str(got.value) == str(want.value)
+
+
+# ------------------------------------ affine whole-row decode (ZHIP_DF_ROWS)
+
+ROWS_CASES = [
+    ((64, 96, 64), (32, 32, 64), "float32", (Ellipsis,)),
+    ((64, 96, 64), (32, 32, 64), "float32", (slice(5, 61), slice(3, 90), slice(None))),
+    ((64, 96, 64), (32, 32, 64), "float32", (7, slice(10, 70), slice(None))),
+    ((40, 64, 64), (20, 32, 64), "int16", (slice(1, 39), slice(31, 33), slice(None))),
+    ((16, 64, 64), (8, 16, 64), "float64", (Ellipsis,)),
+    ((128, 256), (64, 64), "float32", (slice(17, 100), slice(None))),
+    ((4, 512, 16), (2, 256, 16), "uint8", (slice(None), slice(100, 400), slice(None))),
+]
+
+
+@pytest.mark.parametrize("shape,chunks,dtype,sel", ROWS_CASES)
+@pytest.mark.parametrize("endian", [LE, BE])
+def test_rows_kernel(device, shape, chunks, dtype, sel, endian):
+    if dtype == "uint8" and endian is BE:
+        endian = {"name": "bytes"}
+    arr, host, meta = _roundtrip(device, shape, chunks, dtype, [endian, CRC], selection=sel,
+                                 fill=3, drop=["c/0/1/0", "c/1/0"])
+    prog, _ = arr.prepare_read(sel)
+    assert prog.tables.rows
+
+
+def test_rows_kernel_sharded_and_missing_inner(device):
+    import zarr_hip
+
+    codecs = [SHARD((16, 16, 64), [LE, CRC])]
+    meta = O.ArrayMeta((64, 64, 64), (32, 32, 64), np.dtype("float32"), -1.0, codecs=codecs)
+    data = _data((64, 64, 64), "float32")
+    data[0:16, 16:32, :] = -1.0  # an elided inner chunk
+    host = {}
+    O.write(host, meta, (Ellipsis,), data)
+    store = zarr_hip.DeviceStore.from_host(host, device)
+    arr = zarr_hip.Array.create(store, (64, 64, 64), (32, 32, 64), "float32", -1.0, codecs=codecs)
+    for sel in [(Ellipsis,), (slice(3, 50), slice(9, 60), slice(None))]:
+        prog, _ = arr.prepare_read(sel)
+        assert prog.tables.rows and prog.data.n_idx == 4
+        got = arr[sel]
+        assert got.tobytes() == np.ascontiguousarray(O.read(host, meta, sel)).tobytes()
+
+
+def test_c2_takes_rows_kernel(device):
+    arr, _, _ = _roundtrip(device, (128, 128, 128), (64, 64, 64), "float32", [LE, CRC])
+    prog, _ = arr.prepare_read((Ellipsis,))
+    assert prog.tables.fast and prog.tables.rows

@@ -355,6 +355,21 @@ int zhip_decode_indexed(const zhip_plan* plan, const void* src, uint64_t src_siz
     p.fast = (decode_flags & ZHIP_DF_FAST_ROWS) ? 1u : 0u;
     p.tune = g_tune_bits;
     p.tq = -1;
+    p.rows = 0;
+    if (decode_flags & ZHIP_DF_ROWS) {
+        const uint32_t rb = plan->row_bytes;
+        const int nd = L.ndim;
+        const bool pow2 = rb >= 16 && rb <= (uint32_t)kWgStride && (rb & (rb - 1)) == 0;
+        if (!(decode_flags & ZHIP_DF_FAST_ROWS) || (decode_flags & ZHIP_DF_TILE) || nd < 2 || !pow2 ||
+            (L.flags & ZHIP_LF_NO_WRITE) || (uint32_t)L.shape[nd - 2] % ((uint32_t)kWgStride / rb) != 0)
+            return set_err(ZHIP_E_INVALID, "ZHIP_DF_ROWS preconditions do not hold for this layout");
+        p.rows = 1;
+        p.row_shift = (uint32_t)__builtin_ctz(rb);
+        p.r_sy = (uint32_t)L.shape[nd - 2];
+        p.r_dy = make_fdiv(p.r_sy);
+        p.r_oy = L.out_stride[nd - 2];
+        p.nd2 = nd - 2;
+    }
     if ((decode_flags & ZHIP_DF_TILE) && plan->tq >= 0 && plan->d_tile_tables) {
         p.tq = plan->tq;
         p.t_per_chunk = plan->t_per_chunk;

@@ -55,6 +55,13 @@ struct DecodeParams {
     const zhip_chunk* idx_chunks;
     zhip_status* idx_status;
     uint32_t n_idx, idx_nbytes, idx_E, idx_c_inv, idx_c3;
+    // whole-row affine mapping (ZHIP_DF_ROWS, k_decode_rows): rows of 2^row_shift
+    // bytes, 4096 / row_bytes rows per workgroup step, never crossing dim ndim-2
+    uint32_t row_shift, r_sy;  // log2(row_bytes), shape[ndim-2]
+    zhip_fdiv r_dy;            // division by shape[ndim-2]
+    int64_t r_oy;              // out stride of dim ndim-2
+    int32_t nd2;               // ndim - 2
+    uint32_t rows;             // 1: launch k_decode_rows
 };
 
 constexpr int kTileRows = 64;    // rows of the contiguous-in-out dim per tile

@@ -29,6 +29,7 @@ CF_MISSING = 1
 
 DF_FAST_ROWS = 1
 DF_TILE = 2
+DF_ROWS = 4
 
 PF_INDEX_START = 1
 PF_INDEX_CRC = 2

@@ -75,7 +75,8 @@ class DecodeLaunch:
     """One zhip_decode launch with its device-resident tables."""
 
     def __init__(self, layout: N.Layout, chunks: np.ndarray, sels: np.ndarray, src, src_size: int,
-                 out, fast: bool, device, tile: bool = False, index_chunks: np.ndarray | None = None):
+                 out, fast: bool, device, tile: bool = False, index_chunks: np.ndarray | None = None,
+                 rows: bool = False):
         torch = _torch()
         self.plan = get_plan(layout)
         self.n = len(chunks)
@@ -93,7 +94,8 @@ class DecodeLaunch:
         self.src = src
         self.src_size = src_size
         self.out = out
-        self.flags = (N.DF_FAST_ROWS if fast else 0) | (N.DF_TILE if tile else 0)
+        self.flags = (N.DF_FAST_ROWS if fast else 0) | (N.DF_TILE if tile else 0) | \
+            (N.DF_ROWS if fast and rows else 0)
 
     def launch(self, stream: int | None = None) -> None:
         if self.n == 0:
@@ -258,7 +260,7 @@ class HipCodecPipeline:
             fuse = (t.index_layout is not None and resolved is None and chain.inner.crc
                     and not t.tile)
             data = DecodeLaunch(t.layout, t.chunks, t.sels, src, size, out, t.fast, device, t.tile,
-                                t.index_chunks if fuse else None)
+                                t.index_chunks if fuse else None, t.rows)
             index = None
             if t.index_layout is not None and not fuse:
                 index = DecodeLaunch(t.index_layout, t.index_chunks, np.zeros(1, SEL_DT), src, size,

@@ -108,6 +108,7 @@ class Tables:
     fast: bool
     item_of_chunk: np.ndarray     # int64[n]: batch item of each chunk entry
     tile: bool = False            # tiled-transpose decode (ZHIP_DF_TILE)
+    rows: bool = False            # affine whole-row decode (ZHIP_DF_ROWS, k_decode_rows)
     index_layout: N.Layout | None = None
     index_chunks: np.ndarray | None = None
     index_item: np.ndarray | None = None
@@ -166,6 +167,21 @@ def _fast_ok(layout: N.Layout, start, count, step, out_offs, out_base_ptr: int) 
             return False
     return bool(np.all(start[:, last] == 0) and np.all(count[:, last] == layout.shape[last])
                 and np.all(step[:, last] == 1))
+
+
+def _rows_ok(layout: N.Layout, count, step) -> bool:
+    """ZHIP_DF_ROWS preconditions (on top of _fast_ok): unit steps wherever more
+    than one index is selected, rows of 2^k <= 4096 bytes, and shape[ndim-2] a
+    multiple of the rows one 4 KiB workgroup step covers."""
+    nd = layout.ndim
+    if nd < 2:
+        return False
+    rb = layout.shape[nd - 1] * layout.itemsize
+    if rb < 16 or rb > 4096 or rb & (rb - 1):
+        return False
+    if layout.shape[nd - 2] % (4096 // rb):
+        return False
+    return bool(np.all((step == 1) | (count <= 1)))
 
 
 def _tile_ok(layout: N.Layout, start, count, step, out_offs, out_base_ptr: int) -> bool:
@@ -258,7 +274,8 @@ def plan_decode(chain: ChainInfo, spec: ArraySpec, items: list, out_strides_byte
         chunks["sel"] = inv
         fast = _fast_ok(layout, start, count, step, chunks["out_off"], out_base_ptr)
         tile = not fast and _tile_ok(layout, start, count, step, chunks["out_off"], out_base_ptr)
-        return Tables(layout, chunks, sels, fast, np.arange(n), tile=tile)
+        rows = fast and _rows_ok(layout, count, step)
+        return Tables(layout, chunks, sels, fast, np.arange(n), tile=tile, rows=rows)
 
     # ---- sharded: expand every shard item into its inner chunks ----
     sh = chain.shard
@@ -332,7 +349,8 @@ def plan_decode(chain: ChainInfo, spec: ArraySpec, items: list, out_strides_byte
     chunks["sel"] = inv
     fast = _fast_ok(layout, start, count, step, chunks["out_off"], out_base_ptr)
     tile = not fast and _tile_ok(layout, start, count, step, chunks["out_off"], out_base_ptr)
-    t = Tables(layout, chunks, sels, fast, item_of, tile=tile)
+    rows = fast and _rows_ok(layout, count, step)
+    t = Tables(layout, chunks, sels, fast, item_of, tile=tile, rows=rows)
     if idx_rows:
         L2 = _make_layout([16 * n_inner], 1, [0], N.LF_CRC | N.LF_NO_WRITE, b"\0")
         ic = np.zeros(len(idx_rows), CHUNK_DT)
