@@ -22,6 +22,12 @@ if [ "${PROFILE:-1}" = "1" ]; then
   find "$GRAFT_REPO_ROOT/gpurun_out/prof" -name "*stats*" | head
   if [ $rc -ne 0 ]; then exit $rc; fi
 fi
+if [ "${TORCHRUN:-0}" = "1" ]; then
+  cd "$GRAFT_REPO_ROOT"
+  timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --extra "" > gpurun_out/bench_torchrun.json 2> gpurun_out/bench_torchrun.err
+  rc=$?; echo "torchrun bench rc=$rc"; cat gpurun_out/bench_torchrun.json
+  if [ $rc -ne 0 ]; then tail -5 gpurun_out/bench_torchrun.err; exit $rc; fi
+fi
 if [ "${PMC:-0}" = "1" ]; then
   bash "$GRAFT_REPO_ROOT/scripts/gpu_pmc.sh"
   rc=$?

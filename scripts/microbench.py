@@ -62,7 +62,7 @@ def main():
         for prog, out in progs:
             t = prog.tables
             kvar[kb].append(PL.DecodeLaunch(t.layout, t.chunks, t.sels, prog.data.src,
-                                            prog.data.src_size, out, True, dev))
+                                            prog.data.src_size, out, True, dev, rows=t.rows))
         arms.append(("decodeK%d" % kb, 0, 0))
     N.lib().zhip_set_tuning(3, 0)
     PL._PLAN_CACHE.clear()
@@ -82,8 +82,8 @@ def main():
                                        rows=True))
         fastpath.append(DecodeLaunch(t.layout, t.chunks, t.sels, prog.data.src, prog.data.src_size, out,
                                      True, dev, rows=False))
+    arms.append(("fastpath", 0, 8))
     for g in grids:
-        arms.append(("fastpath", g, 8))
         arms.append(("nocrc_rows", g, 0))
     arms.append(("torch_copy", 0, 0))
     arms.append(("torch_read_sum", 0, 0))

@@ -490,12 +490,13 @@ static KernelFn select_tile_kernel(bool crc, int item, bool swap) {
     }
 }
 
-KernelFn select_rows_kernel(bool crc, int item, bool swap);  // decode_rows.hip
+KernelFn select_rows_kernel(bool crc, int item, bool swap, int k);  // decode_rows.hip
 
 int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
     if (g_tune_max_grid > 0) max_grid = g_tune_max_grid;
     if (p.rows) {
-        KernelFn fn = select_rows_kernel((p.lflags & ZHIP_LF_CRC) != 0, p.g.itemsize, (p.lflags & ZHIP_LF_SWAP) != 0);
+        KernelFn fn = select_rows_kernel((p.lflags & ZHIP_LF_CRC) != 0, p.g.itemsize, (p.lflags & ZHIP_LF_SWAP) != 0,
+                                         (int)(p.seg / kWgStride));
         if (!fn) return ZHIP_E_UNSUPPORTED;
         if (p.n_units == 0) return ZHIP_OK;
         if (g_tune_max_grid <= 0) {

@@ -27,8 +27,7 @@ namespace zhip {
 
 namespace {
 
-constexpr int kRowsK = 8;
-
+template <int kRowsK>
 __device__ __forceinline__ void load_unit_rows(const DecodeParams& p, const Unit& U, int t, uint4 (&blk)[kRowsK]) {
     const uint32_t ok = __builtin_amdgcn_readfirstlane(U.mode == ZHIP_ST_OK ? 1u : 0u);
     const uint32_t al4 = __builtin_amdgcn_readfirstlane(
@@ -112,9 +111,8 @@ __device__ __forceinline__ void retire_uniform(const DecodeParams& p, PendingU& 
 
 }  // namespace
 
-template <bool CRC, int ITEM, bool SWAP>
+template <bool CRC, int ITEM, bool SWAP, int K = 8>
 __global__ __launch_bounds__(kThreads) void k_decode_rows(const DecodeParams p) {
-    constexpr int K = kRowsK;
     __shared__ uint32_t s_tab[CRC ? 16 * 256 : 1];
     __shared__ uint32_t s_mul[CRC ? 16 * kThreads : 1];
     __shared__ uint32_t s_r4[16];
@@ -214,7 +212,7 @@ __global__ __launch_bounds__(kThreads) void k_decode_rows(const DecodeParams p) 
                 }
                 run_bits |= 1u << (ua.sidx & 31u);
                 if (run_end) {
-                    uint32_t v = lanemul(s_mul, s_r4, t, acc);
+                    uint32_t v = (p.tune & kTuneNoLaneMul) ? acc : lanemul(s_mul, s_r4, t, acc);
 #pragma unroll
                     for (int off = 32; off > 0; off >>= 1) v ^= __shfl_xor(v, off, 64);
                     if ((t & 63) == 0) s_red[parity][t >> 6] = v;
@@ -223,7 +221,9 @@ __global__ __launch_bounds__(kThreads) void k_decode_rows(const DecodeParams p) 
                         const uint32_t V = gf_mul_uniform(
                             s_red[parity][0] ^ s_red[parity][1] ^ s_red[parity][2] ^ s_red[parity][3],
                             p.kunit[ua.sidx]);
-                        if (one_atomic) {
+                        if (p.tune & kTuneNoTicket) {  // ablation: no publication / last-arriver
+                            if (t == 0 && V == 0x9E3779B9u) p.status[ua.c].aux = V;
+                        } else if (one_atomic) {
                             retire_uniform(p, pend, full, t);  // the previous run's arrival returned by now
                             if (t == 0) {
                                 uint64_t* w = reinterpret_cast<uint64_t*>(p.ws) + 2ull * ua.c;
@@ -284,7 +284,12 @@ __global__ __launch_bounds__(kThreads) void k_decode_rows(const DecodeParams p) 
 
 using KernelFn = void (*)(const DecodeParams);
 
-KernelFn select_rows_kernel(bool crc, int item, bool swap) {
+KernelFn select_rows_kernel(bool crc, int item, bool swap, int k) {
+    if (k == 4) {  // 16 KiB units (tuning arm)
+        if (crc && item == 4 && !swap) return k_decode_rows<true, 4, false, 4>;
+        return nullptr;
+    }
+    if (k != 8) return nullptr;
     switch (item) {
         case 1: return crc ? k_decode_rows<true, 1, false> : k_decode_rows<false, 1, false>;
         case 2: return crc ? (swap ? k_decode_rows<true, 2, true> : k_decode_rows<true, 2, false>)

@@ -72,6 +72,7 @@ constexpr uint32_t kTuneSkipCrc = 1u;   // replace the CRC lookups by a plain xo
 constexpr uint32_t kTuneAcqRel = 2u;    // acq_rel ticket (the round-1 first version)
 constexpr uint32_t kTuneNoTicket = 4u;  // xor only, no last-arriver finalize
 constexpr uint32_t kTuneNT = 8u;        // nontemporal loads / stores (fast rows path)
+constexpr uint32_t kTuneNoLaneMul = 16u; // rows kernel: skip the per-lane shift multiply
 extern int g_tune_max_grid;
 extern int g_tune_blocks;
 extern uint32_t g_tune_bits;
