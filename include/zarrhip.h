@@ -198,6 +198,12 @@ int zhip_decode_indexed(const zhip_plan *plan, const void *src, uint64_t src_siz
 #define ZHIP_TUNE_BLOCKS 3   /* blocks/thread per unit for plans created afterwards (4, 8, 16) */
 int zhip_set_tuning(int key, int value);
 
+/* Diagnostics: with ablation bit 1024 set, k_decode_pair records per-workgroup
+ * phase timestamps (s_memrealtime, 100 MHz) for the first 8192 workgroups of
+ * each launch; copies n_wg * 8 u64 stamps (+ hardware id) to host memory.  Not
+ * used on the product path. */
+int zhip_debug_stamps(uint64_t *host_out, uint32_t n_wg);
+
 /* Encode `n_chunks` chunks gathered from the device array `arr` into `dst`.
  * Per chunk: zhip_chunk.src = byte offset of the encoded chunk in dst (its
  * N [+4] bytes are written there), out_off = byte offset in arr of the chunk's

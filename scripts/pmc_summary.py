@@ -18,7 +18,7 @@ def main():
     pmc_dir, needle, out = sys.argv[1], sys.argv[2], sys.argv[3]
     vals: dict = {}
     names = set()
-    for f in sorted(glob.glob(os.path.join(pmc_dir, "p*", "*counter_collection.csv"))):
+    for f in sorted(glob.glob(os.path.join(pmc_dir, "**", "*counter_collection.csv"), recursive=True)):
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 if needle not in row["Kernel_Name"]:

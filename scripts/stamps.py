@@ -1,0 +1,72 @@
+#!/usr/bin/env python
+"""Per-workgroup phase timeline of k_decode_pair on the headline batch
+(diagnostics: ablation bit 1024 makes every workgroup record s_memrealtime
+stamps; see zhip_debug_stamps).  Prints one JSON line per phase with quantiles
+(microseconds, relative to the earliest workgroup start), plus the number of
+workgroups resident per CU over time.
+
+Slots: 0 start, 1 loads issued, 2 tables + barrier, 3 unit A stored,
+4 unit B stored, 5 CRC lookups done, 6 run end (atomic returned), 7 exit.
+"""
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "zarr-python_amd"))
+
+import bench  # noqa: E402
+
+
+def main():
+    import torch
+
+    from zarr_hip import _native as N
+
+    dev = torch.device("cuda:0")
+    shape, chunks, shards = (256, 256, 256), (64, 64, 64), (128, 128, 128)
+    data = torch.from_numpy(bench.synthetic(shape)).to(dev)
+    tune = int(os.environ.get("TUNE", "0"))
+    progs = []
+    for _ in range(4):
+        codecs = [bench.LE] if os.environ.get("NOCRC") else [bench.LE, bench.CRC]
+        arr = bench.build_replica(dev, data, shape, chunks, codecs, shards=shards)
+        progs.append(arr.prepare_read((Ellipsis,))[0])
+    sh = int(torch.cuda.current_stream(dev).cuda_stream)
+    N.lib().zhip_set_tuning(2, 1024 | tune)
+    for i in range(8):
+        progs[i % 4].launch(sh)
+    torch.cuda.synchronize(dev)
+    N.lib().zhip_set_tuning(2, 0)
+    for p in progs:
+        p.results()
+    n_wg = 2048 if tune & 128 else 1024
+    buf = np.zeros(n_wg * 8, np.uint64)
+    N.check(N.lib().zhip_debug_stamps(buf.ctypes.data, n_wg), "zhip_debug_stamps")
+    st = buf.reshape(n_wg, 8)
+    hw = (st[:, 0] >> np.uint64(32)).astype(np.int64)
+    t = (st & np.uint64(0xFFFFFFFF)).astype(np.int64)
+    t0 = t[:, 0].min()
+    rel = (t - t0) * 0.01  # 100 MHz -> us
+    names = ["start", "loads_issued", "tables_barrier", "A_stored", "B_stored", "runend_barrier", "V_ready", "exit"]
+    for i, nm in enumerate(names):
+        if rel[:, i].min() < -1e3:
+            continue  # slot not recorded by this variant
+        q = np.percentile(rel[:, i], [0, 10, 50, 90, 100])
+        print(json.dumps({"phase": nm, "us_q0_10_50_90_100": [round(float(x), 2) for x in q]}))
+    for a, b in [(0, 1), (1, 2), (2, 3), (3, 4), (4, 5), (5, 6), (6, 7)]:
+        d = rel[:, b] - rel[:, a]
+        if np.abs(d).max() > 1e4:
+            continue
+        q = np.percentile(d, [10, 50, 90])
+        print(json.dumps({"delta": f"{names[a]}->{names[b]}", "us_q10_50_90": [round(float(x), 2) for x in q]}))
+    xcc = (hw >> 24) & 0xF
+    print(json.dumps({"wg_per_xcc": np.bincount(xcc, minlength=8).tolist(),
+                      "kernel_span_us": round(float(rel[:, 7].max()), 2)}))
+
+
+if __name__ == "__main__":
+    main()

@@ -193,6 +193,55 @@ def test_program_relaunch_is_idempotent(device):
     assert to_numpy(out, "float32").tobytes() == O.read(host, meta).tobytes()
 
 
+def test_read_graph_replay(device):
+    """ReadGraph: captured launches over two programs replay to the oracle's bytes."""
+    import torch
+
+    import zarr_hip
+    from zarr_hip.buffer import to_numpy
+
+    codecs = [SHARD((16, 16, 16), [LE, CRC])]
+    arr, host, meta = _roundtrip(device, (64, 64, 64), (32, 32, 32), "float32", codecs)
+    p1, out1 = arr.prepare_read((Ellipsis,))
+    p2, out2 = arr.prepare_read((slice(5, 60), slice(None, None, 2), 7))
+    g = zarr_hip.ReadGraph([p1, p2], 5, device)
+    out1.zero_()
+    out2.zero_()
+    g.replay()
+    g.replay()
+    g.results()
+    torch.cuda.synchronize(device)
+    assert to_numpy(out1, "float32").tobytes() == O.read(host, meta).tobytes()
+    want2 = O.read(host, meta, (slice(5, 60), slice(None, None, 2), 7))
+    assert to_numpy(out2, "float32").tobytes() == np.ascontiguousarray(want2).tobytes()
+
+
+def test_read_graph_replay_detects_corruption(device):
+    import zarr_hip
+
+    meta = O.ArrayMeta((32, 32), (16, 16), np.dtype("float32"), 0.0, codecs=[LE, CRC])
+    host = {}
+    O.write(host, meta, (Ellipsis,), _data((32, 32), "float32"))
+    store = zarr_hip.DeviceStore.from_host(host, device)
+    arr = zarr_hip.Array.create(store, (32, 32), (16, 16), "float32", 0.0, codecs=[LE, CRC])
+    prog, _ = arr.prepare_read((Ellipsis,))
+    g = zarr_hip.ReadGraph([prog], 3, device)
+    g.replay()
+    g.results()
+    # flip one payload bit of chunk c/1/1 in HBM after capture: the replay re-verifies
+    ref = store.get_sync("c/1/1")
+    ref.arena.buf[ref.offset + 17] ^= 0x08
+    bad = bytearray(host["c/1/1"])
+    bad[17] ^= 0x08
+    host["c/1/1"] = bytes(bad)
+    with pytest.raises(ValueError) as want:
+        O.read(host, meta)
+    g.replay()
+    with pytest.raises(ValueError) as got:
+        g.results()
+    assert str(got.value) == str(want.value)
+
+
 # ------------------------------------------------- tiled transpose (ZHIP_DF_TILE)
 
 @pytest.mark.parametrize("order", [(2, 1, 0), (1, 2, 0), (2, 0, 1), (0, 2, 1)])
@@ -308,3 +357,66 @@ def test_c2_takes_rows_kernel(device):
     arr, _, _ = _roundtrip(device, (128, 128, 128), (64, 64, 64), "float32", [LE, CRC])
     prog, _ = arr.prepare_read((Ellipsis,))
     assert prog.tables.fast and prog.tables.rows
+
+
+def _repack_misaligned(blob: bytes, sh, cps) -> bytes:
+    """Re-pack a shard so every inner chunk sits at an odd byte offset (padding
+    between chunks, reverse order).  The index holds absolute offsets
+    (_ShardIndex, sharding.py:205-318), so a reader must accept any placement."""
+    import math
+
+    chunks = O.shard_reader(np.frombuffer(blob, np.uint8), sh, cps)
+    isz = O.shard_index_size(math.prod(cps), sh.index)
+    start = isz if sh.index_location == "start" else 0
+    parts, top = [], start
+    index = np.full(tuple(cps) + (2,), O.MAX_UINT_64, dtype="<u8")
+    for i, coords in enumerate(reversed(O.lexicographic_order_coords(cps))):
+        raw = chunks[coords]
+        if raw is None:
+            continue
+        pad = 1 + 2 * (i % 3)
+        parts.append(b"\xa5" * pad)
+        top += pad
+        index[coords] = (top, len(raw))
+        parts.append(raw.tobytes())
+        top += len(raw)
+    ib = O.encode_shard_index(index, sh.index).tobytes()
+    body = b"".join(parts)
+    return ib + body if sh.index_location == "start" else body + ib
+
+
+@pytest.mark.parametrize("loc", ["end", "start"])
+def test_rows_kernel_misaligned_inner_chunks(device, loc):
+    """Inner chunks at byte-misaligned offsets through the rows kernel: bit-exact,
+    CRC verified (the unaligned nontemporal loads)."""
+    import zarr_hip
+
+    codecs = [SHARD((16, 256), [LE, CRC], loc)]
+    meta = O.ArrayMeta((64, 512), (32, 512), np.dtype("float32"), 0.0, codecs=codecs)
+    host = {}
+    O.write(host, meta, (Ellipsis,), _data((64, 512), "float32"))
+    sh = meta.chain.shard
+    for k in list(host):
+        if k.startswith("c/"):
+            host[k] = _repack_misaligned(host[k], sh, (2, 2))
+    want = O.read(host, meta)
+    store = zarr_hip.DeviceStore.from_host(host, device)
+    arr = zarr_hip.Array.create(store, meta.shape, meta.chunk_shape, "float32", 0.0, codecs=codecs)
+    prog, out = arr.prepare_read((Ellipsis,))
+    assert prog.tables.rows
+    got = arr[...]
+    assert got.tobytes() == want.tobytes()
+    # a flipped payload bit in a misaligned chunk is still caught
+    k0 = "c/1/0"
+    bad = bytearray(host[k0])
+    raw = O.shard_reader(np.frombuffer(bytes(bad), np.uint8), sh, (2, 2))[(1, 1)]
+    off = bytes(bad).find(raw.tobytes())
+    bad[off + 100] ^= 0x01
+    host[k0] = bytes(bad)
+    with pytest.raises(ValueError) as w:
+        O.read(host, meta)
+    store = zarr_hip.DeviceStore.from_host(host, device)
+    arr = zarr_hip.Array.create(store, meta.shape, meta.chunk_shape, "float32", 0.0, codecs=codecs)
+    with pytest.raises(ValueError) as g:
+        arr[...]
+    assert str(g.value) == str(w.value)

@@ -142,6 +142,12 @@ int zhip_set_tuning(int key, int value) {
 
 int zhip_abi_version(void) { return ZHIP_ABI_VERSION; }
 
+int zhip_debug_stamps(uint64_t* host_out, uint32_t n_wg) {
+    if (!host_out) return set_err(ZHIP_E_INVALID, "null argument");
+    if (zhip::debug_stamps(host_out, n_wg) != 0) return set_err(ZHIP_E_HIP, "hipMemcpyFromSymbol failed");
+    return ZHIP_OK;
+}
+
 const char* zhip_last_error(void) { return g_err.c_str(); }
 
 int zhip_device_count(void) {
@@ -175,6 +181,9 @@ int zhip_plan_create(const zhip_layout* layout, zhip_plan** out) {
     p->R = (uint64_t)p->E + kWgStride;
     p->c_inv = xpow8_inv(p->R - n);
     p->c3 = gf_mul(xpow8(n), 0xFFFFFFFFu);
+    for (int op = 0; op < 4; ++op) p->hx[op] = xpow8((uint64_t)kWgStride - 4u * op);
+    for (int a = 0; a < 16; ++a) p->kq[a] = xpow8((uint64_t)kWgStride - 256u * a);
+    for (int b = 0; b < 16; ++b) p->kq[16 + b] = xpow8_inv(16u * b);
     for (int d = 0; d < ZHIP_MAX_DIMS; ++d) p->dshape[d] = make_fdiv(d < L.ndim && L.shape[d] > 0 ? (uint32_t)L.shape[d] : 1u);
     p->row_bytes = (uint32_t)L.shape[L.ndim - 1] * (uint32_t)L.itemsize;
     p->drow = make_fdiv(p->row_bytes ? p->row_bytes : 1u);
@@ -225,10 +234,18 @@ int zhip_plan_upload(zhip_plan* p) {
     int dev = 0;
     HIP_TRY(hipGetDevice(&dev));
     if (p->d_tables && p->device == dev) return ZHIP_OK;
-    std::vector<uint32_t> h(4096 + kThreads + p->nseg);
+    // horner (4096) | kthread (256) | kunit (nseg) | kpair (nseg x 256): the
+    // per-lane constant kthread[t] * kunit[s] * c_inv of k_decode_pair, whose
+    // run ends then need no uniform multiply at all
+    std::vector<uint32_t> h(4096 + kThreads + p->nseg + (size_t)p->nseg * kThreads);
     build_horner(h.data());
     for (int t = 0; t < kThreads; ++t) h[4096 + t] = xpow8((uint64_t)kWgStride - 16u * t);
     for (uint32_t s = 0; s < p->nseg; ++s) h[4096 + kThreads + s] = xpow8((uint64_t)s * p->seg);
+    for (uint32_t s = 0; s < p->nseg; ++s) {
+        const uint32_t ku = gf_mul(h[4096 + kThreads + s], p->c_inv);
+        for (int t = 0; t < kThreads; ++t)
+            h[4096 + kThreads + p->nseg + (size_t)s * kThreads + t] = gf_mul(h[4096 + t], ku);
+    }
     if (p->d_tables) (void)hipFree(p->d_tables);
     p->d_tables = nullptr;
     HIP_TRY(hipMalloc(&p->d_tables, h.size() * sizeof(uint32_t)));
@@ -333,6 +350,9 @@ int zhip_decode_indexed(const zhip_plan* plan, const void* src, uint64_t src_siz
     p.horner = plan->d_tables;
     p.kthread = plan->d_tables + 4096;
     p.kunit = plan->d_tables + 4096 + kThreads;
+    p.kpair = plan->d_tables + 4096 + kThreads + plan->nseg;
+    for (int op = 0; op < 4; ++op) p.hx[op] = plan->hx[op];
+    for (int i = 0; i < 32; ++i) p.kq[i] = plan->kq[i];
     p.n_chunks = n_chunks;
     p.nseg = plan->nseg;
     p.n_units = (uint32_t)units;

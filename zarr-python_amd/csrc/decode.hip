@@ -491,9 +491,21 @@ static KernelFn select_tile_kernel(bool crc, int item, bool swap) {
 }
 
 KernelFn select_rows_kernel(bool crc, int item, bool swap, int k);  // decode_rows.hip
+KernelFn select_pair_kernel(bool crc, int item, bool swap, int nu);  // decode_rows.hip
 
 int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
     if (g_tune_max_grid > 0) max_grid = g_tune_max_grid;
+    if (p.rows && p.seg == (uint32_t)kWgStride * kDefaultBlocks && !(p.tune & kTunePersist)) {
+        // one workgroup per pair of units, non-persistent (k_decode_pair)
+        const int nu = (p.tune & kTuneSingle) ? 1 : 2;
+        KernelFn fn = select_pair_kernel((p.lflags & ZHIP_LF_CRC) != 0, p.g.itemsize, (p.lflags & ZHIP_LF_SWAP) != 0, nu);
+        if (!fn) return ZHIP_E_UNSUPPORTED;
+        const uint32_t pairs = (uint32_t)(((uint64_t)p.n_units + nu - 1u) / nu);
+        const uint32_t grid = pairs > p.n_idx ? pairs : p.n_idx;
+        if (grid == 0) return ZHIP_OK;
+        hipLaunchKernelGGL(fn, dim3(grid), dim3(kThreads), 0, stream, p);
+        return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
+    }
     if (p.rows) {
         KernelFn fn = select_rows_kernel((p.lflags & ZHIP_LF_CRC) != 0, p.g.itemsize, (p.lflags & ZHIP_LF_SWAP) != 0,
                                          (int)(p.seg / kWgStride));

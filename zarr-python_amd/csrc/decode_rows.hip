@@ -27,27 +27,63 @@ namespace zhip {
 
 namespace {
 
-template <int kRowsK>
-__device__ __forceinline__ void load_unit_rows(const DecodeParams& p, const Unit& U, int t, uint4 (&blk)[kRowsK]) {
-    const uint32_t ok = __builtin_amdgcn_readfirstlane(U.mode == ZHIP_ST_OK ? 1u : 0u);
-    const uint32_t al4 = __builtin_amdgcn_readfirstlane(
-        (uint32_t)(reinterpret_cast<uintptr_t>(U.cp) & 3u) == 0u ? 1u : 0u);
-    if (!ok) {
-#pragma unroll
-        for (int k = 0; k < kRowsK; ++k) blk[k] = make_uint4(0, 0, 0, 0);
-    } else if (al4) {
-        // N is a multiple of 4096: a step is wholly inside [0, N) or wholly before it
-#pragma unroll
-        for (int k = 0; k < kRowsK; ++k) {
-            const int32_t base = U.seg_lo + kWgStride * k;
-            blk[k] = base >= 0 ? load_nt16(U.cp + base + 16 * t) : make_uint4(0, 0, 0, 0);
+// Every wave issues exactly K vector loads per unit, whatever the unit's state:
+// blocks outside the chunk and units that are missing or failed read zeros
+// from g_rows_zero (leading zeros do not change a CRC).  With a path-independent
+// count the compiler can wait for a unit's data with vmcnt(N > 0), leaving the
+// next unit's loads in flight (vmcnt counts in issue order; a path with fewer
+// memory operations would force vmcnt(0)).  N is a multiple of 4096 here, so a
+// step lies wholly inside [0, N) or wholly before it.
+typedef unsigned int zhip_v4u_a1 __attribute__((ext_vector_type(4), aligned(1)));
+typedef __attribute__((address_space(1))) const zhip_v4u_a1 zhip_gv4u_a1;
+
+typedef __attribute__((address_space(1))) const uint32_t zhip_gu32_a1 __attribute__((aligned(1)));
+
+__device__ __forceinline__ uint32_t load_u32_any(const uint8_t* a) {  // any alignment, one global dword
+    return *(zhip_gu32_a1*)(reinterpret_cast<uintptr_t>(a));
+}
+
+__device__ __forceinline__ uint4 load_nt16_any(const uint8_t* a) {  // any alignment, one global dwordx4 nt
+    const zhip_v4u_a1 w = __builtin_nontemporal_load((zhip_gv4u_a1*)(reinterpret_cast<uintptr_t>(a)));
+    return make_uint4(w.x, w.y, w.z, w.w);
+}
+
+// phase timestamps (diagnostics, kTuneStamp): [wg][slot]
+__device__ uint64_t g_stamps[kStampWG * kStampSlots];
+
+__device__ __forceinline__ void stamp(const DecodeParams& p, uint32_t g, int t, int slot) {
+    if ((p.tune & kTuneStamp) && t == 0 && g < kStampWG) {
+        uint64_t v = __builtin_amdgcn_s_memrealtime();
+        if (slot == 0) {  // slot 0 also carries the hardware id (XCC / SE / CU) in the top bits
+            uint32_t hw;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+            uint32_t xcc;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+            v = (v & 0xFFFFFFFFull) | ((uint64_t)(hw & 0xFFFFFFu) << 32) | ((uint64_t)(xcc & 0xFu) << 56);
         }
-    } else {
-#pragma unroll
-        for (int k = 0; k < kRowsK; ++k)
-            blk[k] = load_block<false>(U.cp, U.seg_lo + kWgStride * k + 16 * t, p.g.nbytes);
+        g_stamps[g * kStampSlots + slot] = v;
     }
 }
+
+// zeros: blocks outside the chunk and units that are not present read here
+__device__ uint4 g_rows_zero[kThreads];
+
+template <int kRowsK>
+__device__ __forceinline__ void load_unit_rows(const Unit& U, bool live, int t, uint4 (&blk)[kRowsK]) {
+    const bool ok = live && U.mode == ZHIP_ST_OK;
+    const uint8_t* zero = reinterpret_cast<const uint8_t*>(g_rows_zero);
+#pragma unroll
+    for (int k = 0; k < kRowsK; ++k) {
+        // dummy loads: every lane reads the same 16 zero bytes (one cache line
+        // per wave instruction, no traffic to speak of)
+        const int32_t base = U.seg_lo + kWgStride * k;
+        blk[k] = load_nt16_any(ok && base >= 0 ? U.cp + base + 16 * t : zero);
+    }
+}
+
+// Stores that fall outside the selection go to this sink instead of being
+// skipped, so every unit issues exactly K stores (see load_unit_rows).
+__device__ uint4 g_rows_sink[kThreads];
 
 // Per-lane GF(2) multiply by the thread's fixed shift constant kth (4-bit
 // windows): s_mul[v*256 + t] = (v << 28) * kth, s_r4[n] = n * x^4, so
@@ -55,14 +91,14 @@ __device__ __forceinline__ void load_unit_rows(const DecodeParams& p, const Unit
 // 8 conflict-free LDS reads + 7 reduction reads instead of a 32-step loop.
 __device__ __forceinline__ uint32_t mulx1(uint32_t b) { return (b >> 1) ^ (kPoly & (0u - (b & 1u))); }
 
-__device__ __forceinline__ void lanemul_init(uint32_t* s_mul, uint32_t* s_r4, int t, uint32_t kth) {
+__device__ __forceinline__ void lanemul_init(uint32_t* s_mul, int t, uint32_t kth) {
     const uint32_t m8 = kth, m4 = mulx1(m8), m2 = mulx1(m4), m1 = mulx1(m2);
 #pragma unroll
     for (uint32_t v = 0; v < 16; ++v)
         s_mul[v * kThreads + t] = ((v & 8u) ? m8 : 0u) ^ ((v & 4u) ? m4 : 0u) ^ ((v & 2u) ? m2 : 0u) ^
                                   ((v & 1u) ? m1 : 0u);
-    if (t < 16) s_r4[t] = mulx1(mulx1(mulx1(mulx1((uint32_t)t))));
 }
+
 
 __device__ __forceinline__ uint32_t lanemul(const uint32_t* s_mul, const uint32_t* s_r4, int t, uint32_t a) {
     uint32_t p = s_mul[(a & 15u) * kThreads + t];
@@ -85,8 +121,8 @@ struct PendingU {
 };
 
 __device__ __forceinline__ void finalize_uniform(const DecodeParams& p, uint32_t c, uint32_t stored, uint32_t raw,
-                                                 int t) {
-    const uint32_t computed = ~(gf_mul_uniform(raw, p.c_inv) ^ p.c3);
+                                                 int t, bool scaled = false) {
+    const uint32_t computed = ~((scaled ? raw : gf_mul_uniform(raw, p.c_inv)) ^ p.c3);
     const uint32_t code = computed == stored ? ZHIP_ST_OK : ZHIP_ST_CRC_MISMATCH;
     if (t == 0) {
         zhip_status st = {code, stored, computed, 0u};
@@ -95,7 +131,8 @@ __device__ __forceinline__ void finalize_uniform(const DecodeParams& p, uint32_t
     }
 }
 
-__device__ __forceinline__ void retire_uniform(const DecodeParams& p, PendingU& q, uint64_t full, int t) {
+__device__ __forceinline__ void retire_uniform(const DecodeParams& p, PendingU& q, uint64_t full, int t,
+                                               bool scaled = false) {
     if (!q.valid) return;
     q.valid = 0;
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)q.prev);
@@ -105,18 +142,19 @@ __device__ __forceinline__ void retire_uniform(const DecodeParams& p, PendingU& 
             uint64_t* w = reinterpret_cast<uint64_t*>(p.ws) + 2ull * q.c;
             __hip_atomic_store(w, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        finalize_uniform(p, q.c, q.stored, lo ^ q.V, t);
+        finalize_uniform(p, q.c, q.stored, lo ^ q.V, t, scaled);
     }
 }
 
 }  // namespace
 
 template <bool CRC, int ITEM, bool SWAP, int K = 8>
-__global__ __launch_bounds__(kThreads) void k_decode_rows(const DecodeParams p) {
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_decode_rows(const DecodeParams p) {
     __shared__ uint32_t s_tab[CRC ? 16 * 256 : 1];
     __shared__ uint32_t s_mul[CRC ? 16 * kThreads : 1];
     __shared__ uint32_t s_r4[16];
     __shared__ uint32_t s_red[2][kThreads / 64];
+    __shared__ uint4 s_idx[CRC ? kThreads : 1];
     const int t = threadIdx.x;
     const uint32_t G = gridDim.x, g = blockIdx.x;
     const uint32_t per = p.n_units / G, rem = p.n_units % G;
@@ -128,26 +166,39 @@ __global__ __launch_bounds__(kThreads) void k_decode_rows(const DecodeParams p) 
         const uint32_t c = q / p.nseg;
         return c * p.nseg + (p.nseg - 1u - (q - c * p.nseg));
     };
+    const uint8_t* dummy = reinterpret_cast<const uint8_t*>(g_rows_zero);
+    uint8_t* sink = reinterpret_cast<uint8_t*>(g_rows_sink);  // one line: garbage for every lane
+
+    // Prologue.  Memory order per wave: unit q0 (K loads), this workgroup's
+    // first shard-index block (1 load), then at the loop top unit q0+1 (K
+    // loads).  Unit headers (chunk record, shard-index entry, CRC trailer) are
+    // scalar loads and the CRC tables are computed, so nothing here waits on
+    // vector memory: the first wait (unit q0's data) leaves K + 1 loads in
+    // flight.
     uint4 A[K], B[K];
-    Unit ua;
+    Unit ua, ub;
     uint32_t stored = 0;
-    // first unit's loads go out before anything else (tables, index checks)
-    if (q0 < q1) {
+    const bool units = q0 < q1;
+    if (units) {
         ua = resolve_unit(p, unit_of(q0), expected);
-        load_unit_rows(p, ua, t, A);
-        if (CRC && t == 0 && ua.mode == ZHIP_ST_OK) stored = load_trailer(ua.cp, p.g.nbytes);
+        load_unit_rows(ua, true, t, A);
+        if (CRC && ua.mode == ZHIP_ST_OK) stored = load_trailer_uniform(ua.cp, p.g.nbytes);
     }
+    uint4 ipre = make_uint4(0, 0, 0, 0);
     uint32_t kth = 0;
     if constexpr (CRC) {
-        const uint4* gt = reinterpret_cast<const uint4*>(p.horner);
-        uint4* sv = reinterpret_cast<uint4*>(s_tab);
-        for (int i = t; i < 1024; i += kThreads) sv[i] = gt[i];
-        kth = p.kthread[t];
-        lanemul_init(s_mul, s_r4, t, kth);
+        ipre = index_prefetch(p, g, g < p.n_idx, t, dummy);
+        build_horner_lds(s_tab, t, p.hx);
+        kth = lane_kthread(p, t);
+        if (t < 16) s_r4[t] = mulx1(mulx1(mulx1(mulx1((uint32_t)t))));
+        lanemul_init(s_mul, t, kth);
         __syncthreads();
-        for (uint32_t j = g; j < p.n_idx; j += G) verify_index(p, j, t, kth, s_tab, s_red[1]);
     }
-    if (q0 >= q1) return;
+    if (!units) {  // index checks only
+        if constexpr (CRC)
+            for (uint32_t j = g; j < p.n_idx; j += G) verify_index(p, j, t, kth, s_tab, s_red[1], j == g, ipre);
+        return;
+    }
 
     // per-lane part of the out address: row t*16 >> row_shift of the step, column t*16 mod row
     const uint32_t lane_row = (16u * (uint32_t)t) >> p.row_shift;
@@ -155,47 +206,52 @@ __global__ __launch_bounds__(kThreads) void k_decode_rows(const DecodeParams p) 
     const int64_t lane_off = (int64_t)lane_row * p.r_oy + (int64_t)lane_col;
     const bool one_atomic = p.nseg <= 32;
     const uint64_t full = p.nseg >= 32 ? 0xFFFFFFFFull : ((1ull << p.nseg) - 1ull);
+    const uint4 f = make_uint4(p.fill[0], p.fill[1], p.fill[2], p.fill[3]);
     PendingU pend;
     pend.valid = 0;
     uint32_t acc = 0, run_bits = 0, parity = 0;
+    uint32_t first = 1u;
+    ub = ua;
     for (uint32_t q = q0;;) {
+        // the next unit's K loads go out before this one is processed (dummy
+        // loads after the last unit keep the per-iteration count fixed)
         const uint32_t qn = q + 1;
         const bool more = qn < q1;
-        Unit ub;
-        if (more) {
-            ub = resolve_unit(p, unit_of(qn), expected);
-            load_unit_rows(p, ub, t, B);
+        if (more) ub = advance_unit(p, ua, unit_of(qn), expected);
+        load_unit_rows(ub, more, t, B);
+        if constexpr (CRC) {
+            // the prefetched shard-index block (issued after unit q0, before
+            // unit q0+1) parks in LDS until the index checks after the loop
+            if (first) s_idx[t] = ipre;
+            ipre = make_uint4(0, 0, 0, 0);
         }
         const bool run_end = !more || ub.c != ua.c;
-        const zhip_sel& sel = p.sels[ua.sel];
+        const auto& sel = *uniform_ptr(p.sels + ua.sel);
         const bool present = ua.mode == ZHIP_ST_OK;
-        if (present || ua.mode == ZHIP_ST_MISSING) {
-            // selection of dim ndim-2 (unit steps; innermost rows are whole)
-            const int32_t sy0 = sel.start[p.nd2];
-            const uint32_t cy = (uint32_t)sel.count[p.nd2];
-            const uint4 f = make_uint4(p.fill[0], p.fill[1], p.fill[2], p.fill[3]);
+        const bool writes = present || ua.mode == ZHIP_ST_MISSING;
+        // selection of dim ndim-2 (unit steps; innermost rows are whole)
+        const int32_t sy0 = sel.start[p.nd2];
+        const uint32_t cy = (uint32_t)sel.count[p.nd2];
 #pragma unroll
-            for (int k = 0; k < K; ++k) {
-                const int32_t base_o = ua.seg_lo + kWgStride * k;
-                if (base_o < 0) continue;
-                const uint32_t R = (uint32_t)base_o >> p.row_shift;
-                uint32_t r = fdiv_apply(R, p.r_dy.m, p.r_dy.s);
-                const uint32_t y0 = R - r * p.r_sy;
-                int64_t dst = ua.out_off + (int64_t)((int32_t)y0 - sy0) * p.r_oy;
-                bool uok = true;
+        for (int k = 0; k < K; ++k) {
+            const int32_t base_o = ua.seg_lo + kWgStride * k;
+            const uint32_t R = (uint32_t)base_o >> p.row_shift;
+            uint32_t r = fdiv_apply(R, p.r_dy.m, p.r_dy.s);
+            const uint32_t y0 = R - r * p.r_sy;
+            int64_t dst = ua.out_off + (int64_t)((int32_t)y0 - sy0) * p.r_oy;
+            bool uok = writes && base_o >= 0;
 #pragma unroll
-                for (int d = ZHIP_MAX_DIMS - 3; d >= 0; --d) {
-                    if (d >= p.nd2) continue;
-                    const uint32_t qd = d > 0 ? fdiv_apply(r, p.g.dshape[d].m, p.g.dshape[d].s) : 0u;
-                    const int32_t rel = (int32_t)(r - qd * (uint32_t)p.g.shape[d]) - sel.start[d];
-                    r = qd;
-                    uok = uok && rel >= 0 && rel < sel.count[d];
-                    dst += (int64_t)rel * p.g.ostride[d];
-                }
-                if (!uok) continue;
-                if ((uint32_t)((int32_t)(y0 + lane_row) - sy0) >= cy) continue;
-                store_nt16(p.out + dst + lane_off, present ? swap_block<ITEM, SWAP>(A[k]) : f);
+            for (int d = ZHIP_MAX_DIMS - 3; d >= 0; --d) {
+                if (d >= p.nd2) continue;
+                const uint32_t qd = d > 0 ? fdiv_apply(r, p.g.dshape[d].m, p.g.dshape[d].s) : 0u;
+                const int32_t rel = (int32_t)(r - qd * (uint32_t)p.g.shape[d]) - sel.start[d];
+                r = qd;
+                uok = uok && rel >= 0 && rel < sel.count[d];
+                dst += (int64_t)rel * p.g.ostride[d];
             }
+            // every lane stores (to the sink when outside the selection): K stores per unit
+            const bool wr = uok && (uint32_t)((int32_t)(y0 + lane_row) - sy0) < cy;
+            store_nt16(wr ? p.out + dst + lane_off : sink, present ? swap_block<ITEM, SWAP>(A[k]) : f);
         }
         if (present) {
             if constexpr (CRC) {
@@ -205,7 +261,7 @@ __global__ __launch_bounds__(kThreads) void k_decode_rows(const DecodeParams p) 
                 } else {
 #pragma unroll
                     for (int k = 0; k < K; ++k) {
-                        const uint4 v = A[k];
+                        const uint4 v = A[k];  // blocks before the chunk start read zeros
                         acc = tab_apply(s_tab, acc ^ v.x) ^ tab_apply(s_tab + 1024, v.y) ^
                               tab_apply(s_tab + 2048, v.z) ^ tab_apply(s_tab + 3072, v.w);
                     }
@@ -272,17 +328,305 @@ __global__ __launch_bounds__(kThreads) void k_decode_rows(const DecodeParams p) 
             p.status[ua.c] = st;
             if (ua.mode != ZHIP_ST_MISSING) atomicOr(p.errflag, 1u << ua.mode);
         }
+        if constexpr (CRC) {
+            first = 0u;
+            asm volatile("" : "+s"(first));  // opaque: no first-iteration peeling
+        }
         if (!more) break;
-        if (CRC && t == 0 && ub.c != ua.c && ub.mode == ZHIP_ST_OK) stored = load_trailer(ub.cp, p.g.nbytes);
+        if (CRC && ub.c != ua.c && ub.mode == ZHIP_ST_OK) stored = load_trailer_uniform(ub.cp, p.g.nbytes);
         q = qn;
         ua = ub;
 #pragma unroll
         for (int k = 0; k < K; ++k) A[k] = B[k];
     }
+    if constexpr (CRC) {
+        // fused shard-index checks: the first block is resident in LDS
+        __syncthreads();
+        for (uint32_t j = g; j < p.n_idx; j += G) {
+            verify_index(p, j, t, kth, s_tab, s_red[1], j == g, s_idx[t]);
+        }
+    }
     if (t < 64) retire_uniform(p, pend, full, t);
 }
 
+// ---------------------------------------------------------------------------
+// k_decode_pair: the same decode with a non-persistent grid, one workgroup per
+// pair of consecutive units (2 x 32 KiB).  Straight-line: both units' loads go
+// out first, then both units' stores (as each arrives), then both units' CRC
+// lookups — so the writes never queue behind LDS work, and the hardware
+// dispatcher overlaps one workgroup's CRC tail with the next one's loads on
+// the same CU.  The CRC tables are computed in LDS (no loads), so a short-lived
+// workgroup costs no extra memory traffic.  Index checks run in the lowest
+// workgroups (dispatched first, finished early).
+
+__device__ __forceinline__ uint32_t crc_block(const uint32_t* s_tab, uint32_t acc, const uint4 v) {
+    return tab_apply(s_tab, acc ^ v.x) ^ tab_apply(s_tab + 1024, v.y) ^ tab_apply(s_tab + 2048, v.z) ^
+           tab_apply(s_tab + 3072, v.w);
+}
+
+// Stores of one unit; with `crc` the Horner step of each block follows its
+// store (the lookups spread over the data's arrival instead of trailing it).
+template <int ITEM, bool SWAP, int K>
+__device__ __forceinline__ void store_unit_rows(const DecodeParams& p, const Unit& U, bool live, int t,
+                                                uint32_t lane_row, int64_t lane_off, uint8_t* sink,
+                                                const uint4 (&blk)[K], bool crc = false,
+                                                const uint32_t* s_tab = nullptr, uint32_t* acc = nullptr) {
+    const auto& sel = *uniform_ptr(p.sels + U.sel);
+    const bool present = live && U.mode == ZHIP_ST_OK;
+    const bool writes = live && (U.mode == ZHIP_ST_OK || U.mode == ZHIP_ST_MISSING);
+    const int32_t sy0 = sel.start[p.nd2];
+    const uint32_t cy = (uint32_t)sel.count[p.nd2];
+    const uint4 f = make_uint4(p.fill[0], p.fill[1], p.fill[2], p.fill[3]);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int32_t base_o = U.seg_lo + kWgStride * k;
+        const uint32_t R = (uint32_t)base_o >> p.row_shift;
+        uint32_t r = fdiv_apply(R, p.r_dy.m, p.r_dy.s);
+        const uint32_t y0 = R - r * p.r_sy;
+        int64_t dst = U.out_off + (int64_t)((int32_t)y0 - sy0) * p.r_oy;
+        bool uok = writes && base_o >= 0;
+#pragma unroll
+        for (int d = ZHIP_MAX_DIMS - 3; d >= 0; --d) {
+            if (d >= p.nd2) continue;
+            const uint32_t qd = d > 0 ? fdiv_apply(r, p.g.dshape[d].m, p.g.dshape[d].s) : 0u;
+            const int32_t rel = (int32_t)(r - qd * (uint32_t)p.g.shape[d]) - sel.start[d];
+            r = qd;
+            uok = uok && rel >= 0 && rel < sel.count[d];
+            dst += (int64_t)rel * p.g.ostride[d];
+        }
+        const bool wr = uok && (uint32_t)((int32_t)(y0 + lane_row) - sy0) < cy;
+        store_nt16(wr ? p.out + dst + lane_off : sink, present ? swap_block<ITEM, SWAP>(blk[k]) : f);
+        if (crc) *acc = crc_block(s_tab, *acc, blk[k]);
+    }
+}
+
+template <int K>
+__device__ __forceinline__ uint32_t crc_unit_rows(const uint32_t* s_tab, uint32_t acc, const uint4 (&blk)[K],
+                                                  uint32_t tune) {
+    if (tune & kTuneSkipCrc) {  // ablation: lookups replaced by a plain xor
+#pragma unroll
+        for (int k = 0; k < K; ++k) acc ^= blk[k].x ^ blk[k].y ^ blk[k].z ^ blk[k].w;
+        return acc;
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint4 v = blk[k];  // blocks before the chunk start hold zeros
+        acc = tab_apply(s_tab, acc ^ v.x) ^ tab_apply(s_tab + 1024, v.y) ^ tab_apply(s_tab + 2048, v.z) ^
+              tab_apply(s_tab + 3072, v.w);
+    }
+    return acc;
+}
+
+// End of a run (consecutive units of one chunk in this workgroup): reduce the
+// lanes' Horner states, shift to the chunk reference, publish with one 64-bit
+// atomic (CRC contribution | arrival bits); the arrival that completes the
+// chunk finalizes it.  `red` is a 4-word LDS scratch not used concurrently.
+// End of a run (consecutive units of one chunk in this workgroup): shift every
+// lane's Horner state by its kpair constant (lane shift x unit shift x c_inv,
+// so no uniform multiply remains), xor-reduce over the workgroup, publish with
+// one 64-bit atomic (contribution | arrival bits); the arrival that completes
+// the chunk compares with the trailer.  `red` is a 4-word LDS scratch.
+template <bool LDS_MUL>
+__device__ __forceinline__ void run_end_pair(const DecodeParams& p, const Unit& U, uint32_t acc, uint32_t run_bits,
+                                             uint32_t stored, uint32_t klane, const uint32_t* s_mul,
+                                             const uint32_t* s_r4, uint32_t* red, int t, uint32_t g = 0) {
+    uint32_t v = LDS_MUL ? lanemul(s_mul, s_r4, t, acc) : gf_mul(acc, klane);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v ^= __shfl_xor(v, off, 64);
+    if ((t & 63) == 0) red[t >> 6] = v;
+    __syncthreads();
+    stamp(p, g, t, 5);
+    if (t < 64) {  // wave 0, wave-uniform
+        const uint32_t V = __builtin_amdgcn_readfirstlane(red[0] ^ red[1] ^ red[2] ^ red[3]);
+        stamp(p, g, t, 6);
+        if (p.nseg <= 32) {
+            const uint64_t full = p.nseg >= 32 ? 0xFFFFFFFFull : ((1ull << p.nseg) - 1ull);
+            uint64_t prev = 0;
+            if (t == 0) {
+                uint64_t* w = reinterpret_cast<uint64_t*>(p.ws) + 2ull * U.c;
+                prev = __hip_atomic_fetch_xor(w, ((uint64_t)run_bits << 32) | V, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+            }
+            PendingU q;
+            q.prev = prev;
+            q.stored = stored;
+            q.c = U.c;
+            q.bits = run_bits;
+            q.V = V;
+            q.valid = 1;
+            retire_uniform(p, q, full, t, true);
+        } else {  // > 32 units per chunk: xor, then count arrivals
+            uint32_t raw = 0, last = 0;
+            const uint32_t n_run = __builtin_popcount(run_bits);
+            if (t == 0) {
+                uint32_t* accw = p.ws + 4ull * U.c;
+                const uint32_t prev = __hip_atomic_fetch_xor(accw, V, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                asm volatile("s_waitcnt vmcnt(0)" ::"v"(prev) : "memory");
+                const uint32_t tk = __hip_atomic_fetch_add(accw + 2, n_run, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT);
+                if (tk + n_run == p.nseg) {
+                    raw = __hip_atomic_exchange(accw, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(accw + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    last = 1;
+                }
+            }
+            if (__builtin_amdgcn_readfirstlane(last))
+                finalize_uniform(p, U.c, stored, __builtin_amdgcn_readfirstlane(raw), t, true);
+        }
+    }
+}
+
+__device__ __forceinline__ void unit_status_pair(const DecodeParams& p, const Unit& U, bool crc, int t) {
+    // statuses not produced by the CRC finalize: non-CRC chains (OK), missing / failed units
+    if (U.sidx != 0 || t != 0) return;
+    if (U.mode == ZHIP_ST_OK) {
+        if (!crc) {
+            zhip_status st = {ZHIP_ST_OK, 0u, 0u, 0u};
+            p.status[U.c] = st;
+        }
+    } else {
+        zhip_status st = {U.mode, 0u, 0u, 0u};
+        p.status[U.c] = st;
+        if (U.mode != ZHIP_ST_MISSING) atomicOr(p.errflag, 1u << U.mode);
+    }
+}
+
+template <bool CRC, int ITEM, bool SWAP, int NU, int K = 8>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(NU == 1 ? 8 : 4))) void k_decode_pair(const DecodeParams p) {
+    // NU == 1: the lane shift is a VALU multiply (no 16 KiB s_mul), so that
+    // eight workgroups fit a CU's LDS
+    constexpr bool kLdsMul = CRC && NU == 2;
+    __shared__ uint32_t s_tab[CRC ? 16 * 256 : 1];
+    __shared__ uint32_t s_mul[kLdsMul ? 16 * kThreads : 1];
+    __shared__ uint32_t s_r4[16];
+    __shared__ uint32_t s_red[2][kThreads / 64];
+    const int t = threadIdx.x;
+    const uint32_t G = gridDim.x, g = blockIdx.x;
+    const uint32_t q0 = (uint32_t)NU * g;
+    const bool has_a = q0 < p.n_units, has_b = NU == 2 && q0 + 1u < p.n_units;
+    if (!has_a && g >= p.n_idx) return;
+    const uint32_t expected = p.g.nbytes + (CRC ? 4u : 0u);
+    auto unit_of = [&](uint32_t q) {
+        const uint32_t c = q / p.nseg;
+        return c * p.nseg + (p.nseg - 1u - (q - c * p.nseg));
+    };
+    const uint8_t* zero = reinterpret_cast<const uint8_t*>(g_rows_zero);
+    stamp(p, g, t, 0);
+    // 1. vector loads, in this order and count on every path: [CRC: the Horner
+    //    tables (4), lane-shift constants (3), first shard-index block], unit A
+    //    (K), unit B (K), [CRC: the two CRC trailers].  Waiting for any of them
+    //    leaves the later ones in flight; unit headers are scalar loads.
+    uint4 A[K], B[NU == 2 ? K : 1];
+    Unit ua = resolve_unit(p, has_a ? unit_of(q0) : 0u, expected);
+    Unit ub = ua;
+    if constexpr (NU == 2)
+        if (has_b) ub = advance_unit(p, ua, unit_of(q0 + 1u), expected);
+    uint4 tv0, tv1, tv2, tv3;  // scalars, not an array: an array here lands in scratch
+    uint32_t kth = 0, ka = 0, kb = 0;
+    uint4 ipre = make_uint4(0, 0, 0, 0);
+    if constexpr (CRC) {
+        const uint4* gt = reinterpret_cast<const uint4*>(p.horner);
+        tv0 = gt[t];
+        tv1 = gt[t + kThreads];
+        tv2 = gt[t + 2 * kThreads];
+        tv3 = gt[t + 3 * kThreads];
+        kth = load_u32_any(reinterpret_cast<const uint8_t*>(p.kthread + t));
+        ka = load_u32_any(reinterpret_cast<const uint8_t*>(p.kpair + (size_t)ua.sidx * kThreads + t));
+        kb = load_u32_any(reinterpret_cast<const uint8_t*>(p.kpair + (size_t)ub.sidx * kThreads + t));
+        ipre = index_prefetch(p, g, g < p.n_idx, t, zero);
+    }
+    load_unit_rows(ua, has_a, t, A);
+    if constexpr (NU == 2) load_unit_rows(ub, has_b, t, B);
+    uint32_t stored_a = 0, stored_b = 0;
+    if constexpr (CRC) {
+        const bool ta = has_a && ua.mode == ZHIP_ST_OK;
+        const bool tb = has_b && ub.c != ua.c && ub.mode == ZHIP_ST_OK;
+        stored_a = load_u32_any(ta ? ua.cp + p.g.nbytes : zero);  // same address in every lane
+        stored_b = load_u32_any(tb ? ub.cp + p.g.nbytes : zero);
+    }
+    stamp(p, g, t, 1);
+    // 2. tables into LDS (waits for the table loads only), lane-multiply table
+    if constexpr (CRC) {
+        uint4* st = reinterpret_cast<uint4*>(s_tab);
+        st[t] = tv0;
+        st[t + kThreads] = tv1;
+        st[t + 2 * kThreads] = tv2;
+        st[t + 3 * kThreads] = tv3;
+        if (t < 16) s_r4[t] = mulx1(mulx1(mulx1(mulx1((uint32_t)t))));
+        if constexpr (kLdsMul) lanemul_init(s_mul, t, kb);  // own column
+        __syncthreads();
+    }
+    stamp(p, g, t, 2);
+    if (has_a) {
+        if (p.tune & kTuneSerialize) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // ablation
+        // 3. stores: A as soon as it arrives (B still in flight), then B
+        uint8_t* sink = reinterpret_cast<uint8_t*>(g_rows_sink);
+        const uint32_t lane_row = (16u * (uint32_t)t) >> p.row_shift;
+        const uint32_t lane_col = (16u * (uint32_t)t) & ((1u << p.row_shift) - 1u);
+        const int64_t lane_off = (int64_t)lane_row * p.r_oy + (int64_t)lane_col;
+        const bool same = has_b && ub.c == ua.c;
+        const bool ilv = CRC && !(p.tune & kTuneTrailingCrc);
+        uint32_t acc_a = 0, acc_b = 0;
+        store_unit_rows<ITEM, SWAP, K>(p, ua, true, t, lane_row, lane_off, sink, A,
+                                       ilv && ua.mode == ZHIP_ST_OK, s_tab, &acc_a);
+        stamp(p, g, t, 3);
+        if constexpr (NU == 2) {
+            acc_b = same ? acc_a : 0u;
+            store_unit_rows<ITEM, SWAP, K>(p, ub, has_b, t, lane_row, lane_off, sink, B,
+                                           ilv && has_b && ub.mode == ZHIP_ST_OK, s_tab, &acc_b);
+        }
+        stamp(p, g, t, 4);
+        // 4. CRC of the units; a run ends at a chunk change or at the last unit
+        if constexpr (CRC) {
+            const uint32_t sa = __builtin_amdgcn_readfirstlane(stored_a);
+            const uint32_t sb = same ? sa : __builtin_amdgcn_readfirstlane(stored_b);
+            if (ua.mode == ZHIP_ST_OK) {
+                if (!ilv) acc_a = crc_unit_rows(s_tab, 0u, A, p.tune);
+                if (!same) run_end_pair<false>(p, ua, acc_a, 1u << (ua.sidx & 31u), sa, ka, s_mul, s_r4, s_red[0], t, g);
+            }
+            if constexpr (NU == 2) {
+                if (has_b && ub.mode == ZHIP_ST_OK) {
+                    if (!ilv) acc_b = crc_unit_rows(s_tab, same ? acc_a : 0u, B, p.tune);
+                    const uint32_t bits = (same ? 1u << (ua.sidx & 31u) : 0u) | (1u << (ub.sidx & 31u));
+                    run_end_pair<kLdsMul>(p, ub, acc_b, bits, sb, kb, s_mul, s_r4, s_red[1], t, g);
+                }
+            }
+        }
+        unit_status_pair(p, ua, CRC, t);
+        if (has_b) unit_status_pair(p, ub, CRC, t);
+    }
+    // 5. fused shard-index checks (the lowest workgroups: dispatched first); the
+    //    first block of this workgroup's index was prefetched with the units
+    if constexpr (CRC)
+        for (uint32_t j = g; j < p.n_idx; j += G) verify_index(p, j, t, kth, s_tab, s_red[1], j == g, ipre);
+    stamp(p, g, t, 7);
+}
+
+int debug_stamps(uint64_t* host_out, uint32_t n_wg) {
+    if (n_wg > kStampWG) n_wg = kStampWG;
+    return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_stamps), (size_t)n_wg * kStampSlots * sizeof(uint64_t), 0,
+                               hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+
 using KernelFn = void (*)(const DecodeParams);
+
+template <int NU>
+KernelFn select_pair_nu(bool crc, int item, bool swap) {
+    switch (item) {
+        case 1: return crc ? k_decode_pair<true, 1, false, NU> : k_decode_pair<false, 1, false, NU>;
+        case 2: return crc ? (swap ? k_decode_pair<true, 2, true, NU> : k_decode_pair<true, 2, false, NU>)
+                           : (swap ? k_decode_pair<false, 2, true, NU> : k_decode_pair<false, 2, false, NU>);
+        case 4: return crc ? (swap ? k_decode_pair<true, 4, true, NU> : k_decode_pair<true, 4, false, NU>)
+                           : (swap ? k_decode_pair<false, 4, true, NU> : k_decode_pair<false, 4, false, NU>);
+        case 8: return crc ? (swap ? k_decode_pair<true, 8, true, NU> : k_decode_pair<true, 8, false, NU>)
+                           : (swap ? k_decode_pair<false, 8, true, NU> : k_decode_pair<false, 8, false, NU>);
+        default: return nullptr;
+    }
+}
+
+KernelFn select_pair_kernel(bool crc, int item, bool swap, int nu) {
+    return nu == 1 ? select_pair_nu<1>(crc, item, swap) : select_pair_nu<2>(crc, item, swap);
+}
 
 KernelFn select_rows_kernel(bool crc, int item, bool swap, int k) {
     if (k == 4) {  // 16 KiB units (tuning arm)

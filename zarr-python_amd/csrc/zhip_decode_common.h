@@ -23,11 +23,83 @@ struct Unit {
     int64_t out_off;
 };
 
+// Wave-uniform 16-byte read through the scalar data cache (read only): the
+// constant address space makes the compiler emit s_load_dwordx4, which is
+// tracked by lgkmcnt, so waiting for it never waits for the wave's in-flight
+// vector loads or stores.  `a` must be 4-byte aligned and uniform.
+typedef __attribute__((address_space(4))) const uint32_t zhip_const_u32;
+
+// A POD object of T read dword by dword through the scalar cache (T's size a
+// multiple of 4, `a` 4-byte aligned).
+template <typename T>
+__device__ __forceinline__ T load_uniform(const void* a) {
+    static_assert(sizeof(T) % 4 == 0, "dword-sized objects only");
+    const uint64_t v = reinterpret_cast<uintptr_t>(a);
+    const uint64_t u = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
+                       (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
+    const zhip_const_u32* w = (const zhip_const_u32*)u;
+    uint32_t d[sizeof(T) / 4];
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(T) / 4); ++i) d[i] = w[i];
+    T r;
+    __builtin_memcpy(&r, d, sizeof(T));
+    return r;
+}
+
+
+// A wave-uniform pointer into read-only tables, in the constant address space
+// (scalar loads for fields read with compile-time offsets).
+template <typename T>
+__device__ __forceinline__ const __attribute__((address_space(4))) T* uniform_ptr(const T* a) {
+    const uint64_t v = reinterpret_cast<uintptr_t>(a);
+    const uint64_t u = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
+                       (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
+    return (const __attribute__((address_space(4))) T*)u;
+}
+
+// The same address, provably wave-uniform (SGPR pair): lets the compiler use the
+// SGPR-base + VGPR-offset addressing form.
+template <typename T>
+__device__ __forceinline__ T* uniform_addr(T* a) {
+    const uint64_t v = reinterpret_cast<uintptr_t>(a);
+    return reinterpret_cast<T*>(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
+                                (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v));
+}
+
+// Thread t's lane-shift constant x^(8(4096 - 16t)) (the value build_tables
+// stores in kthread[t]) from 32 kernel-argument constants: with t = 16a + b it
+// is kq[a] * kq[16 + b], kq[a] = x^(8(4096 - 256a)), kq[16 + b] = x^(-128b).
+// Computed, not loaded: nothing waits for the unit loads in flight.
+__device__ __forceinline__ uint32_t lane_kthread(const DecodeParams& p, int t) {
+    const uint32_t a = (uint32_t)t >> 4, b = (uint32_t)t & 15u;
+    uint32_t qa = 0, pb = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < 16; ++i) {
+        qa = a == i ? p.kq[i] : qa;
+        pb = b == i ? p.kq[16 + i] : pb;
+    }
+    return gf_mul(qa, pb);
+}
+
+// (offset, nbytes) of one shard-index entry (LE u64 pair), any alignment: the
+// five aligned dwords covering it through the scalar cache, funnel-shifted.
+__device__ __forceinline__ void load_index_entry(const uint8_t* e, uint64_t& off, uint64_t& len) {
+    struct D5 { uint32_t d[5]; };
+    const uint64_t a = reinterpret_cast<uintptr_t>(e);
+    const uint32_t sh = (uint32_t)(a & 3u) * 8u;
+    const D5 w = load_uniform<D5>(reinterpret_cast<const void*>(a & ~3ull));
+    uint32_t x[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) x[i] = (uint32_t)((((uint64_t)w.d[i + 1] << 32) | w.d[i]) >> sh);
+    off = ((uint64_t)x[1] << 32) | x[0];
+    len = ((uint64_t)x[3] << 32) | x[2];
+}
+
 __device__ __forceinline__ Unit resolve_unit(const DecodeParams& p, uint32_t u, uint32_t expected) {
     Unit U;
     U.c = u / p.nseg;
     U.sidx = u - U.c * p.nseg;
-    const zhip_chunk ch = p.chunks[U.c];
+    const zhip_chunk ch = load_uniform<zhip_chunk>(p.chunks + U.c);
     U.mode = ZHIP_ST_OK;
     uint64_t base = ch.src;
     if (ch.flags & ZHIP_CF_MISSING) {
@@ -37,8 +109,8 @@ __device__ __forceinline__ Unit resolve_unit(const DecodeParams& p, uint32_t u, 
         // (2^64-1, 2^64-1) = missing; offsets are absolute within the blob.
         const uint64_t ipos = (p.lflags & ZHIP_LF_INDEX_START) ? 0ull : ch.src_len - p.index_size;
         const uint8_t* e = p.src + ch.src + ipos + 16ull * ch.slot;
-        const uint64_t off = load_u64_le_bytes(e);
-        const uint64_t len = load_u64_le_bytes(e + 8);
+        uint64_t off, len;
+        load_index_entry(e, off, len);
         if (off == ~0ull && len == ~0ull) U.mode = ZHIP_ST_MISSING;
         else if (off > ch.src_len || len > ch.src_len - off) U.mode = ZHIP_ST_INDEX_OOB;
         else if (len != expected) U.mode = ZHIP_ST_LENGTH_MISMATCH;
@@ -51,6 +123,46 @@ __device__ __forceinline__ Unit resolve_unit(const DecodeParams& p, uint32_t u, 
     U.sel = ch.sel;
     U.out_off = ch.out_off;
     return U;
+}
+
+// Unit u given the previous unit: a unit of the same chunk reuses its
+// resolution (no memory access); otherwise resolve from the tables.
+__device__ __forceinline__ Unit advance_unit(const DecodeParams& p, const Unit& prev, uint32_t u,
+                                             uint32_t expected) {
+    const uint32_t c = u / p.nseg;
+    if (c == prev.c) {
+        Unit U = prev;
+        U.sidx = u - c * p.nseg;
+        U.seg_lo = (int32_t)p.E - (int32_t)((U.sidx + 1u) * p.seg);
+        return U;
+    }
+    return resolve_unit(p, u, expected);
+}
+
+// The Horner operator tables [op][slice][256] (op k = A_(4096 - 4k), see
+// build_horner in capi.cpp) computed in LDS: entry b of (op, slice) is
+// gf_mul(x_op, b << 8*slice), linear in b, so thread t = b xors the basis
+// values x_op * x^(31-j) (j = 8*slice + bit) of its set bits.  The basis chain
+// is wave-uniform (scalar ALU); no memory reads, so nothing here waits for the
+// unit loads already in flight.
+__device__ __forceinline__ uint32_t mulx1_u(uint32_t b) { return (b >> 1) ^ (kPoly & (0u - (b & 1u))); }
+
+__device__ __forceinline__ void build_horner_lds(uint32_t* s_tab, int t, const uint32_t (&hx)[4]) {
+    uint32_t m[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) m[i] = 0u - (((uint32_t)t >> i) & 1u);
+#pragma unroll
+    for (int op = 0; op < 4; ++op) {
+        uint32_t v = hx[op];
+        uint32_t e[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int j = 31; j >= 0; --j) {
+            e[j >> 3] ^= v & m[j & 7];
+            v = mulx1_u(v);
+        }
+#pragma unroll
+        for (int sl = 0; sl < 4; ++sl) s_tab[op * 1024 + sl * 256 + t] = e[sl];
+    }
 }
 
 template <int K>
@@ -93,6 +205,15 @@ __device__ __forceinline__ void finalize_chunk(const DecodeParams& p, uint32_t c
     if (code != ZHIP_ST_OK) atomicOr(p.errflag, 1u << code);
 }
 
+// The LE u32 CRC trailer at cp + n through the scalar cache: the aligned dword
+// pair covering it (the arena keeps readable slack past every blob), shifted.
+__device__ __forceinline__ uint32_t load_trailer_uniform(const uint8_t* cp, uint32_t n) {
+    const uint64_t a = reinterpret_cast<uintptr_t>(cp + n);
+    const uint32_t sh = (uint32_t)(a & 3u) * 8u;
+    const uint2 w = load_uniform<uint2>(reinterpret_cast<const void*>(a & ~3ull));
+    return (uint32_t)((((uint64_t)w.y << 32) | w.x) >> sh);
+}
+
 __device__ __forceinline__ uint32_t load_trailer(const uint8_t* cp, uint32_t n) {
     const uint8_t* tr = cp + n;
     return (uint32_t)tr[0] | ((uint32_t)tr[1] << 8) | ((uint32_t)tr[2] << 16) | ((uint32_t)tr[3] << 24);
@@ -102,8 +223,28 @@ __device__ __forceinline__ uint32_t load_trailer(const uint8_t* cp, uint32_t n) 
 // workgroup: the same per-thread Horner chain as a data unit ending at idx_E
 // (reference point idx_E + 4096), reduced over the workgroup.  `red` is a
 // 4-word LDS scratch the caller does not use concurrently.
+// The first 16-byte block thread t reads for index j, loaded with exactly one
+// vector load whatever the lane or index state (`dummy` when out of range), so
+// it can be issued early without making the kernel's load counts path-dependent.
+// Consumed by verify_index(..., &pre).
+__device__ __forceinline__ uint4 index_prefetch(const DecodeParams& p, uint32_t j, bool has, int t,
+                                                const uint8_t* dummy) {
+    const uint8_t* a = dummy;
+    if (has) {
+        const zhip_chunk ch = load_uniform<zhip_chunk>(p.idx_chunks + j);
+        const uint32_t nk = (p.idx_E + kWgStride - 1) / kWgStride;
+        const int32_t o = (int32_t)p.idx_E - (int32_t)(nk * kWgStride) + 16 * t;
+        if (ch.src_len == (uint64_t)p.idx_nbytes + 4u && o >= 0 && (uint32_t)o < p.idx_nbytes)
+            a = p.src + ch.src + o;
+    }
+    uint4 v;
+    __builtin_memcpy(&v, a, 16);
+    return v;
+}
+
 __device__ __forceinline__ void verify_index(const DecodeParams& p, uint32_t j, int t, uint32_t kth,
-                                          const uint32_t* s_tab, uint32_t* red) {
+                                          const uint32_t* s_tab, uint32_t* red, bool has_pre = false,
+                                          uint4 pre = make_uint4(0, 0, 0, 0)) {
     const zhip_chunk ch = p.idx_chunks[j];
     const uint32_t ok = ch.src_len == (uint64_t)p.idx_nbytes + 4u;
     const uint8_t* cp = p.src + ch.src;
@@ -112,7 +253,11 @@ __device__ __forceinline__ void verify_index(const DecodeParams& p, uint32_t j, 
     uint32_t acc = 0;
     if (ok) {
         for (uint32_t k = 0; k < nk; ++k) {
-            const uint4 v = load_block<false>(cp, lo + kWgStride * (int32_t)k + 16 * t, p.idx_nbytes);
+            const int32_t o = lo + kWgStride * (int32_t)k + 16 * t;
+            uint4 v;
+            if (k == 0 && has_pre) v = (o >= 0 && (uint32_t)o < p.idx_nbytes) ? mask_tail(pre, o, p.idx_nbytes)
+                                                                         : make_uint4(0, 0, 0, 0);
+            else v = load_block<false>(cp, o, p.idx_nbytes);
             acc = tab_apply(s_tab, acc ^ v.x) ^ tab_apply(s_tab + 1024, v.y) ^
                   tab_apply(s_tab + 2048, v.z) ^ tab_apply(s_tab + 3072, v.w);
         }

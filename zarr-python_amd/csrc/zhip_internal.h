@@ -34,8 +34,11 @@ struct DecodeParams {
     uint32_t* ws;
     uint32_t* errflag;
     const uint32_t* horner;   // [4 operators][4 byte slices][256]
+    uint32_t hx[4];           // x^(8(4096 - 4k)): the operators, for in-kernel table builds
+    uint32_t kq[32];          // lane-shift factors (lane_kthread)
     const uint32_t* kthread;  // [kThreads]
     const uint32_t* kunit;    // [nseg]
+    const uint32_t* kpair;    // [nseg][kThreads]: kthread * kunit * c_inv (k_decode_pair)
     uint32_t n_chunks, nseg, n_units;
     uint32_t c_inv, c3;
     uint32_t lflags;
@@ -73,6 +76,14 @@ constexpr uint32_t kTuneAcqRel = 2u;    // acq_rel ticket (the round-1 first ver
 constexpr uint32_t kTuneNoTicket = 4u;  // xor only, no last-arriver finalize
 constexpr uint32_t kTuneNT = 8u;        // nontemporal loads / stores (fast rows path)
 constexpr uint32_t kTuneNoLaneMul = 16u; // rows kernel: skip the per-lane shift multiply
+constexpr uint32_t kTunePersist = 64u;   // whole-row layouts: persistent k_decode_rows instead of k_decode_pair
+constexpr uint32_t kTuneSingle = 128u;   // k_decode_pair with one unit per workgroup
+constexpr uint32_t kTuneSerialize = 256u; // k_decode_pair: wait for every load before the first store
+constexpr uint32_t kTuneNoTables = 512u;  // k_decode_pair: skip the in-LDS table build (results invalid)
+constexpr uint32_t kTuneTrailingCrc = 2048u; // k_decode_pair: CRC lookups after all stores (default: per block)
+constexpr uint32_t kTuneStamp = 1024u;    // k_decode_pair: per-workgroup phase timestamps (zhip_debug_stamps)
+constexpr uint32_t kStampWG = 8192u;      // workgroups stamped per launch
+constexpr uint32_t kStampSlots = 8u;
 extern int g_tune_max_grid;
 extern int g_tune_blocks;
 extern uint32_t g_tune_bits;
@@ -114,6 +125,7 @@ struct PackParams {
 int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid);
 int launch_encode(const EncodeParams& p, hipStream_t stream, int max_grid);
 int launch_shard_pack(const PackParams& p, uint32_t n_shards, hipStream_t stream);
+int debug_stamps(uint64_t* host_out, uint32_t n_wg);
 
 }  // namespace zhip
 
@@ -130,13 +142,15 @@ struct zhip_plan {
     uint32_t E;
     uint64_t R;
     uint32_t c_inv, c3;
+    uint32_t hx[4];    // x^(8(4096 - 4k)), k = 0..3: the Horner operators
+    uint32_t kq[32];   // x^(8(4096 - 256a)), a < 16 | x^(-128b), b < 16 (lane_kthread)
     zhip_fdiv dshape[ZHIP_MAX_DIMS];
     uint32_t row_bytes;
     zhip_fdiv drow;
     uint32_t fill[4];
     int device;
     int max_grid;
-    uint32_t* d_tables;  // horner (4096) | kthread (256) | kunit (nseg)
+    uint32_t* d_tables;  // horner (4096) | kthread (256) | kunit (nseg) | kpair (nseg * 256)
     // tile mode (layouts with a transposed dim that is contiguous in out)
     int32_t tq;          // -1: no tile mode
     uint32_t t_per_chunk, n_qb, n_cb;

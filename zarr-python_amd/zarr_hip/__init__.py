@@ -9,12 +9,12 @@ Drop-in for zarr-python's CodecPipeline (src/zarr/abc/codec.py:315-508): see
 
 from .array import Array, ArrayMetadata, ChunkNotFoundError
 from .codecs import BytesCodec, Crc32cCodec, ShardingCodec, TransposeCodec
-from .pipeline import DecodeProgram, HipCodecPipeline
+from .pipeline import DecodeProgram, HipCodecPipeline, ReadGraph
 from .spec import ArrayConfig, ArraySpec, GetResult
 from .store import DeviceStore, LocalStore, MemoryStore, StorePath
 
 __all__ = [
     "Array", "ArrayMetadata", "ArrayConfig", "ArraySpec", "BytesCodec", "ChunkNotFoundError",
     "Crc32cCodec", "DecodeProgram", "DeviceStore", "GetResult", "HipCodecPipeline", "LocalStore",
-    "MemoryStore", "ShardingCodec", "StorePath", "TransposeCodec",
+    "MemoryStore", "ReadGraph", "ShardingCodec", "StorePath", "TransposeCodec",
 ]

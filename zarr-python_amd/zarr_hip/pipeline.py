@@ -178,6 +178,41 @@ class DecodeProgram:
         return tuple(out)
 
 
+class ReadGraph:
+    """A read loop captured once as a hipGraph and replayed with one launch.
+
+    ``programs`` are planned reads (``prepare_read``); the graph holds
+    ``repeats`` launches cycling over them, in order, on one stream.  Replaying
+    it does exactly the work of the eager loop (every launch a full decode with
+    CRC verification and statuses), without one host-side launch per batch —
+    the HIP-graph counterpart of re-issuing the same read in a data-loader
+    loop.  Statuses accumulate in each program's device tables; call
+    ``results()`` to raise like the reference after a replay.
+    """
+
+    def __init__(self, programs: list, repeats: int, device=None):
+        torch = _torch()
+        if not programs or repeats < 1:
+            raise ValueError("ReadGraph needs at least one program and one repeat")
+        self.programs = list(programs)
+        self.repeats = int(repeats)
+        self.device = device if device is not None else self.programs[0].data.device
+        self.graph = torch.cuda.CUDAGraph()
+        self.stream = torch.cuda.Stream(self.device)
+        self.stream.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.device(self.device):
+            with torch.cuda.graph(self.graph, stream=self.stream):
+                for i in range(self.repeats):
+                    self.programs[i % len(self.programs)].launch()
+
+    def replay(self) -> None:
+        self.graph.replay()
+
+    def results(self) -> list:
+        _torch().cuda.synchronize(self.device)
+        return [p.results() for p in self.programs]
+
+
 def _device_resident(batch: list) -> bool:
     """True when every ByteGetter reads from a DeviceStore (bytes already in HBM)."""
     return all(isinstance(getattr(it[0], "store", None), DeviceStore)
