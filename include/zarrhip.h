@@ -190,6 +190,29 @@ int zhip_decode_indexed(const zhip_plan *plan, const void *src, uint64_t src_siz
                         const zhip_chunk *d_index_chunks, uint32_t n_index,
                         zhip_status *d_index_status, uint32_t decode_flags, void *stream);
 
+/* Load-address prediction for whole-row batches (ZHIP_DF_ROWS): the host
+ * asserts that the payload of chunk entry c starts at byte
+ *     base + (c / per) * outer + (c % per) * inner
+ * of src (e.g. inner chunks packed in Morton order inside equally spaced shard
+ * blobs, entries sorted by address), every predicted range lying inside its
+ * entry's blob.  The kernel issues the unit loads from the predicted address
+ * before the chunk record / shard-index entry arrive, then checks the
+ * prediction against the live index and reloads on a mismatch: results never
+ * depend on the prediction being right, only the start-up latency does. */
+typedef struct zhip_predict {
+    uint64_t base, outer, inner;
+    uint32_t per;    /* >= 1 */
+    uint32_t _pad;
+} zhip_predict;
+
+/* zhip_decode_indexed with an optional prediction (NULL = none). */
+int zhip_decode_predicted(const zhip_plan *plan, const void *src, uint64_t src_size, void *out,
+                          const zhip_chunk *d_chunks, uint32_t n_chunks, const zhip_sel *d_sels,
+                          zhip_status *d_status, uint32_t *d_workspace, uint32_t *d_errflag,
+                          const zhip_chunk *d_index_chunks, uint32_t n_index,
+                          zhip_status *d_index_status, uint32_t decode_flags,
+                          const zhip_predict *pred, void *stream);
+
 /* Process-wide tuning / ablation knobs for measurement (never needed for
  * correct operation): ZHIP_TUNE_MAX_GRID = persistent-grid cap (0 = auto),
  * ZHIP_TUNE_ABLATION = ablation bits (0 = production). */

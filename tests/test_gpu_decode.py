@@ -404,6 +404,9 @@ def test_rows_kernel_misaligned_inner_chunks(device, loc):
     arr = zarr_hip.Array.create(store, meta.shape, meta.chunk_shape, "float32", 0.0, codecs=codecs)
     prog, out = arr.prepare_read((Ellipsis,))
     assert prog.tables.rows
+    # the default-packing prediction is wrong for every inner chunk here: the
+    # kernel must notice and reload from the live index
+    assert prog.tables.predict is not None
     got = arr[...]
     assert got.tobytes() == want.tobytes()
     # a flipped payload bit in a misaligned chunk is still caught
@@ -420,3 +423,23 @@ def test_rows_kernel_misaligned_inner_chunks(device, loc):
     with pytest.raises(ValueError) as g:
         arr[...]
     assert str(g.value) == str(w.value)
+
+
+@pytest.mark.parametrize("loc", ["end", "start"])
+def test_predicted_loads_engaged_and_exact(device, loc):
+    """Default Morton packing: the load-address prediction fits (one 2-level
+    progression) and the decode is bit-exact; a missing inner chunk turns the
+    prediction off for its batch."""
+    arr, host, meta = _roundtrip(device, (128, 128, 64), (64, 64, 64), "float32",
+                                 [SHARD((32, 32, 64), [LE, CRC], loc)])
+    prog, out = arr.prepare_read((Ellipsis,))
+    assert prog.tables.rows and prog.tables.predict is not None
+    assert prog.tables.predict.per == 4
+    prog.launch()
+    prog.results()
+    from zarr_hip.buffer import to_numpy
+
+    assert to_numpy(out, "float32").tobytes() == O.read(host, meta).tobytes()
+    sel = (slice(3, 120), slice(None), slice(None))
+    got = arr[sel]
+    assert got.tobytes() == np.ascontiguousarray(O.read(host, meta, sel)).tobytes()

@@ -323,6 +323,15 @@ int zhip_decode_indexed(const zhip_plan* plan, const void* src, uint64_t src_siz
                         zhip_status* d_status, uint32_t* d_workspace, uint32_t* d_errflag,
                         const zhip_chunk* d_index_chunks, uint32_t n_index, zhip_status* d_index_status,
                         uint32_t decode_flags, void* stream) {
+    return zhip_decode_predicted(plan, src, src_size, out, d_chunks, n_chunks, d_sels, d_status, d_workspace,
+                                 d_errflag, d_index_chunks, n_index, d_index_status, decode_flags, nullptr, stream);
+}
+
+int zhip_decode_predicted(const zhip_plan* plan, const void* src, uint64_t src_size, void* out,
+                          const zhip_chunk* d_chunks, uint32_t n_chunks, const zhip_sel* d_sels,
+                          zhip_status* d_status, uint32_t* d_workspace, uint32_t* d_errflag,
+                          const zhip_chunk* d_index_chunks, uint32_t n_index, zhip_status* d_index_status,
+                          uint32_t decode_flags, const zhip_predict* pred, void* stream) {
     if (!plan) return set_err(ZHIP_E_INVALID, "null plan");
     if (!plan->d_tables) return set_err(ZHIP_E_INVALID, "plan not uploaded (zhip_plan_upload)");
     if (n_chunks == 0 && n_index == 0) return ZHIP_OK;
@@ -376,6 +385,7 @@ int zhip_decode_indexed(const zhip_plan* plan, const void* src, uint64_t src_siz
     p.tune = g_tune_bits;
     p.tq = -1;
     p.rows = 0;
+    p.pred = 0;
     if (decode_flags & ZHIP_DF_ROWS) {
         const uint32_t rb = plan->row_bytes;
         const int nd = L.ndim;
@@ -384,6 +394,24 @@ int zhip_decode_indexed(const zhip_plan* plan, const void* src, uint64_t src_siz
             (L.flags & ZHIP_LF_NO_WRITE) || (uint32_t)L.shape[nd - 2] % ((uint32_t)kWgStride / rb) != 0)
             return set_err(ZHIP_E_INVALID, "ZHIP_DF_ROWS preconditions do not hold for this layout");
         p.rows = 1;
+        if (pred) {
+            if (pred->per == 0) return set_err(ZHIP_E_INVALID, "zhip_predict.per must be >= 1");
+            // every predicted unit range must lie inside src (the kernel reads it before checking)
+            const uint64_t last = n_chunks ? (uint64_t)(n_chunks - 1) : 0;
+            const uint64_t gl = last / pred->per;
+            uint64_t top = gl * pred->outer + (last % pred->per) * pred->inner;
+            if (gl >= 1) {
+                const uint64_t full = (gl - 1) * pred->outer + (uint64_t)(pred->per - 1) * pred->inner;
+                if (full > top) top = full;
+            }
+            const uint64_t hi = pred->base + top + plan->E;
+            if (n_chunks && hi > src_size) return set_err(ZHIP_E_INVALID, "zhip_predict range outside src");
+            p.pred = 1;
+            p.pred_base = pred->base;
+            p.pred_outer = pred->outer;
+            p.pred_inner = pred->inner;
+            p.pred_per = pred->per;
+        }
         p.row_shift = (uint32_t)__builtin_ctz(rb);
         p.r_sy = (uint32_t)L.shape[nd - 2];
         p.r_dy = make_fdiv(p.r_sy);

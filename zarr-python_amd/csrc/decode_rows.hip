@@ -81,6 +81,22 @@ __device__ __forceinline__ void load_unit_rows(const Unit& U, bool live, int t, 
     }
 }
 
+// The unit a prediction (zhip_predict) says unit u is: present, at the
+// predicted payload address.  Only its cp / seg_lo are used (for the loads).
+__device__ __forceinline__ Unit predict_unit(const DecodeParams& p, uint32_t u) {
+    Unit U;
+    U.c = u / p.nseg;
+    U.sidx = u - U.c * p.nseg;
+    U.mode = ZHIP_ST_OK;
+    const uint32_t grp = U.c / p.pred_per;
+    const uint64_t off = p.pred_base + (uint64_t)grp * p.pred_outer + (uint64_t)(U.c - grp * p.pred_per) * p.pred_inner;
+    U.cp = p.src + off;
+    U.seg_lo = (int32_t)p.E - (int32_t)((U.sidx + 1u) * p.seg);
+    U.sel = 0;
+    U.out_off = 0;
+    return U;
+}
+
 // Stores that fall outside the selection go to this sink instead of being
 // skipped, so every unit issues exactly K stores (see load_unit_rows).
 __device__ uint4 g_rows_sink[kThreads];
@@ -396,7 +412,8 @@ __device__ __forceinline__ void store_unit_rows(const DecodeParams& p, const Uni
         }
         const bool wr = uok && (uint32_t)((int32_t)(y0 + lane_row) - sy0) < cy;
         store_nt16(wr ? p.out + dst + lane_off : sink, present ? swap_block<ITEM, SWAP>(blk[k]) : f);
-        if (crc) *acc = crc_block(s_tab, *acc, blk[k]);
+        if (crc) *acc = (p.tune & kTuneSkipCrc) ? *acc ^ blk[k].x ^ blk[k].y ^ blk[k].z ^ blk[k].w
+                                                : crc_block(s_tab, *acc, blk[k]);
     }
 }
 
@@ -513,17 +530,15 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(NU == 
     const uint8_t* zero = reinterpret_cast<const uint8_t*>(g_rows_zero);
     stamp(p, g, t, 0);
     // 1. vector loads, in this order and count on every path: [CRC: the Horner
-    //    tables (4), lane-shift constants (3), first shard-index block], unit A
-    //    (K), unit B (K), [CRC: the two CRC trailers].  Waiting for any of them
+    //    tables (4), lane-shift constants (3)], unit headers (scalar), [CRC: the
+    //    first shard-index block], unit A (K), unit B (K), [CRC: the two CRC
+    //    trailers].  Waiting for any of them
     //    leaves the later ones in flight; unit headers are scalar loads.
-    uint4 A[K], B[NU == 2 ? K : 1];
-    Unit ua = resolve_unit(p, has_a ? unit_of(q0) : 0u, expected);
-    Unit ub = ua;
-    if constexpr (NU == 2)
-        if (has_b) ub = advance_unit(p, ua, unit_of(q0 + 1u), expected);
+    // the tables and per-lane constants need no unit header: they go out first,
+    // their latency overlapping the header loads
+    const uint32_t u_a = has_a ? unit_of(q0) : 0u, u_b = has_b ? unit_of(q0 + 1u) : u_a;
     uint4 tv0, tv1, tv2, tv3;  // scalars, not an array: an array here lands in scratch
     uint32_t kth = 0, ka = 0, kb = 0;
-    uint4 ipre = make_uint4(0, 0, 0, 0);
     if constexpr (CRC) {
         const uint4* gt = reinterpret_cast<const uint4*>(p.horner);
         tv0 = gt[t];
@@ -531,12 +546,41 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(NU == 
         tv2 = gt[t + 2 * kThreads];
         tv3 = gt[t + 3 * kThreads];
         kth = load_u32_any(reinterpret_cast<const uint8_t*>(p.kthread + t));
-        ka = load_u32_any(reinterpret_cast<const uint8_t*>(p.kpair + (size_t)ua.sidx * kThreads + t));
-        kb = load_u32_any(reinterpret_cast<const uint8_t*>(p.kpair + (size_t)ub.sidx * kThreads + t));
-        ipre = index_prefetch(p, g, g < p.n_idx, t, zero);
+        ka = load_u32_any(reinterpret_cast<const uint8_t*>(p.kpair + (size_t)(u_a % p.nseg) * kThreads + t));
+        kb = load_u32_any(reinterpret_cast<const uint8_t*>(p.kpair + (size_t)(u_b % p.nseg) * kThreads + t));
     }
-    load_unit_rows(ua, has_a, t, A);
-    if constexpr (NU == 2) load_unit_rows(ub, has_b, t, B);
+    uint4 A[K], B[NU == 2 ? K : 1];
+    Unit ua, ub;
+    uint4 ipre = make_uint4(0, 0, 0, 0);
+    if (p.pred) {
+        // predicted addresses: the unit loads go out before the headers arrive
+        Unit ga = predict_unit(p, u_a), gb = predict_unit(p, u_b);
+        load_unit_rows(ga, has_a, t, A);
+        if constexpr (NU == 2) load_unit_rows(gb, has_b, t, B);
+        ua = resolve_unit(p, u_a, expected);
+        ub = ua;
+        if constexpr (NU == 2)
+            if (has_b) ub = advance_unit(p, ua, u_b, expected);
+        // a wrong prediction (non-default packing, elided inner chunks) reloads
+        // from the live index; the full drain keeps every later wait exact
+        const bool bad_a = has_a && ua.mode == ZHIP_ST_OK && ua.cp != ga.cp;
+        const bool bad_b = has_b && ub.mode == ZHIP_ST_OK && ub.cp != gb.cp;
+        if (bad_a || bad_b) {
+            if (bad_a) load_unit_rows(ua, true, t, A);
+            if constexpr (NU == 2)
+                if (bad_b) load_unit_rows(ub, true, t, B);
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+        }
+        if constexpr (CRC) ipre = index_prefetch(p, g, g < p.n_idx, t, zero);
+    } else {
+        ua = resolve_unit(p, u_a, expected);
+        ub = ua;
+        if constexpr (NU == 2)
+            if (has_b) ub = advance_unit(p, ua, u_b, expected);
+        if constexpr (CRC) ipre = index_prefetch(p, g, g < p.n_idx, t, zero);
+        load_unit_rows(ua, has_a, t, A);
+        if constexpr (NU == 2) load_unit_rows(ub, has_b, t, B);
+    }
     uint32_t stored_a = 0, stored_b = 0;
     if constexpr (CRC) {
         const bool ta = has_a && ua.mode == ZHIP_ST_OK;

@@ -95,6 +95,14 @@ __device__ __forceinline__ void load_index_entry(const uint8_t* e, uint64_t& off
     len = ((uint64_t)x[3] << 32) | x[2];
 }
 
+// a > b for wave-uniform u64 on the scalar ALU (it has no 64-bit ordered
+// compare; the opaque halves keep LLVM from re-forming a VALU i64 compare)
+__device__ __forceinline__ bool u64_gt(uint64_t a, uint64_t b) {
+    uint32_t ah = (uint32_t)(a >> 32), al = (uint32_t)a, bh = (uint32_t)(b >> 32), bl = (uint32_t)b;
+    asm volatile("" : "+s"(ah), "+s"(al), "+s"(bh), "+s"(bl));
+    return ah > bh || (ah == bh && al > bl);
+}
+
 __device__ __forceinline__ Unit resolve_unit(const DecodeParams& p, uint32_t u, uint32_t expected) {
     Unit U;
     U.c = u / p.nseg;
@@ -111,8 +119,10 @@ __device__ __forceinline__ Unit resolve_unit(const DecodeParams& p, uint32_t u, 
         const uint8_t* e = p.src + ch.src + ipos + 16ull * ch.slot;
         uint64_t off, len;
         load_index_entry(e, off, len);
+        // (64-bit compares spelled in 32-bit halves: scalar ALU, no VGPR temporaries
+        // that could alias registers with loads in flight)
         if (off == ~0ull && len == ~0ull) U.mode = ZHIP_ST_MISSING;
-        else if (off > ch.src_len || len > ch.src_len - off) U.mode = ZHIP_ST_INDEX_OOB;
+        else if (u64_gt(off, ch.src_len) || u64_gt(len, ch.src_len - off)) U.mode = ZHIP_ST_INDEX_OOB;
         else if (len != expected) U.mode = ZHIP_ST_LENGTH_MISMATCH;
         else base = ch.src + off;
     } else if (ch.src_len != expected) {

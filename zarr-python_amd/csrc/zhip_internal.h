@@ -65,6 +65,10 @@ struct DecodeParams {
     int64_t r_oy;              // out stride of dim ndim-2
     int32_t nd2;               // ndim - 2
     uint32_t rows;             // 1: launch k_decode_rows
+    // load-address prediction (zhip_predict; k_decode_pair): payload of chunk c
+    // predicted at src + pred_base + (c / pred_per) * pred_outer + (c % pred_per) * pred_inner
+    uint32_t pred, pred_per;
+    uint64_t pred_base, pred_outer, pred_inner;
 };
 
 constexpr int kTileRows = 64;    // rows of the contiguous-in-out dim per tile

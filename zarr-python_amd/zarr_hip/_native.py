@@ -101,6 +101,13 @@ def _np_dtypes():
     return chunk, sel, status
 
 
+class Predict(ctypes.Structure):
+    """zhip_predict (include/zarrhip.h)."""
+
+    _fields_ = [("base", ctypes.c_uint64), ("outer", ctypes.c_uint64), ("inner", ctypes.c_uint64),
+                ("per", ctypes.c_uint32), ("_pad", ctypes.c_uint32)]
+
+
 class NativeError(RuntimeError):
     pass
 
@@ -138,6 +145,12 @@ def lib():
                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                       ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
     L.zhip_decode_indexed.restype = ctypes.c_int
+    L.zhip_decode_predicted.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                        ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(Predict),
+                                        ctypes.c_void_p]
+    L.zhip_decode_predicted.restype = ctypes.c_int
     L.zhip_encode.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                               ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                               ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]

@@ -16,6 +16,7 @@ repeated reads of the same selection) can re-launch without re-planning.
 from __future__ import annotations
 
 import asyncio
+import os
 from dataclasses import dataclass, field
 from typing import Any, Iterable
 
@@ -24,7 +25,7 @@ import numpy as np
 from . import _native as N
 from . import staging
 from .codecs import ShardingCodec, evolve_codecs, parse_codecs, split_codecs
-from .planner import CHUNK_DT, SEL_DT, STATUS_DT, ChainInfo, Tables, analyze_chain, plan_decode
+from .planner import CHUNK_DT, SEL_DT, STATUS_DT, ChainInfo, Tables, analyze_chain, plan_decode, predict_rows
 from .spec import ArraySpec, GetResult
 from .store import DeviceRef, DeviceStore, _resolve_range
 
@@ -76,7 +77,7 @@ class DecodeLaunch:
 
     def __init__(self, layout: N.Layout, chunks: np.ndarray, sels: np.ndarray, src, src_size: int,
                  out, fast: bool, device, tile: bool = False, index_chunks: np.ndarray | None = None,
-                 rows: bool = False):
+                 rows: bool = False, predict: "N.Predict | None" = None):
         torch = _torch()
         self.plan = get_plan(layout)
         self.n = len(chunks)
@@ -96,12 +97,21 @@ class DecodeLaunch:
         self.out = out
         self.flags = (N.DF_FAST_ROWS if fast else 0) | (N.DF_TILE if tile else 0) | \
             (N.DF_ROWS if fast and rows else 0)
+        self.predict = predict if (fast and rows) else None
 
     def launch(self, stream: int | None = None) -> None:
         if self.n == 0:
             return
         s = _stream_handle(self.device) if stream is None else stream
         out_ptr = self.out.data_ptr() if self.out is not None else None
+        if self.predict is not None:
+            N.check(N.lib().zhip_decode_predicted(
+                self.plan.handle, self.src.data_ptr(), self.src_size, out_ptr, self.d_chunks.data_ptr(),
+                self.n, self.d_sels.data_ptr(), self.d_status.data_ptr(), self.d_ws.data_ptr(),
+                self.d_err.data_ptr(), self.d_idx_chunks.data_ptr() if self.n_idx else None, self.n_idx,
+                self.d_idx_status.data_ptr() if self.n_idx else None, self.flags, self.predict, s),
+                "zhip_decode_predicted")
+            return
         if self.n_idx:
             N.check(N.lib().zhip_decode_indexed(
                 self.plan.handle, self.src.data_ptr(), self.src_size, out_ptr, self.d_chunks.data_ptr(),
@@ -172,9 +182,11 @@ class DecodeProgram:
         if self.sharded:
             for i in range(self.n_items):
                 out.append(GetResult(status="missing" if self.item_missing[i] else "present"))
-        else:
+        else:  # one entry per item (entries may be reordered: item_of_chunk maps back)
+            by_item = np.full(self.n_items, N.ST_OK, np.uint32)
+            by_item[self.tables.item_of_chunk] = codes
             for i in range(self.n_items):
-                out.append(GetResult(status="missing" if codes[i] == N.ST_MISSING else "present"))
+                out.append(GetResult(status="missing" if by_item[i] == N.ST_MISSING else "present"))
         return tuple(out)
 
 
@@ -228,6 +240,9 @@ class HipCodecPipeline:
     array_bytes_codec: Any
     bytes_bytes_codecs: tuple
     batch_size: int = 1 << 30
+    # load-address prediction for whole-row batches (planner.predict_rows);
+    # ZARR_HIP_PREDICT=0 turns it off (measurements only)
+    predict_loads: bool = field(default_factory=lambda: os.environ.get("ZARR_HIP_PREDICT", "1") != "0")
 
     @classmethod
     def from_codecs(cls, codecs: Iterable, *, batch_size: int | None = None) -> "HipCodecPipeline":
@@ -238,7 +253,7 @@ class HipCodecPipeline:
     def evolve_from_array_spec(self, array_spec: ArraySpec) -> "HipCodecPipeline":
         ev = evolve_codecs(self.codecs, array_spec)
         aa, ab, bb = split_codecs(ev)
-        return type(self)(ev, aa, ab, bb, self.batch_size)
+        return type(self)(ev, aa, ab, bb, self.batch_size, self.predict_loads)
 
     def __iter__(self):
         return iter(self.codecs)
@@ -289,13 +304,15 @@ class HipCodecPipeline:
         ostr = [int(s) * itemsize for s in out.stride()]
         with torch.cuda.device(device):
             t = plan_decode(chain, spec, items, ostr, out.data_ptr(), drop_axes, resolved)
+            if self.predict_loads:
+                predict_rows(t, chain, spec, size)
             # fuse the shard-index CRC checks into the data launch
             # (zhip_decode_indexed: needs the CRC tables, i.e. an inner crc32c, and
             # the non-tiled kernel); else a second NO_WRITE launch
             fuse = (t.index_layout is not None and resolved is None and chain.inner.crc
                     and not t.tile)
             data = DecodeLaunch(t.layout, t.chunks, t.sels, src, size, out, t.fast, device, t.tile,
-                                t.index_chunks if fuse else None, t.rows)
+                                t.index_chunks if fuse else None, t.rows, t.predict)
             index = None
             if t.index_layout is not None and not fuse:
                 index = DecodeLaunch(t.index_layout, t.index_chunks, np.zeros(1, SEL_DT), src, size,

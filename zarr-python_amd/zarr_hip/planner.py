@@ -17,6 +17,7 @@ import numpy as np
 from . import _native as N
 from .codecs import BytesCodec, Crc32cCodec, ShardingCodec, TransposeCodec, split_codecs
 from .indexing import basic_projections
+from .indexing import morton_order
 from .spec import ArraySpec
 
 CHUNK_DT, SEL_DT, STATUS_DT = N._np_dtypes()
@@ -112,6 +113,7 @@ class Tables:
     index_layout: N.Layout | None = None
     index_chunks: np.ndarray | None = None
     index_item: np.ndarray | None = None
+    predict: "N.Predict | None" = None  # load-address prediction (rows batches, zhip_predict)
     extra: dict = field(default_factory=dict)
 
 
@@ -360,3 +362,57 @@ def plan_decode(chain: ChainInfo, spec: ArraySpec, items: list, out_strides_byte
         t.index_chunks = ic
         t.index_item = np.array([r[0] for r in idx_rows], np.int64)
     return t
+
+
+def predict_rows(t: Tables, chain: ChainInfo, spec: ArraySpec, src_size: int) -> None:
+    """Load-address prediction for a whole-row batch (zhip_decode_predicted).
+
+    Predicts each entry's payload address with the writers' default packing --
+    unsharded: the blob itself; sharded: inner chunks in Morton order
+    (ShardingCodec._subchunk_order_iter, sharding.py:1090-1107), each
+    `encoded size` bytes, after the index when it is at the start -- sorts the
+    entries by that address and, when the sorted addresses follow
+    base + (c // per) * outer + (c % per) * inner, records the prediction in
+    `t.predict`.  Every predicted range is checked to lie inside its entry's
+    blob and inside src, so a wrong guess (another writer's packing, elided
+    inner chunks) only costs the kernel a reload, never a wild read.  The
+    kernel always checks the guess against the live index."""
+    if not t.rows or len(t.chunks) == 0:
+        return
+    ch = t.chunks
+    if np.any(ch["flags"] & N.CF_MISSING):
+        return
+    L = t.layout
+    nbytes = int(L.nbytes)
+    E = (nbytes + 15) & ~15
+    if L.flags & N.LF_SHARDED:
+        sh = chain.shard
+        cps = tuple(int(c) for c in sh.chunks_per_shard(spec.shape))
+        morton = morton_order(cps)
+        cstr = np.array([int(np.prod(cps[d + 1:])) for d in range(len(cps))], np.int64)
+        rank_of_slot = np.zeros(int(np.prod(cps)), np.int64)
+        rank_of_slot[(morton * cstr[None, :]).sum(axis=1)] = np.arange(len(morton))
+        elen = nbytes + (4 if chain.inner.crc else 0)
+        start = int(L.index_size) if L.flags & N.LF_INDEX_START else 0
+        pred = ch["src"].astype(np.int64) + start + rank_of_slot[ch["slot"].astype(np.int64)] * elen
+        blob_end = ch["src"].astype(np.int64) + ch["src_len"].astype(np.int64)
+        if np.any(pred + E > blob_end):
+            return
+    else:
+        pred = ch["src"].astype(np.int64)
+    if np.any(pred < 0) or np.any(pred + E > src_size):
+        return
+    order = np.argsort(pred, kind="stable")
+    ps = pred[order]
+    n = len(ps)
+    inner = int(ps[1] - ps[0]) if n > 1 else 0
+    per = 1
+    while per < n and int(ps[per] - ps[per - 1]) == inner:
+        per += 1
+    outer = int(ps[per] - ps[0]) if per < n else 0
+    c = np.arange(n, dtype=np.int64)
+    if inner < 0 or outer < 0 or not np.array_equal(ps, ps[0] + (c // per) * outer + (c % per) * inner):
+        return
+    t.chunks = ch[order]
+    t.item_of_chunk = t.item_of_chunk[order]
+    t.predict = N.Predict(int(ps[0]), outer, inner, per, 0)
