@@ -82,6 +82,14 @@ def main():
                                        rows=True))
         fastpath.append(DecodeLaunch(t.layout, t.chunks, t.sels, prog.data.src, prog.data.src_size, out,
                                      True, dev, rows=False))
+    # write-locality probe: the same bytes in chunks of whole output planes
+    # (every unit writes contiguous 32 KiB instead of 256-byte rows at 1 KiB stride)
+    alt = {}
+    for name in [a for a in os.environ.get("ALT_CHUNKS", "").split(",") if a]:
+        ck = tuple(int(x) for x in name.split("x"))
+        alt[name] = [bench.build_c2_replica(dev, data, shape, ck).prepare_read((Ellipsis,))[0]
+                     for _ in range(R)]
+        arms.append(("alt_" + name, 0, 0))
     arms.append(("fastpath", 0, 8))
     for g in grids:
         arms.append(("nocrc_rows", g, 0))
@@ -105,6 +113,11 @@ def main():
                 N.lib().zhip_set_tuning(1, g)
                 N.lib().zhip_set_tuning(2, ab)
                 L = {"nocrc": nocrc, "nocrc_rows": nocrc_rows, "fastpath": fastpath}[kind]
+                ms = time_arm(lambda i: L[i % R].launch(sh))
+            elif kind.startswith("alt_"):
+                N.lib().zhip_set_tuning(1, 0)
+                N.lib().zhip_set_tuning(2, 0)
+                L = alt[kind[4:]]
                 ms = time_arm(lambda i: L[i % R].launch(sh))
             elif kind == "torch_copy":
                 ms = time_arm(lambda i: dsts[i % R].copy_(srcs[i % R]))

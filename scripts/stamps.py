@@ -64,8 +64,20 @@ def main():
         q = np.percentile(d, [10, 50, 90])
         print(json.dumps({"delta": f"{names[a]}->{names[b]}", "us_q10_50_90": [round(float(x), 2) for x in q]}))
     xcc = (hw >> 24) & 0xF
+    cu = (hw >> 8) & 0xF
+    sh = (hw >> 12) & 0x1
+    se = (hw >> 13) & 0x7
+    cu_key = ((xcc * 8 + se) * 2 + sh) * 16 + cu
+    per_cu = np.bincount(np.unique(cu_key, return_inverse=True)[1])
     print(json.dumps({"wg_per_xcc": np.bincount(xcc, minlength=8).tolist(),
+                      "distinct_cus": int(len(per_cu)),
+                      "wg_per_cu_histogram": {int(k): int(v) for k, v in zip(*np.unique(per_cu, return_counts=True))},
                       "kernel_span_us": round(float(rel[:, 7].max()), 2)}))
+    # end time vs number of workgroups sharing the CU
+    n_on_cu = per_cu[np.unique(cu_key, return_inverse=True)[1]]
+    for k in sorted(set(n_on_cu.tolist())):
+        print(json.dumps({"wgs_on_cu": int(k), "exit_us_median": round(float(np.median(rel[n_on_cu == k, 7])), 2),
+                          "exit_us_max": round(float(np.max(rel[n_on_cu == k, 7])), 2)}))
 
 
 if __name__ == "__main__":

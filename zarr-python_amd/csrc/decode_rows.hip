@@ -443,11 +443,14 @@ __device__ __forceinline__ uint32_t crc_unit_rows(const uint32_t* s_tab, uint32_
 // so no uniform multiply remains), xor-reduce over the workgroup, publish with
 // one 64-bit atomic (contribution | arrival bits); the arrival that completes
 // the chunk compares with the trailer.  `red` is a 4-word LDS scratch.
-template <bool LDS_MUL>
 __device__ __forceinline__ void run_end_pair(const DecodeParams& p, const Unit& U, uint32_t acc, uint32_t run_bits,
-                                             uint32_t stored, uint32_t klane, const uint32_t* s_mul,
+                                             uint32_t stored, uint32_t klane, bool lds_mul, const uint32_t* s_mul,
                                              const uint32_t* s_r4, uint32_t* red, int t, uint32_t g = 0) {
-    uint32_t v = LDS_MUL ? lanemul(s_mul, s_r4, t, acc) : gf_mul(acc, klane);
+    if (p.tune & kTuneNoRunEnd) {  // ablation: no reduction, no publication
+        if (acc == 0x9E3779B9u) red[0] = acc;
+        return;
+    }
+    uint32_t v = (p.tune & kTuneNoLaneMul) ? acc : lds_mul ? lanemul(s_mul, s_r4, t, acc) : gf_mul(acc, klane);
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v ^= __shfl_xor(v, off, 64);
     if ((t & 63) == 0) red[t >> 6] = v;
@@ -456,7 +459,9 @@ __device__ __forceinline__ void run_end_pair(const DecodeParams& p, const Unit& 
     if (t < 64) {  // wave 0, wave-uniform
         const uint32_t V = __builtin_amdgcn_readfirstlane(red[0] ^ red[1] ^ red[2] ^ red[3]);
         stamp(p, g, t, 6);
-        if (p.nseg <= 32) {
+        if (p.tune & kTuneNoTicket) {  // ablation: no publication / last-arriver
+            if (t == 0 && V == 0x9E3779B9u) p.status[U.c].aux = V;
+        } else if (p.nseg <= 32) {
             const uint64_t full = p.nseg >= 32 ? 0xFFFFFFFFull : ((1ull << p.nseg) - 1ull);
             uint64_t prev = 0;
             if (t == 0) {
@@ -540,11 +545,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(NU == 
     uint4 tv0, tv1, tv2, tv3;  // scalars, not an array: an array here lands in scratch
     uint32_t kth = 0, ka = 0, kb = 0;
     if constexpr (CRC) {
-        const uint4* gt = reinterpret_cast<const uint4*>(p.horner);
-        tv0 = gt[t];
-        tv1 = gt[t + kThreads];
-        tv2 = gt[t + 2 * kThreads];
-        tv3 = gt[t + 3 * kThreads];
+        // (ablation kTuneNoTables: read 64 zero bytes instead; results invalid)
+        const uint4* gt = reinterpret_cast<const uint4*>((p.tune & kTuneNoTables) ? reinterpret_cast<const uint8_t*>(g_rows_zero) : reinterpret_cast<const uint8_t*>(p.horner));
+        tv0 = gt[(p.tune & kTuneNoTables) ? 0 : t];
+        tv1 = gt[(p.tune & kTuneNoTables) ? 0 : t + kThreads];
+        tv2 = gt[(p.tune & kTuneNoTables) ? 0 : t + 2 * kThreads];
+        tv3 = gt[(p.tune & kTuneNoTables) ? 0 : t + 3 * kThreads];
         kth = load_u32_any(reinterpret_cast<const uint8_t*>(p.kthread + t));
         ka = load_u32_any(reinterpret_cast<const uint8_t*>(p.kpair + (size_t)(u_a % p.nseg) * kThreads + t));
         kb = load_u32_any(reinterpret_cast<const uint8_t*>(p.kpair + (size_t)(u_b % p.nseg) * kThreads + t));
@@ -598,7 +604,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(NU == 
         st[t + 3 * kThreads] = tv3;
         if (t < 16) s_r4[t] = mulx1(mulx1(mulx1(mulx1((uint32_t)t))));
         if constexpr (kLdsMul) lanemul_init(s_mul, t, kb);  // own column
-        __syncthreads();
+        if (!(p.tune & kTuneNoBarrier)) __syncthreads();
     }
     stamp(p, g, t, 2);
     if (has_a) {
@@ -609,7 +615,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(NU == 
         const uint32_t lane_col = (16u * (uint32_t)t) & ((1u << p.row_shift) - 1u);
         const int64_t lane_off = (int64_t)lane_row * p.r_oy + (int64_t)lane_col;
         const bool same = has_b && ub.c == ua.c;
-        const bool ilv = CRC && !(p.tune & kTuneTrailingCrc);
+        const bool ilv = CRC;
         uint32_t acc_a = 0, acc_b = 0;
         store_unit_rows<ITEM, SWAP, K>(p, ua, true, t, lane_row, lane_off, sink, A,
                                        ilv && ua.mode == ZHIP_ST_OK, s_tab, &acc_a);
@@ -620,20 +626,22 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(NU == 
                                            ilv && has_b && ub.mode == ZHIP_ST_OK, s_tab, &acc_b);
         }
         stamp(p, g, t, 4);
-        // 4. CRC of the units; a run ends at a chunk change or at the last unit
+        // 4. run ends (the CRC lookups ran with the stores): A alone when B
+        //    starts another chunk, then B (or A+B).  One call site: the kernel
+        //    body is straight-line code run once per workgroup, so its size
+        //    is instruction-cache footprint
         if constexpr (CRC) {
             const uint32_t sa = __builtin_amdgcn_readfirstlane(stored_a);
             const uint32_t sb = same ? sa : __builtin_amdgcn_readfirstlane(stored_b);
-            if (ua.mode == ZHIP_ST_OK) {
-                if (!ilv) acc_a = crc_unit_rows(s_tab, 0u, A, p.tune);
-                if (!same) run_end_pair<false>(p, ua, acc_a, 1u << (ua.sidx & 31u), sa, ka, s_mul, s_r4, s_red[0], t, g);
-            }
-            if constexpr (NU == 2) {
-                if (has_b && ub.mode == ZHIP_ST_OK) {
-                    if (!ilv) acc_b = crc_unit_rows(s_tab, same ? acc_a : 0u, B, p.tune);
-                    const uint32_t bits = (same ? 1u << (ua.sidx & 31u) : 0u) | (1u << (ub.sidx & 31u));
-                    run_end_pair<kLdsMul>(p, ub, acc_b, bits, sb, kb, s_mul, s_r4, s_red[1], t, g);
-                }
+#pragma unroll 1
+            for (int r = 0; r < NU; ++r) {
+                const bool second = r == 1;
+                const bool active = second ? (has_b && ub.mode == ZHIP_ST_OK) : (ua.mode == ZHIP_ST_OK && !same);
+                if (!active) continue;
+                const uint32_t bits = second ? ((same ? 1u << (ua.sidx & 31u) : 0u) | (1u << (ub.sidx & 31u)))
+                                             : 1u << (ua.sidx & 31u);
+                run_end_pair(p, second ? ub : ua, second ? acc_b : acc_a, bits, second ? sb : sa,
+                             second ? kb : ka, kLdsMul && second, s_mul, s_r4, s_red[r], t, g);
             }
         }
         unit_status_pair(p, ua, CRC, t);

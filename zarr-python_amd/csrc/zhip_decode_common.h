@@ -98,7 +98,8 @@ __device__ __forceinline__ void load_index_entry(const uint8_t* e, uint64_t& off
 // a > b for wave-uniform u64 on the scalar ALU (it has no 64-bit ordered
 // compare; the opaque halves keep LLVM from re-forming a VALU i64 compare)
 __device__ __forceinline__ bool u64_gt(uint64_t a, uint64_t b) {
-    uint32_t ah = (uint32_t)(a >> 32), al = (uint32_t)a, bh = (uint32_t)(b >> 32), bl = (uint32_t)b;
+    uint32_t ah = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)), al = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    uint32_t bh = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)), bl = __builtin_amdgcn_readfirstlane((uint32_t)b);
     asm volatile("" : "+s"(ah), "+s"(al), "+s"(bh), "+s"(bl));
     return ah > bh || (ah == bh && al > bl);
 }

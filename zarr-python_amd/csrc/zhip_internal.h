@@ -85,6 +85,8 @@ constexpr uint32_t kTuneSingle = 128u;   // k_decode_pair with one unit per work
 constexpr uint32_t kTuneSerialize = 256u; // k_decode_pair: wait for every load before the first store
 constexpr uint32_t kTuneNoTables = 512u;  // k_decode_pair: skip the in-LDS table build (results invalid)
 constexpr uint32_t kTuneTrailingCrc = 2048u; // k_decode_pair: CRC lookups after all stores (default: per block)
+constexpr uint32_t kTuneNoRunEnd = 4096u;  // k_decode_pair: skip the run-end reduction entirely (results invalid)
+constexpr uint32_t kTuneNoBarrier = 8192u; // k_decode_pair: skip the table barrier (results invalid)
 constexpr uint32_t kTuneStamp = 1024u;    // k_decode_pair: per-workgroup phase timestamps (zhip_debug_stamps)
 constexpr uint32_t kStampWG = 8192u;      // workgroups stamped per launch
 constexpr uint32_t kStampSlots = 8u;
