@@ -161,6 +161,9 @@ def extra_configs(device, args):
 
     out = {}
     steps = max(10, args.steps // 2)
+    if "c1" in args.extra:
+        out["c1_1d_bytes"] = c1_plumbing(device, args)
+        torch.cuda.empty_cache()
     shape, chunks = (256, 256, 256), (64, 64, 64)
     if "c2" in args.extra:
         # BASELINE configs[1]: the same array unsharded (64 chunks of 64^3)
@@ -210,6 +213,42 @@ def extra_configs(device, args):
         out["e2e_c2_host"] = e2e_host(device, args)
         torch.cuda.empty_cache()
     return out
+
+
+def c1_plumbing(device, args):
+    """BASELINE configs[0] (bench/compress_normal.py-style): 1e7 float32 1-D in
+    (2**20,) chunks, bytes codec only (10 chunks, the last a boundary chunk
+    stored at full size).  The reference runs it on the CPU pipeline; here:
+    the device-resident decode (generic k_decode, 1-D) and the MemoryStore
+    round trip (host bytes -> HBM -> host), both checked bit-exact."""
+    import torch
+
+    import zarr_hip
+
+    n, ck = 10 ** 7, 2 ** 20
+    rng = np.random.default_rng(0)
+    a = rng.standard_normal(n, dtype=np.float32)
+    host = zarr_hip.MemoryStore({})
+    harr = zarr_hip.Array.create(host, (n,), (ck,), "float32", 0.0, codecs=[LE])
+    harr.set((Ellipsis,), torch.from_numpy(a).to(device))
+    torch.cuda.synchronize(device)
+    if harr[...].tobytes() != a.tobytes():
+        raise SystemExit("bench c1: host round trip differs from the source")
+    dstore = zarr_hip.DeviceStore.from_host(host.to_dict(), device)
+    darr = zarr_hip.Array.open(dstore)
+    progs = [darr.prepare_read((Ellipsis,))[0] for _ in range(2)]
+    progs[0].launch()
+    progs[0].results()
+    wall, kern = time_programs(progs, max(10, args.steps // 2), 3, device)
+    dec = n * 4
+    t_rt = []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        harr[...]
+        t_rt.append(time.perf_counter() - t0)
+    return _entry(dec, dec + 10 * ck * 4, wall, kern,
+                  host_roundtrip_GiBps=round(dec / float(np.median(t_rt)) / GIB, 2),
+                  note="device decode via generic k_decode (1-D); host_roundtrip = MemoryStore -> HBM -> numpy")
 
 
 def c5_partial(device, args):
@@ -407,8 +446,8 @@ def main():
     ap.add_argument("--eager", action="store_true",
                     help="time one host launch per step instead of a hipGraph replay")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
-    ap.add_argument("--extra", default="c2,c3,c4,c5,e2e",
-                    help="extra configs measured at N=1 (subset of c2,c3,c4,c5,e2e, or '')")
+    ap.add_argument("--extra", default="c1,c2,c3,c4,c5,e2e",
+                    help="extra configs measured at N=1 (subset of c1,c2,c3,c4,c5,e2e, or '')")
     args = ap.parse_args()
 
     import torch

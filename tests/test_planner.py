@@ -83,3 +83,74 @@ def test_codec_order_errors():
         C.split_codecs(C.parse_codecs([{"name": "crc32c"}, {"name": "bytes"}]))
     with pytest.raises(NotImplementedError):
         C.parse_codecs([{"name": "gzip", "configuration": {"level": 1}}])
+
+
+def _sharded_headline_tables(loc="end", shape=(256, 256, 256), shards=(128, 128, 128),
+                             inner=(64, 64, 64)):
+    """Plan the headline-shaped full read exactly as prepare_read would, with the
+    shard blobs where a DeviceStore written in key order puts them (256-aligned,
+    consecutive) -- host logic only, no device."""
+    import zarr_hip.planner as P
+    from zarr_hip.codecs import parse_codecs
+
+    LE = {"name": "bytes", "configuration": {"endian": "little"}}
+    codecs = parse_codecs([{"name": "sharding_indexed", "configuration": {
+        "chunk_shape": list(inner), "codecs": [LE, {"name": "crc32c"}],
+        "index_codecs": [LE, {"name": "crc32c"}], "index_location": loc}}])
+    spec = ArraySpec(shards, "float32", 0.0)
+    chain = analyze_chain(codecs, spec)
+    n_inner = int(np.prod([s // c for s, c in zip(shards, inner)]))
+    elen = int(np.prod(inner)) * 4 + 4
+    blob = n_inner * elen + 16 * n_inner + 4
+    stride = (blob + 255) // 256 * 256
+    grid = [s // k for s, k in zip(shape, shards)]
+    items = []
+    for i, sc in enumerate(np.ndindex(*grid)):
+        csel = tuple(slice(0, k, 1) for k in shards)
+        osel = tuple(slice(c * k, (c + 1) * k, 1) for c, k in zip(sc, shards))
+        items.append((i * stride, blob, False, csel, osel))
+    ostr = [shape[1] * shape[2] * 4, shape[2] * 4, 4]
+    t = P.plan_decode(chain, spec, items, ostr, 0, ())
+    return P, t, chain, spec, stride, elen, len(items) * stride
+
+
+@pytest.mark.parametrize("loc", ["end", "start"])
+def test_predict_rows_fits_default_packing(loc):
+    """planner.predict_rows: entries sorted by predicted address follow one
+    2-level progression (shards x Morton-ranked inner chunks) and every
+    prediction lies inside its blob (zhip_predict contract)."""
+    P, t, chain, spec, stride, elen, size = _sharded_headline_tables(loc)
+    assert t.rows
+    items_before = sorted(t.item_of_chunk.tolist())
+    P.predict_rows(t, chain, spec, size)
+    pr = t.predict
+    assert pr is not None
+    assert (pr.per, pr.inner, pr.outer) == (8, elen, stride)
+    assert pr.base == (16 * 8 + 4 if loc == "start" else 0)
+    c = np.arange(len(t.chunks))
+    pred = pr.base + (c // pr.per) * pr.outer + (c % pr.per) * pr.inner
+    # the sorted entries' own blob + Morton rank give exactly the prediction
+    from zarr_hip.indexing import morton_order
+
+    m = morton_order((2, 2, 2))
+    rank_of_slot = np.zeros(8, np.int64)
+    rank_of_slot[(m * np.array([4, 2, 1])[None, :]).sum(axis=1)] = np.arange(8)
+    start = 16 * 8 + 4 if loc == "start" else 0
+    want = t.chunks["src"].astype(np.int64) + start + rank_of_slot[t.chunks["slot"].astype(np.int64)] * elen
+    assert np.array_equal(pred, want)
+    assert np.all(pred + elen <= t.chunks["src"].astype(np.int64) + t.chunks["src_len"].astype(np.int64))
+    assert sorted(t.item_of_chunk.tolist()) == items_before  # a permutation of the entries
+
+
+def test_predict_rows_declines_missing_and_irregular():
+    P, t, chain, spec, stride, elen, size = _sharded_headline_tables()
+    t.chunks["flags"][3] = 1  # a missing shard
+    P.predict_rows(t, chain, spec, size)
+    assert t.predict is None
+    P, t, chain, spec, stride, elen, size = _sharded_headline_tables()
+    t.chunks["src"][5:] += 256  # blobs no longer equally spaced
+    P.predict_rows(t, chain, spec, size + 256)
+    assert t.predict is None
+    P, t, chain, spec, stride, elen, size = _sharded_headline_tables()
+    P.predict_rows(t, chain, spec, size - 4096)  # a prediction past the end of src
+    assert t.predict is None
