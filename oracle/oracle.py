@@ -203,6 +203,9 @@ class Chain:
                     index=Chain.from_json(conf.get(
                         "index_codecs", [{"name": "bytes"}, {"name": "crc32c"}])),
                     index_location=conf.get("index_location", "end"),
+                    # not part of the stored metadata (sharding.py:462-464); accepted
+                    # here so tests can pick the physical layout a writer uses
+                    subchunk_write_order=conf.get("subchunk_write_order", "morton"),
                 )
             else:
                 raise NotImplementedError(name)

@@ -23,7 +23,7 @@ import numpy as np
 
 from . import _native as N
 from .buffer import torch_dtype
-from .indexing import morton_order
+from .indexing import subchunk_order
 from .planner import SEL_DT, ChainInfo, analyze_chain, plan_encode
 from .spec import ArraySpec
 from .store import DeviceStore, TAIL_SLACK
@@ -236,10 +236,12 @@ class ChunkWriter:
         index_size = sh.shard_index_size(n_inner)
         data_start = index_size if sh.index_location == "start" else 0
         blob_max = n_inner * elen + index_size
-        morton = morton_order(tuple(cps))                       # rank -> coords
+        # rank -> inner coords in the codec's subchunk_write_order (sharding.py:1090-1107;
+        # morton unless the caller chose otherwise -- it is not part of the metadata)
+        order = subchunk_order(tuple(cps), sh.subchunk_write_order)
         cstr = np.array([int(np.prod(cps[d + 1:])) for d in range(len(cps))], np.int64)
         rank_of_slot = np.zeros(n_inner, np.uint32)
-        rank_of_slot[(morton * cstr[None, :]).sum(axis=1)] = np.arange(n_inner, dtype=np.uint32)
+        rank_of_slot[(order * cstr[None, :]).sum(axis=1)] = np.arange(n_inner, dtype=np.uint32)
         setters = [it[0] for it in complete_items] + [it[0] for it in partial_items]
         store = None
         if setters and all(isinstance(getattr(s, "store", None), DeviceStore) for s in setters) and \
@@ -265,7 +267,7 @@ class ChunkWriter:
                 blob = offs[it[1]]
                 region = region_fn(j)
                 for r in range(n_inner):
-                    ic = morton[r]
+                    ic = order[r]
                     lo = [int(c) * s for c, s in zip(ic, inner_shape)]
                     csel = []
                     for d in range(len(ic)):
