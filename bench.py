@@ -551,7 +551,7 @@ def main():
         "roofline": {
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(),
-            "kernel": "zhip::k_decode_pair<CRC,4,noswap,2> (zhip_decode_indexed)",
+            "kernel": "zhip::k_decode_pair<CRC,4,noswap,2> (zhip_decode_mapped)",
             "kernel_ms_avg": round(avg_kern_s * 1e3, 5),
             "kernel_ms_eager_mean": round(float(np.mean(kern_s)) * 1e3, 5),
             "timing": "eager launches" if args.eager else

@@ -213,6 +213,37 @@ int zhip_decode_predicted(const zhip_plan *plan, const void *src, uint64_t src_s
                           zhip_status *d_index_status, uint32_t decode_flags,
                           const zhip_predict *pred, void *stream);
 
+/* Row map for ZHIP_DF_ROWS launches: where each 4096-byte step of every unit
+ * lands in `out`, precomputed on the host from the same selections the device
+ * table holds (the scatter of chunk_utils.py:88-214 for whole-row layouts,
+ * evaluated once per plan instead of per workgroup).  Entry
+ * [(s * nseg + u) * 8 + k] covers step k of unit u (u = 0 ends at the chunk's
+ * last byte) of selection s: lane rows [lo, hi) of the step are inside the
+ * selection and row 0 goes to out + chunk.out_off + rel. */
+typedef struct zhip_rowblk {
+    int32_t rel;
+    uint16_t lo, hi;
+} zhip_rowblk;
+
+/* Number of zhip_rowblk entries zhip_rows_map writes for n_sels selections. */
+uint64_t zhip_rows_map_len(const zhip_plan *plan, uint32_t n_sels);
+
+/* Fill h_map (host memory, map_len entries) from host copies of the
+ * selections.  ZHIP_E_UNSUPPORTED when the plan is not a whole-row layout or
+ * an offset does not fit 32 bits (launch without a map then). */
+int zhip_rows_map(const zhip_plan *plan, const zhip_sel *h_sels, uint32_t n_sels, zhip_rowblk *h_map,
+                  uint64_t map_len);
+
+/* zhip_decode_predicted with the row map uploaded to the device (d_rowmap,
+ * NULL = none): whole-row launches with a map run the two-unit decode
+ * (k_decode_pair), without one the persistent row decode. */
+int zhip_decode_mapped(const zhip_plan *plan, const void *src, uint64_t src_size, void *out,
+                       const zhip_chunk *d_chunks, uint32_t n_chunks, const zhip_sel *d_sels,
+                       zhip_status *d_status, uint32_t *d_workspace, uint32_t *d_errflag,
+                       const zhip_chunk *d_index_chunks, uint32_t n_index,
+                       zhip_status *d_index_status, uint32_t decode_flags,
+                       const zhip_predict *pred, const zhip_rowblk *d_rowmap, void *stream);
+
 /* Process-wide tuning / ablation knobs for measurement (never needed for
  * correct operation): ZHIP_TUNE_MAX_GRID = persistent-grid cap (0 = auto),
  * ZHIP_TUNE_ABLATION = ablation bits (0 = production). */

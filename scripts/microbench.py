@@ -70,7 +70,7 @@ def main():
     dsts = [torch.empty(data.nbytes, dtype=torch.uint8, device=dev) for _ in range(R)]
     # no-CRC twin of the same batch: same kernel structure, no tables / atomics
     from zarr_hip.pipeline import DecodeLaunch
-    nocrc, nocrc_rows, fastpath = [], [], []
+    nocrc, nocrc_rows, fastpath, nocrc_pred, crc_nopred = [], [], [], [], []
     for prog, out in progs:
         t = prog.tables
         L2 = type(t.layout).from_buffer_copy(bytes(t.layout))
@@ -82,6 +82,11 @@ def main():
                                        rows=True))
         fastpath.append(DecodeLaunch(t.layout, t.chunks, t.sels, prog.data.src, prog.data.src_size, out,
                                      True, dev, rows=False))
+        # prediction on / off for both twins (the decode arm uses the program's own setting)
+        nocrc_pred.append(DecodeLaunch(L2, ch, t.sels, prog.data.src, prog.data.src_size, out, True, dev,
+                                       rows=True, predict=t.predict))
+        crc_nopred.append(DecodeLaunch(t.layout, t.chunks, t.sels, prog.data.src, prog.data.src_size, out,
+                                       True, dev, rows=True))
     # write-locality probe: the same bytes in chunks of whole output planes
     # (every unit writes contiguous 32 KiB instead of 256-byte rows at 1 KiB stride)
     alt = {}
@@ -93,6 +98,9 @@ def main():
     arms.append(("fastpath", 0, 8))
     for g in grids:
         arms.append(("nocrc_rows", g, 0))
+    if progs[0][0].tables.predict is not None:
+        arms.append(("nocrc_pred", 0, 0))
+        arms.append(("crc_nopred", 0, 0))
     arms.append(("torch_copy", 0, 0))
     arms.append(("torch_read_sum", 0, 0))
     results = {a: [] for a in arms}
@@ -109,10 +117,11 @@ def main():
                 N.lib().zhip_set_tuning(2, 0)
                 kl = kvar[int(kind[7:])]
                 ms = time_arm(lambda i: kl[i % R].launch(sh))
-            elif kind in ("nocrc", "nocrc_rows", "fastpath"):
+            elif kind in ("nocrc", "nocrc_rows", "fastpath", "nocrc_pred", "crc_nopred"):
                 N.lib().zhip_set_tuning(1, g)
                 N.lib().zhip_set_tuning(2, ab)
-                L = {"nocrc": nocrc, "nocrc_rows": nocrc_rows, "fastpath": fastpath}[kind]
+                L = {"nocrc": nocrc, "nocrc_rows": nocrc_rows, "fastpath": fastpath, "nocrc_pred": nocrc_pred,
+                     "crc_nopred": crc_nopred}[kind]
                 ms = time_arm(lambda i: L[i % R].launch(sh))
             elif kind.startswith("alt_"):
                 N.lib().zhip_set_tuning(1, 0)

@@ -63,6 +63,11 @@ def main():
             continue
         q = np.percentile(d, [10, 50, 90])
         print(json.dumps({"delta": f"{names[a]}->{names[b]}", "us_q10_50_90": [round(float(x), 2) for x in q]}))
+    # the slowest 5 % of workgroups (the kernel's tail): their phase medians
+    tail = rel[:, 7] >= np.percentile(rel[:, 7], 95)
+    print(json.dumps({"tail_wgs": int(tail.sum()), "phase_medians_us": {
+        nm: round(float(np.median(rel[tail, i])), 2) for i, nm in enumerate(names)
+        if rel[:, i].min() > -1e3}}))
     xcc = (hw >> 24) & 0xF
     cu = (hw >> 8) & 0xF
     sh = (hw >> 12) & 0x1

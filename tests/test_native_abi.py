@@ -92,3 +92,86 @@ def test_plan_rejects_bad_layouts():
     L.nbytes = 99
     with pytest.raises(N.NativeError):
         N.Plan(L, upload=False)
+
+
+def _rows_case(shape, itemsize, sels, out_shape):
+    """Layout of a C-contiguous out array of `out_shape` (bytes strides) over
+    stored chunks of `shape`; sels = [(start, count)] per dim."""
+    from zarr_hip import _native as N
+    from zarr_hip.planner import SEL_DT, _make_layout
+
+    nd = len(shape)
+    ost = [int(np.prod(out_shape[d + 1:], dtype=np.int64)) * itemsize for d in range(nd)]
+    L = _make_layout(shape, itemsize, ost, 0, b"\0")
+    table = np.zeros(len(sels), SEL_DT)
+    for i, (st, ct) in enumerate(sels):
+        table[i]["start"][:nd] = st
+        table[i]["count"][:nd] = ct
+        table[i]["step"][:nd] = 1
+    return L, table, ost
+
+
+@pytest.mark.parametrize("case", [
+    # (chunk shape, itemsize, selections, out shape)
+    ((64, 64, 64), 4, [((0, 0, 0), (64, 64, 64))], (256, 256, 256)),
+    ((64, 64, 64), 4, [((3, 0, 0), (50, 64, 64)), ((0, 17, 0), (64, 9, 64)), ((63, 63, 0), (1, 1, 64))],
+     (128, 128, 64)),
+    ((16, 32, 128), 2, [((0, 5, 0), (16, 20, 128)), ((7, 0, 0), (2, 32, 128))], (40, 70, 128)),
+    ((3, 5, 256, 8), 2, [((1, 2, 5, 0), (2, 3, 240, 8)), ((0, 0, 0, 0), (3, 5, 256, 8))], (9, 11, 300, 8)),
+    ((768, 16), 1, [((0, 0), (768, 16)), ((5, 0), (700, 16))], (800, 16)),  # 12 KiB chunks: unit starts before
+    ((4096, 1024), 1, [((100, 0), (3000, 1024))], (5000, 1024)),             # 4 MiB chunks: 128 units
+])
+def test_rows_map_matches_scatter_semantics(case):
+    """zhip_rows_map: for every (selection, unit, step, lane) the destination
+    the row map gives equals the scatter out[out_sel] = chunk[chunk_sel]
+    (chunk_utils.py:88-214) of that lane's 16 bytes, and lanes outside the
+    selection or before the chunk start write nothing."""
+    from zarr_hip import _native as N
+
+    shape, it, sels, out_shape = case
+    L, table, ost = _rows_case(shape, it, sels, out_shape)
+    plan = N.Plan(L, upload=False)
+    nseg = plan.units_per_chunk
+    n = int(N.lib().zhip_rows_map_len(plan.handle, len(table)))
+    assert n == len(table) * nseg * 8
+    m = np.zeros(n, N.ROWBLK_DT)
+    assert N.lib().zhip_rows_map(plan.handle, table.ctypes.data, len(table), m.ctypes.data, n) == 0
+    m = m.reshape(len(table), nseg, 8)
+    nd = len(shape)
+    rb = shape[-1] * it
+    nbytes = int(np.prod(shape)) * it
+    E = -(-nbytes // 16) * 16
+    t = np.arange(256)
+    lane_row = (16 * t) // rb
+    lane_col = (16 * t) % rb
+    lead = shape[:-1]
+    for s, (st, ct) in enumerate(sels):
+        for u in range(nseg):
+            for k in range(8):
+                base_o = E - (u + 1) * 8 * 4096 + 4096 * k
+                e = m[s, u, k]
+                got_ok = (lane_row >= e["lo"]) & (lane_row < e["hi"])
+                got_dst = int(e["rel"]) + lane_row * ost[nd - 2] + lane_col
+                off = base_o + 16 * t
+                R = np.where(off >= 0, off, 0) // rb
+                coords = np.stack(np.unravel_index(np.minimum(R, int(np.prod(lead)) - 1), lead))
+                want_ok = off >= 0
+                dst = lane_col.copy()
+                for d in range(nd - 1):
+                    rel = coords[d] - st[d]
+                    want_ok &= (rel >= 0) & (rel < ct[d])
+                    dst = dst + rel * ost[d]
+                np.testing.assert_array_equal(got_ok, want_ok, err_msg=f"sel {s} unit {u} step {k}")
+                np.testing.assert_array_equal(got_dst[want_ok], dst[want_ok])
+
+
+def test_rows_map_declines_non_row_layouts():
+    from zarr_hip import _native as N
+
+    # 24-byte rows (not 2^k); 16-byte rows but 48 of them (a 4 KiB step would cross dim ndim-2)
+    for shape in [(64, 24), (48, 16)]:
+        L, table, _ = _rows_case(shape, 1, [((0, 0), shape)], shape)
+        plan = N.Plan(L, upload=False)
+        n = int(N.lib().zhip_rows_map_len(plan.handle, 1))
+        m = np.zeros(max(n, 1), N.ROWBLK_DT)
+        assert N.lib().zhip_rows_map(plan.handle, table.ctypes.data, 1, m.ctypes.data, n) == N.E_UNSUPPORTED

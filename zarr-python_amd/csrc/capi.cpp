@@ -3,6 +3,8 @@
 // algebra the kernels rely on.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <climits>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -332,6 +334,78 @@ int zhip_decode_predicted(const zhip_plan* plan, const void* src, uint64_t src_s
                           zhip_status* d_status, uint32_t* d_workspace, uint32_t* d_errflag,
                           const zhip_chunk* d_index_chunks, uint32_t n_index, zhip_status* d_index_status,
                           uint32_t decode_flags, const zhip_predict* pred, void* stream) {
+    return zhip_decode_mapped(plan, src, src_size, out, d_chunks, n_chunks, d_sels, d_status, d_workspace,
+                              d_errflag, d_index_chunks, n_index, d_index_status, decode_flags, pred, nullptr,
+                              stream);
+}
+
+uint64_t zhip_rows_map_len(const zhip_plan* plan, uint32_t n_sels) {
+    if (!plan) return 0;
+    return (uint64_t)n_sels * plan->nseg * (uint64_t)kDefaultBlocks;
+}
+
+// The destination arithmetic of the row decode (per step: row R of the
+// chunk's flattened leading dims, its place in dims 0..ndim-2 and in the
+// selection), evaluated once per (selection, unit, step) on the host.
+int zhip_rows_map(const zhip_plan* plan, const zhip_sel* h_sels, uint32_t n_sels, zhip_rowblk* h_map,
+                  uint64_t map_len) {
+    if (!plan) return set_err(ZHIP_E_INVALID, "null plan");
+    if (n_sels && (!h_sels || !h_map)) return set_err(ZHIP_E_INVALID, "null host pointer");
+    if (map_len < zhip_rows_map_len(plan, n_sels)) return set_err(ZHIP_E_INVALID, "row map too short");
+    const zhip_layout& L = plan->layout;
+    const uint32_t rb = plan->row_bytes;
+    const int nd = L.ndim;
+    if (nd < 2 || rb < 16 || rb > (uint32_t)kWgStride || (rb & (rb - 1)) != 0 ||
+        (uint32_t)L.shape[nd - 2] % ((uint32_t)kWgStride / rb) != 0 || plan->seg != (uint32_t)kWgStride * kDefaultBlocks)
+        return set_err(ZHIP_E_UNSUPPORTED, "not a whole-row layout with 32 KiB units");
+    const uint32_t shift = (uint32_t)__builtin_ctz(rb);
+    const int64_t rps = (int64_t)kWgStride >> shift;  // rows per step
+    const int64_t sy = L.shape[nd - 2];
+    const int64_t oy = L.out_stride[nd - 2];
+    const int nd2 = nd - 2;
+    for (uint32_t s = 0; s < n_sels; ++s) {
+        const zhip_sel& sel = h_sels[s];
+        const int64_t sy0 = sel.start[nd2], cy = sel.count[nd2];
+        for (uint32_t u = 0; u < plan->nseg; ++u) {
+            const int64_t seg_lo = (int64_t)(int32_t)plan->E - (int64_t)(u + 1) * plan->seg;
+            for (int k = 0; k < kDefaultBlocks; ++k) {
+                zhip_rowblk& e = h_map[((uint64_t)s * plan->nseg + u) * kDefaultBlocks + k];
+                e.rel = 0;
+                e.lo = e.hi = 0;
+                const int64_t base_o = seg_lo + (int64_t)kWgStride * k;
+                if (base_o < 0) continue;  // before the chunk start: nothing written
+                const int64_t R = base_o >> shift;
+                int64_t r = R / sy;
+                const int64_t y0 = R - r * sy;
+                int64_t dst = (y0 - sy0) * oy;
+                bool ok = true;
+                for (int d = nd2 - 1; d >= 0; --d) {
+                    const int64_t qd = d > 0 ? r / L.shape[d] : 0;
+                    const int64_t rel = r - qd * L.shape[d] - sel.start[d];
+                    r = qd;
+                    ok = ok && rel >= 0 && rel < sel.count[d];
+                    dst += rel * L.out_stride[d];
+                }
+                const int64_t lo = std::min(std::max(sy0 - y0, (int64_t)0), rps);
+                const int64_t hi = std::min(std::max(sy0 - y0 + cy, (int64_t)0), rps);
+                if (!ok || hi <= lo) continue;
+                if (dst < INT32_MIN || dst > INT32_MAX)
+                    return set_err(ZHIP_E_UNSUPPORTED, "row offset does not fit 32 bits");
+                e.rel = (int32_t)dst;
+                e.lo = (uint16_t)lo;
+                e.hi = (uint16_t)hi;
+            }
+        }
+    }
+    return ZHIP_OK;
+}
+
+int zhip_decode_mapped(const zhip_plan* plan, const void* src, uint64_t src_size, void* out,
+                       const zhip_chunk* d_chunks, uint32_t n_chunks, const zhip_sel* d_sels,
+                       zhip_status* d_status, uint32_t* d_workspace, uint32_t* d_errflag,
+                       const zhip_chunk* d_index_chunks, uint32_t n_index, zhip_status* d_index_status,
+                       uint32_t decode_flags, const zhip_predict* pred, const zhip_rowblk* d_rowmap,
+                       void* stream) {
     if (!plan) return set_err(ZHIP_E_INVALID, "null plan");
     if (!plan->d_tables) return set_err(ZHIP_E_INVALID, "plan not uploaded (zhip_plan_upload)");
     if (n_chunks == 0 && n_index == 0) return ZHIP_OK;
@@ -385,6 +459,7 @@ int zhip_decode_predicted(const zhip_plan* plan, const void* src, uint64_t src_s
     p.tune = g_tune_bits;
     p.tq = -1;
     p.rows = 0;
+    p.rowmap = nullptr;
     p.pred = 0;
     if (decode_flags & ZHIP_DF_ROWS) {
         const uint32_t rb = plan->row_bytes;
@@ -394,6 +469,7 @@ int zhip_decode_predicted(const zhip_plan* plan, const void* src, uint64_t src_s
             (L.flags & ZHIP_LF_NO_WRITE) || (uint32_t)L.shape[nd - 2] % ((uint32_t)kWgStride / rb) != 0)
             return set_err(ZHIP_E_INVALID, "ZHIP_DF_ROWS preconditions do not hold for this layout");
         p.rows = 1;
+        p.rowmap = d_rowmap;
         if (pred) {
             if (pred->per == 0) return set_err(ZHIP_E_INVALID, "zhip_predict.per must be >= 1");
             // every predicted unit range must lie inside src (the kernel reads it before checking)

@@ -495,10 +495,12 @@ KernelFn select_pair_kernel(bool crc, int item, bool swap, int nu);  // decode_r
 
 int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
     if (g_tune_max_grid > 0) max_grid = g_tune_max_grid;
-    if (p.rows && p.seg == (uint32_t)kWgStride * kDefaultBlocks && !(p.tune & kTunePersist)) {
+    if (p.rows && p.rowmap && p.seg == (uint32_t)kWgStride * kDefaultBlocks && !(p.tune & kTunePersist)) {
         // one workgroup per pair of units, non-persistent (k_decode_pair)
         const int nu = (p.tune & kTuneSingle) ? 1 : 2;
-        KernelFn fn = select_pair_kernel((p.lflags & ZHIP_LF_CRC) != 0, p.g.itemsize, (p.lflags & ZHIP_LF_SWAP) != 0, nu);
+        const bool crc = (p.lflags & ZHIP_LF_CRC) != 0, swap = (p.lflags & ZHIP_LF_SWAP) != 0;
+        KernelFn fn = (nu == 2 && (p.tune & kTuneTrailingCrc)) ? select_pair_kernel(crc, p.g.itemsize, swap, 3) : nullptr;
+        if (!fn) fn = select_pair_kernel(crc, p.g.itemsize, swap, nu);
         if (!fn) return ZHIP_E_UNSUPPORTED;
         const uint32_t pairs = (uint32_t)(((uint64_t)p.n_units + nu - 1u) / nu);
         const uint32_t grid = pairs > p.n_idx ? pairs : p.n_idx;

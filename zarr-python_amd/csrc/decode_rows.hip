@@ -380,38 +380,34 @@ __device__ __forceinline__ uint32_t crc_block(const uint32_t* s_tab, uint32_t ac
            tab_apply(s_tab + 3072, v.w);
 }
 
+// The K = 8 steps of one unit in the row map (zhip_rows_map): 64 bytes, one
+// scalar load per unit.
+struct RowSteps {
+    zhip_rowblk e[kDefaultBlocks];
+};
+
+__device__ __forceinline__ RowSteps load_row_steps(const DecodeParams& p, const Unit& U) {
+    return load_uniform<RowSteps>(p.rowmap + ((size_t)U.sel * p.nseg + U.sidx) * kDefaultBlocks);
+}
+
 // Stores of one unit; with `crc` the Horner step of each block follows its
 // store (the lookups spread over the data's arrival instead of trailing it).
+// Destinations come from the row map: no per-step address arithmetic.
 template <int ITEM, bool SWAP, int K>
-__device__ __forceinline__ void store_unit_rows(const DecodeParams& p, const Unit& U, bool live, int t,
+__device__ __forceinline__ void store_unit_rows(const DecodeParams& p, const Unit& U, const RowSteps& m, bool live,
                                                 uint32_t lane_row, int64_t lane_off, uint8_t* sink,
                                                 const uint4 (&blk)[K], bool crc = false,
                                                 const uint32_t* s_tab = nullptr, uint32_t* acc = nullptr) {
-    const auto& sel = *uniform_ptr(p.sels + U.sel);
+    static_assert(K == kDefaultBlocks, "the row map holds kDefaultBlocks steps per unit");
     const bool present = live && U.mode == ZHIP_ST_OK;
     const bool writes = live && (U.mode == ZHIP_ST_OK || U.mode == ZHIP_ST_MISSING);
-    const int32_t sy0 = sel.start[p.nd2];
-    const uint32_t cy = (uint32_t)sel.count[p.nd2];
+    uint8_t* const base = p.out + U.out_off;
     const uint4 f = make_uint4(p.fill[0], p.fill[1], p.fill[2], p.fill[3]);
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-        const int32_t base_o = U.seg_lo + kWgStride * k;
-        const uint32_t R = (uint32_t)base_o >> p.row_shift;
-        uint32_t r = fdiv_apply(R, p.r_dy.m, p.r_dy.s);
-        const uint32_t y0 = R - r * p.r_sy;
-        int64_t dst = U.out_off + (int64_t)((int32_t)y0 - sy0) * p.r_oy;
-        bool uok = writes && base_o >= 0;
-#pragma unroll
-        for (int d = ZHIP_MAX_DIMS - 3; d >= 0; --d) {
-            if (d >= p.nd2) continue;
-            const uint32_t qd = d > 0 ? fdiv_apply(r, p.g.dshape[d].m, p.g.dshape[d].s) : 0u;
-            const int32_t rel = (int32_t)(r - qd * (uint32_t)p.g.shape[d]) - sel.start[d];
-            r = qd;
-            uok = uok && rel >= 0 && rel < sel.count[d];
-            dst += (int64_t)rel * p.g.ostride[d];
-        }
-        const bool wr = uok && (uint32_t)((int32_t)(y0 + lane_row) - sy0) < cy;
-        store_nt16(wr ? p.out + dst + lane_off : sink, present ? swap_block<ITEM, SWAP>(blk[k]) : f);
+        const uint32_t lo = m.e[k].lo, hi = m.e[k].hi;
+        const bool wr = writes && lane_row - lo < hi - lo;  // unsigned: lo <= lane_row < hi
+        store_nt16(wr ? base + m.e[k].rel + lane_off : sink, present ? swap_block<ITEM, SWAP>(blk[k]) : f);
         if (crc) *acc = (p.tune & kTuneSkipCrc) ? *acc ^ blk[k].x ^ blk[k].y ^ blk[k].z ^ blk[k].w
                                                 : crc_block(s_tab, *acc, blk[k]);
     }
@@ -420,6 +416,7 @@ __device__ __forceinline__ void store_unit_rows(const DecodeParams& p, const Uni
 template <int K>
 __device__ __forceinline__ uint32_t crc_unit_rows(const uint32_t* s_tab, uint32_t acc, const uint4 (&blk)[K],
                                                   uint32_t tune) {
+    // (used by the TRAIL tuning variant of k_decode_pair)
     if (tune & kTuneSkipCrc) {  // ablation: lookups replaced by a plain xor
 #pragma unroll
         for (int k = 0; k < K; ++k) acc ^= blk[k].x ^ blk[k].y ^ blk[k].z ^ blk[k].w;
@@ -513,7 +510,7 @@ __device__ __forceinline__ void unit_status_pair(const DecodeParams& p, const Un
     }
 }
 
-template <bool CRC, int ITEM, bool SWAP, int NU, int K = 8>
+template <bool CRC, int ITEM, bool SWAP, int NU, int K = 8, bool TRAIL = false>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(NU == 1 ? 8 : 4))) void k_decode_pair(const DecodeParams p) {
     // NU == 1: the lane shift is a VALU multiply (no 16 KiB s_mul), so that
     // eight workgroups fit a CU's LDS
@@ -551,9 +548,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(NU == 
         tv1 = gt[(p.tune & kTuneNoTables) ? 0 : t + kThreads];
         tv2 = gt[(p.tune & kTuneNoTables) ? 0 : t + 2 * kThreads];
         tv3 = gt[(p.tune & kTuneNoTables) ? 0 : t + 3 * kThreads];
-        kth = load_u32_any(reinterpret_cast<const uint8_t*>(p.kthread + t));
-        ka = load_u32_any(reinterpret_cast<const uint8_t*>(p.kpair + (size_t)(u_a % p.nseg) * kThreads + t));
-        kb = load_u32_any(reinterpret_cast<const uint8_t*>(p.kpair + (size_t)(u_b % p.nseg) * kThreads + t));
+        if (!(p.tune & kTuneNoConsts)) {
+            kth = load_u32_any(reinterpret_cast<const uint8_t*>(p.kthread + t));
+            ka = load_u32_any(reinterpret_cast<const uint8_t*>(p.kpair + (size_t)(u_a % p.nseg) * kThreads + t));
+            kb = load_u32_any(reinterpret_cast<const uint8_t*>(p.kpair + (size_t)(u_b % p.nseg) * kThreads + t));
+        }
     }
     uint4 A[K], B[NU == 2 ? K : 1];
     Unit ua, ub;
@@ -587,12 +586,16 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(NU == 
         load_unit_rows(ua, has_a, t, A);
         if constexpr (NU == 2) load_unit_rows(ub, has_b, t, B);
     }
+    // destinations of both units' steps (scalar loads, consumed at the stores)
+    const RowSteps ma = load_row_steps(p, ua), mb = load_row_steps(p, ub);
     uint32_t stored_a = 0, stored_b = 0;
     if constexpr (CRC) {
         const bool ta = has_a && ua.mode == ZHIP_ST_OK;
         const bool tb = has_b && ub.c != ua.c && ub.mode == ZHIP_ST_OK;
-        stored_a = load_u32_any(ta ? ua.cp + p.g.nbytes : zero);  // same address in every lane
-        stored_b = load_u32_any(tb ? ub.cp + p.g.nbytes : zero);
+        if (!(p.tune & kTuneNoConsts)) {
+            stored_a = load_u32_any(ta ? ua.cp + p.g.nbytes : zero);  // same address in every lane
+            stored_b = load_u32_any(tb ? ub.cp + p.g.nbytes : zero);
+        }
     }
     stamp(p, g, t, 1);
     // 2. tables into LDS (waits for the table loads only), lane-multiply table
@@ -615,15 +618,20 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(NU == 
         const uint32_t lane_col = (16u * (uint32_t)t) & ((1u << p.row_shift) - 1u);
         const int64_t lane_off = (int64_t)lane_row * p.r_oy + (int64_t)lane_col;
         const bool same = has_b && ub.c == ua.c;
-        const bool ilv = CRC;
+        const bool ilv = CRC && !TRAIL;  // TRAIL (tuning): every store first, then the lookups
         uint32_t acc_a = 0, acc_b = 0;
-        store_unit_rows<ITEM, SWAP, K>(p, ua, true, t, lane_row, lane_off, sink, A,
+        store_unit_rows<ITEM, SWAP, K>(p, ua, ma, true, lane_row, lane_off, sink, A,
                                        ilv && ua.mode == ZHIP_ST_OK, s_tab, &acc_a);
         stamp(p, g, t, 3);
         if constexpr (NU == 2) {
             acc_b = same ? acc_a : 0u;
-            store_unit_rows<ITEM, SWAP, K>(p, ub, has_b, t, lane_row, lane_off, sink, B,
+            store_unit_rows<ITEM, SWAP, K>(p, ub, mb, has_b, lane_row, lane_off, sink, B,
                                            ilv && has_b && ub.mode == ZHIP_ST_OK, s_tab, &acc_b);
+        }
+        if constexpr (CRC && TRAIL) {
+            if (ua.mode == ZHIP_ST_OK) acc_a = crc_unit_rows<K>(s_tab, 0u, A, p.tune);
+            if constexpr (NU == 2)
+                if (has_b && ub.mode == ZHIP_ST_OK) acc_b = crc_unit_rows<K>(s_tab, same ? acc_a : 0u, B, p.tune);
         }
         stamp(p, g, t, 4);
         // 4. run ends (the CRC lookups ran with the stores): A alone when B
@@ -677,6 +685,8 @@ KernelFn select_pair_nu(bool crc, int item, bool swap) {
 }
 
 KernelFn select_pair_kernel(bool crc, int item, bool swap, int nu) {
+    if (nu == 3)  // tuning arm: every store before the CRC lookups (headline item type only)
+        return crc && item == 4 && !swap ? k_decode_pair<true, 4, false, 2, 8, true> : nullptr;
     return nu == 1 ? select_pair_nu<1>(crc, item, swap) : select_pair_nu<2>(crc, item, swap);
 }
 

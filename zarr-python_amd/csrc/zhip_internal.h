@@ -65,6 +65,7 @@ struct DecodeParams {
     int64_t r_oy;              // out stride of dim ndim-2
     int32_t nd2;               // ndim - 2
     uint32_t rows;             // 1: launch k_decode_rows
+    const zhip_rowblk* rowmap; // per (sel, unit, step) destinations (zhip_rows_map); k_decode_pair
     // load-address prediction (zhip_predict; k_decode_pair): payload of chunk c
     // predicted at src + pred_base + (c / pred_per) * pred_outer + (c % pred_per) * pred_inner
     uint32_t pred, pred_per;
@@ -84,9 +85,10 @@ constexpr uint32_t kTunePersist = 64u;   // whole-row layouts: persistent k_deco
 constexpr uint32_t kTuneSingle = 128u;   // k_decode_pair with one unit per workgroup
 constexpr uint32_t kTuneSerialize = 256u; // k_decode_pair: wait for every load before the first store
 constexpr uint32_t kTuneNoTables = 512u;  // k_decode_pair: skip the in-LDS table build (results invalid)
-constexpr uint32_t kTuneTrailingCrc = 2048u; // k_decode_pair: CRC lookups after all stores (default: per block)
+constexpr uint32_t kTuneTrailingCrc = 2048u; // k_decode_pair: CRC lookups after all stores (default: per block; headline type)
 constexpr uint32_t kTuneNoRunEnd = 4096u;  // k_decode_pair: skip the run-end reduction entirely (results invalid)
 constexpr uint32_t kTuneNoBarrier = 8192u; // k_decode_pair: skip the table barrier (results invalid)
+constexpr uint32_t kTuneNoConsts = 32768u; // k_decode_pair: skip the lane-constant and trailer loads (results invalid)
 constexpr uint32_t kTuneStamp = 1024u;    // k_decode_pair: per-workgroup phase timestamps (zhip_debug_stamps)
 constexpr uint32_t kStampWG = 8192u;      // workgroups stamped per launch
 constexpr uint32_t kStampSlots = 8u;

@@ -10,6 +10,8 @@ from __future__ import annotations
 import ctypes
 import os
 
+import numpy as np
+
 MAX_DIMS = 8
 
 ST_OK = 0
@@ -26,6 +28,10 @@ LF_NO_WRITE = 16
 LF_FLOAT = 32
 
 CF_MISSING = 1
+
+E_INVALID = -1
+E_HIP = -2
+E_UNSUPPORTED = -3
 
 DF_FAST_ROWS = 1
 DF_TILE = 2
@@ -108,6 +114,10 @@ class Predict(ctypes.Structure):
                 ("per", ctypes.c_uint32), ("_pad", ctypes.c_uint32)]
 
 
+# zhip_rowblk (include/zarrhip.h)
+ROWBLK_DT = np.dtype([("rel", "<i4"), ("lo", "<u2"), ("hi", "<u2")])
+
+
 class NativeError(RuntimeError):
     pass
 
@@ -151,6 +161,13 @@ def lib():
                                         ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(Predict),
                                         ctypes.c_void_p]
     L.zhip_decode_predicted.restype = ctypes.c_int
+    L.zhip_decode_mapped.argtypes = L.zhip_decode_predicted.argtypes[:-1] + [ctypes.c_void_p, ctypes.c_void_p]
+    L.zhip_decode_mapped.restype = ctypes.c_int
+    L.zhip_rows_map_len.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
+    L.zhip_rows_map_len.restype = ctypes.c_uint64
+    L.zhip_rows_map.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                                ctypes.c_uint64]
+    L.zhip_rows_map.restype = ctypes.c_int
     L.zhip_encode.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                               ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                               ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]

@@ -72,6 +72,25 @@ def get_plan(layout: N.Layout) -> N.Plan:
     return p
 
 
+def _rows_map(plan, sels: np.ndarray, device):
+    """zhip_rows_map over the host copy of the selections, uploaded; None when
+    the library declines the layout (then the launch takes the persistent row
+    decode)."""
+    n_sels = max(len(sels), 1)
+    if not len(sels):
+        sels = np.zeros(1, SEL_DT)
+    sels = np.ascontiguousarray(sels)
+    n = int(N.lib().zhip_rows_map_len(plan.handle, n_sels))
+    if n == 0:
+        return None
+    host = np.zeros(n, N.ROWBLK_DT)
+    rc = N.lib().zhip_rows_map(plan.handle, sels.ctypes.data, n_sels, host.ctypes.data, n)
+    if rc == N.E_UNSUPPORTED:
+        return None
+    N.check(rc, "zhip_rows_map")
+    return _upload(host, device)
+
+
 class DecodeLaunch:
     """One zhip_decode launch with its device-resident tables."""
 
@@ -98,12 +117,25 @@ class DecodeLaunch:
         self.flags = (N.DF_FAST_ROWS if fast else 0) | (N.DF_TILE if tile else 0) | \
             (N.DF_ROWS if fast and rows else 0)
         self.predict = predict if (fast and rows) else None
+        # row map (zhip_rows_map): per (selection, unit, step) destinations for the
+        # two-unit row decode; None when the layout does not admit one
+        self.d_rowmap = None
+        if fast and rows:
+            self.d_rowmap = _rows_map(self.plan, sels, device)
 
     def launch(self, stream: int | None = None) -> None:
         if self.n == 0:
             return
         s = _stream_handle(self.device) if stream is None else stream
         out_ptr = self.out.data_ptr() if self.out is not None else None
+        if self.d_rowmap is not None:
+            N.check(N.lib().zhip_decode_mapped(
+                self.plan.handle, self.src.data_ptr(), self.src_size, out_ptr, self.d_chunks.data_ptr(),
+                self.n, self.d_sels.data_ptr(), self.d_status.data_ptr(), self.d_ws.data_ptr(),
+                self.d_err.data_ptr(), self.d_idx_chunks.data_ptr() if self.n_idx else None, self.n_idx,
+                self.d_idx_status.data_ptr() if self.n_idx else None, self.flags, self.predict,
+                self.d_rowmap.data_ptr(), s), "zhip_decode_mapped")
+            return
         if self.predict is not None:
             N.check(N.lib().zhip_decode_predicted(
                 self.plan.handle, self.src.data_ptr(), self.src_size, out_ptr, self.d_chunks.data_ptr(),
