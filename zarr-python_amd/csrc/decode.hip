@@ -139,8 +139,7 @@ __global__ __launch_bounds__(kThreads) void k_decode(const DecodeParams p) {
             if constexpr (CRC) {
                 if (run_end) {
                     uint32_t v = crc_on ? gf_mul(acc, kth) : acc;
-#pragma unroll
-                    for (int off = 32; off > 0; off >>= 1) v ^= __shfl_xor(v, off, 64);
+                    v = wave_xor(v);
                     if ((t & 63) == 0) s_red[parity][t >> 6] = v;
                     __syncthreads();
                     if (t == 0) {
@@ -386,8 +385,7 @@ __global__ __launch_bounds__(kThreads) void k_decode_tile(const DecodeParams p) 
             }
             if constexpr (CRC) {
                 uint32_t v = gf_mul(acc, kth);
-#pragma unroll
-                for (int off = 32; off > 0; off >>= 1) v ^= __shfl_xor(v, off, 64);
+                v = wave_xor(v);
                 if ((t & 63) == 0) s_red[t >> 6] = v;
             }
             __syncthreads();  // LDS tile and s_red reads done before the next tile

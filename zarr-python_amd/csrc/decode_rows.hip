@@ -116,11 +116,26 @@ __device__ __forceinline__ void lanemul_init(uint32_t* s_mul, int t, uint32_t kt
 }
 
 
-__device__ __forceinline__ uint32_t lanemul(const uint32_t* s_mul, const uint32_t* s_r4, int t, uint32_t a) {
-    uint32_t p = s_mul[(a & 15u) * kThreads + t];
+// n * x^4 for a nibble n (the reduction of a 4-bit right shift), from its
+// four basis values: VALU only, so the Horner chain below has no LDS round
+// trips (the s_mul reads do not depend on it and all go out first).
+constexpr uint32_t r4_basis(uint32_t n) {
+    for (int i = 0; i < 4; ++i) n = (n >> 1) ^ (kPoly & (0u - (n & 1u)));
+    return n;
+}
+
+__device__ __forceinline__ uint32_t r4(uint32_t n) {
+    return ((n & 1u) ? r4_basis(1) : 0u) ^ ((n & 2u) ? r4_basis(2) : 0u) ^ ((n & 4u) ? r4_basis(4) : 0u) ^
+           ((n & 8u) ? r4_basis(8) : 0u);
+}
+
+__device__ __forceinline__ uint32_t lanemul(const uint32_t* s_mul, const uint32_t* /*s_r4*/, int t, uint32_t a) {
+    uint32_t m[8];
 #pragma unroll
-    for (int j = 1; j < 8; ++j)
-        p = (p >> 4) ^ s_r4[p & 15u] ^ s_mul[((a >> (4 * j)) & 15u) * kThreads + t];
+    for (int j = 0; j < 8; ++j) m[j] = s_mul[((a >> (4 * j)) & 15u) * kThreads + t];
+    uint32_t p = m[0];
+#pragma unroll
+    for (int j = 1; j < 8; ++j) p = (p >> 4) ^ r4(p & 15u) ^ m[j];
     return p;
 }
 
@@ -285,8 +300,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))
                 run_bits |= 1u << (ua.sidx & 31u);
                 if (run_end) {
                     uint32_t v = (p.tune & kTuneNoLaneMul) ? acc : lanemul(s_mul, s_r4, t, acc);
-#pragma unroll
-                    for (int off = 32; off > 0; off >>= 1) v ^= __shfl_xor(v, off, 64);
+                    v = wave_xor(v);
                     if ((t & 63) == 0) s_red[parity][t >> 6] = v;
                     __syncthreads();
                     if (t < 64) {  // wave 0, wave-uniform
@@ -320,6 +334,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))
                                                                            __HIP_MEMORY_SCOPE_AGENT);
                                 if (tk + n_run == p.nseg) {
                                     raw = __hip_atomic_exchange(accw, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    // consume the returned value here (rare path): a register with a
+                    // load still pending would make every later write to it wait
+                    // for the wave's stores too
+                    asm volatile("s_waitcnt vmcnt(0)" ::"v"(raw) : "memory");
                                     __hip_atomic_store(accw + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                                     last = 1;
                                 }
@@ -448,8 +466,7 @@ __device__ __forceinline__ void run_end_pair(const DecodeParams& p, const Unit& 
         return;
     }
     uint32_t v = (p.tune & kTuneNoLaneMul) ? acc : lds_mul ? lanemul(s_mul, s_r4, t, acc) : gf_mul(acc, klane);
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v ^= __shfl_xor(v, off, 64);
+    v = wave_xor(v);
     if ((t & 63) == 0) red[t >> 6] = v;
     __syncthreads();
     stamp(p, g, t, 5);
@@ -485,6 +502,10 @@ __device__ __forceinline__ void run_end_pair(const DecodeParams& p, const Unit& 
                                                            __HIP_MEMORY_SCOPE_AGENT);
                 if (tk + n_run == p.nseg) {
                     raw = __hip_atomic_exchange(accw, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    // consume the returned value here (rare path): a register with a
+                    // load still pending would make every later write to it wait
+                    // for the wave's stores too
+                    asm volatile("s_waitcnt vmcnt(0)" ::"v"(raw) : "memory");
                     __hip_atomic_store(accw + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     last = 1;
                 }
@@ -533,8 +554,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(NU == 
     stamp(p, g, t, 0);
     // 1. vector loads, in this order and count on every path: [CRC: the Horner
     //    tables (4), lane-shift constants (3)], unit headers (scalar), [CRC: the
-    //    first shard-index block], unit A (K), unit B (K), [CRC: the two CRC
-    //    trailers].  Waiting for any of them
+    //    first shard-index block], unit A (K), unit B (K); the CRC trailers
+    //    are scalar loads.  Waiting for any of them
     //    leaves the later ones in flight; unit headers are scalar loads.
     // the tables and per-lane constants need no unit header: they go out first,
     // their latency overlapping the header loads
@@ -592,9 +613,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(NU == 
     if constexpr (CRC) {
         const bool ta = has_a && ua.mode == ZHIP_ST_OK;
         const bool tb = has_b && ub.c != ua.c && ub.mode == ZHIP_ST_OK;
+        // scalar loads (lgkmcnt): consuming them at the run end never waits
+        // for this wave's stores, which a vector load issued before them would
         if (!(p.tune & kTuneNoConsts)) {
-            stored_a = load_u32_any(ta ? ua.cp + p.g.nbytes : zero);  // same address in every lane
-            stored_b = load_u32_any(tb ? ub.cp + p.g.nbytes : zero);
+            if (ta) stored_a = load_trailer_uniform(ua.cp, p.g.nbytes);
+            if (tb) stored_b = load_trailer_uniform(ub.cp, p.g.nbytes);
         }
     }
     stamp(p, g, t, 1);
@@ -641,16 +664,14 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(NU == 
         if constexpr (CRC) {
             const uint32_t sa = __builtin_amdgcn_readfirstlane(stored_a);
             const uint32_t sb = same ? sa : __builtin_amdgcn_readfirstlane(stored_b);
-#pragma unroll 1
-            for (int r = 0; r < NU; ++r) {
-                const bool second = r == 1;
-                const bool active = second ? (has_b && ub.mode == ZHIP_ST_OK) : (ua.mode == ZHIP_ST_OK && !same);
-                if (!active) continue;
-                const uint32_t bits = second ? ((same ? 1u << (ua.sidx & 31u) : 0u) | (1u << (ub.sidx & 31u)))
-                                             : 1u << (ua.sidx & 31u);
-                run_end_pair(p, second ? ub : ua, second ? acc_b : acc_a, bits, second ? sb : sa,
-                             second ? kb : ka, kLdsMul && second, s_mul, s_r4, s_red[r], t, g);
-            }
+            // two straight-line call sites (a loop here merges the wait state of
+            // its back edge, and the compiler then drains the wave's stores
+            // before the reduction)
+            if (ua.mode == ZHIP_ST_OK && !same)
+                run_end_pair(p, ua, acc_a, 1u << (ua.sidx & 31u), sa, ka, false, s_mul, s_r4, s_red[0], t, g);
+            if (NU == 2 && has_b && ub.mode == ZHIP_ST_OK)
+                run_end_pair(p, ub, acc_b, (same ? 1u << (ua.sidx & 31u) : 0u) | (1u << (ub.sidx & 31u)), sb, kb,
+                             kLdsMul, s_mul, s_r4, s_red[1], t, g);
         }
         unit_status_pair(p, ua, CRC, t);
         if (has_b) unit_status_pair(p, ub, CRC, t);

@@ -186,8 +186,7 @@ __global__ __launch_bounds__(kThreads) void k_encode(const EncodeParams p) {
             alleq = true;
             if constexpr (CRC) {
                 uint32_t v = gf_mul(acc, kth);
-#pragma unroll
-                for (int off = 32; off > 0; off >>= 1) v ^= __shfl_xor(v, off, 64);
+                v = wave_xor(v);
                 if ((t & 63) == 0) s_red[parity][t >> 6] = v;
                 __syncthreads();
                 if (t == 0) {
@@ -361,8 +360,7 @@ __global__ __launch_bounds__(kThreads) void k_shard_pack(const PackParams p) {
     }
     if (p.index_crc) {
         uint32_t v = gf_mul(acc, p.kthread[t]);
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) v ^= __shfl_xor(v, off, 64);
+        v = wave_xor(v);
         if ((t & 63) == 0) s_red[t >> 6] = v;
         __syncthreads();
         if (t == 0) {

@@ -274,8 +274,7 @@ __device__ __forceinline__ void verify_index(const DecodeParams& p, uint32_t j, 
         }
     }
     uint32_t v = gf_mul(acc, kth);
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v ^= __shfl_xor(v, off, 64);
+    v = wave_xor(v);
     __syncthreads();  // red may still be read from a previous index
     if ((t & 63) == 0) red[t >> 6] = v;
     __syncthreads();

@@ -90,6 +90,20 @@ __device__ __forceinline__ uint4 load_block_t(const uint8_t* cp, int32_t o, uint
     }
 }
 
+// XOR of v over the wave's 64 lanes, returned wave-uniform.  Four DPP steps
+// leave every lane holding its 16-lane row's total (quad_perm [1,0,3,2],
+// quad_perm [2,3,0,1], row_half_mirror, row_mirror); the four row totals are
+// then read into scalar registers.  No LDS round trips (a __shfl_xor ladder
+// is six dependent ds_bpermute's).  Every lane of the wave must be active.
+__device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, true);
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, true);
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, true);
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, true);
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 0) ^ (uint32_t)__builtin_amdgcn_readlane((int)v, 16) ^
+           (uint32_t)__builtin_amdgcn_readlane((int)v, 32) ^ (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
+}
+
 __device__ __forceinline__ uint32_t tab_apply(const uint32_t* tab, uint32_t w) {
     return tab[w & 255u] ^ tab[256 + ((w >> 8) & 255u)] ^ tab[512 + ((w >> 16) & 255u)] ^
            tab[768 + (w >> 24)];
