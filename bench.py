@@ -184,10 +184,13 @@ def extra_configs(device, args):
                                 [{"name": "transpose", "configuration": {"order": [2, 1, 0]}}, LE, CRC])
             progs.append(arr.prepare_read((Ellipsis,))[0])
         assert progs[0].tables.tile, "C3 should take the LDS-tiled transpose kernel"
+        from zarr_hip import _native as N
+        tile4 = bool(N.Plan(progs[0].tables.layout, upload=False).kernel_flags & N.PK_TILE4) and \
+            not (args.tune & 65536)
         wall, kern = time_programs(progs, steps, 3, device)
         dec = data.numel() * 4
         out["c3_transpose_210"] = _entry(dec, dec + 64 * (1048576 + 4), wall, kern,
-                                         kernel="k_decode_tile")
+                                         kernel="k_decode_tile4" if tile4 else "k_decode_tile")
         del progs, data
     if "c4" in args.extra:
         shape4, shards, inner = (1024, 1024, 1024), (128, 128, 128), (32, 32, 32)

@@ -146,6 +146,9 @@ int zhip_plan_create(const zhip_layout *layout, zhip_plan **plan);
 int zhip_plan_destroy(zhip_plan *plan);
 /* Units (workgroup work items) per chunk and workspace words per chunk. */
 int zhip_plan_info(const zhip_plan *plan, uint32_t *units_per_chunk, uint32_t *workspace_words);
+/* Which specialised kernels the plan's layout admits (ZHIP_PK_* bits). */
+#define ZHIP_PK_TILE4 1u  /* transposed layout with full 64 x 256-byte tiles: k_decode_tile4 */
+int zhip_plan_kernel_flags(const zhip_plan *plan, uint32_t *flags);
 
 /* decode flags (zhip_decode decode_flags) */
 #define ZHIP_DF_FAST_ROWS 1u  /* every chunk selects whole innermost rows that are

@@ -265,6 +265,59 @@ def test_transpose_tiled_missing_and_sharded(device):
                [SHARD((16, 16, 16), [T((2, 1, 0)), LE, CRC])])
 
 
+# k_decode_tile4: full 64-row x 256-byte tiles, four per workgroup
+TILE4_CASES = [
+    ("float32", LE, (64, 64, 64), (128, 128, 128)),   # the C3 chunk
+    ("float64", BE, (32, 16, 64), (64, 48, 128)),     # 8-byte items, byteswap, 16 tiles per chunk
+    ("int16", LE, (128, 8, 64), (256, 16, 64)),
+    ("uint8", LE, (256, 8, 64), (256, 24, 128)),
+]
+
+
+def _tile4_engaged(arr):
+    from zarr_hip import _native as N
+
+    prog, _ = arr.prepare_read((Ellipsis,))
+    assert prog.tables.tile
+    return bool(N.Plan(prog.tables.layout, upload=False).kernel_flags & N.PK_TILE4)
+
+
+@pytest.mark.parametrize("dtype,endian,chunks,shape", TILE4_CASES)
+def test_transpose_tile4(device, dtype, endian, chunks, shape):
+    arr, _, _ = _roundtrip(device, shape, chunks, dtype, [T((2, 1, 0)), endian, CRC])
+    assert _tile4_engaged(arr)
+
+
+@pytest.mark.parametrize("dtype,endian,chunks,shape", TILE4_CASES[:2])
+def test_transpose_tile4_no_crc_missing_and_sharded(device, dtype, endian, chunks, shape):
+    _roundtrip(device, shape, chunks, dtype, [T((2, 1, 0)), endian])
+    arr, _, _ = _roundtrip(device, shape, chunks, dtype, [T((2, 1, 0)), endian, CRC], fill=-3,
+                           drop=["c/0/0/1", "c/1/1/0"])
+    assert _tile4_engaged(arr)
+    shard = tuple(2 * c for c in chunks[:2]) + (chunks[2],)
+    _roundtrip(device, shard, shard, dtype, [SHARD(chunks, [T((2, 1, 0)), endian, CRC])])
+
+
+def test_transpose_tile4_crc_mismatch(device):
+    import zarr_hip
+
+    codecs = [T((2, 1, 0)), LE, CRC]
+    meta = O.ArrayMeta((128, 64, 64), (64, 64, 64), np.dtype("float32"), 0.0, codecs=codecs)
+    host = {}
+    O.write(host, meta, (Ellipsis,), _data((128, 64, 64), "float32"))
+    bad = bytearray(host["c/1/0/0"])
+    bad[700001] ^= 0x08
+    host["c/1/0/0"] = bytes(bad)
+    with pytest.raises(ValueError) as want:
+        O.read(host, meta)
+    store = zarr_hip.DeviceStore.from_host(host, device)
+    arr = zarr_hip.Array.create(store, (128, 64, 64), (64, 64, 64), "float32", 0.0, codecs=codecs)
+    assert _tile4_engaged(arr)
+    with pytest.raises(ValueError) as got:
+        arr[...]
+    assert str(got.value) == str(want.value)
+
+
 def test_tile_mode_engaged(device):
     import zarr_hip
 

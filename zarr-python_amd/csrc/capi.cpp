@@ -113,6 +113,29 @@ void build_horner(uint32_t* tab) {  // [op][slice][256], op k = A_(4096 - 4k)
 }  // namespace
 
 namespace zhip {
+// Source offset of every tile's first row in the stored chunk (tile index:
+// column block fastest, then row block, then the other dims, last fastest).
+std::vector<uint64_t> tile_bases(const zhip_plan& plan) {
+    const zhip_layout& L = plan.layout;
+    const uint64_t sq = plan.sstride[plan.tq];
+    std::vector<uint64_t> base(plan.t_per_chunk);
+    for (uint32_t ti = 0; ti < plan.t_per_chunk; ++ti) {
+        uint32_t r = ti;
+        const uint32_t cb = r % plan.n_cb;
+        r /= plan.n_cb;
+        const uint32_t qb = r % plan.n_qb;
+        r /= plan.n_qb;
+        uint64_t b = (uint64_t)qb * kTileRows * sq + (uint64_t)cb * kTileCols;
+        for (int d = L.ndim - 2; d >= 0; --d) {
+            if (d == plan.tq) continue;
+            b += (uint64_t)(r % (uint32_t)L.shape[d]) * plan.sstride[d];
+            r /= (uint32_t)L.shape[d];
+        }
+        base[ti] = b;
+    }
+    return base;
+}
+
 void fill_geom(Geom& g, const zhip_plan& plan) {
     const zhip_layout& L = plan.layout;
     g.ndim = L.ndim;
@@ -205,6 +228,7 @@ int zhip_plan_create(const zhip_layout* layout, zhip_plan** out) {
     p->max_grid = 2048;
     p->d_tables = nullptr;
     p->d_tile_tables = nullptr;
+    p->tile4 = 0;
     // tile mode: a stored dim (not the innermost) that is contiguous in out
     p->tq = -1;
     {
@@ -224,6 +248,18 @@ int zhip_plan_create(const zhip_layout* layout, zhip_plan** out) {
             for (int d = 0; d < L.ndim - 1; ++d)
                 if (d != p->tq) other *= (uint64_t)L.shape[d];
             p->t_per_chunk = (uint32_t)(other * p->n_qb * p->n_cb);
+            // k_decode_tile4 eligibility: full tiles, and every group of 4
+            // consecutive tiles at one uniform base step (so one table multiply
+            // carries a thread's Horner state from tile to tile)
+            const uint32_t T = p->t_per_chunk;
+            const std::vector<uint64_t> base = tile_bases(*p);
+            const uint64_t step = T >= 2 ? base[1] - base[0] : 0;
+            bool t4 = (L.shape[p->tq] % kTileRows) == 0 && (p->row_bytes % kTileCols) == 0 && T % 4 == 0 &&
+                      T >= 4 && base[1] > base[0];
+            for (uint32_t ti = 0; t4 && ti < T; ++ti)
+                if (base[ti] != base[ti & ~3u] + (uint64_t)(ti & 3u) * step) t4 = false;
+            p->tile4 = t4 ? 1u : 0u;
+            p->tile4_step = step;
         }
     }
     *out = p;
@@ -258,26 +294,16 @@ int zhip_plan_upload(zhip_plan* p) {
         const uint64_t sq = p->sstride[p->tq];
         const uint64_t REF = (uint64_t)(kTileRows + 16) * sq + kTileCols;
         const uint32_t T = p->t_per_chunk;
-        std::vector<uint64_t> base(T);
+        const std::vector<uint64_t> base = tile_bases(*p);
         const zhip_layout& L = p->layout;
         uint64_t maxb = 0;
-        for (uint32_t ti = 0; ti < T; ++ti) {
-            uint32_t r = ti;
-            const uint32_t cb = r % p->n_cb;
-            r /= p->n_cb;
-            const uint32_t qb = r % p->n_qb;
-            r /= p->n_qb;
-            uint64_t b = (uint64_t)qb * kTileRows * sq + (uint64_t)cb * kTileCols;
-            for (int d = L.ndim - 2; d >= 0; --d) {
-                if (d == p->tq) continue;
-                b += (uint64_t)(r % (uint32_t)L.shape[d]) * p->sstride[d];
-                r /= (uint32_t)L.shape[d];
-            }
-            base[ti] = b;
-            if (b > maxb) maxb = b;
-        }
+        for (uint32_t ti = 0; ti < T; ++ti) maxb = std::max(maxb, base[ti]);
         const uint64_t Rc = maxb + REF;
-        std::vector<uint32_t> ht(4096 + kThreads + T);
+        const bool t4 = p->tile4 != 0;
+        const uint64_t step = p->tile4_step;
+        const size_t n_base = 4096 + kThreads + T;
+        const size_t n_t4 = t4 ? 1024 + (size_t)(T / 4) * kThreads + (size_t)T * 4 : 0;
+        std::vector<uint32_t> ht(n_base + n_t4);
         build_horner_stride(ht.data(), 16ull * sq);
         for (int t = 0; t < kThreads; ++t) {
             const uint64_t rel = (uint64_t)(kTileRows + t / 16) * sq + 16u * (t % 16);
@@ -285,6 +311,38 @@ int zhip_plan_upload(zhip_plan* p) {
         }
         for (uint32_t ti = 0; ti < T; ++ti) ht[4096 + kThreads + ti] = xpow8(Rc - base[ti] - REF);
         p->t_c_inv = xpow8_inv(Rc - L.nbytes);
+        if (t4) {
+            p->tile4_off_tz = n_base;
+            p->tile4_off_kq = n_base + 1024;
+            p->tile4_off_map = n_base + 1024 + (size_t)(T / 4) * kThreads;
+            const uint32_t z = xpow8(step);
+            for (int sl = 0; sl < 4; ++sl)
+                for (uint32_t b = 0; b < 256; ++b) ht[p->tile4_off_tz + sl * 256 + b] = gf_mul(z, b << (8 * sl));
+            for (uint32_t g4 = 0; g4 < T / 4; ++g4) {
+                const uint32_t ku = gf_mul(ht[4096 + kThreads + 4 * g4 + 3], p->t_c_inv);
+                for (int t = 0; t < kThreads; ++t)
+                    ht[p->tile4_off_kq + (size_t)g4 * kThreads + t] = gf_mul(ht[4096 + t], ku);
+            }
+            // out offset of each tile relative to the chunk's out_off (full selection)
+            for (uint32_t ti = 0; ti < T; ++ti) {
+                uint32_t r = ti;
+                const uint32_t cb = r % p->n_cb;
+                r /= p->n_cb;
+                const uint32_t qb = r % p->n_qb;
+                r /= p->n_qb;
+                int64_t o = (int64_t)qb * kTileRows * L.out_stride[p->tq] +
+                            (int64_t)cb * (kTileCols / L.itemsize) * L.out_stride[L.ndim - 1];
+                for (int d = L.ndim - 2; d >= 0; --d) {
+                    if (d == p->tq) continue;
+                    o += (int64_t)(r % (uint32_t)L.shape[d]) * L.out_stride[d];
+                    r /= (uint32_t)L.shape[d];
+                }
+                uint32_t* e = &ht[p->tile4_off_map + 4ull * ti];
+                e[0] = (uint32_t)base[ti];
+                e[1] = 0;
+                std::memcpy(e + 2, &o, sizeof(o));
+            }
+        }
         if (p->d_tile_tables) (void)hipFree(p->d_tile_tables);
         p->d_tile_tables = nullptr;
         HIP_TRY(hipMalloc(&p->d_tile_tables, ht.size() * sizeof(uint32_t)));
@@ -302,6 +360,12 @@ int zhip_plan_destroy(zhip_plan* p) {
     if (p->d_tables) (void)hipFree(p->d_tables);
     if (p->d_tile_tables) (void)hipFree(p->d_tile_tables);
     delete p;
+    return ZHIP_OK;
+}
+
+int zhip_plan_kernel_flags(const zhip_plan* p, uint32_t* flags) {
+    if (!p || !flags) return set_err(ZHIP_E_INVALID, "null argument");
+    *flags = p->tile4 ? ZHIP_PK_TILE4 : 0u;
     return ZHIP_OK;
 }
 
@@ -506,6 +570,12 @@ int zhip_decode_mapped(const zhip_plan* plan, const void* src, uint64_t src_size
         p.kthread = plan->d_tile_tables + 4096;
         p.kunit = plan->d_tile_tables + 4096 + kThreads;
         p.c_inv = plan->t_c_inv;
+        p.tile4 = plan->tile4 && !(g_tune_bits & kTuneTile1);
+        if (p.tile4) {
+            p.tz = plan->d_tile_tables + plan->tile4_off_tz;
+            p.kq4 = plan->d_tile_tables + plan->tile4_off_kq;
+            p.tmap = reinterpret_cast<const TileEnt*>(plan->d_tile_tables + plan->tile4_off_map);
+        }
         const uint64_t tunits = (uint64_t)n_chunks * plan->t_per_chunk;
         if (tunits >= (1ull << 32)) return set_err(ZHIP_E_UNSUPPORTED, "too many tiles in one batch");
         p.n_units = (uint32_t)tunits;

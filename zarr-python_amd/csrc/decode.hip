@@ -490,6 +490,7 @@ static KernelFn select_tile_kernel(bool crc, int item, bool swap) {
 
 KernelFn select_rows_kernel(bool crc, int item, bool swap, int k);  // decode_rows.hip
 KernelFn select_pair_kernel(bool crc, int item, bool swap, int nu);  // decode_rows.hip
+KernelFn select_tile4_kernel(bool crc, int item, bool swap);         // decode_tile.hip
 
 int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
     if (g_tune_max_grid > 0) max_grid = g_tune_max_grid;
@@ -519,6 +520,14 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
         }
         const uint32_t grid = p.n_units < (uint32_t)max_grid ? p.n_units : (uint32_t)max_grid;
         hipLaunchKernelGGL(fn, dim3(grid), dim3(kThreads), 0, stream, p);
+        return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
+    }
+    if (p.tq >= 0 && p.tile4) {
+        // four tiles per workgroup, non-persistent (k_decode_tile4, decode_tile.hip)
+        KernelFn fn = select_tile4_kernel((p.lflags & ZHIP_LF_CRC) != 0, p.g.itemsize, (p.lflags & ZHIP_LF_SWAP) != 0);
+        if (!fn) return ZHIP_E_UNSUPPORTED;
+        if (p.n_units == 0) return ZHIP_OK;
+        hipLaunchKernelGGL(fn, dim3(p.n_units / 4u), dim3(kThreads), 0, stream, p);
         return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
     }
     if (p.tq >= 0) {

@@ -1,0 +1,237 @@
+// k_decode_tile4: decode of transposed chunks (a stored dim other than the
+// innermost is contiguous in out: TransposeCodec, src/zarr/codecs/transpose.py:
+// 89-118), four 64-row x 256-byte LDS tiles per workgroup.
+//
+// Same structure as k_decode_pair (decode_rows.hip): non-persistent, every
+// vector load of the workgroup issued first (4 tiles x 4 blocks per thread,
+// one static count on every path), headers and trailer through the scalar
+// cache, and one CRC run end per workgroup.  Per tile the data goes registers
+// -> LDS (stored order) -> registers (out order) -> 16-byte stores, then the
+// tile's Horner steps (while the stores drain).  The CRC state of
+// a thread carries from tile to tile through one table multiply (the four
+// tiles sit at a uniform base step), and the lane / tile / chunk-end shifts
+// are one host-built per-lane constant (kq4) applied once.
+//
+// Eligible plans (zhip_plan.tile4): full tiles (shape[tq] % 64 == 0,
+// row_bytes % 256 == 0), t_per_chunk % 4 == 0, groups of four consecutive
+// tiles at one base step; the launch covers whole chunks with a full
+// selection (planner _tile_ok).  Others take the persistent k_decode_tile.
+
+#include <hip/hip_runtime.h>
+
+#include "../../include/zarrhip.h"
+#include "zhip_gf2.h"
+#include "zhip_internal.h"
+#include "zhip_device.h"
+#include "zhip_decode_common.h"
+
+namespace zhip {
+namespace {
+
+constexpr int kTiles = 4;                   // tiles per workgroup
+constexpr int kPasses = kTileRows / 16;     // 16-byte blocks per thread per tile
+
+__device__ uint4 g_tile_zero[1];            // dummy-load target (never written)
+__device__ uint4 g_tile_sink[kThreads];     // dummy-store target
+
+typedef unsigned int zhip_v4u_a1t __attribute__((ext_vector_type(4), aligned(1)));
+typedef __attribute__((address_space(1))) const zhip_v4u_a1t zhip_gv4u_a1t;
+
+__device__ __forceinline__ uint4 load_nt16_a1(const uint8_t* a) {  // any alignment, one dwordx4 nt
+    const zhip_v4u_a1t w = __builtin_nontemporal_load((zhip_gv4u_a1t*)(reinterpret_cast<uintptr_t>(a)));
+    return make_uint4(w.x, w.y, w.z, w.w);
+}
+
+struct TileMap4 {
+    TileEnt e[kTiles];
+};
+
+}  // namespace
+
+template <bool CRC, int ITEM, bool SWAP>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_decode_tile4(
+    const DecodeParams p) {
+    constexpr int kPitch = ITEM == 8 ? 264 : 260;  // bytes per LDS tile row (2-way read conflicts)
+    constexpr int kPer = 16 / ITEM;                // rows per 16-byte out piece
+    constexpr int kPiecesPerCol = kTileRows / kPer;
+    __shared__ uint32_t s_tab[CRC ? 16 * 256 : 1];
+    __shared__ uint32_t s_tz[CRC ? 1024 : 1];
+    __shared__ __attribute__((aligned(16))) uint8_t s_tile[kTileRows * kPitch];
+    __shared__ uint32_t s_red[kThreads / 64];
+    const int t = threadIdx.x;
+    const uint32_t g = blockIdx.x;
+    const uint32_t gpc = p.t_per_chunk / kTiles;  // workgroups per chunk (grid = n_chunks * gpc)
+    const uint32_t c = g / gpc;
+    const uint32_t grp = g - c * gpc;
+    const uint32_t expected = p.g.nbytes + (CRC ? 4u : 0u);
+    // 1. loads: tables and the lane constant first (L2 hits), then the chunk
+    //    header (scalar), then the 16 data blocks
+    uint4 tv0, tv1, tv2, tv3, tzv;
+    uint32_t kq = 0;
+    if constexpr (CRC) {
+        const uint4* gt = reinterpret_cast<const uint4*>(p.horner);
+        tv0 = gt[t];
+        tv1 = gt[t + kThreads];
+        tv2 = gt[t + 2 * kThreads];
+        tv3 = gt[t + 3 * kThreads];
+        tzv = reinterpret_cast<const uint4*>(p.tz)[t];
+        kq = p.kq4[(size_t)grp * kThreads + t];
+    }
+    const Unit U = resolve_unit(p, c * p.nseg, expected);
+    const TileMap4 tm = load_uniform<TileMap4>(p.tmap + (size_t)grp * kTiles);
+    const bool ok = U.mode == ZHIP_ST_OK;
+    const uint32_t sq = p.sstride[p.tq];
+    const uint32_t row0 = (uint32_t)t >> 4, col = 16u * (uint32_t)(t & 15);
+    const uint8_t* zero = reinterpret_cast<const uint8_t*>(g_tile_zero);
+    uint4 blk[kTiles][kPasses];
+#pragma unroll
+    for (int j = 0; j < kTiles; ++j)
+#pragma unroll
+        for (int k = 0; k < kPasses; ++k)
+            blk[j][k] = load_nt16_a1(ok ? U.cp + tm.e[j].tbase + (row0 + 16u * k) * sq + col : zero);
+    uint32_t stored = 0;
+    if (CRC && ok) stored = load_trailer_uniform(U.cp, p.g.nbytes);
+    if constexpr (CRC) {
+        uint4* st = reinterpret_cast<uint4*>(s_tab);
+        st[t] = tv0;
+        st[t + kThreads] = tv1;
+        st[t + 2 * kThreads] = tv2;
+        st[t + 3 * kThreads] = tv3;
+        reinterpret_cast<uint4*>(s_tz)[t] = tzv;
+    }
+    // 2. per tile: LDS in stored order, out order back, 16-byte stores, then
+    //    the tile's Horner steps
+    const bool writes = ok || U.mode == ZHIP_ST_MISSING;
+    const uint4 f = make_uint4(p.fill[0], p.fill[1], p.fill[2], p.fill[3]);
+    const int32_t last = p.g.ndim - 1;
+    const int64_t oq = p.g.ostride[p.tq];    // == ITEM
+    const int64_t ocol = p.g.ostride[last];  // out stride of the innermost stored dim
+    uint8_t* const obase = p.out + U.out_off;
+    uint8_t* const sink = reinterpret_cast<uint8_t*>(g_tile_sink) + 16 * t;
+    uint32_t S = 0;  // this thread's CRC state, referenced at the current tile
+#pragma unroll
+    for (int j = 0; j < kTiles; ++j) {
+        if (j > 0) __syncthreads();  // the previous tile's LDS reads are done
+#pragma unroll
+        for (int k = 0; k < kPasses; ++k) {
+            const uint4 v = swap_block<ITEM, SWAP>(blk[j][k]);
+            uint32_t* d = reinterpret_cast<uint32_t*>(s_tile + (16 * k + row0) * kPitch + col);
+            d[0] = v.x;
+            d[1] = v.y;
+            d[2] = v.z;
+            d[3] = v.w;
+        }
+        __syncthreads();  // tile j (and, first time, the tables) in LDS
+#pragma unroll
+        for (int k = 0; k < kPasses; ++k) {
+            const uint32_t pc = (uint32_t)(k * kThreads + t);
+            const uint32_t jc = pc / kPiecesPerCol;          // element of the stored row
+            const uint32_t r0 = (pc % kPiecesPerCol) * kPer; // first of kPer tile rows
+            uint32_t w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int e = 0; e < kPer; ++e) {
+                const uint8_t* src = s_tile + (r0 + e) * kPitch + jc * ITEM;
+                if constexpr (ITEM == 8) {
+                    const uint2 v = *reinterpret_cast<const uint2*>(src);
+                    w[2 * e] = v.x;
+                    w[2 * e + 1] = v.y;
+                } else if constexpr (ITEM == 4) {
+                    w[e] = *reinterpret_cast<const uint32_t*>(src);
+                } else if constexpr (ITEM == 2) {
+                    w[e / 2] |= (uint32_t)(*reinterpret_cast<const uint16_t*>(src)) << (16 * (e & 1));
+                } else {
+                    w[e / 4] |= (uint32_t)(*src) << (8 * (e & 3));
+                }
+            }
+            // every path stores (failed chunks to the sink): a static store count
+            uint8_t* dst = writes ? obase + tm.e[j].orel + (int64_t)jc * ocol + (int64_t)r0 * oq : sink;
+            store_nt16(dst, ok ? make_uint4(w[0], w[1], w[2], w[3]) : f);
+        }
+        // the tile's Horner steps after its stores are out (tables in LDS since
+        // the first barrier); the state moves to this tile's reference
+        if constexpr (CRC) {
+            if (ok) {
+                uint32_t acc = 0;
+#pragma unroll
+                for (int k = 0; k < kPasses; ++k) {
+                    const uint4 v = blk[j][k];
+                    acc = tab_apply(s_tab, acc ^ v.x) ^ tab_apply(s_tab + 1024, v.y) ^
+                          tab_apply(s_tab + 2048, v.z) ^ tab_apply(s_tab + 3072, v.w);
+                }
+                S = (j == 0 ? 0u : tab_apply(s_tz, S)) ^ acc;
+            }
+        }
+    }
+    // 3. run end: shift (lane, last tile, chunk end in one constant), reduce,
+    //    publish; the arrival completing the chunk compares with the trailer
+    if (CRC && ok) {
+        uint32_t v = wave_xor(gf_mul(S, kq));
+        if ((t & 63) == 0) s_red[t >> 6] = v;
+        __syncthreads();
+        if (t < 64) {
+            const uint32_t V = __builtin_amdgcn_readfirstlane(s_red[0] ^ s_red[1] ^ s_red[2] ^ s_red[3]);
+            uint32_t raw = 0, last_arrival = 0;
+            if (t == 0) {
+                if (gpc <= 32) {
+                    const uint64_t full = gpc == 32 ? 0xFFFFFFFFull : ((1ull << gpc) - 1ull);
+                    const uint64_t bits = 1ull << grp;
+                    uint64_t* w = reinterpret_cast<uint64_t*>(p.ws) + 2ull * c;
+                    const uint64_t prev = __hip_atomic_fetch_xor(w, (bits << 32) | V, __ATOMIC_RELAXED,
+                                                                 __HIP_MEMORY_SCOPE_AGENT);
+                    if (((prev >> 32) ^ bits) == full) {
+                        __hip_atomic_store(w, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        raw = (uint32_t)prev ^ V;
+                        last_arrival = 1;
+                    }
+                } else {  // more than 32 workgroups per chunk: xor, then count arrivals
+                    uint32_t* accw = p.ws + 4ull * c;
+                    const uint32_t prev = __hip_atomic_fetch_xor(accw, V, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    asm volatile("s_waitcnt vmcnt(0)" ::"v"(prev) : "memory");
+                    const uint32_t tk = __hip_atomic_fetch_add(accw + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (tk + 1u == gpc) {
+                        raw = __hip_atomic_exchange(accw, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store(accw + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        last_arrival = 1;
+                    }
+                }
+                if (last_arrival) {
+                    const uint32_t computed = ~(raw ^ p.c3);  // kq4 carries t_c_inv
+                    const uint32_t code = computed == stored ? ZHIP_ST_OK : ZHIP_ST_CRC_MISMATCH;
+                    zhip_status st = {code, stored, computed, 0u};
+                    p.status[c] = st;
+                    if (code != ZHIP_ST_OK) atomicOr(p.errflag, 1u << code);
+                }
+            }
+        }
+    }
+    // statuses not produced by the CRC finalize
+    if (grp == 0 && t == 0) {
+        if (ok) {
+            if (!CRC) {
+                zhip_status st = {ZHIP_ST_OK, 0u, 0u, 0u};
+                p.status[c] = st;
+            }
+        } else {
+            zhip_status st = {U.mode, 0u, 0u, 0u};
+            p.status[c] = st;
+            if (U.mode != ZHIP_ST_MISSING) atomicOr(p.errflag, 1u << U.mode);
+        }
+    }
+}
+
+using KernelFn = void (*)(const DecodeParams);
+
+KernelFn select_tile4_kernel(bool crc, int item, bool swap) {
+    switch (item) {
+        case 1: return crc ? k_decode_tile4<true, 1, false> : k_decode_tile4<false, 1, false>;
+        case 2: return crc ? (swap ? k_decode_tile4<true, 2, true> : k_decode_tile4<true, 2, false>)
+                           : (swap ? k_decode_tile4<false, 2, true> : k_decode_tile4<false, 2, false>);
+        case 4: return crc ? (swap ? k_decode_tile4<true, 4, true> : k_decode_tile4<true, 4, false>)
+                           : (swap ? k_decode_tile4<false, 4, true> : k_decode_tile4<false, 4, false>);
+        case 8: return crc ? (swap ? k_decode_tile4<true, 8, true> : k_decode_tile4<true, 8, false>)
+                           : (swap ? k_decode_tile4<false, 8, true> : k_decode_tile4<false, 8, false>);
+        default: return nullptr;
+    }
+}
+
+}  // namespace zhip

@@ -24,6 +24,13 @@ struct Geom {
 
 // Kernel argument block (passed by value; indexed only with compile-time
 // subscripts inside the kernels so it stays in SGPRs / kernarg memory).
+// One tile of a chunk (k_decode_tile4): source offset of its first row in the
+// stored chunk, out offset relative to the chunk's out_off.
+struct TileEnt {
+    uint32_t tbase, _pad;
+    int64_t orel;
+};
+
 struct DecodeParams {
     const uint8_t* src;
     uint64_t src_size;
@@ -54,6 +61,11 @@ struct DecodeParams {
     uint32_t t_per_chunk, n_qb, n_cb;
     uint32_t sstride[ZHIP_MAX_DIMS];  // stored-stream byte stride of each dim
     zhip_fdiv d_qb, d_cb;
+    // k_decode_tile4 (tile4 != 0): see zhip_plan
+    uint32_t tile4;
+    const uint32_t* tz;
+    const uint32_t* kq4;
+    const struct TileEnt* tmap;
     // fused shard-index CRC verification: workgroup g checks indexes g, g+G, ...
     const zhip_chunk* idx_chunks;
     zhip_status* idx_status;
@@ -89,6 +101,7 @@ constexpr uint32_t kTuneTrailingCrc = 2048u; // k_decode_pair: CRC lookups after
 constexpr uint32_t kTuneNoRunEnd = 4096u;  // k_decode_pair: skip the run-end reduction entirely (results invalid)
 constexpr uint32_t kTuneNoBarrier = 8192u; // k_decode_pair: skip the table barrier (results invalid)
 constexpr uint32_t kTuneNoConsts = 32768u; // k_decode_pair: skip the lane-constant and trailer loads (results invalid)
+constexpr uint32_t kTuneTile1 = 65536u;  // transposed layouts: the one-tile persistent k_decode_tile
 constexpr uint32_t kTuneStamp = 1024u;    // k_decode_pair: per-workgroup phase timestamps (zhip_debug_stamps)
 constexpr uint32_t kStampWG = 8192u;      // workgroups stamped per launch
 constexpr uint32_t kStampSlots = 8u;
@@ -164,6 +177,12 @@ struct zhip_plan {
     uint32_t t_per_chunk, n_qb, n_cb;
     uint32_t sstride[ZHIP_MAX_DIMS];
     uint32_t t_c_inv;
+    // k_decode_tile4 (full tiles, groups of 4 tiles at a uniform base step):
+    // d_tile_tables continues with tz (1024: multiply by x^(8 step)) | kq4
+    // ((T/4) * 256: kthread * kunit[last tile of the group] * t_c_inv) | tmap (T)
+    uint32_t tile4;
+    uint64_t tile4_step;                                 // base step between consecutive tiles
+    uint64_t tile4_off_tz, tile4_off_kq, tile4_off_map;  // u32 offsets in d_tile_tables
     uint32_t* d_tile_tables;
     // shard index (sharded layouts): payload 16*n_inner, E, CRC constants
     uint32_t idx_nbytes, idx_E, idx_c_inv, idx_c3;  // horner (stride 16*sstride[tq]) | kthread (256) | kunit (t_per_chunk)

@@ -37,6 +37,8 @@ DF_FAST_ROWS = 1
 DF_TILE = 2
 DF_ROWS = 4
 
+PK_TILE4 = 1
+
 PF_INDEX_START = 1
 PF_INDEX_CRC = 2
 PF_KEEP_EMPTY = 4
@@ -146,6 +148,8 @@ def lib():
     L.zhip_plan_info.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32),
                                  ctypes.POINTER(ctypes.c_uint32)]
     L.zhip_plan_info.restype = ctypes.c_int
+    L.zhip_plan_kernel_flags.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32)]
+    L.zhip_plan_kernel_flags.restype = ctypes.c_int
     L.zhip_decode.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                               ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
                               ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
@@ -226,6 +230,13 @@ class Plan:
     @property
     def handle(self):
         return self._h
+
+    @property
+    def kernel_flags(self) -> int:
+        """ZHIP_PK_* bits: specialised kernels this layout admits."""
+        f = ctypes.c_uint32()
+        check(lib().zhip_plan_kernel_flags(self._h, ctypes.byref(f)), "zhip_plan_kernel_flags")
+        return f.value
 
     def emulate_chunk_crc(self, data: bytes) -> int:
         buf = ctypes.create_string_buffer(bytes(data) + b"\0" * 16)
