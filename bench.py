@@ -222,7 +222,7 @@ def c1_plumbing(device, args):
     """BASELINE configs[0] (bench/compress_normal.py-style): 1e7 float32 1-D in
     (2**20,) chunks, bytes codec only (10 chunks, the last a boundary chunk
     stored at full size).  The reference runs it on the CPU pipeline; here:
-    the device-resident decode (generic k_decode, 1-D) and the MemoryStore
+    the device-resident decode (row decode on 1-D chunks viewed as whole rows) and the MemoryStore
     round trip (host bytes -> HBM -> host), both checked bit-exact."""
     import torch
 
@@ -251,7 +251,7 @@ def c1_plumbing(device, args):
         t_rt.append(time.perf_counter() - t0)
     return _entry(dec, dec + 10 * ck * 4, wall, kern,
                   host_roundtrip_GiBps=round(dec / float(np.median(t_rt)) / GIB, 2),
-                  note="device decode via generic k_decode (1-D); host_roundtrip = MemoryStore -> HBM -> numpy")
+                  note="device decode via k_decode_pair (1-D chunks viewed as whole 512-byte rows, planner._split_1d); host_roundtrip = MemoryStore -> HBM -> numpy")
 
 
 def c5_partial(device, args):

@@ -79,6 +79,21 @@ def test_big_endian(device, dtype):
     _roundtrip(device, (21, 34), (8, 16), dtype, [BE, CRC])
 
 
+@pytest.mark.parametrize("shape,chunks,dtype,codecs,sel", [
+    ((100000,), (16384,), "float32", [LE, CRC], (Ellipsis,)),          # boundary chunk: 128-byte rows
+    ((100000,), (16384,), "float32", [LE, CRC], (slice(1000, 99000),)),  # 32-byte rows
+    ((10 ** 6,), (2 ** 17,), "float32", [LE], (Ellipsis,)),            # C1 at 1/10 size
+    ((300000,), (65536,), "int16", [BE, CRC], (Ellipsis,)),
+    ((300000,), (65536,), "uint8", [LE, CRC], (slice(4096, 200704),)),
+])
+def test_1d_row_decode(device, shape, chunks, dtype, codecs, sel):
+    """1-D chunks whose selections are whole R-item rows take the row decode
+    (planner._split_1d views each chunk as (N/R, R))."""
+    arr, _, _ = _roundtrip(device, shape, chunks, dtype, codecs, fill=5, selection=sel)
+    prog, _ = arr.prepare_read(sel)
+    assert prog.tables.rows and prog.tables.layout.ndim == 2
+
+
 def test_bytes_only_no_crc(device):
     _roundtrip(device, (1000,), (128,), "float32", [LE])
 

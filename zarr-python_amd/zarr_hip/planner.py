@@ -171,6 +171,23 @@ def _fast_ok(layout: N.Layout, start, count, step, out_offs, out_base_ptr: int) 
                 and np.all(step[:, last] == 1))
 
 
+def _split_1d(n_items: int, itemsize: int, ostride: int, start, count, step) -> int:
+    """A 1-D chunk read into contiguous out as whole rows of R items (the bytes
+    unchanged, viewed as (n/R, R)), so the row decode applies: the largest R
+    (a power of two, rows of 16..4096 bytes) dividing the chunk length and every
+    selection's start and count, with (n/R) a multiple of the rows one 4 KiB
+    workgroup step covers.  0 when none (int selections, steps, odd bounds)."""
+    if ostride != itemsize or not len(start) or not np.all(step[:, 0] == 1):
+        return 0
+    r = 4096 // itemsize
+    while r * itemsize >= 16:
+        if n_items % r == 0 and np.all(start[:, 0] % r == 0) and np.all(count[:, 0] % r == 0) and \
+                np.all(count[:, 0] > 0) and (n_items // r) % (4096 // (r * itemsize)) == 0:
+            return r
+        r //= 2
+    return 0
+
+
 def _rows_ok(layout: N.Layout, count, step) -> bool:
     """ZHIP_DF_ROWS preconditions (on top of _fast_ok): unit steps wherever more
     than one index is selected, rows of 2^k <= 4096 bytes, and shape[ndim-2] a
@@ -272,6 +289,14 @@ def plan_decode(chain: ChainInfo, spec: ArraySpec, items: list, out_strides_byte
             chunks["src_len"][i] = sl
             chunks["flags"][i] = N.CF_MISSING if miss else 0
             chunks["out_off"][i] = _out_offset(osel, out_strides_bytes)
+        if ndim == 1:
+            split = _split_1d(shape_st[0], itemsize, ost_st[0], start, count, step)
+            if split:  # the same chunk bytes viewed as (N/R, R): whole rows of R items
+                R = split
+                layout = _make_layout([shape_st[0] // R, R], itemsize, [ost_st[0] * R, ost_st[0]], flags, fill)
+                start = np.stack([start[:, 0] // R, np.zeros(n, np.int64)], axis=1)
+                count = np.stack([count[:, 0] // R, np.full(n, R, np.int64)], axis=1)
+                step = np.ones((n, 2), np.int64)
         sels, inv = _pack_sels(start, count, step)
         chunks["sel"] = inv
         fast = _fast_ok(layout, start, count, step, chunks["out_off"], out_base_ptr)
