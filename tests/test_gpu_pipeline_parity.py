@@ -12,8 +12,10 @@ cell (test_pipeline_parity.py:82-233):
   4. each side reads the other side's store correctly.
 
 Cells the device path does not take (gzip compressor, nested sharding,
-codecs around a sharding serializer) are refused loudly; that is pinned in
-test_gpu_pipeline_suite.py and test_outer_codecs_around_sharding_refused.
+bytes->bytes codecs around a sharding serializer) are refused loudly; that is
+pinned in test_gpu_pipeline_suite.py and test_outer_codecs_around_sharding_refused.
+Transposes around a sharding serializer are supported (the shard is sharded in
+its permuted space) and checked both ways.
 """
 
 from __future__ import annotations
@@ -165,6 +167,57 @@ def test_pipeline_parity_subchunk_write_order(device, order, loc):
     O.write(host, meta, slice(None), np.arange(96, dtype="int32").reshape(shape))
     O.write(host, meta, (slice(3, 9), slice(1, 6)), 777)
     assert _chunk_bytes(store) == host
+
+
+def _outer_t(order, inner, inner_codecs=(LE,)):
+    return [{"name": "transpose", "configuration": {"order": list(order)}},
+            {"name": "sharding_indexed", "configuration": {
+                "chunk_shape": list(inner), "codecs": list(inner_codecs)}}]
+
+
+@pytest.mark.parametrize("direction", ["gpu-write-oracle-read", "oracle-write-gpu-read",
+                                       "oracle-write-gpu-read-host-store"])
+@pytest.mark.parametrize("shape,chunks,order,inner,inner_codecs,sels", [
+    # test_pipeline_parity.py:463-523 ("outer-transpose-around-sharding")
+    ((8, 8), (4, 4), (1, 0), (2, 2), (LE,), [np.s_[...], np.s_[1:3, 2:7]]),
+    # non-square shards, 3-d, crc inside, int selections (the inner chunk also
+    # divides the unpermuted shard: ShardingCodec.validate sees the array's
+    # chunk shape, sharding.py:558-590)
+    ((12, 8, 8), (6, 8, 4), (2, 0, 1), (2, 2, 4), (BE, CRC),
+     [np.s_[...], np.s_[1:11:3, 5, :], np.s_[7, 2:8, 1:5], np.s_[4, 3, 2]]),
+])
+def test_pipeline_parity_outer_transpose_around_sharding(device, direction, shape, chunks, order, inner,
+                                                         inner_codecs, sels):
+    """Transposes in front of the sharding codec: the shard is sharded in its
+    permuted (stored) space.  Whichever side writes (full write, then a region
+    write through the partial-encode branch), the other reads back the same
+    contents, full and partial; and both sides write the same bytes."""
+    import zarr_hip
+
+    codecs = _outer_t(order, inner, inner_codecs)
+    data = (np.arange(int(np.prod(shape))).reshape(shape) + 1).astype("uint16")
+    region = tuple(slice(1, min(4, s)) for s in shape)
+    expected = data.copy()
+    expected[region] = 99
+    meta = O.ArrayMeta(shape, chunks, np.dtype("uint16"), 0, codecs=codecs)
+    host: dict = {}
+    O.write(host, meta, Ellipsis, data)
+    O.write(host, meta, region, 99)
+    if direction == "gpu-write-oracle-read":
+        store = zarr_hip.DeviceStore(device)
+        arr = zarr_hip.Array.create(store, shape, chunks, "uint16", 0, codecs=codecs)
+        arr[...] = data
+        arr[region] = 99
+        got = _chunk_bytes(store)
+        assert got == host
+        for sel in sels:
+            np.testing.assert_array_equal(O.read(got, meta, sel), expected[sel])
+    else:
+        store = zarr_hip.MemoryStore(dict(host)) if direction.endswith("host-store") else \
+            zarr_hip.DeviceStore.from_host(dict(host), device)
+        arr = zarr_hip.Array.create(store, shape, chunks, "uint16", 0, codecs=codecs)
+        for sel in sels:
+            np.testing.assert_array_equal(arr[sel], expected[sel])
 
 
 @pytest.mark.parametrize("codecs", [

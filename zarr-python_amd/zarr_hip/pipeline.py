@@ -17,7 +17,7 @@ from __future__ import annotations
 
 import asyncio
 import os
-from dataclasses import dataclass, field
+from dataclasses import dataclass, field, replace
 from typing import Any, Iterable
 
 import numpy as np
@@ -309,6 +309,41 @@ class HipCodecPipeline:
             byte_length = c.compute_encoded_size(byte_length, array_spec)
         return byte_length
 
+    # ------------------------------------------------- transposes around sharding
+    def _shard_space(self, batch: list, arr, drop_axes: tuple):
+        """Transposes in front of a sharding codec (the codec then sees the
+        permuted shard, chunk_utils.py:304-363): the same read / write expressed
+        in that stored space -- selections, spec and the out / value tensor
+        permuted (a strided view, no copy) -- for the pipeline of the sharding
+        codec alone.  None when the chain has no such transposes."""
+        if not self.array_array_codecs or not isinstance(self.array_bytes_codec, ShardingCodec):
+            return None
+        spec: ArraySpec = batch[0][1]
+        perm = analyze_chain(self.codecs, spec).perm
+        if perm == tuple(range(len(perm))):
+            return None
+        if drop_axes:
+            raise NotImplementedError("drop_axes with transposes around sharding_indexed")
+        torch = _torch()
+        spec_s = replace(spec, shape=tuple(spec.shape[p] for p in perm))
+        pipe = HipCodecPipeline.from_codecs((self.array_bytes_codec,), batch_size=self.batch_size)
+        pipe = replace(pipe.evolve_from_array_spec(spec_s), predict_loads=self.predict_loads)
+        is_int = [isinstance(c, (int, np.integer)) for c in batch[0][2]]
+        kept = [d for d in range(len(perm)) if not is_int[d]]      # decoded dims present in out
+        out_dim = {d: i for i, d in enumerate(kept)}
+        order = [out_dim[perm[i]] for i in range(len(perm)) if not is_int[perm[i]]]
+        batch_s = []
+        for bg, sp, csel, osel, complete in batch:
+            if [isinstance(c, (int, np.integer)) for c in csel] != is_int:
+                raise NotImplementedError("mixed int selections in one batch")
+            batch_s.append((bg, replace(sp, shape=spec_s.shape), tuple(csel[p] for p in perm),
+                            tuple(osel[i] for i in order) if len(osel) == len(order) else osel, complete))
+        if isinstance(arr, torch.Tensor) and arr.dim() == len(order):
+            arr = arr.permute(order)
+        elif isinstance(arr, np.ndarray) and arr.ndim == len(order):
+            arr = arr.transpose(order)
+        return pipe, batch_s, arr
+
     # ---------------------------------------------------------------- read
     def prepare_read(self, batch_info: Iterable, out, drop_axes: tuple = ()) -> DecodeProgram:
         torch = _torch()
@@ -317,6 +352,10 @@ class HipCodecPipeline:
             raise ValueError("empty batch")
         if not isinstance(out, torch.Tensor) or not out.is_cuda:
             raise TypeError("HipCodecPipeline.read needs a device-resident out (torch CUDA tensor)")
+        ss = self._shard_space(batch, out, drop_axes)
+        if ss is not None:
+            pipe, batch_s, out_s = ss
+            return pipe.prepare_read(batch_s, out_s, drop_axes)
         spec: ArraySpec = batch[0][1]
         device = out.device
         chain: ChainInfo = analyze_chain(self.codecs, spec)
@@ -375,6 +414,10 @@ class HipCodecPipeline:
         batch = list(batch_info)
         if not batch:
             return
+        ss = self._shard_space(batch, value, drop_axes)
+        if ss is not None:
+            pipe, batch_s, value_s = ss
+            return pipe.write_sync(batch_s, value_s, drop_axes)
         spec: ArraySpec = batch[0][1]
         device = value.device if isinstance(value, torch.Tensor) and value.is_cuda else None
         if device is None:

@@ -46,9 +46,13 @@ def analyze_chain(codecs, spec: ArraySpec) -> ChainInfo:
                                            spec.fill_value))
         perm = tuple(perm[t.order[i]] for i in range(len(perm)))
     if isinstance(ab, ShardingCodec):
-        if aa or bb:
+        # transposes around the sharding codec permute the shard it sees
+        # (perm = the outer permutation; the pipeline maps batches into that
+        # space, HipCodecPipeline._shard_space); bytes->bytes codecs after it
+        # would hide the index and are not on the GPU path
+        if bb:
             raise NotImplementedError(
-                "array->array / bytes->bytes codecs around sharding_indexed are not on the GPU path")
+                "bytes->bytes codecs around sharding_indexed are not on the GPU path")
         inner_spec = ab.inner_spec(spec)
         inner = analyze_chain(ab.codecs, inner_spec)
         if inner.shard is not None:
@@ -57,7 +61,7 @@ def analyze_chain(codecs, spec: ArraySpec) -> ChainInfo:
         if ia or not isinstance(iab, BytesCodec) or iab.endian not in (None, "little") or \
                 len(ibb) > 1:
             raise NotImplementedError("shard index codecs must be [bytes(little)] + optional crc32c")
-        return ChainInfo(perm, False, False, None, ab, inner)
+        return ChainInfo(tuple(perm), False, False, None, ab, inner)
     assert isinstance(ab, BytesCodec)
     ab = ab.evolve_from_array_spec(spec)
     return ChainInfo(perm, ab.needs_swap(spec.dtype), len(bb) == 1, ab.endian)
