@@ -425,7 +425,10 @@ __device__ __forceinline__ void store_unit_rows(const DecodeParams& p, const Uni
     for (int k = 0; k < K; ++k) {
         const uint32_t lo = m.e[k].lo, hi = m.e[k].hi;
         const bool wr = writes && lane_row - lo < hi - lo;  // unsigned: lo <= lane_row < hi
-        store_nt16(wr ? base + m.e[k].rel + lane_off : sink, present ? swap_block<ITEM, SWAP>(blk[k]) : f);
+        uint8_t* const dst = wr ? base + m.e[k].rel + lane_off : sink;
+        const uint4 val = present ? swap_block<ITEM, SWAP>(blk[k]) : f;
+        if (p.tune & kTuneTemporalStores) *reinterpret_cast<uint4*>(dst) = val;  // ablation
+        else store_nt16(dst, val);
         if (crc) *acc = (p.tune & kTuneSkipCrc) ? *acc ^ blk[k].x ^ blk[k].y ^ blk[k].z ^ blk[k].w
                                                 : crc_block(s_tab, *acc, blk[k]);
     }
@@ -460,12 +463,14 @@ __device__ __forceinline__ uint32_t crc_unit_rows(const uint32_t* s_tab, uint32_
 // the chunk compares with the trailer.  `red` is a 4-word LDS scratch.
 __device__ __forceinline__ void run_end_pair(const DecodeParams& p, const Unit& U, uint32_t acc, uint32_t run_bits,
                                              uint32_t stored, uint32_t klane, bool lds_mul, const uint32_t* s_mul,
-                                             const uint32_t* s_r4, uint32_t* red, int t, uint32_t g = 0) {
+                                             const uint32_t* s_r4, uint32_t* red, int t, uint32_t g = 0,
+                                             uint32_t extra = 0) {
     if (p.tune & kTuneNoRunEnd) {  // ablation: no reduction, no publication
-        if (acc == 0x9E3779B9u) red[0] = acc;
+        if ((acc ^ extra) == 0x9E3779B9u) red[0] = acc;
         return;
     }
-    uint32_t v = (p.tune & kTuneNoLaneMul) ? acc : lds_mul ? lanemul(s_mul, s_r4, t, acc) : gf_mul(acc, klane);
+    // extra: an already shifted contribution of the same run (VARIANT 2)
+    uint32_t v = ((p.tune & kTuneNoLaneMul) ? acc : lds_mul ? lanemul(s_mul, s_r4, t, acc) : gf_mul(acc, klane)) ^ extra;
     v = wave_xor(v);
     if ((t & 63) == 0) red[t >> 6] = v;
     __syncthreads();
@@ -531,7 +536,9 @@ __device__ __forceinline__ void unit_status_pair(const DecodeParams& p, const Un
     }
 }
 
-template <bool CRC, int ITEM, bool SWAP, int NU, int K = 8, bool TRAIL = false>
+// VARIANT (tuning arms, headline item type only): 0 production, 1 every store
+// before the CRC lookups, 2 independent Horner chains for the two units
+template <bool CRC, int ITEM, bool SWAP, int NU, int K = 8, int VARIANT = 0>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(NU == 1 ? 8 : 4))) void k_decode_pair(const DecodeParams p) {
     // NU == 1: the lane shift is a VALU multiply (no 16 KiB s_mul), so that
     // eight workgroups fit a CU's LDS
@@ -641,13 +648,14 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(NU == 
         const uint32_t lane_col = (16u * (uint32_t)t) & ((1u << p.row_shift) - 1u);
         const int64_t lane_off = (int64_t)lane_row * p.r_oy + (int64_t)lane_col;
         const bool same = has_b && ub.c == ua.c;
+        constexpr bool TRAIL = VARIANT == 1, SPLIT = VARIANT == 2;
         const bool ilv = CRC && !TRAIL;  // TRAIL (tuning): every store first, then the lookups
         uint32_t acc_a = 0, acc_b = 0;
         store_unit_rows<ITEM, SWAP, K>(p, ua, ma, true, lane_row, lane_off, sink, A,
                                        ilv && ua.mode == ZHIP_ST_OK, s_tab, &acc_a);
         stamp(p, g, t, 3);
         if constexpr (NU == 2) {
-            acc_b = same ? acc_a : 0u;
+            acc_b = (same && !SPLIT) ? acc_a : 0u;
             store_unit_rows<ITEM, SWAP, K>(p, ub, mb, has_b, lane_row, lane_off, sink, B,
                                            ilv && has_b && ub.mode == ZHIP_ST_OK, s_tab, &acc_b);
         }
@@ -671,7 +679,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(NU == 
                 run_end_pair(p, ua, acc_a, 1u << (ua.sidx & 31u), sa, ka, false, s_mul, s_r4, s_red[0], t, g);
             if (NU == 2 && has_b && ub.mode == ZHIP_ST_OK)
                 run_end_pair(p, ub, acc_b, (same ? 1u << (ua.sidx & 31u) : 0u) | (1u << (ub.sidx & 31u)), sb, kb,
-                             kLdsMul, s_mul, s_r4, s_red[1], t, g);
+                             kLdsMul, s_mul, s_r4, s_red[1], t, g, (SPLIT && same) ? gf_mul(acc_a, ka) : 0u);
         }
         unit_status_pair(p, ua, CRC, t);
         if (has_b) unit_status_pair(p, ub, CRC, t);
@@ -706,8 +714,9 @@ KernelFn select_pair_nu(bool crc, int item, bool swap) {
 }
 
 KernelFn select_pair_kernel(bool crc, int item, bool swap, int nu) {
-    if (nu == 3)  // tuning arm: every store before the CRC lookups (headline item type only)
-        return crc && item == 4 && !swap ? k_decode_pair<true, 4, false, 2, 8, true> : nullptr;
+    if (nu == 3 || nu == 4)  // tuning arms (headline item type only): VARIANT 1 / 2
+        return !(crc && item == 4 && !swap) ? nullptr
+               : nu == 3 ? k_decode_pair<true, 4, false, 2, 8, 1> : k_decode_pair<true, 4, false, 2, 8, 2>;
     return nu == 1 ? select_pair_nu<1>(crc, item, swap) : select_pair_nu<2>(crc, item, swap);
 }
 

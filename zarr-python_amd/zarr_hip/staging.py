@@ -26,7 +26,7 @@ import numpy as np
 
 from .store import ALIGN, TAIL_SLACK, DeviceRef, RangeByteRequest, SuffixByteRequest
 
-WINDOW = 8 << 20
+WINDOW = int(os.environ.get("ZARR_HIP_STAGE_WINDOW", str(8 << 20)))
 MAX_U64 = np.uint64(0xFFFFFFFFFFFFFFFF)
 
 _POOL: ThreadPoolExecutor | None = None
