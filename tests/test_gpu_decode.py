@@ -94,6 +94,23 @@ def test_1d_row_decode(device, shape, chunks, dtype, codecs, sel):
     assert prog.tables.rows and prog.tables.layout.ndim == 2
 
 
+@pytest.mark.parametrize("tune", [64, 65536 | 64])
+def test_rows_fallback_kernels(device, tune):
+    """Whole-row batches without a row map (zhip_decode_predicted, or a map the
+    library declines) take the persistent k_decode_rows; transposed layouts can
+    be forced onto the one-tile k_decode_tile.  Both stay exact."""
+    from zarr_hip import _native as N
+
+    N.lib().zhip_set_tuning(2, tune)
+    try:
+        _roundtrip(device, (128, 128, 128), (64, 64, 64), "float32", [LE, CRC])
+        _roundtrip(device, (128, 128, 64), (64, 64, 64), "float32",
+                   [SHARD((32, 32, 64), [LE, CRC])])
+        _roundtrip(device, (128, 128, 128), (64, 64, 64), "float32", [T((2, 1, 0)), LE, CRC])
+    finally:
+        N.lib().zhip_set_tuning(2, 0)
+
+
 def test_bytes_only_no_crc(device):
     _roundtrip(device, (1000,), (128,), "float32", [LE])
 

@@ -165,6 +165,22 @@ def test_rows_map_matches_scatter_semantics(case):
                 np.testing.assert_array_equal(got_dst[want_ok], dst[want_ok])
 
 
+def test_rows_map_declines_offsets_beyond_32_bits():
+    """A chunk whose footprint in out spans more than 2 GiB has no row map (the
+    launch then takes the persistent row decode)."""
+    from zarr_hip import _native as N
+    from zarr_hip.planner import SEL_DT, _make_layout
+
+    L = _make_layout((4, 64, 64), 4, [1 << 30, 256, 4], 0, b"\0")
+    table = np.zeros(1, SEL_DT)
+    table[0]["count"][:3] = (4, 64, 64)
+    table[0]["step"][:3] = 1
+    plan = N.Plan(L, upload=False)
+    n = int(N.lib().zhip_rows_map_len(plan.handle, 1))
+    m = np.zeros(n, N.ROWBLK_DT)
+    assert N.lib().zhip_rows_map(plan.handle, table.ctypes.data, 1, m.ctypes.data, n) == N.E_UNSUPPORTED
+
+
 def test_rows_map_declines_non_row_layouts():
     from zarr_hip import _native as N
 
