@@ -212,10 +212,69 @@ def extra_configs(device, args):
     if "c5" in args.extra:
         out["c5_partial_2048"] = c5_partial(device, args)
         torch.cuda.empty_cache()
+    if "enc" in args.extra:
+        out["encode_c2"] = encode_c2(device, args)
+        torch.cuda.empty_cache()
     if "e2e" in args.extra:
         out["e2e_c2_host"] = e2e_host(device, args)
         torch.cuda.empty_cache()
     return out
+
+
+class _EncodeProg:
+    """One prepared k_encode launch (what ChunkWriter._encode_chunks issues for
+    complete chunks) in the program interface ReadGraph replays."""
+
+    def __init__(self, launch):
+        self.l = launch
+
+    def launch(self, stream=None):
+        self.l.launch(stream)
+
+    def results(self):
+        return None
+
+
+def encode_c2(device, args):
+    """Encode side of C2 (a2/a4/a15): the 256^3 f32 device array written as 64
+    chunks of 64^3 with bytes+crc32c into a DeviceStore arena -- gather 16-byte
+    rows, empty-chunk check, CRC, trailer -- by k_encode, the launch
+    HipCodecPipeline.write_sync issues for complete chunks.  Timed like the
+    decode (graph replay of K launches); the stored bytes are then decoded back
+    and compared with the source."""
+    import torch
+
+    import zarr_hip
+    from zarr_hip.planner import analyze_chain, plan_encode
+    from zarr_hip.writer import EncodeLaunch
+
+    shape, chunks = (256, 256, 256), (64, 64, 64)
+    data = torch.from_numpy(synthetic(shape, seed=0)).to(device)
+    progs, checks = [], []
+    for _ in range(2):
+        store = zarr_hip.DeviceStore(device, capacity=64 * (1 << 20) + (1 << 20))
+        arr = zarr_hip.Array.create(store, shape, chunks, "float32", 0.0, codecs=[LE, CRC])
+        batch, _ = arr.batch_info((Ellipsis,))
+        spec = batch[0][1]
+        chain = analyze_chain(arr.codec_pipeline.codecs, spec)
+        elen = 64 ** 3 * 4 + 4
+        offs = [store.arena.reserve(elen) for _ in batch]
+        items = [(offs[i], it[2], [sl.start or 0 for sl in it[3]]) for i, it in enumerate(batch)]
+        t = plan_encode(chain, spec, items, [int(x) * 4 for x in data.stride()], data.data_ptr())
+        assert t.rows, "C2 encode should take the row-mapped encode"
+        progs.append(_EncodeProg(EncodeLaunch(t.layout, t.chunks, t.sels, data, store.arena.buf, t.fast,
+                                              device, t.rows)))
+        checks.append((store, arr, batch, offs, elen))
+    wall, kern = time_programs(progs, max(10, args.steps // 2), 3, device)
+    for store, arr, batch, offs, elen in checks:
+        for (bg, *_), off in zip(batch, offs):
+            store.register(bg.path, off, elen)
+        if not torch.equal(arr.get((Ellipsis,)).view(torch.int32), data.view(torch.int32)):  # NaN payloads: bitwise
+            raise SystemExit("bench encode: decoded store differs from the source")
+    src = data.numel() * 4
+    return _entry(src, src + 64 * (1048576 + 4), wall, kern,
+                  kernel="k_encode" if args.tune & 64 else "k_encode_pair",
+                  note="decoded_GiBps = source bytes encoded per second")
 
 
 def c1_plumbing(device, args):
@@ -449,7 +508,7 @@ def main():
     ap.add_argument("--eager", action="store_true",
                     help="time one host launch per step instead of a hipGraph replay")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
-    ap.add_argument("--extra", default="c1,c2,c3,c4,c5,e2e",
+    ap.add_argument("--extra", default="c1,c2,c3,c4,c5,enc,e2e",
                     help="extra configs measured at N=1 (subset of c1,c2,c3,c4,c5,e2e, or '')")
     args = ap.parse_args()
 

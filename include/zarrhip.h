@@ -275,6 +275,13 @@ int zhip_encode(const zhip_plan *plan, const void *arr, void *dst, const zhip_ch
                 uint32_t n_chunks, const zhip_sel *d_sels, zhip_status *d_status,
                 uint32_t *d_workspace, uint32_t *d_nonempty, uint32_t encode_flags, void *stream);
 
+/* zhip_encode with the row map of the batch's selections (zhip_rows_map over
+ * the same layout, where out_stride holds the source array's strides): the
+ * whole-row chunks then encode in the two-unit kernel (k_encode_pair). */
+int zhip_encode_mapped(const zhip_plan *plan, const void *arr, void *dst, const zhip_chunk *d_chunks,
+                       uint32_t n_chunks, const zhip_sel *d_sels, zhip_status *d_status, uint32_t *d_workspace,
+                       uint32_t *d_nonempty, uint32_t encode_flags, const zhip_rowblk *d_rowmap, void *stream);
+
 /* shard pack flags */
 #define ZHIP_PF_INDEX_START 1u   /* index_location == "start" */
 #define ZHIP_PF_INDEX_CRC 2u     /* index codecs end in crc32c */

@@ -590,6 +590,13 @@ int zhip_decode_mapped(const zhip_plan* plan, const void* src, uint64_t src_size
 int zhip_encode(const zhip_plan* plan, const void* arr, void* dst, const zhip_chunk* d_chunks, uint32_t n_chunks,
                 const zhip_sel* d_sels, zhip_status* d_status, uint32_t* d_workspace, uint32_t* d_nonempty,
                 uint32_t encode_flags, void* stream) {
+    return zhip_encode_mapped(plan, arr, dst, d_chunks, n_chunks, d_sels, d_status, d_workspace, d_nonempty,
+                              encode_flags, nullptr, stream);
+}
+
+int zhip_encode_mapped(const zhip_plan* plan, const void* arr, void* dst, const zhip_chunk* d_chunks,
+                       uint32_t n_chunks, const zhip_sel* d_sels, zhip_status* d_status, uint32_t* d_workspace,
+                       uint32_t* d_nonempty, uint32_t encode_flags, const zhip_rowblk* d_rowmap, void* stream) {
     if (!plan) return set_err(ZHIP_E_INVALID, "null plan");
     if (!plan->d_tables) return set_err(ZHIP_E_INVALID, "plan not uploaded (zhip_plan_upload)");
     if (n_chunks == 0) return ZHIP_OK;
@@ -628,6 +635,19 @@ int zhip_encode(const zhip_plan* plan, const void* arr, void* dst, const zhip_ch
             p.fill_nan = ((((uint64_t)p.fill[1] << 32) | p.fill[0]) & 0x7FFFFFFFFFFFFFFFull) > 0x7FF0000000000000ull;
     }
     p.fast = (encode_flags & ZHIP_DF_FAST_ROWS) ? 1u : 0u;
+    p.tune = g_tune_bits;
+    p.rowmap = nullptr;
+    if (d_rowmap) {
+        const uint32_t rb = plan->row_bytes;
+        const int nd = L.ndim;
+        if (!p.fast || nd < 2 || rb < 16 || rb > (uint32_t)kWgStride || (rb & (rb - 1)) != 0 ||
+            (uint32_t)L.shape[nd - 2] % ((uint32_t)kWgStride / rb) != 0)
+            return set_err(ZHIP_E_INVALID, "row map given for a layout without whole-row encode");
+        p.rowmap = d_rowmap;
+        p.kpair = plan->d_tables + 4096 + kThreads + plan->nseg;
+        p.row_shift = (uint32_t)__builtin_ctz(rb);
+        p.r_oy = L.out_stride[nd - 2];
+    }
     int rc = launch_encode(p, static_cast<hipStream_t>(stream), plan->max_grid);
     if (rc == ZHIP_E_UNSUPPORTED) return set_err(rc, "no encode kernel for this layout");
     if (rc != ZHIP_OK) return set_err(rc, std::string("launch failed: ") + hipGetErrorString(hipGetLastError()));

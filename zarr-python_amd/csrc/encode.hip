@@ -24,6 +24,7 @@
 #include "zhip_device.h"
 #include "zhip_gf2.h"
 #include "zhip_internal.h"
+#include "zhip_decode_common.h"
 
 namespace zhip {
 
@@ -127,6 +128,13 @@ __device__ __forceinline__ void store_block(uint8_t* cp, int32_t o, uint4 v, uin
     for (uint32_t i = 0; i < n; ++i) cp[o + i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3u)));
 }
 
+__device__ __forceinline__ void put_le_u32(uint8_t* d, uint32_t v) {  // any alignment
+    d[0] = (uint8_t)v;
+    d[1] = (uint8_t)(v >> 8);
+    d[2] = (uint8_t)(v >> 16);
+    d[3] = (uint8_t)(v >> 24);
+}
+
 template <bool CRC, bool FAST, int ITEM, bool SWAP>
 __global__ __launch_bounds__(kThreads) void k_encode(const EncodeParams p) {
     constexpr int K = kDefaultBlocks;
@@ -221,6 +229,179 @@ __global__ __launch_bounds__(kThreads) void k_encode(const EncodeParams p) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// k_encode_pair: whole-row layouts with a row map (zhip_encode_mapped).  The
+// two-unit structure of k_decode_pair (decode_rows.hip) run in reverse: every
+// gather load of both units first (source rows from the row map; lanes outside
+// the selection read one dummy line and take the fill value), then per block
+// the fill-equality test, byteswap, store and Horner step, then one run end
+// per chunk run whose last arrival writes the CRC trailer.
+// ---------------------------------------------------------------------------
+__device__ uint4 g_enc_zero[1];
+__device__ uint4 g_enc_sink[kThreads];
+
+typedef unsigned int zhip_v4u_ae __attribute__((ext_vector_type(4), aligned(1)));
+typedef __attribute__((address_space(1))) const zhip_v4u_ae zhip_gv4u_ae;
+typedef __attribute__((address_space(1))) zhip_v4u_ae zhip_gv4u_aew;
+
+__device__ __forceinline__ uint4 enc_load16(const uint8_t* a) {  // any alignment, one dwordx4 nt
+    const zhip_v4u_ae w = __builtin_nontemporal_load((zhip_gv4u_ae*)(reinterpret_cast<uintptr_t>(a)));
+    return make_uint4(w.x, w.y, w.z, w.w);
+}
+
+__device__ __forceinline__ void enc_store16(uint8_t* a, uint4 v) {  // any alignment, one dwordx4 nt
+    zhip_v4u_ae w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, (zhip_gv4u_aew*)(reinterpret_cast<uintptr_t>(a)));
+}
+
+struct EncRowSteps {
+    zhip_rowblk e[kDefaultBlocks];
+};
+
+template <bool CRC, int ITEM, bool SWAP>
+__device__ __forceinline__ void enc_unit(const EncodeParams& p, const zhip_chunk& ch, uint32_t sidx, bool live,
+                                        const EncRowSteps& m, uint32_t lane_row, const uint4 (&blk)[kDefaultBlocks],
+                                        const uint32_t* s_tab, uint32_t& acc, bool& alleq, int t) {
+    const uint4 f = make_uint4(p.fill[0], p.fill[1], p.fill[2], p.fill[3]);
+    const int32_t seg_lo = (int32_t)p.E - (int32_t)((sidx + 1u) * p.seg);
+    uint8_t* const cp = p.dst + ch.src;
+    uint8_t* const sink = reinterpret_cast<uint8_t*>(g_enc_sink) + 16 * t;
+#pragma unroll
+    for (int k = 0; k < kDefaultBlocks; ++k) {
+        const int32_t o = seg_lo + kWgStride * k;
+        const bool in_sel = lane_row - m.e[k].lo < (uint32_t)(m.e[k].hi - m.e[k].lo);
+        const uint4 v = in_sel ? blk[k] : f;  // _merge_chunk_array: outside the selection = fill
+        alleq = alleq && block_eq_fill<ITEM>(v, 16u, p);
+        const uint4 e = swap_block<ITEM, SWAP>(v);
+        enc_store16(live && o >= 0 ? cp + o + 16 * t : sink, e);  // every path stores: static count
+        if constexpr (CRC) {
+            if (live && o >= 0)
+                acc = tab_apply(s_tab, acc ^ e.x) ^ tab_apply(s_tab + 1024, e.y) ^ tab_apply(s_tab + 2048, e.z) ^
+                      tab_apply(s_tab + 3072, e.w);
+        }
+    }
+}
+
+template <bool CRC>
+__device__ __forceinline__ void enc_run_end(const EncodeParams& p, const zhip_chunk& ch, uint32_t c, uint32_t acc,
+                                           uint32_t klane, uint32_t bits, uint32_t n_run, uint32_t* red, int t) {
+    if constexpr (!CRC) {
+        if (t == 0 && (bits & 1u)) {  // the unit ending at E is in this run: one status per chunk
+            zhip_status st = {ZHIP_ST_OK, 0u, 0u, 0u};
+            p.status[c] = st;
+        }
+        return;
+    } else {
+        const uint32_t v = wave_xor(gf_mul(acc, klane));
+        __syncthreads();  // red may still be read by the previous run end
+        if ((t & 63) == 0) red[t >> 6] = v;
+        __syncthreads();
+        if (t != 0) return;
+        const uint32_t V = red[0] ^ red[1] ^ red[2] ^ red[3];
+        uint32_t raw = 0, last = 0;
+        if (p.nseg <= 32) {
+            const uint64_t full = p.nseg >= 32 ? 0xFFFFFFFFull : ((1ull << p.nseg) - 1ull);
+            uint64_t* w = reinterpret_cast<uint64_t*>(p.ws) + 2ull * c;
+            const uint64_t prev =
+                __hip_atomic_fetch_xor(w, ((uint64_t)bits << 32) | V, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (((prev >> 32) ^ bits) == full) {
+                __hip_atomic_store(w, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                raw = (uint32_t)prev ^ V;
+                last = 1;
+            }
+        } else {
+            uint32_t* accw = p.ws + 4ull * c;
+            const uint32_t prev = __hip_atomic_fetch_xor(accw, V, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::"v"(prev) : "memory");
+            const uint32_t tk = __hip_atomic_fetch_add(accw + 2, n_run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (tk + n_run == p.nseg) {
+                raw = __hip_atomic_exchange(accw, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(accw + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                last = 1;
+            }
+        }
+        if (last) {
+            const uint32_t crc = ~(raw ^ p.c3);  // kpair carries c_inv
+            put_le_u32(p.dst + ch.src + p.g.nbytes, crc);  // LE trailer (crc32c_.py:64-68)
+            zhip_status st = {ZHIP_ST_OK, crc, crc, 0u};
+            p.status[c] = st;
+        }
+    }
+}
+
+template <bool CRC, int ITEM, bool SWAP>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_encode_pair(const EncodeParams p) {
+    constexpr int K = kDefaultBlocks;
+    __shared__ uint32_t s_tab[CRC ? 16 * 256 : 1];
+    __shared__ uint32_t s_red[2][kThreads / 64];
+    const int t = threadIdx.x;
+    const uint32_t q0 = 2u * blockIdx.x;
+    const bool has_b = q0 + 1u < p.n_units;
+    auto unit_of = [&](uint32_t q) {
+        const uint32_t c = q / p.nseg;
+        return c * p.nseg + (p.nseg - 1u - (q - c * p.nseg));
+    };
+    const uint32_t u_a = unit_of(q0), u_b = has_b ? unit_of(q0 + 1u) : u_a;
+    const uint32_t ca = u_a / p.nseg, sa = u_a - ca * p.nseg, cb = u_b / p.nseg, sb = u_b - cb * p.nseg;
+    uint4 tv0, tv1, tv2, tv3;
+    uint32_t ka = 0, kb = 0;
+    if constexpr (CRC) {
+        const uint4* gt = reinterpret_cast<const uint4*>(p.horner);
+        tv0 = gt[t];
+        tv1 = gt[t + kThreads];
+        tv2 = gt[t + 2 * kThreads];
+        tv3 = gt[t + 3 * kThreads];
+        ka = p.kpair[(size_t)sa * kThreads + t];
+        kb = p.kpair[(size_t)sb * kThreads + t];
+    }
+    const zhip_chunk cha = load_uniform<zhip_chunk>(p.chunks + ca);
+    const zhip_chunk chb = load_uniform<zhip_chunk>(p.chunks + cb);
+    const EncRowSteps ma = load_uniform<EncRowSteps>(p.rowmap + ((size_t)cha.sel * p.nseg + sa) * K);
+    const EncRowSteps mb = load_uniform<EncRowSteps>(p.rowmap + ((size_t)chb.sel * p.nseg + sb) * K);
+    const uint32_t lane_row = (16u * (uint32_t)t) >> p.row_shift;
+    const uint32_t lane_col = (16u * (uint32_t)t) & ((1u << p.row_shift) - 1u);
+    const int64_t lane_off = (int64_t)lane_row * p.r_oy + (int64_t)lane_col;
+    const uint8_t* zero = reinterpret_cast<const uint8_t*>(g_enc_zero);
+    // 1. gather loads of both units (static count: outside the selection -> dummy line)
+    uint4 A[K], B[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const bool in = lane_row - ma.e[k].lo < (uint32_t)(ma.e[k].hi - ma.e[k].lo);
+        A[k] = enc_load16(in ? p.arr + cha.out_off + ma.e[k].rel + lane_off : zero);
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const bool in = has_b && lane_row - mb.e[k].lo < (uint32_t)(mb.e[k].hi - mb.e[k].lo);
+        B[k] = enc_load16(in ? p.arr + chb.out_off + mb.e[k].rel + lane_off : zero);
+    }
+    if constexpr (CRC) {
+        uint4* st = reinterpret_cast<uint4*>(s_tab);
+        st[t] = tv0;
+        st[t + kThreads] = tv1;
+        st[t + 2 * kThreads] = tv2;
+        st[t + 3 * kThreads] = tv3;
+        __syncthreads();
+    }
+    // 2. per block: fill test, byteswap, store, Horner step
+    const bool same = has_b && cb == ca;
+    uint32_t acc_a = 0, acc_b = 0;
+    bool eq_a = true, eq_b = true;
+    enc_unit<CRC, ITEM, SWAP>(p, cha, sa, true, ma, lane_row, A, s_tab, acc_a, eq_a, t);
+    if (same) {
+        acc_b = acc_a;
+        eq_b = eq_a;
+    }
+    enc_unit<CRC, ITEM, SWAP>(p, chb, sb, has_b, mb, lane_row, B, s_tab, acc_b, eq_b, t);
+    // 3. chunk_is_empty (chunk_utils.py:74-85): any element != fill -> non-empty
+    if (!same && __any(!eq_a) && (t & 63) == 0) atomicOr(p.nonempty + ca, 1u);
+    if (has_b && __any(!eq_b) && (t & 63) == 0) atomicOr(p.nonempty + cb, 1u);
+    // 4. run ends: A alone when B starts another chunk, then B (or A+B)
+    if (!same) enc_run_end<CRC>(p, cha, ca, acc_a, ka, 1u << (sa & 31u), 1u, s_red[0], t);
+    if (has_b)
+        enc_run_end<CRC>(p, chb, cb, acc_b, kb, (same ? 1u << (sa & 31u) : 0u) | (1u << (sb & 31u)), same ? 2u : 1u,
+                         s_red[1], t);
+}
+
 using EncodeFn = void (*)(const EncodeParams);
 
 template <bool CRC, bool FAST>
@@ -234,9 +415,29 @@ static EncodeFn pick_encode(int item, bool swap) {
     }
 }
 
+static EncodeFn pick_encode_pair(bool crc, int item, bool swap) {
+    switch (item) {
+        case 1: return crc ? k_encode_pair<true, 1, false> : k_encode_pair<false, 1, false>;
+        case 2: return crc ? (swap ? k_encode_pair<true, 2, true> : k_encode_pair<true, 2, false>)
+                           : (swap ? k_encode_pair<false, 2, true> : k_encode_pair<false, 2, false>);
+        case 4: return crc ? (swap ? k_encode_pair<true, 4, true> : k_encode_pair<true, 4, false>)
+                           : (swap ? k_encode_pair<false, 4, true> : k_encode_pair<false, 4, false>);
+        case 8: return crc ? (swap ? k_encode_pair<true, 8, true> : k_encode_pair<true, 8, false>)
+                           : (swap ? k_encode_pair<false, 8, true> : k_encode_pair<false, 8, false>);
+        default: return nullptr;
+    }
+}
+
 int launch_encode(const EncodeParams& p, hipStream_t stream, int max_grid) {
     const bool crc = (p.lflags & ZHIP_LF_CRC) != 0;
     const bool swap = (p.lflags & ZHIP_LF_SWAP) != 0;
+    if (p.rowmap && p.seg == (uint32_t)kWgStride * kDefaultBlocks && !(p.tune & kTunePersist)) {
+        EncodeFn fn = pick_encode_pair(crc, p.g.itemsize, swap);
+        if (!fn) return ZHIP_E_UNSUPPORTED;
+        if (p.n_units == 0) return ZHIP_OK;
+        hipLaunchKernelGGL(fn, dim3((p.n_units + 1u) / 2u), dim3(kThreads), 0, stream, p);
+        return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
+    }
     EncodeFn fn = crc ? (p.fast ? pick_encode<true, true>(p.g.itemsize, swap) : pick_encode<true, false>(p.g.itemsize, swap))
                       : (p.fast ? pick_encode<false, true>(p.g.itemsize, swap) : pick_encode<false, false>(p.g.itemsize, swap));
     if (!fn) return ZHIP_E_UNSUPPORTED;

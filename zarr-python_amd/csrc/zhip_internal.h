@@ -130,6 +130,13 @@ struct EncodeParams {
     uint32_t fill[4];
     uint32_t fill_nan;
     uint32_t fast;
+    // k_encode_pair (zhip_encode_mapped): row map and per-lane constants as in
+    // the two-unit decode; rows of 2^row_shift bytes, r_oy = arr stride of dim ndim-2
+    const zhip_rowblk* rowmap;
+    const uint32_t* kpair;
+    uint32_t row_shift;
+    int64_t r_oy;
+    uint32_t tune;
 };
 
 struct PackParams {

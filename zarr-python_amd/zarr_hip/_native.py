@@ -176,6 +176,8 @@ def lib():
                               ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                               ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
     L.zhip_encode.restype = ctypes.c_int
+    L.zhip_encode_mapped.argtypes = L.zhip_encode.argtypes[:-1] + [ctypes.c_void_p, ctypes.c_void_p]
+    L.zhip_encode_mapped.restype = ctypes.c_int
     L.zhip_shard_pack.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                   ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,

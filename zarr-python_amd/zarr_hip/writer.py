@@ -48,8 +48,8 @@ class EncodeLaunch:
     """One zhip_encode launch over flat chunk tables."""
 
     def __init__(self, layout: N.Layout, chunks: np.ndarray, sels: np.ndarray, arr, dst, fast: bool,
-                 device):
-        from .pipeline import get_plan
+                 device, rows: bool = False):
+        from .pipeline import _rows_map, get_plan
 
         torch = _torch()
         self.plan = get_plan(layout)
@@ -63,6 +63,8 @@ class EncodeLaunch:
         self.arr = arr
         self.dst = dst
         self.flags = N.DF_FAST_ROWS if fast else 0
+        # whole-row batches encode in k_encode_pair through the row map
+        self.d_rowmap = _rows_map(self.plan, sels, device) if fast and rows else None
 
     def launch(self, stream: int | None = None) -> None:
         from .pipeline import _stream_handle
@@ -71,10 +73,12 @@ class EncodeLaunch:
             return
         self.d_nonempty.zero_()
         s = _stream_handle(self.device) if stream is None else stream
-        N.check(N.lib().zhip_encode(self.plan.handle, self.arr.data_ptr(), self.dst.data_ptr(),
-                                    self.d_chunks.data_ptr(), self.n, self.d_sels.data_ptr(),
-                                    self.d_status.data_ptr(), self.d_ws.data_ptr(),
-                                    self.d_nonempty.data_ptr(), self.flags, s), "zhip_encode")
+        N.check(N.lib().zhip_encode_mapped(self.plan.handle, self.arr.data_ptr(), self.dst.data_ptr(),
+                                           self.d_chunks.data_ptr(), self.n, self.d_sels.data_ptr(),
+                                           self.d_status.data_ptr(), self.d_ws.data_ptr(),
+                                           self.d_nonempty.data_ptr(), self.flags,
+                                           self.d_rowmap.data_ptr() if self.d_rowmap is not None else None,
+                                           s), "zhip_encode_mapped")
 
     def nonempty(self) -> np.ndarray:
         return self.d_nonempty[: self.n].cpu().numpy().astype(bool)
@@ -189,7 +193,7 @@ class ChunkWriter:
             for i, (bs, sp, csel, osel, _) in enumerate(complete_items):
                 items.append((offs[i], csel, [s.start or 0 for s in osel]))
             t = plan_encode(chain, spec, items, vstr, v.data_ptr())
-            launches.append((EncodeLaunch(t.layout, t.chunks, t.sels, v, dst, t.fast, self.device),
+            launches.append((EncodeLaunch(t.layout, t.chunks, t.sels, v, dst, t.fast, self.device, t.rows),
                              list(range(len(complete_items)))))
         if partial_items:
             tstr = [int(s) * itemsize for s in temp.stride()]
@@ -201,7 +205,7 @@ class ChunkWriter:
             t = plan_encode(chain, spec, items, tstr[1:], temp.data_ptr())
             # the leading temp index goes into out_off
             t.chunks["out_off"] = np.arange(len(partial_items)) * tstr[0]
-            launches.append((EncodeLaunch(t.layout, t.chunks, t.sels, temp, dst, t.fast, self.device),
+            launches.append((EncodeLaunch(t.layout, t.chunks, t.sels, temp, dst, t.fast, self.device, t.rows),
                              [base + i for i in range(len(partial_items))]))
         for l, _ in launches:
             l.launch()
@@ -291,7 +295,7 @@ class ChunkWriter:
 
             items = shard_items(src, astart_c, region_c)
             t = plan_encode(inner, inner_spec, items, vstr, v.data_ptr())
-            launches.append(EncodeLaunch(t.layout, t.chunks, t.sels, v, dst, t.fast, self.device))
+            launches.append(EncodeLaunch(t.layout, t.chunks, t.sels, v, dst, t.fast, self.device, t.rows))
         if partial_items:
             tstr = [int(s) * itemsize for s in temp.stride()]
             base = len(complete_items)
@@ -299,7 +303,7 @@ class ChunkWriter:
             items = shard_items(src, lambda j, lo: list(lo), lambda j: list(shard_shape))
             t = plan_encode(inner, inner_spec, items, tstr[1:], temp.data_ptr())
             t.chunks["out_off"] += np.repeat(np.arange(len(partial_items)) * tstr[0], n_inner)
-            launches.append(EncodeLaunch(t.layout, t.chunks, t.sels, temp, dst, t.fast, self.device))
+            launches.append(EncodeLaunch(t.layout, t.chunks, t.sels, temp, dst, t.fast, self.device, t.rows))
         for l in launches:
             l.launch()
         # pack: one workgroup per shard over all launches' inner chunks
