@@ -229,6 +229,16 @@ class _EncodeProg:
         self.l = launch
 
     def launch(self, stream=None):
+        if os.environ.get("ZHIP_BENCH_ENC_NOZERO"):  # measurement: the encode kernel alone
+            from zarr_hip import _native as N
+            from zarr_hip.pipeline import _stream_handle
+            l = self.l
+            N.check(N.lib().zhip_encode_mapped(l.plan.handle, l.arr.data_ptr(), l.dst.data_ptr(),
+                                               l.d_chunks.data_ptr(), l.n, l.d_sels.data_ptr(),
+                                               l.d_status.data_ptr(), l.d_ws.data_ptr(), l.d_nonempty.data_ptr(),
+                                               l.flags, l.d_rowmap.data_ptr(),
+                                               _stream_handle(l.device) if stream is None else stream), "enc")
+            return
         self.l.launch(stream)
 
     def results(self):
@@ -265,7 +275,14 @@ def encode_c2(device, args):
         progs.append(_EncodeProg(EncodeLaunch(t.layout, t.chunks, t.sels, data, store.arena.buf, t.fast,
                                               device, t.rows)))
         checks.append((store, arr, batch, offs, elen))
+    enc_tune = int(os.environ.get("ZHIP_BENCH_ENC_TUNE", "0"))  # measurement-only ablations
+    if enc_tune:
+        from zarr_hip import _native as N
+        N.lib().zhip_set_tuning(2, enc_tune)
     wall, kern = time_programs(progs, max(10, args.steps // 2), 3, device)
+    if enc_tune:
+        N.lib().zhip_set_tuning(2, args.tune)
+        checks = []  # ablated results are not valid encodes
     for store, arr, batch, offs, elen in checks:
         for (bg, *_), off in zip(batch, offs):
             store.register(bg.path, off, elen)

@@ -157,3 +157,30 @@ def test_roundtrip_c2_like(device):
 def test_sharded_c4_like(device):
     _run(device, (128, 128, 128), (64, 64, 64), "float32", [SHARD((16, 16, 16), [LE, CRC])], 0.0,
          [((Ellipsis,), _data((128, 128, 128), "float32"))])
+
+
+# ---- k_encode_pair regular pairing (even units per chunk): non-empty flags and
+#      trailers written by the last arrival of each chunk
+
+@pytest.mark.parametrize("codecs", [[LE, CRC], [LE], [BE, CRC]])
+@pytest.mark.parametrize("fill", [0.0, np.nan])
+def test_encode_pair_elision_and_merges(device, codecs, fill):
+    shape, chunks = (32, 64, 128), (8, 64, 64)  # 128 KiB chunks: 4 units each
+    d = _data(shape, "float32")
+    d[0:8, :, 0:64] = fill        # one chunk entirely fill -> elided
+    d[16:24, :, 64:128] = fill    # another
+    w = [((Ellipsis,), d),
+         ((slice(8, 16), slice(None), slice(64, 128)), fill),             # a full chunk back to fill
+         ((slice(3, 29), slice(5, 60), slice(10, 100)), _data((26, 55, 90), "float32", 3))]
+    _run(device, shape, chunks, "float32", codecs, fill, w)
+    _run(device, shape, chunks, "float32", codecs, fill, w[:2], write_empty=True)
+
+
+def test_encode_pair_sharded_empty_inner(device):
+    shape = (32, 64, 64)
+    codecs = [SHARD((8, 64, 64), [LE, CRC])]   # 128 KiB inner chunks
+    d = _data(shape, "float32")
+    d[8:16] = 0.0
+    d[24:32] = 0.0
+    _run(device, shape, (16, 64, 64), "float32", codecs, 0.0,
+         [((Ellipsis,), d), ((slice(0, 8),), 0.0), ((slice(2, 30, 3), slice(1, 63)), 5.0)])

@@ -329,6 +329,39 @@ __device__ __forceinline__ void enc_run_end(const EncodeParams& p, const zhip_ch
     }
 }
 
+// Run end of a workgroup whose two units are pair `pr` of chunk c (regular
+// pairing, see k_encode_pair): word = CRC contribution | arrival bit of the
+// pair (bits 32..47) | non-empty bit of the pair (bits 48..63).  Each pair
+// sets its bits once per launch, so XOR accumulates them like OR.
+template <bool CRC>
+__device__ __forceinline__ void enc_run_end_pair(const EncodeParams& p, const zhip_chunk& ch, uint32_t c, uint32_t acc,
+                                                uint32_t klane, uint32_t pr, bool wave_ne, uint32_t* red, int t) {
+    uint32_t v = 0;
+    if constexpr (CRC) v = wave_xor(gf_mul(acc, klane));
+    if ((t & 63) == 0) red[t >> 6] = v | 0u;
+    __shared__ uint32_t s_ne[kThreads / 64];
+    if ((t & 63) == 0) s_ne[t >> 6] = wave_ne ? 1u : 0u;
+    __syncthreads();
+    if (t != 0) return;
+    const uint32_t V = CRC ? (red[0] ^ red[1] ^ red[2] ^ red[3]) : 0u;
+    const bool ne = (s_ne[0] | s_ne[1] | s_ne[2] | s_ne[3]) != 0u;
+    const uint64_t pb = 1ull << pr;
+    const uint64_t full = (1ull << (p.nseg >> 1)) - 1ull;
+    uint64_t* w = reinterpret_cast<uint64_t*>(p.ws) + 2ull * c;
+    const uint64_t word = (pb << 32) | (ne ? pb << 48 : 0ull) | V;
+    const uint64_t prev = __hip_atomic_fetch_xor(w, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((((prev >> 32) & 0xFFFFull) ^ pb) != full) return;
+    __hip_atomic_store(w, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    p.nonempty[c] = (((prev >> 48) ^ (ne ? pb : 0ull)) != 0ull) ? 1u : 0u;
+    uint32_t crc = 0;
+    if constexpr (CRC) {
+        crc = ~(((uint32_t)prev ^ V) ^ p.c3);  // kpair carries c_inv
+        put_le_u32(p.dst + ch.src + p.g.nbytes, crc);  // LE trailer (crc32c_.py:64-68)
+    }
+    zhip_status st = {ZHIP_ST_OK, crc, crc, 0u};
+    p.status[c] = st;
+}
+
 template <bool CRC, int ITEM, bool SWAP>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_encode_pair(const EncodeParams p) {
     constexpr int K = kDefaultBlocks;
@@ -392,9 +425,20 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
         eq_b = eq_a;
     }
     enc_unit<CRC, ITEM, SWAP>(p, chb, sb, has_b, mb, lane_row, B, s_tab, acc_b, eq_b, t);
+    // 3./4. regular pairing (an even number of units per chunk, at most 32): the
+    //    two units always share a chunk and the workgroup publishes CRC, its
+    //    pair's arrival bit and its pair's non-empty bit in ONE 64-bit atomic;
+    //    the last arrival writes trailer, status and the chunk's non-empty flag
+    //    (so the flags need no zeroing and no same-address atomic storm)
+    if (p.nseg % 2u == 0u && p.nseg <= 32u) {
+        enc_run_end_pair<CRC>(p, chb, cb, acc_b, kb, (p.nseg - 1u - sb) >> 1, __any(!eq_b), s_red[1], t);
+        return;
+    }
     // 3. chunk_is_empty (chunk_utils.py:74-85): any element != fill -> non-empty
-    if (!same && __any(!eq_a) && (t & 63) == 0) atomicOr(p.nonempty + ca, 1u);
-    if (has_b && __any(!eq_b) && (t & 63) == 0) atomicOr(p.nonempty + cb, 1u);
+    if (!(p.tune & kTuneEncNoFlags)) {  // (ablation: no flag atomics; results invalid)
+        if (!same && __any(!eq_a) && (t & 63) == 0) atomicOr(p.nonempty + ca, 1u);
+        if (has_b && __any(!eq_b) && (t & 63) == 0) atomicOr(p.nonempty + cb, 1u);
+    }
     // 4. run ends: A alone when B starts another chunk, then B (or A+B)
     if (!same) enc_run_end<CRC>(p, cha, ca, acc_a, ka, 1u << (sa & 31u), 1u, s_red[0], t);
     if (has_b)

@@ -65,13 +65,19 @@ class EncodeLaunch:
         self.flags = N.DF_FAST_ROWS if fast else 0
         # whole-row batches encode in k_encode_pair through the row map
         self.d_rowmap = _rows_map(self.plan, sels, device) if fast and rows else None
+        # k_encode_pair with an even number of units per chunk (<= 32) writes every
+        # chunk's non-empty flag itself (last arrival); otherwise flags are OR-ed
+        # into a zeroed array
+        upc = self.plan.units_per_chunk
+        self.flags_by_kernel = self.d_rowmap is not None and upc % 2 == 0 and upc <= 32
 
     def launch(self, stream: int | None = None) -> None:
         from .pipeline import _stream_handle
 
         if self.n == 0:
             return
-        self.d_nonempty.zero_()
+        if not self.flags_by_kernel:
+            self.d_nonempty.zero_()
         s = _stream_handle(self.device) if stream is None else stream
         N.check(N.lib().zhip_encode_mapped(self.plan.handle, self.arr.data_ptr(), self.dst.data_ptr(),
                                            self.d_chunks.data_ptr(), self.n, self.d_sels.data_ptr(),
