@@ -229,16 +229,6 @@ class _EncodeProg:
         self.l = launch
 
     def launch(self, stream=None):
-        if os.environ.get("ZHIP_BENCH_ENC_NOZERO"):  # measurement: the encode kernel alone
-            from zarr_hip import _native as N
-            from zarr_hip.pipeline import _stream_handle
-            l = self.l
-            N.check(N.lib().zhip_encode_mapped(l.plan.handle, l.arr.data_ptr(), l.dst.data_ptr(),
-                                               l.d_chunks.data_ptr(), l.n, l.d_sels.data_ptr(),
-                                               l.d_status.data_ptr(), l.d_ws.data_ptr(), l.d_nonempty.data_ptr(),
-                                               l.flags, l.d_rowmap.data_ptr(),
-                                               _stream_handle(l.device) if stream is None else stream), "enc")
-            return
         self.l.launch(stream)
 
     def results(self):
