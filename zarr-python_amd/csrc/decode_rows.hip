@@ -425,10 +425,7 @@ __device__ __forceinline__ void store_unit_rows(const DecodeParams& p, const Uni
     for (int k = 0; k < K; ++k) {
         const uint32_t lo = m.e[k].lo, hi = m.e[k].hi;
         const bool wr = writes && lane_row - lo < hi - lo;  // unsigned: lo <= lane_row < hi
-        uint8_t* const dst = wr ? base + m.e[k].rel + lane_off : sink;
-        const uint4 val = present ? swap_block<ITEM, SWAP>(blk[k]) : f;
-        if (p.tune & kTuneTemporalStores) *reinterpret_cast<uint4*>(dst) = val;  // ablation
-        else store_nt16(dst, val);
+        store_nt16(wr ? base + m.e[k].rel + lane_off : sink, present ? swap_block<ITEM, SWAP>(blk[k]) : f);
         if (crc) *acc = (p.tune & kTuneSkipCrc) ? *acc ^ blk[k].x ^ blk[k].y ^ blk[k].z ^ blk[k].w
                                                 : crc_block(s_tab, *acc, blk[k]);
     }

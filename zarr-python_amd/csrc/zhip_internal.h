@@ -102,7 +102,6 @@ constexpr uint32_t kTuneNoRunEnd = 4096u;  // k_decode_pair: skip the run-end re
 constexpr uint32_t kTuneNoBarrier = 8192u; // k_decode_pair: skip the table barrier (results invalid)
 constexpr uint32_t kTuneNoConsts = 32768u; // k_decode_pair: skip the lane-constant and trailer loads (results invalid)
 constexpr uint32_t kTuneTile1 = 65536u;  // transposed layouts: the one-tile persistent k_decode_tile
-constexpr uint32_t kTuneTemporalStores = 131072u; // k_decode_pair: plain (temporal) stores instead of nontemporal
 constexpr uint32_t kTuneSplitChain = 262144u; // k_decode_pair: independent Horner chains for the two units
 constexpr uint32_t kTuneEncNoFlags = 524288u; // k_encode_pair: skip the non-empty flag atomics (results invalid)
 constexpr uint32_t kTuneStamp = 1024u;    // k_decode_pair: per-workgroup phase timestamps (zhip_debug_stamps)
