@@ -500,7 +500,8 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
         const bool crc = (p.lflags & ZHIP_LF_CRC) != 0, swap = (p.lflags & ZHIP_LF_SWAP) != 0;
         KernelFn fn = nu != 2 ? nullptr
                       : (p.tune & kTuneTrailingCrc) ? select_pair_kernel(crc, p.g.itemsize, swap, 3)
-                      : (p.tune & kTuneSplitChain) ? select_pair_kernel(crc, p.g.itemsize, swap, 4) : nullptr;
+                      : (p.tune & kTuneSplitChain) ? select_pair_kernel(crc, p.g.itemsize, swap, 4)
+                      : (p.tune & kTuneSkipCrc) ? select_pair_kernel(crc, p.g.itemsize, swap, 5) : nullptr;
         if (!fn) fn = select_pair_kernel(crc, p.g.itemsize, swap, nu);
         if (!fn) return ZHIP_E_UNSUPPORTED;
         const uint32_t pairs = (uint32_t)(((uint64_t)p.n_units + nu - 1u) / nu);

@@ -411,7 +411,7 @@ __device__ __forceinline__ RowSteps load_row_steps(const DecodeParams& p, const 
 // Stores of one unit; with `crc` the Horner step of each block follows its
 // store (the lookups spread over the data's arrival instead of trailing it).
 // Destinations come from the row map: no per-step address arithmetic.
-template <int ITEM, bool SWAP, int K>
+template <int ITEM, bool SWAP, int K, bool SKIP = false>
 __device__ __forceinline__ void store_unit_rows(const DecodeParams& p, const Unit& U, const RowSteps& m, bool live,
                                                 uint32_t lane_row, int64_t lane_off, uint8_t* sink,
                                                 const uint4 (&blk)[K], bool crc = false,
@@ -426,8 +426,9 @@ __device__ __forceinline__ void store_unit_rows(const DecodeParams& p, const Uni
         const uint32_t lo = m.e[k].lo, hi = m.e[k].hi;
         const bool wr = writes && lane_row - lo < hi - lo;  // unsigned: lo <= lane_row < hi
         store_nt16(wr ? base + m.e[k].rel + lane_off : sink, present ? swap_block<ITEM, SWAP>(blk[k]) : f);
-        if (crc) *acc = (p.tune & kTuneSkipCrc) ? *acc ^ blk[k].x ^ blk[k].y ^ blk[k].z ^ blk[k].w
-                                                : crc_block(s_tab, *acc, blk[k]);
+        // (SKIP: ablation arm, lookups replaced by a plain xor; a compile-time
+        // choice -- a runtime test here doubles the loop's branches)
+        if (crc) *acc = SKIP ? *acc ^ blk[k].x ^ blk[k].y ^ blk[k].z ^ blk[k].w : crc_block(s_tab, *acc, blk[k]);
     }
 }
 
@@ -534,7 +535,8 @@ __device__ __forceinline__ void unit_status_pair(const DecodeParams& p, const Un
 }
 
 // VARIANT (tuning arms, headline item type only): 0 production, 1 every store
-// before the CRC lookups, 2 independent Horner chains for the two units
+// before the CRC lookups, 2 independent Horner chains for the two units, 3 no
+// CRC lookups (a plain xor; results invalid)
 template <bool CRC, int ITEM, bool SWAP, int NU, int K = 8, int VARIANT = 0>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(NU == 1 ? 8 : 4))) void k_decode_pair(const DecodeParams p) {
     // NU == 1: the lane shift is a VALU multiply (no 16 KiB s_mul), so that
@@ -645,15 +647,15 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(NU == 
         const uint32_t lane_col = (16u * (uint32_t)t) & ((1u << p.row_shift) - 1u);
         const int64_t lane_off = (int64_t)lane_row * p.r_oy + (int64_t)lane_col;
         const bool same = has_b && ub.c == ua.c;
-        constexpr bool TRAIL = VARIANT == 1, SPLIT = VARIANT == 2;
+        constexpr bool TRAIL = VARIANT == 1, SPLIT = VARIANT == 2, SKIP = VARIANT == 3;
         const bool ilv = CRC && !TRAIL;  // TRAIL (tuning): every store first, then the lookups
         uint32_t acc_a = 0, acc_b = 0;
-        store_unit_rows<ITEM, SWAP, K>(p, ua, ma, true, lane_row, lane_off, sink, A,
+        store_unit_rows<ITEM, SWAP, K, SKIP>(p, ua, ma, true, lane_row, lane_off, sink, A,
                                        ilv && ua.mode == ZHIP_ST_OK, s_tab, &acc_a);
         stamp(p, g, t, 3);
         if constexpr (NU == 2) {
             acc_b = (same && !SPLIT) ? acc_a : 0u;
-            store_unit_rows<ITEM, SWAP, K>(p, ub, mb, has_b, lane_row, lane_off, sink, B,
+            store_unit_rows<ITEM, SWAP, K, SKIP>(p, ub, mb, has_b, lane_row, lane_off, sink, B,
                                            ilv && has_b && ub.mode == ZHIP_ST_OK, s_tab, &acc_b);
         }
         if constexpr (CRC && TRAIL) {
@@ -711,9 +713,10 @@ KernelFn select_pair_nu(bool crc, int item, bool swap) {
 }
 
 KernelFn select_pair_kernel(bool crc, int item, bool swap, int nu) {
-    if (nu == 3 || nu == 4)  // tuning arms (headline item type only): VARIANT 1 / 2
+    if (nu >= 3 && nu <= 5)  // tuning arms (headline item type only): VARIANT 1 / 2 / 3
         return !(crc && item == 4 && !swap) ? nullptr
-               : nu == 3 ? k_decode_pair<true, 4, false, 2, 8, 1> : k_decode_pair<true, 4, false, 2, 8, 2>;
+               : nu == 3 ? k_decode_pair<true, 4, false, 2, 8, 1>
+               : nu == 4 ? k_decode_pair<true, 4, false, 2, 8, 2> : k_decode_pair<true, 4, false, 2, 8, 3>;
     return nu == 1 ? select_pair_nu<1>(crc, item, swap) : select_pair_nu<2>(crc, item, swap);
 }
 
