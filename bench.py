@@ -215,6 +215,8 @@ def extra_configs(device, args):
     if "enc" in args.extra:
         out["encode_c2"] = encode_c2(device, args)
         torch.cuda.empty_cache()
+        out["encode_c3"] = encode_c3(device, args)
+        torch.cuda.empty_cache()
     if "e2e" in args.extra:
         out["e2e_c2_host"] = e2e_host(device, args)
         torch.cuda.empty_cache()
@@ -233,6 +235,48 @@ class _EncodeProg:
 
     def results(self):
         return None
+
+
+def encode_c3(device, args):
+    """Encode side of C3: the 256^3 f32 array written through transpose(2,1,0) +
+    bytes + crc32c into 64 chunks of 64^3 by k_encode_tile4 (four LDS tiles
+    per workgroup), timed like encode_c2 and decoded back for the check."""
+    import torch
+
+    import zarr_hip
+    from zarr_hip import _native as N
+    from zarr_hip.planner import analyze_chain, plan_encode
+    from zarr_hip.writer import EncodeLaunch
+
+    shape, chunks = (256, 256, 256), (64, 64, 64)
+    codecs = [{"name": "transpose", "configuration": {"order": [2, 1, 0]}}, LE, CRC]
+    data = torch.from_numpy(synthetic(shape, seed=0)).to(device)
+    progs, checks = [], []
+    for _ in range(2):
+        store = zarr_hip.DeviceStore(device, capacity=64 * (1 << 20) + (1 << 20))
+        arr = zarr_hip.Array.create(store, shape, chunks, "float32", 0.0, codecs=codecs)
+        batch, _ = arr.batch_info((Ellipsis,))
+        spec = batch[0][1]
+        chain = analyze_chain(arr.codec_pipeline.codecs, spec)
+        elen = 64 ** 3 * 4 + 4
+        offs = [store.arena.reserve(elen) for _ in batch]
+        items = [(offs[i], it[2], [sl.start or 0 for sl in it[3]]) for i, it in enumerate(batch)]
+        t = plan_encode(chain, spec, items, [int(x) * 4 for x in data.stride()], data.data_ptr())
+        assert t.tile, "C3 encode should take the tiled encode"
+        el = EncodeLaunch(t.layout, t.chunks, t.sels, data, store.arena.buf, t.fast, device, t.rows, t.tile)
+        assert el.flags & N.DF_TILE
+        progs.append(_EncodeProg(el))
+        checks.append((store, arr, batch, offs, elen))
+    wall, kern = time_programs(progs, max(10, args.steps // 2), 3, device)
+    for store, arr, batch, offs, elen in checks:
+        for (bg, *_), off in zip(batch, offs):
+            store.register(bg.path, off, elen)
+        if not torch.equal(arr.get((Ellipsis,)).view(torch.int32), data.view(torch.int32)):
+            raise SystemExit("bench encode_c3: decoded store differs from the source")
+    src = data.numel() * 4
+    return _entry(src, src + 64 * (1048576 + 4), wall, kern,
+                  kernel="k_encode" if args.tune & 65536 else "k_encode_tile4",
+                  note="decoded_GiBps = source bytes encoded per second")
 
 
 def encode_c2(device, args):

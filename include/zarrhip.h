@@ -148,6 +148,8 @@ int zhip_plan_destroy(zhip_plan *plan);
 int zhip_plan_info(const zhip_plan *plan, uint32_t *units_per_chunk, uint32_t *workspace_words);
 /* Which specialised kernels the plan's layout admits (ZHIP_PK_* bits). */
 #define ZHIP_PK_TILE4 1u  /* transposed layout with full 64 x 256-byte tiles: k_decode_tile4 */
+#define ZHIP_PK_TILE4_ENCODE 2u  /* ... and at most 64 tiles per chunk: zhip_encode_mapped with
+                                    ZHIP_DF_TILE runs k_encode_tile4 (writes every non-empty flag) */
 int zhip_plan_kernel_flags(const zhip_plan *plan, uint32_t *flags);
 
 /* decode flags (zhip_decode decode_flags) */

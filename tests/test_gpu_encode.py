@@ -184,3 +184,44 @@ def test_encode_pair_sharded_empty_inner(device):
     d[24:32] = 0.0
     _run(device, shape, (16, 64, 64), "float32", codecs, 0.0,
          [((Ellipsis,), d), ((slice(0, 8),), 0.0), ((slice(2, 30, 3), slice(1, 63)), 5.0)])
+
+
+# ---- k_encode_tile4: transposed chunks with full 64-row x 256-byte tiles
+
+@pytest.mark.parametrize("dtype,endian,chunks,shape", [
+    ("float32", LE, (64, 64, 64), (128, 128, 64)),
+    ("float64", BE, (32, 16, 64), (64, 48, 128)),
+    ("int16", LE, (128, 8, 64), (256, 16, 64)),
+    ("uint8", LE, (256, 8, 64), (256, 24, 128)),
+])
+def test_encode_tile4(device, dtype, endian, chunks, shape):
+    from zarr_hip import _native as N
+    from zarr_hip.planner import _make_layout
+
+    codecs = [T((2, 1, 0)), endian, CRC]
+    d = _data(shape, dtype)
+    fill = 0
+    sl = tuple(slice(0, c) for c in chunks)  # one chunk entirely fill -> elided
+    d[sl] = fill
+    _run(device, shape, chunks, dtype, codecs, fill, [((Ellipsis,), d)])
+    # the layout qualifies for the four-tile encode
+    st = [chunks[p] for p in (2, 1, 0)]
+    it = np.dtype(dtype).itemsize
+    L = _make_layout(st, it, [it, shape[2] * it * 999, shape[2] * shape[1] * it], 0, b"\0")
+    assert N.Plan(L, upload=False).kernel_flags & N.PK_TILE4_ENCODE
+
+
+def test_encode_tile4_nan_fill_merges_and_no_crc(device):
+    shape, chunks = (128, 64, 128), (64, 64, 64)
+    d = _data(shape, "float32")
+    d[64:128, :, 0:64] = np.nan
+    w = [((Ellipsis,), d), ((slice(0, 64), slice(None), slice(64, 128)), np.nan),
+         ((slice(10, 100), slice(3, 60), slice(5, 120)), 2.5)]
+    _run(device, shape, chunks, "float32", [T((2, 1, 0)), LE, CRC], np.nan, w)
+    _run(device, shape, chunks, "float32", [T((2, 1, 0)), LE], np.nan, w[:2], write_empty=True)
+
+
+def test_encode_tile4_sharded_inner(device):
+    _run(device, (128, 128, 64), (128, 128, 64), "float32",
+         [SHARD((64, 64, 64), [T((2, 1, 0)), LE, CRC])], 0.0,
+         [((Ellipsis,), _data((128, 128, 64), "float32")), ((slice(0, 64), slice(64, 128)), 0.0)])

@@ -365,7 +365,7 @@ int zhip_plan_destroy(zhip_plan* p) {
 
 int zhip_plan_kernel_flags(const zhip_plan* p, uint32_t* flags) {
     if (!p || !flags) return set_err(ZHIP_E_INVALID, "null argument");
-    *flags = p->tile4 ? ZHIP_PK_TILE4 : 0u;
+    *flags = (p->tile4 ? ZHIP_PK_TILE4 : 0u) | (p->tile4 && p->t_per_chunk <= 64 ? ZHIP_PK_TILE4_ENCODE : 0u);
     return ZHIP_OK;
 }
 
@@ -637,6 +637,21 @@ int zhip_encode_mapped(const zhip_plan* plan, const void* arr, void* dst, const 
     p.fast = (encode_flags & ZHIP_DF_FAST_ROWS) ? 1u : 0u;
     p.tune = g_tune_bits;
     p.rowmap = nullptr;
+    p.tile4 = 0;
+    if ((encode_flags & ZHIP_DF_TILE) && plan->tile4 && plan->t_per_chunk <= 64 && plan->d_tile_tables &&
+        !(g_tune_bits & kTuneTile1)) {
+        // transposed chunks, full tiles, at most 16 workgroups per chunk (the
+        // arrival / non-empty bits of one 64-bit word): k_encode_tile4
+        p.tile4 = 1;
+        p.tq = plan->tq;
+        p.t_per_chunk = plan->t_per_chunk;
+        for (int d = 0; d < ZHIP_MAX_DIMS; ++d) p.sstride[d] = plan->sstride[d];
+        p.horner = plan->d_tile_tables;
+        p.tz = plan->d_tile_tables + plan->tile4_off_tz;
+        p.kq4 = plan->d_tile_tables + plan->tile4_off_kq;
+        p.tmap = reinterpret_cast<const TileEnt*>(plan->d_tile_tables + plan->tile4_off_map);
+        d_rowmap = nullptr;
+    }
     if (d_rowmap) {
         const uint32_t rb = plan->row_bytes;
         const int nd = L.ndim;

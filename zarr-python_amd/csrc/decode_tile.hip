@@ -42,6 +42,37 @@ __device__ __forceinline__ uint4 load_nt16_a1(const uint8_t* a) {  // any alignm
     return make_uint4(w.x, w.y, w.z, w.w);
 }
 
+typedef __attribute__((address_space(1))) zhip_v4u_a1t zhip_gv4u_a1tw;
+
+__device__ __forceinline__ void store_nt16_a1(uint8_t* a, uint4 v) {  // any alignment, one dwordx4 nt
+    zhip_v4u_a1t w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, (zhip_gv4u_a1tw*)(reinterpret_cast<uintptr_t>(a)));
+}
+
+// NDBuffer.all_equal against the fill (buffer/core.py:534-558): bitwise, except
+// that any NaN equals a NaN fill; 16 native-order bytes.
+template <int ITEM>
+__device__ __forceinline__ bool block_eq_fill_e(uint4 v, const EncodeParams& p) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    bool all = true;
+#pragma unroll
+    for (int j = 0; j < 16 / ITEM; ++j) {
+        if constexpr (ITEM == 8) {
+            const uint64_t x = ((uint64_t)w[2 * j + 1] << 32) | w[2 * j];
+            const bool e = w[2 * j] == p.fill[0] && w[2 * j + 1] == p.fill[1];
+            all = all && (e || (p.fill_nan && (x & 0x7FFFFFFFFFFFFFFFull) > 0x7FF0000000000000ull));
+        } else {
+            constexpr uint32_t m = ITEM == 4 ? 0xFFFFFFFFu : ((1u << (8 * ITEM)) - 1u);
+            const uint32_t x = (w[(j * ITEM) / 4] >> (8 * ((j * ITEM) % 4))) & m;
+            bool e = x == (p.fill[0] & m);
+            if constexpr (ITEM == 4) e = e || (p.fill_nan && (x & 0x7FFFFFFFu) > 0x7F800000u);
+            if constexpr (ITEM == 2) e = e || (p.fill_nan && (x & 0x7FFFu) > 0x7C00u);
+            all = all && e;
+        }
+    }
+    return all;
+}
+
 struct TileMap4 {
     TileEnt e[kTiles];
 };
@@ -219,7 +250,160 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     }
 }
 
+// k_encode_tile4: the same four tiles per workgroup in reverse (TransposeCodec
+// _encode_sync, transpose.py:113-118): 16-byte pieces of the source array's
+// out-contiguous rows are gathered (all 16 per thread issued first), written
+// into the LDS image at their transposed place, read back in stored order,
+// fill-tested, byteswapped, stored as whole 256-byte rows of the stored chunk
+// and run through the tile's Horner steps.  One 64-bit atomic per workgroup
+// carries CRC | tile-group arrival | tile-group non-empty bits (at most 16
+// workgroups per chunk); the last arrival writes trailer, status and the
+// chunk's non-empty flag.
+template <bool CRC, int ITEM, bool SWAP>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_encode_tile4(
+    const EncodeParams p) {
+    constexpr int kPitch = ITEM == 8 ? 264 : 260;
+    constexpr int kPer = 16 / ITEM;
+    constexpr int kPiecesPerCol = kTileRows / kPer;
+    __shared__ uint32_t s_tab[CRC ? 16 * 256 : 1];
+    __shared__ uint32_t s_tz[CRC ? 1024 : 1];
+    __shared__ __attribute__((aligned(16))) uint8_t s_tile[kTileRows * kPitch];
+    __shared__ uint32_t s_red[kThreads / 64];
+    __shared__ uint32_t s_ne[kThreads / 64];
+    const int t = threadIdx.x;
+    const uint32_t g = blockIdx.x;
+    const uint32_t gpc = p.t_per_chunk / kTiles;
+    const uint32_t c = g / gpc;
+    const uint32_t grp = g - c * gpc;
+    uint4 tv0, tv1, tv2, tv3, tzv;
+    uint32_t kq = 0;
+    if constexpr (CRC) {
+        const uint4* gt = reinterpret_cast<const uint4*>(p.horner);
+        tv0 = gt[t];
+        tv1 = gt[t + kThreads];
+        tv2 = gt[t + 2 * kThreads];
+        tv3 = gt[t + 3 * kThreads];
+        tzv = reinterpret_cast<const uint4*>(p.tz)[t];
+        kq = p.kq4[(size_t)grp * kThreads + t];
+    }
+    const zhip_chunk ch = load_uniform<zhip_chunk>(p.chunks + c);  // src: dst offset, out_off: source offset
+    const TileMap4 tm = load_uniform<TileMap4>(p.tmap + (size_t)grp * kTiles);
+    const int32_t last = p.g.ndim - 1;
+    const int64_t oq = p.g.ostride[p.tq];    // == ITEM (source stride of the out-contiguous dim)
+    const int64_t ocol = p.g.ostride[last];  // source stride of the innermost stored dim
+    const uint8_t* const abase = p.arr + ch.out_off;
+    uint8_t* const cp = p.dst + ch.src;
+    const uint32_t sq = p.sstride[p.tq];
+    const uint32_t row0 = (uint32_t)t >> 4, col = 16u * (uint32_t)(t & 15);
+    // 1. gather every piece of the four tiles
+    uint4 pcs[kTiles][kPasses];
+#pragma unroll
+    for (int j = 0; j < kTiles; ++j)
+#pragma unroll
+        for (int k = 0; k < kPasses; ++k) {
+            const uint32_t pc = (uint32_t)(k * kThreads + t);
+            const uint32_t jc = pc / kPiecesPerCol;
+            const uint32_t r0 = (pc % kPiecesPerCol) * kPer;
+            pcs[j][k] = load_nt16_a1(abase + tm.e[j].orel + (int64_t)jc * ocol + (int64_t)r0 * oq);
+        }
+    if constexpr (CRC) {
+        uint4* st = reinterpret_cast<uint4*>(s_tab);
+        st[t] = tv0;
+        st[t + kThreads] = tv1;
+        st[t + 2 * kThreads] = tv2;
+        st[t + 3 * kThreads] = tv3;
+        reinterpret_cast<uint4*>(s_tz)[t] = tzv;
+    }
+    uint32_t S = 0;
+    bool eq = true;
+#pragma unroll
+    for (int j = 0; j < kTiles; ++j) {
+        if (j > 0) __syncthreads();  // the previous tile's LDS reads are done
+        // 2. pieces into the LDS image at their stored (row, column) place
+#pragma unroll
+        for (int k = 0; k < kPasses; ++k) {
+            const uint32_t pc = (uint32_t)(k * kThreads + t);
+            const uint32_t jc = pc / kPiecesPerCol;
+            const uint32_t r0 = (pc % kPiecesPerCol) * kPer;
+            const uint32_t w[4] = {pcs[j][k].x, pcs[j][k].y, pcs[j][k].z, pcs[j][k].w};
+#pragma unroll
+            for (int e = 0; e < kPer; ++e) {
+                uint8_t* dst = s_tile + (r0 + e) * kPitch + jc * ITEM;
+                if constexpr (ITEM == 8) {
+                    *reinterpret_cast<uint2*>(dst) = make_uint2(w[2 * e], w[2 * e + 1]);
+                } else if constexpr (ITEM == 4) {
+                    *reinterpret_cast<uint32_t*>(dst) = w[e];
+                } else if constexpr (ITEM == 2) {
+                    *reinterpret_cast<uint16_t*>(dst) = (uint16_t)(w[e / 2] >> (16 * (e & 1)));
+                } else {
+                    *dst = (uint8_t)(w[e / 4] >> (8 * (e & 3)));
+                }
+            }
+        }
+        __syncthreads();  // tile j (and, first time, the tables) in LDS
+        // 3. stored-order blocks: fill test, byteswap, store, Horner steps
+        uint32_t acc = 0;
+#pragma unroll
+        for (int k = 0; k < kPasses; ++k) {
+            const uint32_t* sv = reinterpret_cast<const uint32_t*>(s_tile + (16 * k + row0) * kPitch + col);
+            const uint4 v = make_uint4(sv[0], sv[1], sv[2], sv[3]);
+            eq = eq && block_eq_fill_e<ITEM>(v, p);
+            const uint4 e = swap_block<ITEM, SWAP>(v);
+            store_nt16_a1(cp + tm.e[j].tbase + (row0 + 16u * k) * sq + col, e);
+            if constexpr (CRC)
+                acc = tab_apply(s_tab, acc ^ e.x) ^ tab_apply(s_tab + 1024, e.y) ^ tab_apply(s_tab + 2048, e.z) ^
+                      tab_apply(s_tab + 3072, e.w);
+        }
+        if constexpr (CRC) S = (j == 0 ? 0u : tab_apply(s_tz, S)) ^ acc;
+    }
+    // 4. run end
+    uint32_t v = 0;
+    if constexpr (CRC) v = wave_xor(gf_mul(S, kq));
+    const bool wne = __any(!eq);
+    if ((t & 63) == 0) {
+        s_red[t >> 6] = v;
+        s_ne[t >> 6] = wne ? 1u : 0u;
+    }
+    __syncthreads();
+    if (t != 0) return;
+    const uint32_t V = CRC ? (s_red[0] ^ s_red[1] ^ s_red[2] ^ s_red[3]) : 0u;
+    const bool ne = (s_ne[0] | s_ne[1] | s_ne[2] | s_ne[3]) != 0u;
+    const uint64_t pb = 1ull << grp;
+    const uint64_t full = (1ull << gpc) - 1ull;
+    uint64_t* w = reinterpret_cast<uint64_t*>(p.ws) + 2ull * c;
+    const uint64_t prev = __hip_atomic_fetch_xor(w, (pb << 32) | (ne ? pb << 48 : 0ull) | V, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+    if ((((prev >> 32) & 0xFFFFull) ^ pb) != full) return;
+    __hip_atomic_store(w, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    p.nonempty[c] = (((prev >> 48) ^ (ne ? pb : 0ull)) != 0ull) ? 1u : 0u;
+    uint32_t crc = 0;
+    if constexpr (CRC) {
+        crc = ~(((uint32_t)prev ^ V) ^ p.c3);  // kq4 carries t_c_inv
+        uint8_t* tr = cp + p.g.nbytes;  // LE trailer (crc32c_.py:64-68)
+        tr[0] = (uint8_t)crc;
+        tr[1] = (uint8_t)(crc >> 8);
+        tr[2] = (uint8_t)(crc >> 16);
+        tr[3] = (uint8_t)(crc >> 24);
+    }
+    zhip_status st = {ZHIP_ST_OK, crc, crc, 0u};
+    p.status[c] = st;
+}
+
 using KernelFn = void (*)(const DecodeParams);
+using EncodeFn = void (*)(const EncodeParams);
+
+EncodeFn select_encode_tile4_kernel(bool crc, int item, bool swap) {
+    switch (item) {
+        case 1: return crc ? k_encode_tile4<true, 1, false> : k_encode_tile4<false, 1, false>;
+        case 2: return crc ? (swap ? k_encode_tile4<true, 2, true> : k_encode_tile4<true, 2, false>)
+                           : (swap ? k_encode_tile4<false, 2, true> : k_encode_tile4<false, 2, false>);
+        case 4: return crc ? (swap ? k_encode_tile4<true, 4, true> : k_encode_tile4<true, 4, false>)
+                           : (swap ? k_encode_tile4<false, 4, true> : k_encode_tile4<false, 4, false>);
+        case 8: return crc ? (swap ? k_encode_tile4<true, 8, true> : k_encode_tile4<true, 8, false>)
+                           : (swap ? k_encode_tile4<false, 8, true> : k_encode_tile4<false, 8, false>);
+        default: return nullptr;
+    }
+}
 
 KernelFn select_tile4_kernel(bool crc, int item, bool swap) {
     switch (item) {

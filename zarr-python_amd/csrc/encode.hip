@@ -472,9 +472,18 @@ static EncodeFn pick_encode_pair(bool crc, int item, bool swap) {
     }
 }
 
+EncodeFn select_encode_tile4_kernel(bool crc, int item, bool swap);  // decode_tile.hip
+
 int launch_encode(const EncodeParams& p, hipStream_t stream, int max_grid) {
     const bool crc = (p.lflags & ZHIP_LF_CRC) != 0;
     const bool swap = (p.lflags & ZHIP_LF_SWAP) != 0;
+    if (p.tile4) {  // transposed layouts with full tiles (k_encode_tile4)
+        EncodeFn fn = select_encode_tile4_kernel(crc, p.g.itemsize, swap);
+        if (!fn) return ZHIP_E_UNSUPPORTED;
+        if (p.n_chunks == 0) return ZHIP_OK;
+        hipLaunchKernelGGL(fn, dim3(p.n_chunks * (p.t_per_chunk / 4u)), dim3(kThreads), 0, stream, p);
+        return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
+    }
     if (p.rowmap && p.seg == (uint32_t)kWgStride * kDefaultBlocks && !(p.tune & kTunePersist)) {
         EncodeFn fn = pick_encode_pair(crc, p.g.itemsize, swap);
         if (!fn) return ZHIP_E_UNSUPPORTED;

@@ -137,6 +137,13 @@ struct EncodeParams {
     uint32_t row_shift;
     int64_t r_oy;
     uint32_t tune;
+    // k_encode_tile4 (ZHIP_DF_TILE on a tile4 plan): see zhip_plan / k_decode_tile4
+    int32_t tq;
+    uint32_t t_per_chunk, tile4;
+    uint32_t sstride[ZHIP_MAX_DIMS];
+    const uint32_t* tz;
+    const uint32_t* kq4;
+    const struct TileEnt* tmap;
 };
 
 struct PackParams {

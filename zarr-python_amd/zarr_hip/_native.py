@@ -38,6 +38,7 @@ DF_TILE = 2
 DF_ROWS = 4
 
 PK_TILE4 = 1
+PK_TILE4_ENCODE = 2
 
 PF_INDEX_START = 1
 PF_INDEX_CRC = 2

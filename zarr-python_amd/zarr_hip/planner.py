@@ -254,7 +254,8 @@ def plan_encode(chain: ChainInfo, spec: ArraySpec, items: list, arr_strides_byte
     chunks["sel"] = inv
     fast = _fast_ok(layout, start, count, step, chunks["out_off"], arr_base_ptr)
     rows = fast and _rows_ok(layout, count, step)
-    return Tables(layout, chunks, sels, fast, np.arange(n), rows=rows)
+    tile = not fast and _tile_ok(layout, start, count, step, chunks["out_off"], arr_base_ptr)
+    return Tables(layout, chunks, sels, fast, np.arange(n), rows=rows, tile=tile)
 
 
 def plan_decode(chain: ChainInfo, spec: ArraySpec, items: list, out_strides_bytes,

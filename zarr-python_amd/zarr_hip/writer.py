@@ -48,7 +48,7 @@ class EncodeLaunch:
     """One zhip_encode launch over flat chunk tables."""
 
     def __init__(self, layout: N.Layout, chunks: np.ndarray, sels: np.ndarray, arr, dst, fast: bool,
-                 device, rows: bool = False):
+                 device, rows: bool = False, tile: bool = False):
         from .pipeline import _rows_map, get_plan
 
         torch = _torch()
@@ -70,6 +70,10 @@ class EncodeLaunch:
         # into a zeroed array
         upc = self.plan.units_per_chunk
         self.flags_by_kernel = self.d_rowmap is not None and upc % 2 == 0 and upc <= 32
+        # transposed layouts with full tiles: k_encode_tile4 (also writes every flag)
+        if tile and not fast and self.plan.kernel_flags & N.PK_TILE4_ENCODE:
+            self.flags |= N.DF_TILE
+            self.flags_by_kernel = True
 
     def launch(self, stream: int | None = None) -> None:
         from .pipeline import _stream_handle
@@ -199,7 +203,7 @@ class ChunkWriter:
             for i, (bs, sp, csel, osel, _) in enumerate(complete_items):
                 items.append((offs[i], csel, [s.start or 0 for s in osel]))
             t = plan_encode(chain, spec, items, vstr, v.data_ptr())
-            launches.append((EncodeLaunch(t.layout, t.chunks, t.sels, v, dst, t.fast, self.device, t.rows),
+            launches.append((EncodeLaunch(t.layout, t.chunks, t.sels, v, dst, t.fast, self.device, t.rows, t.tile),
                              list(range(len(complete_items)))))
         if partial_items:
             tstr = [int(s) * itemsize for s in temp.stride()]
@@ -211,7 +215,7 @@ class ChunkWriter:
             t = plan_encode(chain, spec, items, tstr[1:], temp.data_ptr())
             # the leading temp index goes into out_off
             t.chunks["out_off"] = np.arange(len(partial_items)) * tstr[0]
-            launches.append((EncodeLaunch(t.layout, t.chunks, t.sels, temp, dst, t.fast, self.device, t.rows),
+            launches.append((EncodeLaunch(t.layout, t.chunks, t.sels, temp, dst, t.fast, self.device, t.rows, t.tile),
                              [base + i for i in range(len(partial_items))]))
         for l, _ in launches:
             l.launch()
@@ -301,7 +305,7 @@ class ChunkWriter:
 
             items = shard_items(src, astart_c, region_c)
             t = plan_encode(inner, inner_spec, items, vstr, v.data_ptr())
-            launches.append(EncodeLaunch(t.layout, t.chunks, t.sels, v, dst, t.fast, self.device, t.rows))
+            launches.append(EncodeLaunch(t.layout, t.chunks, t.sels, v, dst, t.fast, self.device, t.rows, t.tile))
         if partial_items:
             tstr = [int(s) * itemsize for s in temp.stride()]
             base = len(complete_items)
@@ -309,7 +313,7 @@ class ChunkWriter:
             items = shard_items(src, lambda j, lo: list(lo), lambda j: list(shard_shape))
             t = plan_encode(inner, inner_spec, items, tstr[1:], temp.data_ptr())
             t.chunks["out_off"] += np.repeat(np.arange(len(partial_items)) * tstr[0], n_inner)
-            launches.append(EncodeLaunch(t.layout, t.chunks, t.sels, temp, dst, t.fast, self.device, t.rows))
+            launches.append(EncodeLaunch(t.layout, t.chunks, t.sels, temp, dst, t.fast, self.device, t.rows, t.tile))
         for l in launches:
             l.launch()
         # pack: one workgroup per shard over all launches' inner chunks
