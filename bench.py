@@ -3,17 +3,25 @@
 
   python bench.py --gpus N --steps K --warmup W
 
-Workload (BASELINE.json configs[1], "C2"): a 256^3 float32 array in 64^3 chunks,
-codecs [bytes(little), crc32c], every encoded chunk resident in HBM; one step =
-one full-array decode (CRC verify + scatter of all 64 chunks) by the HIP
-kernel.  Synthetic data: seed 0 standard normal with planted NaN payload and
--0.0.  To keep the measurement an HBM measurement (the 256 MiB Infinity Cache
-would otherwise hold the 128 MiB working set), steps rotate over 4 independent
-replicas (inputs + outputs), 512 MiB in total.
+Headline workload (BASELINE.json metric: "sharded 256^3 f32 64^3 chunks"): a
+256^3 float32 array in 128^3 shards of 64^3 inner chunks, inner codecs
+bytes(little)+crc32c, index bytes+crc32c at the end, every encoded shard
+resident in HBM; one step = one full-array decode (CRC verify of 64 inner
+chunks and 8 shard indexes + scatter) by one HIP launch.  Synthetic data: seed
+0 standard normal with a planted NaN payload and -0.0.  To keep it an HBM
+measurement (the 256 MiB Infinity Cache would otherwise hold the 128 MiB
+working set) steps rotate over 4 independent replicas (inputs + outputs).
 
-Multi-GPU (weak scaling): one process per GPU (torchrun), each decoding its own
-replica set; chunks are independent so there is no collective on the data
-path — RCCL only carries the timing barrier and the max-over-ranks reduction.
+Multi-GPU (one process per GPU, torchrun): chunks are independent, so ONE batch
+is partitioned across the ranks with no collective on the data path (the
+reference's disjoint-output pool map, src/zarr/core/codec_pipeline.py:
+1104-1109, 1169-1171).  The headline's global batch at N ranks is the
+(256N) x 256 x 256 array (8N shards), split round-robin by shard
+(zarr_hip.parallel.rank_batch): every rank stages and decodes only its own 8
+shards, so per-GPU work is fixed (weak scaling) and N=1 is exactly the
+headline.  The C4 (1024^3) and C5 (2048^3, 10 % inner chunks) legs split their
+fixed batch round-robin by shard (strong scaling).  RCCL carries only the
+barrier and the max-over-ranks of the timed wall.
 
 Prints ONE JSON line (rank 0) with the driver's contract fields plus
 "roofline" (dominant kernel vs 8 TB/s HBM, per-launch kernel time from HIP
@@ -36,11 +44,17 @@ for p in (ROOT, os.path.join(ROOT, "zarr-python_amd")):
     if p not in sys.path:
         sys.path.insert(0, p)
 
+import workloads as W  # noqa: E402
+
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # per-launch HBM bytes of the headline kernel from separate rocprofv3 --pmc passes
-# of this same command (scripts/gpu_pmc.sh -> scripts/pmc_summary.py)
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json")
+# of this same command (scripts/gpu_pmc.sh -> scripts/pmc_summary.py); counters
+# cannot be read from inside the timed process, so the value is labelled with
+# the file it comes from
+TRAFFIC_JSON = os.path.join("profiles", "r02", "pmc_traffic.json")
 GIB = float(1 << 30)
+LE, CRC = W.LE, W.CRC
+synthetic = W.synthetic
 
 
 def log(*a):
@@ -48,17 +62,55 @@ def log(*a):
         print(*a, file=sys.stderr, flush=True)
 
 
-def synthetic(shape, seed=0):
-    rng = np.random.default_rng(seed)
-    a = rng.standard_normal(shape, dtype=np.float32)
-    flat = a.reshape(-1)
-    flat[7] = -0.0
-    flat[11:12].view(np.uint32)[0] = 0x7FC00001
-    return a
+class Ctx:
+    """Rank / device / process-group context of one bench process."""
 
+    def __init__(self):
+        import torch
+        import torch.distributed as dist
 
-LE = {"name": "bytes", "configuration": {"endian": "little"}}
-CRC = {"name": "crc32c"}
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        # launched by torchrun (even with one rank): use the process group for the
+        # barrier / max-over-ranks timing so the N>1 code path is the one exercised
+        self.distributed = "RANK" in os.environ and "MASTER_ADDR" in os.environ
+        self.rank = int(os.environ.get("RANK", "0"))
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        # rehearsal of the N>1 path on a one-GPU box: every rank on device 0 with
+        # a gloo group (RCCL refuses two ranks on one device).  Never the driver's
+        # configuration: the numbers of such a run are not a scaling measurement.
+        self.rehearsal = os.environ.get("ZHIP_BENCH_REHEARSAL") == "1"
+        backend = "gloo" if self.rehearsal else "nccl"
+        if self.rehearsal:
+            local = 0
+        if self.distributed:
+            torch.cuda.set_device(local)
+            if backend == "nccl":
+                dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            else:
+                dist.init_process_group("gloo")
+        self.device = torch.device("cuda", local)
+        torch.cuda.set_device(self.device)
+        self.dist = dist
+        self._red_dev = torch.device("cpu") if self.rehearsal else self.device
+
+    def barrier(self):
+        if self.distributed:
+            self.dist.barrier()
+
+    def _reduce(self, x: float, op) -> float:
+        import torch
+
+        if not self.distributed:
+            return float(x)
+        t = torch.tensor([float(x)], dtype=torch.float64, device=self._red_dev)
+        self.dist.all_reduce(t, op=op)
+        return float(t.item())
+
+    def max(self, x: float) -> float:
+        return self._reduce(x, self.dist.ReduceOp.MAX)
+
+    def sum(self, x: float) -> float:
+        return self._reduce(x, self.dist.ReduceOp.SUM)
 
 
 def build_replica(device, data_dev, shape, chunks, codecs, shards=None):
@@ -80,10 +132,38 @@ def build_replica(device, data_dev, shape, chunks, codecs, shards=None):
     return arr
 
 
-def build_c2_replica(device, data_np, shape, chunks):
+def build_partitioned(ctx, src, shape, inner, shards, dtype, fill, capacity):
+    """One replica of a sharded array whose batch is split round-robin by shard:
+    this rank encodes only its own shards (from the full-shape device source)
+    into its own DeviceStore and plans the decode of exactly those shards into a
+    full-shape out.  Returns (program, out, my batch items)."""
     import torch
 
-    return build_replica(device, torch.from_numpy(data_np).to(device), shape, chunks, [LE, CRC])
+    import zarr_hip
+    from zarr_hip import buffer, parallel
+
+    store = zarr_hip.DeviceStore(ctx.device, capacity=int(capacity))
+    arr = zarr_hip.Array.create(store, shape, inner, dtype, fill, shards=shards,
+                                inner_codecs=[LE, CRC])
+    batch, out_shape = arr.batch_info((Ellipsis,))
+    mine = parallel.rank_batch(batch, ctx.world, ctx.rank)
+    arr.codec_pipeline.write_sync(mine, src)
+    out = buffer.empty(out_shape, dtype, ctx.device)
+    prog = arr.codec_pipeline.prepare_read(mine, out)
+    torch.cuda.synchronize(ctx.device)
+    return prog, out, mine
+
+
+def check_regions(out, src, items, what):
+    """Byte-compare every owned out region with the source (int views: NaN
+    payloads and -0.0 count)."""
+    import torch
+
+    iv = {1: torch.uint8, 2: torch.int16, 4: torch.int32, 8: torch.int64}[out.element_size()]
+    for it in items:
+        osel = tuple(it[3])
+        if not torch.equal(out[osel].view(iv), src[osel].view(iv)):
+            raise SystemExit(f"bench {what}: decoded bytes differ from the source in {osel}")
 
 
 def eager_kernel_times(progs, steps, device):
@@ -104,11 +184,11 @@ def eager_kernel_times(progs, steps, device):
     return [a.elapsed_time(b) / 1e3 for a, b in ev]
 
 
-def graph_steps(progs, steps, warmup, device, barrier=None):
+def graph_steps(progs, steps, warmup, device, ctx=None):
     """The timed region: ``steps`` full decodes rotating over the programs,
     captured once as a hipGraph (zarr_hip.ReadGraph) and replayed with one
-    launch, bracketed by barrier + synchronize.  Returns (wall seconds,
-    event span on the launch stream in seconds)."""
+    launch, bracketed by barrier + synchronize.  Returns (this rank's wall
+    seconds, max over ranks, event span on the launch stream in seconds)."""
     import torch
 
     import zarr_hip
@@ -118,8 +198,8 @@ def graph_steps(progs, steps, warmup, device, barrier=None):
     g_warm.replay()
     stream = torch.cuda.current_stream(device)
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    if barrier is not None:
-        barrier()
+    if ctx is not None:
+        ctx.barrier()
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
     a.record(stream)
@@ -127,21 +207,22 @@ def graph_steps(progs, steps, warmup, device, barrier=None):
     b.record(stream)
     torch.cuda.synchronize(device)
     wall = time.perf_counter() - t0
-    if barrier is not None:
-        barrier()
+    if ctx is not None:
+        ctx.barrier()
     for p in progs:
         p.results()  # raises on any CRC / status error accumulated during the run
-    return wall, a.elapsed_time(b) / 1e3
+    wall_max = ctx.max(wall) if ctx is not None else wall
+    return wall, wall_max, a.elapsed_time(b) / 1e3
 
 
-def time_programs(progs, steps, warmup, device):
-    """(wall seconds per step of the graph-replayed loop, median eager per-launch
-    kernel seconds)."""
-    wall, _ = graph_steps(progs, steps, warmup, device)
+def time_programs(progs, steps, warmup, device, ctx=None):
+    """(max-over-ranks wall seconds per step of the graph-replayed loop, median
+    eager per-launch kernel seconds of this rank)."""
+    _, wall_max, _ = graph_steps(progs, steps, warmup, device, ctx)
     kern = eager_kernel_times(progs, steps, device)
     for p in progs:
         p.results()
-    return wall / steps, float(np.median(kern))
+    return wall_max / steps, float(np.median(kern))
 
 
 def _entry(dec, alg, wall, kern, **kw):
@@ -152,75 +233,162 @@ def _entry(dec, alg, wall, kern, **kw):
     return d
 
 
-def extra_configs(device, args):
-    """Configs measured beside the headline at N=1 (BASELINE.json configs[1..4]
-    plus the host-memory end-to-end rate)."""
+# --------------------------------------------------------------------- configs
+
+def extra_configs(ctx, args):
+    """Configs measured beside the headline: BASELINE.json configs[0..4] plus the
+    host-memory end-to-end rate.  C4 and C5 run at every N (partitioned); the
+    single-GPU configs only at N=1."""
     import torch
 
-    import zarr_hip
-
+    device = ctx.device
     out = {}
     steps = max(10, args.steps // 2)
-    if "c1" in args.extra:
+    single = ctx.world == 1
+    if single and "c1" in args.extra:
         out["c1_1d_bytes"] = c1_plumbing(device, args)
         torch.cuda.empty_cache()
     shape, chunks = (256, 256, 256), (64, 64, 64)
-    if "c2" in args.extra:
+    if single and "c2" in args.extra:
         # BASELINE configs[1]: the same array unsharded (64 chunks of 64^3)
         data = torch.from_numpy(synthetic(shape, seed=0)).to(device)
-        progs = [build_replica(device, data, shape, chunks, [LE, CRC]).prepare_read((Ellipsis,))[0]
-                 for _ in range(args.replicas)]
-        progs[0].launch()
-        progs[0].results()
-        wall, kern = time_programs(progs, steps, 3, device)
+        progs = []
+        for _ in range(args.replicas):
+            p, o = build_replica(device, data, shape, chunks, [LE, CRC]).prepare_read((Ellipsis,))
+            progs.append((p, o))
+        progs[0][0].launch()
+        progs[0][0].results()
+        if not torch.equal(progs[0][1].view(torch.int32), data.view(torch.int32)):
+            raise SystemExit("bench c2: decoded bytes differ from the source")
+        wall, kern = time_programs([p for p, _ in progs], steps, 3, device)
         dec = data.numel() * 4
-        out["c2_unsharded_256"] = _entry(dec, dec + 64 * (1048576 + 4), wall, kern)
+        out["c2_unsharded_256"] = _entry(dec, dec + 64 * (1048576 + 4), wall, kern, checked="bytes")
         del progs, data
-    if "c3" in args.extra:
+    if single and "c3" in args.extra:
         data = torch.from_numpy(synthetic(shape, seed=0)).to(device)
         progs = []
         for _ in range(args.replicas):
             arr = build_replica(device, data, shape, chunks,
                                 [{"name": "transpose", "configuration": {"order": [2, 1, 0]}}, LE, CRC])
-            progs.append(arr.prepare_read((Ellipsis,))[0])
-        assert progs[0].tables.tile, "C3 should take the LDS-tiled transpose kernel"
+            progs.append(arr.prepare_read((Ellipsis,)))
+        assert progs[0][0].tables.tile, "C3 should take the LDS-tiled transpose kernel"
+        progs[0][0].launch()
+        progs[0][0].results()
+        if not torch.equal(progs[0][1].view(torch.int32), data.view(torch.int32)):
+            raise SystemExit("bench c3: decoded bytes differ from the source")
         from zarr_hip import _native as N
-        tile4 = bool(N.Plan(progs[0].tables.layout, upload=False).kernel_flags & N.PK_TILE4) and \
+        tile4 = bool(N.Plan(progs[0][0].tables.layout, upload=False).kernel_flags & N.PK_TILE4) and \
             not (args.tune & 65536)
-        wall, kern = time_programs(progs, steps, 3, device)
+        wall, kern = time_programs([p for p, _ in progs], steps, 3, device)
         dec = data.numel() * 4
         out["c3_transpose_210"] = _entry(dec, dec + 64 * (1048576 + 4), wall, kern,
-                                         kernel="k_decode_tile4" if tile4 else "k_decode_tile")
+                                         kernel="k_decode_tile4" if tile4 else "k_decode_tile",
+                                         checked="bytes")
         del progs, data
     if "c4" in args.extra:
-        shape4, shards, inner = (1024, 1024, 1024), (128, 128, 128), (32, 32, 32)
-        g = torch.Generator(device=device).manual_seed(0)
-        data = torch.randn(shape4, generator=g, device=device, dtype=torch.float32)
-        progs = []
-        for _ in range(2):
-            arr = build_replica(device, data, shape4, inner, [LE, CRC], shards=shards)
-            progs.append(arr.prepare_read((Ellipsis,))[0])
-        del data
-        progs[0].launch()
-        progs[0].results()
-        wall, kern = time_programs(progs, 6, 2, device)
-        dec = (1 << 30) * 4
-        alg = dec + 512 * (64 * (131072 + 4) + 64 * 16 + 4)
-        out["c4_sharded_1024"] = _entry(dec, alg, wall, kern)
-        del progs
-    torch.cuda.empty_cache()
-    if "c5" in args.extra:
-        out["c5_partial_2048"] = c5_partial(device, args)
+        out["c4_sharded_1024"] = c4_partitioned(ctx, args)
         torch.cuda.empty_cache()
-    if "enc" in args.extra:
+    if "c5" in args.extra:
+        out["c5_partial_2048"] = c5_partial(ctx, args)
+        torch.cuda.empty_cache()
+    if single and "enc" in args.extra:
         out["encode_c2"] = encode_c2(device, args)
         torch.cuda.empty_cache()
         out["encode_c3"] = encode_c3(device, args)
         torch.cuda.empty_cache()
-    if "e2e" in args.extra:
+    if single and "e2e" in args.extra:
         out["e2e_c2_host"] = e2e_host(device, args)
         torch.cuda.empty_cache()
     return out
+
+
+def c4_partitioned(ctx, args):
+    """BASELINE configs[3]: 1024^3 f32, 128^3 shards of 32^3 inner chunks
+    (bytes+crc32c; 512 shards, 32 768 inner chunks), the shards split
+    round-robin over the ranks (strong scaling: the batch is fixed).  Each rank
+    encodes and decodes only its shards; every decoded byte is compared with the
+    source; aggregate = all ranks' decoded bytes / max rank time."""
+    import torch
+
+    g = W.C4
+    shape, shards, inner = g["shape"], g["shards"], g["inner"]
+    gen = torch.Generator(device=ctx.device).manual_seed(0)
+    data = torch.randn(shape, generator=gen, device=ctx.device, dtype=torch.float32)
+    n_shards = int(np.prod([s // c for s, c in zip(shape, shards)]))
+    mine_n = len(range(ctx.rank, n_shards, ctx.world))
+    blob = 64 * (131072 + 4) + 64 * 16 + 4
+    cap = mine_n * (blob + 256) + (1 << 20)
+    progs = []
+    for r in range(2):
+        prog, out, mine = build_partitioned(ctx, data, shape, inner, shards, "float32", 0.0, cap)
+        if r == 0:
+            prog.launch()
+            prog.results()
+            check_regions(out, data, mine, "c4")
+        progs.append(prog)
+    del data
+    wall, kern = time_programs(progs, 6, 2, ctx.device, ctx)
+    my_dec = mine_n * 128 ** 3 * 4
+    dec = ctx.sum(my_dec)
+    my_alg = my_dec + mine_n * blob
+    del progs
+    return _entry(dec, my_alg, wall, kern, checked="bytes", shards_per_rank=mine_n,
+                  partition=f"round-robin by shard over {ctx.world} rank(s)",
+                  note="decoded_GiBps = all ranks' decoded bytes / max rank step time; "
+                       "kernel_ms / hbm_frac are this rank's")
+
+
+def c5_partial(ctx, args):
+    """BASELINE configs[4]: 2048^3 int16 in 256^3 shards of 64^3 inner chunks
+    (512 shards x 64 inner, 512 KiB each), bytes+crc32c; a random 10 % of the
+    inner chunks (seed 1, workloads.partial_selection) decoded per step, one
+    batch item per inner chunk, each into its region of a full-shape device
+    output.  The shards are split round-robin over the ranks; a rank stages and
+    decodes the selected inner chunks of its own shards.  Kernels locate every
+    inner chunk through its shard index in HBM; each touched shard's index CRC
+    is verified once per step; every selected region is compared with the source."""
+    import torch
+
+    import zarr_hip
+    from zarr_hip import parallel
+
+    g = W.C5
+    shape, shards, inner = g["shape"], g["shards"], g["inner"]
+    gen = torch.Generator(device=ctx.device).manual_seed(0)
+    data = torch.randint(-2 ** 15, 2 ** 15, shape, generator=gen, device=ctx.device, dtype=torch.int16)
+    n_shards = int(np.prod([s // c for s, c in zip(shape, shards)]))
+    mine_n = len(range(ctx.rank, n_shards, ctx.world))
+    shard_bytes = int(np.prod(shards)) * 2 + 64 * 4 + 64 * 16 + 4
+    store = zarr_hip.DeviceStore(ctx.device, capacity=mine_n * (shard_bytes + 256) + (1 << 24))
+    arr = zarr_hip.Array.create(store, shape, inner, "int16", 0, shards=shards, inner_codecs=[LE, CRC])
+    sbatch, _ = arr.batch_info((Ellipsis,))
+    my_shards = parallel.rank_batch(sbatch, ctx.world, ctx.rank)
+    for i in range(0, len(my_shards), 64):  # encode in groups to bound temporaries
+        arr.codec_pipeline.write_sync(my_shards[i:i + 64], data)
+    torch.cuda.synchronize(ctx.device)
+    mine_keys = {it[0].path for it in my_shards}
+    grid = tuple(s // i for s, i in zip(shape, inner))
+    coords = W.partial_selection(grid)
+    batch = [it for it in W.inner_chunk_batch(arr, store, coords, inner) if it[0].path in mine_keys]
+    out = torch.empty(shape, dtype=torch.int16, device=ctx.device)
+    prog = arr.codec_pipeline.prepare_read(batch, out)
+    prog.launch()
+    prog.results()
+    check_regions(out, data, batch, "c5")
+    del data
+    wall, kern = time_programs([prog], max(10, args.steps // 2), 3, ctx.device, ctx)
+    n_sel = len(batch)
+    touched = len({it[0].path for it in batch})
+    my_dec = n_sel * 64 ** 3 * 2
+    dec = ctx.sum(my_dec)
+    alg = my_dec + n_sel * (64 ** 3 * 2 + 4) + touched * (64 * 16 + 4)
+    del prog, out, store, arr
+    return _entry(dec, alg, wall, kern, inner_chunks=n_sel, inner_chunks_total=len(coords),
+                  shards_touched=touched, checked="bytes",
+                  layout="256^3 shards of 64^3 int16 inner chunks",
+                  partition=f"round-robin by shard over {ctx.world} rank(s)",
+                  note="one output replica; selection 10% random inner chunks, seed 1; "
+                       "decoded_GiBps = all ranks' decoded bytes / max rank step time")
 
 
 class _EncodeProg:
@@ -237,19 +405,14 @@ class _EncodeProg:
         return None
 
 
-def encode_c3(device, args):
-    """Encode side of C3: the 256^3 f32 array written through transpose(2,1,0) +
-    bytes + crc32c into 64 chunks of 64^3 by k_encode_tile4 (four LDS tiles
-    per workgroup), timed like encode_c2 and decoded back for the check."""
+def _encode_bench(device, args, codecs, want_tile):
     import torch
 
     import zarr_hip
-    from zarr_hip import _native as N
     from zarr_hip.planner import analyze_chain, plan_encode
     from zarr_hip.writer import EncodeLaunch
 
     shape, chunks = (256, 256, 256), (64, 64, 64)
-    codecs = [{"name": "transpose", "configuration": {"order": [2, 1, 0]}}, LE, CRC]
     data = torch.from_numpy(synthetic(shape, seed=0)).to(device)
     progs, checks = [], []
     for _ in range(2):
@@ -262,9 +425,12 @@ def encode_c3(device, args):
         offs = [store.arena.reserve(elen) for _ in batch]
         items = [(offs[i], it[2], [sl.start or 0 for sl in it[3]]) for i, it in enumerate(batch)]
         t = plan_encode(chain, spec, items, [int(x) * 4 for x in data.stride()], data.data_ptr())
-        assert t.tile, "C3 encode should take the tiled encode"
-        el = EncodeLaunch(t.layout, t.chunks, t.sels, data, store.arena.buf, t.fast, device, t.rows, t.tile)
-        assert el.flags & N.DF_TILE
+        if want_tile:
+            assert t.tile, "C3 encode should take the tiled encode"
+        else:
+            assert t.rows, "C2 encode should take the row-mapped encode"
+        el = EncodeLaunch(t.layout, t.chunks, t.sels, data, store.arena.buf, t.fast, device, t.rows,
+                          t.tile)
         progs.append(_EncodeProg(el))
         checks.append((store, arr, batch, offs, elen))
     wall, kern = time_programs(progs, max(10, args.steps // 2), 3, device)
@@ -272,59 +438,32 @@ def encode_c3(device, args):
         for (bg, *_), off in zip(batch, offs):
             store.register(bg.path, off, elen)
         if not torch.equal(arr.get((Ellipsis,)).view(torch.int32), data.view(torch.int32)):
-            raise SystemExit("bench encode_c3: decoded store differs from the source")
+            raise SystemExit("bench encode: decoded store differs from the source")
     src = data.numel() * 4
+    return src, wall, kern
+
+
+def encode_c3(device, args):
+    """Encode side of C3: the 256^3 f32 array written through transpose(2,1,0) +
+    bytes + crc32c into 64 chunks of 64^3 by k_encode_tile4 (four LDS tiles
+    per workgroup), timed like the decode and decoded back for the check."""
+    codecs = [{"name": "transpose", "configuration": {"order": [2, 1, 0]}}, LE, CRC]
+    src, wall, kern = _encode_bench(device, args, codecs, True)
     return _entry(src, src + 64 * (1048576 + 4), wall, kern,
-                  kernel="k_encode" if args.tune & 65536 else "k_encode_tile4",
+                  kernel="k_encode" if args.tune & 65536 else "k_encode_tile4", checked="bytes",
                   note="decoded_GiBps = source bytes encoded per second")
 
 
 def encode_c2(device, args):
     """Encode side of C2 (a2/a4/a15): the 256^3 f32 device array written as 64
     chunks of 64^3 with bytes+crc32c into a DeviceStore arena -- gather 16-byte
-    rows, empty-chunk check, CRC, trailer -- by k_encode, the launch
+    rows, empty-chunk check, CRC, trailer -- by k_encode_pair, the launch
     HipCodecPipeline.write_sync issues for complete chunks.  Timed like the
     decode (graph replay of K launches); the stored bytes are then decoded back
     and compared with the source."""
-    import torch
-
-    import zarr_hip
-    from zarr_hip.planner import analyze_chain, plan_encode
-    from zarr_hip.writer import EncodeLaunch
-
-    shape, chunks = (256, 256, 256), (64, 64, 64)
-    data = torch.from_numpy(synthetic(shape, seed=0)).to(device)
-    progs, checks = [], []
-    for _ in range(2):
-        store = zarr_hip.DeviceStore(device, capacity=64 * (1 << 20) + (1 << 20))
-        arr = zarr_hip.Array.create(store, shape, chunks, "float32", 0.0, codecs=[LE, CRC])
-        batch, _ = arr.batch_info((Ellipsis,))
-        spec = batch[0][1]
-        chain = analyze_chain(arr.codec_pipeline.codecs, spec)
-        elen = 64 ** 3 * 4 + 4
-        offs = [store.arena.reserve(elen) for _ in batch]
-        items = [(offs[i], it[2], [sl.start or 0 for sl in it[3]]) for i, it in enumerate(batch)]
-        t = plan_encode(chain, spec, items, [int(x) * 4 for x in data.stride()], data.data_ptr())
-        assert t.rows, "C2 encode should take the row-mapped encode"
-        progs.append(_EncodeProg(EncodeLaunch(t.layout, t.chunks, t.sels, data, store.arena.buf, t.fast,
-                                              device, t.rows)))
-        checks.append((store, arr, batch, offs, elen))
-    enc_tune = int(os.environ.get("ZHIP_BENCH_ENC_TUNE", "0"))  # measurement-only ablations
-    if enc_tune:
-        from zarr_hip import _native as N
-        N.lib().zhip_set_tuning(2, enc_tune)
-    wall, kern = time_programs(progs, max(10, args.steps // 2), 3, device)
-    if enc_tune:
-        N.lib().zhip_set_tuning(2, args.tune)
-        checks = []  # ablated results are not valid encodes
-    for store, arr, batch, offs, elen in checks:
-        for (bg, *_), off in zip(batch, offs):
-            store.register(bg.path, off, elen)
-        if not torch.equal(arr.get((Ellipsis,)).view(torch.int32), data.view(torch.int32)):  # NaN payloads: bitwise
-            raise SystemExit("bench encode: decoded store differs from the source")
-    src = data.numel() * 4
+    src, wall, kern = _encode_bench(device, args, [LE, CRC], False)
     return _entry(src, src + 64 * (1048576 + 4), wall, kern,
-                  kernel="k_encode" if args.tune & 64 else "k_encode_pair",
+                  kernel="k_encode" if args.tune & 64 else "k_encode_pair", checked="bytes",
                   note="decoded_GiBps = source bytes encoded per second")
 
 
@@ -349,77 +488,27 @@ def c1_plumbing(device, args):
         raise SystemExit("bench c1: host round trip differs from the source")
     dstore = zarr_hip.DeviceStore.from_host(host.to_dict(), device)
     darr = zarr_hip.Array.open(dstore)
-    progs = [darr.prepare_read((Ellipsis,))[0] for _ in range(2)]
-    progs[0].launch()
-    progs[0].results()
-    wall, kern = time_programs(progs, max(10, args.steps // 2), 3, device)
+    progs = [darr.prepare_read((Ellipsis,)) for _ in range(2)]
+    progs[0][0].launch()
+    progs[0][0].results()
+    if progs[0][1].cpu().numpy().tobytes() != a.tobytes():
+        raise SystemExit("bench c1: device decode differs from the source")
+    wall, kern = time_programs([p for p, _ in progs], max(10, args.steps // 2), 3, device)
     dec = n * 4
     t_rt = []
     for _ in range(5):
         t0 = time.perf_counter()
         harr[...]
         t_rt.append(time.perf_counter() - t0)
-    return _entry(dec, dec + 10 * ck * 4, wall, kern,
+    return _entry(dec, dec + 10 * ck * 4, wall, kern, checked="bytes",
                   host_roundtrip_GiBps=round(dec / float(np.median(t_rt)) / GIB, 2),
                   note="device decode via k_decode_pair (1-D chunks viewed as whole 512-byte rows, planner._split_1d); host_roundtrip = MemoryStore -> HBM -> numpy")
-
-
-def c5_partial(device, args):
-    """BASELINE configs[4] at N=1: 2048^3 int16 in 256^3 shards of 64^3 inner
-    chunks (512 shards x 64 inner, 512 KiB each), bytes+crc32c; a random 10 %
-    of the inner chunks (seed 1) decoded per step, each into its region of a
-    full-shape device output.  Device-resident: kernels locate every inner
-    chunk through its shard index in HBM; each touched shard's index CRC is
-    verified once per step."""
-    import torch
-
-    import zarr_hip
-    from zarr_hip.store import StorePath
-
-    shape, shards, inner = (2048,) * 3, (256,) * 3, (64,) * 3
-    g = torch.Generator(device=device).manual_seed(0)
-    data = torch.randint(-2 ** 15, 2 ** 15, shape, generator=g, device=device, dtype=torch.int16)
-    store = zarr_hip.DeviceStore(device, capacity=int(data.numel() * 2 * 1.01) + (1 << 26))
-    arr = zarr_hip.Array.create(store, shape, inner, "int16", 0, shards=shards, inner_codecs=[LE, CRC])
-    for z in range(0, 2048, 512):  # encode in slabs to bound temporaries
-        arr.set((slice(z, z + 512),), data[z:z + 512])
-    torch.cuda.synchronize(device)
-    n_inner_total = (2048 // 64) ** 3
-    rng = np.random.default_rng(1)
-    pick = rng.choice(n_inner_total, size=int(np.ceil(0.1 * n_inner_total)), replace=False)
-    g3 = np.stack(np.unravel_index(np.sort(pick), (32, 32, 32)), axis=1)
-    batch = []
-    for c in g3:
-        sc = tuple(int(x) // 4 for x in c)
-        key = arr._key(sc)
-        lo = [int(x) % 4 * 64 for x in c]
-        csel = tuple(slice(l, l + 64, 1) for l in lo)
-        osel = tuple(slice(int(x) * 64, int(x) * 64 + 64, 1) for x in c)
-        batch.append((StorePath(store, key), arr.spec, csel, osel, False))
-    out = torch.empty(shape, dtype=torch.int16, device=device)
-    prog = arr.codec_pipeline.prepare_read(batch, out)
-    prog.launch()
-    prog.results()
-    # spot-check a few selected inner chunks against the source
-    for c in g3[:: max(1, len(g3) // 16)]:
-        sl = tuple(slice(int(x) * 64, int(x) * 64 + 64) for x in c)
-        if not torch.equal(out[sl], data[sl]):
-            raise SystemExit("bench c5: decoded inner chunk differs from the source")
-    wall, kern = time_programs([prog], max(10, args.steps // 2), 3, device)
-    n_sel = len(g3)
-    touched = len({tuple(int(x) // 4 for x in c) for c in g3})
-    dec = n_sel * 64 ** 3 * 2
-    alg = dec + n_sel * (64 ** 3 * 2 + 4) + touched * (64 * 16 + 4)
-    del prog, out, data, store, arr
-    return _entry(dec, alg, wall, kern, inner_chunks=n_sel, shards_touched=touched,
-                  layout="256^3 shards of 64^3 int16 inner chunks",
-                  note="one output replica; selection 10% random inner chunks, seed 1")
 
 
 def e2e_host(device, args):
     """Host memory -> host memory (the path's full IO):
     C2's encoded chunks in a host MemoryStore; arr[...] stages them into
-    pinned memory (thread pool), H2D on a copy stream, decodes, and copies the
+    pinned memory, H2D on a copy stream, decodes per window, and copies the
     result back through pinned memory into a numpy array."""
     import torch
 
@@ -427,7 +516,7 @@ def e2e_host(device, args):
 
     shape, chunks = (256, 256, 256), (64, 64, 64)
     data_np = synthetic(shape, seed=0)
-    dev_arr = build_c2_replica(device, data_np, shape, chunks)
+    dev_arr = build_replica(device, torch.from_numpy(data_np).to(device), shape, chunks, [LE, CRC])
     host = zarr_hip.MemoryStore(dev_arr.store_path.store.to_dict())
     arr = zarr_hip.Array.open(host)
     got = arr[...]
@@ -444,6 +533,8 @@ def e2e_host(device, args):
         arr.get((Ellipsis,), out=out)
         torch.cuda.synchronize(device)
         t_h2d.append(time.perf_counter() - t0)
+    if not torch.equal(out.view(torch.int32).cpu(), torch.from_numpy(data_np).view(torch.int32)):
+        raise SystemExit("bench e2e: device read differs from the source")
     pin = torch.empty(data_np.nbytes, dtype=torch.uint8, pin_memory=True)
     dbuf = torch.empty(data_np.nbytes, dtype=torch.uint8, device=device)
     dbuf.copy_(pin, non_blocking=True)
@@ -458,7 +549,17 @@ def e2e_host(device, args):
             "host_to_hbm_decoded_GiBps": round(dec / float(np.median(t_h2d)) / GIB, 2),
             "pinned_h2d_copy_GiBps": round(h2d_raw, 2),
             "host_to_host_ms": round(float(np.median(t_h2h)) * 1e3, 3),
-            "host_to_hbm_ms": round(float(np.median(t_h2d)) * 1e3, 3)}
+            "host_to_hbm_ms": round(float(np.median(t_h2d)) * 1e3, 3), "checked": "bytes"}
+
+
+# ------------------------------------------------------------------ CPU baseline
+
+def box_cores() -> int:
+    """The host cores this process may use: the affinity mask, capped by the
+    box's share (OMP_NUM_THREADS is set to the share on the GPU boxes)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return max(1, min(n, cap) if cap else n)
 
 
 def cpu_baseline(data_np, shape, chunks, shards, budget_s=12.0):
@@ -467,8 +568,9 @@ def cpu_baseline(data_np, shape, chunks, shards, budget_s=12.0):
     (codec_pipeline.py:1095-1172) running ShardingCodec._decode_partial_sync
     (sharding.py:1222-1309): index by suffix read -> index CRC -> per inner chunk
     CRC-32C (SSE4.2 instruction, as google_crc32c) -> zero-copy view -> scatter
-    into the shard array -> scatter of the shard into out.  Pool sized like
-    _resolve_max_workers (codec_pipeline.py:53-73), capped by the box's share."""
+    into the shard array -> scatter of the shard into out.  Timed at the pool
+    size _resolve_max_workers (codec_pipeline.py:53-73) would give on this
+    box's share of cores, and at 1 worker."""
     from concurrent.futures import ThreadPoolExecutor
 
     from oracle import oracle as O
@@ -514,37 +616,78 @@ def cpu_baseline(data_np, shape, chunks, shards, budget_s=12.0):
         return None
 
     keys = list(store.keys())
-    workers = os.cpu_count() or 1
-    box_cores = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
-    if box_cores:
-        workers = min(workers, box_cores)
-    workers = min(workers, len(keys))
-    pool = ThreadPoolExecutor(max_workers=workers)
-    list(pool.map(read_shard, keys))  # warm-up
-    n = 0
-    t0 = time.perf_counter()
-    while True:
-        list(pool.map(read_shard, keys))
-        n += 1
-        if time.perf_counter() - t0 > budget_s:
-            break
-    dt = (time.perf_counter() - t0) / n
-    assert out.tobytes() == data_np.tobytes()
-    pool.shutdown()
+
+    def run(workers, budget):
+        pool = ThreadPoolExecutor(max_workers=workers)
+        list(pool.map(read_shard, keys))  # warm-up
+        n = 0
+        t0 = time.perf_counter()
+        while True:
+            list(pool.map(read_shard, keys))
+            n += 1
+            if time.perf_counter() - t0 > budget:
+                break
+        dt = (time.perf_counter() - t0) / n
+        pool.shutdown()
+        assert out.tobytes() == data_np.tobytes()
+        return dt, n
+
+    cores = box_cores()
+    workers = min(cores, len(keys))
+    dt, n = run(workers, budget_s * 0.6)
+    dt1, n1 = run(1, budget_s * 0.4)
     return {"value": round(data_np.nbytes / dt / GIB, 3), "unit": "GiB/s", "cores": workers,
             "kind": "port",
             "sample": f"{n} full decodes of the headline array ({len(keys)} shards x {n_inner} "
                       f"inner chunks of 1 MiB + crc) in {n * dt:.1f}s; {workers} worker threads "
-                      f"(one task per shard), {os.cpu_count()} cpus visible"}
+                      f"(one task per shard; {cores} cores in this box's share, "
+                      f"{os.cpu_count()} cpus visible)",
+            "single_worker": {"value": round(data_np.nbytes / dt1 / GIB, 3), "unit": "GiB/s",
+                              "cores": 1, "sample": f"{n1} full decodes in {n1 * dt1:.1f}s"}}
 
 
 def pmc_traffic():
     """HBM bytes per launch measured by the PMC passes (null if not collected)."""
     try:
-        with open(TRAFFIC_JSON) as fh:
+        with open(os.path.join(ROOT, TRAFFIC_JSON)) as fh:
             return json.load(fh).get("traffic_bytes_per_launch")
     except (OSError, ValueError):
         return None
+
+
+# ------------------------------------------------------------------------ main
+
+def headline(ctx, args):
+    """The headline batch partitioned round-robin by shard (weak scaling: the
+    global array is (256N) x 256 x 256, every rank owns 8 shards = one 256^3
+    array's worth).  Returns (programs, decoded bytes per step on this rank,
+    algorithmic bytes per launch on this rank)."""
+    import torch
+
+    g = W.HEADLINE
+    shape1, shards, inner = g["shape"], g["shards"], g["inner"]
+    data = synthetic(shape1, seed=0)
+    src = torch.from_numpy(data).to(ctx.device)
+    if ctx.world > 1:
+        src = src.repeat(ctx.world, 1, 1)
+    shape = (shape1[0] * ctx.world,) + shape1[1:]
+    blob = 8 * (1048576 + 4) + 8 * 16 + 4
+    progs = []
+    for r in range(args.replicas):
+        prog, out, mine = build_partitioned(ctx, src, shape, inner, shards, "float32", 0.0,
+                                            8 * (blob + 256) + (1 << 20))
+        if r == 0:  # correctness gate: every decoded byte of this rank's shards
+            prog.launch()
+            prog.results()
+            check_regions(out, src, mine, "headline")
+        assert len(mine) == 8, "every rank owns 8 shards of the headline batch"
+        assert prog.tables.fast and prog.tables.rows, "the headline should take the whole-row kernel"
+        assert prog.index is None and prog.data.n_idx == 8, "index CRC checks should be fused"
+        progs.append(prog)
+    del src
+    decoded = data.nbytes
+    encoded = 64 * (1048576 + 4) + 8 * (8 * 16 + 4)  # inner chunks + 8 shard indexes
+    return progs, decoded, encoded
 
 
 def main():
@@ -560,81 +703,46 @@ def main():
                     help="time one host launch per step instead of a hipGraph replay")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--extra", default="c1,c2,c3,c4,c5,enc,e2e",
-                    help="extra configs measured at N=1 (subset of c1,c2,c3,c4,c5,e2e, or '')")
+                    help="extra configs (subset of c1,c2,c3,c4,c5,enc,e2e, or ''); c4/c5 run "
+                         "partitioned at every N, the others at N=1")
     args = ap.parse_args()
 
     import torch
-    import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    # launched by torchrun (even with one rank): use the process group for the
-    # barrier / max-over-ranks timing so the N>1 code path is the one exercised
-    distributed = "RANK" in os.environ and "MASTER_ADDR" in os.environ
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if distributed:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    device = torch.device("cuda", local)
-    torch.cuda.set_device(device)
-
+    ctx = Ctx()
+    device = ctx.device
     if args.tune:
         from zarr_hip import _native as N
 
         N.lib().zhip_set_tuning(2, args.tune)
-    shape, chunks, shards = (256, 256, 256), (64, 64, 64), (128, 128, 128)
-    data = synthetic(shape, seed=0)
-    log(f"[bench] building {args.replicas} replicas of the headline config on {device}")
-    data_dev = torch.from_numpy(data).to(device)
-    progs = []
-    for r in range(args.replicas):
-        arr = build_replica(device, data_dev, shape, chunks, [LE, CRC], shards=shards)
-        prog, out = arr.prepare_read((Ellipsis,))
-        progs.append((prog, out))
-    del data_dev
-    # correctness gate on the first replica
-    prog0, out0 = progs[0]
-    prog0.launch()
-    prog0.results()
-    if out0.view(torch.int32).cpu().numpy().tobytes() != data.view(np.int32).tobytes():
-        raise SystemExit("bench: decoded output differs from the synthetic input")
-    for p, _ in progs:
-        assert p.tables.fast, "the headline should take the whole-row fast path"
-        assert p.index is None and p.data.n_idx == 8, "index CRC checks should be fused"
-        assert p.tables.rows, "the headline should take k_decode_rows (affine whole-row path)"
+    log(f"[bench] building {args.replicas} replicas of the headline batch on {device} "
+        f"(rank {ctx.rank} of {ctx.world})")
+    plist, decoded, encoded = headline(ctx, args)
 
-    plist = [p for p, _ in progs]
     if args.eager:
         stream = torch.cuda.current_stream(device)
         sh = int(stream.cuda_stream)
         for i in range(args.warmup):
             plist[i % len(plist)].launch(sh)
-        if distributed:
-            dist.barrier()
+        ctx.barrier()
         torch.cuda.synchronize(device)
         t0 = time.perf_counter()
         kern_s = eager_kernel_times(plist, args.steps, device)
         wall = time.perf_counter() - t0
-        if distributed:
-            dist.barrier()
+        ctx.barrier()
         for p in plist:
             p.results()
         span_s = float(np.sum(kern_s))
+        wall_max = ctx.max(wall)
     else:
-        wall, span_s = graph_steps(plist, args.steps, args.warmup, device,
-                                   barrier=dist.barrier if distributed else None)
+        wall, wall_max, span_s = graph_steps(plist, args.steps, args.warmup, device, ctx)
         # per-launch durations of the same kernel, eager (for the rocprof cross-check)
         kern_s = eager_kernel_times(plist, args.steps, device)
         for p in plist:
             p.results()
-    t = torch.tensor([wall], dtype=torch.float64, device=device)
-    if distributed:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    wall_max = float(t.item())
 
-    decoded = data.nbytes
-    encoded = 64 * (1048576 + 4) + 8 * (8 * 16 + 4)  # inner chunks + 8 shard indexes
-    value = world * args.steps * decoded / wall_max / GIB
+    total_decoded = ctx.sum(args.steps * decoded)  # every rank's own shards
+    value = total_decoded / wall_max / GIB
     # kernel time per launch over the timed region: event span on the launch
     # stream / steps (includes the graph's inter-launch gaps, so it is an upper
     # bound on the kernel duration and `achieved` a lower bound)
@@ -644,7 +752,7 @@ def main():
         "metric": "decoded GiB/s (device-resident), sharded 256^3 f32 64^3 chunks, 1/2/4/8 GPU",
         "value": round(value, 2),
         "unit": "GiB/s",
-        "n_gpus": world,
+        "n_gpus": ctx.world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(wall_max / args.steps * 1e3, 4),
@@ -656,14 +764,19 @@ def main():
         "config": {
             "workload": "sharded 256^3 float32, 64^3 chunks (128^3 shards of 8 inner chunks; inner "
                         "codecs bytes(little)+crc32c, index bytes+crc32c at end), device-resident "
-                        "decode of the full array per step (64 inner chunks + 8 index checks, one "
-                        "launch), 4 rotating replicas per GPU",
-            "chunks_per_step": 64, "shards_per_step": 8, "decoded_bytes_per_step": decoded,
-            "encoded_bytes_per_step": encoded, "parallelism": f"chunk-parallel x{world} (weak)",
+                        "decode of the full array per step per GPU (64 inner chunks + 8 index "
+                        "checks, one launch), 4 rotating replicas per GPU; at N GPUs the batch is "
+                        "the (256N)x256x256 array split round-robin by shard (8 shards per rank)",
+            "chunks_per_step": 64 * ctx.world, "shards_per_step": 8 * ctx.world,
+            "decoded_bytes_per_step": decoded * ctx.world,
+            "encoded_bytes_per_step": encoded * ctx.world,
+            "parallelism": f"shard-partitioned x{ctx.world} (weak, no collective on the data path)",
         },
         "roofline": {
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(),
+            "traffic_source": TRAFFIC_JSON + " (FETCH_SIZE x2 + WRITE_SIZE per launch from "
+                              "separate rocprofv3 --pmc passes of this command)",
             "kernel": "zhip::k_decode_pair<CRC,4,noswap,2> (zhip_decode_mapped)",
             "kernel_ms_avg": round(avg_kern_s * 1e3, 5),
             "kernel_ms_eager_mean": round(float(np.mean(kern_s)) * 1e3, 5),
@@ -672,16 +785,20 @@ def main():
             "algorithmic_bytes_per_launch": encoded + decoded,
         },
     }
-    if world == 1 and args.extra:
+    del plist
+    torch.cuda.empty_cache()
+    if args.extra:
         log("[bench] extra configs " + args.extra)
-        res["extra"] = extra_configs(device, args)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        res["extra"] = extra_configs(ctx, args)
+    if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu_baseline:
         log("[bench] cpu baseline")
-        res["cpu_baseline"] = cpu_baseline(data, shape, chunks, shards, args.cpu_budget)
-    if rank == 0:
+        g = W.HEADLINE
+        res["cpu_baseline"] = cpu_baseline(synthetic(g["shape"], seed=0), g["shape"], g["inner"],
+                                           g["shards"], args.cpu_budget)
+    if ctx.rank == 0:
         print(json.dumps(res), flush=True)
-    if distributed:
-        dist.destroy_process_group()
+    if ctx.distributed:
+        ctx.dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -28,6 +28,13 @@ if [ "${TORCHRUN:-0}" = "1" ]; then
   rc=$?; echo "torchrun bench rc=$rc"; cat gpurun_out/bench_torchrun.json
   if [ $rc -ne 0 ]; then tail -5 gpurun_out/bench_torchrun.err; exit $rc; fi
 fi
+if [ "${REHEARSAL:-0}" = "1" ]; then
+  # the N>1 code path with 2 ranks on this one GPU (gloo group; not a scaling number)
+  cd "$GRAFT_REPO_ROOT"
+  ZHIP_BENCH_REHEARSAL=1 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29513 bench.py --gpus 2 --steps 20 --warmup 5 --extra "${REHEARSAL_EXTRA:-c4,c5}" > gpurun_out/bench_rehearsal2.json 2> gpurun_out/bench_rehearsal2.err
+  rc=$?; echo "rehearsal bench rc=$rc"; cat gpurun_out/bench_rehearsal2.json
+  if [ $rc -ne 0 ]; then tail -15 gpurun_out/bench_rehearsal2.err; exit $rc; fi
+fi
 if [ "${PMC:-0}" = "1" ]; then
   bash "$GRAFT_REPO_ROOT/scripts/gpu_pmc.sh"
   rc=$?

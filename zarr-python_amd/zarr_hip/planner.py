@@ -330,6 +330,10 @@ def plan_decode(chain: ChainInfo, spec: ArraySpec, items: list, out_strides_byte
     proj_cache: dict = {}
     parts = []
     for i, (so, sl, miss, csel, osel) in enumerate(items):
+        if resolved is None and not miss and sl < index_size:
+            # the kernels locate the index at blob end - index_size (or the
+            # start): a short blob must never reach them (staging.py raises the same)
+            raise ValueError("shard blob is shorter than its index")
         key = tuple((s.start, s.stop, s.step) if isinstance(s, slice) else int(s) for s in csel)
         pr = proj_cache.get(key)
         if pr is None:
