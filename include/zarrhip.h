@@ -269,8 +269,10 @@ int zhip_debug_stamps(uint64_t *host_out, uint32_t n_wg);
  * selection origin, sel = selection (stored dims) — elements outside it are
  * written as the fill value (edge chunks, _merge_chunk_array).  With
  * ZHIP_LF_CRC the CRC-32C trailer is appended and also reported in
- * d_status[i].computed.  d_nonempty[i] (zeroed by the caller) is set to 1 if
- * any element differs from the fill value under NDBuffer.all_equal rules.
+ * d_status[i].computed.  d_nonempty[i] is set to 1 if any element differs
+ * from the fill value under NDBuffer.all_equal rules, else 0 (every launch
+ * writes every flag: kernels that OR flags are preceded by an async zeroing
+ * of d_nonempty on the same stream).
  * ZHIP_DF_FAST_ROWS: every chunk selects whole rows that are contiguous and
  * 16-byte aligned in arr.  Asynchronous. */
 int zhip_encode(const zhip_plan *plan, const void *arr, void *dst, const zhip_chunk *d_chunks,

@@ -582,13 +582,62 @@ def read(store: dict, meta: ArrayMeta, selection: Any = Ellipsis) -> np.ndarray:
     return out
 
 
+def _merge(existing: np.ndarray | None, value: np.ndarray, osel, spec: Spec, csel,
+           complete: bool) -> np.ndarray:
+    """_merge_chunk_array (chunk_utils.py:115-162)."""
+    if complete and value.shape != ():
+        selected = value[osel]
+        if selected.shape == tuple(spec.shape):
+            return selected
+    chunk = np.full(spec.shape, spec.fill_value, dtype=spec.dtype) if existing is None \
+        else existing.copy()
+    chunk[csel] = value if value.shape == () else value[osel].reshape(chunk[csel].shape)
+    return chunk
+
+
+def shard_encode_partial(store: dict, key: str, chunk_value: np.ndarray, selection: tuple,
+                         sh: ShardSpec, shard_spec: Spec) -> None:
+    """ShardingCodec._encode_partial_sync (sharding.py:774-885), reached from
+    FusedCodecPipeline.write_sync when the chain is a sharding codec alone
+    (codec_pipeline.py:1211-1220): only the inner chunks the selection touches
+    are merged and re-encoded; the others keep their stored bytes (or absence)."""
+    cps = _cps(shard_spec, sh)
+    inner_spec = Spec(sh.chunk_shape, shard_spec.dtype, shard_spec.fill_value,
+                      shard_spec.write_empty_chunks, shard_spec.order)
+    projections, _ = basic_indexer(selection, shard_spec.shape, sh.chunk_shape)
+    touched = {c for c, *_ in projections}
+    complete_shard = touched == set(lexicographic_order_coords(cps)) and all(
+        p[3] for p in projections)  # _is_complete_shard_write (1437-1445)
+    existing = None if complete_shard else store.get(key)
+    if existing is None:
+        shard_dict = dict.fromkeys(lexicographic_order_coords(cps))
+    else:
+        shard_dict = shard_reader(_as_u8(existing), sh, cps)
+    for coords, csel, osel, complete in projections:
+        raw = None if complete else shard_dict.get(coords)
+        old = None if raw is None else chain_decode(raw, sh.inner, inner_spec)
+        merged = _merge(old, chunk_value, osel, inner_spec, csel, complete)
+        shard_dict[coords] = encode_or_elide(merged, sh.inner, inner_spec)
+    blob = assemble_shard(shard_dict, sh, cps)
+    if blob is None:
+        store.pop(key, None)
+    else:
+        store[key] = bytes(blob)
+
+
 def write(store: dict, meta: ArrayMeta, selection: Any, value: Any) -> None:
-    """Array._set_selection + FusedCodecPipeline.write_sync + merge_and_encode_chunk."""
+    """Array._set_selection + FusedCodecPipeline.write_sync + merge_and_encode_chunk
+    (partial shard encode when the chain is a sharding codec alone)."""
     projections, out_shape = basic_indexer(selection if isinstance(selection, tuple)
                                            else (selection,), meta.shape, meta.chunk_shape)
     value = np.asarray(value, dtype=meta.dtype)
     chain = meta.chain
     spec = meta.spec()
+    if chain.shard is not None and not chain.aa and not chain.bb:
+        for coords, csel, osel, complete in projections:
+            chunk_value = value if value.shape == () else value[osel]
+            shard_encode_partial(store, meta.chunk_key(coords), chunk_value, csel, chain.shard, spec)
+        return
     for coords, csel, osel, complete in projections:
         key = meta.chunk_key(coords)
         if complete and value.shape != ():

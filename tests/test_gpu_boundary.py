@@ -1,0 +1,264 @@
+"""The CodecPipeline boundary driven the way zarr's Array layer drives it, on the
+GPU: zarr-shaped stores, specs, codecs and NDBuffers (tests/zarr_fakes.py),
+compared byte for byte with the CPU oracle.  Also the ROCm Buffer / NDBuffer
+prototypes, the encode / decode batch API, the partial shard encode and the
+bounded HBM arena under rewrites."""
+
+import asyncio
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from tests import zarr_fakes as Z
+
+pytestmark = pytest.mark.gpu
+
+LE = {"name": "bytes", "configuration": {"endian": "little"}}
+BE = {"name": "bytes", "configuration": {"endian": "big"}}
+CRC = {"name": "crc32c"}
+
+
+def SHARD(inner, codecs, loc="end"):
+    return {"name": "sharding_indexed", "configuration": {
+        "chunk_shape": list(inner), "codecs": list(codecs), "index_location": loc}}
+
+
+def _data(shape, dtype="float32", seed=0):
+    rng = np.random.default_rng(seed)
+    a = rng.standard_normal(shape).astype(dtype)
+    if a.size > 8 and a.dtype == np.float32:
+        a.reshape(-1)[3] = -0.0
+        a.reshape(-1)[5:6].view(np.uint32)[0] = 0x7FC00001
+    return a
+
+
+def _setup(shape, chunks, codecs, dtype="float32", fill=0.0, wec=False):
+    from zarr_hip import HipCodecPipeline
+
+    meta = O.ArrayMeta(shape, chunks, np.dtype(dtype), fill, codecs=codecs, write_empty_chunks=wec)
+    spec = Z.ArraySpec(chunks, Z.ZDType(dtype), np.dtype(dtype).type(fill),
+                       Z.ArrayConfig(write_empty_chunks=wec), Z.cpu_prototype)
+    pipe = HipCodecPipeline.from_codecs(Z.zcodecs(codecs)).evolve_from_array_spec(spec)
+    return meta, spec, pipe
+
+
+CASES = [
+    ((40, 36), (16, 16), [LE, CRC]),
+    ((40, 36), (16, 16), [{"name": "transpose", "configuration": {"order": [1, 0]}}, BE, CRC]),
+    ((64, 48), (32, 48), [SHARD((16, 16), [LE, CRC])]),
+    ((64, 48), (32, 48), [SHARD((16, 16), [BE], "start")]),
+]
+
+
+@pytest.mark.parametrize("shape,chunks,codecs", CASES)
+@pytest.mark.parametrize("out_kind", ["host_ndbuffer", "rocm_ndbuffer", "torch"])
+def test_read_zarr_shaped(device, shape, chunks, codecs, out_kind):
+    import torch
+
+    from zarr_hip.buffer import NDBuffer
+
+    meta, spec, pipe = _setup(shape, chunks, codecs)
+    host = {}
+    O.write(host, meta, (Ellipsis,), _data(shape))
+    store = Z.MemoryStore(dict(host))
+    for sel in [(Ellipsis,), (slice(3, 39), slice(None, None, 3)), (7, slice(2, 30))]:
+        batch, out_shape = Z.batch_for(shape, chunks, sel, store, spec)
+        want = O.read(host, meta, sel)
+        if out_kind == "host_ndbuffer":
+            out = Z.NDBuffer.create(shape=out_shape, dtype="float32")
+            res = pipe.read_sync(batch, out)
+            got = out.as_numpy_array()
+        elif out_kind == "rocm_ndbuffer":
+            out = NDBuffer.create(shape=out_shape, dtype=Z.ZDType("float32").to_native_dtype())
+            res = asyncio.run(pipe.read(batch, out))
+            got = out.as_numpy_array()
+        else:
+            out = torch.empty(out_shape, dtype=torch.float32, device=device)
+            res = pipe.read_sync(batch, out)
+            got = out.cpu().numpy()
+        assert len(res) == len(batch) and all(r["status"] == "present" for r in res)
+        assert got.tobytes() == np.ascontiguousarray(want).tobytes()
+
+
+def test_read_host_out_keeps_unselected_regions(device):
+    meta, spec, pipe = _setup((32, 32), (16, 16), [LE, CRC])
+    host = {}
+    O.write(host, meta, (Ellipsis,), _data((32, 32)))
+    store = Z.MemoryStore(dict(host))
+    batch, _ = Z.batch_for((32, 32), (16, 16), (Ellipsis,), store, spec)
+    out = Z.NDBuffer(np.full((40, 40), 9.0, np.float32))
+    # two chunks only, into a bigger out: the rest must stay 9.0
+    pipe.read_sync([batch[0], batch[3]], out)
+    a = out.as_numpy_array()
+    want = O.read(host, meta)
+    assert a[:16, :16].tobytes() == want[:16, :16].tobytes()
+    assert a[16:32, 16:32].tobytes() == want[16:, 16:].tobytes()
+    assert (a[:16, 16:] == 9.0).all() and (a[32:] == 9.0).all()
+
+
+def test_missing_chunks_status_and_fill(device):
+    meta, spec, pipe = _setup((32, 32), (16, 16), [LE, CRC], fill=-2.5)
+    host = {}
+    O.write(host, meta, (Ellipsis,), _data((32, 32)))
+    host.pop("c/1/0")
+    store = Z.MemoryStore(dict(host))
+    batch, shp = Z.batch_for((32, 32), (16, 16), (Ellipsis,), store, spec)
+    out = Z.NDBuffer.create(shape=shp, dtype="float32")
+    res = pipe.read_sync(batch, out)
+    assert [r["status"] for r in res] == ["present", "present", "missing", "present"]
+    assert out.as_numpy_array().tobytes() == O.read(host, meta).tobytes()
+
+
+WRITES = [
+    ((Ellipsis,), None),
+    ((slice(5, 30), slice(3, 17)), None),
+    ((slice(0, 40), 7), None),
+    ((slice(10, 20), slice(10, 20)), 0.0),    # scalar equal to the fill
+    ((slice(None), slice(None)), 1.25),       # scalar fill of everything
+]
+
+
+@pytest.mark.parametrize("codecs", [[LE, CRC], [SHARD((8, 8), [LE, CRC])],
+                                    [SHARD((8, 8), [BE, CRC], "start")]])
+@pytest.mark.parametrize("wec", [False, True])
+def test_write_zarr_shaped_matches_oracle(device, codecs, wec):
+    """zarr-style StorePaths that only accept Buffers; a sequence of writes
+    (partial, strided, int-dropped, scalar); edge chunks / shards (40x36 over
+    16x16); the stored keys and bytes match the oracle after every write."""
+    shape, chunks = (40, 36), (16, 16)
+    meta, spec, pipe = _setup(shape, chunks, codecs, wec=wec)
+    ours, want = Z.MemoryStore(), {}
+    rng = np.random.default_rng(3)
+    for sel, scalar in WRITES:
+        batch, shp = Z.batch_for(shape, chunks, sel, ours, spec)
+        val = np.float32(scalar) if scalar is not None else rng.standard_normal(shp).astype(np.float32)
+        pipe.write_sync(batch, Z.NDBuffer(np.asarray(val)))
+        O.write(want, meta, sel, val)
+        assert sorted(ours._store_dict) == sorted(want)
+        for k in want:
+            assert ours._store_dict[k] == want[k], k
+    asyncio.run(pipe.write(Z.batch_for(shape, chunks, (Ellipsis,), ours, spec)[0],
+                           Z.NDBuffer(np.zeros(shape, np.float32))))
+    O.write(want, meta, (Ellipsis,), np.zeros(shape, np.float32))
+    assert sorted(ours._store_dict) == sorted(want)
+
+
+@pytest.mark.parametrize("wec", [False, True])
+def test_partial_shard_encode_on_device_store(device, wec):
+    """The partial shard encode on a DeviceStore (the reference's
+    _encode_partial_sync): untouched inner chunks keep their state, edge
+    shards never gain out-of-array inner chunks."""
+    import zarr_hip
+
+    shape, shards, inner = (40, 36), (16, 16), (8, 8)
+    codecs = [SHARD(inner, [LE, CRC])]
+    meta = O.ArrayMeta(shape, shards, np.dtype("float32"), 0.0, codecs=codecs, write_empty_chunks=wec)
+    st = zarr_hip.DeviceStore(device)
+    arr = zarr_hip.Array.create(st, shape, shards, "float32", 0.0, codecs=codecs,
+                                config=zarr_hip.ArrayConfig(write_empty_chunks=wec))
+    want = {}
+    rng = np.random.default_rng(9)
+    for sel in [(slice(0, 5), slice(0, 3)), (slice(30, 40), slice(20, 36)), (Ellipsis,),
+                (slice(2, 9), slice(9, 10)), (slice(16, 32), slice(0, 16))]:
+        shp = O.basic_indexer(sel, shape, shards)[1]
+        v = rng.standard_normal(shp).astype(np.float32)
+        if sel == (slice(16, 32), slice(0, 16)):
+            v[:] = 0.0  # a whole shard of fill
+        arr[sel] = v
+        O.write(want, meta, sel, v)
+        got = {k: v for k, v in st.to_dict().items() if k.startswith("c/")}
+        assert sorted(got) == sorted(want)
+        for k in want:
+            assert got[k] == want[k], (sel, k)
+
+
+def test_encode_decode_batch_api(device):
+    from zarr_hip import HipCodecPipeline
+    from zarr_hip.buffer import Buffer, NDBuffer
+
+    meta, spec, pipe = _setup((16, 16), (16, 16), [LE, CRC])
+    a = _data((16, 16))
+    z = np.zeros((16, 16), np.float32)
+    enc = asyncio.run(pipe.encode([(NDBuffer(a), spec), (None, spec), (Z.NDBuffer(z), spec)]))
+    assert enc[1] is None and enc[2] is None  # all-fill chunk elided (chunk_utils.py:43-58)
+    chain = O.Chain.from_json([LE, CRC])
+    assert enc[0].to_bytes() == bytes(O.chain_encode(a, chain, meta.spec()))
+    dec = asyncio.run(pipe.decode([(enc[0], spec), (None, spec)]))
+    assert dec[1] is None
+    assert dec[0].as_numpy_array().tobytes() == a.tobytes()
+    # a device Buffer straight in, a ROCm NDBuffer (no prototype) out
+    pipe2 = HipCodecPipeline.from_codecs([LE, CRC]).evolve_from_array_spec(spec)
+    spec2 = Z.ArraySpec((16, 16), Z.ZDType("float32"), np.float32(0), Z.ArrayConfig(), None)
+    d2 = pipe2.decode_sync([(Buffer.from_bytes(enc[0].to_bytes()), spec2)])
+    assert isinstance(d2[0], NDBuffer) and d2[0].as_numpy_array().tobytes() == a.tobytes()
+    e2 = pipe2.encode_sync([(d2[0], spec2)])
+    assert isinstance(e2[0], Buffer) and e2[0].to_bytes() == enc[0].to_bytes()
+
+
+def test_rocm_buffer_prototype(device):
+    from zarr_hip.buffer import Buffer, NDBuffer, buffer_prototype
+
+    b = buffer_prototype.buffer.from_bytes(b"abcdef")
+    assert len(b) == 6 and b[1:4].to_bytes() == b"bcd"
+    assert (b + Buffer.from_bytes(b"gh")).to_bytes() == b"abcdefgh"
+    assert b.as_array_like().is_cuda
+    nd = NDBuffer.create(shape=(4, 5), dtype=np.dtype("float32"), fill_value=0.0)
+    assert nd.all_equal(0.0)
+    nd[1:3, 2] = np.float32(-0.0)
+    assert not nd.all_equal(0.0)  # bitwise against +0.0 (buffer/core.py:539-547)
+    assert nd.all_equal(np.float32(-0.0)) is False
+    n2 = NDBuffer.create(shape=(3,), dtype=np.dtype("float32"), fill_value=np.nan)
+    assert n2.all_equal(np.nan)
+    f = NDBuffer.create(shape=(4, 6), dtype=np.dtype("int16"), order="F")
+    assert f.as_ndarray_like().stride() == (1, 4)
+    assert NDBuffer.from_numpy_array(np.arange(3)).as_numpy_array().tolist() == [0, 1, 2]
+
+
+def test_metadata_hook_pipeline_reads(device):
+    from zarr_hip import HipCodecPipeline
+
+    codecs = [SHARD((8, 8), [LE, CRC])]
+    md = Z.ArrayV3Metadata((32, 32), Z.ZDType("float32"), Z.RegularChunkGrid((16, 16)), np.float32(0),
+                           Z.zcodecs(codecs))
+    pipe = HipCodecPipeline.from_array_metadata_and_store(md, None)
+    meta = O.ArrayMeta((32, 32), (16, 16), np.dtype("float32"), 0.0, codecs=codecs)
+    host = {}
+    O.write(host, meta, (Ellipsis,), _data((32, 32)))
+    spec = Z.ArraySpec((16, 16), md.data_type, md.fill_value, Z.ArrayConfig(), Z.cpu_prototype)
+    store = Z.MemoryStore(dict(host))
+    batch, shp = Z.batch_for((32, 32), (16, 16), (slice(3, 29), slice(None)), store, spec)
+    out = Z.NDBuffer.create(shape=shp, dtype="float32")
+    pipe.read_sync(batch, out)
+    assert out.as_numpy_array().tobytes() == O.read(host, meta, (slice(3, 29), slice(None))).tobytes()
+    # partial shard reads went through ranged gets (index suffix + coalesced inner chunks)
+    assert any(c[2] is not None for c in store.calls)
+
+
+def test_arena_bounded_under_rewrites(device):
+    """A sharded DeviceStore array overwritten 10 times: deleted / replaced
+    shards give their HBM back, so the arena does not grow."""
+    import zarr_hip
+
+    shape, shards, inner = (128, 128), (64, 64), (16, 16)
+    codecs = [SHARD(inner, [LE, CRC])]
+    st = zarr_hip.DeviceStore(device, capacity=1 << 16)
+    arr = zarr_hip.Array.create(st, shape, shards, "float32", 0.0, codecs=codecs)
+    meta = O.ArrayMeta(shape, shards, np.dtype("float32"), 0.0, codecs=codecs)
+    rng = np.random.default_rng(1)
+    tops, caps = [], []
+    for i in range(10):
+        v = rng.standard_normal(shape).astype(np.float32)
+        if i % 3 == 2:
+            v[:64] = 0.0  # two shards elided -> deleted
+        arr[...] = v
+        arr[5:70, 9:11] = np.float32(i)
+        tops.append(st.arena.top)
+        caps.append(st.arena.capacity)
+    assert max(tops[2:]) <= 2 * tops[0] + (1 << 16)
+    assert caps[-1] == caps[2]  # no growth after the first rewrites
+    want = {}
+    O.write(want, meta, (Ellipsis,), v)
+    O.write(want, meta, (slice(5, 70), slice(9, 11)), np.float32(9))
+    got = {k: b for k, b in st.to_dict().items() if k.startswith("c/")}
+    assert got == want

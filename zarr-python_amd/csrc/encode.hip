@@ -488,6 +488,12 @@ int launch_encode(const EncodeParams& p, hipStream_t stream, int max_grid) {
         EncodeFn fn = pick_encode_pair(crc, p.g.itemsize, swap);
         if (!fn) return ZHIP_E_UNSUPPORTED;
         if (p.n_units == 0) return ZHIP_OK;
+        // an even unit count <= 32 per chunk: the last arrival of each chunk writes
+        // its non-empty flag; otherwise the kernel ORs into the flags -> zero them
+        if ((p.nseg & 1u) || p.nseg > 32u) {
+            if (hipMemsetAsync(p.nonempty, 0, (size_t)p.n_chunks * sizeof(uint32_t), stream) != hipSuccess)
+                return ZHIP_E_HIP;
+        }
         hipLaunchKernelGGL(fn, dim3((p.n_units + 1u) / 2u), dim3(kThreads), 0, stream, p);
         return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
     }
@@ -495,6 +501,9 @@ int launch_encode(const EncodeParams& p, hipStream_t stream, int max_grid) {
                       : (p.fast ? pick_encode<false, true>(p.g.itemsize, swap) : pick_encode<false, false>(p.g.itemsize, swap));
     if (!fn) return ZHIP_E_UNSUPPORTED;
     if (p.n_units == 0) return ZHIP_OK;
+    // the persistent encode ORs each unit's non-empty bit into its chunk's flag
+    if (hipMemsetAsync(p.nonempty, 0, (size_t)p.n_chunks * sizeof(uint32_t), stream) != hipSuccess)
+        return ZHIP_E_HIP;
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(fn), kThreads, 0) ==
             hipSuccess && per_cu > 0)

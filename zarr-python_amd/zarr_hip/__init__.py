@@ -8,13 +8,15 @@ Drop-in for zarr-python's CodecPipeline (src/zarr/abc/codec.py:315-508): see
 """
 
 from .array import Array, ArrayMetadata, ChunkNotFoundError
+from .buffer import Buffer, BufferPrototype, NDBuffer, buffer_prototype
 from .codecs import BytesCodec, Crc32cCodec, ShardingCodec, TransposeCodec
 from .pipeline import DecodeProgram, HipCodecPipeline, ReadGraph
 from .spec import ArrayConfig, ArraySpec, GetResult
 from .store import DeviceStore, LocalStore, MemoryStore, StorePath
 
 __all__ = [
-    "Array", "ArrayMetadata", "ArrayConfig", "ArraySpec", "BytesCodec", "ChunkNotFoundError",
+    "Array", "ArrayMetadata", "ArrayConfig", "ArraySpec", "Buffer", "BufferPrototype", "BytesCodec",
+    "ChunkNotFoundError", "NDBuffer", "buffer_prototype",
     "Crc32cCodec", "DecodeProgram", "DeviceStore", "GetResult", "HipCodecPipeline", "LocalStore",
     "MemoryStore", "ReadGraph", "ShardingCodec", "StorePath", "TransposeCodec",
 ]

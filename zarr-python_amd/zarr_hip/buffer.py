@@ -1,9 +1,23 @@
-"""Device buffers on ROCm: torch tensors stand in for the reference's CuPy-backed
-gpu.Buffer / gpu.NDBuffer (src/zarr/core/buffer/gpu.py:34-237), which cannot
-run on ROCm.  torch is used for device memory and streams only; every codec
-operation on these buffers is a HIP kernel of this package."""
+"""Device buffers on ROCm: the counterpart of the reference's CuPy-backed
+``zarr.buffer.gpu.Buffer`` / ``NDBuffer`` (src/zarr/core/buffer/gpu.py:34-237),
+which cannot run on ROCm.  Both wrap torch tensors in HBM: torch is used for
+device memory and streams only; every codec operation on these buffers is a
+HIP kernel of this package.
+
+``Buffer`` / ``NDBuffer`` implement the reference's buffer interface
+(src/zarr/core/buffer/core.py:130-567) and ``buffer_prototype`` is the
+``BufferPrototype`` (core.py:570-586) a zarr array is given to get device
+arrays back.  ``register()`` registers both with zarr's registry under the
+qualnames ``zarr_hip.buffer.Buffer`` / ``zarr_hip.buffer.NDBuffer``
+(src/zarr/registry.py:270-294; selected with the ``buffer`` / ``ndbuffer``
+config keys, src/zarr/core/config.py:155-156) when zarr is importable; when it
+is, the classes also subclass zarr's abstract bases, so the stores' isinstance
+checks accept them.
+"""
 
 from __future__ import annotations
+
+from typing import Any, Iterable, NamedTuple
 
 import numpy as np
 
@@ -24,10 +38,26 @@ def torch_dtype(dtype) -> "torch.dtype":
             np.dtype("float32"): torch.float32, np.dtype("float64"): torch.float64,
             np.dtype("complex64"): torch.complex64,
         }
-    dt = np.dtype(dtype).newbyteorder("=")
+    from .interop import native_dtype
+
+    dt = native_dtype(dtype).newbyteorder("=")
     if dt not in _MAP:
         raise TypeError(f"dtype {dt} has no device representation")
     return _MAP[dt]
+
+
+def numpy_dtype(td) -> np.dtype:
+    torch_dtype(np.float32)  # build the map
+    for k, v in _MAP.items():
+        if v == td:
+            return k
+    raise TypeError(f"torch dtype {td} has no numpy counterpart here")
+
+
+def default_device():
+    import torch
+
+    return torch.device("cuda", torch.cuda.current_device())
 
 
 def empty(shape, dtype, device, order: str = "C"):
@@ -48,7 +78,9 @@ def to_numpy(t, dtype) -> np.ndarray:
     pageable bounce); the returned array keeps the pinned block alive."""
     import torch
 
-    dt = np.dtype(dtype).newbyteorder("=")
+    from .interop import native_dtype
+
+    dt = native_dtype(dtype).newbyteorder("=")
     c = t.contiguous() if not t.is_contiguous() else t
     flat = c.reshape(-1).view(torch.uint8)
     if not flat.is_cuda:
@@ -57,3 +89,272 @@ def to_numpy(t, dtype) -> np.ndarray:
     host.copy_(flat, non_blocking=True)
     torch.cuda.current_stream(flat.device).synchronize()
     return host.numpy().view(dt).reshape(tuple(t.shape))
+
+
+def _to_device(a, dtype=None):
+    """Any array-like -> torch CUDA tensor (zero-copy when already on the device)."""
+    import torch
+
+    from .interop import device_tensor, host_array
+
+    t = device_tensor(a)
+    if t is not None:
+        return t
+    h = host_array(a)
+    if h is None:
+        h = np.asarray(a)
+    if dtype is not None:
+        h = h.astype(dtype, copy=False)
+    h = np.ascontiguousarray(h)
+    if h.dtype.byteorder not in ("=", "|"):
+        h = h.astype(h.dtype.newbyteorder("="))
+    flat = torch.from_numpy(h.reshape(-1).view(np.uint8).copy()).to(default_device())
+    if h.dtype == np.uint8 or h.size == 0:
+        return flat.view(torch.uint8).reshape(h.shape) if h.size else \
+            torch.empty(h.shape, dtype=torch_dtype(h.dtype), device=default_device())
+    return flat.view(torch_dtype(h.dtype)).reshape(h.shape)
+
+
+def _zarr_bases():
+    try:  # pragma: no cover - zarr needs Python >= 3.12
+        from zarr.core.buffer import core as zcore
+
+        return zcore.Buffer, zcore.NDBuffer
+    except Exception:
+        return object, object
+
+
+_BufferBase, _NDBufferBase = _zarr_bases()
+
+
+class Buffer(_BufferBase):
+    """A flat contiguous byte block in HBM (1-D uint8 torch tensor).
+
+    gpu.Buffer (src/zarr/core/buffer/gpu.py:34-118) restated for ROCm: host
+    inputs are copied to the device; device inputs (torch, DLPack, this
+    package's buffers) are wrapped without a copy."""
+
+    def __init__(self, array_like) -> None:
+        import torch
+
+        t = _to_device(array_like)
+        if t.dim() != 1:
+            raise ValueError("array_like: only 1-dim allowed")
+        if t.dtype != torch.uint8:
+            raise ValueError("array_like: only byte dtype allowed")
+        self._data = t
+
+    @classmethod
+    def create_zero_length(cls) -> "Buffer":
+        import torch
+
+        return cls(torch.empty(0, dtype=torch.uint8, device=default_device()))
+
+    @classmethod
+    def from_array_like(cls, array_like) -> "Buffer":
+        return cls(array_like)
+
+    @classmethod
+    def from_buffer(cls, buffer) -> "Buffer":
+        if isinstance(buffer, Buffer):
+            return cls(buffer._data)
+        from .interop import byte_payload
+
+        return cls(byte_payload(buffer))
+
+    @classmethod
+    def from_bytes(cls, bytes_like) -> "Buffer":
+        return cls(np.frombuffer(bytes(bytes_like), dtype=np.uint8))
+
+    def as_array_like(self):
+        return self._data
+
+    def as_numpy_array(self) -> np.ndarray:
+        return to_numpy(self._data, np.uint8)
+
+    def as_buffer_like(self):
+        return self.as_numpy_array()
+
+    def to_bytes(self) -> bytes:
+        return self.as_numpy_array().tobytes()
+
+    def __getitem__(self, key: slice) -> "Buffer":
+        if not isinstance(key, slice) or key.step not in (None, 1):
+            raise TypeError("Buffer only supports 1-d contiguous slices")
+        return self.__class__(self._data[key])
+
+    def __setitem__(self, key: slice, value: Any) -> None:
+        if not isinstance(key, slice) or key.step not in (None, 1):
+            raise TypeError("Buffer only supports 1-d contiguous slices")
+        self._data[key] = _to_device(value.as_array_like() if hasattr(value, "as_array_like")
+                                     else value, np.uint8)
+
+    def __len__(self) -> int:
+        return int(self._data.numel())
+
+    def combine(self, others: Iterable) -> "Buffer":
+        import torch
+
+        parts = [self._data] + [Buffer.from_buffer(o)._data for o in others]
+        return self.__class__(torch.cat(parts))
+
+    def __add__(self, other) -> "Buffer":
+        return self.combine([other])
+
+    def __eq__(self, other: object) -> bool:
+        import torch
+
+        if not hasattr(other, "__len__") or len(other) != len(self):
+            return False
+        o = other._data if isinstance(other, Buffer) else Buffer.from_buffer(other)._data
+        return bool(torch.equal(self._data, o))
+
+    __hash__ = None
+
+
+class NDBuffer(_NDBufferBase):
+    """An n-dimensional array in HBM (any-strided torch tensor).
+
+    gpu.NDBuffer (src/zarr/core/buffer/gpu.py:121-227) restated for ROCm.  The
+    codec pipeline decodes straight into ``as_ndarray_like()`` (the tensor
+    itself), so an ``out`` NDBuffer of this class is written in place by the
+    HIP kernels."""
+
+    def __init__(self, array) -> None:
+        self._data = _to_device(array)
+
+    @classmethod
+    def create(cls, *, shape: Iterable[int], dtype, order: str = "C", fill_value: Any | None = None):
+        ret = cls(empty(tuple(shape), dtype, default_device(), order))
+        if fill_value is not None:
+            ret.fill(fill_value)
+        return ret
+
+    @classmethod
+    def empty(cls, shape: tuple[int, ...], dtype, order: str = "C"):
+        return cls(empty(tuple(shape), dtype, default_device(), order))
+
+    @classmethod
+    def from_ndarray_like(cls, ndarray_like):
+        return cls(ndarray_like)
+
+    @classmethod
+    def from_numpy_array(cls, array_like):
+        return cls(np.asarray(array_like))
+
+    def as_ndarray_like(self):
+        return self._data
+
+    def as_numpy_array(self) -> np.ndarray:
+        return to_numpy(self._data, self.dtype)
+
+    def as_scalar(self):
+        if self._data.numel() != 1:
+            raise ValueError("Buffer does not contain a single scalar value")
+        return self.as_numpy_array().reshape(()).item() if self.dtype.kind != "f" else \
+            self.dtype.type(self.as_numpy_array().reshape(())[()])
+
+    @property
+    def dtype(self) -> np.dtype:
+        return numpy_dtype(self._data.dtype)
+
+    @property
+    def shape(self) -> tuple[int, ...]:
+        return tuple(self._data.shape)
+
+    @property
+    def byteorder(self) -> str:
+        import sys
+
+        return sys.byteorder
+
+    def reshape(self, newshape):
+        return self.__class__(self._data.reshape(newshape))
+
+    def squeeze(self, axis: tuple[int, ...]):
+        t = self._data
+        for a in sorted(axis, reverse=True):
+            t = t.squeeze(a)
+        return self.__class__(t)
+
+    def astype(self, dtype, order: str = "K"):
+        from .interop import native_dtype
+
+        return self.__class__(self._data.to(torch_dtype(native_dtype(dtype))))
+
+    def __getitem__(self, key: Any):
+        return self.__class__(self._data[key])
+
+    def __setitem__(self, key: Any, value: Any) -> None:
+        if isinstance(value, NDBuffer):
+            value = value._data
+        elif hasattr(value, "as_ndarray_like"):
+            value = _to_device(value.as_ndarray_like(), self.dtype)
+        else:  # numpy / python scalars and arrays (0-d keeps NaN payloads and -0.0)
+            value = _to_device(np.asarray(value) if np.isscalar(value) else value, self.dtype)
+        self._data[key] = value
+
+    def __len__(self) -> int:
+        return int(self._data.shape[0])
+
+    def __repr__(self) -> str:
+        return f"<NDBuffer shape={self.shape} dtype={self.dtype} device={self._data.device}>"
+
+    def all_equal(self, other: Any, equal_nan: bool = True) -> bool:
+        """NDBuffer.all_equal (core.py:534-558): bitwise against 0 (so -0.0 and NaN
+        payloads count as non-empty), NaN-equal otherwise when equal_nan."""
+        import torch
+
+        if other is None:
+            return False
+        t = self._data
+        fv = np.asarray(other, dtype=self.dtype)
+        if np.asarray(other).dtype.kind == "f" and other == 0.0:
+            # bit patterns, so -0.0 and +0.0 differ (core.py:539-547)
+            iv = {1: torch.uint8, 2: torch.int16, 4: torch.int32, 8: torch.int64}[t.element_size()]
+            bits = int(fv.reshape(1).view({1: np.uint8, 2: np.int16, 4: np.int32, 8: np.int64}[
+                fv.itemsize])[0])
+            return bool((t.contiguous().view(iv) == bits).all().item())
+        ref = torch.as_tensor(fv, device=t.device).to(t.dtype)
+        eq = t == ref
+        if equal_nan and self.dtype.kind in "fc" and bool(np.isnan(fv).all()):
+            eq = eq | torch.isnan(t)
+        return bool(eq.all().item())
+
+    def fill(self, value: Any) -> None:
+        import torch
+
+        fv = np.asarray(value, dtype=self.dtype).reshape(1)
+        self._data.copy_(torch.from_numpy(fv.copy()).to(self._data.device).reshape(
+            (1,) * self._data.dim()).expand_as(self._data) if self._data.dim() else
+            torch.from_numpy(fv.copy()).to(self._data.device).reshape(()))
+
+    def copy(self):
+        return self.__class__(self._data.clone())
+
+    def transpose(self, axes):
+        if axes is None:
+            axes = tuple(reversed(range(self._data.dim())))
+        return self.__class__(self._data.permute(*axes))
+
+
+class BufferPrototype(NamedTuple):
+    """core.BufferPrototype (src/zarr/core/buffer/core.py:570-586)."""
+
+    buffer: type
+    nd_buffer: type
+
+
+buffer_prototype = BufferPrototype(buffer=Buffer, nd_buffer=NDBuffer)
+
+
+def register() -> bool:
+    """Register the ROCm buffers with zarr's registry (registry.py:270-294);
+    False when zarr is not importable (Python < 3.12 here)."""
+    try:  # pragma: no cover - needs zarr
+        from zarr.registry import register_buffer, register_ndbuffer
+    except Exception:
+        return False
+    register_buffer(Buffer, qualname="zarr_hip.buffer.Buffer")
+    register_ndbuffer(NDBuffer, qualname="zarr_hip.buffer.NDBuffer")
+    return True

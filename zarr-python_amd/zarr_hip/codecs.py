@@ -48,7 +48,8 @@ class BytesCodec:
     @classmethod
     def from_dict(cls, data: Any) -> "BytesCodec":
         conf = _named(data, "bytes")
-        return cls(endian=conf.get("endian"))
+        e = conf.get("endian")
+        return cls(endian=None if e is None else str(getattr(e, "value", e)))
 
     def to_dict(self) -> dict:
         if self.endian is None:
@@ -183,7 +184,8 @@ class ShardingCodec:
                    index_codecs=tuple(conf.get("index_codecs", (
                        {"name": "bytes", "configuration": {"endian": "little"}},
                        {"name": "crc32c"}))),
-                   index_location=conf.get("index_location", "end"))
+                   index_location=str(getattr(conf.get("index_location", "end"), "value",
+                                              conf.get("index_location", "end"))))
 
     def to_dict(self) -> dict:
         return {"name": "sharding_indexed", "configuration": {
@@ -243,16 +245,27 @@ _REGISTRY = {
 
 
 def parse_codecs(codecs) -> list:
+    """Codec configurations -> this package's codec objects.  Accepts its own
+    codecs, JSON dicts / names (the zarr.json form), and zarr's Codec instances
+    (duck-typed through ``to_dict()``, src/zarr/abc/codec.py:99-225, the form
+    ``CodecPipeline.from_codecs`` receives); a sharding codec's write-time
+    ``subchunk_write_order`` (not part of its metadata, sharding.py:402-446) is
+    carried over from the instance."""
     out = []
     for c in codecs:
         if isinstance(c, (BytesCodec, Crc32cCodec, TransposeCodec, ShardingCodec)):
             out.append(c)
             continue
-        name = c if isinstance(c, str) else c["name"]
+        conf = c.to_dict() if hasattr(c, "to_dict") and not isinstance(c, dict) else c
+        name = conf if isinstance(conf, str) else conf["name"]
         if name not in _REGISTRY:
             raise NotImplementedError(
                 f"codec {name!r} is not on the GPU fixed-size path (compression stays on the host)")
-        out.append(_REGISTRY[name].from_dict(c))
+        parsed = _REGISTRY[name].from_dict(conf)
+        order = getattr(c, "subchunk_write_order", None)
+        if isinstance(parsed, ShardingCodec) and order is not None and not isinstance(c, dict):
+            parsed = replace(parsed, subchunk_write_order=str(order))
+        out.append(parsed)
     return out
 
 

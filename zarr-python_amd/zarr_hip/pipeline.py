@@ -25,8 +25,9 @@ import numpy as np
 from . import _native as N
 from . import staging
 from .codecs import ShardingCodec, evolve_codecs, parse_codecs, split_codecs
+from .interop import device_tensor, host_array
 from .planner import CHUNK_DT, SEL_DT, STATUS_DT, ChainInfo, Tables, analyze_chain, plan_decode, predict_rows
-from .spec import ArraySpec, GetResult
+from .spec import ArraySpec, GetResult, coerce_spec
 from .store import DeviceRef, DeviceStore, _resolve_range
 
 
@@ -258,9 +259,18 @@ class ReadGraph:
 
 
 def _device_resident(batch: list) -> bool:
-    """True when every ByteGetter reads from a DeviceStore (bytes already in HBM)."""
-    return all(isinstance(getattr(it[0], "store", None), DeviceStore)
-               or isinstance(getattr(it[0], "value", None), DeviceRef) for it in batch)
+    """True when every ByteGetter reads from a DeviceStore (bytes already in HBM);
+    raw getters holding nothing (absent chunks) go with either."""
+    def dev(it):
+        bg = it[0]
+        if isinstance(getattr(bg, "store", None), DeviceStore):
+            return True
+        if isinstance(bg, _Raw):
+            return bg.value is None or isinstance(bg.value, DeviceRef)
+        return False
+
+    return all(dev(it) for it in batch) and any(
+        not (isinstance(it[0], _Raw) and it[0].value is None) for it in batch)
 
 
 @dataclass(frozen=True)
@@ -282,7 +292,27 @@ class HipCodecPipeline:
         aa, ab, bb = split_codecs(cl)
         return cls(cl, aa, ab, bb, batch_size or (1 << 30))
 
-    def evolve_from_array_spec(self, array_spec: ArraySpec) -> "HipCodecPipeline":
+    @classmethod
+    def from_array_metadata_and_store(cls, array_metadata, store) -> "HipCodecPipeline":
+        """The hook create_codec_pipeline tries first (src/zarr/core/array.py:221-228,
+        src/zarr/abc/codec.py:352-369): the v3 metadata's codecs evolved against
+        its chunk spec (array.py:237-254).  v2 metadata and irregular chunk grids
+        raise NotImplementedError, which sends zarr down its from_codecs path
+        (and, for codecs off the GPU path, to a loud NotImplementedError there)."""
+        codecs = getattr(array_metadata, "codecs", None)
+        grid = getattr(array_metadata, "chunk_grid", None)
+        chunk_shape = getattr(grid, "chunk_shape", None)
+        if codecs is None or chunk_shape is None:
+            raise NotImplementedError(
+                "HipCodecPipeline.from_array_metadata_and_store needs v3 metadata on a regular grid")
+        dtype = getattr(array_metadata, "data_type", None)
+        if dtype is None:
+            dtype = getattr(array_metadata, "dtype")
+        spec = ArraySpec(tuple(chunk_shape), dtype, getattr(array_metadata, "fill_value", None))
+        return cls.from_codecs(codecs).evolve_from_array_spec(spec)
+
+    def evolve_from_array_spec(self, array_spec) -> "HipCodecPipeline":
+        array_spec = coerce_spec(array_spec)
         ev = evolve_codecs(self.codecs, array_spec)
         aa, ab, bb = split_codecs(ev)
         return type(self)(ev, aa, ab, bb, self.batch_size, self.predict_loads)
@@ -301,10 +331,13 @@ class HipCodecPipeline:
         return self.supports_partial_decode
 
     def validate(self, *, shape, dtype=None, chunk_grid=None, chunk_shape=None) -> None:
+        if chunk_shape is None and chunk_grid is not None:
+            chunk_shape = getattr(chunk_grid, "chunk_shape", None)
         for c in self.codecs:
             c.validate(shape=shape, dtype=dtype, chunk_grid=chunk_grid, chunk_shape=chunk_shape)
 
-    def compute_encoded_size(self, byte_length: int, array_spec: ArraySpec | None = None) -> int:
+    def compute_encoded_size(self, byte_length: int, array_spec=None) -> int:
+        array_spec = None if array_spec is None else coerce_spec(array_spec)
         for c in self.codecs:
             byte_length = c.compute_encoded_size(byte_length, array_spec)
         return byte_length
@@ -345,9 +378,13 @@ class HipCodecPipeline:
         return pipe, batch_s, arr
 
     # ---------------------------------------------------------------- read
-    def prepare_read(self, batch_info: Iterable, out, drop_axes: tuple = ()) -> DecodeProgram:
+    def prepare_read(self, batch_info: Iterable, out, drop_axes: tuple = (),
+                     item_out_extra=None) -> DecodeProgram:
+        """Plan a batch once: tables uploaded, launches ready.  `out` is a device
+        tensor; item_out_extra (bytes per item) shifts each item's out position,
+        so one launch can decode a batch into the slices of a stacked out."""
         torch = _torch()
-        batch = list(batch_info)
+        batch = normalize_batch(batch_info)
         if not batch:
             raise ValueError("empty batch")
         if not isinstance(out, torch.Tensor) or not out.is_cuda:
@@ -355,7 +392,7 @@ class HipCodecPipeline:
         ss = self._shard_space(batch, out, drop_axes)
         if ss is not None:
             pipe, batch_s, out_s = ss
-            return pipe.prepare_read(batch_s, out_s, drop_axes)
+            return pipe.prepare_read(batch_s, out_s, drop_axes, item_out_extra)
         spec: ArraySpec = batch[0][1]
         device = out.device
         chain: ChainInfo = analyze_chain(self.codecs, spec)
@@ -374,7 +411,7 @@ class HipCodecPipeline:
             raise TypeError("out dtype itemsize does not match the array dtype")
         ostr = [int(s) * itemsize for s in out.stride()]
         with torch.cuda.device(device):
-            t = plan_decode(chain, spec, items, ostr, out.data_ptr(), drop_axes, resolved)
+            t = plan_decode(chain, spec, items, ostr, out.data_ptr(), drop_axes, resolved, item_out_extra)
             if self.predict_loads:
                 predict_rows(t, chain, spec, size)
             # fuse the shard-index CRC checks into the data launch
@@ -393,12 +430,25 @@ class HipCodecPipeline:
 
     def read_sync(self, batch_info: Iterable, out, drop_axes: tuple = (),
                   max_workers: int = 1) -> tuple[GetResult, ...]:
-        batch = list(batch_info)
+        """FusedCodecPipeline.read_sync (codec_pipeline.py:1095-1172) on the GPU.
+
+        `out` is a device tensor, this package's NDBuffer, any NDBuffer whose
+        ``as_ndarray_like()`` is a ROCm tensor / DLPack capsule (decoded in
+        place), or a host NDBuffer / numpy array: then the batch decodes into an
+        HBM twin of `out` and the result is copied back (the regions no item
+        selects are carried through unchanged)."""
+        batch = normalize_batch(batch_info)
         if not batch:
             return ()
-        prog = self.prepare_read(batch, out, drop_axes)
+        dev_out, host_out = _resolve_out(out, batch, drop_axes)
+        prog = self.prepare_read(batch, dev_out, drop_axes)
         prog.launch()
-        return prog.results()
+        res = prog.results()
+        if host_out is not None:
+            from .buffer import to_numpy
+
+            np.copyto(host_out, to_numpy(dev_out, host_out.dtype), casting="no")
+        return res
 
     async def read(self, batch_info: Iterable, out, drop_axes: tuple = ()) -> tuple[GetResult, ...]:
         # one thread hop per batch, as FusedCodecPipeline.read (codec_pipeline.py:1287-1289)
@@ -407,17 +457,26 @@ class HipCodecPipeline:
     # --------------------------------------------------------------- write
     def write_sync(self, batch_info: Iterable, value, drop_axes: tuple = (),
                    max_workers: int = 1) -> None:
-        """FusedCodecPipeline.write_sync (codec_pipeline.py:1174-1253) on the GPU."""
+        """FusedCodecPipeline.write_sync (codec_pipeline.py:1174-1253) on the GPU.
+        `value` is a device tensor, an NDBuffer (device or host), a numpy array
+        or a scalar."""
+        return self._write_sync(batch_info, value, drop_axes, partial_encode=True)
+
+    def _write_sync(self, batch_info, value, drop_axes=(), partial_encode=True) -> None:
         from .writer import ChunkWriter
 
         torch = _torch()
-        batch = list(batch_info)
+        batch = normalize_batch(batch_info)
         if not batch:
             return
+        value = _resolve_value(value)
         ss = self._shard_space(batch, value, drop_axes)
         if ss is not None:
             pipe, batch_s, value_s = ss
-            return pipe.write_sync(batch_s, value_s, drop_axes)
+            # with array->array codecs around it the sharding codec encodes whole
+            # shards (ChunkTransform -> ShardingCodec._encode_sync, sharding.py:716-772),
+            # not the partial-encode path (codec_pipeline.py:1212)
+            return pipe._write_sync(batch_s, value_s, drop_axes, partial_encode=False)
         spec: ArraySpec = batch[0][1]
         device = value.device if isinstance(value, torch.Tensor) and value.is_cuda else None
         if device is None:
@@ -425,27 +484,151 @@ class HipCodecPipeline:
             device = getattr(st, "device", None) or torch.device("cuda", torch.cuda.current_device())
         with torch.cuda.device(device):
             w = ChunkWriter(self.codecs, spec, None or spec.shape, device)
-            w.write(batch, value, self.codecs, drop_axes)
+            w.write(batch, value, self.codecs, drop_axes, partial_encode=partial_encode)
 
     async def write(self, batch_info: Iterable, value, drop_axes: tuple = ()) -> None:
         await asyncio.to_thread(self.write_sync, list(batch_info), value, drop_axes)
 
-    async def decode(self, chunk_bytes_and_specs: Iterable) -> list:
-        """Decode standalone chunks (Buffer | None, ArraySpec) -> device arrays."""
+    def decode_sync(self, chunk_bytes_and_specs: Iterable) -> list:
+        """Decode standalone chunks (Buffer | None, ArraySpec) -> NDBuffer | None
+        (abc/codec.py:417-434): one GPU decode per chunk into a device array,
+        returned as an NDBuffer of the spec's prototype (this package's device
+        NDBuffer when the spec names none)."""
         torch = _torch()
+        from .buffer import torch_dtype
+
         res = []
         for raw, spec in chunk_bytes_and_specs:
             if raw is None:
                 res.append(None)
                 continue
-            from .buffer import torch_dtype
-
-            dev = raw.arena.device if isinstance(raw, DeviceRef) else torch.device("cuda")
+            spec = coerce_spec(spec)
+            raw = raw if isinstance(raw, (DeviceRef, bytes, bytearray, memoryview)) else \
+                staging.staged_bytes(raw)
+            dev = raw.arena.device if isinstance(raw, DeviceRef) else (
+                raw.device if isinstance(raw, torch.Tensor) else torch.device("cuda", torch.cuda.current_device()))
             out = torch.empty(spec.shape, dtype=torch_dtype(spec.dtype), device=dev)
             sel = tuple(slice(0, s, 1) for s in spec.shape)
             self.read_sync([(_Raw(raw), spec, sel, sel, True)], out)
-            res.append(out)
+            res.append(_as_nd_buffer(out, spec))
         return res
+
+    async def decode(self, chunk_bytes_and_specs: Iterable) -> list:
+        return await asyncio.to_thread(self.decode_sync, list(chunk_bytes_and_specs))
+
+    def encode_sync(self, chunk_arrays_and_specs: Iterable) -> list:
+        """Encode standalone chunks (NDBuffer | None, ArraySpec) -> Buffer | None
+        (abc/codec.py:436-453): the GPU encode of each chunk (empty chunks are
+        None unless write_empty_chunks, chunk_utils.py:43-58), returned as a
+        Buffer of the spec's prototype (this package's device Buffer when the
+        spec names none).  The encoded bytes stay in HBM for device Buffers."""
+        res = []
+        for arr, spec in chunk_arrays_and_specs:
+            if arr is None:
+                res.append(None)
+                continue
+            spec = coerce_spec(spec)
+            sink = _CollectSetter()
+            full = tuple(slice(0, s, 1) for s in spec.shape)
+            self._write_sync([(sink, spec, full, full, True)], arr, partial_encode=False)
+            res.append(None if sink.value is None else _as_buffer(sink.value, spec))
+        return res
+
+    async def encode(self, chunk_arrays_and_specs: Iterable) -> list:
+        return await asyncio.to_thread(self.encode_sync, list(chunk_arrays_and_specs))
+
+
+def normalize_batch(batch_info: Iterable) -> list:
+    """batch_info with every spec as this package's ArraySpec (zarr's ArraySpec
+    carries a ZDType dtype, array_spec.py:137-186)."""
+    out = []
+    for it in batch_info:
+        it = tuple(it)
+        out.append((it[0], coerce_spec(it[1])) + it[2:])
+    return out
+
+
+def _selection_items(osel) -> int:
+    n = 1
+    for s in osel:
+        if isinstance(s, slice):
+            a, b, st = s.start or 0, s.stop, s.step or 1
+            n *= max(0, -((a - b) // st))
+    return n
+
+
+def _resolve_out(out, batch, drop_axes):
+    """(device tensor decoded into, host array to copy back into | None)."""
+    torch = _torch()
+    t = device_tensor(out)
+    if t is not None:
+        return t, None
+    h = host_array(out)
+    if h is None:
+        raise TypeError(f"cannot decode into a {type(out).__name__}")
+    if not h.flags.writeable:
+        raise ValueError("out is read-only")
+    from .buffer import torch_dtype
+
+    dev = None
+    for it in batch:
+        st = getattr(it[0], "store", None)
+        dev = getattr(st, "device", None)
+        if dev is not None:
+            break
+    dev = dev or torch.device("cuda", torch.cuda.current_device())
+    twin = torch.empty(h.shape, dtype=torch_dtype(h.dtype), device=dev)
+    covered = sum(_selection_items(it[3]) for it in batch)
+    if covered < h.size:  # regions no chunk writes keep their host values
+        twin.copy_(torch.from_numpy(np.ascontiguousarray(h).astype(h.dtype.newbyteorder("="))))
+    return twin, h
+
+
+def _resolve_value(value):
+    """A write's value as a device tensor or a host numpy array / scalar."""
+    t = device_tensor(value)
+    if t is not None:
+        return t
+    if isinstance(value, np.ndarray) or np.isscalar(value):
+        return value
+    h = host_array(value)
+    return value if h is None else h
+
+
+class _CollectSetter:
+    """A ByteSetter that keeps what the writer stores (encode())."""
+
+    value = None
+
+    def get_sync(self, prototype=None, byte_range=None):
+        return None
+
+    def set_sync(self, value) -> None:
+        self.value = value
+
+    def delete_sync(self) -> None:
+        self.value = None
+
+
+def _as_nd_buffer(t, spec):
+    from .buffer import NDBuffer, to_numpy
+
+    proto = getattr(spec, "prototype", None)
+    cls = getattr(proto, "nd_buffer", None)
+    if cls is None or cls is NDBuffer:
+        return NDBuffer(t)
+    return cls.from_numpy_array(to_numpy(t, spec.dtype))
+
+
+def _as_buffer(value, spec):
+    from .buffer import Buffer
+    from .interop import byte_payload
+
+    proto = getattr(spec, "prototype", None)
+    cls = getattr(proto, "buffer", None)
+    if cls is None or cls is Buffer:
+        return Buffer(byte_payload(value))
+    return cls.from_bytes(byte_payload(value, host=True).tobytes())
 
 
 @dataclass(frozen=True)
@@ -456,9 +639,14 @@ class _Raw:
 
     def get_sync(self, prototype=None, byte_range=None):
         v = self.value
+        if v is not None and not isinstance(v, (DeviceRef, bytes, bytearray, memoryview)):
+            v = staging.staged_bytes(v)  # zarr Buffers, device tensors -> bytes / tensor
         if byte_range is None or v is None:
             return v
-        a, b = _resolve_range(byte_range, len(v))
+        n = v.numel() if hasattr(v, "numel") else len(v)
+        a, b = _resolve_range(byte_range, n)
         if isinstance(v, DeviceRef):
             return DeviceRef(v.arena, v.offset + a, b - a)
-        return memoryview(v)[a:b]
+        if isinstance(v, (bytes, bytearray, memoryview)):
+            return memoryview(v)[a:b]
+        return v[a:b]

@@ -259,8 +259,11 @@ def plan_encode(chain: ChainInfo, spec: ArraySpec, items: list, arr_strides_byte
 
 
 def plan_decode(chain: ChainInfo, spec: ArraySpec, items: list, out_strides_bytes,
-                out_base_ptr: int, drop_axes=(), resolved: list | None = None) -> Tables:
+                out_base_ptr: int, drop_axes=(), resolved: list | None = None,
+                item_out_extra=None) -> Tables:
     """items: list of (src_off, src_len, missing, chunk_selection, out_selection).
+    item_out_extra: optional per-item byte offset added to the item's out
+    position (one launch decoding into the slices of a stacked out).
 
     Sharded chains: by default every inner chunk is located by the kernel
     through the shard index in HBM.  With `resolved` (host-staged partial
@@ -294,7 +297,8 @@ def plan_decode(chain: ChainInfo, spec: ArraySpec, items: list, out_strides_byte
             chunks["src"][i] = so
             chunks["src_len"][i] = sl
             chunks["flags"][i] = N.CF_MISSING if miss else 0
-            chunks["out_off"][i] = _out_offset(osel, out_strides_bytes)
+            chunks["out_off"][i] = _out_offset(osel, out_strides_bytes) + \
+                (0 if item_out_extra is None else int(item_out_extra[i]))
         if ndim == 1:
             split = _split_1d(shape_st[0], itemsize, ost_st[0], start, count, step)
             if split:  # the same chunk bytes viewed as (N/R, R): whole rows of R items
@@ -339,7 +343,8 @@ def plan_decode(chain: ChainInfo, spec: ArraySpec, items: list, out_strides_byte
         if pr is None:
             pr = basic_projections(tuple(csel), spec.shape, inner_shape)
             proj_cache[key] = pr
-        base = _out_offset(osel, out_strides_bytes)
+        base = _out_offset(osel, out_strides_bytes) + \
+            (0 if item_out_extra is None else int(item_out_extra[i]))
         m = len(pr.coords)
         oo = base + (pr.out_start * ost_dec[None, :]).sum(axis=1)
         parts.append((i, so, sl, miss, pr, oo, m))
@@ -356,6 +361,7 @@ def plan_decode(chain: ChainInfo, spec: ArraySpec, items: list, out_strides_byte
         sl_ = slice(pos, pos + m)
         slots = (pr.coords * cps_strides[None, :]).sum(axis=1)
         chunks["out_off"][sl_] = oo
+        chunks["slot"][sl_] = slots
         if resolved is not None:
             r = resolved[i]
             if r is None or miss:

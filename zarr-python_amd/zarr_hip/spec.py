@@ -34,7 +34,10 @@ class ArraySpec:
 
     def __post_init__(self):
         object.__setattr__(self, "shape", tuple(int(s) for s in self.shape))
-        object.__setattr__(self, "dtype", np.dtype(self.dtype))
+        dt = self.dtype
+        object.__setattr__(self, "dtype", np.dtype(dt.to_native_dtype() if hasattr(dt, "to_native_dtype")
+                                                   else dt))
+        object.__setattr__(self, "config", coerce_config(self.config))
 
     @property
     def ndim(self) -> int:
@@ -51,3 +54,36 @@ class ArraySpec:
         if fv is None:
             fv = 0
         return np.asarray(fv, dtype=self.dtype).astype(self.dtype.newbyteorder("=")).tobytes()
+
+
+def coerce_config(config) -> ArrayConfig:
+    """This package's ArrayConfig from zarr's (array_spec.py:39-119) or a dict."""
+    if isinstance(config, ArrayConfig):
+        return config
+    if config is None:
+        return ArrayConfig()
+    get = config.get if isinstance(config, dict) else (lambda k, d: getattr(config, k, d))
+    base = ArrayConfig()
+    return ArrayConfig(
+        order=get("order", base.order),
+        write_empty_chunks=bool(get("write_empty_chunks", base.write_empty_chunks)),
+        read_missing_chunks=bool(get("read_missing_chunks", base.read_missing_chunks)),
+        sharding_coalesce_max_gap_bytes=int(get("sharding_coalesce_max_gap_bytes",
+                                                base.sharding_coalesce_max_gap_bytes)),
+        sharding_coalesce_max_bytes=int(get("sharding_coalesce_max_bytes",
+                                            base.sharding_coalesce_max_bytes)))
+
+
+def coerce_spec(spec) -> ArraySpec:
+    """This package's ArraySpec from zarr's (array_spec.py:137-186): the dtype is
+    a ZDType there (``to_native_dtype()``), the fill value a numpy scalar, the
+    prototype a BufferPrototype (kept: writes hand it back to the store)."""
+    if isinstance(spec, ArraySpec):
+        return spec
+    from .interop import native_dtype
+
+    fv = spec.fill_value
+    if hasattr(fv, "item") and not isinstance(fv, np.generic):
+        fv = fv.item()
+    return ArraySpec(tuple(int(s) for s in spec.shape), native_dtype(spec.dtype), fv,
+                     coerce_config(getattr(spec, "config", None)), getattr(spec, "prototype", None))

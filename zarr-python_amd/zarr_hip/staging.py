@@ -24,7 +24,8 @@ from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 
-from .store import ALIGN, TAIL_SLACK, DeviceRef, RangeByteRequest, SuffixByteRequest
+from .interop import byte_payload, is_missing_key_error, request_classes, staged_bytes
+from .store import ALIGN, TAIL_SLACK, DeviceRef
 
 WINDOW = int(os.environ.get("ZARR_HIP_STAGE_WINDOW", str(8 << 20)))
 MAX_U64 = np.uint64(0xFFFFFFFFFFFFFFFF)
@@ -119,13 +120,15 @@ def stage(layout: StagingLayout, device):
 def gather_sources(batch: list, device):
     """Resolve every ByteGetter to (offset, length, missing) inside ONE device
     buffer: the shared arena for DeviceStore batches, else a staged copy.
+    ByteGetters may be this package's or zarr's (whose get_sync returns a
+    Buffer, src/zarr/storage/_common.py:247-258).
     Returns (src, size, [(off, len, missing)], keepalive)."""
     import torch
 
     raws = []
     for item in batch:
         bg = item[0]
-        raws.append(bg.get_sync(prototype=None) if hasattr(bg, "get_sync") else bg)
+        raws.append(staged_bytes(bg.get_sync(prototype=None) if hasattr(bg, "get_sync") else bg))
     arenas = {id(r.arena): r.arena for r in raws if isinstance(r, DeviceRef)}
     all_dev = all(r is None or isinstance(r, DeviceRef) for r in raws)
     if all_dev and len(arenas) <= 1:
@@ -143,17 +146,26 @@ def gather_sources(batch: list, device):
     for r in raws:
         if r is None:
             srcs.append((0, 0, True))
-        elif isinstance(r, DeviceRef):  # a foreign arena: device-to-device copy below
-            off = lay.reserve(r.length)
+        elif isinstance(r, (DeviceRef, torch.Tensor)):  # device bytes elsewhere: D2D copy below
+            n = r.length if isinstance(r, DeviceRef) else r.numel()
+            off = lay.reserve(n)
             dev_refs.append((r, off))
-            srcs.append((off, r.length, False))
+            srcs.append((off, n, False))
         else:
             off, n = lay.add(r)
             srcs.append((off, n, False))
     dev, keep = stage(lay, device)
     for r, off in dev_refs:
-        dev[off: off + r.length].copy_(r.arena.view(r.offset, r.length))
+        v = r.arena.view(r.offset, r.length) if isinstance(r, DeviceRef) else r
+        dev[off: off + v.numel()].copy_(v)
     return dev, lay.top, srcs, keep
+
+
+def staged_host(buf):
+    """A fetched byte range as host bytes for the pinned packer."""
+    if isinstance(buf, (bytes, bytearray, memoryview)):
+        return buf
+    return byte_payload(buf, host=True)
 
 
 def _shard_key(bg):
@@ -185,11 +197,14 @@ def gather_sharded_partial(batch: list, sh, cps, n_inner: int, inner_shape, spec
     out_of_shard = {}
     for k, s in shards.items():
         bg = s["bg"]
-        req = SuffixByteRequest(isz) if sh.index_location == "end" else RangeByteRequest(0, isz)
+        st = getattr(bg, "store", None)
+        Range, Suffix = request_classes(st)
+        req = Suffix(isz) if sh.index_location == "end" else Range(0, isz)
         raw = bg.get_sync(prototype=None, byte_range=req)
         if raw is None:
             out_of_shard[k] = None  # whole shard missing -> fill (status "missing")
             continue
+        raw = byte_payload(raw, host=True)
         if len(raw) < isz:
             raise ValueError("shard blob is shorter than its index")
         idx = np.frombuffer(raw, dtype="<u8", count=2 * n_inner).reshape(n_inner, 2)
@@ -204,20 +219,25 @@ def gather_sharded_partial(batch: list, sh, cps, n_inner: int, inner_shape, spec
             o, n = idx[slot]
             if o == MAX_U64 and n == MAX_U64:
                 continue  # missing inner chunk -> fill (sharding.py:700-712)
-            reqs.append(RangeByteRequest(int(o), int(o) + int(n)))
+            reqs.append(Range(int(o), int(o) + int(n)))
             want.append(slot)
         if reqs:
-            st = getattr(bg, "store", None)
-            if st is not None and hasattr(st, "get_ranges_sync"):
-                cfg = spec.config  # forwarded like sharding.py:1695-1752
-                got = st.get_ranges_sync(bg.path, reqs,
-                                         max_gap_bytes=cfg.sharding_coalesce_max_gap_bytes,
-                                         max_coalesced_bytes=cfg.sharding_coalesce_max_bytes)
-            else:
-                got = [(j, bg.get_sync(prototype=None, byte_range=r)) for j, r in enumerate(reqs)]
+            cfg = spec.config  # forwarded like sharding.py:1695-1752
+            try:
+                if st is not None and hasattr(st, "get_ranges_sync"):
+                    got = st.get_ranges_sync(bg.path, reqs, prototype=spec.prototype,
+                                             max_gap_bytes=cfg.sharding_coalesce_max_gap_bytes,
+                                             max_coalesced_bytes=cfg.sharding_coalesce_max_bytes)
+                else:
+                    got = [(j, bg.get_sync(prototype=None, byte_range=r)) for j, r in enumerate(reqs)]
+            except Exception as e:  # the shard vanished between the index and data reads
+                if not is_missing_key_error(e):
+                    raise
+                out_of_shard[k] = None
+                continue
             for j, buf in got:
                 slot = want[j]
-                off, n = lay.add(buf)
+                off, n = lay.add(staged_host(buf))
                 src_by[slot], len_by[slot], miss_by[slot] = off, n, False
         out_of_shard[k] = (src_by, len_by, miss_by, idx_off)
     dev, keep = stage(lay, device)

@@ -54,11 +54,12 @@ def _resolve_range(req, n: int) -> tuple[int, int]:
     """Byte request -> clamped [a, b) over a value of length n."""
     if req is None:
         return 0, n
-    if isinstance(req, RangeByteRequest):
+    # by attribute, so zarr's own request classes (src/zarr/abc/store.py) work too
+    if hasattr(req, "start") and hasattr(req, "end"):
         a, b = req.start, req.end
-    elif isinstance(req, SuffixByteRequest):
+    elif hasattr(req, "suffix"):
         a, b = max(n - req.suffix, 0), n
-    elif isinstance(req, OffsetByteRequest):
+    elif hasattr(req, "offset"):
         a, b = req.offset, n
     else:
         a, b = req
@@ -92,7 +93,8 @@ def coalesce_ranges(byte_ranges, *, max_gap_bytes: int = MAX_GAP_BYTES,
 
 
 class _RangesMixin:
-    def get_ranges_sync(self, key: str, byte_ranges, *, max_gap_bytes: int = MAX_GAP_BYTES,
+    def get_ranges_sync(self, key: str, byte_ranges, *, prototype=None,
+                        max_gap_bytes: int = MAX_GAP_BYTES,
                         max_coalesced_bytes: int = MAX_COALESCED_BYTES):
         """Store.get_ranges_sync (src/zarr/abc/store.py:474-539): one fetch per
         coalesced group, sliced back per input; yields (input_index, buf)."""
@@ -122,7 +124,7 @@ class MemoryStore(_RangesMixin):
     def __init__(self, data: dict | None = None):
         self._d: dict[str, bytes] = {} if data is None else data
 
-    def get_sync(self, key: str, byte_range: tuple[int, int] | None = None):
+    def get_sync(self, key: str, byte_range=None, prototype=None):
         v = self._d.get(key)
         if v is None:
             return None
@@ -132,7 +134,9 @@ class MemoryStore(_RangesMixin):
         return memoryview(v)[a:b]
 
     def set_sync(self, key: str, value) -> None:
-        self._d[key] = bytes(value)
+        from .interop import byte_payload
+
+        self._d[key] = value if isinstance(value, bytes) else byte_payload(value, host=True).tobytes()
 
     def delete_sync(self, key: str) -> None:
         self._d.pop(key, None)
@@ -161,7 +165,7 @@ class LocalStore(MemoryStore):
     def _path(self, key):
         return os.path.join(self.root, *key.split("/"))
 
-    def get_sync(self, key, byte_range=None):
+    def get_sync(self, key, byte_range=None, prototype=None):
         p = self._path(key)
         if not os.path.exists(p):
             return None
@@ -173,10 +177,12 @@ class LocalStore(MemoryStore):
             return memoryview(f.read(b - a))
 
     def set_sync(self, key, value):
+        from .interop import byte_payload
+
         p = self._path(key)
         os.makedirs(os.path.dirname(p), exist_ok=True)
         with open(p, "wb") as f:
-            f.write(bytes(value))
+            f.write(value if isinstance(value, bytes) else byte_payload(value, host=True).tobytes())
 
     def delete_sync(self, key):
         p = self._path(key)
@@ -200,40 +206,103 @@ class LocalStore(MemoryStore):
         return {k: bytes(self.get_sync(k)) for k in self.keys()}
 
 
+def _aligned(n: int) -> int:
+    return (int(n) + ALIGN - 1) // ALIGN * ALIGN
+
+
 class DeviceArena:
-    """A growable HBM byte arena (torch uint8 tensor) holding encoded blobs."""
+    """A growable HBM byte arena (torch uint8 tensor) holding encoded blobs.
+
+    Space is handed out in ALIGN-byte granules, first fit from a free list of
+    released regions (kept sorted and coalesced), else from the top.  Deleting
+    or overwriting a key gives its region back (the reference's MemoryStore /
+    GpuMemoryStore drop the value on delete, src/zarr/storage/_memory.py:
+    140-146, 317-328), so rewrite loops stay bounded.  Freed bytes are reused
+    by work enqueued later on the same device stream, which orders it after
+    every earlier reader.
+
+    ``lock`` (re-entrant) serialises placement changes AND the enqueue of a
+    device write into ``buf``: a writer holds it from reserve() until its encode
+    is launched, so a concurrent grow (which swaps ``buf``) can never leave that
+    launch writing into an abandoned buffer."""
 
     def __init__(self, device, capacity: int = 1 << 24):
         import torch
 
         self.device = torch.device(device)
-        self.buf = torch.empty(int(capacity) + TAIL_SLACK, dtype=torch.uint8, device=self.device)
+        self.buf = torch.empty(_aligned(capacity) + TAIL_SLACK, dtype=torch.uint8, device=self.device)
         self.top = 0
         self.version = 0
-        self._lock = threading.Lock()
+        self.lock = threading.RLock()
+        self._free: list[list[int]] = []  # [offset, nbytes], sorted, coalesced, ALIGN granules
 
     @property
     def capacity(self) -> int:
         return self.buf.numel() - TAIL_SLACK
 
+    @property
+    def free_bytes(self) -> int:
+        return sum(n for _, n in self._free)
+
+    @property
+    def used_bytes(self) -> int:
+        return self.top - self.free_bytes
+
     def _grow(self, need: int) -> None:
         import torch
 
-        cap = max(need, 2 * self.capacity)
+        cap = _aligned(max(need, 2 * self.capacity))
         nb = torch.empty(cap + TAIL_SLACK, dtype=torch.uint8, device=self.device)
         nb[: self.top].copy_(self.buf[: self.top])
         self.buf = nb
         self.version += 1
 
     def reserve(self, nbytes: int) -> int:
-        """Reserve an aligned region; returns its offset."""
-        with self._lock:
-            off = (self.top + ALIGN - 1) // ALIGN * ALIGN
-            end = off + int(nbytes)
+        """Reserve an aligned region of at least nbytes; returns its offset."""
+        need = max(_aligned(nbytes), ALIGN)
+        with self.lock:
+            for i, (off, n) in enumerate(self._free):
+                if n >= need:
+                    if n == need:
+                        del self._free[i]
+                    else:
+                        self._free[i] = [off + need, n - need]
+                    return off
+            off = self.top
+            end = off + need
             if end > self.capacity:
                 self._grow(end)
             self.top = end
             return off
+
+    def free(self, off: int, nbytes: int) -> None:
+        """Give back a region returned by reserve() (or its aligned tail)."""
+        off = int(off)
+        n = _aligned(nbytes)
+        if n <= 0:
+            return
+        with self.lock:
+            fl = self._free
+            lo, hi = 0, len(fl)
+            while lo < hi:
+                mid = (lo + hi) // 2
+                if fl[mid][0] < off:
+                    lo = mid + 1
+                else:
+                    hi = mid
+            fl.insert(lo, [off, n])
+            # coalesce with the neighbours
+            if lo + 1 < len(fl) and fl[lo][0] + fl[lo][1] == fl[lo + 1][0]:
+                fl[lo][1] += fl[lo + 1][1]
+                del fl[lo + 1]
+            if lo > 0 and fl[lo - 1][0] + fl[lo - 1][1] == fl[lo][0]:
+                fl[lo - 1][1] += fl[lo][1]
+                del fl[lo]
+                lo -= 1
+            # a free block that reaches the top lowers it
+            if fl and fl[-1][0] + fl[-1][1] == self.top:
+                self.top = fl[-1][0]
+                del fl[-1]
 
     def put(self, data) -> tuple[int, int]:
         """Copy host bytes / numpy / device tensor into the arena."""
@@ -241,14 +310,16 @@ class DeviceArena:
 
         if isinstance(data, torch.Tensor):
             t = data.reshape(-1).view(torch.uint8)
-            off = self.reserve(t.numel())
-            self.buf[off: off + t.numel()].copy_(t, non_blocking=True)
+            with self.lock:
+                off = self.reserve(t.numel())
+                self.buf[off: off + t.numel()].copy_(t, non_blocking=True)
             return off, t.numel()
         arr = np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray) \
             else np.ascontiguousarray(data).reshape(-1).view(np.uint8)
-        off = self.reserve(arr.size)
-        if arr.size:
-            self.buf[off: off + arr.size].copy_(torch.from_numpy(arr.copy()))
+        with self.lock:
+            off = self.reserve(arr.size)
+            if arr.size:
+                self.buf[off: off + arr.size].copy_(torch.from_numpy(arr.copy()))
         return off, int(arr.size)
 
     def view(self, off: int, n: int):
@@ -284,7 +355,7 @@ class DeviceStore:
     def device(self):
         return self.arena.device
 
-    def get_sync(self, key: str, byte_range=None) -> DeviceRef | None:
+    def get_sync(self, key: str, byte_range=None, prototype=None) -> DeviceRef | None:
         if key.endswith("zarr.json"):
             m = self._meta.get(key)
             return None if m is None else memoryview(m)
@@ -297,25 +368,59 @@ class DeviceStore:
             return DeviceRef(self.arena, off + a, b - a)
         return DeviceRef(self.arena, off, n)
 
-    def set_sync(self, key: str, value: Any) -> None:
+    def set_sync(self, key: str, value: Any, *, byte_range=None) -> None:
+        from .interop import byte_payload
+
         if key.endswith("zarr.json"):
-            self._meta[key] = bytes(value)
+            self._meta[key] = bytes(byte_payload(value, host=True))
             return
         if isinstance(value, DeviceRef):
             value = value.arena.view(value.offset, value.length)
-        self._index[key] = self.arena.put(value)
+        else:
+            value = byte_payload(value)
+        with self.arena.lock:
+            placed = self.arena.put(value)
+            self._release(key)
+            self._index[key] = placed
 
     def set_reserved(self, key: str, nbytes: int) -> int:
-        off = self.arena.reserve(nbytes)
-        self._index[key] = (off, nbytes)
+        with self.arena.lock:
+            off = self.arena.reserve(nbytes)
+            self._release(key)
+            self._index[key] = (off, nbytes)
         return off
 
+    def _release(self, key: str) -> None:
+        old = self._index.pop(key, None)
+        if old is not None:
+            self.arena.free(old[0], max(old[1], 1))
+
     def register(self, key: str, off: int, nbytes: int) -> None:
-        """Bind a key to bytes already written in the arena (device encode output)."""
-        self._index[key] = (int(off), int(nbytes))
+        """Bind a key to bytes already written in the arena (device encode output);
+        the key's previous region goes back to the arena."""
+        with self.arena.lock:
+            self._release(key)
+            self._index[key] = (int(off), int(nbytes))
+
+    def commit(self, key: str, off: int, nbytes: int, reserved: int) -> None:
+        """register() for a region of `reserved` bytes of which the encode used
+        `nbytes` (0 = the chunk / shard was elided: the key is deleted); the
+        unused aligned tail goes back to the arena."""
+        with self.arena.lock:
+            if nbytes <= 0:
+                self._release(key)
+                self.arena.free(off, max(reserved, 1))
+                return
+            used = -(-int(nbytes) // ALIGN) * ALIGN
+            tail = -(-int(reserved) // ALIGN) * ALIGN - used
+            if tail > 0:
+                self.arena.free(int(off) + used, tail)
+            self._release(key)
+            self._index[key] = (int(off), int(nbytes))
 
     def delete_sync(self, key: str) -> None:
-        self._index.pop(key, None)
+        with self.arena.lock:
+            self._release(key)
 
     def exists(self, key: str) -> bool:
         return key in self._index
