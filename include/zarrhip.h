@@ -306,6 +306,9 @@ int zhip_shard_pack(const zhip_plan *plan, void *dst, const zhip_shard *d_shards
 /* CPU-only test hooks (no GPU needed). */
 int zhip_selftest(void);                                  /* 0 = all identities hold */
 uint32_t zhip_emulate_chunk_crc(const zhip_plan *plan, const uint8_t *data);
+/* The same for k_decode_pair's scheme (11/11/10-bit tables, four word
+ * accumulators per lane, windowed per-lane multiply).  Test hook. */
+uint32_t zhip_emulate_chunk_crc_pair(const zhip_plan *plan, const uint8_t *data);
 uint32_t zhip_fdiv_eval(uint32_t n, uint32_t d);
 
 #ifdef __cplusplus

@@ -58,3 +58,97 @@ extern "C" int cb_copy(const void* src, void* dst, uint64_t nbytes, uint32_t spa
                        span16);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
+
+// Persistent grid-stride copy: `grid` workgroups, each walking 16-byte blocks
+// b = (g * 256 + t) + k * 256 * grid, K blocks in flight per thread.
+template <int K, bool NT>
+__global__ __launch_bounds__(256) void k_copy_persist(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                      uint64_t n16) {
+    const uint64_t stride = (uint64_t)gridDim.x * 256ull;
+    for (uint64_t b = (uint64_t)blockIdx.x * 256ull + threadIdx.x; b < n16; b += stride * K) {
+        uint4 v[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint64_t i = b + stride * k;
+            if (i < n16) {
+                if constexpr (NT) {
+                    const v4u w = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(src) + i);
+                    v[k] = make_uint4(w.x, w.y, w.z, w.w);
+                } else v[k] = src[i];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint64_t i = b + stride * k;
+            if (i < n16) {
+                if constexpr (NT) {
+                    v4u w = {v[k].x, v[k].y, v[k].z, v[k].w};
+                    __builtin_nontemporal_store(w, reinterpret_cast<v4u*>(dst) + i);
+                } else dst[i] = v[k];
+            }
+        }
+    }
+}
+
+extern "C" int cb_copy_persist(const void* src, void* dst, uint64_t nbytes, uint32_t grid, int K, int nt,
+                               void* stream) {
+    typedef void (*PFn)(const uint4*, uint4*, uint64_t);
+    PFn fn = nullptr;
+#define PSEL(KK) if (K == KK) fn = nt ? (PFn)k_copy_persist<KK, true> : (PFn)k_copy_persist<KK, false>;
+    PSEL(2) PSEL(4) PSEL(8)
+    if (!fn) return -1;
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const uint4*)src, (uint4*)dst,
+                       nbytes / 16);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+// The headline's access pattern without any codec work: 64 chunks of 64^3 f32
+// (1 MiB each, at `cstride` bytes apart in src -- 1048580 for the shard's
+// inner-chunk packing, 4-byte aligned) scattered as 256-byte rows into a
+// 256^3 f32 out (row stride 1 KiB).  Each workgroup copies `units` consecutive
+// 32 KiB units, every thread 8 x 16 bytes per unit (unaligned nt loads).
+typedef unsigned int v4u_a1 __attribute__((ext_vector_type(4), aligned(1)));
+template <int UNITS>
+__global__ __launch_bounds__(256) void k_scatter(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                 uint64_t cstride) {
+    const int t = threadIdx.x;
+    uint4 v[UNITS][8];
+#pragma unroll
+    for (int u = 0; u < UNITS; ++u) {
+        const uint32_t q = blockIdx.x * UNITS + u;
+        const uint32_t c = q >> 5, s = q & 31;
+        const uint8_t* cp = src + (uint64_t)c * cstride + (uint64_t)s * 32768;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const v4u_a1 w = __builtin_nontemporal_load(reinterpret_cast<const v4u_a1*>(cp + 4096 * k + 16 * t));
+            v[u][k] = make_uint4(w.x, w.y, w.z, w.w);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < UNITS; ++u) {
+        const uint32_t q = blockIdx.x * UNITS + u;
+        const uint32_t c = q >> 5, s = q & 31;
+        const uint32_t cz = c >> 4, cy = (c >> 2) & 3, cx = c & 3;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t b = s * 32768 + 4096 * k + 16 * t;  // byte in the chunk
+            const uint32_t z = b >> 14, y = (b >> 8) & 63, xb = b & 255;
+            const uint64_t o = ((uint64_t)(cz * 64 + z) * 256 + cy * 64 + y) * 1024 + cx * 256 + xb;
+            v4u w = {v[u][k].x, v[u][k].y, v[u][k].z, v[u][k].w};
+            __builtin_nontemporal_store(w, reinterpret_cast<v4u*>(dst + o));
+        }
+    }
+}
+
+extern "C" int cb_scatter(const void* src, void* dst, uint64_t cstride, int units, void* stream) {
+    const uint32_t n_units = 64 * 32;
+    if (units == 1)
+        hipLaunchKernelGGL(k_scatter<1>, dim3(n_units), dim3(256), 0, (hipStream_t)stream, (const uint8_t*)src,
+                           (uint8_t*)dst, cstride);
+    else if (units == 2)
+        hipLaunchKernelGGL(k_scatter<2>, dim3(n_units / 2), dim3(256), 0, (hipStream_t)stream, (const uint8_t*)src,
+                           (uint8_t*)dst, cstride);
+    else
+        return -1;
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}

@@ -77,6 +77,9 @@ def test_emulated_kernel_crc_matches_oracle(n):
     L.nbytes = n
     plan = N.Plan(L, upload=False)
     assert plan.emulate_chunk_crc(data) == O.crc32c(data)
+    # k_decode_pair's scheme: 11/11/10-bit tables, four word accumulators, A4
+    # fold, windowed per-lane multiply
+    assert plan.emulate_chunk_crc(data, pair=True) == O.crc32c(data)
 
 
 def test_plan_rejects_bad_layouts():

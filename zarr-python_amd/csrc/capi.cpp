@@ -102,6 +102,20 @@ uint32_t crc_bytewise(const uint8_t* p, size_t n) {
     return ~c;
 }
 
+// k_decode_pair tables (kPairTab* layout): A4096 over 11/11/10-bit slices of a
+// word, and the byte slices of A4 that fold the four word accumulators
+void build_pair_tables(uint32_t* tab) {
+    const uint32_t x = xpow8((uint64_t)kWgStride);
+    for (uint32_t i = 0; i < 2048; ++i) {
+        tab[kPairT1 + i] = gf_mul(x, i);
+        tab[kPairT2 + i] = gf_mul(x, i << 11);
+    }
+    for (uint32_t i = 0; i < 1024; ++i) tab[kPairT3 + i] = gf_mul(x, i << 22);
+    const uint32_t x4 = xpow8(4);
+    for (int sl = 0; sl < 4; ++sl)
+        for (uint32_t b = 0; b < 256; ++b) tab[kPairA4 + sl * 256 + b] = gf_mul(x4, b << (8 * sl));
+}
+
 void build_horner(uint32_t* tab) {  // [op][slice][256], op k = A_(4096 - 4k)
     for (int op = 0; op < 4; ++op) {
         const uint32_t x = xpow8((uint64_t)kWgStride - 4u * op);
@@ -275,7 +289,8 @@ int zhip_plan_upload(zhip_plan* p) {
     // horner (4096) | kthread (256) | kunit (nseg) | kpair (nseg x 256): the
     // per-lane constant kthread[t] * kunit[s] * c_inv of k_decode_pair, whose
     // run ends then need no uniform multiply at all
-    std::vector<uint32_t> h(4096 + kThreads + p->nseg + (size_t)p->nseg * kThreads);
+    const size_t n_old = 4096 + kThreads + p->nseg + (size_t)p->nseg * kThreads;
+    std::vector<uint32_t> h(n_old + kPairTabWords + (size_t)p->nseg * kThreads + kThreads);
     build_horner(h.data());
     for (int t = 0; t < kThreads; ++t) h[4096 + t] = xpow8((uint64_t)kWgStride - 16u * t);
     for (uint32_t s = 0; s < p->nseg; ++s) h[4096 + kThreads + s] = xpow8((uint64_t)s * p->seg);
@@ -284,6 +299,15 @@ int zhip_plan_upload(zhip_plan* p) {
         for (int t = 0; t < kThreads; ++t)
             h[4096 + kThreads + p->nseg + (size_t)s * kThreads + t] = gf_mul(h[4096 + t], ku);
     }
+    // pair tables; the combined four-accumulator state sits 12 bytes later than
+    // the single-chain one, so the lane constants carry x^(-96)
+    p->off_pair = n_old;
+    build_pair_tables(h.data() + n_old);
+    const uint32_t c96 = xpow8_inv(12);
+    for (size_t i = 0; i < (size_t)p->nseg * kThreads; ++i)
+        h[n_old + kPairTabWords + i] = gf_mul(h[4096 + kThreads + p->nseg + i], c96);
+    for (int t = 0; t < kThreads; ++t)
+        h[n_old + kPairTabWords + (size_t)p->nseg * kThreads + t] = gf_mul(h[4096 + t], c96);
     if (p->d_tables) (void)hipFree(p->d_tables);
     p->d_tables = nullptr;
     HIP_TRY(hipMalloc(&p->d_tables, h.size() * sizeof(uint32_t)));
@@ -498,6 +522,9 @@ int zhip_decode_mapped(const zhip_plan* plan, const void* src, uint64_t src_size
     p.kthread = plan->d_tables + 4096;
     p.kunit = plan->d_tables + 4096 + kThreads;
     p.kpair = plan->d_tables + 4096 + kThreads + plan->nseg;
+    p.pair_tab = plan->d_tables + plan->off_pair;
+    p.kpair11 = p.pair_tab + kPairTabWords;
+    p.kthread11 = p.kpair11 + (size_t)plan->nseg * kThreads;
     for (int op = 0; op < 4; ++op) p.hx[op] = plan->hx[op];
     for (int i = 0; i < 32; ++i) p.kq[i] = plan->kq[i];
     p.n_chunks = n_chunks;
@@ -749,6 +776,58 @@ uint32_t zhip_emulate_chunk_crc(const zhip_plan* plan, const uint8_t* data) {
     return ~(gf_mul(V, plan->c_inv) ^ plan->c3);
 }
 
+// CPU emulation of k_decode_pair's CRC for one chunk: 11/11/10-bit A4096
+// tables, four word accumulators per lane folded with the A4 tables, the
+// windowed per-lane multiply by kpair11 (3-bit windows + a 2-bit top window,
+// as the kernel's LDS tables), unit contributions xor-combined.  Test hook.
+uint32_t zhip_emulate_chunk_crc_pair(const zhip_plan* plan, const uint8_t* data) {
+    std::call_once(g_once, init_tables);
+    std::vector<uint32_t> tab(kPairTabWords);
+    build_pair_tables(tab.data());
+    const uint32_t* T = tab.data();
+    auto a11 = [&](uint32_t w) { return T[kPairT1 + (w & 2047u)] ^ T[kPairT2 + ((w >> 11) & 2047u)] ^ T[kPairT3 + (w >> 22)]; };
+    auto a4 = [&](uint32_t w) {
+        const uint32_t* t4 = T + kPairA4;
+        return t4[w & 255u] ^ t4[256 + ((w >> 8) & 255u)] ^ t4[512 + ((w >> 16) & 255u)] ^ t4[768 + (w >> 24)];
+    };
+    auto mulx = [](uint32_t b) { return (b >> 1) ^ (kPoly & (0u - (b & 1u))); };
+    auto lanemul3 = [&](uint32_t a, uint32_t k) {  // the kernel's windowed multiply
+        uint32_t m3[8], m2[4];
+        const uint32_t k1 = mulx(k), k2 = mulx(k1);
+        for (uint32_t v = 0; v < 8; ++v) m3[v] = ((v & 4u) ? k : 0u) ^ ((v & 2u) ? k1 : 0u) ^ ((v & 1u) ? k2 : 0u);
+        for (uint32_t v = 0; v < 4; ++v) m2[v] = ((v & 2u) ? k : 0u) ^ ((v & 1u) ? k1 : 0u);
+        uint32_t p = m3[a & 7u];
+        for (int j = 1; j < 10; ++j) p = mulx(mulx(mulx(p))) ^ m3[(a >> (3 * j)) & 7u];
+        return mulx(mulx(p)) ^ m2[a >> 30];
+    };
+    const uint32_t N = (uint32_t)plan->layout.nbytes;
+    const uint32_t c96 = xpow8_inv(12);
+    uint32_t V = 0;
+    for (uint32_t s = 0; s < plan->nseg; ++s) {
+        const int32_t hi = (int32_t)plan->E - (int32_t)(s * plan->seg);
+        const int32_t lo = hi - (int32_t)plan->seg;
+        const uint32_t ku = gf_mul(xpow8((uint64_t)s * plan->seg), plan->c_inv);
+        for (int t = 0; t < kThreads; ++t) {
+            uint32_t a[4] = {0, 0, 0, 0};
+            for (int k = 0; k < (int)plan->kblocks; ++k) {
+                const int32_t o = lo + kWgStride * k + 16 * t;
+                uint8_t b[16] = {0};
+                for (int i = 0; i < 16; ++i) {
+                    const int64_t q = (int64_t)o + i;
+                    if (q >= 0 && q < (int64_t)N) b[i] = data[q];
+                }
+                uint32_t w[4];
+                std::memcpy(w, b, 16);
+                for (int j = 0; j < 4; ++j) a[j] = a11(a[j] ^ w[j]);
+            }
+            const uint32_t S = a4(a4(a4(a[0]) ^ a[1]) ^ a[2]) ^ a[3];
+            const uint32_t k11 = gf_mul(gf_mul(xpow8((uint64_t)kWgStride - 16u * t), ku), c96);
+            V ^= lanemul3(S, k11);
+        }
+    }
+    return ~(V ^ plan->c3);
+}
+
 // CPU self-test of the identities the kernels rely on.  Returns 0 when all hold.
 int zhip_selftest(void) {
     std::call_once(g_once, init_tables);
@@ -797,8 +876,11 @@ int zhip_selftest(void) {
         zhip_plan* p = nullptr;
         if (zhip_plan_create(&L, &p) != ZHIP_OK) return 6;
         const uint32_t got = zhip_emulate_chunk_crc(p, buf.data());
+        const uint32_t got_pair = zhip_emulate_chunk_crc_pair(p, buf.data());
         zhip_plan_destroy(p);
         if (got != crc_bytewise(buf.data(), n)) return set_err(7, "emulated kernel CRC wrong at n=" + std::to_string(n));
+        if (got_pair != crc_bytewise(buf.data(), n))
+            return set_err(8, "emulated pair-kernel CRC wrong at n=" + std::to_string(n));
     }
     return 0;
 }

@@ -398,6 +398,109 @@ __device__ __forceinline__ uint32_t crc_block(const uint32_t* s_tab, uint32_t ac
            tab_apply(s_tab + 3072, v.w);
 }
 
+// ---- k_decode_pair's CRC (tables: kPairTab* layout, built by capi.cpp) ----
+// Every word of a 16-byte block is carried by its own accumulator through ONE
+// operator, A4096 (multiply by x^(8*4096)), looked up by the word's 11 low,
+// 11 middle and 10 high bits: 3 LDS reads per word instead of 4 byte reads
+// into four per-position tables.  At a run end the four accumulators fold
+// into one state with the A4 byte tables, a3 ^ A4(a2 ^ A4(a1 ^ A4(a0))), which
+// sits 12 bytes after the single-chain state of the other kernels; the lane
+// constants kpair11 / kthread11 carry the x^(-96) that undoes it.  (The CPU
+// emulation zhip_emulate_chunk_crc_pair checks this decomposition.)
+struct Acc4 {
+    uint32_t a0, a1, a2, a3;
+};
+
+__device__ __forceinline__ uint32_t t11(const uint32_t* s, uint32_t w) {
+    return s[kPairT1 + (w & 2047u)] ^ s[kPairT2 + ((w >> 11) & 2047u)] ^ s[kPairT3 + (w >> 22)];
+}
+
+__device__ __forceinline__ void crc_block4(const uint32_t* s, Acc4& a, const uint4 v) {
+    a.a0 = t11(s, a.a0 ^ v.x);
+    a.a1 = t11(s, a.a1 ^ v.y);
+    a.a2 = t11(s, a.a2 ^ v.z);
+    a.a3 = t11(s, a.a3 ^ v.w);
+}
+
+__device__ __forceinline__ uint32_t fold4(const uint32_t* s, const Acc4& a) {
+    const uint32_t* t4 = s + kPairA4;
+    return tab_apply(t4, tab_apply(t4, tab_apply(t4, a.a0) ^ a.a1) ^ a.a2) ^ a.a3;
+}
+
+// Per-lane multiply by the lane's constant k from a 12-entry LDS column: 3-bit
+// windows of the operand (bits 0..29, entries 0..7) and a 2-bit top window
+// (bits 30..31, entries 8..11); Horner over the windows with x^3 / x^2 steps
+// whose reductions are VALU.  12 KiB for 256 lanes (the 4-bit form needs 16).
+constexpr uint32_t rbasis(uint32_t n, int steps) {
+    for (int i = 0; i < steps; ++i) n = (n >> 1) ^ (kPoly & (0u - (n & 1u)));
+    return n;
+}
+
+__device__ __forceinline__ uint32_t r3(uint32_t n) {
+    return ((n & 1u) ? rbasis(1, 3) : 0u) ^ ((n & 2u) ? rbasis(2, 3) : 0u) ^ ((n & 4u) ? rbasis(4, 3) : 0u);
+}
+
+__device__ __forceinline__ uint32_t r2(uint32_t n) {
+    return ((n & 1u) ? rbasis(1, 2) : 0u) ^ ((n & 2u) ? rbasis(2, 2) : 0u);
+}
+
+__device__ __forceinline__ void lanemul3_init(uint32_t* s_mul, int t, uint32_t k) {
+    const uint32_t k1 = mulx1(k), k2 = mulx1(k1);
+#pragma unroll
+    for (uint32_t v = 0; v < 8; ++v)
+        s_mul[v * kThreads + t] = ((v & 4u) ? k : 0u) ^ ((v & 2u) ? k1 : 0u) ^ ((v & 1u) ? k2 : 0u);
+#pragma unroll
+    for (uint32_t v = 0; v < 4; ++v) s_mul[(8u + v) * kThreads + t] = ((v & 2u) ? k : 0u) ^ ((v & 1u) ? k1 : 0u);
+}
+
+__device__ __forceinline__ uint32_t lanemul3(const uint32_t* s_mul, int t, uint32_t a) {
+    uint32_t m[11];
+#pragma unroll
+    for (int j = 0; j < 10; ++j) m[j] = s_mul[((a >> (3 * j)) & 7u) * kThreads + t];
+    m[10] = s_mul[(8u + (a >> 30)) * kThreads + t];
+    uint32_t q = m[0];
+#pragma unroll
+    for (int j = 1; j < 10; ++j) q = (q >> 3) ^ r3(q & 7u) ^ m[j];
+    return (q >> 2) ^ r2(q & 3u) ^ m[10];
+}
+
+// Shard-index CRC check by one workgroup with the pair tables (verify_index's
+// chain, four accumulators, folded, shifted by kthread11).
+__device__ __forceinline__ void verify_index_pair(const DecodeParams& p, uint32_t j, int t, uint32_t kth11,
+                                                  const uint32_t* s_tab, uint32_t* red, bool has_pre, uint4 pre) {
+    const zhip_chunk ch = p.idx_chunks[j];
+    const uint32_t ok = ch.src_len == (uint64_t)p.idx_nbytes + 4u;
+    const uint8_t* cp = p.src + ch.src;
+    const uint32_t nk = (p.idx_E + kWgStride - 1) / kWgStride;
+    const int32_t lo = (int32_t)p.idx_E - (int32_t)(nk * kWgStride);
+    Acc4 a = {0u, 0u, 0u, 0u};
+    if (ok) {
+        for (uint32_t k = 0; k < nk; ++k) {
+            const int32_t o = lo + kWgStride * (int32_t)k + 16 * t;
+            uint4 v;
+            if (k == 0 && has_pre) v = (o >= 0 && (uint32_t)o < p.idx_nbytes) ? mask_tail(pre, o, p.idx_nbytes)
+                                                                         : make_uint4(0, 0, 0, 0);
+            else v = load_block<false>(cp, o, p.idx_nbytes);
+            crc_block4(s_tab, a, v);
+        }
+    }
+    uint32_t v = wave_xor(gf_mul(fold4(s_tab, a), kth11));
+    __syncthreads();  // red may still be read from a previous index
+    if ((t & 63) == 0) red[t >> 6] = v;
+    __syncthreads();
+    if (t == 0) {
+        zhip_status st = {ZHIP_ST_LENGTH_MISMATCH, 0u, 0u, 0u};
+        if (ok) {
+            const uint32_t V = red[0] ^ red[1] ^ red[2] ^ red[3];
+            st.stored = load_trailer(cp, p.idx_nbytes);
+            st.computed = ~(gf_mul(V, p.idx_c_inv) ^ p.idx_c3);
+            st.code = st.computed == st.stored ? ZHIP_ST_OK : ZHIP_ST_CRC_MISMATCH;
+        }
+        p.idx_status[j] = st;
+        if (st.code != ZHIP_ST_OK) atomicOr(p.errflag, 1u << st.code);
+    }
+}
+
 // The K = 8 steps of one unit in the row map (zhip_rows_map): 64 bytes, one
 // scalar load per unit.
 struct RowSteps {
@@ -415,7 +518,7 @@ template <int ITEM, bool SWAP, int K, bool SKIP = false>
 __device__ __forceinline__ void store_unit_rows(const DecodeParams& p, const Unit& U, const RowSteps& m, bool live,
                                                 uint32_t lane_row, int64_t lane_off, uint8_t* sink,
                                                 const uint4 (&blk)[K], bool crc = false,
-                                                const uint32_t* s_tab = nullptr, uint32_t* acc = nullptr) {
+                                                const uint32_t* s_tab = nullptr, Acc4* acc = nullptr) {
     static_assert(K == kDefaultBlocks, "the row map holds kDefaultBlocks steps per unit");
     const bool present = live && U.mode == ZHIP_ST_OK;
     const bool writes = live && (U.mode == ZHIP_ST_OK || U.mode == ZHIP_ST_MISSING);
@@ -428,26 +531,11 @@ __device__ __forceinline__ void store_unit_rows(const DecodeParams& p, const Uni
         store_nt16(wr ? base + m.e[k].rel + lane_off : sink, present ? swap_block<ITEM, SWAP>(blk[k]) : f);
         // (SKIP: ablation arm, lookups replaced by a plain xor; a compile-time
         // choice -- a runtime test here doubles the loop's branches)
-        if (crc) *acc = SKIP ? *acc ^ blk[k].x ^ blk[k].y ^ blk[k].z ^ blk[k].w : crc_block(s_tab, *acc, blk[k]);
+        if (crc) {
+            if constexpr (SKIP) acc->a0 ^= blk[k].x ^ blk[k].y ^ blk[k].z ^ blk[k].w;
+            else crc_block4(s_tab, *acc, blk[k]);
+        }
     }
-}
-
-template <int K>
-__device__ __forceinline__ uint32_t crc_unit_rows(const uint32_t* s_tab, uint32_t acc, const uint4 (&blk)[K],
-                                                  uint32_t tune) {
-    // (used by the TRAIL tuning variant of k_decode_pair)
-    if (tune & kTuneSkipCrc) {  // ablation: lookups replaced by a plain xor
-#pragma unroll
-        for (int k = 0; k < K; ++k) acc ^= blk[k].x ^ blk[k].y ^ blk[k].z ^ blk[k].w;
-        return acc;
-    }
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-        const uint4 v = blk[k];  // blocks before the chunk start hold zeros
-        acc = tab_apply(s_tab, acc ^ v.x) ^ tab_apply(s_tab + 1024, v.y) ^ tab_apply(s_tab + 2048, v.z) ^
-              tab_apply(s_tab + 3072, v.w);
-    }
-    return acc;
 }
 
 // End of a run (consecutive units of one chunk in this workgroup): reduce the
@@ -461,14 +549,13 @@ __device__ __forceinline__ uint32_t crc_unit_rows(const uint32_t* s_tab, uint32_
 // the chunk compares with the trailer.  `red` is a 4-word LDS scratch.
 __device__ __forceinline__ void run_end_pair(const DecodeParams& p, const Unit& U, uint32_t acc, uint32_t run_bits,
                                              uint32_t stored, uint32_t klane, bool lds_mul, const uint32_t* s_mul,
-                                             const uint32_t* s_r4, uint32_t* red, int t, uint32_t g = 0,
-                                             uint32_t extra = 0) {
+                                             uint32_t* red, int t, uint32_t g = 0) {
     if (p.tune & kTuneNoRunEnd) {  // ablation: no reduction, no publication
-        if ((acc ^ extra) == 0x9E3779B9u) red[0] = acc;
+        if (acc == 0x9E3779B9u) red[0] = acc;
         return;
     }
-    // extra: an already shifted contribution of the same run (VARIANT 2)
-    uint32_t v = ((p.tune & kTuneNoLaneMul) ? acc : lds_mul ? lanemul(s_mul, s_r4, t, acc) : gf_mul(acc, klane)) ^ extra;
+    // acc: the lane's folded state (fold4); klane / the s_mul column: kpair11
+    uint32_t v = (p.tune & kTuneNoLaneMul) ? acc : lds_mul ? lanemul3(s_mul, t, acc) : gf_mul(acc, klane);
     v = wave_xor(v);
     if ((t & 63) == 0) red[t >> 6] = v;
     __syncthreads();
@@ -534,17 +621,18 @@ __device__ __forceinline__ void unit_status_pair(const DecodeParams& p, const Un
     }
 }
 
-// VARIANT (tuning arms, headline item type only): 0 production, 1 every store
-// before the CRC lookups, 2 independent Horner chains for the two units, 3 no
-// CRC lookups (a plain xor; results invalid)
+// VARIANT (tuning arm, headline item type only): 0 production, 3 no CRC
+// lookups (a plain xor; results invalid).  (Round-1 arms 1 -- every store
+// before the lookups -- and 2 -- independent chains for the two units --
+// measured slower and were retired with the single-operator tables.)
 template <bool CRC, int ITEM, bool SWAP, int NU, int K = 8, int VARIANT = 0>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(NU == 1 ? 8 : 4))) void k_decode_pair(const DecodeParams p) {
-    // NU == 1: the lane shift is a VALU multiply (no 16 KiB s_mul), so that
-    // eight workgroups fit a CU's LDS
+    // NU == 1: the lane shift is a VALU multiply (no s_mul), so that eight
+    // workgroups fit a CU's LDS
     constexpr bool kLdsMul = CRC && NU == 2;
-    __shared__ uint32_t s_tab[CRC ? 16 * 256 : 1];
-    __shared__ uint32_t s_mul[kLdsMul ? 16 * kThreads : 1];
-    __shared__ uint32_t s_r4[16];
+    constexpr bool SKIP = VARIANT == 3;
+    __shared__ uint32_t s_tab[CRC ? kPairTabWords : 1];
+    __shared__ uint32_t s_mul[kLdsMul ? 12 * kThreads : 1];
     __shared__ uint32_t s_red[2][kThreads / 64];
     const int t = threadIdx.x;
     const uint32_t G = gridDim.x, g = blockIdx.x;
@@ -558,27 +646,28 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(NU == 
     };
     const uint8_t* zero = reinterpret_cast<const uint8_t*>(g_rows_zero);
     stamp(p, g, t, 0);
-    // 1. vector loads, in this order and count on every path: [CRC: the Horner
-    //    tables (4), lane-shift constants (3)], unit headers (scalar), [CRC: the
-    //    first shard-index block], unit A (K), unit B (K); the CRC trailers
-    //    are scalar loads.  Waiting for any of them
-    //    leaves the later ones in flight; unit headers are scalar loads.
-    // the tables and per-lane constants need no unit header: they go out first,
-    // their latency overlapping the header loads
+    // 1. vector loads, in this order and count on every path: [CRC: the pair
+    //    tables (6), lane constants (3)], [CRC: the first shard-index block],
+    //    unit A (K), unit B (K); unit headers and CRC trailers are scalar
+    //    loads.  Waiting for any of them leaves the later ones in flight.
     const uint32_t u_a = has_a ? unit_of(q0) : 0u, u_b = has_b ? unit_of(q0 + 1u) : u_a;
-    uint4 tv0, tv1, tv2, tv3;  // scalars, not an array: an array here lands in scratch
+    uint4 tv0, tv1, tv2, tv3, tv4, tv5;  // scalars, not an array: an array here lands in scratch
     uint32_t kth = 0, ka = 0, kb = 0;
     if constexpr (CRC) {
-        // (ablation kTuneNoTables: read 64 zero bytes instead; results invalid)
-        const uint4* gt = reinterpret_cast<const uint4*>((p.tune & kTuneNoTables) ? reinterpret_cast<const uint8_t*>(g_rows_zero) : reinterpret_cast<const uint8_t*>(p.horner));
-        tv0 = gt[(p.tune & kTuneNoTables) ? 0 : t];
-        tv1 = gt[(p.tune & kTuneNoTables) ? 0 : t + kThreads];
-        tv2 = gt[(p.tune & kTuneNoTables) ? 0 : t + 2 * kThreads];
-        tv3 = gt[(p.tune & kTuneNoTables) ? 0 : t + 3 * kThreads];
+        // (ablation kTuneNoTables: read zero bytes instead; results invalid)
+        const bool nt = (p.tune & kTuneNoTables) != 0;
+        const uint4* gt = reinterpret_cast<const uint4*>(nt ? reinterpret_cast<const uint8_t*>(g_rows_zero)
+                                                            : reinterpret_cast<const uint8_t*>(p.pair_tab));
+        tv0 = gt[nt ? 0 : t];
+        tv1 = gt[nt ? 0 : t + kThreads];
+        tv2 = gt[nt ? 0 : t + 2 * kThreads];
+        tv3 = gt[nt ? 0 : t + 3 * kThreads];
+        tv4 = gt[nt ? 0 : t + 4 * kThreads];
+        tv5 = gt[nt ? 0 : t + 5 * kThreads];
         if (!(p.tune & kTuneNoConsts)) {
-            kth = load_u32_any(reinterpret_cast<const uint8_t*>(p.kthread + t));
-            ka = load_u32_any(reinterpret_cast<const uint8_t*>(p.kpair + (size_t)(u_a % p.nseg) * kThreads + t));
-            kb = load_u32_any(reinterpret_cast<const uint8_t*>(p.kpair + (size_t)(u_b % p.nseg) * kThreads + t));
+            kth = load_u32_any(reinterpret_cast<const uint8_t*>(p.kthread11 + t));
+            ka = load_u32_any(reinterpret_cast<const uint8_t*>(p.kpair11 + (size_t)(u_a % p.nseg) * kThreads + t));
+            kb = load_u32_any(reinterpret_cast<const uint8_t*>(p.kpair11 + (size_t)(u_b % p.nseg) * kThreads + t));
         }
     }
     uint4 A[K], B[NU == 2 ? K : 1];
@@ -627,58 +716,52 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(NU == 
         }
     }
     stamp(p, g, t, 1);
-    // 2. tables into LDS (waits for the table loads only), lane-multiply table
+    // 2. tables into LDS (waits for the table loads only), lane-multiply column
     if constexpr (CRC) {
         uint4* st = reinterpret_cast<uint4*>(s_tab);
         st[t] = tv0;
         st[t + kThreads] = tv1;
         st[t + 2 * kThreads] = tv2;
         st[t + 3 * kThreads] = tv3;
-        if (t < 16) s_r4[t] = mulx1(mulx1(mulx1(mulx1((uint32_t)t))));
-        if constexpr (kLdsMul) lanemul_init(s_mul, t, kb);  // own column
+        st[t + 4 * kThreads] = tv4;
+        st[t + 5 * kThreads] = tv5;
+        if constexpr (kLdsMul) lanemul3_init(s_mul, t, kb);  // own column
         if (!(p.tune & kTuneNoBarrier)) __syncthreads();
     }
     stamp(p, g, t, 2);
     if (has_a) {
         if (p.tune & kTuneSerialize) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // ablation
-        // 3. stores: A as soon as it arrives (B still in flight), then B
+        // 3. stores: A as soon as it arrives (B still in flight), then B; the
+        //    Horner step of each block right after its store
         uint8_t* sink = reinterpret_cast<uint8_t*>(g_rows_sink);
         const uint32_t lane_row = (16u * (uint32_t)t) >> p.row_shift;
         const uint32_t lane_col = (16u * (uint32_t)t) & ((1u << p.row_shift) - 1u);
         const int64_t lane_off = (int64_t)lane_row * p.r_oy + (int64_t)lane_col;
         const bool same = has_b && ub.c == ua.c;
-        constexpr bool TRAIL = VARIANT == 1, SPLIT = VARIANT == 2, SKIP = VARIANT == 3;
-        const bool ilv = CRC && !TRAIL;  // TRAIL (tuning): every store first, then the lookups
-        uint32_t acc_a = 0, acc_b = 0;
+        Acc4 acc_a = {0u, 0u, 0u, 0u}, acc_b = {0u, 0u, 0u, 0u};
         store_unit_rows<ITEM, SWAP, K, SKIP>(p, ua, ma, true, lane_row, lane_off, sink, A,
-                                       ilv && ua.mode == ZHIP_ST_OK, s_tab, &acc_a);
+                                             CRC && ua.mode == ZHIP_ST_OK, s_tab, &acc_a);
         stamp(p, g, t, 3);
         if constexpr (NU == 2) {
-            acc_b = (same && !SPLIT) ? acc_a : 0u;
+            if (same) acc_b = acc_a;
             store_unit_rows<ITEM, SWAP, K, SKIP>(p, ub, mb, has_b, lane_row, lane_off, sink, B,
-                                           ilv && has_b && ub.mode == ZHIP_ST_OK, s_tab, &acc_b);
-        }
-        if constexpr (CRC && TRAIL) {
-            if (ua.mode == ZHIP_ST_OK) acc_a = crc_unit_rows<K>(s_tab, 0u, A, p.tune);
-            if constexpr (NU == 2)
-                if (has_b && ub.mode == ZHIP_ST_OK) acc_b = crc_unit_rows<K>(s_tab, same ? acc_a : 0u, B, p.tune);
+                                                 CRC && has_b && ub.mode == ZHIP_ST_OK, s_tab, &acc_b);
         }
         stamp(p, g, t, 4);
         // 4. run ends (the CRC lookups ran with the stores): A alone when B
-        //    starts another chunk, then B (or A+B).  One call site: the kernel
-        //    body is straight-line code run once per workgroup, so its size
-        //    is instruction-cache footprint
+        //    starts another chunk, then B (or A+B).  Two straight-line call
+        //    sites (a loop here merges the wait state of its back edge, and the
+        //    compiler then drains the wave's stores before the reduction)
         if constexpr (CRC) {
             const uint32_t sa = __builtin_amdgcn_readfirstlane(stored_a);
             const uint32_t sb = same ? sa : __builtin_amdgcn_readfirstlane(stored_b);
-            // two straight-line call sites (a loop here merges the wait state of
-            // its back edge, and the compiler then drains the wave's stores
-            // before the reduction)
             if (ua.mode == ZHIP_ST_OK && !same)
-                run_end_pair(p, ua, acc_a, 1u << (ua.sidx & 31u), sa, ka, false, s_mul, s_r4, s_red[0], t, g);
+                run_end_pair(p, ua, SKIP ? acc_a.a0 : fold4(s_tab, acc_a), 1u << (ua.sidx & 31u), sa, ka, false,
+                             s_mul, s_red[0], t, g);
             if (NU == 2 && has_b && ub.mode == ZHIP_ST_OK)
-                run_end_pair(p, ub, acc_b, (same ? 1u << (ua.sidx & 31u) : 0u) | (1u << (ub.sidx & 31u)), sb, kb,
-                             kLdsMul, s_mul, s_r4, s_red[1], t, g, (SPLIT && same) ? gf_mul(acc_a, ka) : 0u);
+                run_end_pair(p, ub, SKIP ? acc_b.a0 : fold4(s_tab, acc_b),
+                             (same ? 1u << (ua.sidx & 31u) : 0u) | (1u << (ub.sidx & 31u)), sb, kb, kLdsMul, s_mul,
+                             s_red[1], t, g);
         }
         unit_status_pair(p, ua, CRC, t);
         if (has_b) unit_status_pair(p, ub, CRC, t);
@@ -686,7 +769,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(NU == 
     // 5. fused shard-index checks (the lowest workgroups: dispatched first); the
     //    first block of this workgroup's index was prefetched with the units
     if constexpr (CRC)
-        for (uint32_t j = g; j < p.n_idx; j += G) verify_index(p, j, t, kth, s_tab, s_red[1], j == g, ipre);
+        for (uint32_t j = g; j < p.n_idx; j += G) verify_index_pair(p, j, t, kth, s_tab, s_red[1], j == g, ipre);
     stamp(p, g, t, 7);
 }
 
@@ -713,10 +796,9 @@ KernelFn select_pair_nu(bool crc, int item, bool swap) {
 }
 
 KernelFn select_pair_kernel(bool crc, int item, bool swap, int nu) {
-    if (nu >= 3 && nu <= 5)  // tuning arms (headline item type only): VARIANT 1 / 2 / 3
-        return !(crc && item == 4 && !swap) ? nullptr
-               : nu == 3 ? k_decode_pair<true, 4, false, 2, 8, 1>
-               : nu == 4 ? k_decode_pair<true, 4, false, 2, 8, 2> : k_decode_pair<true, 4, false, 2, 8, 3>;
+    if (nu == 5)  // tuning arm (headline item type only): VARIANT 3, no lookups
+        return !(crc && item == 4 && !swap) ? nullptr : k_decode_pair<true, 4, false, 2, 8, 3>;
+    if (nu == 3 || nu == 4) return nullptr;  // retired arms
     return nu == 1 ? select_pair_nu<1>(crc, item, swap) : select_pair_nu<2>(crc, item, swap);
 }
 

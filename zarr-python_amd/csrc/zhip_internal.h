@@ -31,6 +31,11 @@ struct TileEnt {
     int64_t orel;
 };
 
+// k_decode_pair CRC table layout (u32 words): A4096 by the 11 low, 11 middle
+// and 10 high bits of a word, then the four byte slices of A4 (x^32).
+constexpr int kPairT1 = 0, kPairT2 = 2048, kPairT3 = 4096, kPairA4 = 5120;
+constexpr int kPairTabWords = 6144;
+
 struct DecodeParams {
     const uint8_t* src;
     uint64_t src_size;
@@ -46,6 +51,13 @@ struct DecodeParams {
     const uint32_t* kthread;  // [kThreads]
     const uint32_t* kunit;    // [nseg]
     const uint32_t* kpair;    // [nseg][kThreads]: kthread * kunit * c_inv (k_decode_pair)
+    // k_decode_pair's CRC tables (kPairTab* layout): A4096 in 11/11/10-bit
+    // slices (one operator for all four words: four accumulators per lane) and
+    // the A4 byte tables that combine them, then kpair and kthread times
+    // x^(-96) (the frame of the combined state), [nseg][kThreads] and [kThreads]
+    const uint32_t* pair_tab;
+    const uint32_t* kpair11;
+    const uint32_t* kthread11;
     uint32_t n_chunks, nseg, n_units;
     uint32_t c_inv, c3;
     uint32_t lflags;
@@ -187,7 +199,9 @@ struct zhip_plan {
     uint32_t fill[4];
     int device;
     int max_grid;
-    uint32_t* d_tables;  // horner (4096) | kthread (256) | kunit (nseg) | kpair (nseg * 256)
+    uint32_t* d_tables;  // horner (4096) | kthread (256) | kunit (nseg) | kpair (nseg * 256) |
+                         // pair tables (kPairTabWords) | kpair11 (nseg * 256) | kthread11 (256)
+    uint64_t off_pair;   // u32 offset of the pair tables in d_tables
     // tile mode (layouts with a transposed dim that is contiguous in out)
     int32_t tq;          // -1: no tile mode
     uint32_t t_per_chunk, n_qb, n_cb;

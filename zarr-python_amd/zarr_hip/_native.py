@@ -191,6 +191,8 @@ def lib():
     L.zhip_selftest.restype = ctypes.c_int
     L.zhip_emulate_chunk_crc.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
     L.zhip_emulate_chunk_crc.restype = ctypes.c_uint32
+    L.zhip_emulate_chunk_crc_pair.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    L.zhip_emulate_chunk_crc_pair.restype = ctypes.c_uint32
     L.zhip_fdiv_eval.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
     L.zhip_fdiv_eval.restype = ctypes.c_uint32
     if L.zhip_abi_version() != 1:
@@ -241,9 +243,10 @@ class Plan:
         check(lib().zhip_plan_kernel_flags(self._h, ctypes.byref(f)), "zhip_plan_kernel_flags")
         return f.value
 
-    def emulate_chunk_crc(self, data: bytes) -> int:
+    def emulate_chunk_crc(self, data: bytes, pair: bool = False) -> int:
         buf = ctypes.create_string_buffer(bytes(data) + b"\0" * 16)
-        return int(lib().zhip_emulate_chunk_crc(self._h, buf))
+        fn = lib().zhip_emulate_chunk_crc_pair if pair else lib().zhip_emulate_chunk_crc
+        return int(fn(self._h, buf))
 
     def __del__(self):
         h = getattr(self, "_h", None)
