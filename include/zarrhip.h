@@ -286,6 +286,35 @@ int zhip_encode_mapped(const zhip_plan *plan, const void *arr, void *dst, const 
                        uint32_t n_chunks, const zhip_sel *d_sels, zhip_status *d_status, uint32_t *d_workspace,
                        uint32_t *d_nonempty, uint32_t encode_flags, const zhip_rowblk *d_rowmap, void *stream);
 
+/* Host -> HBM staging (replaces the host-buffer fetches the reference's
+ * pipelines do per chunk: ByteGetter.get_sync / Store.get_ranges_sync,
+ * src/zarr/abc/store.py:474-539, src/zarr/core/codec_pipeline.py:1095-1172).
+ * One piece = `nbytes` host bytes at `host`, bound for `dst_off` in the
+ * staging buffer; pieces sorted by dst_off, non-overlapping. */
+typedef struct zhip_piece {
+    uint64_t host;     /* host address */
+    uint64_t nbytes;
+    uint64_t dst_off;  /* offset in the pinned and device buffers */
+} zhip_piece;
+
+/* Pack the pieces into `pinned` (total bytes) with `nthreads` host threads,
+ * window by window; each window's bytes are copied to `dev` by
+ * hipMemcpyAsync on `stream` as soon as the window is packed.  Returns once
+ * every copy is enqueued (they complete asynchronously on `stream`). */
+int zhip_stage_h2d(const zhip_piece *pieces, uint32_t n_pieces, uint8_t *pinned, void *dev, uint64_t total,
+                   uint64_t window, uint32_t nthreads, void *stream);
+
+/* zhip_stage_h2d started on a library thread: returns at once (NULL on
+ * allocation failure); the pieces array is copied.  zhip_stage_end waits for
+ * every copy to be enqueued and returns zhip_stage_h2d's code. */
+typedef struct zhip_stage_job zhip_stage_job;
+zhip_stage_job *zhip_stage_begin(const zhip_piece *pieces, uint32_t n_pieces, uint8_t *pinned, void *dev,
+                                 uint64_t total, uint64_t window, uint32_t nthreads, void *stream);
+int zhip_stage_end(zhip_stage_job *job);
+
+/* memcpy with `nthreads` host threads (pinned result -> a caller's host array). */
+int zhip_host_copy(void *dst, const void *src, uint64_t nbytes, uint32_t nthreads);
+
 /* shard pack flags */
 #define ZHIP_PF_INDEX_START 1u   /* index_location == "start" */
 #define ZHIP_PF_INDEX_CRC 2u     /* index codecs end in crc32c */

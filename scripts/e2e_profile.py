@@ -1,0 +1,102 @@
+#!/usr/bin/env python
+"""Phase breakdown of a host-resident read (measurement only): C2's 64 encoded
+chunks in a host MemoryStore read into a device out by Array.get, with wall
+time per phase (fetch + pack + H2D enqueue, planning, table uploads, launch,
+sync/results) from wrappers around the product functions, plus the raw pinned
+H2D rate on the same box.  One JSON line per phase."""
+
+import json
+import os
+import sys
+import time
+from collections import defaultdict
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "zarr-python_amd"))
+
+import bench  # noqa: E402
+
+
+def main():
+    import torch
+
+    import zarr_hip
+    from zarr_hip import pipeline as PL
+    from zarr_hip import planner, staging
+
+    dev = torch.device("cuda:0")
+    shape, chunks = (256, 256, 256), (64, 64, 64)
+    data = bench.synthetic(shape)
+    darr = bench.build_replica(dev, torch.from_numpy(data).to(dev), shape, chunks, [bench.LE, bench.CRC])
+    host = zarr_hip.MemoryStore(darr.store_path.store.to_dict())
+    arr = zarr_hip.Array.open(host)
+    out = torch.empty(shape, dtype=torch.float32, device=dev)
+    acc = defaultdict(list)
+
+    def wrap(mod, name, key):
+        fn = getattr(mod, name)
+
+        def w(*a, **k):
+            t0 = time.perf_counter()
+            r = fn(*a, **k)
+            acc[key].append(time.perf_counter() - t0)
+            return r
+        setattr(mod, name, w)
+
+    wrap(staging, "gather_sources", "gather_sources(fetch+pack+h2d enqueue)")
+    wrap(staging, "stage", "  stage(pack+h2d enqueue)")
+    wrap(PL, "plan_decode", "plan_decode")
+    wrap(PL.DecodeProgram, "launch", "launch")
+    wrap(PL.DecodeProgram, "results", "results(sync)")
+    orig_init = PL.DecodeLaunch.__init__
+
+    def init(self, *a, **k):
+        t0 = time.perf_counter()
+        orig_init(self, *a, **k)
+        acc["DecodeLaunch.__init__(uploads)"].append(time.perf_counter() - t0)
+    PL.DecodeLaunch.__init__ = init
+    for win in [int(x) for x in os.environ.get("WINDOWS", "1,2,4,8").split(",")]:
+        staging.WINDOW = win << 20
+        for i in range(12):
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            arr.get((Ellipsis,), out=out)
+            torch.cuda.synchronize(dev)
+            if i >= 2:
+                acc[f"TOTAL get(out=device) window {win} MiB"].append(time.perf_counter() - t0)
+            t0 = time.perf_counter()
+            arr[...]
+            if i >= 2:
+                acc[f"TOTAL __getitem__ (host out) window {win} MiB"].append(time.perf_counter() - t0)
+    assert out.view(torch.int32).cpu().numpy().tobytes() == data.view(np.int32).tobytes()
+    if os.environ.get("CPROFILE"):
+        import cProfile
+        import io
+        import pstats
+
+        pr = cProfile.Profile()
+        pr.enable()
+        for _ in range(20):
+            arr.get((Ellipsis,), out=out)
+        torch.cuda.synchronize(dev)
+        pr.disable()
+        s = io.StringIO()
+        pstats.Stats(pr, stream=s).sort_stats("tottime").print_stats(25)
+        print(s.getvalue(), file=sys.stderr)
+    pin = torch.empty(data.nbytes, dtype=torch.uint8, pin_memory=True)
+    dbuf = torch.empty(data.nbytes, dtype=torch.uint8, device=dev)
+    for _ in range(3):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        dbuf.copy_(pin, non_blocking=True)
+        torch.cuda.synchronize(dev)
+        acc["raw pinned H2D 64 MiB"].append(time.perf_counter() - t0)
+    for k, v in acc.items():
+        print(json.dumps({"phase": k, "ms_med": round(float(np.median(v)) * 1e3, 3), "n": len(v)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

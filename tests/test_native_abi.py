@@ -194,3 +194,16 @@ def test_rows_map_declines_non_row_layouts():
         n = int(N.lib().zhip_rows_map_len(plan.handle, 1))
         m = np.zeros(max(n, 1), N.ROWBLK_DT)
         assert N.lib().zhip_rows_map(plan.handle, table.ctypes.data, 1, m.ctypes.data, n) == N.E_UNSUPPORTED
+
+
+@pytest.mark.parametrize("n", [0, 1, 4095, (1 << 20) + 7, (3 << 20) + 123])
+def test_host_copy_pool(n):
+    """zhip_host_copy (the parallel memcpy of the staging path) is a memcpy."""
+    from zarr_hip import _native as N
+
+    src = np.random.default_rng(n).integers(0, 256, n, dtype=np.uint8)
+    dst = np.zeros(n, np.uint8)
+    for threads in (1, 4, 16):
+        dst[:] = 0
+        assert N.lib().zhip_host_copy(dst.ctypes.data, src.ctypes.data, n, threads) == 0
+        assert dst.tobytes() == src.tobytes()

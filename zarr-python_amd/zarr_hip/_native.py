@@ -117,6 +117,9 @@ class Predict(ctypes.Structure):
                 ("per", ctypes.c_uint32), ("_pad", ctypes.c_uint32)]
 
 
+# zhip_piece (include/zarrhip.h)
+PIECE_DT = np.dtype([("host", "<u8"), ("nbytes", "<u8"), ("dst_off", "<u8")])
+
 # zhip_rowblk (include/zarrhip.h)
 ROWBLK_DT = np.dtype([("rel", "<i4"), ("lo", "<u2"), ("hi", "<u2")])
 
@@ -191,6 +194,15 @@ def lib():
     L.zhip_selftest.restype = ctypes.c_int
     L.zhip_emulate_chunk_crc.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
     L.zhip_emulate_chunk_crc.restype = ctypes.c_uint32
+    L.zhip_stage_h2d.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+                                 ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p]
+    L.zhip_stage_h2d.restype = ctypes.c_int
+    L.zhip_stage_begin.argtypes = list(L.zhip_stage_h2d.argtypes)
+    L.zhip_stage_begin.restype = ctypes.c_void_p
+    L.zhip_stage_end.argtypes = [ctypes.c_void_p]
+    L.zhip_stage_end.restype = ctypes.c_int
+    L.zhip_host_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32]
+    L.zhip_host_copy.restype = ctypes.c_int
     L.zhip_emulate_chunk_crc_pair.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
     L.zhip_emulate_chunk_crc_pair.restype = ctypes.c_uint32
     L.zhip_fdiv_eval.argtypes = [ctypes.c_uint32, ctypes.c_uint32]

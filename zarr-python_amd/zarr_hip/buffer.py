@@ -91,6 +91,23 @@ def to_numpy(t, dtype) -> np.ndarray:
     return host.numpy().view(dt).reshape(tuple(t.shape))
 
 
+def copy_to_host(t, dst: np.ndarray) -> None:
+    """Device tensor -> an existing host array (same shape and dtype), through
+    pinned memory; a C-contiguous destination is filled by the library's host
+    thread pool (zhip_host_copy), anything else by numpy."""
+    src = to_numpy(t, dst.dtype)
+    if dst.flags.c_contiguous and src.flags.c_contiguous and dst.dtype == src.dtype:
+        import os
+
+        from . import _native as N
+
+        threads = max(1, min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "0") or 16), 16))
+        N.check(N.lib().zhip_host_copy(dst.ctypes.data, src.ctypes.data, dst.nbytes, threads),
+                "zhip_host_copy")
+    else:
+        np.copyto(dst, src, casting="no")
+
+
 def _to_device(a, dtype=None):
     """Any array-like -> torch CUDA tensor (zero-copy when already on the device)."""
     import torch

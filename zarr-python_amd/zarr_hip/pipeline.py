@@ -51,6 +51,33 @@ def _upload(arr: np.ndarray, device):
     return t
 
 
+class _Upload:
+    """Several host tables in ONE pinned host -> device copy (256-byte aligned
+    slices of one device buffer), instead of one pageable copy each."""
+
+    def __init__(self, device):
+        self.device = device
+        self.parts: list = []
+        self.top = 0
+
+    def add(self, arr: np.ndarray) -> int:
+        b = np.ascontiguousarray(arr).view(np.uint8).reshape(-1)
+        off = self.top
+        self.parts.append((off, b))
+        self.top = (off + max(b.size, 16) + 255) // 256 * 256
+        return len(self.parts) - 1
+
+    def commit(self) -> list:
+        torch = _torch()
+        host = torch.empty(max(self.top, 16), dtype=torch.uint8, pin_memory=True)
+        hv = host.numpy()
+        for off, b in self.parts:
+            hv[off: off + b.size] = b
+        dev = torch.empty(max(self.top, 16), dtype=torch.uint8, device=self.device)
+        dev.copy_(host, non_blocking=True)  # torch keeps the pinned block until the copy is done
+        return [dev[off: off + max(b.size, 16)] for off, b in self.parts]
+
+
 def crc_error_message(stored: int, computed: int) -> str:
     """The reference's message (src/zarr/codecs/crc32c_.py:46-49)."""
     s = np.uint32(stored).tobytes()
@@ -73,9 +100,9 @@ def get_plan(layout: N.Layout) -> N.Plan:
     return p
 
 
-def _rows_map(plan, sels: np.ndarray, device):
-    """zhip_rows_map over the host copy of the selections, uploaded; None when
-    the library declines the layout (then the launch takes the persistent row
+def _rows_map_host(plan, sels: np.ndarray):
+    """zhip_rows_map over the host copy of the selections; None when the
+    library declines the layout (then the launch takes the persistent row
     decode)."""
     n_sels = max(len(sels), 1)
     if not len(sels):
@@ -89,7 +116,13 @@ def _rows_map(plan, sels: np.ndarray, device):
     if rc == N.E_UNSUPPORTED:
         return None
     N.check(rc, "zhip_rows_map")
-    return _upload(host, device)
+    return host
+
+
+def _rows_map(plan, sels: np.ndarray, device):
+    """_rows_map_host, uploaded."""
+    host = _rows_map_host(plan, sels)
+    return None if host is None else _upload(host, device)
 
 
 class DecodeLaunch:
@@ -104,14 +137,6 @@ class DecodeLaunch:
         self.device = device
         # shard-index CRC checks fused into this launch (zhip_decode_indexed)
         self.n_idx = 0 if index_chunks is None else len(index_chunks)
-        if self.n_idx:
-            self.d_idx_chunks = _upload(index_chunks, device)
-            self.d_idx_status = torch.zeros(self.n_idx * 4, dtype=torch.int32, device=device)
-        self.d_chunks = _upload(chunks, device)
-        self.d_sels = _upload(sels if len(sels) else np.zeros(1, SEL_DT), device)
-        self.d_status = torch.zeros(max(self.n, 1) * 4, dtype=torch.int32, device=device)
-        self.d_ws = torch.zeros(max(self.n, 1) * 4, dtype=torch.int32, device=device)
-        self.d_err = torch.zeros(4, dtype=torch.int32, device=device)
         self.src = src
         self.src_size = src_size
         self.out = out
@@ -120,9 +145,26 @@ class DecodeLaunch:
         self.predict = predict if (fast and rows) else None
         # row map (zhip_rows_map): per (selection, unit, step) destinations for the
         # two-unit row decode; None when the layout does not admit one
-        self.d_rowmap = None
-        if fast and rows:
-            self.d_rowmap = _rows_map(self.plan, sels, device)
+        rowmap = _rows_map_host(self.plan, sels) if fast and rows else None
+        # every table in one host -> device copy; statuses and workspaces in
+        # one zeroed buffer
+        up = _Upload(device)
+        i_ch = up.add(chunks)
+        i_sel = up.add(sels if len(sels) else np.zeros(1, SEL_DT))
+        i_idx = up.add(index_chunks) if self.n_idx else None
+        i_map = up.add(rowmap) if rowmap is not None else None
+        views = up.commit()
+        self.d_chunks, self.d_sels = views[i_ch], views[i_sel]
+        self.d_idx_chunks = views[i_idx] if i_idx is not None else None
+        self.d_rowmap = views[i_map] if i_map is not None else None
+        nw = max(self.n, 1) * 4
+        ni = self.n_idx * 4
+        z = torch.zeros(2 * nw + 64 + ni, dtype=torch.int32, device=device)
+        self.d_status = z[:nw]
+        self.d_ws = z[nw: 2 * nw]
+        self.d_err = z[2 * nw: 2 * nw + 4]
+        if self.n_idx:
+            self.d_idx_status = z[2 * nw + 64: 2 * nw + 64 + ni]
 
     def launch(self, stream: int | None = None) -> None:
         if self.n == 0:
@@ -181,8 +223,12 @@ class DecodeProgram:
     sharded: bool
     item_missing: np.ndarray
     keepalive: list = field(default_factory=list)
+    pending: Any = None  # staging.Pending: host bytes still on their way to HBM
 
     def launch(self, stream: int | None = None) -> None:
+        if self.pending is not None:
+            self.pending.finish(stream)  # the launch stream waits for the staged copies
+            self.pending = None
         if self.index is not None:
             self.index.launch(stream)
         self.data.launch(stream)
@@ -397,14 +443,16 @@ class HipCodecPipeline:
         device = out.device
         chain: ChainInfo = analyze_chain(self.codecs, spec)
         resolved = None
+        # host-resident bytes are packed and copied on the stager thread while
+        # this thread plans; the launch waits for them (DecodeProgram.pending)
         if chain.shard is not None and not _device_resident(batch):
             sh = chain.shard
             cps = sh.chunks_per_shard(spec.shape)
-            src, size, item_missing, resolved, keep = staging.gather_sharded_partial(
-                batch, sh, cps, int(np.prod(cps)), sh.chunk_shape, spec, device)
+            src, size, item_missing, resolved, keep, pending = staging.gather_sharded_partial(
+                batch, sh, cps, int(np.prod(cps)), sh.chunk_shape, spec, device, defer=True)
             srcs = [(0, 0, bool(m)) for m in item_missing]
         else:
-            src, size, srcs, keep = staging.gather_sources(batch, device)
+            src, size, srcs, keep, pending = staging.gather_sources(batch, device, defer=True)
         items = [(o, n, miss, it[2], it[3]) for (o, n, miss), it in zip(srcs, batch)]
         itemsize = out.element_size()
         if np.dtype(spec.dtype).itemsize != itemsize:
@@ -426,7 +474,7 @@ class HipCodecPipeline:
                 index = DecodeLaunch(t.index_layout, t.index_chunks, np.zeros(1, SEL_DT), src, size,
                                      None, False, device)
         return DecodeProgram(t, data, index, len(batch), chain.shard is not None,
-                             np.array([s[2] for s in srcs], bool), keepalive=keep)
+                             np.array([s[2] for s in srcs], bool), keepalive=keep, pending=pending)
 
     def read_sync(self, batch_info: Iterable, out, drop_axes: tuple = (),
                   max_workers: int = 1) -> tuple[GetResult, ...]:
@@ -445,9 +493,9 @@ class HipCodecPipeline:
         prog.launch()
         res = prog.results()
         if host_out is not None:
-            from .buffer import to_numpy
+            from .buffer import copy_to_host
 
-            np.copyto(host_out, to_numpy(dev_out, host_out.dtype), casting="no")
+            copy_to_host(dev_out, host_out)
         return res
 
     async def read(self, batch_info: Iterable, out, drop_axes: tuple = ()) -> tuple[GetResult, ...]:

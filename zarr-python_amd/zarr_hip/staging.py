@@ -4,10 +4,13 @@ The reference reads chunk bytes into host buffers (``ByteGetter.get_sync``,
 ``Store.get_ranges_sync`` with ``coalesce_ranges`` for partial shards:
 src/zarr/abc/store.py:474-539, src/zarr/core/_coalesce.py:61-135,
 src/zarr/codecs/sharding.py:1695-1752).  Here those bytes are packed into one
-pinned buffer (256-byte aligned placements) by a small thread pool, in
-windows of ``WINDOW`` bytes; each window's ``hipMemcpyAsync`` is issued on a
-dedicated copy stream as soon as the window is filled, so host packing
-overlaps PCIe transfer.  The compute stream waits on the copy stream once.
+pinned buffer (256-byte aligned placements) by the library's host thread pool
+(zhip_stage_h2d, csrc/staging.cpp), in windows of ``WINDOW`` bytes; each
+window's ``hipMemcpyAsync`` is issued on a dedicated copy stream by the thread
+that packs it, so host packing overlaps PCIe transfer with no per-window
+Python.  The packing job runs on a stager thread while the caller plans the
+decode (tables, uploads); the consuming launch waits for the copy stream once
+(``Pending.finish``).
 
 Partial shard reads follow the reference's IO shape: the index is fetched
 by a suffix (or prefix) range request, the touched inner chunks' byte ranges
@@ -20,17 +23,17 @@ launch), so errors surface with the reference's message.
 from __future__ import annotations
 
 import os
-from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 
 from .interop import byte_payload, is_missing_key_error, request_classes, staged_bytes
 from .store import ALIGN, TAIL_SLACK, DeviceRef
 
-WINDOW = int(os.environ.get("ZARR_HIP_STAGE_WINDOW", str(8 << 20)))
+# 4 MiB windows: smaller ones pay ~10 us per hipMemcpyAsync, larger ones start
+# the DMA late (scripts/stage_micro.py)
+WINDOW = int(os.environ.get("ZARR_HIP_STAGE_WINDOW", str(4 << 20)))
 MAX_U64 = np.uint64(0xFFFFFFFFFFFFFFFF)
 
-_POOL: ThreadPoolExecutor | None = None
 _COPY_STREAMS: dict = {}
 
 
@@ -38,13 +41,6 @@ def _workers() -> int:
     n = os.cpu_count() or 1
     cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
     return max(1, min(n, cap or 8, 16))
-
-
-def _pool() -> ThreadPoolExecutor:
-    global _POOL
-    if _POOL is None:
-        _POOL = ThreadPoolExecutor(max_workers=_workers(), thread_name_prefix="zhip-stage")
-    return _POOL
 
 
 def _copy_stream(device):
@@ -80,49 +76,79 @@ class StagingLayout:
         return off
 
 
-def _fill_window(hv: np.ndarray, parts: list) -> None:
-    for buf, dst, a, b in parts:
-        hv[dst + a: dst + b] = np.frombuffer(buf, dtype=np.uint8)[a:b]
+def _host_view(buf) -> np.ndarray:
+    return buf if isinstance(buf, np.ndarray) else np.frombuffer(buf, dtype=np.uint8)
 
 
-def stage(layout: StagingLayout, device):
-    """Copy every piece to one new device buffer; returns (dev, keepalive)."""
+class Pending:
+    """Staged bytes on their way to HBM: the device buffer (allocated now,
+    filled on the copy stream by a library packing job that runs without the
+    Python GIL) and what the consuming launch must wait for.  ``finish()``
+    (idempotent) joins the job, makes the launch stream wait for the copy
+    stream, then runs the device-to-device copies of pieces that were already
+    on the device."""
+
+    def __init__(self, dev, job, cs, post):
+        self.dev = dev
+        self._job = job
+        self._cs = cs
+        self._post = post
+
+    def finish(self, stream: int | None = None) -> None:
+        if self._job is None:
+            return
+        import torch
+
+        from . import _native as N
+
+        rc = N.lib().zhip_stage_end(self._job)
+        self._job = None
+        N.check(rc, "zhip_stage_h2d")
+        st = torch.cuda.current_stream(self.dev.device) if stream is None else \
+            torch.cuda.ExternalStream(stream, device=self.dev.device)
+        st.wait_stream(self._cs)  # every window's copy was enqueued on cs before this
+        for fn in self._post:
+            fn(self.dev)
+        self._post = []
+
+
+def stage(layout: StagingLayout, device, post=(), defer: bool = False):
+    """Copy every piece to one new device buffer.  Returns (dev, keepalive,
+    pending); with defer the packing job keeps running when this returns and
+    the caller must ``pending.finish()`` before the first use of dev."""
     import torch
+
+    from . import _native as N
 
     total = max(layout.top, 16)
     host = torch.empty(total + TAIL_SLACK, dtype=torch.uint8, pin_memory=True)
     dev = torch.empty(total + TAIL_SLACK, dtype=torch.uint8, device=device)
-    hv = host.numpy()
-    by_window: dict = {}
-    for buf, off, n in layout.pieces:
-        a = 0
-        while a < n:
-            wi = (off + a) // WINDOW
-            b = min(n, (wi + 1) * WINDOW - off)
-            by_window.setdefault(wi, []).append((buf, off, a, b))
-            a = b
-    windows = [(wi * WINDOW, min((wi + 1) * WINDOW, total), by_window[wi])
-               for wi in sorted(by_window)]
-    pool = _pool()
-    futs = [pool.submit(_fill_window, hv, parts) for _, _, parts in windows]
+    views = [_host_view(buf) for buf, _, _ in layout.pieces]
+    pieces = np.zeros(len(views), N.PIECE_DT)
+    for i, (v, (_, off, n)) in enumerate(zip(views, layout.pieces)):
+        pieces[i] = (v.ctypes.data if n else 0, n, off)
     compute = torch.cuda.current_stream(device)
     cs = _copy_stream(device)
     cs.wait_stream(compute)
-    with torch.cuda.stream(cs):
-        for (a, b, _), f in zip(windows, futs):
-            f.result()
-            dev[a:b].copy_(host[a:b], non_blocking=True)
     dev.record_stream(cs)
-    compute.wait_stream(cs)
-    return dev, [dev, host]
+    job = N.lib().zhip_stage_begin(pieces.ctypes.data, len(pieces), host.data_ptr(), dev.data_ptr(), total,
+                                   WINDOW, _workers(), cs.cuda_stream)
+    if not job:
+        raise N.NativeError("zhip_stage_begin: out of memory")
+    pending = Pending(dev, job, cs, list(post))
+    if not defer:
+        pending.finish()
+    # the pinned block and the host views must outlive the copies: keep them
+    # with the program (dropped after its results() synchronised)
+    return dev, [dev, host, views], pending
 
 
-def gather_sources(batch: list, device):
+def gather_sources(batch: list, device, defer: bool = False):
     """Resolve every ByteGetter to (offset, length, missing) inside ONE device
     buffer: the shared arena for DeviceStore batches, else a staged copy.
     ByteGetters may be this package's or zarr's (whose get_sync returns a
     Buffer, src/zarr/storage/_common.py:247-258).
-    Returns (src, size, [(off, len, missing)], keepalive)."""
+    Returns (src, size, [(off, len, missing)], keepalive, pending | None)."""
     import torch
 
     raws = []
@@ -139,7 +165,7 @@ def gather_sources(batch: list, device):
             src = torch.zeros(TAIL_SLACK + 16, dtype=torch.uint8, device=device)
             size = 0
         srcs = [(0, 0, True) if r is None else (r.offset, r.length, False) for r in raws]
-        return src, size, srcs, [src]
+        return src, size, srcs, [src], None
     lay = StagingLayout()
     srcs = []
     dev_refs = []
@@ -154,11 +180,13 @@ def gather_sources(batch: list, device):
         else:
             off, n = lay.add(r)
             srcs.append((off, n, False))
-    dev, keep = stage(lay, device)
-    for r, off in dev_refs:
-        v = r.arena.view(r.offset, r.length) if isinstance(r, DeviceRef) else r
-        dev[off: off + v.numel()].copy_(v)
-    return dev, lay.top, srcs, keep
+    def d2d(dev):  # after the H2D windows (which also cover the reserved gaps)
+        for r, off in dev_refs:
+            v = r.arena.view(r.offset, r.length) if isinstance(r, DeviceRef) else r
+            dev[off: off + v.numel()].copy_(v)
+
+    dev, keep, pending = stage(lay, device, post=[d2d] if dev_refs else [], defer=defer)
+    return dev, lay.top, srcs, keep, pending
 
 
 def staged_host(buf):
@@ -173,7 +201,8 @@ def _shard_key(bg):
     return (id(st), getattr(bg, "path", id(bg)))
 
 
-def gather_sharded_partial(batch: list, sh, cps, n_inner: int, inner_shape, spec, device):
+def gather_sharded_partial(batch: list, sh, cps, n_inner: int, inner_shape, spec, device,
+                           defer: bool = False):
     """Host-sourced sharded batch: index by range request, touched inner chunks
     by coalesced range requests, staged into one device buffer.
 
@@ -240,7 +269,7 @@ def gather_sharded_partial(batch: list, sh, cps, n_inner: int, inner_shape, spec
                 off, n = lay.add(staged_host(buf))
                 src_by[slot], len_by[slot], miss_by[slot] = off, n, False
         out_of_shard[k] = (src_by, len_by, miss_by, idx_off)
-    dev, keep = stage(lay, device)
+    dev, keep, pending = stage(lay, device, defer=defer)
     missing = np.array([out_of_shard[k] is None for k in item_shard], bool)
     resolved = [out_of_shard[k] for k in item_shard]
-    return dev, lay.top, missing, resolved, keep
+    return dev, lay.top, missing, resolved, keep, pending
