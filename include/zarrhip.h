@@ -295,22 +295,35 @@ typedef struct zhip_piece {
     uint64_t host;     /* host address */
     uint64_t nbytes;
     uint64_t dst_off;  /* offset in the pinned and device buffers */
+    uint64_t flags;    /* ZHIP_PIECE_* */
 } zhip_piece;
 
-/* Pack the pieces into `pinned` (total bytes) with `nthreads` host threads,
- * window by window; each window's bytes are copied to `dev` by
- * hipMemcpyAsync on `stream` as soon as the window is packed.  Returns once
- * every copy is enqueued (they complete asynchronously on `stream`). */
+/* The piece's host bytes are page-locked (a pinned store's arena, a pinned
+ * tensor): DMA them straight to `dev`, no packing.  Runs of such pieces that
+ * are contiguous in both host and device order go as one copy. */
+#define ZHIP_PIECE_PINNED 1u
+
+/* Pack the pageable pieces into `pinned` (total bytes) with `nthreads` host
+ * threads, window by window; each window's packed runs are copied to `dev`
+ * by hipMemcpyAsync on `stream` as soon as the window is packed (pinned
+ * pieces are copied directly first).  Gaps of 256 bytes or more that no
+ * piece covers are left as they are in `dev`.  Returns once every copy is enqueued (they complete
+ * asynchronously on `stream`). */
 int zhip_stage_h2d(const zhip_piece *pieces, uint32_t n_pieces, uint8_t *pinned, void *dev, uint64_t total,
                    uint64_t window, uint32_t nthreads, void *stream);
 
-/* zhip_stage_h2d started on a library thread: returns at once (NULL on
+/* zhip_stage_h2d started on a library thread: the pinned pieces' copies are
+ * enqueued before it returns, the packing runs on the thread (NULL on
  * allocation failure); the pieces array is copied.  zhip_stage_end waits for
  * every copy to be enqueued and returns zhip_stage_h2d's code. */
 typedef struct zhip_stage_job zhip_stage_job;
 zhip_stage_job *zhip_stage_begin(const zhip_piece *pieces, uint32_t n_pieces, uint8_t *pinned, void *dev,
                                  uint64_t total, uint64_t window, uint32_t nthreads, void *stream);
 int zhip_stage_end(zhip_stage_job *job);
+
+/* 1 when p points into page-locked host memory known to HIP (a pinned
+ * result buffer can take the D2H DMA directly), else 0. */
+int zhip_host_pinned(const void *p);
 
 /* memcpy with `nthreads` host threads (pinned result -> a caller's host array). */
 int zhip_host_copy(void *dst, const void *src, uint64_t nbytes, uint32_t nthreads);

@@ -31,7 +31,8 @@ def main():
     shape, chunks = (256, 256, 256), (64, 64, 64)
     data = bench.synthetic(shape)
     darr = bench.build_replica(dev, torch.from_numpy(data).to(dev), shape, chunks, [bench.LE, bench.CRC])
-    host = zarr_hip.MemoryStore(darr.store_path.store.to_dict())
+    kind = os.environ.get("STORE", "memory")
+    host = (zarr_hip.PinnedMemoryStore if kind == "pinned" else zarr_hip.MemoryStore)(darr.store_path.store.to_dict())
     arr = zarr_hip.Array.open(host)
     out = torch.empty(shape, dtype=torch.float32, device=dev)
     acc = defaultdict(list)
@@ -48,6 +49,15 @@ def main():
 
     wrap(staging, "gather_sources", "gather_sources(fetch+pack+h2d enqueue)")
     wrap(staging, "stage", "  stage(pack+h2d enqueue)")
+    runs = []
+    inner_stage = staging.stage
+
+    def count_runs(layout, *a, **k):
+        addrs = [(staging._host_view(b).ctypes.data, off, n) for b, off, n in layout.pieces]
+        r = 1 + sum(1 for (h0, d0, _), (h1, d1, _) in zip(addrs, addrs[1:]) if h1 - h0 != d1 - d0)
+        runs.append(r)
+        return inner_stage(layout, *a, **k)
+    staging.stage = count_runs
     wrap(PL, "plan_decode", "plan_decode")
     wrap(PL.DecodeProgram, "launch", "launch")
     wrap(PL.DecodeProgram, "results", "results(sync)")
@@ -58,19 +68,31 @@ def main():
         orig_init(self, *a, **k)
         acc["DecodeLaunch.__init__(uploads)"].append(time.perf_counter() - t0)
     PL.DecodeLaunch.__init__ = init
+    from zarr_hip import _native as N
+
+    lib = N.lib()
+    begin = lib.zhip_stage_begin
+    t_get = [0.0]
+
+    def begin_w(*a):
+        if t_get[0]:
+            acc["get() start -> zhip_stage_begin call"].append(time.perf_counter() - t_get[0])
+        return begin(*a)
+    lib.zhip_stage_begin = begin_w
     for win in [int(x) for x in os.environ.get("WINDOWS", "1,2,4,8").split(",")]:
         staging.WINDOW = win << 20
         for i in range(12):
             torch.cuda.synchronize(dev)
-            t0 = time.perf_counter()
+            t0 = t_get[0] = time.perf_counter()
             arr.get((Ellipsis,), out=out)
+            t_get[0] = 0.0
             torch.cuda.synchronize(dev)
             if i >= 2:
-                acc[f"TOTAL get(out=device) window {win} MiB"].append(time.perf_counter() - t0)
+                acc[f"TOTAL get(out=device) {kind} window {win} MiB"].append(time.perf_counter() - t0)
             t0 = time.perf_counter()
             arr[...]
             if i >= 2:
-                acc[f"TOTAL __getitem__ (host out) window {win} MiB"].append(time.perf_counter() - t0)
+                acc[f"TOTAL __getitem__ (host out) {kind} window {win} MiB"].append(time.perf_counter() - t0)
     assert out.view(torch.int32).cpu().numpy().tobytes() == data.view(np.int32).tobytes()
     if os.environ.get("CPROFILE"):
         import cProfile
@@ -94,6 +116,7 @@ def main():
         dbuf.copy_(pin, non_blocking=True)
         torch.cuda.synchronize(dev)
         acc["raw pinned H2D 64 MiB"].append(time.perf_counter() - t0)
+    print(json.dumps({"phase": "host-contiguous runs per stage", "runs": runs[-1:], "store": kind}), flush=True)
     for k, v in acc.items():
         print(json.dumps({"phase": k, "ms_med": round(float(np.median(v)) * 1e3, 3), "n": len(v)}), flush=True)
 

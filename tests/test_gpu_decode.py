@@ -54,8 +54,12 @@ def _roundtrip(device, shape, chunks, dtype, codecs, fill=0, selection=(Ellipsis
     O.write(host, meta, (Ellipsis,), data)
     for k in drop or []:
         host.pop(k, None)
-    store = zarr_hip.MemoryStore(dict(host)) if host_store else zarr_hip.DeviceStore.from_host(
-        host, device)
+    if host_store == "pinned":
+        store = zarr_hip.PinnedMemoryStore(dict(host))
+    elif host_store:
+        store = zarr_hip.MemoryStore(dict(host))
+    else:
+        store = zarr_hip.DeviceStore.from_host(host, device)
     arr = zarr_hip.Array.create(store, shape, chunks, dtype, fill, codecs=codecs,
                                 config=ArrayConfig(order=order))
     got = arr[selection]

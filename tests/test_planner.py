@@ -10,7 +10,7 @@ import pytest
 
 from oracle import oracle as O
 from zarr_hip import codecs as C
-from zarr_hip.indexing import basic_projections, morton_order, subchunk_order, to_chunk_selection
+from zarr_hip.indexing import basic_projections, chunk_batch, morton_order, subchunk_order, to_chunk_selection
 from zarr_hip.planner import analyze_chain
 from zarr_hip.spec import ArraySpec
 
@@ -41,6 +41,26 @@ def test_projections_match_oracle(sel, shape, chunks):
         return sorted(out)
 
     assert norm(got) == norm(want)
+    # the batch builder (lists, Array.batch_info) gives the same rows in the same order
+    rows, shape_b = chunk_batch(sel, shape, chunks)
+    assert shape_b == pr.out_shape
+    assert [(tuple(c), cs, os_, cp) for c, cs, os_, cp in rows] == got
+
+
+def test_chunk_batch_long_dims_match_projections():
+    rng = np.random.default_rng(3)
+    for _ in range(40):
+        n = int(rng.integers(1, 5000))
+        c = int(rng.integers(1, 9))
+        a, b = sorted(int(x) for x in rng.integers(0, n + 1, 2))
+        st = int(rng.integers(1, 6))
+        sel = (slice(a, b, st),)
+        pr = basic_projections(sel, (n,), (c,))
+        rows, out_shape = chunk_batch(sel, (n,), (c,))
+        assert out_shape == pr.out_shape
+        assert [(co, cs, os_, cp) for co, cs, os_, cp in rows] == [
+            ((int(pr.coords[i][0]),), *to_chunk_selection(pr, i), bool(pr.complete[i]))
+            for i in range(len(pr.coords))]
 
 
 def test_morton_matches_reference_vectors():

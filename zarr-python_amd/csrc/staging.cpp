@@ -83,6 +83,92 @@ Pool& pool() {
     return *p;
 }
 
+// Page-locked pieces: straight DMA, merged while both the host and the
+// device sides stay contiguous (a pinned store's values lie in its arena in
+// write order, with the same alignment gaps as the layout).  Returns whether
+// any pageable piece is left for pack_windows; *rc is set on a HIP error.
+static bool enqueue_pinned(const zhip_piece* pieces, uint32_t n_pieces, uint8_t* d, hipStream_t st, int* rc) {
+    bool any_packed = false;
+    for (uint32_t i = 0; i < n_pieces;) {
+        if (!(pieces[i].flags & ZHIP_PIECE_PINNED) || pieces[i].nbytes == 0) {
+            any_packed |= pieces[i].nbytes != 0;
+            ++i;
+            continue;
+        }
+        uint32_t j = i + 1;
+        while (j < n_pieces && (pieces[j].flags & ZHIP_PIECE_PINNED) && pieces[j].nbytes &&
+               pieces[j].host - pieces[i].host == pieces[j].dst_off - pieces[i].dst_off &&
+               pieces[j].host >= pieces[j - 1].host + pieces[j - 1].nbytes &&
+               pieces[j].host - (pieces[j - 1].host + pieces[j - 1].nbytes) < 256)
+            ++j;
+        const uint64_t n = pieces[j - 1].dst_off + pieces[j - 1].nbytes - pieces[i].dst_off;
+        if (hipMemcpyAsync(d + pieces[i].dst_off, reinterpret_cast<const void*>(pieces[i].host), n,
+                           hipMemcpyHostToDevice, st) != hipSuccess)
+            *rc = ZHIP_E_HIP;
+        i = j;
+    }
+    return any_packed;
+}
+
+static int pack_windows(const zhip_piece* pieces, uint32_t n_pieces, uint8_t* pinned, uint8_t* d, uint64_t total,
+                        uint64_t window, uint32_t nthreads, hipStream_t st) {
+    std::atomic<int> rc{ZHIP_OK};
+    if (window < 4096) window = 4096;
+    // Pageable pieces: windows ramp up from window/16 (the first DMA starts
+    // after a small pack, not a whole window) to `window`; one window per
+    // task, taken in order, packed by one thread, which then enqueues the
+    // window's packed runs.  (Packing a window by all threads together in
+    // 256 KiB sub-ranges starts the first DMA sooner too but measured 30 %
+    // slower end to end: scripts/stage_micro.py.)
+    std::vector<uint64_t> edge{0};
+    for (uint64_t w = window >= (64u << 10) ? window / 16 : window; edge.back() < total; w = w * 2 < window ? w * 2 : window)
+        edge.push_back(edge.back() + w < total ? edge.back() + w : total);
+    const uint64_t n_win = edge.size() - 1;
+    // pieces are sorted by destination offset: window w starts at the first
+    // piece reaching past its start
+    std::vector<uint32_t> first(n_win + 1, n_pieces);
+    {
+        uint32_t i = 0;
+        for (uint64_t w = 0; w < n_win; ++w) {
+            while (i < n_pieces && pieces[i].dst_off + pieces[i].nbytes <= edge[w]) ++i;
+            first[w] = i;
+        }
+    }
+    std::atomic<uint64_t> next{0};
+    auto worker = [&](int) {
+        for (;;) {
+            const uint64_t w = next.fetch_add(1);
+            if (w >= n_win) return;
+            const uint64_t a = edge[w], b = edge[w + 1];
+            uint64_t run_s = 0, run_e = 0;  // packed run (alignment pads between pieces ride along)
+            auto flush = [&] {
+                if (run_e > run_s &&
+                    hipMemcpyAsync(d + run_s, pinned + run_s, run_e - run_s, hipMemcpyHostToDevice, st) != hipSuccess)
+                    rc.store(ZHIP_E_HIP);
+                run_s = run_e = 0;
+            };
+            for (uint32_t i = first[w]; i < n_pieces && pieces[i].dst_off < b; ++i) {
+                const zhip_piece& pc = pieces[i];
+                if (pc.flags & ZHIP_PIECE_PINNED) {
+                    if (pc.nbytes) flush();
+                    continue;
+                }
+                const uint64_t s = pc.dst_off > a ? pc.dst_off : a;
+                const uint64_t e = pc.dst_off + pc.nbytes < b ? pc.dst_off + pc.nbytes : b;
+                if (s >= e) continue;
+                std::memcpy(pinned + s, reinterpret_cast<const uint8_t*>(pc.host) + (s - pc.dst_off), e - s);
+                if (run_e > run_s && s - run_e >= 256) flush();  // a real gap: leave it alone
+                if (run_e == run_s) run_s = s;
+                run_e = e;
+            }
+            flush();
+        }
+    };
+    const uint32_t nt = nthreads == 0 ? 1u : (nthreads > 64 ? 64u : nthreads);
+    pool().run((int)(nt < n_win ? nt : n_win), worker);
+    return rc.load();
+}
+
 }  // namespace
 
 extern "C" {
@@ -91,45 +177,14 @@ int zhip_stage_h2d(const zhip_piece* pieces, uint32_t n_pieces, uint8_t* pinned,
                    uint64_t window, uint32_t nthreads, void* stream) {
     if (total == 0) return ZHIP_OK;
     if (!pinned || !dev || (!pieces && n_pieces)) return ZHIP_E_INVALID;
-    if (window < 4096) window = 4096;
-    // One window per task, taken in order: each thread packs a whole window
-    // and hands it to the copy engine.  (Packing a window by all threads
-    // together in 256 KiB sub-ranges starts the first DMA sooner but measured
-    // 30 % slower end to end: scripts/stage_micro.py.)
-    const uint64_t n_win = (total + window - 1) / window;
-    // pieces are sorted by destination offset: window w starts at the first
-    // piece reaching past w * window
-    std::vector<uint32_t> first(n_win + 1, n_pieces);
-    {
-        uint32_t i = 0;
-        for (uint64_t w = 0; w < n_win; ++w) {
-            while (i < n_pieces && pieces[i].dst_off + pieces[i].nbytes <= w * window) ++i;
-            first[w] = i;
-        }
+    int rc = ZHIP_OK;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    uint8_t* const d = static_cast<uint8_t*>(dev);
+    if (enqueue_pinned(pieces, n_pieces, d, st, &rc)) {
+        const int r2 = pack_windows(pieces, n_pieces, pinned, d, total, window, nthreads, st);
+        if (r2 != ZHIP_OK) rc = r2;
     }
-    std::atomic<uint64_t> next{0};
-    std::atomic<int> rc{ZHIP_OK};
-    auto worker = [&](int) {
-        for (;;) {
-            const uint64_t w = next.fetch_add(1);
-            if (w >= n_win) return;
-            const uint64_t a = w * window, b = a + window < total ? a + window : total;
-            for (uint32_t i = first[w]; i < n_pieces && pieces[i].dst_off < b; ++i) {
-                const zhip_piece& pc = pieces[i];
-                const uint64_t s = pc.dst_off > a ? pc.dst_off : a;
-                const uint64_t e = pc.dst_off + pc.nbytes < b ? pc.dst_off + pc.nbytes : b;
-                if (s < e)
-                    std::memcpy(pinned + s, reinterpret_cast<const uint8_t*>(pc.host) + (s - pc.dst_off), e - s);
-            }
-            // gaps between pieces stay as they are: the kernels never read them
-            if (hipMemcpyAsync(static_cast<uint8_t*>(dev) + a, pinned + a, b - a, hipMemcpyHostToDevice,
-                               static_cast<hipStream_t>(stream)) != hipSuccess)
-                rc.store(ZHIP_E_HIP);
-        }
-    };
-    const uint32_t nt = nthreads == 0 ? 1u : (nthreads > 64 ? 64u : nthreads);
-    pool().run((int)(nt < n_win ? nt : n_win), worker);
-    return rc.load();
+    return rc;
 }
 
 // The same job started on a host thread of the library (no caller thread, no
@@ -149,6 +204,16 @@ zhip_stage_job* zhip_stage_begin(const zhip_piece* pieces, uint32_t n_pieces, ui
                                  uint64_t total, uint64_t window, uint32_t nthreads, void* stream) {
     zhip_stage_job* j = new (std::nothrow) zhip_stage_job();
     if (!j) return nullptr;
+    j->rc = ZHIP_OK;
+    if (total == 0) return j;
+    if (!pinned || !dev || (!pieces && n_pieces)) {
+        j->rc = ZHIP_E_INVALID;
+        return j;
+    }
+    // pinned pieces are enqueued right here (a few hipMemcpyAsync calls);
+    // only packing needs the library thread
+    if (!enqueue_pinned(pieces, n_pieces, static_cast<uint8_t*>(dev), static_cast<hipStream_t>(stream), &j->rc))
+        return j;
     j->pieces.assign(pieces, pieces + n_pieces);
     j->pinned = pinned;
     j->dev = dev;
@@ -156,10 +221,11 @@ zhip_stage_job* zhip_stage_begin(const zhip_piece* pieces, uint32_t n_pieces, ui
     j->window = window;
     j->nthreads = nthreads;
     j->stream = stream;
-    j->rc = ZHIP_OK;
     j->th = std::thread([j] {
-        j->rc = zhip_stage_h2d(j->pieces.data(), (uint32_t)j->pieces.size(), j->pinned, j->dev, j->total,
-                               j->window, j->nthreads, j->stream);
+        const int r = pack_windows(j->pieces.data(), (uint32_t)j->pieces.size(), j->pinned,
+                                   static_cast<uint8_t*>(j->dev), j->total, j->window, j->nthreads,
+                                   static_cast<hipStream_t>(j->stream));
+        if (r != ZHIP_OK) j->rc = r;
     });
     return j;
 }
@@ -170,6 +236,16 @@ int zhip_stage_end(zhip_stage_job* j) {
     const int rc = j->rc;
     delete j;
     return rc;
+}
+
+int zhip_host_pinned(const void* p) {
+    if (!p) return 0;
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();  // pageable memory: not an error for the caller
+        return 0;
+    }
+    return a.type == hipMemoryTypeHost ? 1 : 0;
 }
 
 int zhip_host_copy(void* dst, const void* src, uint64_t nbytes, uint32_t nthreads) {

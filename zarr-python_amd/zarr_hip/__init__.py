@@ -12,11 +12,11 @@ from .buffer import Buffer, BufferPrototype, NDBuffer, buffer_prototype
 from .codecs import BytesCodec, Crc32cCodec, ShardingCodec, TransposeCodec
 from .pipeline import DecodeProgram, HipCodecPipeline, ReadGraph
 from .spec import ArrayConfig, ArraySpec, GetResult
-from .store import DeviceStore, LocalStore, MemoryStore, StorePath
+from .store import DeviceStore, LocalStore, MemoryStore, PinnedMemoryStore, StorePath
 
 __all__ = [
     "Array", "ArrayMetadata", "ArrayConfig", "ArraySpec", "Buffer", "BufferPrototype", "BytesCodec",
     "ChunkNotFoundError", "NDBuffer", "buffer_prototype",
     "Crc32cCodec", "DecodeProgram", "DeviceStore", "GetResult", "HipCodecPipeline", "LocalStore",
-    "MemoryStore", "ReadGraph", "ShardingCodec", "StorePath", "TransposeCodec",
+    "MemoryStore", "PinnedMemoryStore", "ReadGraph", "ShardingCodec", "StorePath", "TransposeCodec",
 ]

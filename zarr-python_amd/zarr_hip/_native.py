@@ -118,7 +118,8 @@ class Predict(ctypes.Structure):
 
 
 # zhip_piece (include/zarrhip.h)
-PIECE_DT = np.dtype([("host", "<u8"), ("nbytes", "<u8"), ("dst_off", "<u8")])
+PIECE_DT = np.dtype([("host", "<u8"), ("nbytes", "<u8"), ("dst_off", "<u8"), ("flags", "<u8")])
+PIECE_PINNED = 1
 
 # zhip_rowblk (include/zarrhip.h)
 ROWBLK_DT = np.dtype([("rel", "<i4"), ("lo", "<u2"), ("hi", "<u2")])
@@ -201,6 +202,8 @@ def lib():
     L.zhip_stage_begin.restype = ctypes.c_void_p
     L.zhip_stage_end.argtypes = [ctypes.c_void_p]
     L.zhip_stage_end.restype = ctypes.c_int
+    L.zhip_host_pinned.argtypes = [ctypes.c_void_p]
+    L.zhip_host_pinned.restype = ctypes.c_int
     L.zhip_host_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32]
     L.zhip_host_copy.restype = ctypes.c_int
     L.zhip_emulate_chunk_crc_pair.argtypes = [ctypes.c_void_p, ctypes.c_void_p]

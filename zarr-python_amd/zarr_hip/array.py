@@ -19,10 +19,10 @@ import numpy as np
 
 from . import buffer
 from .codecs import BytesCodec, Crc32cCodec, ShardingCodec, parse_codecs
-from .indexing import basic_projections, to_chunk_selection
+from .indexing import basic_projections, chunk_batch
 from .pipeline import DecodeProgram, HipCodecPipeline
 from .spec import ArrayConfig, ArraySpec
-from .store import StorePath
+from .store import DeviceStore, StorePath
 
 
 def _fill_from_json(v, dtype: np.dtype):
@@ -151,13 +151,12 @@ class Array:
         return f"{self.store_path.path}/{k}" if self.store_path.path else k
 
     def batch_info(self, selection):
-        pr = basic_projections(selection, self.metadata.shape, self.metadata.chunk_shape)
-        batch = []
-        for i in range(len(pr.coords)):
-            csel, osel = to_chunk_selection(pr, i)
-            batch.append((StorePath(self.store_path.store, self._key(pr.coords[i])), self.spec,
-                          csel, osel, bool(pr.complete[i])))
-        return batch, pr.out_shape
+        rows, out_shape = chunk_batch(selection, self.metadata.shape, self.metadata.chunk_shape)
+        store, spec, sep = self.store_path.store, self.spec, self.metadata.separator
+        prefix = f"{self.store_path.path}/c" if self.store_path.path else "c"
+        batch = [(StorePath(store, sep.join([prefix, *map(str, co)])), spec, csel, osel, comp)
+                 for co, csel, osel, comp in rows]
+        return batch, out_shape
 
     # ------------------------------------------------------------------- read
     def prepare_read(self, selection=Ellipsis, out=None, device=None) -> tuple[DecodeProgram, Any]:
@@ -189,7 +188,23 @@ class Array:
         return out
 
     def __getitem__(self, selection) -> np.ndarray:
-        return buffer.to_numpy(self.get(selection), self.metadata.dtype)
+        """Host result.  Host-resident stores read into a pinned numpy array:
+        the pipeline streams slabs back while later slabs still decode
+        (HipCodecPipeline._read_slabs); HBM-resident stores decode on the
+        device and copy the result back once."""
+        st = self.store_path.store
+        if isinstance(st, DeviceStore):
+            return buffer.to_numpy(self.get(selection), self.metadata.dtype)
+        batch, out_shape = self.batch_info(selection)
+        out = buffer.empty_pinned(out_shape, self.metadata.dtype, self.config.order)
+        if not batch:
+            return out
+        results = self.codec_pipeline.read_sync(batch, out)
+        if not self.config.read_missing_chunks:
+            for (bg, *_), r in zip(batch, results):
+                if r["status"] == "missing":
+                    raise ChunkNotFoundError(f"chunk {bg.path!r} is missing")
+        return out
 
     # ------------------------------------------------------------------ write
     def set(self, selection, value) -> None:

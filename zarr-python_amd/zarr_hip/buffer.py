@@ -108,6 +108,35 @@ def copy_to_host(t, dst: np.ndarray) -> None:
         np.copyto(dst, src, casting="no")
 
 
+def copy_to_host_from_pinned(src, dst: np.ndarray) -> None:
+    """A pinned uint8 tensor holding a C-contiguous image of dst's values ->
+    dst (any layout), by the library's host thread pool when dst is
+    C-contiguous."""
+    a = src.numpy()[: dst.nbytes].view(dst.dtype.newbyteorder("=")).reshape(dst.shape)
+    if dst.flags.c_contiguous and dst.dtype.isnative:
+        import os
+
+        from . import _native as N
+
+        threads = max(1, min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "0") or 16), 16))
+        N.check(N.lib().zhip_host_copy(dst.ctypes.data, a.ctypes.data, dst.nbytes, threads), "zhip_host_copy")
+    else:
+        np.copyto(dst, a, casting="unsafe")
+
+
+def empty_pinned(shape, dtype, order: str = "C") -> np.ndarray:
+    """A host array in page-locked memory (torch's caching host allocator):
+    reads decode into its device twin and DMA the result straight into it."""
+    import torch
+
+    from .interop import native_dtype
+
+    dt = native_dtype(dtype).newbyteorder("=")
+    n = int(np.prod(shape, dtype=np.int64)) * dt.itemsize
+    a = torch.empty(max(n, 1), dtype=torch.uint8, pin_memory=True).numpy()[:n].view(dt)
+    return a.reshape(tuple(shape), order="F" if order == "F" else "C")
+
+
 def _to_device(a, dtype=None):
     """Any array-like -> torch CUDA tensor (zero-copy when already on the device)."""
     import torch

@@ -150,6 +150,90 @@ def to_chunk_selection(p: Projections, i: int) -> tuple:
     return tuple(csel), tuple(osel)
 
 
+def _project_dim_lists(sel, dim_len: int, chunk_len: int):
+    """project_dim as Python lists (ix, sel_start, sel_count, out_start,
+    complete, step, dropped, nitems); numpy only for long dims."""
+    if isinstance(sel, int):
+        ix = sel // chunk_len
+        return ([ix], [sel - ix * chunk_len], [1], [0], [min(chunk_len, dim_len - ix * chunk_len) == 1], 1,
+                True, 1)
+    start, stop, step = sel.start, sel.stop, sel.step
+    nitems = max(0, -((start - stop) // step))
+    if start >= stop:
+        return [], [], [], [], [], step, False, 0
+    ix_from, ix_to = start // chunk_len, (stop - 1) // chunk_len + 1
+    if ix_to - ix_from > 256:
+        d = project_dim(sel, dim_len, chunk_len)
+        return (d.chunk_ix.tolist(), d.sel_start.tolist(), d.sel_count.tolist(), d.out_start.tolist(),
+                d.complete.tolist(), step, False, nitems)
+    ixs, s0s, cnts, oos, cps = [], [], [], [], []
+    for ix in range(ix_from, ix_to):
+        off = ix * chunk_len
+        clen = min(chunk_len, dim_len - off)
+        limit = off + clen
+        if start < off:
+            rem = (off - start) % step
+            s0 = step - rem if rem else 0
+            oo = -((start - off) // step)
+        else:
+            s0, oo = start - off, 0
+        s1 = clen if stop > limit else stop - off
+        cnt = max(0, -((s0 - s1) // step))
+        if cnt > 0:
+            ixs.append(ix)
+            s0s.append(s0)
+            cnts.append(cnt)
+            oos.append(oo)
+            cps.append(s0 == 0 and stop >= limit and step == 1)
+    return ixs, s0s, cnts, oos, cps, step, False, nitems
+
+
+def chunk_batch(selection, shape: tuple[int, ...], chunk_shape: tuple[int, ...]):
+    """basic_projections + chunk_selections for a batch: per-dim projections,
+    then their Cartesian product (C order over chunk coordinates, as
+    basic_projections) built from Python lists.  Returns
+    ([(coords, chunk_selection, out_selection, complete)], out_shape)."""
+    import itertools
+
+    sel = normalize_selection(selection, shape)
+    ixs, csels, osels, cps = [], [], [], []
+    out_shape = []
+    for s, n, c in zip(sel, shape, chunk_shape):
+        ix, s0, cnt, oo, cp, st, dropped, nitems = _project_dim_lists(s, n, c)
+        ixs.append(ix)
+        cps.append(cp)
+        if dropped:
+            csels.append(s0)
+        else:
+            out_shape.append(nitems)
+            csels.append([slice(a, a + (k - 1) * st + 1, st) for a, k in zip(s0, cnt)])
+            osels.append([slice(o, o + k) for o, k in zip(oo, cnt)])
+    P = itertools.product
+    out = list(zip(P(*ixs), P(*csels), P(*osels), map(all, P(*cps))))
+    return out, tuple(out_shape)
+
+
+def chunk_selections(p: Projections) -> list:
+    """to_chunk_selection for every row, from Python lists (one pass)."""
+    nd = p.coords.shape[1]
+    ss, cc, oo = p.sel_start.tolist(), p.sel_count.tolist(), p.out_start.tolist()
+    steps = p.step.tolist()
+    drop = p.dropped
+    out = []
+    for s_row, c_row, o_row in zip(ss, cc, oo):
+        csel, osel = [], []
+        for d in range(nd):
+            s0 = s_row[d]
+            if drop[d]:
+                csel.append(s0)
+                continue
+            st, cnt, o = steps[d], c_row[d], o_row[d]
+            csel.append(slice(s0, s0 + (cnt - 1) * st + 1, st))
+            osel.append(slice(o, o + cnt))
+        out.append((tuple(csel), tuple(osel)))
+    return out
+
+
 # --- Morton / lexicographic orders (src/zarr/core/indexing.py:1524-1643) -------
 
 def morton_order(shape: tuple[int, ...]) -> np.ndarray:

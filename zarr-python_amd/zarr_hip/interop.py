@@ -18,6 +18,8 @@ from typing import Any
 
 import numpy as np
 
+from .store import DeviceRef, DeviceStore, MemoryStore
+
 KDL_ROCM = 10  # DLPack device type of ROCm/HIP memory
 
 
@@ -92,8 +94,6 @@ def byte_payload(value, host: bool = False):
     (and host=False), else a 1-D uint8 numpy array.  Accepts bytes-likes, numpy,
     torch, zarr Buffers and this package's buffers."""
     torch = _torch()
-    from .store import DeviceRef
-
     if isinstance(value, (bytes, bytearray, memoryview)):
         return np.frombuffer(value, dtype=np.uint8)
     if isinstance(value, DeviceRef):
@@ -111,12 +111,10 @@ def byte_payload(value, host: bool = False):
 def staged_bytes(raw):
     """What a ByteGetter returned, as something staging can pack: a DeviceRef /
     device tensor stays on the device; host buffers become uint8 numpy views."""
-    from .store import DeviceRef
-
-    if raw is None or isinstance(raw, DeviceRef):
+    if raw is None or isinstance(raw, (DeviceRef, bytes, bytearray, memoryview)):
         return raw
-    if isinstance(raw, (bytes, bytearray, memoryview)):
-        return raw
+    if type(raw) is np.ndarray and raw.dtype == np.uint8 and raw.ndim == 1 and raw.flags.c_contiguous:
+        return raw  # a pinned store's arena view, already host bytes
     t = device_tensor(raw)
     if t is not None:
         return t.reshape(-1).view(_torch().uint8)
@@ -134,8 +132,6 @@ def wrap_for_setter(data: bytes, prototype):
 
 
 def is_own_store(obj) -> bool:
-    from .store import DeviceStore, MemoryStore
-
     return isinstance(obj, (DeviceStore, MemoryStore))
 
 

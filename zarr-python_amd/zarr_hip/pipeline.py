@@ -489,14 +489,62 @@ class HipCodecPipeline:
         if not batch:
             return ()
         dev_out, host_out = _resolve_out(out, batch, drop_axes)
+        direct = host_out is not None and _pinned_host(host_out, dev_out)
+        if host_out is not None and not drop_axes and not _device_resident(batch):
+            groups = _slab_groups(batch, dev_out)
+            if groups is not None:
+                return self._read_slabs(batch, groups, dev_out, host_out, direct)
         prog = self.prepare_read(batch, dev_out, drop_axes)
         prog.launch()
         res = prog.results()
-        if host_out is not None:
+        if direct:
+            _d2h(dev_out, host_out, 0, dev_out.numel() * dev_out.element_size())
+            _torch().cuda.current_stream(dev_out.device).synchronize()
+        elif host_out is not None:
             from .buffer import copy_to_host
 
             copy_to_host(dev_out, host_out)
         return res
+
+    def _read_slabs(self, batch, groups, dev_out, host_out, direct: bool) -> tuple[GetResult, ...]:
+        """A host-sourced read into a host out, pipelined over row slabs of
+        out: slab k's chunks decode on the compute stream while slab k+1's
+        bytes cross PCIe on the copy stream (staging), and slab k's rows go
+        back on a D2H stream meanwhile -- H2D, decode and D2H overlap (PCIe
+        is full duplex).  The result is what one whole-batch read gives:
+        slabs are disjoint, every chunk lands in exactly one."""
+        torch = _torch()
+        dev = dev_out.device
+        compute = torch.cuda.current_stream(dev)
+        d2h = _d2h_stream(dev)
+        nbytes = dev_out.numel() * dev_out.element_size()
+        bounce = None if direct else torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+        done = []
+        for a, b, idx in groups:
+            prog = self.prepare_read([batch[i] for i in idx], dev_out)
+            prog.launch()
+            ev = torch.cuda.Event()
+            ev.record(compute)
+            d2h.wait_event(ev)
+            with torch.cuda.stream(d2h):
+                if direct:
+                    _d2h(dev_out, host_out, a, b)
+                else:
+                    flat = dev_out.reshape(-1).view(torch.uint8)
+                    bounce[a:b].copy_(flat[a:b], non_blocking=True)
+            done.append((prog, idx))
+        results: list = [None] * len(batch)
+        try:
+            for prog, idx in done:
+                for i, r in zip(idx, prog.results()):
+                    results[i] = r
+        finally:
+            d2h.synchronize()
+        if not direct:
+            from .buffer import copy_to_host_from_pinned
+
+            copy_to_host_from_pinned(bounce, host_out)
+        return tuple(results)
 
     async def read(self, batch_info: Iterable, out, drop_axes: tuple = ()) -> tuple[GetResult, ...]:
         # one thread hop per batch, as FusedCodecPipeline.read (codec_pipeline.py:1287-1289)
@@ -589,8 +637,11 @@ class HipCodecPipeline:
 def normalize_batch(batch_info: Iterable) -> list:
     """batch_info with every spec as this package's ArraySpec (zarr's ArraySpec
     carries a ZDType dtype, array_spec.py:137-186)."""
+    items = batch_info if isinstance(batch_info, list) else list(batch_info)
+    if all(type(it) is tuple and type(it[1]) is ArraySpec for it in items):
+        return items  # already normalized (read_sync -> prepare_read)
     out = []
-    for it in batch_info:
+    for it in items:
         it = tuple(it)
         out.append((it[0], coerce_spec(it[1])) + it[2:])
     return out
@@ -630,6 +681,69 @@ def _resolve_out(out, batch, drop_axes):
     if covered < h.size:  # regions no chunk writes keep their host values
         twin.copy_(torch.from_numpy(np.ascontiguousarray(h).astype(h.dtype.newbyteorder("="))))
     return twin, h
+
+
+_D2H_STREAMS: dict = {}
+
+
+def _d2h_stream(device):
+    torch = _torch()
+    key = torch.device(device).index
+    st = _D2H_STREAMS.get(key)
+    if st is None:
+        st = _D2H_STREAMS[key] = torch.cuda.Stream(device=device)
+    return st
+
+
+def _pinned_host(h: np.ndarray, dev_out) -> bool:
+    """A C-contiguous host out in page-locked memory, byte-compatible with the
+    device twin: the D2H DMA can write it directly."""
+    return (h.flags.c_contiguous and h.dtype.isnative and h.nbytes == dev_out.numel() * dev_out.element_size()
+            and h.nbytes > 0 and N.lib().zhip_host_pinned(h.ctypes.data) == 1)
+
+
+def _d2h(dev_out, host_out: np.ndarray, a: int, b: int) -> None:
+    """Bytes [a, b) of the (contiguous) device twin into the pinned host out,
+    on the current stream."""
+    torch = _torch()
+    if b <= a:
+        return
+    flat = dev_out.reshape(-1).view(torch.uint8)
+    dst = torch.from_numpy(host_out.reshape(-1).view(np.uint8))
+    dst[a:b].copy_(flat[a:b], non_blocking=True)
+
+
+def _slab_groups(batch: list, dev_out, min_bytes: int = 8 << 20, max_groups: int = 8):
+    """Items grouped by disjoint row slabs of a C-contiguous out (out dim 0):
+    [(byte_lo, byte_hi, item indices)], at least two groups of about
+    max(min_bytes, out / max_groups) bytes each; None when the batch does not
+    split that way (one chunk row, strided rows, small outs)."""
+    if dev_out.dim() == 0 or not dev_out.is_contiguous() or dev_out.shape[0] == 0:
+        return None
+    row_bytes = dev_out[0].numel() * dev_out.element_size()
+    total = row_bytes * dev_out.shape[0]
+    if total < 2 * min_bytes:
+        return None
+    rows: dict = {}
+    for i, it in enumerate(batch):
+        osel = it[3]
+        if not osel or not isinstance(osel[0], slice) or (osel[0].step or 1) != 1:
+            return None
+        rows.setdefault((osel[0].start or 0, osel[0].stop), []).append(i)
+    keys = sorted(rows)
+    if len(keys) < 2 or any(k1[0] < k0[1] for k0, k1 in zip(keys, keys[1:])):
+        return None
+    target = max(min_bytes, total // max_groups)
+    groups, cur, lo = [], [], None
+    for a, b in keys:
+        lo = a if lo is None else lo
+        cur += rows[(a, b)]
+        if (b - lo) * row_bytes >= target:
+            groups.append((lo * row_bytes, b * row_bytes, cur))
+            cur, lo = [], None
+    if cur:
+        groups.append((lo * row_bytes, keys[-1][1] * row_bytes, cur))
+    return groups if len(groups) >= 2 else None
 
 
 def _resolve_value(value):

@@ -84,6 +84,22 @@ def _sel_fields(csel, ndim):
     return start, count, step, is_int
 
 
+def _sel_lists(csel):
+    """_sel_fields as Python lists (the per-item planning loop)."""
+    st, ct, sp = [], [], []
+    for s in csel:
+        if isinstance(s, slice):
+            a, k = s.start or 0, s.step or 1
+            st.append(a)
+            sp.append(k)
+            ct.append(max(0, -((a - s.stop) // k)))
+        else:
+            st.append(int(s))
+            ct.append(1)
+            sp.append(1)
+    return st, ct, sp
+
+
 def out_dim_strides(ndim: int, is_int: np.ndarray, drop_axes, out_strides_bytes) -> np.ndarray:
     """Per decoded dim: the out byte stride (0 for dims absent from out)."""
     kept = [d for d in range(ndim) if not is_int[d]]
@@ -143,7 +159,10 @@ def _pack_sels(start, count, step) -> tuple[np.ndarray, np.ndarray]:
     """Dedup selection rows; returns (SEL_DT table, row index per entry)."""
     n, nd = start.shape
     key = np.concatenate([start, count, step], axis=1)
-    uniq, inv = np.unique(key, axis=0, return_inverse=True)
+    if n and (key == key[0]).all():  # the common case: every chunk selected alike
+        uniq, inv = key[:1], np.zeros(n, np.int64)
+    else:
+        uniq, inv = np.unique(key, axis=0, return_inverse=True)
     sels = np.zeros(len(uniq), SEL_DT)
     for r, row in enumerate(uniq):
         st, ct, sp = row[:nd], row[nd:2 * nd], row[2 * nd:]
@@ -288,17 +307,25 @@ def plan_decode(chain: ChainInfo, spec: ArraySpec, items: list, out_strides_byte
         layout = _make_layout(shape_st, itemsize, ost_st, flags, fill)
         n = len(items)
         chunks = np.zeros(n, CHUNK_DT)
-        start = np.zeros((n, ndim), np.int64)
-        count = np.zeros((n, ndim), np.int64)
-        step = np.zeros((n, ndim), np.int64)
-        for i, (so, sl, miss, csel, osel) in enumerate(items):
-            st, ct, sp, _ = _sel_fields(csel, ndim)
-            start[i], count[i], step[i] = st[list(perm)], ct[list(perm)], sp[list(perm)]
-            chunks["src"][i] = so
-            chunks["src_len"][i] = sl
-            chunks["flags"][i] = N.CF_MISSING if miss else 0
-            chunks["out_off"][i] = _out_offset(osel, out_strides_bytes) + \
-                (0 if item_out_extra is None else int(item_out_extra[i]))
+        S, C, P, oo = [], [], [], []
+        ostr = [int(x) for x in out_strides_bytes]
+        for so, sl, miss, csel, osel in items:
+            st, ct, sp = _sel_lists(csel)
+            S.append(st)
+            C.append(ct)
+            P.append(sp)
+            oo.append(sum(((s.start or 0) if isinstance(s, slice) else int(s)) * o for s, o in zip(osel, ostr)))
+        pl = list(perm)
+        start = np.array(S, np.int64).reshape(n, ndim)[:, pl]
+        count = np.array(C, np.int64).reshape(n, ndim)[:, pl]
+        step = np.array(P, np.int64).reshape(n, ndim)[:, pl]
+        chunks["src"] = [it[0] for it in items]
+        chunks["src_len"] = [it[1] for it in items]
+        chunks["flags"] = [N.CF_MISSING if it[2] else 0 for it in items]
+        oo = np.array(oo, np.int64)
+        if item_out_extra is not None:
+            oo += np.asarray(item_out_extra, np.int64)
+        chunks["out_off"] = oo
         if ndim == 1:
             split = _split_1d(shape_st[0], itemsize, ost_st[0], start, count, step)
             if split:  # the same chunk bytes viewed as (N/R, R): whole rows of R items

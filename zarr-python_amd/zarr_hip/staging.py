@@ -27,7 +27,7 @@ import os
 import numpy as np
 
 from .interop import byte_payload, is_missing_key_error, request_classes, staged_bytes
-from .store import ALIGN, TAIL_SLACK, DeviceRef
+from .store import ALIGN, TAIL_SLACK, DeviceRef, pinned_spans
 
 # 4 MiB windows: smaller ones pay ~10 us per hipMemcpyAsync, larger ones start
 # the DMA late (scripts/stage_micro.py)
@@ -52,6 +52,13 @@ def _copy_stream(device):
         s = torch.cuda.Stream(device=device)
         _COPY_STREAMS[key] = s
     return s
+
+
+def quiesce() -> None:
+    """Wait for every staging copy already enqueued (before host bytes they
+    read are reused)."""
+    for s in list(_COPY_STREAMS.values()):
+        s.synchronize()
 
 
 class StagingLayout:
@@ -121,12 +128,22 @@ def stage(layout: StagingLayout, device, post=(), defer: bool = False):
     from . import _native as N
 
     total = max(layout.top, 16)
-    host = torch.empty(total + TAIL_SLACK, dtype=torch.uint8, pin_memory=True)
-    dev = torch.empty(total + TAIL_SLACK, dtype=torch.uint8, device=device)
     views = [_host_view(buf) for buf, _, _ in layout.pieces]
     pieces = np.zeros(len(views), N.PIECE_DT)
-    for i, (v, (_, off, n)) in enumerate(zip(views, layout.pieces)):
-        pieces[i] = (v.ctypes.data if n else 0, n, off)
+    addrs = [v.ctypes.data for v in views]
+    pieces["host"] = addrs
+    pieces["nbytes"] = [n for _, _, n in layout.pieces]
+    pieces["dst_off"] = [off for _, off, _ in layout.pieces]
+    spans = pinned_spans()
+    all_pinned = False
+    if spans:
+        flags = [N.PIECE_PINNED if any(lo <= a and a + n <= hi for lo, hi in spans) else 0
+                 for a, (_, _, n) in zip(addrs, layout.pieces)]
+        pieces["flags"] = flags
+        all_pinned = all(flags)
+    # the packing buffer (pinned, reused through torch's caching host allocator)
+    host = torch.empty(16 if all_pinned else total + TAIL_SLACK, dtype=torch.uint8, pin_memory=True)
+    dev = torch.empty(total + TAIL_SLACK, dtype=torch.uint8, device=device)
     compute = torch.cuda.current_stream(device)
     cs = _copy_stream(device)
     cs.wait_stream(compute)

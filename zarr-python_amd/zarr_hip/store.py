@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import os
 import threading
+import weakref
 from dataclasses import dataclass
 from typing import Any
 
@@ -226,15 +227,23 @@ class DeviceArena:
     is launched, so a concurrent grow (which swaps ``buf``) can never leave that
     launch writing into an abandoned buffer."""
 
-    def __init__(self, device, capacity: int = 1 << 24):
+    def __init__(self, device, capacity: int = 1 << 24, pinned: bool = False):
         import torch
 
         self.device = torch.device(device)
-        self.buf = torch.empty(_aligned(capacity) + TAIL_SLACK, dtype=torch.uint8, device=self.device)
+        self.pinned = pinned and self.device.type == "cpu"
+        self.buf = self._alloc(_aligned(capacity) + TAIL_SLACK)
         self.top = 0
         self.version = 0
         self.lock = threading.RLock()
         self._free: list[list[int]] = []  # [offset, nbytes], sorted, coalesced, ALIGN granules
+
+    def _alloc(self, n: int):
+        import torch
+
+        if self.pinned:
+            return torch.empty(n, dtype=torch.uint8, pin_memory=True)
+        return torch.empty(n, dtype=torch.uint8, device=self.device)
 
     @property
     def capacity(self) -> int:
@@ -252,7 +261,7 @@ class DeviceArena:
         import torch
 
         cap = _aligned(max(need, 2 * self.capacity))
-        nb = torch.empty(cap + TAIL_SLACK, dtype=torch.uint8, device=self.device)
+        nb = self._alloc(cap + TAIL_SLACK)
         nb[: self.top].copy_(self.buf[: self.top])
         self.buf = nb
         self.version += 1
@@ -314,6 +323,13 @@ class DeviceArena:
                 off = self.reserve(t.numel())
                 self.buf[off: off + t.numel()].copy_(t, non_blocking=True)
             return off, t.numel()
+        if self.device.type == "cpu":
+            arr = np.frombuffer(data, dtype=np.uint8) if isinstance(data, (bytes, bytearray, memoryview)) \
+                else np.ascontiguousarray(data).reshape(-1).view(np.uint8)
+            with self.lock:
+                off = self.reserve(arr.size)
+                self.buf[off: off + arr.size].numpy()[:] = arr
+            return off, int(arr.size)
         arr = np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray) \
             else np.ascontiguousarray(data).reshape(-1).view(np.uint8)
         with self.lock:
@@ -461,6 +477,69 @@ class DeviceStore:
         st.arena.top = top
         st._index = placements
         return st
+
+
+_PINNED_ARENAS: "weakref.WeakSet[DeviceArena]" = weakref.WeakSet()
+
+
+def pinned_spans() -> list[tuple[int, int]]:
+    """Host address spans of the live pinned store arenas.  Staged pieces
+    inside one are DMA'd to HBM directly (ZHIP_PIECE_PINNED), never packed."""
+    return [(a.buf.data_ptr(), a.buf.data_ptr() + a.buf.numel()) for a in list(_PINNED_ARENAS)]
+
+
+class PinnedMemoryStore(MemoryStore):
+    """A MemoryStore whose values live in page-locked host memory: one pinned
+    arena (DeviceArena on "cpu", same first-fit free list), so a read stages
+    its chunk bytes to HBM by DMA straight from the store -- no packing copy --
+    and consecutive values go as one copy (csrc/staging.cpp).  Same store
+    interface as MemoryStore (src/zarr/storage/_memory.py:32-170); get_sync
+    returns uint8 numpy views of the arena.  A value's bytes change only when
+    its key is overwritten or deleted, which first waits for the staging copy
+    streams so no DMA in flight reads reused space."""
+
+    def __init__(self, data: dict | None = None, capacity: int = 1 << 24):
+        self.arena = DeviceArena("cpu", capacity, pinned=True)
+        _PINNED_ARENAS.add(self.arena)
+        self._d: dict[str, tuple[int, int]] = {}
+        self._np, self._np_of = None, None
+        for k, v in (data or {}).items():
+            self.set_sync(k, v)
+
+    def get_sync(self, key: str, byte_range=None, prototype=None):
+        p = self._d.get(key)
+        if p is None:
+            return None
+        off, n = p
+        a, b = (0, n) if byte_range is None else _resolve_range(byte_range, n)
+        buf = self.arena.buf
+        if self._np_of is not buf:  # numpy alias of the (possibly regrown) arena
+            self._np, self._np_of = buf.numpy(), buf
+        return self._np[off + a: off + b]
+
+    def _release(self, key: str) -> None:
+        p = self._d.pop(key, None)
+        if p is not None:
+            from .staging import quiesce
+
+            quiesce()
+            self.arena.free(*p)
+
+    def set_sync(self, key: str, value) -> None:
+        from .interop import byte_payload
+
+        data = value if isinstance(value, (bytes, bytearray, memoryview, np.ndarray)) else \
+            byte_payload(value, host=True)
+        with self.arena.lock:
+            self._release(key)
+            self._d[key] = self.arena.put(data)
+
+    def delete_sync(self, key: str) -> None:
+        with self.arena.lock:
+            self._release(key)
+
+    def to_dict(self) -> dict[str, bytes]:
+        return {k: self.arena.buf[o: o + n].numpy().tobytes() for k, (o, n) in self._d.items()}
 
 
 @dataclass(frozen=True)
