@@ -296,6 +296,8 @@ def extra_configs(ctx, args):
         torch.cuda.empty_cache()
         out["encode_c3"] = encode_c3(device, args)
         torch.cuda.empty_cache()
+        out["encode_c3_chunks128"] = encode_c3_general(device, args)
+        torch.cuda.empty_cache()
     if single and "e2e" in args.extra:
         out["e2e_c2_host"] = e2e_host(device, args)
         torch.cuda.empty_cache()
@@ -405,32 +407,38 @@ class _EncodeProg:
         return None
 
 
-def _encode_bench(device, args, codecs, want_tile):
+def _encode_bench(device, args, codecs, want, chunks=(64, 64, 64)):
+    """want: "rows" (k_encode_pair), "tile4" (k_encode_tile4) or "tile"
+    (k_encode_tile, the general transposed encode)."""
     import torch
 
     import zarr_hip
+    from zarr_hip import _native as N
     from zarr_hip.planner import analyze_chain, plan_encode
     from zarr_hip.writer import EncodeLaunch
 
-    shape, chunks = (256, 256, 256), (64, 64, 64)
+    shape = (256, 256, 256)
     data = torch.from_numpy(synthetic(shape, seed=0)).to(device)
     progs, checks = [], []
+    elen = int(np.prod(chunks)) * 4 + 4
+    n_chunks = int(np.prod([s // c for s, c in zip(shape, chunks)]))
     for _ in range(2):
-        store = zarr_hip.DeviceStore(device, capacity=64 * (1 << 20) + (1 << 20))
+        store = zarr_hip.DeviceStore(device, capacity=n_chunks * (elen + 256) + (1 << 20))
         arr = zarr_hip.Array.create(store, shape, chunks, "float32", 0.0, codecs=codecs)
         batch, _ = arr.batch_info((Ellipsis,))
         spec = batch[0][1]
         chain = analyze_chain(arr.codec_pipeline.codecs, spec)
-        elen = 64 ** 3 * 4 + 4
         offs = [store.arena.reserve(elen) for _ in batch]
         items = [(offs[i], it[2], [sl.start or 0 for sl in it[3]]) for i, it in enumerate(batch)]
         t = plan_encode(chain, spec, items, [int(x) * 4 for x in data.stride()], data.data_ptr())
-        if want_tile:
-            assert t.tile, "C3 encode should take the tiled encode"
-        else:
-            assert t.rows, "C2 encode should take the row-mapped encode"
         el = EncodeLaunch(t.layout, t.chunks, t.sels, data, store.arena.buf, t.fast, device, t.rows,
-                          t.tile)
+                          t.tile, t.tile_prefix)
+        if want == "rows":
+            assert t.rows, "C2 encode should take the row-mapped encode"
+        else:
+            assert t.tile and el.flags & N.DF_TILE, "C3 encode should take a tiled encode"
+            t4 = bool(el.plan.kernel_flags & N.PK_TILE4_ENCODE)
+            assert t4 == (want == "tile4"), f"expected the {want} encode"
         progs.append(_EncodeProg(el))
         checks.append((store, arr, batch, offs, elen))
     wall, kern = time_programs(progs, max(10, args.steps // 2), 3, device)
@@ -448,10 +456,25 @@ def encode_c3(device, args):
     bytes + crc32c into 64 chunks of 64^3 by k_encode_tile4 (four LDS tiles
     per workgroup), timed like the decode and decoded back for the check."""
     codecs = [{"name": "transpose", "configuration": {"order": [2, 1, 0]}}, LE, CRC]
-    src, wall, kern = _encode_bench(device, args, codecs, True)
+    src, wall, kern = _encode_bench(device, args, codecs, "tile4")
     return _entry(src, src + 64 * (1048576 + 4), wall, kern,
                   kernel="k_encode" if args.tune & 65536 else "k_encode_tile4", checked="bytes",
                   note="decoded_GiBps = source bytes encoded per second")
+
+
+def encode_c3_general(device, args):
+    """A transposed encode k_encode_tile4 does not take: the C3 array through
+    transpose(2,1,0) into 8 chunks of 128^3 (512 tiles of 64 x 256 B per
+    chunk, more than the four-tile kernel's 64, and groups of four
+    consecutive tiles at two different steps): k_encode_tileg, tiles grouped
+    by four along the stored dim 1 (round 1 sent these to the per-element
+    k_encode at 0.05; --tune 65536 runs the one-group-per-workgroup general
+    k_encode_tile instead)."""
+    codecs = [{"name": "transpose", "configuration": {"order": [2, 1, 0]}}, LE, CRC]
+    src, wall, kern = _encode_bench(device, args, codecs, "tile", chunks=(128, 128, 128))
+    return _entry(src, src + 8 * (128 ** 3 * 4 + 4), wall, kern,
+                  kernel="k_encode_tile" if args.tune & 65536 else "k_encode_tileg", checked="bytes",
+                  note="decoded_GiBps = source bytes encoded per second; 128^3 chunks")
 
 
 def encode_c2(device, args):
@@ -461,7 +484,7 @@ def encode_c2(device, args):
     HipCodecPipeline.write_sync issues for complete chunks.  Timed like the
     decode (graph replay of K launches); the stored bytes are then decoded back
     and compared with the source."""
-    src, wall, kern = _encode_bench(device, args, [LE, CRC], False)
+    src, wall, kern = _encode_bench(device, args, [LE, CRC], "rows")
     return _entry(src, src + 64 * (1048576 + 4), wall, kern,
                   kernel="k_encode" if args.tune & 64 else "k_encode_pair", checked="bytes",
                   note="decoded_GiBps = source bytes encoded per second")

@@ -150,6 +150,10 @@ int zhip_plan_info(const zhip_plan *plan, uint32_t *units_per_chunk, uint32_t *w
 #define ZHIP_PK_TILE4 1u  /* transposed layout with full 64 x 256-byte tiles: k_decode_tile4 */
 #define ZHIP_PK_TILE4_ENCODE 2u  /* ... and at most 64 tiles per chunk: zhip_encode_mapped with
                                     ZHIP_DF_TILE runs k_encode_tile4 (writes every non-empty flag) */
+#define ZHIP_PK_TILE 4u  /* transposed layout tiled through LDS (a stored dim other than the
+                            innermost is contiguous in out, rows of 16-byte multiples):
+                            ZHIP_DF_TILE / ZHIP_DF_TILE_PREFIX encodes take k_encode_tile
+                            when k_encode_tile4 does not apply */
 int zhip_plan_kernel_flags(const zhip_plan *plan, uint32_t *flags);
 
 /* decode flags (zhip_decode decode_flags) */
@@ -159,6 +163,9 @@ int zhip_plan_kernel_flags(const zhip_plan *plan, uint32_t *flags);
 #define ZHIP_DF_TILE 2u       /* transposed layout: every chunk fully selected, the
                                  out-contiguous stored dim is tiled through LDS;
                                  out offsets/strides 16-byte aligned */
+#define ZHIP_DF_TILE_PREFIX 8u /* encode, transposed layout (ZHIP_PK_TILE): every
+                                  selection is a prefix box (start 0, unit steps,
+                                  counts <= shape); elements past it are fill */
 #define ZHIP_DF_ROWS 4u       /* with ZHIP_DF_FAST_ROWS: every selection has unit
                                  steps, innermost rows are 2^k <= 4096 bytes and
                                  shape[ndim-2] is a multiple of 4096/row_bytes

@@ -225,3 +225,81 @@ def test_encode_tile4_sharded_inner(device):
     _run(device, (128, 128, 64), (128, 128, 64), "float32",
          [SHARD((64, 64, 64), [T((2, 1, 0)), LE, CRC])], 0.0,
          [((Ellipsis,), _data((128, 128, 64), "float32")), ((slice(0, 64), slice(64, 128)), 0.0)])
+
+
+# ---- k_encode_tile: the general transposed encode (partial tiles, > 64
+# tiles per chunk, other base steps, prefix-box edge chunks)
+
+def _record_encode_flags(monkeypatch):
+    from zarr_hip import writer
+
+    seen = []
+    orig = writer.EncodeLaunch.launch
+
+    def launch(self, stream=None):
+        seen.append((self.flags, self.plan.kernel_flags))
+        return orig(self, stream)
+    monkeypatch.setattr(writer.EncodeLaunch, "launch", launch)
+    return seen
+
+
+def _took_general_tile(seen) -> bool:
+    from zarr_hip import _native as N
+
+    return any((f & (N.DF_TILE | N.DF_TILE_PREFIX)) and (kf & N.PK_TILE) and
+               not ((f & N.DF_TILE) and (kf & N.PK_TILE4_ENCODE)) for f, kf in seen)
+
+
+@pytest.mark.parametrize("order", [(2, 1, 0), (1, 2, 0), (0, 2, 1), (2, 0, 1)])
+@pytest.mark.parametrize("dtype,endian", [("float32", LE), ("int16", BE), ("float64", LE), ("uint8", LE)])
+def test_encode_tile_general(device, monkeypatch, order, dtype, endian):
+    """Partial tiles and edge chunks (prefix selections): (100, 72, 48) over
+    (64, 48, 32) chunks; stored rows stay 16-byte multiples for every order."""
+    seen = _record_encode_flags(monkeypatch)
+    shape, chunks = (100, 72, 48), (64, 48, 32)
+    d = _data(shape, dtype)
+    d[0:64, 0:48, 0:32] = 0  # one whole chunk of fill: elided
+    _run(device, shape, chunks, dtype, [T(order), endian, CRC], 0, [((Ellipsis,), d)])
+    assert _took_general_tile(seen)
+
+
+def test_encode_tile_many_tiles_per_chunk(device, monkeypatch):
+    """128 x 128 x 64 float32 chunks, order (2, 1, 0): 256 tiles per chunk."""
+    seen = _record_encode_flags(monkeypatch)
+    shape = (256, 128, 64)
+    d = _data(shape, "float32")
+    _run(device, shape, (128, 128, 64), "float32", [T((2, 1, 0)), LE, CRC], np.nan,
+         [((Ellipsis,), d), ((slice(5, 200), slice(7, 100), slice(0, 33)), 1.5)])
+    assert _took_general_tile(seen)
+
+
+def test_encode_tile_no_crc_nan_fill_and_sharded(device, monkeypatch):
+    seen = _record_encode_flags(monkeypatch)
+    shape = (96, 80, 48)
+    d = _data(shape, "float32")
+    d[0:32, 0:40, 0:48] = np.nan
+    _run(device, shape, (32, 40, 48), "float32", [T((2, 0, 1)), LE], np.nan, [((Ellipsis,), d)])
+    _run(device, (96, 80, 48), (96, 80, 48), "float32", [SHARD((48, 40, 24), [T((1, 2, 0)), LE, CRC])], 0.0,
+         [((Ellipsis,), d), ((slice(0, 48), slice(40, 80)), 0.0)])
+    assert _took_general_tile(seen)
+
+
+def _took(seen, kind) -> bool:
+    """kind "g": k_encode_tileg engaged (full selections, a group dim)."""
+    from zarr_hip import _native as N
+
+    return any((f & N.DF_TILE) and (kf & N.PK_TILE) and not (kf & N.PK_TILE4_ENCODE) for f, kf in seen)
+
+
+@pytest.mark.parametrize("order", [(2, 1, 0), (1, 2, 0), (0, 2, 1), (2, 0, 1)])
+@pytest.mark.parametrize("dtype,endian", [("float32", LE), ("int16", BE), ("float64", LE), ("uint8", LE)])
+def test_encode_tileg_full_chunks(device, monkeypatch, order, dtype, endian):
+    """Full chunks, partial tiles (80 rows) and > 64 tiles per chunk: (96, 160,
+    160) over (96, 80, 80) chunks -- every order has a stored dim with shape
+    % 4 == 0 other than tq and the innermost, so the grouped kernel runs."""
+    seen = _record_encode_flags(monkeypatch)
+    shape, chunks = (96, 160, 160), (96, 80, 80)
+    d = _data(shape, dtype)
+    d[0:96, 0:80, 0:80] = 0  # one whole chunk of fill: elided
+    _run(device, shape, chunks, dtype, [T(order), endian, CRC], 0, [((Ellipsis,), d)])
+    assert _took(seen, "g")

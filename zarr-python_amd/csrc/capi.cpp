@@ -243,6 +243,8 @@ int zhip_plan_create(const zhip_layout* layout, zhip_plan** out) {
     p->d_tables = nullptr;
     p->d_tile_tables = nullptr;
     p->tile4 = 0;
+    p->gd = -1;
+    p->n_groups = 0;
     // tile mode: a stored dim (not the innermost) that is contiguous in out
     p->tq = -1;
     {
@@ -274,6 +276,10 @@ int zhip_plan_create(const zhip_layout* layout, zhip_plan** out) {
                 if (base[ti] != base[ti & ~3u] + (uint64_t)(ti & 3u) * step) t4 = false;
             p->tile4 = t4 ? 1u : 0u;
             p->tile4_step = step;
+            // k_encode_tileg: the innermost other stored dim with shape % 4 == 0
+            for (int d = L.ndim - 2; d >= 0 && p->gd < 0; --d)
+                if (d != p->tq && L.shape[d] % 4 == 0) p->gd = d;
+            if (p->gd >= 0) p->n_groups = T / 4;
         }
     }
     *out = p;
@@ -327,7 +333,8 @@ int zhip_plan_upload(zhip_plan* p) {
         const uint64_t step = p->tile4_step;
         const size_t n_base = 4096 + kThreads + T;
         const size_t n_t4 = t4 ? 1024 + (size_t)(T / 4) * kThreads + (size_t)T * 4 : 0;
-        std::vector<uint32_t> ht(n_base + n_t4);
+        const size_t n_g = p->gd >= 0 ? 1024 + (size_t)p->n_groups * (sizeof(GroupEnt) / 4) : 0;
+        std::vector<uint32_t> ht(n_base + n_t4 + n_g);
         build_horner_stride(ht.data(), 16ull * sq);
         for (int t = 0; t < kThreads; ++t) {
             const uint64_t rel = (uint64_t)(kTileRows + t / 16) * sq + 16u * (t % 16);
@@ -367,6 +374,43 @@ int zhip_plan_upload(zhip_plan* p) {
                 std::memcpy(e + 2, &o, sizeof(o));
             }
         }
+        if (p->gd >= 0) {
+            // groups: tiles whose gd coordinate is 4m .. 4m+3, others equal
+            p->g_off_tz = n_base + n_t4;
+            p->g_off_map = p->g_off_tz + 1024;
+            const uint32_t z = xpow8(p->sstride[p->gd]);
+            for (int sl = 0; sl < 4; ++sl)
+                for (uint32_t b = 0; b < 256; ++b) ht[p->g_off_tz + sl * 256 + b] = gf_mul(z, b << (8 * sl));
+            // tile-index stride of the gd coordinate (natural order: cb, qb, then
+            // the other dims from ndim-2 down)
+            uint64_t tstride = (uint64_t)p->n_cb * p->n_qb;
+            for (int d = L.ndim - 2; d > p->gd; --d)
+                if (d != p->tq) tstride *= (uint64_t)L.shape[d];
+            GroupEnt* gm = reinterpret_cast<GroupEnt*>(&ht[p->g_off_map]);
+            uint32_t g = 0;
+            for (uint32_t ti = 0; ti < T; ++ti) {
+                if ((ti / tstride) % (uint64_t)L.shape[p->gd] % 4u != 0u) continue;
+                uint32_t r = ti;
+                const uint32_t cb = r % p->n_cb;
+                r /= p->n_cb;
+                const uint32_t qb = r % p->n_qb;
+                r /= p->n_qb;
+                int64_t o = (int64_t)qb * kTileRows * L.out_stride[p->tq] +
+                            (int64_t)cb * (kTileCols / L.itemsize) * L.out_stride[L.ndim - 1];
+                for (int d = L.ndim - 2; d >= 0; --d) {
+                    if (d == p->tq) continue;
+                    o += (int64_t)(r % (uint32_t)L.shape[d]) * L.out_stride[d];
+                    r /= (uint32_t)L.shape[d];
+                }
+                GroupEnt e{};
+                e.tbase = (uint32_t)base[ti];
+                e.rows = (uint16_t)std::min<int64_t>(kTileRows, (int64_t)L.shape[p->tq] - (int64_t)qb * kTileRows);
+                e.cols = (uint16_t)std::min<int64_t>(kTileCols, (int64_t)p->row_bytes - (int64_t)cb * kTileCols);
+                e.orel = o;
+                e.ku = gf_mul(ht[4096 + kThreads + ti + 3 * tstride], p->t_c_inv);
+                gm[g++] = e;
+            }
+        }
         if (p->d_tile_tables) (void)hipFree(p->d_tile_tables);
         p->d_tile_tables = nullptr;
         HIP_TRY(hipMalloc(&p->d_tile_tables, ht.size() * sizeof(uint32_t)));
@@ -389,7 +433,8 @@ int zhip_plan_destroy(zhip_plan* p) {
 
 int zhip_plan_kernel_flags(const zhip_plan* p, uint32_t* flags) {
     if (!p || !flags) return set_err(ZHIP_E_INVALID, "null argument");
-    *flags = (p->tile4 ? ZHIP_PK_TILE4 : 0u) | (p->tile4 && p->t_per_chunk <= 64 ? ZHIP_PK_TILE4_ENCODE : 0u);
+    *flags = (p->tile4 ? ZHIP_PK_TILE4 : 0u) | (p->tile4 && p->t_per_chunk <= 64 ? ZHIP_PK_TILE4_ENCODE : 0u) |
+             (p->tq >= 0 ? ZHIP_PK_TILE : 0u);
     return ZHIP_OK;
 }
 
@@ -677,6 +722,38 @@ int zhip_encode_mapped(const zhip_plan* plan, const void* arr, void* dst, const 
         p.tz = plan->d_tile_tables + plan->tile4_off_tz;
         p.kq4 = plan->d_tile_tables + plan->tile4_off_kq;
         p.tmap = reinterpret_cast<const TileEnt*>(plan->d_tile_tables + plan->tile4_off_map);
+        d_rowmap = nullptr;
+    } else if ((encode_flags & ZHIP_DF_TILE) && plan->gd >= 0 && plan->d_tile_tables && !(g_tune_bits & kTuneTile1) &&
+               L.shape[plan->tq] % (16 / L.itemsize) == 0) {
+        // (whole 16-byte pieces along tq: a piece never reaches past the chunk)
+        // full selections, tiles grouped by four at a uniform step: k_encode_tileg
+        p.tile = 2;
+        p.tq = plan->tq;
+        p.t_per_chunk = plan->t_per_chunk;
+        for (int d = 0; d < ZHIP_MAX_DIMS; ++d) p.sstride[d] = plan->sstride[d];
+        p.horner = plan->d_tile_tables;
+        p.kthread = plan->d_tile_tables + 4096;
+        p.gtz = plan->d_tile_tables + plan->g_off_tz;
+        p.gmap = reinterpret_cast<const GroupEnt*>(plan->d_tile_tables + plan->g_off_map);
+        p.n_groups = plan->n_groups;
+        p.g_step_t = plan->sstride[plan->gd];
+        p.g_step_o = L.out_stride[plan->gd];
+        d_rowmap = nullptr;
+    } else if ((encode_flags & (ZHIP_DF_TILE | ZHIP_DF_TILE_PREFIX)) && plan->tq >= 0 && plan->d_tile_tables) {
+        // every other transposed batch (partial tiles, many tiles per chunk,
+        // edge chunks with prefix selections): k_encode_tile
+        p.tile = 1;
+        p.tq = plan->tq;
+        p.t_per_chunk = plan->t_per_chunk;
+        p.n_qb = plan->n_qb;
+        p.n_cb = plan->n_cb;
+        p.d_qb = make_fdiv(plan->n_qb);
+        p.d_cb = make_fdiv(plan->n_cb);
+        for (int d = 0; d < ZHIP_MAX_DIMS; ++d) p.sstride[d] = plan->sstride[d];
+        p.horner = plan->d_tile_tables;
+        p.kthread = plan->d_tile_tables + 4096;
+        p.kunit = plan->d_tile_tables + 4096 + kThreads;
+        p.c_inv = plan->t_c_inv;
         d_rowmap = nullptr;
     }
     if (d_rowmap) {

@@ -389,8 +389,421 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     p.status[c] = st;
 }
 
+// k_encode_tile: the general transposed encode (TransposeCodec._encode_sync,
+// transpose.py:113-118) for layouts k_encode_tile4 does not take -- partial
+// tiles (shape[tq] % 64, row_bytes % 256), any number of tiles per chunk, any
+// base steps -- and for edge chunks whose selection is a prefix box (start 0,
+// unit steps: the array covers [0, count) of every stored dim, the rest of the
+// chunk is fill, as _merge_chunk_array writes it).  Up to four consecutive
+// 64-row x 256-byte tiles of one chunk per workgroup, every gather issued
+// first: the array's out-contiguous 16-byte pieces (kPer rows of the tq dim at
+// one column element) go into the LDS image at their stored place and come
+// back as stored 16-byte blocks (fill test, byteswap, store, Horner steps with
+// k_decode_tile's stride tables).  A thread's per-tile states are shifted by
+// the tile constants and summed (CRC linearity), so one reduction and one
+// XOR + arrival pair per workgroup remain; the last arrival writes the
+// trailer and the status.
+namespace {
+struct TileGeo {
+    uint32_t tbase;
+    int64_t aoff;
+    int32_t rows_here, cols_here, rows_sel, cols_sel;  // cols_sel in elements
+};
+}  // namespace
+
+template <int ITEM>
+__device__ __forceinline__ TileGeo encode_tile_geo(const EncodeParams& p, uint32_t ti, const int32_t (&cnt)[ZHIP_MAX_DIMS],
+                                                   int32_t cnt_q, int32_t cnt_l) {
+    const int32_t last = p.g.ndim - 1;
+    const uint32_t sq = p.sstride[p.tq];
+    uint32_t r = ti;
+    const uint32_t rq = fdiv_apply(r, p.d_cb.m, p.d_cb.s);
+    const uint32_t cb = r - rq * p.n_cb;
+    r = rq;
+    const uint32_t rr = fdiv_apply(r, p.d_qb.m, p.d_qb.s);
+    const uint32_t qb = r - rr * p.n_qb;
+    r = rr;
+    TileGeo g;
+    g.tbase = qb * (uint32_t)kTileRows * sq + cb * (uint32_t)kTileCols;
+    g.aoff = (int64_t)qb * kTileRows * p.g.ostride[p.tq] + (int64_t)(cb * (kTileCols / ITEM)) * p.g.ostride[last];
+    bool inside = true;
+#pragma unroll
+    for (int d = ZHIP_MAX_DIMS - 1; d >= 0; --d) {
+        if (d >= last || d == p.tq) continue;
+        const uint32_t qd = fdiv_apply(r, p.g.dshape[d].m, p.g.dshape[d].s);
+        const uint32_t sd = r - qd * (uint32_t)p.g.shape[d];
+        r = qd;
+        g.tbase += sd * p.sstride[d];
+        g.aoff += (int64_t)sd * p.g.ostride[d];
+        inside = inside && (int32_t)sd < cnt[d];
+    }
+    g.rows_here = min(kTileRows, p.g.shape[p.tq] - (int32_t)qb * kTileRows);
+    g.cols_here = min(kTileCols, (int32_t)p.g.row_bytes - (int32_t)cb * kTileCols);
+    g.rows_sel = inside ? max(0, min(g.rows_here, cnt_q - (int32_t)qb * kTileRows)) : 0;
+    g.cols_sel = max(0, min(g.cols_here / ITEM, cnt_l - (int32_t)cb * (kTileCols / ITEM)));
+    return g;
+}
+
+template <bool CRC, int ITEM, bool SWAP>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_encode_tile(
+    const EncodeParams p) {
+    constexpr int kPitch = ITEM == 8 ? 264 : 260;
+    constexpr int kPer = 16 / ITEM;
+    constexpr int kPiecesPerCol = kTileRows / kPer;
+    constexpr int G = kTiles;  // tiles per workgroup
+    __shared__ uint32_t s_tab[CRC ? 16 * 256 : 1];
+    __shared__ __attribute__((aligned(16))) uint8_t s_tile[kTileRows * kPitch];
+    __shared__ uint32_t s_red[kThreads / 64];
+    __shared__ uint32_t s_ne[kThreads / 64];
+    struct Counts {
+        int32_t v[ZHIP_MAX_DIMS];
+    };
+    const int t = threadIdx.x;
+    const uint32_t T = p.t_per_chunk;
+    const uint32_t gpc = (T + G - 1) / G;  // workgroups per chunk
+    const uint32_t c = blockIdx.x / gpc;
+    const uint32_t grp = blockIdx.x - c * gpc;
+    const uint32_t ti0 = grp * G;
+    const uint32_t nt = min((uint32_t)G, T - ti0);  // tiles of this workgroup
+    uint4 tv0, tv1, tv2, tv3;
+    uint32_t kth = 0;
+    if constexpr (CRC) {
+        const uint4* gt = reinterpret_cast<const uint4*>(p.horner);
+        tv0 = gt[t];
+        tv1 = gt[t + kThreads];
+        tv2 = gt[t + 2 * kThreads];
+        tv3 = gt[t + 3 * kThreads];
+        kth = p.kthread[t];
+    }
+    const zhip_chunk ch = load_uniform<zhip_chunk>(p.chunks + c);  // src: dst offset, out_off: array offset
+    const Counts cs = load_uniform<Counts>(&p.sels[ch.sel].count[0]);
+    const int32_t last = p.g.ndim - 1;
+    int32_t cnt_q = 0, cnt_l = 0;  // (select by compile-time index: no dynamic indexing of registers)
+#pragma unroll
+    for (int d = 0; d < ZHIP_MAX_DIMS; ++d) {
+        cnt_q = d == p.tq ? cs.v[d] : cnt_q;
+        cnt_l = d == last ? cs.v[d] : cnt_l;
+    }
+    TileGeo geo[G];
+#pragma unroll
+    for (int j = 0; j < G; ++j) geo[j] = encode_tile_geo<ITEM>(p, ti0 + min((uint32_t)j, nt - 1u), cs.v, cnt_q, cnt_l);
+    const uint32_t sq = p.sstride[p.tq];
+    const int64_t oq = p.g.ostride[p.tq];    // == ITEM
+    const int64_t ocol = p.g.ostride[last];  // array stride of the innermost stored dim
+    const uint8_t* const abase = p.arr + ch.out_off;
+    uint8_t* const cp = p.dst + ch.src;
+    const uint4 f = make_uint4(p.fill[0], p.fill[1], p.fill[2], p.fill[3]);
+    // 1. gather every whole piece of the workgroup's tiles (the rest: fill;
+    //    pieces crossing the selection's row end are completed in step 2)
+    //    Every lane issues every load (a dummy address where the piece is not
+    //    whole) and picks the fill only when the tile is consumed: a select
+    //    right after a conditional load would wait for it, serialising them.
+    uint4 pcs[G][kPasses];
+    uint32_t wmask = 0;  // bit j * kPasses + k: piece (j, k) was loaded whole
+    const uint8_t* zero = reinterpret_cast<const uint8_t*>(g_tile_zero);
+#pragma unroll
+    for (int j = 0; j < G; ++j)
+#pragma unroll
+        for (int k = 0; k < kPasses; ++k) {
+            const int32_t pc = k * kThreads + t;
+            const int32_t jc = pc / kPiecesPerCol;
+            const int32_t r0 = (pc % kPiecesPerCol) * kPer;
+            const bool whole = (uint32_t)j < nt && jc < geo[j].cols_sel && r0 + kPer <= geo[j].rows_sel;
+            wmask |= whole ? 1u << (j * kPasses + k) : 0u;
+            pcs[j][k] = load_nt16_a1(whole ? abase + geo[j].aoff + (int64_t)jc * ocol + (int64_t)r0 * oq : zero);
+        }
+    if constexpr (CRC) {
+        uint4* st = reinterpret_cast<uint4*>(s_tab);
+        st[t] = tv0;
+        st[t + kThreads] = tv1;
+        st[t + 2 * kThreads] = tv2;
+        st[t + 3 * kThreads] = tv3;
+    }
+    const uint32_t row0 = (uint32_t)t >> 4, col = 16u * (uint32_t)(t & 15);
+    uint32_t S = 0;  // sum over tiles of this thread's tile state x tile constant
+    bool eq = true;
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+        if ((uint32_t)j >= nt) break;
+        if (j > 0) __syncthreads();  // the previous tile's LDS reads are done
+        // 2. pieces into the LDS image at their stored (row, column) place;
+        //    pieces crossing the selection's row end are gathered element by
+        //    element here (only this tile's loads are waited for)
+#pragma unroll
+        for (int k = 0; k < kPasses; ++k) {
+            const uint32_t pc = (uint32_t)(k * kThreads + t);
+            const uint32_t jc = pc / kPiecesPerCol;
+            const uint32_t r0 = (pc % kPiecesPerCol) * kPer;
+            const uint4 pv = (wmask >> (j * kPasses + k)) & 1u ? pcs[j][k] : f;
+            uint32_t w[4] = {pv.x, pv.y, pv.z, pv.w};
+            const int32_t rs = geo[j].rows_sel;
+            if ((int32_t)jc < geo[j].cols_sel && (int32_t)r0 < rs && (int32_t)r0 + kPer > rs) {
+                const uint8_t* a = abase + geo[j].aoff + (int64_t)jc * ocol + (int64_t)r0 * oq;
+                for (int32_t e = 0; e < rs - (int32_t)r0; ++e) {
+                    if constexpr (ITEM == 8) {
+                        const uint2 v = *reinterpret_cast<const uint2*>(a + 8 * e);
+                        w[2 * e] = v.x;
+                        w[2 * e + 1] = v.y;
+                    } else if constexpr (ITEM == 4) {
+                        w[e] = *reinterpret_cast<const uint32_t*>(a + 4 * e);
+                    } else if constexpr (ITEM == 2) {
+                        const uint32_t sh = 16 * (e & 1);
+                        w[e / 2] = (w[e / 2] & ~(0xFFFFu << sh)) |
+                                   ((uint32_t)*reinterpret_cast<const uint16_t*>(a + 2 * e) << sh);
+                    } else {
+                        const uint32_t sh = 8 * (e & 3);
+                        w[e / 4] = (w[e / 4] & ~(0xFFu << sh)) | ((uint32_t)a[e] << sh);
+                    }
+                }
+            }
+#pragma unroll
+            for (int e = 0; e < kPer; ++e) {
+                uint8_t* dst = s_tile + (r0 + e) * kPitch + jc * ITEM;
+                if constexpr (ITEM == 8) {
+                    *reinterpret_cast<uint2*>(dst) = make_uint2(w[2 * e], w[2 * e + 1]);
+                } else if constexpr (ITEM == 4) {
+                    *reinterpret_cast<uint32_t*>(dst) = w[e];
+                } else if constexpr (ITEM == 2) {
+                    *reinterpret_cast<uint16_t*>(dst) = (uint16_t)(w[e / 2] >> (16 * (e & 1)));
+                } else {
+                    *dst = (uint8_t)(w[e / 4] >> (8 * (e & 3)));
+                }
+            }
+        }
+        __syncthreads();  // tile j (and, first time, the tables) in LDS
+        // 3. stored-order blocks inside the chunk: fill test, byteswap, store,
+        //    Horner steps (blocks past the chunk's rows / row end count as zeros)
+        uint32_t acc = 0;
+#pragma unroll
+        for (int k = 0; k < kPasses; ++k) {
+            const uint32_t row = 16u * k + row0;
+            uint4 e = make_uint4(0, 0, 0, 0);
+            if ((int32_t)row < geo[j].rows_here && (int32_t)col < geo[j].cols_here) {
+                const uint32_t* sv = reinterpret_cast<const uint32_t*>(s_tile + row * kPitch + col);
+                const uint4 v = make_uint4(sv[0], sv[1], sv[2], sv[3]);
+                eq = eq && block_eq_fill_e<ITEM>(v, p);
+                e = swap_block<ITEM, SWAP>(v);
+                store_nt16_a1(cp + geo[j].tbase + row * sq + col, e);
+            }
+            if constexpr (CRC)
+                acc = tab_apply(s_tab, acc ^ e.x) ^ tab_apply(s_tab + 1024, e.y) ^ tab_apply(s_tab + 2048, e.z) ^
+                      tab_apply(s_tab + 3072, e.w);
+        }
+        if constexpr (CRC) S ^= gf_mul(acc, __builtin_amdgcn_readfirstlane(p.kunit[ti0 + j]));
+    }
+    // 4. the workgroup's contribution and arrival
+    uint32_t v = 0;
+    if constexpr (CRC) v = wave_xor(gf_mul(S, kth));
+    const bool wne = __any(!eq);
+    if ((t & 63) == 0) {
+        s_red[t >> 6] = v;
+        s_ne[t >> 6] = wne ? 1u : 0u;
+    }
+    __syncthreads();
+    if (t != 0) return;
+    if (s_ne[0] | s_ne[1] | s_ne[2] | s_ne[3]) p.nonempty[c] = 1u;  // flags zeroed before the launch
+    if constexpr (CRC) {
+        const uint32_t V = s_red[0] ^ s_red[1] ^ s_red[2] ^ s_red[3];
+        uint32_t* accw = p.ws + 4ull * c;
+        const uint32_t prev = __hip_atomic_fetch_xor(accw, V, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::"v"(prev) : "memory");
+        const uint32_t tk = __hip_atomic_fetch_add(accw + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (tk + 1u != gpc) return;
+        const uint32_t raw = __hip_atomic_exchange(accw, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(accw + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t crc = ~(gf_mul(raw, p.c_inv) ^ p.c3);
+        uint8_t* tr = cp + p.g.nbytes;  // LE trailer (crc32c_.py:64-68)
+        tr[0] = (uint8_t)crc;
+        tr[1] = (uint8_t)(crc >> 8);
+        tr[2] = (uint8_t)(crc >> 16);
+        tr[3] = (uint8_t)(crc >> 24);
+        zhip_status st = {ZHIP_ST_OK, crc, crc, 0u};
+        p.status[c] = st;
+    } else if (grp == 0) {
+        zhip_status st = {ZHIP_ST_OK, 0u, 0u, 0u};
+        p.status[c] = st;
+    }
+}
+
+// k_encode_tileg: k_encode_tile4's recipe for every other transposed layout
+// with full selections, as long as some stored dim gd (not tq, not the
+// innermost) has shape % 4 == 0: the tiles are grouped by four along gd, so
+// inside a group the stored (and array) offsets step uniformly -- one table
+// multiply carries a thread's CRC state from tile to tile whatever the natural
+// tile order -- and partial tiles (shape[tq] % 64, row_bytes % 256) are masked
+// (the group's tiles share their row / byte extent).  Per workgroup: one
+// 24-byte group record (scalar), all 16 loads per thread issued first (a dummy
+// line outside the tile), per tile LDS image -> stored blocks -> fill test,
+// byteswap, store, Horner; one lane multiply, one reduction, one XOR + arrival
+// pair per workgroup (any number of groups per chunk).
+template <bool CRC, int ITEM, bool SWAP>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_encode_tileg(
+    const EncodeParams p) {
+    constexpr int kPitch = ITEM == 8 ? 264 : 260;
+    constexpr int kPer = 16 / ITEM;
+    constexpr int kPiecesPerCol = kTileRows / kPer;
+    __shared__ uint32_t s_tab[CRC ? 16 * 256 : 1];
+    __shared__ uint32_t s_tz[CRC ? 1024 : 1];
+    __shared__ __attribute__((aligned(16))) uint8_t s_tile[kTileRows * kPitch];
+    __shared__ uint32_t s_red[kThreads / 64];
+    __shared__ uint32_t s_ne[kThreads / 64];
+    const int t = threadIdx.x;
+    const uint32_t gpc = p.n_groups;
+    const uint32_t c = blockIdx.x / gpc;
+    const uint32_t grp = blockIdx.x - c * gpc;
+    uint4 tv0, tv1, tv2, tv3, tzv;
+    uint32_t kth = 0;
+    if constexpr (CRC) {
+        const uint4* gt = reinterpret_cast<const uint4*>(p.horner);
+        tv0 = gt[t];
+        tv1 = gt[t + kThreads];
+        tv2 = gt[t + 2 * kThreads];
+        tv3 = gt[t + 3 * kThreads];
+        tzv = reinterpret_cast<const uint4*>(p.gtz)[t];
+        kth = p.kthread[t];
+    }
+    const zhip_chunk ch = load_uniform<zhip_chunk>(p.chunks + c);  // src: dst offset, out_off: array offset
+    const GroupEnt ge = load_uniform<GroupEnt>(p.gmap + grp);
+    const int32_t last = p.g.ndim - 1;
+    const int64_t oq = p.g.ostride[p.tq];    // == ITEM
+    const int64_t ocol = p.g.ostride[last];  // array stride of the innermost stored dim
+    const uint32_t sq = p.sstride[p.tq];
+    const uint8_t* const abase = p.arr + ch.out_off + ge.orel;
+    uint8_t* const cp = p.dst + ch.src + ge.tbase;
+    const int32_t rows = ge.rows, cols = ge.cols;
+    const uint8_t* zero = reinterpret_cast<const uint8_t*>(g_tile_zero);
+    // 1. every load of the four tiles (pieces outside the tile read a dummy line)
+    uint4 pcs[kTiles][kPasses];
+#pragma unroll
+    for (int j = 0; j < kTiles; ++j)
+#pragma unroll
+        for (int k = 0; k < kPasses; ++k) {
+            const int32_t pc = k * kThreads + t;
+            const int32_t jc = pc / kPiecesPerCol;
+            const int32_t r0 = (pc % kPiecesPerCol) * kPer;
+            const bool in = jc * ITEM < cols && r0 < rows;  // rows % kPer == 0 (zhip_encode_mapped)
+            pcs[j][k] = load_nt16_a1(in ? abase + (int64_t)j * p.g_step_o + (int64_t)jc * ocol + (int64_t)r0 * oq
+                                        : zero);
+        }
+    if constexpr (CRC) {
+        uint4* st = reinterpret_cast<uint4*>(s_tab);
+        st[t] = tv0;
+        st[t + kThreads] = tv1;
+        st[t + 2 * kThreads] = tv2;
+        st[t + 3 * kThreads] = tv3;
+        reinterpret_cast<uint4*>(s_tz)[t] = tzv;
+    }
+    const uint32_t row0 = (uint32_t)t >> 4, col = 16u * (uint32_t)(t & 15);
+    uint32_t S = 0;
+    bool eq = true;
+#pragma unroll
+    for (int j = 0; j < kTiles; ++j) {
+        if (j > 0) __syncthreads();  // the previous tile's LDS reads are done
+        // 2. pieces into the LDS image at their stored (row, column) place
+#pragma unroll
+        for (int k = 0; k < kPasses; ++k) {
+            const uint32_t pc = (uint32_t)(k * kThreads + t);
+            const uint32_t jc = pc / kPiecesPerCol;
+            const uint32_t r0 = (pc % kPiecesPerCol) * kPer;
+            const uint32_t w[4] = {pcs[j][k].x, pcs[j][k].y, pcs[j][k].z, pcs[j][k].w};
+#pragma unroll
+            for (int e = 0; e < kPer; ++e) {
+                uint8_t* dst = s_tile + (r0 + e) * kPitch + jc * ITEM;
+                if constexpr (ITEM == 8) {
+                    *reinterpret_cast<uint2*>(dst) = make_uint2(w[2 * e], w[2 * e + 1]);
+                } else if constexpr (ITEM == 4) {
+                    *reinterpret_cast<uint32_t*>(dst) = w[e];
+                } else if constexpr (ITEM == 2) {
+                    *reinterpret_cast<uint16_t*>(dst) = (uint16_t)(w[e / 2] >> (16 * (e & 1)));
+                } else {
+                    *dst = (uint8_t)(w[e / 4] >> (8 * (e & 3)));
+                }
+            }
+        }
+        __syncthreads();  // tile j (and, first time, the tables) in LDS
+        // 3. stored-order blocks inside the tile: fill test, byteswap, store,
+        //    Horner steps (blocks outside the tile count as zeros)
+        uint32_t acc = 0;
+#pragma unroll
+        for (int k = 0; k < kPasses; ++k) {
+            const uint32_t row = 16u * k + row0;
+            uint4 e = make_uint4(0, 0, 0, 0);
+            if ((int32_t)row < rows && (int32_t)col < cols) {
+                const uint32_t* sv = reinterpret_cast<const uint32_t*>(s_tile + row * kPitch + col);
+                const uint4 v = make_uint4(sv[0], sv[1], sv[2], sv[3]);
+                eq = eq && block_eq_fill_e<ITEM>(v, p);
+                e = swap_block<ITEM, SWAP>(v);
+                store_nt16_a1(cp + (size_t)j * p.g_step_t + row * sq + col, e);
+            }
+            if constexpr (CRC)
+                acc = tab_apply(s_tab, acc ^ e.x) ^ tab_apply(s_tab + 1024, e.y) ^ tab_apply(s_tab + 2048, e.z) ^
+                      tab_apply(s_tab + 3072, e.w);
+        }
+        if constexpr (CRC) S = (j == 0 ? 0u : tab_apply(s_tz, S)) ^ acc;
+    }
+    // 4. run end: lane shift, reduction, the group's tile / chunk-end shift
+    uint32_t v = 0;
+    if constexpr (CRC) v = wave_xor(gf_mul(S, kth));
+    const bool wne = __any(!eq);
+    if ((t & 63) == 0) {
+        s_red[t >> 6] = v;
+        s_ne[t >> 6] = wne ? 1u : 0u;
+    }
+    __syncthreads();
+    if (t != 0) return;
+    if (s_ne[0] | s_ne[1] | s_ne[2] | s_ne[3]) p.nonempty[c] = 1u;  // flags zeroed before the launch
+    uint8_t* const chunk = p.dst + ch.src;
+    if constexpr (CRC) {
+        const uint32_t V = gf_mul(s_red[0] ^ s_red[1] ^ s_red[2] ^ s_red[3], ge.ku);
+        uint32_t* accw = p.ws + 4ull * c;
+        const uint32_t prev = __hip_atomic_fetch_xor(accw, V, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::"v"(prev) : "memory");
+        const uint32_t tk = __hip_atomic_fetch_add(accw + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (tk + 1u != gpc) return;
+        const uint32_t raw = __hip_atomic_exchange(accw, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(accw + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t crc = ~(raw ^ p.c3);  // ku carries t_c_inv
+        uint8_t* tr = chunk + p.g.nbytes;    // LE trailer (crc32c_.py:64-68)
+        tr[0] = (uint8_t)crc;
+        tr[1] = (uint8_t)(crc >> 8);
+        tr[2] = (uint8_t)(crc >> 16);
+        tr[3] = (uint8_t)(crc >> 24);
+        zhip_status st = {ZHIP_ST_OK, crc, crc, 0u};
+        p.status[c] = st;
+    } else if (grp == 0) {
+        zhip_status st = {ZHIP_ST_OK, 0u, 0u, 0u};
+        p.status[c] = st;
+    }
+}
+
 using KernelFn = void (*)(const DecodeParams);
 using EncodeFn = void (*)(const EncodeParams);
+
+EncodeFn select_encode_tileg_kernel(bool crc, int item, bool swap) {
+    switch (item) {
+        case 1: return crc ? k_encode_tileg<true, 1, false> : k_encode_tileg<false, 1, false>;
+        case 2: return crc ? (swap ? k_encode_tileg<true, 2, true> : k_encode_tileg<true, 2, false>)
+                           : (swap ? k_encode_tileg<false, 2, true> : k_encode_tileg<false, 2, false>);
+        case 4: return crc ? (swap ? k_encode_tileg<true, 4, true> : k_encode_tileg<true, 4, false>)
+                           : (swap ? k_encode_tileg<false, 4, true> : k_encode_tileg<false, 4, false>);
+        case 8: return crc ? (swap ? k_encode_tileg<true, 8, true> : k_encode_tileg<true, 8, false>)
+                           : (swap ? k_encode_tileg<false, 8, true> : k_encode_tileg<false, 8, false>);
+        default: return nullptr;
+    }
+}
+
+EncodeFn select_encode_tile_kernel(bool crc, int item, bool swap) {
+    switch (item) {
+        case 1: return crc ? k_encode_tile<true, 1, false> : k_encode_tile<false, 1, false>;
+        case 2: return crc ? (swap ? k_encode_tile<true, 2, true> : k_encode_tile<true, 2, false>)
+                           : (swap ? k_encode_tile<false, 2, true> : k_encode_tile<false, 2, false>);
+        case 4: return crc ? (swap ? k_encode_tile<true, 4, true> : k_encode_tile<true, 4, false>)
+                           : (swap ? k_encode_tile<false, 4, true> : k_encode_tile<false, 4, false>);
+        case 8: return crc ? (swap ? k_encode_tile<true, 8, true> : k_encode_tile<true, 8, false>)
+                           : (swap ? k_encode_tile<false, 8, true> : k_encode_tile<false, 8, false>);
+        default: return nullptr;
+    }
+}
 
 EncodeFn select_encode_tile4_kernel(bool crc, int item, bool swap) {
     switch (item) {

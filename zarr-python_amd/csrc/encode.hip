@@ -473,6 +473,8 @@ static EncodeFn pick_encode_pair(bool crc, int item, bool swap) {
 }
 
 EncodeFn select_encode_tile4_kernel(bool crc, int item, bool swap);  // decode_tile.hip
+EncodeFn select_encode_tile_kernel(bool crc, int item, bool swap);   // decode_tile.hip
+EncodeFn select_encode_tileg_kernel(bool crc, int item, bool swap);  // decode_tile.hip
 
 int launch_encode(const EncodeParams& p, hipStream_t stream, int max_grid) {
     const bool crc = (p.lflags & ZHIP_LF_CRC) != 0;
@@ -482,6 +484,28 @@ int launch_encode(const EncodeParams& p, hipStream_t stream, int max_grid) {
         if (!fn) return ZHIP_E_UNSUPPORTED;
         if (p.n_chunks == 0) return ZHIP_OK;
         hipLaunchKernelGGL(fn, dim3(p.n_chunks * (p.t_per_chunk / 4u)), dim3(kThreads), 0, stream, p);
+        return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
+    }
+    if (p.tile == 2) {  // full selections, tiles grouped by four at a uniform step (k_encode_tileg)
+        EncodeFn fn = select_encode_tileg_kernel(crc, p.g.itemsize, swap);
+        if (!fn) return ZHIP_E_UNSUPPORTED;
+        if (p.n_chunks == 0) return ZHIP_OK;
+        if ((uint64_t)p.n_chunks * p.n_groups >= (1ull << 31)) return ZHIP_E_UNSUPPORTED;
+        if (hipMemsetAsync(p.nonempty, 0, (size_t)p.n_chunks * sizeof(uint32_t), stream) != hipSuccess)
+            return ZHIP_E_HIP;
+        hipLaunchKernelGGL(fn, dim3(p.n_chunks * p.n_groups), dim3(kThreads), 0, stream, p);
+        return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
+    }
+    if (p.tile) {  // other transposed layouts / prefix selections (k_encode_tile)
+        EncodeFn fn = select_encode_tile_kernel(crc, p.g.itemsize, swap);
+        if (!fn) return ZHIP_E_UNSUPPORTED;
+        if (p.n_chunks == 0) return ZHIP_OK;
+        const uint64_t gpc = (p.t_per_chunk + 3u) / 4u;  // four tiles per workgroup
+        if ((uint64_t)p.n_chunks * gpc >= (1ull << 31)) return ZHIP_E_UNSUPPORTED;
+        // tiles set their chunk's non-empty flag: zero the flags first
+        if (hipMemsetAsync(p.nonempty, 0, (size_t)p.n_chunks * sizeof(uint32_t), stream) != hipSuccess)
+            return ZHIP_E_HIP;
+        hipLaunchKernelGGL(fn, dim3((uint32_t)(p.n_chunks * gpc)), dim3(kThreads), 0, stream, p);
         return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
     }
     if (p.rowmap && p.seg == (uint32_t)kWgStride * kDefaultBlocks && !(p.tune & kTunePersist)) {

@@ -31,6 +31,16 @@ struct TileEnt {
     int64_t orel;
 };
 
+// One group of k_encode_tileg: its first tile's stored offset and array
+// offset (relative to the chunk), the tiles' row / byte extent (partial tiles
+// at the chunk's edges), and kunit[its last tile] * t_c_inv.
+struct GroupEnt {
+    uint32_t tbase;
+    uint16_t rows, cols;
+    int64_t orel;
+    uint32_t ku, _pad;
+};
+
 // k_decode_pair CRC table layout (u32 words): A4096 by the 11 low, 11 middle
 // and 10 high bits of a word, then the four byte slices of A4 (x^32).
 constexpr int kPairT1 = 0, kPairT2 = 2048, kPairT3 = 4096, kPairA4 = 5120;
@@ -156,6 +166,15 @@ struct EncodeParams {
     const uint32_t* tz;
     const uint32_t* kq4;
     const struct TileEnt* tmap;
+    // k_encode_tile (ZHIP_DF_TILE / ZHIP_DF_TILE_PREFIX, not tile4): one tile
+    // per workgroup; horner / kthread / kunit / c_inv are the tile tables then
+    uint32_t tile, n_qb, n_cb;
+    zhip_fdiv d_qb, d_cb;
+    // k_encode_tileg (tile == 2): group map, step multiply table, steps
+    const struct GroupEnt* gmap;
+    const uint32_t* gtz;
+    uint32_t n_groups, g_step_t;
+    int64_t g_step_o;
 };
 
 struct PackParams {
@@ -213,6 +232,13 @@ struct zhip_plan {
     uint32_t tile4;
     uint64_t tile4_step;                                 // base step between consecutive tiles
     uint64_t tile4_off_tz, tile4_off_kq, tile4_off_map;  // u32 offsets in d_tile_tables
+    // k_encode_tileg (full selections): tiles grouped by four along the
+    // innermost other stored dim gd with shape[gd] % 4 == 0 (uniform step
+    // sstride[gd] inside every group, whatever the natural tile order); tables
+    // tzg (1024: multiply by x^(8 sstride[gd])) | gmap (n_groups GroupEnt)
+    int32_t gd;                      // -1: no such dim
+    uint32_t n_groups;
+    uint64_t g_off_tz, g_off_map;    // u32 offsets in d_tile_tables
     uint32_t* d_tile_tables;
     // shard index (sharded layouts): payload 16*n_inner, E, CRC constants
     uint32_t idx_nbytes, idx_E, idx_c_inv, idx_c3;  // horner (stride 16*sstride[tq]) | kthread (256) | kunit (t_per_chunk)

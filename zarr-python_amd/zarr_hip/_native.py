@@ -36,9 +36,11 @@ E_UNSUPPORTED = -3
 DF_FAST_ROWS = 1
 DF_TILE = 2
 DF_ROWS = 4
+DF_TILE_PREFIX = 8
 
 PK_TILE4 = 1
 PK_TILE4_ENCODE = 2
+PK_TILE = 4
 
 PF_INDEX_START = 1
 PF_INDEX_CRC = 2

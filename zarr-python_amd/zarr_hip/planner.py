@@ -129,6 +129,7 @@ class Tables:
     fast: bool
     item_of_chunk: np.ndarray     # int64[n]: batch item of each chunk entry
     tile: bool = False            # tiled-transpose decode (ZHIP_DF_TILE)
+    tile_prefix: bool = False     # tiled-transpose encode of prefix-box selections (ZHIP_DF_TILE_PREFIX)
     rows: bool = False            # affine whole-row decode (ZHIP_DF_ROWS, k_decode_rows)
     index_layout: N.Layout | None = None
     index_chunks: np.ndarray | None = None
@@ -226,6 +227,17 @@ def _rows_ok(layout: N.Layout, count, step) -> bool:
     return bool(np.all((step == 1) | (count <= 1)))
 
 
+def _tiled_layout(layout: N.Layout) -> bool:
+    """A stored dim other than the innermost is contiguous in the array / out
+    and innermost rows are 16-byte multiples (zhip_plan.tq >= 0)."""
+    nd = layout.ndim
+    it = layout.itemsize
+    last = nd - 1
+    if nd < 2 or layout.out_stride[last] == it or (layout.shape[last] * it) % 16:
+        return False
+    return any(layout.out_stride[d] == it and layout.shape[d] > 1 for d in range(last))
+
+
 def _tile_ok(layout: N.Layout, start, count, step, out_offs, out_base_ptr: int) -> bool:
     """Transposed layouts: a stored dim other than the innermost is contiguous in
     out, every chunk is fully selected and out is 16-byte aligned."""
@@ -274,7 +286,11 @@ def plan_encode(chain: ChainInfo, spec: ArraySpec, items: list, arr_strides_byte
     fast = _fast_ok(layout, start, count, step, chunks["out_off"], arr_base_ptr)
     rows = fast and _rows_ok(layout, count, step)
     tile = not fast and _tile_ok(layout, start, count, step, chunks["out_off"], arr_base_ptr)
-    return Tables(layout, chunks, sels, fast, np.arange(n), rows=rows, tile=tile)
+    # transposed chunks whose selections are prefix boxes (edge chunks): the
+    # general tiled encode (k_encode_tile) writes the rest of the chunk as fill
+    tile_prefix = not fast and not tile and _tiled_layout(layout) and bool(np.all(start == 0)) and \
+        bool(np.all(step == 1))
+    return Tables(layout, chunks, sels, fast, np.arange(n), rows=rows, tile=tile, tile_prefix=tile_prefix)
 
 
 def plan_decode(chain: ChainInfo, spec: ArraySpec, items: list, out_strides_bytes,

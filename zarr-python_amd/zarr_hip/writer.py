@@ -60,7 +60,7 @@ class EncodeLaunch:
     that ORs them, include/zarrhip.h), so a prepared launch can be replayed."""
 
     def __init__(self, layout: N.Layout, chunks: np.ndarray, sels: np.ndarray, arr, dst, fast: bool,
-                 device, rows: bool = False, tile: bool = False):
+                 device, rows: bool = False, tile: bool = False, tile_prefix: bool = False):
         from .pipeline import _rows_map, get_plan
 
         torch = _torch()
@@ -77,9 +77,14 @@ class EncodeLaunch:
         self.flags = N.DF_FAST_ROWS if fast else 0
         # whole-row batches encode in k_encode_pair through the row map
         self.d_rowmap = _rows_map(self.plan, sels, device) if fast and rows else None
-        # transposed layouts with full tiles: k_encode_tile4
-        if tile and not fast and self.plan.kernel_flags & N.PK_TILE4_ENCODE:
-            self.flags |= N.DF_TILE
+        # transposed layouts: k_encode_tile4 (full selections, full tiles, <= 64
+        # tiles per chunk: the library decides) or k_encode_tile (any tiling,
+        # prefix-box selections of edge chunks)
+        if not fast and self.plan.kernel_flags & N.PK_TILE:
+            if tile:
+                self.flags |= N.DF_TILE
+            elif tile_prefix:
+                self.flags |= N.DF_TILE_PREFIX
 
     def launch(self, stream: int | None = None) -> None:
         from .pipeline import _stream_handle
@@ -272,7 +277,7 @@ class ChunkWriter:
                     items.append((dest.offs[i], csel, [s.start or 0 for s in osel]))
                 t = plan_encode(chain, spec, items, vstr, v.data_ptr())
                 launches.append((EncodeLaunch(t.layout, t.chunks, t.sels, v, dest.buf, t.fast, self.device,
-                                              t.rows, t.tile), list(range(len(complete_items)))))
+                                              t.rows, t.tile, t.tile_prefix), list(range(len(complete_items)))))
             if partial_items:
                 tstr = [int(s) * itemsize for s in temp.stride()]
                 base = len(complete_items)
@@ -284,7 +289,7 @@ class ChunkWriter:
                 # the leading temp index goes into out_off
                 t.chunks["out_off"] = np.arange(len(partial_items)) * tstr[0]
                 launches.append((EncodeLaunch(t.layout, t.chunks, t.sels, temp, dest.buf, t.fast,
-                                              self.device, t.rows, t.tile),
+                                              self.device, t.rows, t.tile, t.tile_prefix),
                                  [base + i for i in range(len(partial_items))]))
             for l, _ in launches:
                 l.launch()
@@ -373,7 +378,7 @@ class ChunkWriter:
                 items = shard_items(src, astart_c, region_c)
                 t = plan_encode(inner, inner_spec, items, vstr, v.data_ptr())
                 launches.append(EncodeLaunch(t.layout, t.chunks, t.sels, v, dest.buf, t.fast, self.device,
-                                             t.rows, t.tile))
+                                             t.rows, t.tile, t.tile_prefix))
             if partial_items:
                 tstr = [int(s) * itemsize for s in temp.stride()]
                 base = len(complete_items)
@@ -382,7 +387,7 @@ class ChunkWriter:
                 t = plan_encode(inner, inner_spec, items, tstr[1:], temp.data_ptr())
                 t.chunks["out_off"] += np.repeat(np.arange(len(partial_items)) * tstr[0], n_inner)
                 launches.append(EncodeLaunch(t.layout, t.chunks, t.sels, temp, dest.buf, t.fast,
-                                             self.device, t.rows, t.tile))
+                                             self.device, t.rows, t.tile, t.tile_prefix))
             for l in launches:
                 l.launch()
             # pack: one workgroup per shard over all launches' inner chunks
