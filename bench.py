@@ -284,6 +284,24 @@ def extra_configs(ctx, args):
         out["c3_transpose_210"] = _entry(dec, dec + 64 * (1048576 + 4), wall, kern,
                                          kernel="k_decode_tile4" if tile4 else "k_decode_tile",
                                          checked="bytes")
+        del progs
+        # the same array in 128^3 chunks: k_decode_tile4 declines (512 tiles per
+        # chunk, two different steps between consecutive tiles) -> k_decode_tileg
+        progs = []
+        for _ in range(args.replicas):
+            arr = build_replica(device, data, shape, (128, 128, 128),
+                                [{"name": "transpose", "configuration": {"order": [2, 1, 0]}}, LE, CRC])
+            progs.append(arr.prepare_read((Ellipsis,)))
+        progs[0][0].launch()
+        progs[0][0].results()
+        if not torch.equal(progs[0][1].view(torch.int32), data.view(torch.int32)):
+            raise SystemExit("bench c3 (128^3 chunks): decoded bytes differ from the source")
+        kf = N.Plan(progs[0][0].tables.layout, upload=False).kernel_flags
+        wall, kern = time_programs([p for p, _ in progs], steps, 3, device)
+        out["c3_transpose_210_chunks128"] = _entry(
+            dec, dec + 8 * (128 ** 3 * 4 + 4), wall, kern, checked="bytes",
+            kernel="k_decode_tile" if (args.tune & 65536) or not (kf & N.PK_TILEG) else "k_decode_tileg",
+            note="8 chunks of 128^3: no k_decode_tile4 (round 1: persistent k_decode_tile)")
         del progs, data
     if "c4" in args.extra:
         out["c4_sharded_1024"] = c4_partitioned(ctx, args)

@@ -154,6 +154,10 @@ int zhip_plan_info(const zhip_plan *plan, uint32_t *units_per_chunk, uint32_t *w
                             innermost is contiguous in out, rows of 16-byte multiples):
                             ZHIP_DF_TILE / ZHIP_DF_TILE_PREFIX encodes take k_encode_tile
                             when k_encode_tile4 does not apply */
+#define ZHIP_PK_TILEG 8u /* ... and its tiles group by four along a stored dim with shape % 4 == 0
+                            (whole 16-byte pieces along the out-contiguous dim): where
+                            k_decode_tile4 / k_encode_tile4 do not apply, full-selection
+                            batches run k_decode_tileg / k_encode_tileg */
 int zhip_plan_kernel_flags(const zhip_plan *plan, uint32_t *flags);
 
 /* decode flags (zhip_decode decode_flags) */

@@ -532,3 +532,48 @@ def test_predicted_loads_engaged_and_exact(device, loc):
     sel = (slice(3, 120), slice(None), slice(None))
     got = arr[sel]
     assert got.tobytes() == np.ascontiguousarray(O.read(host, meta, sel)).tobytes()
+
+
+# k_decode_tileg: transposed layouts k_decode_tile4 declines (partial tiles,
+# > 64 tiles per chunk, irregular steps between consecutive tiles), tiles
+# grouped by four along a stored dim with shape % 4 == 0
+def _tileg_engaged(arr):
+    from zarr_hip import _native as N
+
+    prog, _ = arr.prepare_read((Ellipsis,))
+    kf = N.Plan(prog.tables.layout, upload=False).kernel_flags
+    return prog.tables.tile and (kf & N.PK_TILEG) and not (kf & N.PK_TILE4)
+
+
+@pytest.mark.parametrize("order", [(2, 1, 0), (1, 2, 0), (0, 2, 1), (2, 0, 1)])
+@pytest.mark.parametrize("dtype,endian", [("float32", LE), ("int16", BE), ("float64", LE), ("uint8", LE)])
+def test_transpose_tileg(device, order, dtype, endian):
+    arr, _, _ = _roundtrip(device, (96, 160, 160), (96, 80, 80), dtype, [T(order), endian, CRC], fill=3)
+    assert _tileg_engaged(arr)
+
+
+def test_transpose_tileg_missing_sharded_and_crc(device):
+    import zarr_hip
+
+    # missing chunks -> fill
+    arr, host, meta = _roundtrip(device, (96, 160, 160), (96, 80, 80), "float32", [T((2, 1, 0)), LE, CRC],
+                                 fill=np.nan, drop=["c/0/1/0", "c/0/0/1"])
+    assert _tileg_engaged(arr)
+    # transposed inner chunks of a shard (128^3-like geometry, 512 tiles per inner chunk)
+    _roundtrip(device, (128, 128, 128), (128, 128, 128), "float32",
+               [SHARD((128, 64, 128), [T((2, 1, 0)), LE, CRC])])
+    # CRC mismatch: the reference's message
+    meta = O.ArrayMeta((96, 80, 80), (96, 80, 80), np.dtype("float32"), 0.0, codecs=[T((2, 1, 0)), LE, CRC])
+    host = {}
+    O.write(host, meta, (Ellipsis,), _data((96, 80, 80), "float32"))
+    bad = bytearray(host["c/0/0/0"])
+    bad[12345] ^= 4
+    host["c/0/0/0"] = bytes(bad)
+    with pytest.raises(ValueError) as want:
+        O.read(host, meta)
+    arr = zarr_hip.Array.create(zarr_hip.DeviceStore.from_host(host, device), (96, 80, 80), (96, 80, 80),
+                                "float32", 0.0, codecs=[T((2, 1, 0)), LE, CRC])
+    assert _tileg_engaged(arr)
+    with pytest.raises(ValueError) as got:
+        arr[...]
+    assert str(got.value) == str(want.value)

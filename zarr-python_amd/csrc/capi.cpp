@@ -434,7 +434,8 @@ int zhip_plan_destroy(zhip_plan* p) {
 int zhip_plan_kernel_flags(const zhip_plan* p, uint32_t* flags) {
     if (!p || !flags) return set_err(ZHIP_E_INVALID, "null argument");
     *flags = (p->tile4 ? ZHIP_PK_TILE4 : 0u) | (p->tile4 && p->t_per_chunk <= 64 ? ZHIP_PK_TILE4_ENCODE : 0u) |
-             (p->tq >= 0 ? ZHIP_PK_TILE : 0u);
+             (p->tq >= 0 ? ZHIP_PK_TILE : 0u) |
+             (p->gd >= 0 && p->layout.shape[p->tq] % (16 / p->layout.itemsize) == 0 ? ZHIP_PK_TILEG : 0u);
     return ZHIP_OK;
 }
 
@@ -647,6 +648,15 @@ int zhip_decode_mapped(const zhip_plan* plan, const void* src, uint64_t src_size
             p.tz = plan->d_tile_tables + plan->tile4_off_tz;
             p.kq4 = plan->d_tile_tables + plan->tile4_off_kq;
             p.tmap = reinterpret_cast<const TileEnt*>(plan->d_tile_tables + plan->tile4_off_map);
+        } else if (plan->gd >= 0 && !(g_tune_bits & kTuneTile1) &&
+                   L.shape[plan->tq] % (16 / L.itemsize) == 0) {
+            // k_decode_tileg: tiles grouped by four along gd, whole out pieces
+            p.tileg = 1;
+            p.gtz = plan->d_tile_tables + plan->g_off_tz;
+            p.gmap = reinterpret_cast<const GroupEnt*>(plan->d_tile_tables + plan->g_off_map);
+            p.n_groups = plan->n_groups;
+            p.g_step_t = plan->sstride[plan->gd];
+            p.g_step_o = L.out_stride[plan->gd];
         }
         const uint64_t tunits = (uint64_t)n_chunks * plan->t_per_chunk;
         if (tunits >= (1ull << 32)) return set_err(ZHIP_E_UNSUPPORTED, "too many tiles in one batch");

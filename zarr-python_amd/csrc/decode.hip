@@ -491,6 +491,7 @@ static KernelFn select_tile_kernel(bool crc, int item, bool swap) {
 KernelFn select_rows_kernel(bool crc, int item, bool swap, int k);  // decode_rows.hip
 KernelFn select_pair_kernel(bool crc, int item, bool swap, int nu);  // decode_rows.hip
 KernelFn select_tile4_kernel(bool crc, int item, bool swap);         // decode_tile.hip
+KernelFn select_tileg_kernel(bool crc, int item, bool swap);         // decode_tile.hip
 
 int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
     if (g_tune_max_grid > 0) max_grid = g_tune_max_grid;
@@ -531,6 +532,15 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
         if (!fn) return ZHIP_E_UNSUPPORTED;
         if (p.n_units == 0) return ZHIP_OK;
         hipLaunchKernelGGL(fn, dim3(p.n_units / 4u), dim3(kThreads), 0, stream, p);
+        return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
+    }
+    if (p.tq >= 0 && p.tileg) {
+        // tiles grouped by four along a stored dim (k_decode_tileg, decode_tile.hip)
+        KernelFn fn = select_tileg_kernel((p.lflags & ZHIP_LF_CRC) != 0, p.g.itemsize, (p.lflags & ZHIP_LF_SWAP) != 0);
+        if (!fn) return ZHIP_E_UNSUPPORTED;
+        if (p.n_chunks == 0) return ZHIP_OK;
+        if ((uint64_t)p.n_chunks * p.n_groups >= (1ull << 31)) return ZHIP_E_UNSUPPORTED;
+        hipLaunchKernelGGL(fn, dim3(p.n_chunks * p.n_groups), dim3(kThreads), 0, stream, p);
         return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
     }
     if (p.tq >= 0) {

@@ -250,6 +250,165 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     }
 }
 
+// k_decode_tileg: k_decode_tile4 for the transposed layouts it declines
+// (partial tiles, more tiles per chunk, irregular steps between consecutive
+// tiles), as long as some stored dim gd other than tq and the innermost has
+// shape % 4 == 0: tiles are grouped by four along gd (a uniform stored and out
+// step inside every group), partial tiles masked with the group's row / byte
+// extent.  Same structure as k_decode_tile4 -- every load first, per tile LDS
+// image -> out pieces -> 16-byte stores (failed chunks to a sink, a static
+// count) -> Horner steps, the state carried by one table multiply -- and one
+// lane multiply, one reduction and one XOR + arrival pair per workgroup (any
+// number of groups per chunk).
+template <bool CRC, int ITEM, bool SWAP>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_decode_tileg(
+    const DecodeParams p) {
+    constexpr int kPitch = ITEM == 8 ? 264 : 260;
+    constexpr int kPer = 16 / ITEM;
+    constexpr int kPiecesPerCol = kTileRows / kPer;
+    __shared__ uint32_t s_tab[CRC ? 16 * 256 : 1];
+    __shared__ uint32_t s_tz[CRC ? 1024 : 1];
+    __shared__ __attribute__((aligned(16))) uint8_t s_tile[kTileRows * kPitch];
+    __shared__ uint32_t s_red[kThreads / 64];
+    const int t = threadIdx.x;
+    const uint32_t gpc = p.n_groups;
+    const uint32_t c = blockIdx.x / gpc;
+    const uint32_t grp = blockIdx.x - c * gpc;
+    const uint32_t expected = p.g.nbytes + (CRC ? 4u : 0u);
+    uint4 tv0, tv1, tv2, tv3, tzv;
+    uint32_t kth = 0;
+    if constexpr (CRC) {
+        const uint4* gt = reinterpret_cast<const uint4*>(p.horner);
+        tv0 = gt[t];
+        tv1 = gt[t + kThreads];
+        tv2 = gt[t + 2 * kThreads];
+        tv3 = gt[t + 3 * kThreads];
+        tzv = reinterpret_cast<const uint4*>(p.gtz)[t];
+        kth = p.kthread[t];
+    }
+    const Unit U = resolve_unit(p, c * p.nseg, expected);
+    const GroupEnt ge = load_uniform<GroupEnt>(p.gmap + grp);
+    const bool ok = U.mode == ZHIP_ST_OK;
+    const uint32_t sq = p.sstride[p.tq];
+    const int32_t rows = ge.rows, cols = ge.cols;
+    const uint32_t row0 = (uint32_t)t >> 4, col = 16u * (uint32_t)(t & 15);
+    const uint8_t* zero = reinterpret_cast<const uint8_t*>(g_tile_zero);
+    const bool lane_in = (int32_t)col < cols;
+    uint4 blk[kTiles][kPasses];
+#pragma unroll
+    for (int j = 0; j < kTiles; ++j)
+#pragma unroll
+        for (int k = 0; k < kPasses; ++k) {
+            const uint32_t row = row0 + 16u * k;
+            blk[j][k] = load_nt16_a1(ok && lane_in && (int32_t)row < rows
+                                         ? U.cp + ge.tbase + (size_t)j * p.g_step_t + row * sq + col
+                                         : zero);
+        }
+    uint32_t stored = 0;
+    if (CRC && ok) stored = load_trailer_uniform(U.cp, p.g.nbytes);
+    if constexpr (CRC) {
+        uint4* st = reinterpret_cast<uint4*>(s_tab);
+        st[t] = tv0;
+        st[t + kThreads] = tv1;
+        st[t + 2 * kThreads] = tv2;
+        st[t + 3 * kThreads] = tv3;
+        reinterpret_cast<uint4*>(s_tz)[t] = tzv;
+    }
+    const bool writes = ok || U.mode == ZHIP_ST_MISSING;
+    const uint4 f = make_uint4(p.fill[0], p.fill[1], p.fill[2], p.fill[3]);
+    const int32_t last = p.g.ndim - 1;
+    const int64_t oq = p.g.ostride[p.tq];    // == ITEM
+    const int64_t ocol = p.g.ostride[last];  // out stride of the innermost stored dim
+    uint8_t* const obase = p.out + U.out_off + ge.orel;
+    uint8_t* const sink = reinterpret_cast<uint8_t*>(g_tile_sink) + 16 * t;
+    uint32_t S = 0;
+#pragma unroll
+    for (int j = 0; j < kTiles; ++j) {
+        if (j > 0) __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kPasses; ++k) {
+            const uint4 v = swap_block<ITEM, SWAP>(blk[j][k]);
+            uint32_t* d = reinterpret_cast<uint32_t*>(s_tile + (16 * k + row0) * kPitch + col);
+            d[0] = v.x;
+            d[1] = v.y;
+            d[2] = v.z;
+            d[3] = v.w;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kPasses; ++k) {
+            const uint32_t pc = (uint32_t)(k * kThreads + t);
+            const uint32_t jc = pc / kPiecesPerCol;
+            const uint32_t r0 = (pc % kPiecesPerCol) * kPer;
+            uint32_t w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int e = 0; e < kPer; ++e) {
+                const uint8_t* src = s_tile + (r0 + e) * kPitch + jc * ITEM;
+                if constexpr (ITEM == 8) {
+                    const uint2 v = *reinterpret_cast<const uint2*>(src);
+                    w[2 * e] = v.x;
+                    w[2 * e + 1] = v.y;
+                } else if constexpr (ITEM == 4) {
+                    w[e] = *reinterpret_cast<const uint32_t*>(src);
+                } else if constexpr (ITEM == 2) {
+                    w[e / 2] |= (uint32_t)(*reinterpret_cast<const uint16_t*>(src)) << (16 * (e & 1));
+                } else {
+                    w[e / 4] |= (uint32_t)(*src) << (8 * (e & 3));
+                }
+            }
+            // pieces outside the tile (and failed chunks) store to the sink
+            const bool in = writes && (int32_t)(jc * ITEM) < cols && (int32_t)r0 < rows;
+            uint8_t* dst = in ? obase + (int64_t)j * p.g_step_o + (int64_t)jc * ocol + (int64_t)r0 * oq : sink;
+            store_nt16(dst, ok ? make_uint4(w[0], w[1], w[2], w[3]) : f);
+        }
+        if constexpr (CRC) {
+            if (ok) {
+                uint32_t acc = 0;
+#pragma unroll
+                for (int k = 0; k < kPasses; ++k) {
+                    const uint4 v = blk[j][k];
+                    acc = tab_apply(s_tab, acc ^ v.x) ^ tab_apply(s_tab + 1024, v.y) ^
+                          tab_apply(s_tab + 2048, v.z) ^ tab_apply(s_tab + 3072, v.w);
+                }
+                S = (j == 0 ? 0u : tab_apply(s_tz, S)) ^ acc;
+            }
+        }
+    }
+    if (CRC && ok) {
+        uint32_t v = wave_xor(gf_mul(S, kth));
+        if ((t & 63) == 0) s_red[t >> 6] = v;
+        __syncthreads();
+        if (t == 0) {
+            const uint32_t V = gf_mul(s_red[0] ^ s_red[1] ^ s_red[2] ^ s_red[3], ge.ku);
+            uint32_t* accw = p.ws + 4ull * c;
+            const uint32_t prev = __hip_atomic_fetch_xor(accw, V, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::"v"(prev) : "memory");
+            const uint32_t tk = __hip_atomic_fetch_add(accw + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (tk + 1u == gpc) {
+                const uint32_t raw = __hip_atomic_exchange(accw, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(accw + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint32_t computed = ~(raw ^ p.c3);  // ku carries t_c_inv
+                const uint32_t code = computed == stored ? ZHIP_ST_OK : ZHIP_ST_CRC_MISMATCH;
+                zhip_status st = {code, stored, computed, 0u};
+                p.status[c] = st;
+                if (code != ZHIP_ST_OK) atomicOr(p.errflag, 1u << code);
+            }
+        }
+    }
+    if (grp == 0 && t == 0) {
+        if (ok) {
+            if (!CRC) {
+                zhip_status st = {ZHIP_ST_OK, 0u, 0u, 0u};
+                p.status[c] = st;
+            }
+        } else {
+            zhip_status st = {U.mode, 0u, 0u, 0u};
+            p.status[c] = st;
+            if (U.mode != ZHIP_ST_MISSING) atomicOr(p.errflag, 1u << U.mode);
+        }
+    }
+}
+
 // k_encode_tile4: the same four tiles per workgroup in reverse (TransposeCodec
 // _encode_sync, transpose.py:113-118): 16-byte pieces of the source array's
 // out-contiguous rows are gathered (all 16 per thread issued first), written
@@ -814,6 +973,19 @@ EncodeFn select_encode_tile4_kernel(bool crc, int item, bool swap) {
                            : (swap ? k_encode_tile4<false, 4, true> : k_encode_tile4<false, 4, false>);
         case 8: return crc ? (swap ? k_encode_tile4<true, 8, true> : k_encode_tile4<true, 8, false>)
                            : (swap ? k_encode_tile4<false, 8, true> : k_encode_tile4<false, 8, false>);
+        default: return nullptr;
+    }
+}
+
+KernelFn select_tileg_kernel(bool crc, int item, bool swap) {
+    switch (item) {
+        case 1: return crc ? k_decode_tileg<true, 1, false> : k_decode_tileg<false, 1, false>;
+        case 2: return crc ? (swap ? k_decode_tileg<true, 2, true> : k_decode_tileg<true, 2, false>)
+                           : (swap ? k_decode_tileg<false, 2, true> : k_decode_tileg<false, 2, false>);
+        case 4: return crc ? (swap ? k_decode_tileg<true, 4, true> : k_decode_tileg<true, 4, false>)
+                           : (swap ? k_decode_tileg<false, 4, true> : k_decode_tileg<false, 4, false>);
+        case 8: return crc ? (swap ? k_decode_tileg<true, 8, true> : k_decode_tileg<true, 8, false>)
+                           : (swap ? k_decode_tileg<false, 8, true> : k_decode_tileg<false, 8, false>);
         default: return nullptr;
     }
 }

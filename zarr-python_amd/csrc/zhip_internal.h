@@ -88,6 +88,12 @@ struct DecodeParams {
     const uint32_t* tz;
     const uint32_t* kq4;
     const struct TileEnt* tmap;
+    // k_decode_tileg (tileg != 0): group map, step multiply table, steps
+    uint32_t tileg;
+    const struct GroupEnt* gmap;
+    const uint32_t* gtz;
+    uint32_t n_groups, g_step_t;
+    int64_t g_step_o;
     // fused shard-index CRC verification: workgroup g checks indexes g, g+G, ...
     const zhip_chunk* idx_chunks;
     zhip_status* idx_status;
