@@ -174,3 +174,26 @@ def test_predict_rows_declines_missing_and_irregular():
     P, t, chain, spec, stride, elen, size = _sharded_headline_tables()
     P.predict_rows(t, chain, spec, size - 4096)  # a prediction past the end of src
     assert t.predict is None
+
+
+def test_plan_encode_tile_modes():
+    """Transposed encodes: full chunks -> tile (k_encode_tile4 / k_encode_tileg
+    by the library), edge chunks with prefix-box selections -> tile_prefix
+    (k_encode_tile); strided selections -> neither (persistent k_encode)."""
+    from zarr_hip.planner import plan_encode
+    from zarr_hip.spec import ArraySpec
+
+    codecs = C.parse_codecs([{"name": "transpose", "configuration": {"order": [2, 1, 0]}},
+                             {"name": "bytes", "configuration": {"endian": "little"}}, {"name": "crc32c"}])
+    spec = ArraySpec((64, 48, 32), np.dtype("float32"), 0.0)
+    chain = analyze_chain(codecs, spec)
+    astr = [72 * 48 * 4, 48 * 4, 4]  # a (100, 72, 48) float32 array, C order, byte strides
+    full = tuple(slice(0, n, 1) for n in (64, 48, 32))
+    t = plan_encode(chain, spec, [(0, full, [0, 0, 0])], astr, 0)
+    assert t.tile and not t.tile_prefix
+    edge = (slice(0, 36, 1), slice(0, 48, 1), slice(0, 16, 1))
+    t = plan_encode(chain, spec, [(0, full, [0, 0, 0]), (1 << 20, edge, [64, 0, 32])], astr, 0)
+    assert t.tile_prefix and not t.tile
+    strided = (slice(0, 64, 2), slice(0, 48, 1), slice(0, 32, 1))
+    t = plan_encode(chain, spec, [(0, strided, [0, 0, 0])], astr, 0)
+    assert not t.tile and not t.tile_prefix

@@ -99,3 +99,53 @@ def test_staging_layout_alignment():
     offs = [lay.add(b"x" * n)[0] for n in (1, 300, 0, 256, 7)]
     assert all(o % 256 == 0 for o in offs)
     assert offs == [0, 256, 768, 768, 1024]
+
+
+# ------------------------------------------- slab groups of host-out reads
+def _batch_for(shape, chunks, sel=(Ellipsis,)):
+    from zarr_hip.indexing import chunk_batch
+
+    rows, out_shape = chunk_batch(sel, shape, chunks)
+    return [(None, None, csel, osel, comp) for _, csel, osel, comp in rows], out_shape
+
+
+@pytest.mark.parametrize("shape,chunks,sel", [
+    ((256, 256, 128), (64, 64, 64), (Ellipsis,)),
+    ((256, 256, 128), (64, 64, 64), (slice(5, 250), slice(None), slice(3, 128))),
+    ((512, 64, 64), (48, 64, 64), (Ellipsis,)),      # ragged last slab
+    ((256, 128, 128), (32, 64, 64), (7, slice(None), slice(None))),
+])
+def test_slab_groups_partition_out_rows(shape, chunks, sel):
+    """HipCodecPipeline._read_slabs' groups: disjoint byte ranges of out in
+    row order, every item in exactly one group, each item's rows inside its
+    group's range."""
+    import torch
+
+    from zarr_hip.pipeline import _slab_groups
+
+    batch, out_shape = _batch_for(shape, chunks, sel)
+    out = torch.empty(out_shape, dtype=torch.float32)
+    g = _slab_groups(batch, out)
+    if out.numel() * 4 < 16 << 20:
+        assert g is None
+        return
+    assert g is not None and len(g) >= 2
+    row_bytes = out[0].numel() * 4
+    assert sorted(i for _, _, idx in g for i in idx) == list(range(len(batch)))
+    for (a0, b0, _), (a1, b1, _) in zip(g, g[1:]):
+        assert b0 <= a1
+    for a, b, idx in g:
+        for i in idx:
+            r = batch[i][3][0]
+            assert a <= r.start * row_bytes and r.stop * row_bytes <= b
+
+
+def test_slab_groups_declines():
+    import torch
+
+    from zarr_hip.pipeline import _slab_groups
+
+    batch, out_shape = _batch_for((256, 256, 128), (64, 64, 64))
+    assert _slab_groups(batch, torch.empty(out_shape, dtype=torch.float32).transpose(0, 1)) is None  # strided
+    one_row, shp = _batch_for((64, 512, 512), (64, 64, 64))  # a single chunk row along dim 0
+    assert _slab_groups(one_row, torch.empty(shp, dtype=torch.float32)) is None
