@@ -57,6 +57,7 @@ extern "C" {
 #define ZHIP_E_INVALID -1
 #define ZHIP_E_HIP -2
 #define ZHIP_E_UNSUPPORTED -3
+#define ZHIP_E_IO -4          /* a file piece could not be read in full (zhip_stage_*) */
 
 /* per-chunk status codes (zhip_status.code) */
 #define ZHIP_ST_OK 0u
@@ -303,16 +304,21 @@ int zhip_encode_mapped(const zhip_plan *plan, const void *arr, void *dst, const 
  * One piece = `nbytes` host bytes at `host`, bound for `dst_off` in the
  * staging buffer; pieces sorted by dst_off, non-overlapping. */
 typedef struct zhip_piece {
-    uint64_t host;     /* host address */
+    uint64_t host;     /* host address (ZHIP_PIECE_FILE: a NUL-terminated file path) */
     uint64_t nbytes;
     uint64_t dst_off;  /* offset in the pinned and device buffers */
     uint64_t flags;    /* ZHIP_PIECE_* */
+    uint64_t file_off; /* ZHIP_PIECE_FILE: byte offset in the file */
 } zhip_piece;
 
 /* The piece's host bytes are page-locked (a pinned store's arena, a pinned
  * tensor): DMA them straight to `dev`, no packing.  Runs of such pieces that
  * are contiguous in both host and device order go as one copy. */
 #define ZHIP_PIECE_PINNED 1u
+/* The piece is nbytes of a file (LocalStore, src/zarr/storage/_local.py):
+ * the packing thread preads them straight into the pinned window -- no
+ * Python read, no intermediate bytes object. */
+#define ZHIP_PIECE_FILE 2u
 
 /* Pack the pageable pieces into `pinned` (total bytes) with `nthreads` host
  * threads, window by window; each window's packed runs are copied to `dev`

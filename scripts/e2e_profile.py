@@ -32,7 +32,18 @@ def main():
     data = bench.synthetic(shape)
     darr = bench.build_replica(dev, torch.from_numpy(data).to(dev), shape, chunks, [bench.LE, bench.CRC])
     kind = os.environ.get("STORE", "memory")
-    host = (zarr_hip.PinnedMemoryStore if kind == "pinned" else zarr_hip.MemoryStore)(darr.store_path.store.to_dict())
+    if kind == "local":
+        import tempfile
+
+        if os.environ.get("NOFILE"):  # A/B: LocalStore bytes through Python reads + packing
+            del zarr_hip.store.LocalStore.locate_sync
+            kind = "local-pyread"
+        host = zarr_hip.LocalStore(tempfile.mkdtemp(prefix="zhip_e2e_"))
+        for k, v in darr.store_path.store.to_dict().items():
+            host.set_sync(k, v)
+    else:
+        host = (zarr_hip.PinnedMemoryStore if kind == "pinned" else zarr_hip.MemoryStore)(
+            darr.store_path.store.to_dict())
     arr = zarr_hip.Array.open(host)
     out = torch.empty(shape, dtype=torch.float32, device=dev)
     acc = defaultdict(list)

@@ -43,7 +43,7 @@ def main():
         def pack_par():
             pieces = np.zeros(64, N.PIECE_DT)
             for i, v in enumerate(views):
-                pieces[i] = (v.ctypes.data, 1 << 20, i << 20, 0)
+                pieces[i] = (v.ctypes.data, 1 << 20, i << 20, 0, 0)
             big = np.empty(0)
             # one host copy per piece through the pool: emulate with host_copy of a packed staging
             for i, v in enumerate(views):
@@ -54,7 +54,7 @@ def main():
     cs = torch.cuda.Stream(dev)
     pieces = np.zeros(64, N.PIECE_DT)
     for i, v in enumerate(views):
-        pieces[i] = (v.ctypes.data, 1 << 20, i << 20, 0)
+        pieces[i] = (v.ctypes.data, 1 << 20, i << 20, 0, 0)
     for win in (1, 2, 4, 8, 16):
         for th in (8, 16):
             def run():

@@ -186,12 +186,12 @@ def test_stage_mixed_pinned_and_pageable_pieces(device):
         if i % 2 == 0 or i % 7 == 0:  # pinned: consecutive ones are contiguous in host and dst order
             n = int(rng.integers(1, 200000))
             poff = (poff + 255) // 256 * 256
-            rows.append((pin.data_ptr() + poff, n, off, N.PIECE_PINNED))
+            rows.append((pin.data_ptr() + poff, n, off, N.PIECE_PINNED, 0))
             want[off] = pin.numpy()[poff: poff + n].copy()
             poff += n
         else:
             v = pageable[i % len(pageable)]
-            rows.append((v.ctypes.data, v.size, off, 0))
+            rows.append((v.ctypes.data, v.size, off, 0, 0))
             want[off] = v.copy()
             n = v.size
         off = (off + n + 255) // 256 * 256
@@ -280,3 +280,32 @@ def test_slab_read_crc_error_in_later_slab(device):
 def test_slab_read_sharded_host(device):
     _roundtrip(device, (256, 128, 128), (64, 128, 128), "float32",
                [SHARD((32, 64, 64), [LE, CRC], "end")], host_store="pinned")
+
+
+# --------------------------------------------- local files: pread by the pool
+def test_local_store_file_pieces(device, tmp_path):
+    """LocalStore chunks reach HBM as ZHIP_PIECE_FILE pieces (the staging
+    pool preads them into the pinned windows): multi-window unsharded reads,
+    missing chunks, and a file piece that cannot be read in full."""
+    import zarr_hip
+    from zarr_hip import staging
+    from zarr_hip.store import FileRef
+
+    meta = O.ArrayMeta((256, 128, 128), (64, 64, 64), np.dtype("float32"), 1.5, codecs=[LE, CRC])
+    host = {}
+    data = _data((256, 128, 128), "float32")
+    O.write(host, meta, (Ellipsis,), data)
+    host.pop("c/1/0/1")
+    st = zarr_hip.LocalStore(str(tmp_path))
+    arr = zarr_hip.Array.create(st, (256, 128, 128), (64, 64, 64), "float32", 1.5, codecs=[LE, CRC])
+    for k, v in host.items():
+        st.set_sync(k, v)
+    assert isinstance(st.locate_sync("c/0/0/0"), FileRef) and st.locate_sync("c/1/0/1") is None
+    for sel in [(Ellipsis,), (slice(3, 200), 5, slice(None, None, 3))]:
+        assert arr[sel].tobytes() == np.ascontiguousarray(O.read(host, meta, sel)).tobytes()
+    # a piece that claims more bytes than its file holds fails loudly
+    lay = staging.StagingLayout()
+    lay.add(FileRef(st._path("c/0/0/0"), 0, len(host["c/0/0/0"]) + 4096))
+    with pytest.raises(Exception):
+        _, _, pend = staging.stage(lay, device, defer=True)
+        pend.finish()

@@ -734,7 +734,7 @@ int zhip_encode_mapped(const zhip_plan* plan, const void* arr, void* dst, const 
         p.tmap = reinterpret_cast<const TileEnt*>(plan->d_tile_tables + plan->tile4_off_map);
         d_rowmap = nullptr;
     } else if ((encode_flags & ZHIP_DF_TILE) && plan->gd >= 0 && plan->d_tile_tables && !(g_tune_bits & kTuneTile1) &&
-               L.shape[plan->tq] % (16 / L.itemsize) == 0) {
+               L.shape[plan->tq] % (16 / L.itemsize) == 0 && plan->n_groups < 65536u) {
         // (whole 16-byte pieces along tq: a piece never reaches past the chunk)
         // full selections, tiles grouped by four at a uniform step: k_encode_tileg
         p.tile = 2;
@@ -749,7 +749,8 @@ int zhip_encode_mapped(const zhip_plan* plan, const void* arr, void* dst, const 
         p.g_step_t = plan->sstride[plan->gd];
         p.g_step_o = L.out_stride[plan->gd];
         d_rowmap = nullptr;
-    } else if ((encode_flags & (ZHIP_DF_TILE | ZHIP_DF_TILE_PREFIX)) && plan->tq >= 0 && plan->d_tile_tables) {
+    } else if ((encode_flags & (ZHIP_DF_TILE | ZHIP_DF_TILE_PREFIX)) && plan->tq >= 0 && plan->d_tile_tables &&
+               (plan->t_per_chunk + 3u) / 4u < 65536u) {
         // every other transposed batch (partial tiles, many tiles per chunk,
         // edge chunks with prefix selections): k_encode_tile
         p.tile = 1;

@@ -760,16 +760,21 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     }
     __syncthreads();
     if (t != 0) return;
-    if (s_ne[0] | s_ne[1] | s_ne[2] | s_ne[3]) p.nonempty[c] = 1u;  // flags zeroed before the launch
+    // arrival word: workgroups arrived (low 16 bits) | non-empty ones (high 16)
+    const bool ne = (s_ne[0] | s_ne[1] | s_ne[2] | s_ne[3]) != 0u;
+    uint32_t* accw = p.ws + 4ull * c;
     if constexpr (CRC) {
         const uint32_t V = s_red[0] ^ s_red[1] ^ s_red[2] ^ s_red[3];
-        uint32_t* accw = p.ws + 4ull * c;
         const uint32_t prev = __hip_atomic_fetch_xor(accw, V, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::"v"(prev) : "memory");
-        const uint32_t tk = __hip_atomic_fetch_add(accw + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (tk + 1u != gpc) return;
+    }
+    const uint32_t tk = __hip_atomic_fetch_add(accw + 2, ne ? 0x10001u : 1u, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+    if ((tk & 0xFFFFu) + 1u != gpc) return;
+    __hip_atomic_store(accw + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    p.nonempty[c] = ((tk >> 16) != 0u || ne) ? 1u : 0u;
+    if constexpr (CRC) {
         const uint32_t raw = __hip_atomic_exchange(accw, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(accw + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const uint32_t crc = ~(gf_mul(raw, p.c_inv) ^ p.c3);
         uint8_t* tr = cp + p.g.nbytes;  // LE trailer (crc32c_.py:64-68)
         tr[0] = (uint8_t)crc;
@@ -778,7 +783,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
         tr[3] = (uint8_t)(crc >> 24);
         zhip_status st = {ZHIP_ST_OK, crc, crc, 0u};
         p.status[c] = st;
-    } else if (grp == 0) {
+    } else {
         zhip_status st = {ZHIP_ST_OK, 0u, 0u, 0u};
         p.status[c] = st;
     }
@@ -910,17 +915,24 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     }
     __syncthreads();
     if (t != 0) return;
-    if (s_ne[0] | s_ne[1] | s_ne[2] | s_ne[3]) p.nonempty[c] = 1u;  // flags zeroed before the launch
+    // arrival word: groups arrived (low 16 bits) | non-empty groups (high 16);
+    // the last arrival writes the chunk's non-empty flag (no zeroing pass)
+    const bool ne = (s_ne[0] | s_ne[1] | s_ne[2] | s_ne[3]) != 0u;
     uint8_t* const chunk = p.dst + ch.src;
+    uint32_t* accw = p.ws + 4ull * c;
+    uint32_t raw = 0;
     if constexpr (CRC) {
         const uint32_t V = gf_mul(s_red[0] ^ s_red[1] ^ s_red[2] ^ s_red[3], ge.ku);
-        uint32_t* accw = p.ws + 4ull * c;
         const uint32_t prev = __hip_atomic_fetch_xor(accw, V, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::"v"(prev) : "memory");
-        const uint32_t tk = __hip_atomic_fetch_add(accw + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (tk + 1u != gpc) return;
-        const uint32_t raw = __hip_atomic_exchange(accw, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(accw + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    const uint32_t tk = __hip_atomic_fetch_add(accw + 2, ne ? 0x10001u : 1u, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+    if ((tk & 0xFFFFu) + 1u != gpc) return;
+    __hip_atomic_store(accw + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    p.nonempty[c] = ((tk >> 16) != 0u || ne) ? 1u : 0u;
+    if constexpr (CRC) {
+        raw = __hip_atomic_exchange(accw, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const uint32_t crc = ~(raw ^ p.c3);  // ku carries t_c_inv
         uint8_t* tr = chunk + p.g.nbytes;    // LE trailer (crc32c_.py:64-68)
         tr[0] = (uint8_t)crc;
@@ -929,7 +941,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
         tr[3] = (uint8_t)(crc >> 24);
         zhip_status st = {ZHIP_ST_OK, crc, crc, 0u};
         p.status[c] = st;
-    } else if (grp == 0) {
+    } else {
         zhip_status st = {ZHIP_ST_OK, 0u, 0u, 0u};
         p.status[c] = st;
     }

@@ -490,9 +490,8 @@ int launch_encode(const EncodeParams& p, hipStream_t stream, int max_grid) {
         EncodeFn fn = select_encode_tileg_kernel(crc, p.g.itemsize, swap);
         if (!fn) return ZHIP_E_UNSUPPORTED;
         if (p.n_chunks == 0) return ZHIP_OK;
-        if ((uint64_t)p.n_chunks * p.n_groups >= (1ull << 31)) return ZHIP_E_UNSUPPORTED;
-        if (hipMemsetAsync(p.nonempty, 0, (size_t)p.n_chunks * sizeof(uint32_t), stream) != hipSuccess)
-            return ZHIP_E_HIP;
+        if ((uint64_t)p.n_chunks * p.n_groups >= (1ull << 31) || p.n_groups >= 65536u) return ZHIP_E_UNSUPPORTED;
+        // (the last arrival of each chunk writes its non-empty flag)
         hipLaunchKernelGGL(fn, dim3(p.n_chunks * p.n_groups), dim3(kThreads), 0, stream, p);
         return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
     }
@@ -501,10 +500,8 @@ int launch_encode(const EncodeParams& p, hipStream_t stream, int max_grid) {
         if (!fn) return ZHIP_E_UNSUPPORTED;
         if (p.n_chunks == 0) return ZHIP_OK;
         const uint64_t gpc = (p.t_per_chunk + 3u) / 4u;  // four tiles per workgroup
-        if ((uint64_t)p.n_chunks * gpc >= (1ull << 31)) return ZHIP_E_UNSUPPORTED;
-        // tiles set their chunk's non-empty flag: zero the flags first
-        if (hipMemsetAsync(p.nonempty, 0, (size_t)p.n_chunks * sizeof(uint32_t), stream) != hipSuccess)
-            return ZHIP_E_HIP;
+        if ((uint64_t)p.n_chunks * gpc >= (1ull << 31) || gpc >= 65536u) return ZHIP_E_UNSUPPORTED;
+        // (the last arrival of each chunk writes its non-empty flag)
         hipLaunchKernelGGL(fn, dim3((uint32_t)(p.n_chunks * gpc)), dim3(kThreads), 0, stream, p);
         return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
     }

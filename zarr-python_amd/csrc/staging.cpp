@@ -7,9 +7,12 @@
 // transfer and the caller's planning all overlap, with no per-window work in
 // Python.  A parallel host memcpy serves the way back (pinned result -> a
 // caller's host array).
+#include <fcntl.h>
 #include <hip/hip_runtime.h>
+#include <unistd.h>
 
 #include <atomic>
+#include <cerrno>
 #include <condition_variable>
 #include <cstring>
 #include <functional>
@@ -110,6 +113,26 @@ static bool enqueue_pinned(const zhip_piece* pieces, uint32_t n_pieces, uint8_t*
     return any_packed;
 }
 
+// pread [off, off + n) of a file into dst; false unless every byte arrived
+static bool read_file_range(const char* path, uint64_t off, uint8_t* dst, uint64_t n) {
+    const int fd = ::open(path, O_RDONLY | O_CLOEXEC);
+    if (fd < 0) return false;
+    bool ok = true;
+    while (n > 0) {
+        const ssize_t r = ::pread(fd, dst, n, (off_t)off);
+        if (r <= 0) {
+            if (r < 0 && errno == EINTR) continue;
+            ok = false;
+            break;
+        }
+        dst += r;
+        off += (uint64_t)r;
+        n -= (uint64_t)r;
+    }
+    ::close(fd);
+    return ok;
+}
+
 static int pack_windows(const zhip_piece* pieces, uint32_t n_pieces, uint8_t* pinned, uint8_t* d, uint64_t total,
                         uint64_t window, uint32_t nthreads, hipStream_t st) {
     std::atomic<int> rc{ZHIP_OK};
@@ -156,7 +179,13 @@ static int pack_windows(const zhip_piece* pieces, uint32_t n_pieces, uint8_t* pi
                 const uint64_t s = pc.dst_off > a ? pc.dst_off : a;
                 const uint64_t e = pc.dst_off + pc.nbytes < b ? pc.dst_off + pc.nbytes : b;
                 if (s >= e) continue;
-                std::memcpy(pinned + s, reinterpret_cast<const uint8_t*>(pc.host) + (s - pc.dst_off), e - s);
+                if (pc.flags & ZHIP_PIECE_FILE) {
+                    if (!read_file_range(reinterpret_cast<const char*>(pc.host), pc.file_off + (s - pc.dst_off),
+                                         pinned + s, e - s))
+                        rc.store(ZHIP_E_IO);
+                } else {
+                    std::memcpy(pinned + s, reinterpret_cast<const uint8_t*>(pc.host) + (s - pc.dst_off), e - s);
+                }
                 if (run_e > run_s && s - run_e >= 256) flush();  // a real gap: leave it alone
                 if (run_e == run_s) run_s = s;
                 run_e = e;

@@ -31,6 +31,7 @@ CF_MISSING = 1
 
 E_INVALID = -1
 E_HIP = -2
+E_IO = -4
 E_UNSUPPORTED = -3
 
 DF_FAST_ROWS = 1
@@ -121,8 +122,10 @@ class Predict(ctypes.Structure):
 
 
 # zhip_piece (include/zarrhip.h)
-PIECE_DT = np.dtype([("host", "<u8"), ("nbytes", "<u8"), ("dst_off", "<u8"), ("flags", "<u8")])
+PIECE_DT = np.dtype([("host", "<u8"), ("nbytes", "<u8"), ("dst_off", "<u8"), ("flags", "<u8"),
+                     ("file_off", "<u8")])
 PIECE_PINNED = 1
+PIECE_FILE = 2
 
 # zhip_rowblk (include/zarrhip.h)
 ROWBLK_DT = np.dtype([("rel", "<i4"), ("lo", "<u2"), ("hi", "<u2")])

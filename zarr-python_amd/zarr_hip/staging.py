@@ -27,7 +27,7 @@ import os
 import numpy as np
 
 from .interop import byte_payload, is_missing_key_error, request_classes, staged_bytes
-from .store import ALIGN, TAIL_SLACK, DeviceRef, pinned_spans
+from .store import ALIGN, TAIL_SLACK, DeviceRef, FileRef, pinned_spans
 
 # 4 MiB windows: smaller ones pay ~10 us per hipMemcpyAsync, larger ones start
 # the DMA late (scripts/stage_micro.py)
@@ -128,19 +128,24 @@ def stage(layout: StagingLayout, device, post=(), defer: bool = False):
     from . import _native as N
 
     total = max(layout.top, 16)
-    views = [_host_view(buf) for buf, _, _ in layout.pieces]
+    # file pieces carry an encoded path (kept alive with the job) and an offset
+    views = [np.frombuffer(buf.path.encode() + b"\0", np.uint8) if isinstance(buf, FileRef) else _host_view(buf)
+             for buf, _, _ in layout.pieces]
     pieces = np.zeros(len(views), N.PIECE_DT)
     addrs = [v.ctypes.data for v in views]
     pieces["host"] = addrs
     pieces["nbytes"] = [n for _, _, n in layout.pieces]
     pieces["dst_off"] = [off for _, off, _ in layout.pieces]
+    files = [isinstance(buf, FileRef) for buf, _, _ in layout.pieces]
+    flags = [N.PIECE_FILE if f else 0 for f in files]
+    if any(files):
+        pieces["file_off"] = [buf.offset if f else 0 for f, (buf, _, _) in zip(files, layout.pieces)]
     spans = pinned_spans()
-    all_pinned = False
     if spans:
-        flags = [N.PIECE_PINNED if any(lo <= a and a + n <= hi for lo, hi in spans) else 0
-                 for a, (_, _, n) in zip(addrs, layout.pieces)]
-        pieces["flags"] = flags
-        all_pinned = all(flags)
+        flags = [fl or (N.PIECE_PINNED if any(lo <= a and a + n <= hi for lo, hi in spans) else 0)
+                 for fl, a, (_, _, n) in zip(flags, addrs, layout.pieces)]
+    pieces["flags"] = flags
+    all_pinned = bool(flags) and all(fl == N.PIECE_PINNED for fl in flags)
     # the packing buffer (pinned, reused through torch's caching host allocator)
     host = torch.empty(16 if all_pinned else total + TAIL_SLACK, dtype=torch.uint8, pin_memory=True)
     dev = torch.empty(total + TAIL_SLACK, dtype=torch.uint8, device=device)
@@ -171,7 +176,11 @@ def gather_sources(batch: list, device, defer: bool = False):
     raws = []
     for item in batch:
         bg = item[0]
-        raws.append(staged_bytes(bg.get_sync(prototype=None) if hasattr(bg, "get_sync") else bg))
+        loc = getattr(getattr(bg, "store", None), "locate_sync", None)
+        if loc is not None:  # a local file: the staging pool preads it (ZHIP_PIECE_FILE)
+            raws.append(loc(bg.path))
+        else:
+            raws.append(staged_bytes(bg.get_sync(prototype=None) if hasattr(bg, "get_sync") else bg))
     arenas = {id(r.arena): r.arena for r in raws if isinstance(r, DeviceRef)}
     all_dev = all(r is None or isinstance(r, DeviceRef) for r in raws)
     if all_dev and len(arenas) <= 1:
@@ -267,6 +276,20 @@ def gather_sharded_partial(batch: list, sh, cps, n_inner: int, inner_shape, spec
                 continue  # missing inner chunk -> fill (sharding.py:700-712)
             reqs.append(Range(int(o), int(o) + int(n)))
             want.append(slot)
+        if reqs and st is not None and hasattr(st, "locate_sync"):
+            # a local file: each touched inner chunk is one pread of the shard
+            # file by the staging pool (no coalescing needed: no request cost)
+            whole = st.locate_sync(bg.path)
+            if whole is None:
+                out_of_shard[k] = None
+                continue
+            for slot, r in zip(want, reqs):
+                if r.end > whole.length:
+                    raise ValueError("shard index entry points outside the shard blob")
+                off, n = lay.add(FileRef(whole.path, r.start, r.end - r.start))
+                src_by[slot], len_by[slot], miss_by[slot] = off, n, False
+            out_of_shard[k] = (src_by, len_by, miss_by, idx_off)
+            continue
         if reqs:
             cfg = spec.config  # forwarded like sharding.py:1695-1752
             try:

@@ -155,6 +155,20 @@ class MemoryStore(_RangesMixin):
         return dict(self._d)
 
 
+@dataclass(frozen=True)
+class FileRef:
+    """Bytes [offset, offset + length) of a file: what LocalStore.locate_sync
+    returns so staging can pread them straight into pinned memory
+    (ZHIP_PIECE_FILE) instead of reading them into Python bytes first."""
+
+    path: str
+    offset: int
+    length: int
+
+    def __len__(self):
+        return self.length
+
+
 class LocalStore(MemoryStore):
     """Files under a root directory (LocalStore restated, host side only)."""
 
@@ -176,6 +190,18 @@ class LocalStore(MemoryStore):
             a, b = _resolve_range(byte_range, os.fstat(f.fileno()).st_size)
             f.seek(a)
             return memoryview(f.read(b - a))
+
+    def locate_sync(self, key, byte_range=None) -> FileRef | None:
+        """Where get_sync's bytes are, without reading them (None: missing key)."""
+        p = self._path(key)
+        try:
+            n = os.stat(p).st_size
+        except FileNotFoundError:
+            return None
+        if byte_range is None:
+            return FileRef(p, 0, n)
+        a, b = _resolve_range(byte_range, n)
+        return FileRef(p, a, b - a)
 
     def set_sync(self, key, value):
         from .interop import byte_payload
