@@ -64,8 +64,9 @@ def main():
     inner_stage = staging.stage
 
     def count_runs(layout, *a, **k):
-        addrs = [(staging._host_view(b).ctypes.data, off, n) for b, off, n in layout.pieces]
-        r = 1 + sum(1 for (h0, d0, _), (h1, d1, _) in zip(addrs, addrs[1:]) if h1 - h0 != d1 - d0)
+        addrs = [(staging._host_view(b).ctypes.data, off, n) for b, off, n in layout.pieces
+                 if not isinstance(b, staging.FileRef)]
+        r = min(1, len(addrs)) + sum(1 for (h0, d0, _), (h1, d1, _) in zip(addrs, addrs[1:]) if h1 - h0 != d1 - d0)
         runs.append(r)
         return inner_stage(layout, *a, **k)
     staging.stage = count_runs
