@@ -182,7 +182,8 @@ int zhip_plan_upload(zhip_plan *plan);
 /* Decode `n_chunks` chunks of `src` (device) into `out` (device).
  * src must stay readable for 64 bytes past src_size (loads are 16-byte wide).
  * d_chunks/d_sels/d_status/d_workspace/d_errflag are device pointers;
- * d_workspace holds 4*n_chunks zeroed uint32 words (8-byte aligned) (self-resetting: keep it
+ * d_workspace holds workspace_words (zhip_plan_info; 4 for most layouts) * n_chunks zeroed
+ * uint32 words (8-byte aligned) (self-resetting: keep it
  * for the next call).  *d_errflag gets the OR of (1 << status code) over all
  * chunks whose status is an error (not OK, not MISSING).  `stream` is a
  * hipStream_t (NULL = default stream).  Asynchronous.  With ZHIP_LF_NO_WRITE

@@ -29,17 +29,19 @@ def main():
     data = torch.from_numpy(bench.synthetic(shape, seed=0)).to(dev)
     codecs = [{"name": "transpose", "configuration": {"order": [2, 1, 0]}}, bench.LE, bench.CRC]
     steps = int(os.environ.get("STEPS", "20"))
-    for name, chunks in (("c3_64", (64, 64, 64)), ("c3_128", (128, 128, 128))):
-        if name not in os.environ.get("ARMS", "c3_64,c3_128"):
+    nocrc = codecs[:2]
+    for name, chunks, cod in (("c3_64", (64, 64, 64), codecs), ("c3_128", (128, 128, 128), codecs),
+                              ("c3_64_nocrc", (64, 64, 64), nocrc), ("c3_128_nocrc", (128, 128, 128), nocrc)):
+        if name not in os.environ.get("ARMS", "c3_64,c3_128").split(","):
             continue
-        progs = [bench.build_replica(dev, data, shape, chunks, codecs).prepare_read((Ellipsis,)) for _ in range(4)]
+        progs = [bench.build_replica(dev, data, shape, chunks, cod).prepare_read((Ellipsis,)) for _ in range(4)]
         progs[0][0].launch()
         progs[0][0].results()
         assert torch.equal(progs[0][1].view(torch.int32), data.view(torch.int32)), name
         flags = N.Plan(progs[0][0].tables.layout, upload=False).kernel_flags
         wall, kern = bench.time_programs([p for p, _ in progs], steps, 3, dev)
         n_chunks = int(torch.tensor([s // c for s, c in zip(shape, chunks)]).prod())
-        alg = data.numel() * 4 * 2 + 4 * n_chunks
+        alg = data.numel() * 4 * 2 + (4 * n_chunks if cod is codecs else 0)
         print(json.dumps({"arm": name, "tune": tune, "tile4": bool(flags & N.PK_TILE4),
                           "us_graph": round(wall * 1e6, 2), "us_eager": round(kern * 1e6, 2),
                           "hbm_frac": round(alg / wall / 8e12, 4)}), flush=True)

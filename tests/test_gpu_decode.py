@@ -577,3 +577,19 @@ def test_transpose_tileg_missing_sharded_and_crc(device):
     with pytest.raises(ValueError) as got:
         arr[...]
     assert str(got.value) == str(want.value)
+
+
+def test_transpose_tileg_many_groups(device):
+    """1024 groups per chunk (> 256: the arrival-count protocol) and 128
+    groups (two-level 64-bit arrival, 8 subgroups of 16): decode and encode
+    exact.  80-row tiles keep k_decode_tile4 out."""
+    import zarr_hip
+
+    for shape in [(512, 256, 80), (128, 128, 80)]:
+        arr, host, meta = _roundtrip(device, shape, shape, "float32", [T((2, 1, 0)), LE, CRC])
+        assert _tileg_engaged(arr)
+        st = zarr_hip.DeviceStore(device, capacity=1 << 20)
+        warr = zarr_hip.Array.create(st, shape, shape, "float32", 0.0, codecs=[T((2, 1, 0)), LE, CRC])
+        warr[...] = O.read(host, meta)
+        got = {k: v for k, v in st.to_dict().items() if not k.endswith("zarr.json")}
+        assert got == host

@@ -245,6 +245,7 @@ int zhip_plan_create(const zhip_layout* layout, zhip_plan** out) {
     p->tile4 = 0;
     p->gd = -1;
     p->n_groups = 0;
+    p->n_sub = 0;
     // tile mode: a stored dim (not the innermost) that is contiguous in out
     p->tq = -1;
     {
@@ -279,7 +280,11 @@ int zhip_plan_create(const zhip_layout* layout, zhip_plan** out) {
             // k_encode_tileg: the innermost other stored dim with shape % 4 == 0
             for (int d = L.ndim - 2; d >= 0 && p->gd < 0; --d)
                 if (d != p->tq && L.shape[d] % 4 == 0) p->gd = d;
-            if (p->gd >= 0) p->n_groups = T / 4;
+            if (p->gd >= 0) {
+                p->n_groups = T / 4;
+                // two-level arrival (subgroups of 16 workgroups) for 17..256 groups
+                p->n_sub = (p->n_groups > 16u && p->n_groups <= 256u) ? (p->n_groups + 15u) / 16u : 0u;
+            }
         }
     }
     *out = p;
@@ -442,7 +447,7 @@ int zhip_plan_kernel_flags(const zhip_plan* p, uint32_t* flags) {
 int zhip_plan_info(const zhip_plan* p, uint32_t* units_per_chunk, uint32_t* workspace_words) {
     if (!p) return set_err(ZHIP_E_INVALID, "null plan");
     if (units_per_chunk) *units_per_chunk = p->nseg;
-    if (workspace_words) *workspace_words = 4;
+    if (workspace_words) *workspace_words = 4 + 2 * p->n_sub;  // + the grouped kernels' subgroup words
     return ZHIP_OK;
 }
 
@@ -655,6 +660,7 @@ int zhip_decode_mapped(const zhip_plan* plan, const void* src, uint64_t src_size
             p.gtz = plan->d_tile_tables + plan->g_off_tz;
             p.gmap = reinterpret_cast<const GroupEnt*>(plan->d_tile_tables + plan->g_off_map);
             p.n_groups = plan->n_groups;
+            p.n_sub = plan->n_sub;
             p.g_step_t = plan->sstride[plan->gd];
             p.g_step_o = L.out_stride[plan->gd];
         }
@@ -746,6 +752,7 @@ int zhip_encode_mapped(const zhip_plan* plan, const void* arr, void* dst, const 
         p.gtz = plan->d_tile_tables + plan->g_off_tz;
         p.gmap = reinterpret_cast<const GroupEnt*>(plan->d_tile_tables + plan->g_off_map);
         p.n_groups = plan->n_groups;
+        p.n_sub = plan->n_sub;
         p.g_step_t = plan->sstride[plan->gd];
         p.g_step_o = L.out_stride[plan->gd];
         d_rowmap = nullptr;

@@ -250,6 +250,42 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     }
 }
 
+// Arrival of one workgroup of a grouped tile kernel (k_decode_tileg /
+// k_encode_tileg) with its CRC contribution v and non-empty bit: 64-bit words
+// CRC (low 32) | arrival bits (32..47) | non-empty bits (48..63), one relaxed
+// XOR per level.  Up to 16 groups per chunk the chunk word is the only level;
+// up to 256 the groups first meet in words of 16 (the workspace tail after the
+// 4 words per chunk), whose completing arrival carries the subgroup's XOR on
+// to the chunk word.  True for the arrival completing the chunk, with the
+// XOR of every contribution and whether any group was non-empty.
+__device__ __forceinline__ bool tileg_arrive(uint32_t* ws, uint32_t n_chunks, uint32_t c, uint32_t grp,
+                                             uint32_t gpc, uint32_t n_sub, uint32_t v, bool ne, uint32_t& raw,
+                                             bool& any_ne) {
+    if (n_sub) {
+        const uint32_t sg = grp >> 4;
+        const uint32_t in_sg = min(16u, gpc - (sg << 4));
+        uint64_t* sw = reinterpret_cast<uint64_t*>(ws + 4ull * n_chunks) + (uint64_t)c * n_sub + sg;
+        const uint64_t b = 1ull << (grp & 15u);
+        const uint64_t prev = __hip_atomic_fetch_xor(sw, (b << 32) | (ne ? b << 48 : 0ull) | v, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+        if ((((prev >> 32) & 0xFFFFull) ^ b) != (1ull << in_sg) - 1ull) return false;
+        __hip_atomic_store(sw, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        v ^= (uint32_t)prev;
+        ne = ne || ((prev >> 48) & 0xFFFFull) != 0ull;
+        grp = sg;
+        gpc = n_sub;
+    }
+    uint64_t* cw = reinterpret_cast<uint64_t*>(ws) + 2ull * c;
+    const uint64_t b = 1ull << grp;
+    const uint64_t prev = __hip_atomic_fetch_xor(cw, (b << 32) | (ne ? b << 48 : 0ull) | v, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+    if ((((prev >> 32) & 0xFFFFull) ^ b) != (1ull << gpc) - 1ull) return false;
+    __hip_atomic_store(cw, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    raw = (uint32_t)prev ^ v;
+    any_ne = ne || ((prev >> 48) & 0xFFFFull) != 0ull;
+    return true;
+}
+
 // k_decode_tileg: k_decode_tile4 for the transposed layouts it declines
 // (partial tiles, more tiles per chunk, irregular steps between consecutive
 // tiles), as long as some stored dim gd other than tq and the innermost has
@@ -380,13 +416,23 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
         __syncthreads();
         if (t == 0) {
             const uint32_t V = gf_mul(s_red[0] ^ s_red[1] ^ s_red[2] ^ s_red[3], ge.ku);
-            uint32_t* accw = p.ws + 4ull * c;
-            const uint32_t prev = __hip_atomic_fetch_xor(accw, V, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            asm volatile("s_waitcnt vmcnt(0)" ::"v"(prev) : "memory");
-            const uint32_t tk = __hip_atomic_fetch_add(accw + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (tk + 1u == gpc) {
-                const uint32_t raw = __hip_atomic_exchange(accw, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(accw + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            uint32_t raw = 0;
+            bool last_one = false;
+            if (gpc <= 16u || p.n_sub) {
+                bool any_ne;
+                last_one = tileg_arrive(p.ws, p.n_chunks, c, grp, gpc, p.n_sub, V, false, raw, any_ne);
+            } else {  // more than 256 groups per chunk: XOR, then count arrivals
+                uint32_t* accw = p.ws + 4ull * c;
+                const uint32_t prev = __hip_atomic_fetch_xor(accw, V, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                asm volatile("s_waitcnt vmcnt(0)" ::"v"(prev) : "memory");
+                const uint32_t tk = __hip_atomic_fetch_add(accw + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (tk + 1u == gpc) {
+                    raw = __hip_atomic_exchange(accw, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(accw + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    last_one = true;
+                }
+            }
+            if (last_one) {
                 const uint32_t computed = ~(raw ^ p.c3);  // ku carries t_c_inv
                 const uint32_t code = computed == stored ? ZHIP_ST_OK : ZHIP_ST_CRC_MISMATCH;
                 zhip_status st = {code, stored, computed, 0u};
@@ -915,24 +961,29 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     }
     __syncthreads();
     if (t != 0) return;
-    // arrival word: groups arrived (low 16 bits) | non-empty groups (high 16);
     // the last arrival writes the chunk's non-empty flag (no zeroing pass)
     const bool ne = (s_ne[0] | s_ne[1] | s_ne[2] | s_ne[3]) != 0u;
     uint8_t* const chunk = p.dst + ch.src;
-    uint32_t* accw = p.ws + 4ull * c;
     uint32_t raw = 0;
-    if constexpr (CRC) {
-        const uint32_t V = gf_mul(s_red[0] ^ s_red[1] ^ s_red[2] ^ s_red[3], ge.ku);
-        const uint32_t prev = __hip_atomic_fetch_xor(accw, V, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::"v"(prev) : "memory");
+    const uint32_t V = CRC ? gf_mul(s_red[0] ^ s_red[1] ^ s_red[2] ^ s_red[3], ge.ku) : 0u;
+    if (gpc <= 16u || p.n_sub) {
+        bool any_ne = false;
+        if (!tileg_arrive(p.ws, p.n_chunks, c, grp, gpc, p.n_sub, V, ne, raw, any_ne)) return;
+        p.nonempty[c] = any_ne ? 1u : 0u;
+    } else {  // more than 256 groups per chunk: arrival count | non-empty count word
+        uint32_t* accw = p.ws + 4ull * c;
+        if constexpr (CRC) {
+            const uint32_t prev = __hip_atomic_fetch_xor(accw, V, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::"v"(prev) : "memory");
+        }
+        const uint32_t tk = __hip_atomic_fetch_add(accw + 2, ne ? 0x10001u : 1u, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+        if ((tk & 0xFFFFu) + 1u != gpc) return;
+        __hip_atomic_store(accw + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        p.nonempty[c] = ((tk >> 16) != 0u || ne) ? 1u : 0u;
+        if constexpr (CRC) raw = __hip_atomic_exchange(accw, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    const uint32_t tk = __hip_atomic_fetch_add(accw + 2, ne ? 0x10001u : 1u, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
-    if ((tk & 0xFFFFu) + 1u != gpc) return;
-    __hip_atomic_store(accw + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    p.nonempty[c] = ((tk >> 16) != 0u || ne) ? 1u : 0u;
     if constexpr (CRC) {
-        raw = __hip_atomic_exchange(accw, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const uint32_t crc = ~(raw ^ p.c3);  // ku carries t_c_inv
         uint8_t* tr = chunk + p.g.nbytes;    // LE trailer (crc32c_.py:64-68)
         tr[0] = (uint8_t)crc;

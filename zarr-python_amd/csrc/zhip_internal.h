@@ -92,7 +92,7 @@ struct DecodeParams {
     uint32_t tileg;
     const struct GroupEnt* gmap;
     const uint32_t* gtz;
-    uint32_t n_groups, g_step_t;
+    uint32_t n_groups, g_step_t, n_sub;
     int64_t g_step_o;
     // fused shard-index CRC verification: workgroup g checks indexes g, g+G, ...
     const zhip_chunk* idx_chunks;
@@ -179,7 +179,7 @@ struct EncodeParams {
     // k_encode_tileg (tile == 2): group map, step multiply table, steps
     const struct GroupEnt* gmap;
     const uint32_t* gtz;
-    uint32_t n_groups, g_step_t;
+    uint32_t n_groups, g_step_t, n_sub;
     int64_t g_step_o;
 };
 
@@ -244,6 +244,7 @@ struct zhip_plan {
     // tzg (1024: multiply by x^(8 sstride[gd])) | gmap (n_groups GroupEnt)
     int32_t gd;                      // -1: no such dim
     uint32_t n_groups;
+    uint32_t n_sub;                  // > 16 groups per chunk: arrival subgroups of 16 (workspace tail)
     uint64_t g_off_tz, g_off_map;    // u32 offsets in d_tile_tables
     uint32_t* d_tile_tables;
     // shard index (sharded layouts): payload 16*n_inner, E, CRC constants

@@ -158,13 +158,14 @@ class DecodeLaunch:
         self.d_idx_chunks = views[i_idx] if i_idx is not None else None
         self.d_rowmap = views[i_map] if i_map is not None else None
         nw = max(self.n, 1) * 4
+        nws = max(self.n, 1) * max(4, self.plan.workspace_words)  # zhip_plan_info
         ni = self.n_idx * 4
-        z = torch.zeros(2 * nw + 64 + ni, dtype=torch.int32, device=device)
+        z = torch.zeros(nw + nws + 64 + ni, dtype=torch.int32, device=device)
         self.d_status = z[:nw]
-        self.d_ws = z[nw: 2 * nw]
-        self.d_err = z[2 * nw: 2 * nw + 4]
+        self.d_ws = z[nw: nw + nws]
+        self.d_err = z[nw + nws: nw + nws + 4]
         if self.n_idx:
-            self.d_idx_status = z[2 * nw + 64: 2 * nw + 64 + ni]
+            self.d_idx_status = z[nw + nws + 64: nw + nws + 64 + ni]
 
     def launch(self, stream: int | None = None) -> None:
         if self.n == 0:

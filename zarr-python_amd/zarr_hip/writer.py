@@ -70,7 +70,8 @@ class EncodeLaunch:
         self.d_chunks = _upload(chunks, device)
         self.d_sels = _upload(sels if len(sels) else np.zeros(1, SEL_DT), device)
         self.d_status = torch.zeros(max(self.n, 1) * 4, dtype=torch.int32, device=device)
-        self.d_ws = torch.zeros(max(self.n, 1) * 4, dtype=torch.int32, device=device)
+        self.d_ws = torch.zeros(max(self.n, 1) * max(4, self.plan.workspace_words), dtype=torch.int32,
+                                device=device)  # zhip_plan_info
         self.d_nonempty = torch.zeros(max(self.n, 1), dtype=torch.int32, device=device)
         self.arr = arr
         self.dst = dst
