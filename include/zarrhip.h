@@ -268,6 +268,7 @@ int zhip_decode_mapped(const zhip_plan *plan, const void *src, uint64_t src_size
 #define ZHIP_TUNE_MAX_GRID 1
 #define ZHIP_TUNE_ABLATION 2
 #define ZHIP_TUNE_BLOCKS 3   /* blocks/thread per unit for plans created afterwards (4, 8, 16) */
+#define ZHIP_TUNE_STAGE_STREAMS 4  /* host staging: packed windows on 1 (default) or 2 copy streams */
 int zhip_set_tuning(int key, int value);
 
 /* Diagnostics: with ablation bit 1024 set, k_decode_pair records per-workgroup

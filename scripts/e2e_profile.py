@@ -83,6 +83,8 @@ def main():
     from zarr_hip import _native as N
 
     lib = N.lib()
+    if os.environ.get("STREAMS"):
+        lib.zhip_set_tuning(4, int(os.environ["STREAMS"]))
     begin = lib.zhip_stage_begin
     t_get = [0.0]
 
@@ -100,7 +102,7 @@ def main():
             t_get[0] = 0.0
             torch.cuda.synchronize(dev)
             if i >= 2:
-                acc[f"TOTAL get(out=device) {kind} window {win} MiB"].append(time.perf_counter() - t0)
+                acc[f"TOTAL get(out=device) {kind} window {win} MiB streams {os.environ.get('STREAMS', '1')}"].append(time.perf_counter() - t0)
             t0 = time.perf_counter()
             arr[...]
             if i >= 2:

@@ -55,14 +55,15 @@ def main():
     pieces = np.zeros(64, N.PIECE_DT)
     for i, v in enumerate(views):
         pieces[i] = (v.ctypes.data, 1 << 20, i << 20, 0, 0)
-    for win in (1, 2, 4, 8, 16):
-        for th in (8, 16):
+    for win, th, ns in [(w, 16, n) for w in (2, 4, 8, 16) for n in (1, 2)]:
+        N.lib().zhip_set_tuning(4, ns)
+        if True:
             def run():
                 N.lib().zhip_stage_h2d(pieces.ctypes.data, 64, pin.data_ptr(), dbuf.data_ptr(), n, win << 20, th,
                                        cs.cuda_stream)
                 cs.synchronize()
             t = med(run)
-            out.append({"what": f"stage_h2d window={win}MiB threads={th} (incl. sync)", "ms": t * 1e3,
+            out.append({"what": f"stage_h2d window={win}MiB threads={th} streams={ns} (incl. sync)", "ms": t * 1e3,
                         "GBps": n / t / 1e9})
     def h2d():
         dbuf[:n].copy_(pin[:n], non_blocking=True)

@@ -175,6 +175,7 @@ int zhip_set_tuning(int key, int value) {
         case ZHIP_TUNE_MAX_GRID: g_tune_max_grid = value; return ZHIP_OK;
         case ZHIP_TUNE_ABLATION: g_tune_bits = (uint32_t)value; return ZHIP_OK;
         case ZHIP_TUNE_BLOCKS: g_tune_blocks = value; return ZHIP_OK;
+        case ZHIP_TUNE_STAGE_STREAMS: zhip_stage_set_streams(value >= 2 ? 2u : 1u); return ZHIP_OK;
         default: return set_err(ZHIP_E_INVALID, "unknown tuning key");
     }
 }

@@ -136,6 +136,9 @@ constexpr uint32_t kTuneStamp = 1024u;    // k_decode_pair: per-workgroup phase 
 constexpr uint32_t kStampWG = 8192u;      // workgroups stamped per launch
 constexpr uint32_t kStampSlots = 8u;
 extern int g_tune_max_grid;
+}  // namespace zhip
+extern "C" void zhip_stage_set_streams(uint32_t n);  // staging.cpp (ZHIP_TUNE_STAGE_STREAMS)
+namespace zhip {
 extern int g_tune_blocks;
 extern uint32_t g_tune_bits;
 
