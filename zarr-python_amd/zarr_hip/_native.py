@@ -146,6 +146,11 @@ def lib():
         raise NativeError(
             f"zarr_hip native library not built: {LIB_PATH} is missing "
             "(run __graft_entry__.build() or `make -C zarr-python_amd`)")
+    # torch first: the library then binds to the HIP runtime torch loaded
+    # (one runtime per process; loading ours first leaves two, and the
+    # second to initialise sees no device)
+    import torch  # noqa: F401
+
     L = ctypes.CDLL(LIB_PATH)
     L.zhip_abi_version.restype = ctypes.c_int
     L.zhip_last_error.restype = ctypes.c_char_p
