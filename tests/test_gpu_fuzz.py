@@ -1,0 +1,115 @@
+"""Seeded randomized parity: random shapes, chunk grids (edge chunks
+included), dtypes, endianness, crc32c on/off, transposes, sharding (inner
+shape, index location, transposes inside the shard), fill values and
+selections (slices with steps, integers); each case writes the whole array,
+overwrites two random selections (an array and a scalar), then reads the whole
+array and two random selections.  The store's bytes are compared with the
+oracle's after every write, and every read as raw bytes -- through whichever
+kernels the planner picks for that geometry."""
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from test_gpu_decode import BE, CRC, LE, SHARD, T, _data
+
+pytestmark = pytest.mark.gpu
+
+DTYPES = ["float32", "int16", "uint8", "float64", "int32", "uint16"]
+
+
+def _rand_sel(rng, shape):
+    sel = []
+    for n in shape:
+        r = rng.random()
+        if r < 0.2 and n > 0:
+            sel.append(int(rng.integers(0, n)))
+        elif r < 0.35:
+            sel.append(slice(None))
+        else:
+            a = int(rng.integers(0, n))
+            b = int(rng.integers(a + 1, n + 1))
+            st = int(rng.choice([1, 1, 2, 3]))
+            sel.append(slice(a, b, st))
+    return tuple(sel)
+
+
+def _case(seed):
+    rng = np.random.default_rng(1000 + seed)
+    nd = int(rng.choice([1, 2, 2, 3, 3, 3]))
+    dtype = str(rng.choice(DTYPES))
+    sharded = nd >= 2 and rng.random() < 0.4
+    aligned = rng.random() < 0.3  # power-of-two geometries: the row / tile kernels' layouts
+    if aligned:
+        inner = tuple(int(rng.choice([8, 16, 32, 64])) for _ in range(nd))
+        per = tuple(int(rng.integers(1, 3)) for _ in range(nd)) if sharded else (1,) * nd
+        chunks = tuple(i * p for i, p in zip(inner, per))
+        shape = tuple(int(c * rng.integers(1, 3) + (0 if rng.random() < 0.7 else rng.integers(1, c)))
+                      for c in chunks)
+        if int(np.prod(shape)) > (1 << 21):  # keep the oracle fast
+            shape = tuple(min(s, 64) for s in shape)
+    elif sharded:
+        inner = tuple(int(rng.integers(2, 9)) for _ in range(nd))
+        per = tuple(int(rng.integers(1, 4)) for _ in range(nd))
+        chunks = tuple(i * p for i, p in zip(inner, per))
+    else:
+        chunks = tuple(int(rng.integers(1, 17)) for _ in range(nd))
+    if not aligned:
+        shape = tuple(int(rng.integers(1, 3 * c + 2)) for c in chunks)
+    endian = BE if (rng.random() < 0.3 and np.dtype(dtype).itemsize > 1) else LE
+    crc = rng.random() < 0.7
+    chain = []
+    if nd >= 2 and rng.random() < 0.4:
+        chain.append(T(tuple(int(x) for x in rng.permutation(nd))))
+    chain.append(endian)
+    if crc:
+        chain.append(CRC)
+    if sharded:
+        codecs = [SHARD(inner, chain, str(rng.choice(["end", "start"])))]
+    else:
+        codecs = chain
+    fill = 0
+    if np.dtype(dtype).kind == "f" and rng.random() < 0.3:
+        fill = float("nan")
+    elif rng.random() < 0.3:
+        fill = 7
+    return rng, shape, chunks, dtype, codecs, fill
+
+
+@pytest.mark.parametrize("seed", range(160))
+def test_random_roundtrip(device, seed):
+    import zarr_hip
+
+    rng, shape, chunks, dtype, codecs, fill = _case(seed)
+    meta = O.ArrayMeta(shape, chunks, np.dtype(dtype), fill, codecs=codecs)
+    host = {}
+    store = zarr_hip.DeviceStore(device) if seed % 2 == 0 else zarr_hip.MemoryStore()
+    arr = zarr_hip.Array.create(store, shape, chunks, dtype, fill, codecs=codecs)
+
+    def check_store():
+        got = {k: bytes(v) for k, v in store.to_dict().items() if not k.endswith("zarr.json")}
+        assert sorted(got) == sorted(host), (shape, chunks, codecs)
+        for k in host:
+            assert got[k] == host[k], (k, shape, chunks, codecs)
+
+    data = _data(shape, dtype, seed)
+    O.write(host, meta, (Ellipsis,), data)
+    arr[...] = data
+    check_store()
+    # an array overwrite and a scalar overwrite of random selections
+    sel = _rand_sel(rng, shape)
+    want_shape = O.read(host, meta, sel).shape
+    val = _data(want_shape, dtype, seed + 7) if want_shape else _data((1,), dtype, seed + 7)[0]
+    O.write(host, meta, sel, val)
+    arr[sel] = val
+    check_store()
+    sel = _rand_sel(rng, shape)
+    scalar = np.array(fill if rng.random() < 0.5 else 3, dtype=dtype)[()]
+    O.write(host, meta, sel, scalar)
+    arr[sel] = scalar
+    check_store()
+    for sel in [(Ellipsis,), _rand_sel(rng, shape), _rand_sel(rng, shape)]:
+        want = O.read(host, meta, sel)
+        got = arr[sel]
+        assert got.shape == want.shape, (sel, shape, chunks, codecs)
+        assert got.tobytes() == np.ascontiguousarray(want).tobytes(), (sel, shape, chunks, codecs)
