@@ -1,7 +1,7 @@
 """Seeded randomized parity: random shapes, chunk grids (edge chunks
 included), dtypes, endianness, crc32c on/off, transposes, sharding (inner
 shape, index location, transposes inside the shard), fill values and
-selections (slices with steps, integers); each case writes the whole array,
+selections (slices with steps, integers); each case (C or F order, write_empty_chunks on or off) writes the whole array,
 overwrites two random selections (an array and a scalar), then reads the whole
 array and two random selections.  The store's bytes are compared with the
 oracle's after every write, and every read as raw bytes -- through whichever
@@ -79,12 +79,16 @@ def _case(seed):
 @pytest.mark.parametrize("seed", range(160))
 def test_random_roundtrip(device, seed):
     import zarr_hip
+    from zarr_hip.spec import ArrayConfig
 
     rng, shape, chunks, dtype, codecs, fill = _case(seed)
-    meta = O.ArrayMeta(shape, chunks, np.dtype(dtype), fill, codecs=codecs)
+    wec = seed % 5 == 0
+    order = "F" if seed % 3 == 0 else "C"
+    meta = O.ArrayMeta(shape, chunks, np.dtype(dtype), fill, codecs=codecs, write_empty_chunks=wec)
     host = {}
     store = zarr_hip.DeviceStore(device) if seed % 2 == 0 else zarr_hip.MemoryStore()
-    arr = zarr_hip.Array.create(store, shape, chunks, dtype, fill, codecs=codecs)
+    arr = zarr_hip.Array.create(store, shape, chunks, dtype, fill, codecs=codecs,
+                                config=ArrayConfig(order=order, write_empty_chunks=wec))
 
     def check_store():
         got = {k: bytes(v) for k, v in store.to_dict().items() if not k.endswith("zarr.json")}
