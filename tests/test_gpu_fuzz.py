@@ -117,3 +117,39 @@ def test_random_roundtrip(device, seed):
         got = arr[sel]
         assert got.shape == want.shape, (sel, shape, chunks, codecs)
         assert got.tobytes() == np.ascontiguousarray(want).tobytes(), (sel, shape, chunks, codecs)
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_random_host_reads_large(device, tmp_path, seed):
+    """Host-sourced reads big enough for the slab pipeline (>= 16 MiB outs):
+    random chunking (sharded or not, transposed or not), host stores of the
+    three kinds, random selections, compared with the oracle."""
+    import zarr_hip
+
+    rng = np.random.default_rng(5000 + seed)
+    dtype = str(rng.choice(["float32", "int16", "float64"]))
+    it = np.dtype(dtype).itemsize
+    shape = (int(rng.choice([160, 256, 320])), 128, int(rng.choice([96, 128])) * 4 // it)
+    chunks = tuple(int(rng.choice([16, 32, 64])) for _ in range(3))
+    chain = ([T(tuple(int(x) for x in rng.permutation(3)))] if rng.random() < 0.5 else []) + [LE, CRC]
+    codecs = [SHARD(chunks, chain)] if rng.random() < 0.4 else chain
+    if codecs is not chain:
+        chunks = tuple(2 * c for c in chunks)
+    meta = O.ArrayMeta(shape, chunks, np.dtype(dtype), 0, codecs=codecs)
+    host = {}
+    O.write(host, meta, (Ellipsis,), _data(shape, dtype, seed))
+    kind = seed % 3
+    if kind == 0:
+        store = zarr_hip.MemoryStore(dict(host))
+    elif kind == 1:
+        store = zarr_hip.PinnedMemoryStore(dict(host))
+    else:
+        store = zarr_hip.LocalStore(str(tmp_path))
+        for k, v in host.items():
+            store.set_sync(k, v)
+    arr = zarr_hip.Array.create(store, shape, chunks, dtype, 0, codecs=codecs)
+    for sel in [(Ellipsis,), _rand_sel(rng, shape), (slice(3, shape[0] - 5), slice(None), slice(1, None, 2))]:
+        want = O.read(host, meta, sel)
+        got = arr[sel]
+        assert got.shape == want.shape
+        assert got.tobytes() == np.ascontiguousarray(want).tobytes(), (sel, shape, chunks, codecs)
