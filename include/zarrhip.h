@@ -331,14 +331,15 @@ typedef struct zhip_piece {
 int zhip_stage_h2d(const zhip_piece *pieces, uint32_t n_pieces, uint8_t *pinned, void *dev, uint64_t total,
                    uint64_t window, uint32_t nthreads, void *stream);
 
-/* zhip_stage_h2d started on a library thread: the pinned pieces' copies are
- * enqueued before it returns, the packing runs on the thread (NULL on
- * allocation failure); the pieces array is copied.  zhip_stage_end waits for
- * every copy to be enqueued and returns zhip_stage_h2d's code. */
+/* zhip_stage_h2d started on a library thread: returns at once (NULL on
+ * allocation failure); the pieces array is copied.  Jobs run in the order they
+ * were begun.  zhip_stage_end waits for the job's copies to be enqueued, makes
+ * `wait_stream` (a hipStream_t; NULL is the default stream) wait for exactly
+ * them (and earlier jobs'), and returns zhip_stage_h2d's code. */
 typedef struct zhip_stage_job zhip_stage_job;
 zhip_stage_job *zhip_stage_begin(const zhip_piece *pieces, uint32_t n_pieces, uint8_t *pinned, void *dev,
                                  uint64_t total, uint64_t window, uint32_t nthreads, void *stream);
-int zhip_stage_end(zhip_stage_job *job);
+int zhip_stage_end(zhip_stage_job *job, void *wait_stream);
 
 /* 1 when p points into page-locked host memory known to HIP (a pinned
  * result buffer can take the D2H DMA directly), else 0. */

@@ -60,6 +60,11 @@ def main():
 
     wrap(staging, "gather_sources", "gather_sources(fetch+pack+h2d enqueue)")
     wrap(staging, "stage", "  stage(pack+h2d enqueue)")
+    from zarr_hip import buffer as B
+    wrap(B, "empty_pinned", "empty_pinned(out)")
+    wrap(B, "copy_to_host_from_pinned", "copy_to_host_from_pinned")
+    wrap(PL, "_slab_groups", "_slab_groups")
+    wrap(PL.HipCodecPipeline, "_read_slabs", "_read_slabs(total)")
     runs = []
     inner_stage = staging.stage
 
@@ -83,6 +88,10 @@ def main():
     from zarr_hip import _native as N
 
     lib = N.lib()
+    if os.environ.get("SLAB"):  # measurement: slab group sizing (min MiB, max groups)
+        mb, mg = (int(x) for x in os.environ["SLAB"].split(","))
+        orig_groups = PL._slab_groups
+        PL._slab_groups = lambda b, o, min_bytes=0, max_groups=0: orig_groups(b, o, mb << 20, mg)
     if os.environ.get("STREAMS"):
         lib.zhip_set_tuning(4, int(os.environ["STREAMS"]))
     begin = lib.zhip_stage_begin
@@ -97,6 +106,12 @@ def main():
         staging.WINDOW = win << 20
         for i in range(12):
             torch.cuda.synchronize(dev)
+            if os.environ.get("ONLY_HOST"):
+                t0 = time.perf_counter()
+                arr[...]
+                if i >= 2:
+                    acc["TOTAL __getitem__ only"].append(time.perf_counter() - t0)
+                continue
             t0 = t_get[0] = time.perf_counter()
             arr.get((Ellipsis,), out=out)
             t_get[0] = 0.0
@@ -106,7 +121,7 @@ def main():
             t0 = time.perf_counter()
             arr[...]
             if i >= 2:
-                acc[f"TOTAL __getitem__ (host out) {kind} window {win} MiB"].append(time.perf_counter() - t0)
+                acc[f"TOTAL __getitem__ (host out) {kind} window {win} MiB slab {os.environ.get('SLAB', '8,8')}"].append(time.perf_counter() - t0)
     assert out.view(torch.int32).cpu().numpy().tobytes() == data.view(np.int32).tobytes()
     if os.environ.get("CPROFILE"):
         import cProfile

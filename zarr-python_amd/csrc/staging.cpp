@@ -260,6 +260,13 @@ int zhip_stage_h2d(const zhip_piece* pieces, uint32_t n_pieces, uint8_t* pinned,
 
 // The same job started on a host thread of the library (no caller thread, no
 // Python GIL needed while it runs); zhip_stage_end joins it.
+// Staging jobs run in the order they were begun (a ticket each): a caller
+// that begins several jobs at once (one per slab of a read) gets its slabs
+// packed and copied in slab order.
+static std::mutex g_job_mu;
+static std::condition_variable g_job_cv;
+static uint64_t g_job_next = 0, g_job_serving = 0;
+
 struct zhip_stage_job {
     std::vector<zhip_piece> pieces;
     uint8_t* pinned;
@@ -268,6 +275,7 @@ struct zhip_stage_job {
     uint32_t nthreads;
     void* stream;
     int rc;
+    hipEvent_t done;  // recorded on `stream` after the job's last copy
     std::thread th;
 };
 
@@ -276,15 +284,24 @@ zhip_stage_job* zhip_stage_begin(const zhip_piece* pieces, uint32_t n_pieces, ui
     zhip_stage_job* j = new (std::nothrow) zhip_stage_job();
     if (!j) return nullptr;
     j->rc = ZHIP_OK;
+    j->done = nullptr;
     if (total == 0) return j;
     if (!pinned || !dev || (!pieces && n_pieces)) {
         j->rc = ZHIP_E_INVALID;
         return j;
     }
-    // pinned pieces are enqueued right here (a few hipMemcpyAsync calls);
-    // only packing needs the library thread
-    if (!enqueue_pinned(pieces, n_pieces, static_cast<uint8_t*>(dev), static_cast<hipStream_t>(stream), &j->rc))
+    if (hipEventCreateWithFlags(&j->done, hipEventDisableTiming) != hipSuccess) {
+        j->done = nullptr;
+        j->rc = ZHIP_E_HIP;
         return j;
+    }
+    // page-locked pieces: enqueued here, in the caller's order (a few
+    // hipMemcpyAsync calls); a job with nothing to pack is complete now
+    hipStream_t st0 = static_cast<hipStream_t>(stream);
+    if (!enqueue_pinned(pieces, n_pieces, static_cast<uint8_t*>(dev), st0, &j->rc)) {
+        if (hipEventRecord(j->done, st0) != hipSuccess) j->rc = ZHIP_E_HIP;
+        return j;
+    }
     j->pieces.assign(pieces, pieces + n_pieces);
     j->pinned = pinned;
     j->dev = dev;
@@ -292,19 +309,62 @@ zhip_stage_job* zhip_stage_begin(const zhip_piece* pieces, uint32_t n_pieces, ui
     j->window = window;
     j->nthreads = nthreads;
     j->stream = stream;
-    j->th = std::thread([j] {
-        const int r = pack_windows(j->pieces.data(), (uint32_t)j->pieces.size(), j->pinned,
-                                   static_cast<uint8_t*>(j->dev), j->total, j->window, j->nthreads,
-                                   static_cast<hipStream_t>(j->stream));
-        if (r != ZHIP_OK) j->rc = r;
+    uint64_t ticket;
+    {
+        std::lock_guard<std::mutex> g(g_job_mu);
+        ticket = g_job_next++;
+    }
+    j->th = std::thread([j, ticket] {
+        {
+            std::unique_lock<std::mutex> g(g_job_mu);
+            g_job_cv.wait(g, [&] { return g_job_serving == ticket; });
+        }
+        hipStream_t st = static_cast<hipStream_t>(j->stream);
+        int r = j->rc;
+        const int r2 = pack_windows(j->pieces.data(), (uint32_t)j->pieces.size(), j->pinned,
+                                    static_cast<uint8_t*>(j->dev), j->total, j->window, j->nthreads, st);
+        if (r2 != ZHIP_OK) r = r2;
+        // in ticket order: the event covers this job's windows and earlier
+        // jobs' (and pinned copies already enqueued by later begins)
+        if (hipEventRecord(j->done, st) != hipSuccess) r = ZHIP_E_HIP;
+        j->rc = r;
+        {
+            std::lock_guard<std::mutex> g(g_job_mu);
+            ++g_job_serving;
+        }
+        g_job_cv.notify_all();
     });
     return j;
 }
 
-int zhip_stage_end(zhip_stage_job* j) {
+// Events a stream was told to wait for are destroyed only once they have
+// completed (checked at later stage_end calls), never right after the wait.
+static std::mutex g_retire_mu;
+static std::vector<hipEvent_t> g_retire;
+
+static void retire_event(hipEvent_t ev) {
+    std::lock_guard<std::mutex> g(g_retire_mu);
+    g_retire.push_back(ev);
+    size_t k = 0;
+    for (size_t i = 0; i < g_retire.size(); ++i) {
+        if (i + 1 < g_retire.size() && hipEventQuery(g_retire[i]) == hipSuccess)
+            (void)hipEventDestroy(g_retire[i]);
+        else
+            g_retire[k++] = g_retire[i];
+    }
+    g_retire.resize(k);
+}
+
+int zhip_stage_end(zhip_stage_job* j, void* wait_stream) {
     if (!j) return ZHIP_E_INVALID;
     if (j->th.joinable()) j->th.join();
-    const int rc = j->rc;
+    int rc = j->rc;
+    if (j->done) {
+        // (wait_stream NULL is the default stream, which waits like any other)
+        if (rc == ZHIP_OK && hipStreamWaitEvent(static_cast<hipStream_t>(wait_stream), j->done, 0) != hipSuccess)
+            rc = ZHIP_E_HIP;
+        retire_event(j->done);
+    }
     delete j;
     return rc;
 }

@@ -211,7 +211,7 @@ def lib():
     L.zhip_stage_h2d.restype = ctypes.c_int
     L.zhip_stage_begin.argtypes = list(L.zhip_stage_h2d.argtypes)
     L.zhip_stage_begin.restype = ctypes.c_void_p
-    L.zhip_stage_end.argtypes = [ctypes.c_void_p]
+    L.zhip_stage_end.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
     L.zhip_stage_end.restype = ctypes.c_int
     L.zhip_host_pinned.argtypes = [ctypes.c_void_p]
     L.zhip_host_pinned.restype = ctypes.c_int

@@ -200,6 +200,30 @@ class DecodeLaunch:
                                     self.d_status.data_ptr(), self.d_ws.data_ptr(),
                                     self.d_err.data_ptr(), self.flags, s), "zhip_decode")
 
+    def launch_range(self, first: int, count: int, src, src_size: int, stream: int | None = None) -> None:
+        """Chunks [first, first + count) of the table, reading from `src` (the
+        slab pipeline: one plan, one staging buffer per slab).  Statuses and
+        workspace regions are the same slices a whole launch uses.  Plain
+        launches only (no fused index checks, no load prediction)."""
+        if count == 0:
+            return
+        assert self.n_idx == 0 and self.predict is None
+        s = _stream_handle(self.device) if stream is None else stream
+        out_ptr = self.out.data_ptr() if self.out is not None else None
+        wsw = max(4, self.plan.workspace_words)
+        chunks = self.d_chunks.data_ptr() + first * CHUNK_DT.itemsize
+        status = self.d_status.data_ptr() + first * 16
+        ws = self.d_ws.data_ptr() + first * wsw * 4
+        if self.d_rowmap is not None:
+            N.check(N.lib().zhip_decode_mapped(
+                self.plan.handle, src.data_ptr(), src_size, out_ptr, chunks, count, self.d_sels.data_ptr(),
+                status, ws, self.d_err.data_ptr(), None, 0, None, self.flags, None, self.d_rowmap.data_ptr(), s),
+                "zhip_decode_mapped")
+            return
+        N.check(N.lib().zhip_decode(self.plan.handle, src.data_ptr(), src_size, out_ptr, chunks, count,
+                                    self.d_sels.data_ptr(), status, ws, self.d_err.data_ptr(), self.flags, s),
+                "zhip_decode")
+
     def statuses(self) -> np.ndarray:
         return self.d_status[: self.n * 4].cpu().numpy().view(STATUS_DT)
 
@@ -507,6 +531,77 @@ class HipCodecPipeline:
             copy_to_host(dev_out, host_out)
         return res
 
+    def _read_slabs_one_plan(self, batch, groups, dev_out, host_out, direct: bool):
+        """_read_slabs for unsharded chains: the batch is planned ONCE (in slab
+        order), each slab's bytes are staged into its own buffer (every slab's
+        staging job begun at once; the library runs them in order), and each
+        slab is one range launch over the shared tables.  None when the chain is
+        sharded (per-slab prepare_read then)."""
+        torch = _torch()
+        spec: ArraySpec = batch[0][1]
+        if isinstance(self.array_bytes_codec, ShardingCodec):
+            return None
+        chain = analyze_chain(self.codecs, spec)
+        dev = dev_out.device
+        order = [i for _, _, idx in groups for i in idx]
+        staged = []
+        for _, _, idx in groups:
+            src, size, srcs, keep, starter = staging.gather_sources([batch[i] for i in idx], dev, start=False)
+            staged.append([src, size, srcs, keep, starter, None])
+        itemsize = dev_out.element_size()
+        if np.dtype(spec.dtype).itemsize != itemsize:
+            raise TypeError("out dtype itemsize does not match the array dtype")
+
+        def start(g):
+            st = staged[g]
+            if st[0] is None:  # host-sourced: begin its staging job now
+                st[0], keep, st[5] = st[4]()
+                st[3] = keep
+        for g in range(len(groups)):  # the library packs and copies them in this order
+            start(g)
+        items = []
+        for (_, _, idx), st in zip(groups, staged):
+            items += [(o, n, miss, batch[i][2], batch[i][3]) for (o, n, miss), i in zip(st[2], idx)]
+        ostr = [int(x) * itemsize for x in dev_out.stride()]
+        with torch.cuda.device(dev):
+            t = plan_decode(chain, spec, items, ostr, dev_out.data_ptr(), (), None, None)
+            launch = DecodeLaunch(t.layout, t.chunks, t.sels, None, 0, dev_out, t.fast, dev, t.tile, None,
+                                  t.rows, None)
+        compute = torch.cuda.current_stream(dev)
+        d2h = _d2h_stream(dev)
+        nbytes = dev_out.numel() * dev_out.element_size()
+        bounce = None if direct else torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+        first = 0
+        for g, ((a, b, idx), st) in enumerate(zip(groups, staged)):
+            if st[5] is not None:
+                st[5].finish()  # the launch stream waits for this slab's copies
+            launch.launch_range(first, len(idx), st[0], st[1])
+            first += len(idx)
+            ev = torch.cuda.Event()
+            ev.record(compute)
+            d2h.wait_event(ev)
+            with torch.cuda.stream(d2h):
+                if direct:
+                    _d2h(dev_out, host_out, a, b)
+                else:
+                    flat = dev_out.reshape(-1).view(torch.uint8)
+                    bounce[a:b].copy_(flat[a:b], non_blocking=True)
+        prog = DecodeProgram(t, launch, None, len(items), False,
+                             np.array([m for st in staged for (_, _, m) in st[2]], bool),
+                             keepalive=[st[0] for st in staged] + [k for st in staged for k in st[3]])
+        try:
+            res = prog.results()
+        finally:
+            d2h.synchronize()
+        if not direct:
+            from .buffer import copy_to_host_from_pinned
+
+            copy_to_host_from_pinned(bounce, host_out)
+        out = [None] * len(batch)
+        for j, i in enumerate(order):
+            out[i] = res[j]
+        return tuple(out)
+
     def _read_slabs(self, batch, groups, dev_out, host_out, direct: bool) -> tuple[GetResult, ...]:
         """A host-sourced read into a host out, pipelined over row slabs of
         out: slab k's chunks decode on the compute stream while slab k+1's
@@ -514,6 +609,9 @@ class HipCodecPipeline:
         back on a D2H stream meanwhile -- H2D, decode and D2H overlap (PCIe
         is full duplex).  The result is what one whole-batch read gives:
         slabs are disjoint, every chunk lands in exactly one."""
+        r = self._read_slabs_one_plan(batch, groups, dev_out, host_out, direct)
+        if r is not None:
+            return r
         torch = _torch()
         dev = dev_out.device
         compute = torch.cuda.current_stream(dev)

@@ -108,14 +108,18 @@ class Pending:
 
         from . import _native as N
 
-        rc = N.lib().zhip_stage_end(self._job)
-        self._job = None
-        N.check(rc, "zhip_stage_h2d")
         st = torch.cuda.current_stream(self.dev.device) if stream is None else \
             torch.cuda.ExternalStream(stream, device=self.dev.device)
-        st.wait_stream(self._cs)  # every window's copy was enqueued on cs before this
-        for fn in self._post:
-            fn(self.dev)
+        # the launch stream waits for this job's copies (an event the library
+        # recorded after its last one), not for later jobs already queued on
+        # cs; handle 0 is the default stream and waits like any other
+        rc = N.lib().zhip_stage_end(self._job, int(st.cuda_stream))
+        self._job = None
+        N.check(rc, "zhip_stage_h2d")
+        if self._post:
+            with torch.cuda.stream(st):
+                for fn in self._post:
+                    fn(self.dev)
         self._post = []
 
 
@@ -165,12 +169,15 @@ def stage(layout: StagingLayout, device, post=(), defer: bool = False):
     return dev, [dev, host, views], pending
 
 
-def gather_sources(batch: list, device, defer: bool = False):
+def gather_sources(batch: list, device, defer: bool = False, start: bool = True):
     """Resolve every ByteGetter to (offset, length, missing) inside ONE device
     buffer: the shared arena for DeviceStore batches, else a staged copy.
     ByteGetters may be this package's or zarr's (whose get_sync returns a
     Buffer, src/zarr/storage/_common.py:247-258).
-    Returns (src, size, [(off, len, missing)], keepalive, pending | None)."""
+    Returns (src, size, [(off, len, missing)], keepalive, pending | None).
+    With start=False a host-sourced batch is laid out but not staged yet:
+    src is None and the last element is a callable that starts the staging
+    (deferred) and returns (src, keepalive, pending)."""
     import torch
 
     raws = []
@@ -211,6 +218,8 @@ def gather_sources(batch: list, device, defer: bool = False):
             v = r.arena.view(r.offset, r.length) if isinstance(r, DeviceRef) else r
             dev[off: off + v.numel()].copy_(v)
 
+    if not start:
+        return None, lay.top, srcs, [], lambda: stage(lay, device, post=[d2d] if dev_refs else [], defer=True)
     dev, keep, pending = stage(lay, device, post=[d2d] if dev_refs else [], defer=defer)
     return dev, lay.top, srcs, keep, pending
 
