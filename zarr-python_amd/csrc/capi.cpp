@@ -649,7 +649,7 @@ int zhip_decode_mapped(const zhip_plan* plan, const void* src, uint64_t src_size
         p.kthread = plan->d_tile_tables + 4096;
         p.kunit = plan->d_tile_tables + 4096 + kThreads;
         p.c_inv = plan->t_c_inv;
-        p.tile4 = plan->tile4 && !(g_tune_bits & kTuneTile1);
+        p.tile4 = plan->tile4 && !(g_tune_bits & (kTuneTile1 | kTuneNoTile4));
         if (p.tile4) {
             p.tz = plan->d_tile_tables + plan->tile4_off_tz;
             p.kq4 = plan->d_tile_tables + plan->tile4_off_kq;
@@ -728,7 +728,7 @@ int zhip_encode_mapped(const zhip_plan* plan, const void* arr, void* dst, const 
     p.rowmap = nullptr;
     p.tile4 = 0;
     if ((encode_flags & ZHIP_DF_TILE) && plan->tile4 && plan->t_per_chunk <= 64 && plan->d_tile_tables &&
-        !(g_tune_bits & kTuneTile1)) {
+        !(g_tune_bits & (kTuneTile1 | kTuneNoTile4))) {
         // transposed chunks, full tiles, at most 16 workgroups per chunk (the
         // arrival / non-empty bits of one 64-bit word): k_encode_tile4
         p.tile4 = 1;
