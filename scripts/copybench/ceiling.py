@@ -3,7 +3,8 @@
 -> S bytes, timed as a hipGraph of R launches rotating over buffers (so the
 Infinity Cache cannot serve re-reads and launch gaps are excluded), for the
 headline's 64 MiB and C4's 4 GiB.  Non-persistent (one span per workgroup)
-and persistent grid-stride arms.  One JSON line per arm."""
+and persistent grid-stride arms, each under
+the default and nontemporal cache policies; torch's own D2D copy.  One JSON line per arm."""
 import ctypes
 import json
 import os
@@ -25,17 +26,24 @@ def main():
         n = size_mb << 20
         srcs = [torch.empty(n, dtype=torch.uint8, device=dev).fill_(7) for _ in range(R)]
         dsts = [torch.empty(n, dtype=torch.uint8, device=dev) for _ in range(R)]
-        arms = [("span", s, k) for s in (32 << 10, 64 << 10) for k in (4, 8)] + \
-               [("persist", g, k) for g in (1024, 2048, 4096) for k in (4, 8)]
-        for kind, a, K in arms:
+        # nt: 0 default policy, 1 nontemporal loads+stores, 2 loads only, 3 stores only
+        arms = [("span", s, s // 4096, nt) for s in (4 << 10, 8 << 10, 16 << 10, 32 << 10)
+                for nt in (0, 1, 2, 3)] + \
+               [("span", 64 << 10, 8, 1)] + \
+               [("persist", g, k, nt) for g in (1024, 2048) for k in (4, 8) for nt in (0, 1)] + \
+               [("torch", 0, 0, 0)]
+        for kind, a, K, nt in arms:
             stream = torch.cuda.Stream(dev)
 
             def launch(i):
                 sh = ctypes.c_void_p(int(torch.cuda.current_stream(dev).cuda_stream))
                 if kind == "span":
-                    rc = lib.cb_copy(srcs[i % R].data_ptr(), dsts[i % R].data_ptr(), n, a, K, 1, 1, sh)
+                    rc = lib.cb_copy(srcs[i % R].data_ptr(), dsts[i % R].data_ptr(), n, a, K, 1, nt, sh)
+                elif kind == "persist":
+                    rc = lib.cb_copy_persist(srcs[i % R].data_ptr(), dsts[i % R].data_ptr(), n, a, K, nt, sh)
                 else:
-                    rc = lib.cb_copy_persist(srcs[i % R].data_ptr(), dsts[i % R].data_ptr(), n, a, K, 1, sh)
+                    dsts[i % R].copy_(srcs[i % R])
+                    rc = 0
                 assert rc == 0
 
             g = torch.cuda.CUDAGraph()
@@ -53,7 +61,7 @@ def main():
                 torch.cuda.synchronize()
                 ts.append(e0.elapsed_time(e1) / reps * 1e3)
             us = min(ts)
-            print(json.dumps({"size_MiB": size_mb, "arm": kind, "span_or_grid": a, "K": K,
+            print(json.dumps({"size_MiB": size_mb, "arm": kind, "span_or_grid": a, "K": K, "nt": nt,
                               "us_per_copy": round(us, 2), "TBps": round(2 * n / us / 1e6, 3),
                               "frac_of_8TBps": round(2 * n / us / 1e6 / 8.0, 3)}), flush=True)
         del srcs, dsts

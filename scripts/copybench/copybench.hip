@@ -6,7 +6,7 @@
 
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 
-template <int K, bool STORE, bool NT>
+template <int K, bool STORE, bool NTL, bool NTS = NTL>
 __global__ __launch_bounds__(256) void k_copy(const uint4* __restrict__ src, uint4* __restrict__ dst,
                                               uint64_t n16, uint32_t span16) {
     const uint64_t b0 = (uint64_t)blockIdx.x * span16;
@@ -19,7 +19,7 @@ __global__ __launch_bounds__(256) void k_copy(const uint4* __restrict__ src, uin
         for (int k = 0; k < K; ++k) {
             const uint64_t i = b + 256ull * k;
             if (i < b1) {
-                if constexpr (NT) {
+                if constexpr (NTL) {
                     const v4u w = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(src) + i);
                     v[k] = make_uint4(w.x, w.y, w.z, w.w);
                 } else v[k] = src[i];
@@ -30,7 +30,7 @@ __global__ __launch_bounds__(256) void k_copy(const uint4* __restrict__ src, uin
             const uint64_t i = b + 256ull * k;
             if constexpr (STORE) {
                 if (i < b1) {
-                    if constexpr (NT) {
+                    if constexpr (NTS) {
                         v4u w = {v[k].x, v[k].y, v[k].z, v[k].w};
                         __builtin_nontemporal_store(w, reinterpret_cast<v4u*>(dst) + i);
                     } else dst[i] = v[k];
@@ -49,9 +49,15 @@ extern "C" int cb_copy(const void* src, void* dst, uint64_t nbytes, uint32_t spa
     const uint32_t span16 = span / 16;
     const uint32_t grid = (uint32_t)((n16 + span16 - 1) / span16);
     Fn fn = nullptr;
+// nt: 0 = default policy, 1 = nontemporal loads and stores, 2 = nontemporal
+// loads only, 3 = nontemporal stores only.
 #define SEL(KK)                                                                                   \
-    if (K == KK) fn = store ? (nt ? (Fn)k_copy<KK, true, true> : (Fn)k_copy<KK, true, false>)     \
-                            : (nt ? (Fn)k_copy<KK, false, true> : (Fn)k_copy<KK, false, false>);
+    if (K == KK)                                                                                  \
+        fn = store ? (nt == 1   ? (Fn)k_copy<KK, true, true, true>                                \
+                      : nt == 2 ? (Fn)k_copy<KK, true, true, false>                               \
+                      : nt == 3 ? (Fn)k_copy<KK, true, false, true>                               \
+                                : (Fn)k_copy<KK, true, false, false>)                             \
+                   : (nt ? (Fn)k_copy<KK, false, true> : (Fn)k_copy<KK, false, false>);
     SEL(1) SEL(2) SEL(4) SEL(8) SEL(16)
     if (!fn) return -1;
     hipLaunchKernelGGL(fn, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const uint4*)src, (uint4*)dst, n16,
@@ -108,7 +114,7 @@ extern "C" int cb_copy_persist(const void* src, void* dst, uint64_t nbytes, uint
 // 256^3 f32 out (row stride 1 KiB).  Each workgroup copies `units` consecutive
 // 32 KiB units, every thread 8 x 16 bytes per unit (unaligned nt loads).
 typedef unsigned int v4u_a1 __attribute__((ext_vector_type(4), aligned(1)));
-template <int UNITS>
+template <int UNITS, bool NTL = true>
 __global__ __launch_bounds__(256) void k_scatter(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                                                  uint64_t cstride) {
     const int t = threadIdx.x;
@@ -120,7 +126,8 @@ __global__ __launch_bounds__(256) void k_scatter(const uint8_t* __restrict__ src
         const uint8_t* cp = src + (uint64_t)c * cstride + (uint64_t)s * 32768;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            const v4u_a1 w = __builtin_nontemporal_load(reinterpret_cast<const v4u_a1*>(cp + 4096 * k + 16 * t));
+            const v4u_a1 w = NTL ? __builtin_nontemporal_load(reinterpret_cast<const v4u_a1*>(cp + 4096 * k + 16 * t))
+                                 : *reinterpret_cast<const v4u_a1*>(cp + 4096 * k + 16 * t);
             v[u][k] = make_uint4(w.x, w.y, w.z, w.w);
         }
     }
@@ -142,7 +149,10 @@ __global__ __launch_bounds__(256) void k_scatter(const uint8_t* __restrict__ src
 
 extern "C" int cb_scatter(const void* src, void* dst, uint64_t cstride, int units, void* stream) {
     const uint32_t n_units = 64 * 32;
-    if (units == 1)
+    if (units == 12)  // two units per workgroup, default-policy loads
+        hipLaunchKernelGGL((k_scatter<2, false>), dim3(n_units / 2), dim3(256), 0, (hipStream_t)stream,
+                           (const uint8_t*)src, (uint8_t*)dst, cstride);
+    else if (units == 1)
         hipLaunchKernelGGL(k_scatter<1>, dim3(n_units), dim3(256), 0, (hipStream_t)stream, (const uint8_t*)src,
                            (uint8_t*)dst, cstride);
     else if (units == 2)

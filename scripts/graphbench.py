@@ -76,12 +76,15 @@ def main():
         arms["nocrc_twin"] = graph_of(lambda i, sh: nocrc[i % R][0].launch(sh))
     arms["copy_32k"] = graph_of(lambda i, sh: cb.cb_copy(srcs[i % Rc].data_ptr(), dsts[i % Rc].data_ptr(), n,
                                                          32 << 10, 8, 1, 1, ctypes.c_void_p(sh)))
+    # default-policy loads, nontemporal stores (the better copy policy at 64 MiB)
+    arms["copy_8k_ldef"] = graph_of(lambda i, sh: cb.cb_copy(srcs[i % Rc].data_ptr(), dsts[i % Rc].data_ptr(), n,
+                                                             8 << 10, 2, 1, 3, ctypes.c_void_p(sh)))
     # the headline's access pattern without codec work (scripts/copybench k_scatter)
     cb.cb_scatter.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p]
     ssrc = [torch.empty(64 * 1048580 + 64, dtype=torch.uint8, device=dev).fill_(5) for _ in range(R)] \
         if cfg == "headline" else []
     for cs, nm in (((1048576, "al"), (1048580, "mis")) if cfg == "headline" else ()):
-        for u in (1, 2):
+        for u in (1, 2, 12):
             arms[f"scatter_{nm}_u{u}"] = graph_of(
                 lambda i, sh, cs=cs, u=u: cb.cb_scatter(ssrc[i % R].data_ptr(), dsts[i % R].data_ptr(), cs, u,
                                                         ctypes.c_void_p(sh)))
@@ -104,7 +107,7 @@ def main():
     if not torch.equal(crc[0][1].view(torch.int32), data.view(torch.int32)):
         raise SystemExit("graphbench: production decode output differs")
     for k, v in res.items():
-        byt = 2 * n if (k == "copy_32k" or k.startswith("scatter")) else alg
+        byt = 2 * n if (k.startswith("copy") or k.startswith("scatter")) else alg
         print(json.dumps({"arm": k, "us_min": round(min(v), 2), "us_med": round(float(np.median(v)), 2),
                           "hbm_frac_min": round(byt / (min(v) * 1e-6) / 8e12, 4)}), flush=True)
 

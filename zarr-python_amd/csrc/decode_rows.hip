@@ -9,7 +9,8 @@
 // run, so the out address of thread t's block is
 //     base(R_k)  (wave-uniform, scalar ALU)  +  lane_off(t)  (per lane, once)
 // and the per-block selection test is one compare on the dim-(ndim-2)
-// coordinate.  Loads and stores are nontemporal (every byte is touched once).
+// coordinate.  Stores are nontemporal (every byte is touched once); loads take
+// the default policy (kNtLoads: measured faster).
 //
 // Reference behaviour restated: Crc32cCodec._decode_sync (crc32c_.py:34-50),
 // BytesCodec._decode_sync (bytes.py:97-131), scatter_chunk /
@@ -43,7 +44,13 @@ __device__ __forceinline__ uint32_t load_u32_any(const uint8_t* a) {  // any ali
     return *(zhip_gu32_a1*)(reinterpret_cast<uintptr_t>(a));
 }
 
-__device__ __forceinline__ uint4 load_nt16_any(const uint8_t* a) {  // any alignment, one global dwordx4 nt
+__device__ __forceinline__ uint4 load16_any(const uint8_t* a) {  // any alignment, one global dwordx4, default policy
+    const zhip_v4u_a1 w = *(zhip_gv4u_a1*)(reinterpret_cast<uintptr_t>(a));
+    return make_uint4(w.x, w.y, w.z, w.w);
+}
+
+__device__ __forceinline__ uint4 load_stream16_any(const uint8_t* a) {  // any alignment, one global dwordx4 (kNtLoads)
+    if constexpr (!kNtLoads) return load16_any(a);
     const zhip_v4u_a1 w = __builtin_nontemporal_load((zhip_gv4u_a1*)(reinterpret_cast<uintptr_t>(a)));
     return make_uint4(w.x, w.y, w.z, w.w);
 }
@@ -77,7 +84,7 @@ __device__ __forceinline__ void load_unit_rows(const Unit& U, bool live, int t, 
         // dummy loads: every lane reads the same 16 zero bytes (one cache line
         // per wave instruction, no traffic to speak of)
         const int32_t base = U.seg_lo + kWgStride * k;
-        blk[k] = load_nt16_any(ok && base >= 0 ? U.cp + base + 16 * t : zero);
+        blk[k] = load_stream16_any(ok && base >= 0 ? U.cp + base + 16 * t : zero);
     }
 }
 

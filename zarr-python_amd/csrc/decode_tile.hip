@@ -37,8 +37,10 @@ __device__ uint4 g_tile_sink[kThreads];     // dummy-store target
 typedef unsigned int zhip_v4u_a1t __attribute__((ext_vector_type(4), aligned(1)));
 typedef __attribute__((address_space(1))) const zhip_v4u_a1t zhip_gv4u_a1t;
 
-__device__ __forceinline__ uint4 load_nt16_a1(const uint8_t* a) {  // any alignment, one dwordx4 nt
-    const zhip_v4u_a1t w = __builtin_nontemporal_load((zhip_gv4u_a1t*)(reinterpret_cast<uintptr_t>(a)));
+__device__ __forceinline__ uint4 load_stream16_a1(const uint8_t* a) {  // any alignment, one dwordx4 (kNtLoads)
+    zhip_v4u_a1t w;
+    if constexpr (kNtLoads) w = __builtin_nontemporal_load((zhip_gv4u_a1t*)(reinterpret_cast<uintptr_t>(a)));
+    else w = *(zhip_gv4u_a1t*)(reinterpret_cast<uintptr_t>(a));
     return make_uint4(w.x, w.y, w.z, w.w);
 }
 
@@ -119,7 +121,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     for (int j = 0; j < kTiles; ++j)
 #pragma unroll
         for (int k = 0; k < kPasses; ++k)
-            blk[j][k] = load_nt16_a1(ok ? U.cp + tm.e[j].tbase + (row0 + 16u * k) * sq + col : zero);
+            blk[j][k] = load_stream16_a1(ok ? U.cp + tm.e[j].tbase + (row0 + 16u * k) * sq + col : zero);
     uint32_t stored = 0;
     if (CRC && ok) stored = load_trailer_uniform(U.cp, p.g.nbytes);
     if constexpr (CRC) {
@@ -336,7 +338,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
 #pragma unroll
         for (int k = 0; k < kPasses; ++k) {
             const uint32_t row = row0 + 16u * k;
-            blk[j][k] = load_nt16_a1(ok && lane_in && (int32_t)row < rows
+            blk[j][k] = load_stream16_a1(ok && lane_in && (int32_t)row < rows
                                          ? U.cp + ge.tbase + (size_t)j * p.g_step_t + row * sq + col
                                          : zero);
         }
@@ -509,7 +511,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
             const uint32_t pc = (uint32_t)(k * kThreads + t);
             const uint32_t jc = pc / kPiecesPerCol;
             const uint32_t r0 = (pc % kPiecesPerCol) * kPer;
-            pcs[j][k] = load_nt16_a1(abase + tm.e[j].orel + (int64_t)jc * ocol + (int64_t)r0 * oq);
+            pcs[j][k] = load_stream16_a1(abase + tm.e[j].orel + (int64_t)jc * ocol + (int64_t)r0 * oq);
         }
     if constexpr (CRC) {
         uint4* st = reinterpret_cast<uint4*>(s_tab);
@@ -715,7 +717,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
             const int32_t r0 = (pc % kPiecesPerCol) * kPer;
             const bool whole = (uint32_t)j < nt && jc < geo[j].cols_sel && r0 + kPer <= geo[j].rows_sel;
             wmask |= whole ? 1u << (j * kPasses + k) : 0u;
-            pcs[j][k] = load_nt16_a1(whole ? abase + geo[j].aoff + (int64_t)jc * ocol + (int64_t)r0 * oq : zero);
+            pcs[j][k] = load_stream16_a1(whole ? abase + geo[j].aoff + (int64_t)jc * ocol + (int64_t)r0 * oq : zero);
         }
     if constexpr (CRC) {
         uint4* st = reinterpret_cast<uint4*>(s_tab);
@@ -892,7 +894,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
             const int32_t jc = pc / kPiecesPerCol;
             const int32_t r0 = (pc % kPiecesPerCol) * kPer;
             const bool in = jc * ITEM < cols && r0 < rows;  // rows % kPer == 0 (zhip_encode_mapped)
-            pcs[j][k] = load_nt16_a1(in ? abase + (int64_t)j * p.g_step_o + (int64_t)jc * ocol + (int64_t)r0 * oq
+            pcs[j][k] = load_stream16_a1(in ? abase + (int64_t)j * p.g_step_o + (int64_t)jc * ocol + (int64_t)r0 * oq
                                         : zero);
         }
     if constexpr (CRC) {

@@ -244,8 +244,10 @@ typedef unsigned int zhip_v4u_ae __attribute__((ext_vector_type(4), aligned(1)))
 typedef __attribute__((address_space(1))) const zhip_v4u_ae zhip_gv4u_ae;
 typedef __attribute__((address_space(1))) zhip_v4u_ae zhip_gv4u_aew;
 
-__device__ __forceinline__ uint4 enc_load16(const uint8_t* a) {  // any alignment, one dwordx4 nt
-    const zhip_v4u_ae w = __builtin_nontemporal_load((zhip_gv4u_ae*)(reinterpret_cast<uintptr_t>(a)));
+__device__ __forceinline__ uint4 enc_load16(const uint8_t* a) {  // any alignment, one dwordx4 (kNtLoads)
+    zhip_v4u_ae w;
+    if constexpr (kNtLoads) w = __builtin_nontemporal_load((zhip_gv4u_ae*)(reinterpret_cast<uintptr_t>(a)));
+    else w = *(zhip_gv4u_ae*)(reinterpret_cast<uintptr_t>(a));
     return make_uint4(w.x, w.y, w.z, w.w);
 }
 

@@ -68,10 +68,21 @@ __device__ __forceinline__ uint4 load_block(const uint8_t* cp, int32_t o, uint32
 
 typedef unsigned int zhip_v4u __attribute__((ext_vector_type(4)));
 
-// Streaming (nontemporal) 16-byte load / store: the decode touches every
-// encoded and decoded byte exactly once.
-__device__ __forceinline__ uint4 load_nt16(const uint8_t* p) {
-    const zhip_v4u w = __builtin_nontemporal_load(reinterpret_cast<const zhip_v4u*>(p));
+// Cache policy of the streaming 16-byte loads of every kernel.  Default
+// policy: measured 9-13 % faster than nontemporal loads on the headline, up to
+// 50 % on C1, 14-18 % on the encodes (profiles/r02/load_policy_ab.jsonl);
+// nontemporal stays a build-time measurement switch (EXTRA=-DZHIP_NT_LOADS=1).
+#ifndef ZHIP_NT_LOADS
+#define ZHIP_NT_LOADS 0
+#endif
+constexpr bool kNtLoads = ZHIP_NT_LOADS != 0;
+
+// Streaming 16-byte load / store: the decode touches every encoded and
+// decoded byte exactly once (stores nontemporal; loads per kNtLoads).
+__device__ __forceinline__ uint4 load_stream16(const uint8_t* p) {
+    zhip_v4u w;
+    if constexpr (kNtLoads) w = __builtin_nontemporal_load(reinterpret_cast<const zhip_v4u*>(p));
+    else w = *reinterpret_cast<const zhip_v4u*>(p);
     return make_uint4(w.x, w.y, w.z, w.w);
 }
 
@@ -84,7 +95,7 @@ template <bool AL4, bool NT>
 __device__ __forceinline__ uint4 load_block_t(const uint8_t* cp, int32_t o, uint32_t n) {
     if constexpr (AL4 && NT) {
         if (o < 0 || (uint32_t)o >= n) return make_uint4(0, 0, 0, 0);
-        return mask_tail(load_nt16(cp + o), o, n);
+        return mask_tail(load_stream16(cp + o), o, n);
     } else {
         return load_block<AL4>(cp, o, n);
     }

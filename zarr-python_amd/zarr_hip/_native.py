@@ -49,7 +49,8 @@ PF_INDEX_CRC = 2
 PF_KEEP_EMPTY = 4
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "libzarrhip.so")
+# ZHIP_LIB: an alternative build of the same library (measurement variants)
+LIB_PATH = os.environ.get("ZHIP_LIB") or os.path.join(_HERE, "_lib", "libzarrhip.so")
 
 
 class FDiv(ctypes.Structure):
