@@ -19,6 +19,8 @@ def main():
     lib = ctypes.CDLL(os.path.join(HERE, "libcopybench.so"))
     lib.cb_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
                             ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    lib.cb_copy_rot.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
+                                ctypes.c_void_p]
     lib.cb_copy_persist.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
                                     ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
     dev = torch.device("cuda:0")
@@ -27,11 +29,15 @@ def main():
         srcs = [torch.empty(n, dtype=torch.uint8, device=dev).fill_(7) for _ in range(R)]
         dsts = [torch.empty(n, dtype=torch.uint8, device=dev) for _ in range(R)]
         # nt: 0 default policy, 1 nontemporal loads+stores, 2 loads only, 3 stores only
-        arms = [("span", s, s // 4096, nt) for s in (4 << 10, 8 << 10, 16 << 10, 32 << 10)
-                for nt in (0, 1, 2, 3)] + \
-               [("span", 64 << 10, 8, 1)] + \
-               [("persist", g, k, nt) for g in (1024, 2048) for k in (4, 8) for nt in (0, 1)] + \
-               [("torch", 0, 0, 0)]
+        if os.environ.get("ROT"):  # spans with and without the rotated step order
+            arms = [(kind, s, s // 4096, nt) for s in (32 << 10, 64 << 10) for nt in (1, 3)
+                    for kind in ("span", "rot")] + [("span", 4 << 10, 1, 1)]
+        else:
+            arms = [("span", s, s // 4096, nt) for s in (4 << 10, 8 << 10, 16 << 10, 32 << 10)
+                    for nt in (0, 1, 2, 3)] + \
+                   [("span", 64 << 10, 8, 1)] + \
+                   [("persist", g, k, nt) for g in (1024, 2048) for k in (4, 8) for nt in (0, 1)] + \
+                   [("torch", 0, 0, 0)]
         for kind, a, K, nt in arms:
             stream = torch.cuda.Stream(dev)
 
@@ -39,6 +45,8 @@ def main():
                 sh = ctypes.c_void_p(int(torch.cuda.current_stream(dev).cuda_stream))
                 if kind == "span":
                     rc = lib.cb_copy(srcs[i % R].data_ptr(), dsts[i % R].data_ptr(), n, a, K, 1, nt, sh)
+                elif kind == "rot":
+                    rc = lib.cb_copy_rot(srcs[i % R].data_ptr(), dsts[i % R].data_ptr(), n, K, nt, sh)
                 elif kind == "persist":
                     rc = lib.cb_copy_persist(srcs[i % R].data_ptr(), dsts[i % R].data_ptr(), n, a, K, nt, sh)
                 else:

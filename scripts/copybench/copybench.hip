@@ -65,6 +65,47 @@ extern "C" int cb_copy(const void* src, void* dst, uint64_t nbytes, uint32_t spa
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
+// Span copy with a per-workgroup rotation of the 4 KiB step order: workgroup
+// g visits steps (k + g) % K, so workgroups running in lockstep are at
+// different offsets of their spans (the decode kernels' unit = 8 such steps).
+template <int K, bool NTL, bool NTS>
+__global__ __launch_bounds__(256) void k_copy_rot(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                  uint64_t n16) {
+    const uint64_t b0 = (uint64_t)blockIdx.x * 256ull * K;
+    uint4 v[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint64_t i = b0 + 256ull * ((k + blockIdx.x) % K) + threadIdx.x;
+        if constexpr (NTL) {
+            const v4u w = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(src) + i);
+            v[k] = make_uint4(w.x, w.y, w.z, w.w);
+        } else v[k] = src[i];
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint64_t i = b0 + 256ull * ((k + blockIdx.x) % K) + threadIdx.x;
+        if constexpr (NTS) {
+            v4u w = {v[k].x, v[k].y, v[k].z, v[k].w};
+            __builtin_nontemporal_store(w, reinterpret_cast<v4u*>(dst) + i);
+        } else dst[i] = v[k];
+    }
+}
+
+extern "C" int cb_copy_rot(const void* src, void* dst, uint64_t nbytes, int K, int nt, void* stream) {
+    typedef void (*RFn)(const uint4*, uint4*, uint64_t);
+    RFn fn = nullptr;
+#define RSEL(KK)                                                                                  \
+    if (K == KK) fn = nt == 1 ? (RFn)k_copy_rot<KK, true, true> : nt == 3 ? (RFn)k_copy_rot<KK, false, true> \
+                                                                : (RFn)k_copy_rot<KK, false, false>;
+    RSEL(8) RSEL(16)
+    if (!fn) return -1;
+    const uint64_t per = 4096ull * K;
+    if (nbytes % per) return -3;
+    hipLaunchKernelGGL(fn, dim3((uint32_t)(nbytes / per)), dim3(256), 0, (hipStream_t)stream, (const uint4*)src,
+                       (uint4*)dst, nbytes / 16);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
 // Persistent grid-stride copy: `grid` workgroups, each walking 16-byte blocks
 // b = (g * 256 + t) + k * 256 * grid, K blocks in flight per thread.
 template <int K, bool NT>
@@ -114,10 +155,16 @@ extern "C" int cb_copy_persist(const void* src, void* dst, uint64_t nbytes, uint
 // 256^3 f32 out (row stride 1 KiB).  Each workgroup copies `units` consecutive
 // 32 KiB units, every thread 8 x 16 bytes per unit (unaligned nt loads).
 typedef unsigned int v4u_a1 __attribute__((ext_vector_type(4), aligned(1)));
-template <int UNITS, bool NTL = true>
+template <int UNITS, bool NTL = true, int LDS_WORDS = 0>
 __global__ __launch_bounds__(256) void k_scatter(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                                                  uint64_t cstride) {
     const int t = threadIdx.x;
+    // LDS_WORDS > 0: reserve the decode kernel's LDS footprint (residency arm)
+    __shared__ uint32_t s_pad[LDS_WORDS > 0 ? LDS_WORDS : 1];
+    if constexpr (LDS_WORDS > 0) {
+        s_pad[t] = t;
+        if (t == 0 && cstride == 0) dst[0] = (uint8_t)s_pad[255];
+    }
     uint4 v[UNITS][8];
 #pragma unroll
     for (int u = 0; u < UNITS; ++u) {
@@ -149,7 +196,13 @@ __global__ __launch_bounds__(256) void k_scatter(const uint8_t* __restrict__ src
 
 extern "C" int cb_scatter(const void* src, void* dst, uint64_t cstride, int units, void* stream) {
     const uint32_t n_units = 64 * 32;
-    if (units == 12)  // two units per workgroup, default-policy loads
+    if (units == 11)  // one unit per workgroup, default-policy loads
+        hipLaunchKernelGGL((k_scatter<1, false>), dim3(n_units), dim3(256), 0, (hipStream_t)stream,
+                           (const uint8_t*)src, (uint8_t*)dst, cstride);
+    else if (units == 22)  // two units, default-policy loads, 36 KiB of LDS reserved (4 workgroups per CU)
+        hipLaunchKernelGGL((k_scatter<2, false, 9216>), dim3(n_units / 2), dim3(256), 0, (hipStream_t)stream,
+                           (const uint8_t*)src, (uint8_t*)dst, cstride);
+    else if (units == 12)  // two units per workgroup, default-policy loads
         hipLaunchKernelGGL((k_scatter<2, false>), dim3(n_units / 2), dim3(256), 0, (hipStream_t)stream,
                            (const uint8_t*)src, (uint8_t*)dst, cstride);
     else if (units == 1)

@@ -84,7 +84,7 @@ def main():
     ssrc = [torch.empty(64 * 1048580 + 64, dtype=torch.uint8, device=dev).fill_(5) for _ in range(R)] \
         if cfg == "headline" else []
     for cs, nm in (((1048576, "al"), (1048580, "mis")) if cfg == "headline" else ()):
-        for u in (1, 2, 12):
+        for u in (1, 2, 11, 12, 22):
             arms[f"scatter_{nm}_u{u}"] = graph_of(
                 lambda i, sh, cs=cs, u=u: cb.cb_scatter(ssrc[i % R].data_ptr(), dsts[i % R].data_ptr(), cs, u,
                                                         ctypes.c_void_p(sh)))

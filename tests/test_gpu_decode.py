@@ -98,11 +98,13 @@ def test_1d_row_decode(device, shape, chunks, dtype, codecs, sel):
     assert prog.tables.rows and prog.tables.layout.ndim == 2
 
 
-@pytest.mark.parametrize("tune", [64, 65536 | 64])
+@pytest.mark.parametrize("tune", [64, 65536 | 64, 128, 2097152])
 def test_rows_fallback_kernels(device, tune):
     """Whole-row batches without a row map (zhip_decode_predicted, or a map the
     library declines) take the persistent k_decode_rows; transposed layouts can
-    be forced onto the one-tile k_decode_tile.  Both stay exact."""
+    be forced onto the one-tile k_decode_tile; whole-row batches with a row map
+    can be forced onto one unit per workgroup (128) or k_decode_duo (2097152,
+    the kernel chunks of > 32 units take by default).  All stay exact."""
     from zarr_hip import _native as N
 
     N.lib().zhip_set_tuning(2, tune)
@@ -113,6 +115,57 @@ def test_rows_fallback_kernels(device, tune):
         _roundtrip(device, (128, 128, 128), (64, 64, 64), "float32", [T((2, 1, 0)), LE, CRC])
     finally:
         N.lib().zhip_set_tuning(2, 0)
+
+
+@pytest.mark.parametrize("case", ["missing", "partial", "sharded_missing_inner", "odd_units", "big_endian"])
+def test_duo_kernel_cases(device, case):
+    """k_decode_duo forced on whole-row layouts it does not take by default
+    (chunks of <= 32 units): absent chunks -> fill, partial row selections,
+    shard-index checks with absent inner chunks, an odd unit count (the last
+    workgroup's second half idle), big-endian items.  Compared byte for byte
+    with the oracle."""
+    from zarr_hip import _native as N
+
+    N.lib().zhip_set_tuning(2, 2097152)
+    try:
+        if case == "missing":
+            _roundtrip(device, (128, 128, 128), (64, 64, 64), "float32", [LE, CRC], fill=7,
+                       drop=["c/0/1/0", "c/1/1/1"])
+        elif case == "partial":
+            _roundtrip(device, (128, 128, 128), (64, 64, 64), "float32", [LE, CRC],
+                       selection=(slice(3, 120), slice(16, 112), slice(None)))
+        elif case == "sharded_missing_inner":
+            _roundtrip(device, (128, 128, 64), (64, 64, 64), "float32",
+                       [SHARD((32, 32, 64), [LE, CRC])], fill=3, drop=["c/1/0/0"])
+        elif case == "odd_units":
+            # 3 chunks of 32 KiB rows: 3 units -> 2 workgroups, one half idle
+            _roundtrip(device, (96, 256), (32, 256), "float32", [LE, CRC])
+        else:
+            _roundtrip(device, (128, 64, 64), (64, 64, 64), "int16", [BE, CRC])
+    finally:
+        N.lib().zhip_set_tuning(2, 0)
+
+
+def test_duo_crc_mismatch(device):
+    """A corrupted chunk of > 32 units (the duo kernel by default) raises the
+    reference's message."""
+    import zarr_hip
+
+    meta = O.ArrayMeta((1024, 1024), (512, 1024), np.dtype("float32"), 0.0, codecs=[LE, CRC])
+    host = {}
+    O.write(host, meta, (Ellipsis,), _data((1024, 1024), "float32"))
+    bad = bytearray(host["c/1/0"])
+    bad[123457] ^= 0x08
+    host["c/1/0"] = bytes(bad)
+    with pytest.raises(ValueError) as want:
+        O.read(host, meta)
+    store = zarr_hip.DeviceStore.from_host(host, device)
+    arr = zarr_hip.Array.create(store, (1024, 1024), (512, 1024), "float32", 0.0, codecs=[LE, CRC])
+    prog, _ = arr.prepare_read((Ellipsis,))
+    assert prog.tables.rows
+    with pytest.raises(ValueError) as got:
+        arr[...]
+    assert str(got.value) == str(want.value)
 
 
 def test_bytes_only_no_crc(device):

@@ -490,6 +490,7 @@ static KernelFn select_tile_kernel(bool crc, int item, bool swap) {
 
 KernelFn select_rows_kernel(bool crc, int item, bool swap, int k);  // decode_rows.hip
 KernelFn select_pair_kernel(bool crc, int item, bool swap, int nu);  // decode_rows.hip
+KernelFn select_duo_kernel(bool crc, int item, bool swap);           // decode_rows.hip
 KernelFn select_tile4_kernel(bool crc, int item, bool swap);         // decode_tile.hip
 KernelFn select_tileg_kernel(bool crc, int item, bool swap);         // decode_tile.hip
 
@@ -505,6 +506,18 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
                       : (p.tune & kTuneSkipCrc) ? select_pair_kernel(crc, p.g.itemsize, swap, 5) : nullptr;
         if (!fn) fn = select_pair_kernel(crc, p.g.itemsize, swap, nu);
         if (!fn) return ZHIP_E_UNSUPPORTED;
+        // chunks of more than 32 units (> 1 MiB): one unit per 256-thread half of
+        // a 512-thread workgroup (k_decode_duo; C1 0.55 -> 0.62 of HBM peak,
+        // profiles/r02/kernel_arms_ab.jsonl); kTuneDuo forces it
+        if ((p.tune & kTuneDuo) || (p.nseg > 32 && !(p.tune & (kTuneSingle | kTuneSkipCrc)))) {
+            KernelFn dfn = select_duo_kernel(crc, p.g.itemsize, swap);
+            if (!dfn) return ZHIP_E_UNSUPPORTED;
+            const uint32_t duos = (uint32_t)(((uint64_t)p.n_units + 1u) / 2u);
+            const uint32_t dgrid = duos > p.n_idx ? duos : p.n_idx;
+            if (dgrid == 0) return ZHIP_OK;
+            hipLaunchKernelGGL(dfn, dim3(dgrid), dim3(2 * kThreads), 0, stream, p);
+            return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
+        }
         const uint32_t pairs = (uint32_t)(((uint64_t)p.n_units + nu - 1u) / nu);
         const uint32_t grid = pairs > p.n_idx ? pairs : p.n_idx;
         if (grid == 0) return ZHIP_OK;

@@ -473,10 +473,12 @@ __device__ __forceinline__ uint32_t lanemul3(const uint32_t* s_mul, int t, uint3
 
 // Shard-index CRC check by one workgroup with the pair tables (verify_index's
 // chain, four accumulators, folded, shifted by kthread11).
+// (`active` false: a second half-workgroup that only joins the barriers)
 __device__ __forceinline__ void verify_index_pair(const DecodeParams& p, uint32_t j, int t, uint32_t kth11,
-                                                  const uint32_t* s_tab, uint32_t* red, bool has_pre, uint4 pre) {
+                                                  const uint32_t* s_tab, uint32_t* red, bool has_pre, uint4 pre,
+                                                  bool active = true) {
     const zhip_chunk ch = p.idx_chunks[j];
-    const uint32_t ok = ch.src_len == (uint64_t)p.idx_nbytes + 4u;
+    const uint32_t ok = active && ch.src_len == (uint64_t)p.idx_nbytes + 4u;
     const uint8_t* cp = p.src + ch.src;
     const uint32_t nk = (p.idx_E + kWgStride - 1) / kWgStride;
     const int32_t lo = (int32_t)p.idx_E - (int32_t)(nk * kWgStride);
@@ -493,9 +495,9 @@ __device__ __forceinline__ void verify_index_pair(const DecodeParams& p, uint32_
     }
     uint32_t v = wave_xor(gf_mul(fold4(s_tab, a), kth11));
     __syncthreads();  // red may still be read from a previous index
-    if ((t & 63) == 0) red[t >> 6] = v;
+    if (active && (t & 63) == 0) red[t >> 6] = v;
     __syncthreads();
-    if (t == 0) {
+    if (active && t == 0) {
         zhip_status st = {ZHIP_ST_LENGTH_MISMATCH, 0u, 0u, 0u};
         if (ok) {
             const uint32_t V = red[0] ^ red[1] ^ red[2] ^ red[3];
@@ -545,6 +547,53 @@ __device__ __forceinline__ void store_unit_rows(const DecodeParams& p, const Uni
     }
 }
 
+// Publication of a run's reduced contribution V by wave 0 (wave-uniform, lane 0
+// touches memory): one 64-bit atomic (contribution | arrival bits) when a chunk
+// has <= 32 units, else xor + arrival count; the arrival that completes the
+// chunk compares with the trailer.
+__device__ __forceinline__ void publish_run(const DecodeParams& p, const Unit& U, uint32_t V, uint32_t run_bits,
+                                            uint32_t stored, int t) {
+    if (p.tune & kTuneNoTicket) {  // ablation: no publication / last-arriver
+        if (t == 0 && V == 0x9E3779B9u) p.status[U.c].aux = V;
+    } else if (p.nseg <= 32) {
+        const uint64_t full = p.nseg >= 32 ? 0xFFFFFFFFull : ((1ull << p.nseg) - 1ull);
+        uint64_t prev = 0;
+        if (t == 0) {
+            uint64_t* w = reinterpret_cast<uint64_t*>(p.ws) + 2ull * U.c;
+            prev = __hip_atomic_fetch_xor(w, ((uint64_t)run_bits << 32) | V, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+        }
+        PendingU q;
+        q.prev = prev;
+        q.stored = stored;
+        q.c = U.c;
+        q.bits = run_bits;
+        q.V = V;
+        q.valid = 1;
+        retire_uniform(p, q, full, t, true);
+    } else {  // > 32 units per chunk: xor, then count arrivals
+        uint32_t raw = 0, last = 0;
+        const uint32_t n_run = __builtin_popcount(run_bits);
+        if (t == 0) {
+            uint32_t* accw = p.ws + 4ull * U.c;
+            const uint32_t prev = __hip_atomic_fetch_xor(accw, V, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::"v"(prev) : "memory");
+            const uint32_t tk = __hip_atomic_fetch_add(accw + 2, n_run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (tk + n_run == p.nseg) {
+                raw = __hip_atomic_exchange(accw, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                // consume the returned value here (rare path): a register with a
+                // load still pending would make every later write to it wait
+                // for the wave's stores too
+                asm volatile("s_waitcnt vmcnt(0)" ::"v"(raw) : "memory");
+                __hip_atomic_store(accw + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                last = 1;
+            }
+        }
+        if (__builtin_amdgcn_readfirstlane(last))
+            finalize_uniform(p, U.c, stored, __builtin_amdgcn_readfirstlane(raw), t, true);
+    }
+}
+
 // End of a run (consecutive units of one chunk in this workgroup): reduce the
 // lanes' Horner states, shift to the chunk reference, publish with one 64-bit
 // atomic (CRC contribution | arrival bits); the arrival that completes the
@@ -570,46 +619,7 @@ __device__ __forceinline__ void run_end_pair(const DecodeParams& p, const Unit& 
     if (t < 64) {  // wave 0, wave-uniform
         const uint32_t V = __builtin_amdgcn_readfirstlane(red[0] ^ red[1] ^ red[2] ^ red[3]);
         stamp(p, g, t, 6);
-        if (p.tune & kTuneNoTicket) {  // ablation: no publication / last-arriver
-            if (t == 0 && V == 0x9E3779B9u) p.status[U.c].aux = V;
-        } else if (p.nseg <= 32) {
-            const uint64_t full = p.nseg >= 32 ? 0xFFFFFFFFull : ((1ull << p.nseg) - 1ull);
-            uint64_t prev = 0;
-            if (t == 0) {
-                uint64_t* w = reinterpret_cast<uint64_t*>(p.ws) + 2ull * U.c;
-                prev = __hip_atomic_fetch_xor(w, ((uint64_t)run_bits << 32) | V, __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_AGENT);
-            }
-            PendingU q;
-            q.prev = prev;
-            q.stored = stored;
-            q.c = U.c;
-            q.bits = run_bits;
-            q.V = V;
-            q.valid = 1;
-            retire_uniform(p, q, full, t, true);
-        } else {  // > 32 units per chunk: xor, then count arrivals
-            uint32_t raw = 0, last = 0;
-            const uint32_t n_run = __builtin_popcount(run_bits);
-            if (t == 0) {
-                uint32_t* accw = p.ws + 4ull * U.c;
-                const uint32_t prev = __hip_atomic_fetch_xor(accw, V, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                asm volatile("s_waitcnt vmcnt(0)" ::"v"(prev) : "memory");
-                const uint32_t tk = __hip_atomic_fetch_add(accw + 2, n_run, __ATOMIC_RELAXED,
-                                                           __HIP_MEMORY_SCOPE_AGENT);
-                if (tk + n_run == p.nseg) {
-                    raw = __hip_atomic_exchange(accw, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    // consume the returned value here (rare path): a register with a
-                    // load still pending would make every later write to it wait
-                    // for the wave's stores too
-                    asm volatile("s_waitcnt vmcnt(0)" ::"v"(raw) : "memory");
-                    __hip_atomic_store(accw + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    last = 1;
-                }
-            }
-            if (__builtin_amdgcn_readfirstlane(last))
-                finalize_uniform(p, U.c, stored, __builtin_amdgcn_readfirstlane(raw), t, true);
-        }
+        publish_run(p, U, V, run_bits, stored, t);
     }
 }
 
@@ -807,6 +817,106 @@ KernelFn select_pair_kernel(bool crc, int item, bool swap, int nu) {
         return !(crc && item == 4 && !swap) ? nullptr : k_decode_pair<true, 4, false, 2, 8, 3>;
     if (nu == 3 || nu == 4) return nullptr;  // retired arms
     return nu == 1 ? select_pair_nu<1>(crc, item, swap) : select_pair_nu<2>(crc, item, swap);
+}
+
+// ---------------------------------------------------------------------------
+// k_decode_duo: k_decode_pair's decode with one unit per 256-thread half of a
+// 512-thread workgroup, so the 24 KiB of CRC tables in LDS serve two units
+// while every unit keeps its own waves: 8 waves per workgroup, 4 workgroups
+// (32 waves) per CU, the whole headline batch resident at once.  Each half
+// runs the NU == 1 arm of k_decode_pair (own Horner chain, VALU lane multiply
+// by kpair11, own publication); barriers are workgroup-wide, so both halves
+// pass every one of them whatever their unit's state.
+template <bool CRC, int ITEM, bool SWAP, int K = 8>
+__global__ __launch_bounds__(2 * kThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_decode_duo(
+    const DecodeParams p) {
+    __shared__ uint32_t s_tab[CRC ? kPairTabWords : 1];
+    __shared__ uint32_t s_red[3][kThreads / 64];
+    const int t = threadIdx.x, h = t >> 8, tl = t & (kThreads - 1);
+    const uint32_t G = gridDim.x, g = blockIdx.x;
+    const uint32_t q = 2u * g + (uint32_t)h;
+    if (2u * g >= p.n_units && g >= p.n_idx) return;  // workgroup-uniform
+    const bool has = q < p.n_units;
+    const uint32_t expected = p.g.nbytes + (CRC ? 4u : 0u);
+    const uint32_t u = has ? (q / p.nseg) * p.nseg + (p.nseg - 1u - q % p.nseg) : 0u;
+    const uint8_t* zero = reinterpret_cast<const uint8_t*>(g_rows_zero);
+    // 1. vector loads in a path-independent order and count: [CRC: tables (3),
+    //    lane constants (2), first shard-index block], the unit (K)
+    uint4 tv0, tv1, tv2;
+    uint32_t kth = 0, ku = 0;
+    if constexpr (CRC) {
+        const uint4* gt = reinterpret_cast<const uint4*>(p.pair_tab);
+        tv0 = gt[t];
+        tv1 = gt[t + 2 * kThreads];
+        tv2 = gt[t + 4 * kThreads];
+        kth = load_u32_any(reinterpret_cast<const uint8_t*>(p.kthread11 + tl));
+        ku = load_u32_any(reinterpret_cast<const uint8_t*>(p.kpair11 + (size_t)(u % p.nseg) * kThreads + tl));
+    }
+    uint4 A[K];
+    Unit ua;
+    uint4 ipre = make_uint4(0, 0, 0, 0);
+    if (p.pred) {
+        const Unit ga = predict_unit(p, u);
+        load_unit_rows(ga, has, tl, A);
+        ua = resolve_unit(p, u, expected);
+        if (has && ua.mode == ZHIP_ST_OK && ua.cp != ga.cp) {  // wrong guess: reload, full drain
+            load_unit_rows(ua, true, tl, A);
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+        }
+        if constexpr (CRC) ipre = index_prefetch(p, g, g < p.n_idx && h == 0, tl, zero);
+    } else {
+        ua = resolve_unit(p, u, expected);
+        if constexpr (CRC) ipre = index_prefetch(p, g, g < p.n_idx && h == 0, tl, zero);
+        load_unit_rows(ua, has, tl, A);
+    }
+    const RowSteps ma = load_row_steps(p, ua);
+    const bool crc_on = CRC && has && ua.mode == ZHIP_ST_OK;
+    uint32_t stored = 0;
+    if (crc_on) stored = load_trailer_uniform(ua.cp, p.g.nbytes);
+    // 2. tables into LDS
+    if constexpr (CRC) {
+        uint4* st = reinterpret_cast<uint4*>(s_tab);
+        st[t] = tv0;
+        st[t + 2 * kThreads] = tv1;
+        st[t + 4 * kThreads] = tv2;
+        __syncthreads();
+    }
+    // 3. stores, each block's Horner step after its store
+    uint8_t* sink = reinterpret_cast<uint8_t*>(g_rows_sink);
+    const uint32_t lane_row = (16u * (uint32_t)tl) >> p.row_shift;
+    const uint32_t lane_col = (16u * (uint32_t)tl) & ((1u << p.row_shift) - 1u);
+    const int64_t lane_off = (int64_t)lane_row * p.r_oy + (int64_t)lane_col;
+    Acc4 acc = {0u, 0u, 0u, 0u};
+    store_unit_rows<ITEM, SWAP, K>(p, ua, ma, has, lane_row, lane_off, sink, A, crc_on, s_tab, &acc);
+    // 4. run end: every half reaches the barrier; only a valid one publishes
+    if constexpr (CRC) {
+        uint32_t v = crc_on ? gf_mul(fold4(s_tab, acc), ku) : 0u;
+        v = wave_xor(v);
+        if ((tl & 63) == 0) s_red[h][tl >> 6] = v;
+        __syncthreads();
+        if (crc_on && tl < 64) {
+            const uint32_t V = __builtin_amdgcn_readfirstlane(s_red[h][0] ^ s_red[h][1] ^ s_red[h][2] ^ s_red[h][3]);
+            publish_run(p, ua, V, 1u << (ua.sidx & 31u), __builtin_amdgcn_readfirstlane(stored), tl);
+        }
+    }
+    if (has) unit_status_pair(p, ua, CRC, tl);
+    // 5. fused shard-index checks by half 0 (half 1 joins the barriers)
+    if constexpr (CRC)
+        for (uint32_t j = g; j < p.n_idx; j += G)
+            verify_index_pair(p, j, tl, kth, s_tab, s_red[2], j == g, ipre, h == 0);
+}
+
+KernelFn select_duo_kernel(bool crc, int item, bool swap) {
+    switch (item) {
+        case 1: return crc ? k_decode_duo<true, 1, false> : k_decode_duo<false, 1, false>;
+        case 2: return crc ? (swap ? k_decode_duo<true, 2, true> : k_decode_duo<true, 2, false>)
+                           : (swap ? k_decode_duo<false, 2, true> : k_decode_duo<false, 2, false>);
+        case 4: return crc ? (swap ? k_decode_duo<true, 4, true> : k_decode_duo<true, 4, false>)
+                           : (swap ? k_decode_duo<false, 4, true> : k_decode_duo<false, 4, false>);
+        case 8: return crc ? (swap ? k_decode_duo<true, 8, true> : k_decode_duo<true, 8, false>)
+                           : (swap ? k_decode_duo<false, 8, true> : k_decode_duo<false, 8, false>);
+        default: return nullptr;
+    }
 }
 
 KernelFn select_rows_kernel(bool crc, int item, bool swap, int k) {

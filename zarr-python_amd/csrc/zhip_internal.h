@@ -133,6 +133,7 @@ constexpr uint32_t kTuneTile1 = 65536u;  // transposed layouts: the one-tile per
 constexpr uint32_t kTuneSplitChain = 262144u; // k_decode_pair: independent Horner chains for the two units
 constexpr uint32_t kTuneEncNoFlags = 524288u; // k_encode_pair: skip the non-empty flag atomics (results invalid)
 constexpr uint32_t kTuneNoTile4 = 1048576u;   // transposed layouts: grouped k_*_tileg where k_*_tile4 would run
+constexpr uint32_t kTuneDuo = 2097152u;       // whole-row layouts: k_decode_duo (one unit per half of a 512-thread workgroup)
 constexpr uint32_t kTuneStamp = 1024u;    // k_decode_pair: per-workgroup phase timestamps (zhip_debug_stamps)
 constexpr uint32_t kStampWG = 8192u;      // workgroups stamped per launch
 constexpr uint32_t kStampSlots = 8u;

@@ -224,6 +224,10 @@ def lib():
     L.zhip_fdiv_eval.restype = ctypes.c_uint32
     if L.zhip_abi_version() != 1:
         raise NativeError("libzarrhip ABI version mismatch")
+    # ZHIP_TUNE: kernel-variant bits for measurement runs (0 = production)
+    tune = int(os.environ.get("ZHIP_TUNE", "0") or 0)
+    if tune:
+        L.zhip_set_tuning(2, tune)
     _lib = L
     return L
 
