@@ -21,6 +21,8 @@ def main():
                             ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
     lib.cb_copy_rot.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
                                 ctypes.c_void_p]
+    lib.cb_copy_il.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_uint32,
+                               ctypes.c_int, ctypes.c_void_p]
     lib.cb_copy_persist.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
                                     ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
     dev = torch.device("cuda:0")
@@ -29,7 +31,10 @@ def main():
         srcs = [torch.empty(n, dtype=torch.uint8, device=dev).fill_(7) for _ in range(R)]
         dsts = [torch.empty(n, dtype=torch.uint8, device=dev) for _ in range(R)]
         # nt: 0 default policy, 1 nontemporal loads+stores, 2 loads only, 3 stores only
-        if os.environ.get("ROT"):  # spans with and without the rotated step order
+        if os.environ.get("IL"):  # interleaved 32 KiB footprints vs plain spans
+            arms = [("il", S, 8, nt) for S in (1, 2, 4, 8, 16, 64) for nt in (1, 3)] + \
+                   [("span", 4 << 10, 1, 1), ("span", 4 << 10, 1, 3)]
+        elif os.environ.get("ROT"):  # spans with and without the rotated step order
             arms = [(kind, s, s // 4096, nt) for s in (32 << 10, 64 << 10) for nt in (1, 3)
                     for kind in ("span", "rot")] + [("span", 4 << 10, 1, 1)]
         else:
@@ -45,6 +50,8 @@ def main():
                 sh = ctypes.c_void_p(int(torch.cuda.current_stream(dev).cuda_stream))
                 if kind == "span":
                     rc = lib.cb_copy(srcs[i % R].data_ptr(), dsts[i % R].data_ptr(), n, a, K, 1, nt, sh)
+                elif kind == "il":
+                    rc = lib.cb_copy_il(srcs[i % R].data_ptr(), dsts[i % R].data_ptr(), n, K, a, nt, sh)
                 elif kind == "rot":
                     rc = lib.cb_copy_rot(srcs[i % R].data_ptr(), dsts[i % R].data_ptr(), n, K, nt, sh)
                 elif kind == "persist":

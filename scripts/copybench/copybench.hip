@@ -106,6 +106,49 @@ extern "C" int cb_copy_rot(const void* src, void* dst, uint64_t nbytes, int K, i
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
+// Interleaved spans: groups of S consecutive workgroups share S*K 4 KiB steps;
+// workgroup j of a group takes steps j, j + S, j + 2S, ... (K of them), so a
+// workgroup's footprint is spread over S*K*4 KiB while the group, like
+// S*K one-step workgroups, covers it densely.
+template <int K, bool NTL, bool NTS>
+__global__ __launch_bounds__(256) void k_copy_il(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                 uint32_t S) {
+    const uint32_t grp = blockIdx.x / S, j = blockIdx.x - grp * S;
+    const uint64_t b0 = (uint64_t)grp * S * K * 256ull;
+    uint4 v[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint64_t i = b0 + 256ull * (j + S * (uint32_t)k) + threadIdx.x;
+        if constexpr (NTL) {
+            const v4u w = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(src) + i);
+            v[k] = make_uint4(w.x, w.y, w.z, w.w);
+        } else v[k] = src[i];
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint64_t i = b0 + 256ull * (j + S * (uint32_t)k) + threadIdx.x;
+        if constexpr (NTS) {
+            v4u w = {v[k].x, v[k].y, v[k].z, v[k].w};
+            __builtin_nontemporal_store(w, reinterpret_cast<v4u*>(dst) + i);
+        } else dst[i] = v[k];
+    }
+}
+
+extern "C" int cb_copy_il(const void* src, void* dst, uint64_t nbytes, int K, uint32_t S, int nt, void* stream) {
+    typedef void (*IFn)(const uint4*, uint4*, uint32_t);
+    IFn fn = nullptr;
+#define ISEL(KK)                                                                                  \
+    if (K == KK) fn = nt == 1 ? (IFn)k_copy_il<KK, true, true> : nt == 3 ? (IFn)k_copy_il<KK, false, true> \
+                                                               : (IFn)k_copy_il<KK, false, false>;
+    ISEL(8) ISEL(16)
+    if (!fn || S == 0) return -1;
+    const uint64_t per = 4096ull * K * S;
+    if (nbytes % per) return -3;
+    hipLaunchKernelGGL(fn, dim3((uint32_t)(nbytes / (4096ull * K))), dim3(256), 0, (hipStream_t)stream,
+                       (const uint4*)src, (uint4*)dst, S);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
 // Persistent grid-stride copy: `grid` workgroups, each walking 16-byte blocks
 // b = (g * 256 + t) + k * 256 * grid, K blocks in flight per thread.
 template <int K, bool NT>
