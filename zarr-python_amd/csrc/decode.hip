@@ -521,7 +521,12 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
         const uint32_t pairs = (uint32_t)(((uint64_t)p.n_units + nu - 1u) / nu);
         const uint32_t grid = pairs > p.n_idx ? pairs : p.n_idx;
         if (grid == 0) return ZHIP_OK;
-        hipLaunchKernelGGL(fn, dim3(grid), dim3(kThreads), 0, stream, p);
+        // one resident wave of workgroups (4 per CU; max_grid = 8 per CU): the
+        // workgroups of one XCD take a contiguous eighth of the batch
+        DecodeParams q = p;
+        q.xcd_run = (nu == 2 && !(p.tune & kTuneNoXcd) && grid % 8u == 0u &&
+                     grid <= (uint32_t)(max_grid / 8) * 4u) ? grid / 8u : 0u;
+        hipLaunchKernelGGL(fn, dim3(grid), dim3(kThreads), 0, stream, q);
         return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
     }
     if (p.rows) {

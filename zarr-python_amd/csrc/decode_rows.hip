@@ -652,7 +652,17 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(NU == 
     __shared__ uint32_t s_mul[kLdsMul ? 12 * kThreads : 1];
     __shared__ uint32_t s_red[2][kThreads / 64];
     const int t = threadIdx.x;
-    const uint32_t G = gridDim.x, g = blockIdx.x;
+    const uint32_t G = gridDim.x;
+    // XCD-contiguous runs (launch_decode sets xcd_run = G / 8 when the whole
+    // grid is resident at once): the workgroups the dispatcher sends to one
+    // XCD (blockIdx % 8) take one contiguous eighth of the batch instead of
+    // every eighth pair; measured 1-2 us faster on the headline, slower on
+    // multi-wave grids such as C4 (profiles/r02/kernel_arms_ab.jsonl)
+    uint32_t g = blockIdx.x;
+    if (p.xcd_run) {
+        const uint32_t x = blockIdx.x & 7u, slot = blockIdx.x >> 3;
+        g = ((slot / p.xcd_run) * 8u + x) * p.xcd_run + slot % p.xcd_run;
+    }
     const uint32_t q0 = (uint32_t)NU * g;
     const bool has_a = q0 < p.n_units, has_b = NU == 2 && q0 + 1u < p.n_units;
     if (!has_a && g >= p.n_idx) return;

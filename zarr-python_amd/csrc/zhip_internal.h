@@ -105,6 +105,7 @@ struct DecodeParams {
     int64_t r_oy;              // out stride of dim ndim-2
     int32_t nd2;               // ndim - 2
     uint32_t rows;             // 1: launch k_decode_rows
+    uint32_t xcd_run;          // k_decode_pair: pairs per XCD-contiguous run (0: dispatch order)
     const zhip_rowblk* rowmap; // per (sel, unit, step) destinations (zhip_rows_map); k_decode_pair
     // load-address prediction (zhip_predict; k_decode_pair): payload of chunk c
     // predicted at src + pred_base + (c / pred_per) * pred_outer + (c % pred_per) * pred_inner
@@ -134,6 +135,7 @@ constexpr uint32_t kTuneSplitChain = 262144u; // k_decode_pair: independent Horn
 constexpr uint32_t kTuneEncNoFlags = 524288u; // k_encode_pair: skip the non-empty flag atomics (results invalid)
 constexpr uint32_t kTuneNoTile4 = 1048576u;   // transposed layouts: grouped k_*_tileg where k_*_tile4 would run
 constexpr uint32_t kTuneDuo = 2097152u;       // whole-row layouts: k_decode_duo (one unit per half of a 512-thread workgroup)
+constexpr uint32_t kTuneNoXcd = 8388608u;     // k_decode_pair: plain dispatch order (no XCD-contiguous runs)
 constexpr uint32_t kTuneStamp = 1024u;    // k_decode_pair: per-workgroup phase timestamps (zhip_debug_stamps)
 constexpr uint32_t kStampWG = 8192u;      // workgroups stamped per launch
 constexpr uint32_t kStampSlots = 8u;
