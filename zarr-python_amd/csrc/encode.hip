@@ -370,7 +370,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     __shared__ uint32_t s_tab[CRC ? 16 * 256 : 1];
     __shared__ uint32_t s_red[2][kThreads / 64];
     const int t = threadIdx.x;
-    const uint32_t q0 = 2u * blockIdx.x;
+    // XCD-contiguous runs for a one-wave grid (launch_encode's xcd_run, as k_decode_pair)
+    const uint32_t b = p.xcd_run ? ((blockIdx.x >> 3) / p.xcd_run * 8u + (blockIdx.x & 7u)) * p.xcd_run +
+                                       (blockIdx.x >> 3) % p.xcd_run
+                                 : blockIdx.x;
+    const uint32_t q0 = 2u * b;
     const bool has_b = q0 + 1u < p.n_units;
     auto unit_of = [&](uint32_t q) {
         const uint32_t c = q / p.nseg;
@@ -517,7 +521,11 @@ int launch_encode(const EncodeParams& p, hipStream_t stream, int max_grid) {
             if (hipMemsetAsync(p.nonempty, 0, (size_t)p.n_chunks * sizeof(uint32_t), stream) != hipSuccess)
                 return ZHIP_E_HIP;
         }
-        hipLaunchKernelGGL(fn, dim3((p.n_units + 1u) / 2u), dim3(kThreads), 0, stream, p);
+        const uint32_t grid = (p.n_units + 1u) / 2u;
+        EncodeParams q = p;
+        q.xcd_run = (!(p.tune & kTuneNoXcd) && grid % 8u == 0u && grid <= (uint32_t)(max_grid / 8) * 4u) ? grid / 8u
+                                                                                                      : 0u;
+        hipLaunchKernelGGL(fn, dim3(grid), dim3(kThreads), 0, stream, q);
         return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
     }
     EncodeFn fn = crc ? (p.fast ? pick_encode<true, true>(p.g.itemsize, swap) : pick_encode<true, false>(p.g.itemsize, swap))

@@ -188,6 +188,7 @@ struct EncodeParams {
     const uint32_t* gtz;
     uint32_t n_groups, g_step_t, n_sub;
     int64_t g_step_o;
+    uint32_t xcd_run;     // k_encode_pair: pairs per XCD-contiguous run (0: dispatch order)
 };
 
 struct PackParams {
