@@ -321,7 +321,76 @@ def extra_configs(ctx, args):
     if single and "e2e" in args.extra:
         out["e2e_c2_host"] = e2e_host(device, args)
         torch.cuda.empty_cache()
+    if single and "call" in args.extra:
+        out["device_read_call"] = device_read_call(device, args)
+        torch.cuda.empty_cache()
     return out
+
+
+def device_read_call(device, args):
+    """The headline read as a zarr caller issues it: one
+    HipCodecPipeline.read_sync per call (eager, no graph, synchronised: the
+    call returns with statuses checked), device-resident store and out,
+    rotating over the replicas.  Three ways: read_sync on a built batch
+    through the per-call plan cache (a repeated read re-launches the cached
+    program: no planning, no table upload, one 4-byte error word back);
+    Array.get, which also rebuilds the batch (BasicIndexer) every call; and
+    read_sync with the cache off (plans and uploads every call, round 2's
+    path).  ms_per_call is host wall per call; host_overhead_ms subtracts the
+    kernel's own time."""
+    import torch
+
+    from zarr_hip import pipeline as P
+
+    g = W.HEADLINE
+    shape, shards, inner = g["shape"], g["shards"], g["inner"]
+    src = torch.from_numpy(synthetic(shape, seed=0)).to(device)
+    R = args.replicas
+    arrs = [build_replica(device, src, shape, inner, [LE, CRC], shards=shards) for _ in range(R)]
+    batches = [a.batch_info((Ellipsis,))[0] for a in arrs]
+    outs = [torch.empty(shape, dtype=torch.float32, device=device) for _ in range(R)]
+    t0 = time.perf_counter()
+    arrs[0].codec_pipeline.read_sync(batches[0], outs[0])
+    first_ms = (time.perf_counter() - t0) * 1e3
+    for i in range(R):
+        arrs[i].codec_pipeline.read_sync(batches[i], outs[i])
+        if not torch.equal(outs[i].view(torch.int32), src.view(torch.int32)):
+            raise SystemExit("bench device_read_call: decoded bytes differ from the source")
+    progs = [a.prepare_read((Ellipsis,))[0] for a in arrs]
+    kern = float(np.median(eager_kernel_times(progs, max(20, args.steps), device)))
+    del progs
+    n = max(50, 2 * args.steps)
+
+    def timed(fn):
+        for i in range(R):
+            fn(i)
+        torch.cuda.synchronize(device)
+        t = time.perf_counter()
+        for i in range(n):
+            fn(i % R)
+        return (time.perf_counter() - t) / n
+
+    cached = timed(lambda i: arrs[i].codec_pipeline.read_sync(batches[i], outs[i]))
+    get = timed(lambda i: arrs[i].get((Ellipsis,), out=outs[i]))
+    keep, P.READ_CACHE_SIZE = P.READ_CACHE_SIZE, 0
+    try:
+        uncached = timed(lambda i: arrs[i].codec_pipeline.read_sync(batches[i], outs[i]))
+    finally:
+        P.READ_CACHE_SIZE = keep
+    for i in range(R):
+        if not torch.equal(outs[i].view(torch.int32), src.view(torch.int32)):
+            raise SystemExit("bench device_read_call: decoded bytes differ from the source")
+    dec = src.numel() * 4
+
+    def line(w):
+        return {"ms_per_call": round(w * 1e3, 4), "decoded_GiBps": round(dec / w / GIB, 1),
+                "host_overhead_ms": round((w - kern) * 1e3, 4)}
+
+    return {"kernel_ms": round(kern * 1e3, 4), "calls": n, "first_call_ms": round(first_ms, 3),
+            "read_sync_cached": line(cached), "array_get_cached": line(get),
+            "read_sync_uncached": line(uncached), "checked": "bytes",
+            "note": "headline config; eager per-call reads, each synchronised; kernel_ms = median "
+                    "event-timed eager launch of the same program"}
 
 
 def c4_partitioned(ctx, args):
@@ -800,8 +869,8 @@ def main():
     ap.add_argument("--eager", action="store_true",
                     help="time one host launch per step instead of a hipGraph replay")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
-    ap.add_argument("--extra", default="c1,c2,c3,c4,c5,enc,e2e",
-                    help="extra configs (subset of c1,c2,c3,c4,c5,enc,e2e, or ''); c4/c5 run "
+    ap.add_argument("--extra", default="c1,c2,c3,c4,c5,enc,e2e,call",
+                    help="extra configs (subset of c1,c2,c3,c4,c5,enc,e2e,call, or ''); c4/c5 run "
                          "partitioned at every N, the others at N=1")
     args = ap.parse_args()
 

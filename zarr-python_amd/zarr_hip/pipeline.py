@@ -249,14 +249,54 @@ class DecodeProgram:
     item_missing: np.ndarray
     keepalive: list = field(default_factory=list)
     pending: Any = None  # staging.Pending: host bytes still on their way to HBM
+    # ((DeviceArena, gen), ...) of the device stores the batch reads: a launch
+    # after any of them changed placements would read moved or reused bytes
+    generations: tuple = ()
+
+    def stale(self) -> bool:
+        return any(a.gen != g for a, g in self.generations)
+
+    def check_fresh(self) -> None:
+        if self.stale():
+            raise RuntimeError("the device store changed since this read was planned (a key was written or "
+                               "deleted, its bytes may have moved): plan the read again")
 
     def launch(self, stream: int | None = None) -> None:
+        self.check_fresh()
         if self.pending is not None:
             self.pending.finish(stream)  # the launch stream waits for the staged copies
             self.pending = None
         if self.index is not None:
             self.index.launch(stream)
         self.data.launch(stream)
+
+    def retarget(self, out) -> None:
+        """Point the data launch at another out of the same shape, strides,
+        dtype and 16-byte alignment class (the tables hold out offsets, not
+        addresses; the kernel choice depends only on the alignment), or at
+        None to drop the reference (the per-call plan cache keeps programs,
+        not outs)."""
+        self.data.out = out
+
+    def results_fast(self) -> tuple[GetResult, ...]:
+        """results() for the per-call path: synchronise on ONE 4-byte error
+        word per launch (every non-OK, non-missing status of the data and the
+        fused index checks ORs a bit into it); the full status table is read
+        only when it is set.  Missing items are known on the host at planning
+        (absent keys, absent shards), so the GetResults are prebuilt."""
+        err = self.data.errflag()
+        if self.index is not None:
+            err |= self.index.errflag()
+        if err:
+            self.data.reset_errflag()
+            if self.index is not None:
+                self.index.reset_errflag()
+            return self.results()
+        ok = getattr(self, "_ok_results", None)
+        if ok is None:
+            ok = tuple(GetResult(status="missing" if m else "present") for m in self.item_missing)
+            self._ok_results = ok
+        return ok
 
     def results(self) -> tuple[GetResult, ...]:
         """Synchronise, then raise like the reference or return per-item statuses."""
@@ -322,11 +362,66 @@ class ReadGraph:
                     self.programs[i % len(self.programs)].launch()
 
     def replay(self) -> None:
+        for p in self.programs:  # the graph holds the programs' planned offsets
+            p.check_fresh()
         self.graph.replay()
 
     def results(self) -> list:
         _torch().cuda.synchronize(self.device)
         return [p.results() for p in self.programs]
+
+
+# entries of the per-call plan cache (per pipeline instance); 0 disables it
+READ_CACHE_SIZE = int(os.environ.get("ZARR_HIP_READ_CACHE", "16"))
+
+
+def _sel_key(sel):
+    """A hashable image of a basic selection (slices are unhashable before
+    Python 3.12); None for selections the cache does not key (arrays)."""
+    out = []
+    for s in sel:
+        t = type(s)
+        if t is slice:
+            out.append((s.start, s.stop, s.step))
+        elif t is int or isinstance(s, (int, np.integer)):
+            out.append(int(s))
+        else:
+            return None
+    return tuple(out)
+
+
+def _read_key(batch: list, dev_out, drop_axes):
+    """Cache key of a device-resident read, or None when it is not cacheable
+    (getters without a store path, array selections).  The out enters by
+    geometry and 16-byte alignment only (see DecodeProgram.retarget)."""
+    spec = batch[0][1]
+    fv = spec.fill_value
+    parts = [spec.shape, spec.dtype.str, type(fv).__name__, repr(fv), spec.config, tuple(drop_axes),
+             tuple(dev_out.shape), tuple(dev_out.stride()), str(dev_out.dtype), dev_out.data_ptr() % 16,
+             str(dev_out.device)]
+    for it in batch:
+        bg = it[0]
+        st = getattr(bg, "store", None)
+        if not isinstance(st, DeviceStore):
+            return None
+        cs, os_ = _sel_key(it[2]), _sel_key(it[3])
+        if cs is None or os_ is None or it[1] is not spec and it[1] != spec:
+            return None
+        parts.append((id(st), bg.path, cs, os_, bool(it[4])))
+    return tuple(parts)
+
+
+def _generations(batch: list) -> tuple:
+    """((arena, gen), ...) of the DeviceStore arenas a batch reads."""
+    seen: dict = {}
+    for it in batch:
+        bg = it[0]
+        st = getattr(bg, "store", None)
+        arena = st.arena if isinstance(st, DeviceStore) else (
+            bg.value.arena if isinstance(bg, _Raw) and isinstance(bg.value, DeviceRef) else None)
+        if arena is not None and id(arena) not in seen:
+            seen[id(arena)] = (arena, arena.gen)
+    return tuple(seen.values())
 
 
 def _device_resident(batch: list) -> bool:
@@ -356,6 +451,9 @@ class HipCodecPipeline:
     # load-address prediction for whole-row batches (planner.predict_rows);
     # ZARR_HIP_PREDICT=0 turns it off (measurements only)
     predict_loads: bool = field(default_factory=lambda: os.environ.get("ZARR_HIP_PREDICT", "1") != "0")
+    # per-call plan cache for device-resident reads (read_sync): batch key ->
+    # DecodeProgram; entries hold tables, never outs (retargeted per call)
+    _read_cache: dict = field(default_factory=dict, compare=False, hash=False, repr=False)
 
     @classmethod
     def from_codecs(cls, codecs: Iterable, *, batch_size: int | None = None) -> "HipCodecPipeline":
@@ -466,6 +564,9 @@ class HipCodecPipeline:
             return pipe.prepare_read(batch_s, out_s, drop_axes, item_out_extra)
         spec: ArraySpec = batch[0][1]
         device = out.device
+        itemsize = out.element_size()
+        if np.dtype(spec.dtype).itemsize != itemsize:
+            raise TypeError("out dtype itemsize does not match the array dtype")
         chain: ChainInfo = analyze_chain(self.codecs, spec)
         resolved = None
         # host-resident bytes are packed and copied on the stager thread while
@@ -478,28 +579,31 @@ class HipCodecPipeline:
             srcs = [(0, 0, bool(m)) for m in item_missing]
         else:
             src, size, srcs, keep, pending = staging.gather_sources(batch, device, defer=True)
-        items = [(o, n, miss, it[2], it[3]) for (o, n, miss), it in zip(srcs, batch)]
-        itemsize = out.element_size()
-        if np.dtype(spec.dtype).itemsize != itemsize:
-            raise TypeError("out dtype itemsize does not match the array dtype")
-        ostr = [int(s) * itemsize for s in out.stride()]
-        with torch.cuda.device(device):
-            t = plan_decode(chain, spec, items, ostr, out.data_ptr(), drop_axes, resolved, item_out_extra)
-            if self.predict_loads:
-                predict_rows(t, chain, spec, size)
-            # fuse the shard-index CRC checks into the data launch
-            # (zhip_decode_indexed: needs the CRC tables, i.e. an inner crc32c, and
-            # the non-tiled kernel); else a second NO_WRITE launch
-            fuse = (t.index_layout is not None and resolved is None and chain.inner.crc
-                    and not t.tile)
-            data = DecodeLaunch(t.layout, t.chunks, t.sels, src, size, out, t.fast, device, t.tile,
-                                t.index_chunks if fuse else None, t.rows, t.predict)
-            index = None
-            if t.index_layout is not None and not fuse:
-                index = DecodeLaunch(t.index_layout, t.index_chunks, np.zeros(1, SEL_DT), src, size,
-                                     None, False, device)
+        try:
+            items = [(o, n, miss, it[2], it[3]) for (o, n, miss), it in zip(srcs, batch)]
+            ostr = [int(s) * itemsize for s in out.stride()]
+            with torch.cuda.device(device):
+                t = plan_decode(chain, spec, items, ostr, out.data_ptr(), drop_axes, resolved, item_out_extra)
+                if self.predict_loads:
+                    predict_rows(t, chain, spec, size)
+                # fuse the shard-index CRC checks into the data launch
+                # (zhip_decode_indexed: needs the CRC tables, i.e. an inner crc32c, and
+                # the non-tiled kernel); else a second NO_WRITE launch
+                fuse = (t.index_layout is not None and resolved is None and chain.inner.crc
+                        and not t.tile)
+                data = DecodeLaunch(t.layout, t.chunks, t.sels, src, size, out, t.fast, device, t.tile,
+                                    t.index_chunks if fuse else None, t.rows, t.predict)
+                index = None
+                if t.index_layout is not None and not fuse:
+                    index = DecodeLaunch(t.index_layout, t.index_chunks, np.zeros(1, SEL_DT), src, size,
+                                         None, False, device)
+        except BaseException:
+            if pending is not None:
+                pending.abort()  # the staging job must not outlive the buffers it fills
+            raise
         return DecodeProgram(t, data, index, len(batch), chain.shard is not None,
-                             np.array([s[2] for s in srcs], bool), keepalive=keep, pending=pending)
+                             np.array([s[2] for s in srcs], bool), keepalive=keep, pending=pending,
+                             generations=_generations(batch))
 
     def read_sync(self, batch_info: Iterable, out, drop_axes: tuple = (),
                   max_workers: int = 1) -> tuple[GetResult, ...]:
@@ -514,6 +618,10 @@ class HipCodecPipeline:
         if not batch:
             return ()
         dev_out, host_out = _resolve_out(out, batch, drop_axes)
+        if host_out is None and READ_CACHE_SIZE:
+            key = _read_key(batch, dev_out, drop_axes)
+            if key is not None:
+                return self._read_cached(key, batch, dev_out, drop_axes)
         direct = host_out is not None and _pinned_host(host_out, dev_out)
         if host_out is not None and not drop_axes and not _device_resident(batch):
             groups = _slab_groups(batch, dev_out)
@@ -530,6 +638,40 @@ class HipCodecPipeline:
 
             copy_to_host(dev_out, host_out)
         return res
+
+    def _read_cached(self, key, batch, dev_out, drop_axes) -> tuple[GetResult, ...]:
+        """A device-resident read through the per-call plan cache: a repeated
+        read of the same selection (same keys, selections, spec, out geometry,
+        no write to the store since: the arena generation) skips planning and
+        table uploads -- one launch, one 4-byte error word back.  The
+        reference re-plans every read (codec_pipeline.py:1257-1319); its
+        plans are Python objects, these are device tables."""
+        cache = self._read_cache
+        # checked out while in use: a concurrent read of the same key (another
+        # thread, another stream) plans its own program instead of sharing
+        # this one's status and arrival workspace
+        prog = cache.pop(key, None)
+        if prog is not None and prog.stale():
+            prog = None
+        if prog is None:
+            if not _device_resident(batch):
+                return self._read_uncached(batch, dev_out, drop_axes)
+            prog = self.prepare_read(batch, dev_out, drop_axes)
+        prog.retarget(dev_out)
+        try:
+            prog.launch()
+            res = prog.results_fast()
+        finally:
+            prog.retarget(None)
+        while len(cache) >= READ_CACHE_SIZE:  # oldest first (insertion order = LRU)
+            cache.pop(next(iter(cache)), None)
+        cache[key] = prog
+        return res
+
+    def _read_uncached(self, batch, dev_out, drop_axes) -> tuple[GetResult, ...]:
+        prog = self.prepare_read(batch, dev_out, drop_axes)
+        prog.launch()
+        return prog.results()
 
     def _read_slabs_one_plan(self, batch, groups, dev_out, host_out, direct: bool):
         """_read_slabs for unsharded chains: the batch is planned ONCE (in slab
@@ -557,41 +699,41 @@ class HipCodecPipeline:
             if st[0] is None:  # host-sourced: begin its staging job now
                 st[0], keep, st[5] = st[4]()
                 st[3] = keep
-        for g in range(len(groups)):  # the library packs and copies them in this order
-            start(g)
-        items = []
-        for (_, _, idx), st in zip(groups, staged):
-            items += [(o, n, miss, batch[i][2], batch[i][3]) for (o, n, miss), i in zip(st[2], idx)]
-        ostr = [int(x) * itemsize for x in dev_out.stride()]
-        with torch.cuda.device(dev):
-            t = plan_decode(chain, spec, items, ostr, dev_out.data_ptr(), (), None, None)
-            launch = DecodeLaunch(t.layout, t.chunks, t.sels, None, 0, dev_out, t.fast, dev, t.tile, None,
-                                  t.rows, None)
         compute = torch.cuda.current_stream(dev)
         d2h = _d2h_stream(dev)
         nbytes = dev_out.numel() * dev_out.element_size()
-        bounce = None if direct else torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
-        first = 0
-        for g, ((a, b, idx), st) in enumerate(zip(groups, staged)):
-            if st[5] is not None:
-                st[5].finish()  # the launch stream waits for this slab's copies
-            launch.launch_range(first, len(idx), st[0], st[1])
-            first += len(idx)
-            ev = torch.cuda.Event()
-            ev.record(compute)
-            d2h.wait_event(ev)
-            with torch.cuda.stream(d2h):
-                if direct:
-                    _d2h(dev_out, host_out, a, b)
-                else:
-                    flat = dev_out.reshape(-1).view(torch.uint8)
-                    bounce[a:b].copy_(flat[a:b], non_blocking=True)
-        prog = DecodeProgram(t, launch, None, len(items), False,
-                             np.array([m for st in staged for (_, _, m) in st[2]], bool),
-                             keepalive=[st[0] for st in staged] + [k for st in staged for k in st[3]])
         try:
+            for g in range(len(groups)):  # the library packs and copies them in this order
+                start(g)
+            items = []
+            for (_, _, idx), st in zip(groups, staged):
+                items += [(o, n, miss, batch[i][2], batch[i][3]) for (o, n, miss), i in zip(st[2], idx)]
+            ostr = [int(x) * itemsize for x in dev_out.stride()]
+            with torch.cuda.device(dev):
+                t = plan_decode(chain, spec, items, ostr, dev_out.data_ptr(), (), None, None)
+                launch = DecodeLaunch(t.layout, t.chunks, t.sels, None, 0, dev_out, t.fast, dev, t.tile, None,
+                                      t.rows, None)
+            bounce = None if direct else torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+            first = 0
+            for g, ((a, b, idx), st) in enumerate(zip(groups, staged)):
+                if st[5] is not None:
+                    st[5].finish()  # the launch stream waits for this slab's copies
+                launch.launch_range(first, len(idx), st[0], st[1])
+                first += len(idx)
+                _slab_back(compute, d2h, dev_out, host_out, bounce, a, b, direct)
+            if not direct:
+                _fill_gaps(d2h, dev_out, bounce, groups, nbytes)
+            prog = DecodeProgram(t, launch, None, len(items), False,
+                                 np.array([m for st in staged for (_, _, m) in st[2]], bool),
+                                 keepalive=[st[0] for st in staged] + [k for st in staged for k in st[3]])
             res = prog.results()
         finally:
+            # every begun slab job ends here, consumed or not (a failed slab
+            # leaves the later ones running in the library's threads)
+            for st in staged:
+                if st[5] is not None:
+                    st[5].abort()
+            compute.synchronize()
             d2h.synchronize()
         if not direct:
             from .buffer import copy_to_host_from_pinned
@@ -619,25 +761,20 @@ class HipCodecPipeline:
         nbytes = dev_out.numel() * dev_out.element_size()
         bounce = None if direct else torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
         done = []
-        for a, b, idx in groups:
-            prog = self.prepare_read([batch[i] for i in idx], dev_out)
-            prog.launch()
-            ev = torch.cuda.Event()
-            ev.record(compute)
-            d2h.wait_event(ev)
-            with torch.cuda.stream(d2h):
-                if direct:
-                    _d2h(dev_out, host_out, a, b)
-                else:
-                    flat = dev_out.reshape(-1).view(torch.uint8)
-                    bounce[a:b].copy_(flat[a:b], non_blocking=True)
-            done.append((prog, idx))
         results: list = [None] * len(batch)
         try:
+            for a, b, idx in groups:
+                prog = self.prepare_read([batch[i] for i in idx], dev_out)
+                prog.launch()
+                _slab_back(compute, d2h, dev_out, host_out, bounce, a, b, direct)
+                done.append((prog, idx))
+            if not direct:
+                _fill_gaps(d2h, dev_out, bounce, groups, nbytes)
             for prog, idx in done:
                 for i, r in zip(idx, prog.results()):
                     results[i] = r
         finally:
+            compute.synchronize()
             d2h.synchronize()
         if not direct:
             from .buffer import copy_to_host_from_pinned
@@ -810,6 +947,39 @@ def _d2h(dev_out, host_out: np.ndarray, a: int, b: int) -> None:
     flat = dev_out.reshape(-1).view(torch.uint8)
     dst = torch.from_numpy(host_out.reshape(-1).view(np.uint8))
     dst[a:b].copy_(flat[a:b], non_blocking=True)
+
+
+def _slab_back(compute, d2h, dev_out, host_out, bounce, a: int, b: int, direct: bool) -> None:
+    """Bytes [a, b) of a decoded slab back to the host on the D2H stream, after
+    the slab's launch on `compute`: straight into a pinned host out, else into
+    the pinned bounce image."""
+    torch = _torch()
+    ev = torch.cuda.Event()
+    ev.record(compute)
+    d2h.wait_event(ev)
+    with torch.cuda.stream(d2h):
+        if direct:
+            _d2h(dev_out, host_out, a, b)
+        else:
+            flat = dev_out.reshape(-1).view(torch.uint8)
+            bounce[a:b].copy_(flat[a:b], non_blocking=True)
+
+
+def _fill_gaps(d2h, dev_out, bounce, groups, nbytes: int) -> None:
+    """The bounce image is copied to the host out whole: the bytes no slab
+    covers (rows before, between and after the groups) come from the device
+    twin, which holds the out's own values there (_resolve_out prefilled it),
+    so regions no item selects are carried through unchanged."""
+    torch = _torch()
+    flat = dev_out.reshape(-1).view(torch.uint8)
+    at = 0
+    with torch.cuda.stream(d2h):
+        for a, b, _ in sorted(groups, key=lambda g: g[0]):
+            if a > at:
+                bounce[at:a].copy_(flat[at:a], non_blocking=True)
+            at = max(at, b)
+        if at < nbytes:
+            bounce[at:nbytes].copy_(flat[at:nbytes], non_blocking=True)
 
 
 def _slab_groups(batch: list, dev_out, min_bytes: int = 8 << 20, max_groups: int = 8):

@@ -93,13 +93,26 @@ class Pending:
     Python GIL) and what the consuming launch must wait for.  ``finish()``
     (idempotent) joins the job, makes the launch stream wait for the copy
     stream, then runs the device-to-device copies of pieces that were already
-    on the device."""
+    on the device.
 
-    def __init__(self, dev, job, cs, post):
+    The job owns what it reads and writes (``keepalive``: the device buffer,
+    the pinned packing block, the host views and encoded file paths): a
+    begun job keeps running in a library thread until it is ended, so every
+    path that drops a Pending without consuming it -- an exception between
+    begin and launch, a slab loop that stops early -- must ``abort()`` it.
+    ``abort()`` joins the job and waits for its copies before the buffers can
+    go back to torch's caching allocators; ``__del__`` is the safety net."""
+
+    def __init__(self, dev, job, cs, post, keepalive=()):
         self.dev = dev
         self._job = job
         self._cs = cs
         self._post = post
+        self.keepalive = list(keepalive)
+
+    @property
+    def active(self) -> bool:
+        return self._job is not None
 
     def finish(self, stream: int | None = None) -> None:
         if self._job is None:
@@ -115,12 +128,37 @@ class Pending:
         # cs; handle 0 is the default stream and waits like any other
         rc = N.lib().zhip_stage_end(self._job, int(st.cuda_stream))
         self._job = None
-        N.check(rc, "zhip_stage_h2d")
+        if rc != 0:
+            # a failed job may have enqueued some copies: they must be done
+            # before the caller's exception frees the buffers they touch
+            self._cs.synchronize()
+            self._post = []
+            N.check(rc, "zhip_stage_h2d")
         if self._post:
             with torch.cuda.stream(st):
                 for fn in self._post:
                     fn(self.dev)
         self._post = []
+
+    def abort(self) -> None:
+        """End a job that will not be consumed: join the packing thread, wait
+        for every copy it enqueued; errors are swallowed (the caller is already
+        unwinding, or nobody will read the bytes)."""
+        job, self._job = self._job, None
+        self._post = []
+        if job is None:
+            return
+        try:
+            from . import _native as N
+
+            N.lib().zhip_stage_end(job, self._cs.cuda_stream)
+            self._cs.synchronize()
+        except Exception:  # pragma: no cover - interpreter shutdown
+            pass
+
+    def __del__(self):
+        if getattr(self, "_job", None) is not None:
+            self.abort()
 
 
 def stage(layout: StagingLayout, device, post=(), defer: bool = False):
@@ -161,12 +199,14 @@ def stage(layout: StagingLayout, device, post=(), defer: bool = False):
                                    WINDOW, _workers(), cs.cuda_stream)
     if not job:
         raise N.NativeError("zhip_stage_begin: out of memory")
-    pending = Pending(dev, job, cs, list(post))
+    # the pinned block and the host views must outlive the copies: the job
+    # holds them until it is finished or aborted, the program afterwards
+    # (dropped after its results() synchronised)
+    keep = [dev, host, views]
+    pending = Pending(dev, job, cs, list(post), keep)
     if not defer:
         pending.finish()
-    # the pinned block and the host views must outlive the copies: keep them
-    # with the program (dropped after its results() synchronised)
-    return dev, [dev, host, views], pending
+    return dev, keep, pending
 
 
 def gather_sources(batch: list, device, defer: bool = False, start: bool = True):

@@ -261,6 +261,11 @@ class DeviceArena:
         self.buf = self._alloc(_aligned(capacity) + TAIL_SLACK)
         self.top = 0
         self.version = 0
+        # placement generation: bumped by every reserve / free / grow, so a read
+        # planned against these offsets (a DecodeProgram, a ReadGraph, the
+        # pipeline's per-call plan cache) can tell that a key it reads may have
+        # moved or been reused (freed regions are handed out again at once)
+        self.gen = 0
         self.lock = threading.RLock()
         self._free: list[list[int]] = []  # [offset, nbytes], sorted, coalesced, ALIGN granules
 
@@ -291,11 +296,13 @@ class DeviceArena:
         nb[: self.top].copy_(self.buf[: self.top])
         self.buf = nb
         self.version += 1
+        self.gen += 1
 
     def reserve(self, nbytes: int) -> int:
         """Reserve an aligned region of at least nbytes; returns its offset."""
         need = max(_aligned(nbytes), ALIGN)
         with self.lock:
+            self.gen += 1
             for i, (off, n) in enumerate(self._free):
                 if n >= need:
                     if n == need:
@@ -317,6 +324,7 @@ class DeviceArena:
         if n <= 0:
             return
         with self.lock:
+            self.gen += 1
             fl = self._free
             lo, hi = 0, len(fl)
             while lo < hi:
