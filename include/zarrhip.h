@@ -365,6 +365,14 @@ int zhip_shard_pack(const zhip_plan *plan, void *dst, const zhip_shard *d_shards
                     const uint32_t *d_nonempty, uint32_t *d_newrank, const uint32_t *d_rank_of_slot,
                     uint64_t *d_blob_len, void *stream);
 
+/* Host CRC-32C (reflected 0x82F63B78, init / xorout 0xFFFFFFFF) of nbytes at
+ * data: the host stage of a chain, where the bytes never reach the GPU -- a
+ * crc32c after a host-side compressor (Crc32cCodec._decode_sync / _encode_sync,
+ * src/zarr/codecs/crc32c_.py:34-68, on compressed bytes) and the index of a
+ * shard whose inner chunks are compressed on the host
+ * (ShardingCodec._encode_shard_index_sync, sharding.py:633-640). */
+uint32_t zhip_crc32c_host(const void *data, uint64_t nbytes);
+
 /* CPU-only test hooks (no GPU needed). */
 int zhip_selftest(void);                                  /* 0 = all identities hold */
 uint32_t zhip_emulate_chunk_crc(const zhip_plan *plan, const uint8_t *data);

@@ -122,6 +122,29 @@ def crc32c_encode(chunk_bytes: np.ndarray) -> np.ndarray:
     return np.append(data, checksum.view("B"))
 
 
+def gzip_decode(chunk_bytes: np.ndarray) -> np.ndarray:
+    """GzipCodec._decode_sync (src/zarr/codecs/gzip.py:56-61) -> numcodecs.GZip.decode
+    (numcodecs 0.16, not vendored under /root/reference): a gzip member, else a
+    raw zlib stream; restated over the stdlib."""
+    import gzip
+    import zlib
+
+    b = _as_u8(chunk_bytes).tobytes()
+    out = gzip.decompress(b) if b[:2] == b"\x1f\x8b" else zlib.decompress(b)
+    return np.frombuffer(out, dtype=np.uint8)
+
+
+def gzip_encode(chunk_bytes: np.ndarray, level: int) -> np.ndarray:
+    """GzipCodec._encode_sync (gzip.py:70-75) -> numcodecs.GZip.encode: one gzip
+    member written by GzipFile at `level` with mtime 0 (byte identity with
+    numcodecs' header is unpinned here: numcodecs is absent; the round trip and
+    the decode of any valid member are what the tests rely on)."""
+    import gzip
+
+    return np.frombuffer(gzip.compress(_as_u8(chunk_bytes).tobytes(), compresslevel=level, mtime=0),
+                         dtype=np.uint8)
+
+
 def _stored_dtype(dtype: np.dtype, endian: str | None) -> np.dtype:
     if dtype.itemsize == 1 or endian is None:
         return dtype
@@ -173,7 +196,7 @@ class Chain:
     """A v3 codec list split as codecs_from_list does (codec_pipeline.py:859-944).
 
     aa: transpose orders (ArrayArray), ab: ("bytes", endian) or ("sharding", ShardSpec),
-    bb: tuple of "crc32c" (BytesBytes).
+    bb: "crc32c" or ("gzip", level) entries (BytesBytes), in chain order.
     """
 
     aa: tuple[tuple[int, ...], ...] = ()
@@ -196,6 +219,8 @@ class Chain:
                 endian = conf.get("endian")
             elif name == "crc32c":
                 bb.append("crc32c")
+            elif name == "gzip":
+                bb.append(("gzip", int(conf.get("level", 5))))
             elif name == "sharding_indexed":
                 shard = ShardSpec(
                     chunk_shape=tuple(conf["chunk_shape"]),
@@ -242,8 +267,11 @@ def chain_decode(chunk_bytes: np.ndarray, chain: Chain, spec: Spec) -> np.ndarra
         shape = transpose_resolve_shape(shape, order)
     data = _as_u8(chunk_bytes)
     for name in reversed(chain.bb):
-        assert name == "crc32c"
-        data = crc32c_decode(data)
+        if name == "crc32c":
+            data = crc32c_decode(data)
+        else:
+            assert name[0] == "gzip"
+            data = gzip_decode(data)
     if chain.shard is not None:
         arr = shard_decode(data, chain.shard, Spec(shape, spec.dtype, spec.fill_value,
                                                     spec.write_empty_chunks, spec.order))
@@ -269,12 +297,15 @@ def chain_encode(chunk_array: np.ndarray, chain: Chain, spec: Spec) -> np.ndarra
     else:
         data = bytes_encode(arr, chain.endian)
     for name in chain.bb:
-        data = crc32c_encode(data)
+        data = crc32c_encode(data) if name == "crc32c" else gzip_encode(data, name[1])
     return data
 
 
 def chain_encoded_size(nbytes: int, chain: Chain) -> int:
-    """compute_encoded_size: bytes +0, crc32c +4 (crc32c_.py:77-78)."""
+    """compute_encoded_size: bytes +0, crc32c +4 (crc32c_.py:77-78); gzip has
+    none (gzip.py:89-95)."""
+    if any(name != "crc32c" for name in chain.bb):
+        raise NotImplementedError("gzip output is not fixed-size")
     return nbytes + 4 * len(chain.bb)
 
 

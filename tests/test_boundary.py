@@ -37,10 +37,18 @@ def test_from_codecs_accepts_zarr_codec_objects():
 
 
 def test_unsupported_codec_is_loud():
+    """A compressor named only by its JSON form with no built-in here (zstd:
+    no module in this image) is refused; gzip has a built-in host stage; a
+    codec INSTANCE with sync methods runs through them (HostCodec)."""
     from zarr_hip import HipCodecPipeline
+    from zarr_hip.codecs import GzipCodec, HostCodec
 
-    with pytest.raises(NotImplementedError, match="gzip"):
-        HipCodecPipeline.from_codecs([LE, Z.FakeCodec({"name": "gzip", "configuration": {"level": 5}})])
+    with pytest.raises(NotImplementedError, match="zstd"):
+        HipCodecPipeline.from_codecs([LE, Z.FakeCodec({"name": "zstd", "configuration": {"level": 5}})])
+    p = HipCodecPipeline.from_codecs([LE, Z.FakeCodec({"name": "gzip", "configuration": {"level": 5}})])
+    assert isinstance(p.bytes_bytes_codecs[0], GzipCodec) and p.bytes_bytes_codecs[0].level == 5
+    p = HipCodecPipeline.from_codecs([LE, Z.LzmaCodec()])
+    assert isinstance(p.bytes_bytes_codecs[0], HostCodec) and p.bytes_bytes_codecs[0].name == "numcodecs.lzma"
 
 
 def test_zarr_array_spec_and_zdtype_coerced():

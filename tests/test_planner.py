@@ -102,7 +102,35 @@ def test_codec_order_errors():
     with pytest.raises(TypeError):
         C.split_codecs(C.parse_codecs([{"name": "crc32c"}, {"name": "bytes"}]))
     with pytest.raises(NotImplementedError):
-        C.parse_codecs([{"name": "gzip", "configuration": {"level": 1}}])
+        C.parse_codecs([{"name": "zstd", "configuration": {"level": 1}}])
+    with pytest.raises(TypeError):  # a compressor is a BytesBytesCodec too
+        C.split_codecs(C.parse_codecs([{"name": "gzip", "configuration": {"level": 1}}, {"name": "bytes"}]))
+    with pytest.raises(ValueError):
+        C.parse_codecs([{"name": "gzip", "configuration": {"level": 11}}])
+
+
+def test_split_host_tail():
+    """The host stage starts at the first compressor; a crc32c after it stays
+    on the host (it checks the compressed bytes); every bytes->bytes codec
+    after a sharding codec is host-side."""
+    LE = {"name": "bytes", "configuration": {"endian": "little"}}
+    GZ = {"name": "gzip", "configuration": {"level": 1}}
+    CRC = {"name": "crc32c"}
+    T = {"name": "transpose", "configuration": {"order": [1, 0]}}
+    SH = {"name": "sharding_indexed", "configuration": {"chunk_shape": [2, 2], "codecs": [LE, GZ]}}
+
+    def names(cs):
+        return [c.to_dict()["name"] for c in cs]
+
+    for chain, gpu, host in [([LE, CRC], ["bytes", "crc32c"], []),
+                             ([LE, GZ], ["bytes"], ["gzip"]),
+                             ([T, LE, CRC, GZ], ["transpose", "bytes", "crc32c"], ["gzip"]),
+                             ([LE, GZ, CRC], ["bytes"], ["gzip", "crc32c"]),
+                             ([SH, CRC], ["sharding_indexed"], ["crc32c"])]:
+        g, h = C.split_host_tail(C.parse_codecs(chain))
+        assert names(g) == gpu and names(h) == host, chain
+    sh = C.parse_codecs([SH])[0]
+    assert names(C.split_host_tail(sh.codecs)[1]) == ["gzip"]
 
 
 def _sharded_headline_tables(loc="end", shape=(256, 256, 256), shards=(128, 128, 128),

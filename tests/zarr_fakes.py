@@ -251,3 +251,76 @@ def batch_for(meta_shape, chunk_shape, selection, store, spec):
     batch = [(StorePath(store, "/".join(map(str, ("c",) + c))), spec, cs, os_, comp)
              for c, cs, os_, comp in projections]
     return batch, out_shape
+
+
+class GzipCodec:
+    """zarr's GzipCodec (src/zarr/codecs/gzip.py:31-95) as the pipeline sees it:
+    a BytesBytesCodec instance whose sync methods run numcodecs.GZip through
+    as_numpy_array_wrapper (src/zarr/core/buffer/cpu.py:194-219) -- here over
+    the stdlib (numcodecs is absent).  Counts its calls."""
+
+    is_fixed_size = False
+
+    def __init__(self, *, level: int = 5):
+        self.level = level
+        self.calls = {"decode": 0, "encode": 0}
+
+    def to_dict(self) -> dict:
+        return {"name": "gzip", "configuration": {"level": self.level}}
+
+    def evolve_from_array_spec(self, array_spec):
+        return self
+
+    def _decode_sync(self, chunk_bytes, chunk_spec):
+        import gzip
+
+        self.calls["decode"] += 1
+        return chunk_spec.prototype.buffer.from_bytes(gzip.decompress(chunk_bytes.as_numpy_array().tobytes()))
+
+    def _encode_sync(self, chunk_bytes, chunk_spec):
+        import gzip
+
+        self.calls["encode"] += 1
+        return chunk_spec.prototype.buffer.from_bytes(
+            gzip.compress(chunk_bytes.as_numpy_array().tobytes(), compresslevel=self.level, mtime=0))
+
+    def compute_encoded_size(self, n, spec):
+        raise NotImplementedError
+
+
+class LzmaCodec(GzipCodec):
+    """A compressor this package has no built-in for (zarr's numcodecs wrapper
+    naming, "numcodecs.lzma"): only the instance can run it."""
+
+    def to_dict(self) -> dict:
+        return {"name": "numcodecs.lzma", "configuration": {"preset": 1}}
+
+    def _decode_sync(self, chunk_bytes, chunk_spec):
+        import lzma
+
+        self.calls["decode"] += 1
+        return chunk_spec.prototype.buffer.from_bytes(lzma.decompress(chunk_bytes.as_numpy_array().tobytes()))
+
+    def _encode_sync(self, chunk_bytes, chunk_spec):
+        import lzma
+
+        self.calls["encode"] += 1
+        return chunk_spec.prototype.buffer.from_bytes(
+            lzma.compress(chunk_bytes.as_numpy_array().tobytes(), preset=1))
+
+
+class ShardingCodec:
+    """zarr's ShardingCodec instance surface (sharding.py:402-539): attributes
+    holding the inner codec INSTANCES, plus to_dict."""
+
+    def __init__(self, chunk_shape, codecs, index_codecs=None, index_location="end"):
+        self.chunk_shape = tuple(chunk_shape)
+        self.codecs = tuple(codecs)
+        self.index_codecs = tuple(index_codecs or (FakeCodec({"name": "bytes", "configuration": {"endian": "little"}}),
+                                                   FakeCodec({"name": "crc32c"})))
+        self.index_location = index_location
+
+    def to_dict(self) -> dict:
+        return {"name": "sharding_indexed", "configuration": {
+            "chunk_shape": list(self.chunk_shape), "codecs": [c.to_dict() for c in self.codecs],
+            "index_codecs": [c.to_dict() for c in self.index_codecs], "index_location": self.index_location}}

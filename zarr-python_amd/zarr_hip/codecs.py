@@ -8,6 +8,13 @@ their compute lives in the HIP kernels, driven by ``pipeline.HipCodecPipeline``.
   Crc32cCodec     src/zarr/codecs/crc32c_.py:20-78
   TransposeCodec  src/zarr/codecs/transpose.py:29-128
   ShardingCodec   src/zarr/codecs/sharding.py:402-1756 (configuration + layout rules)
+
+Compression codecs stay on the host (the north star): ``GzipCodec`` (the
+``gzip`` name from JSON metadata, stdlib gzip as numcodecs.GZip) and
+``HostCodec`` (any bytes->bytes codec INSTANCE a caller hands over -- zarr's
+GzipCodec / ZstdCodec / BloscCodec -- driven through its own ``_decode_sync`` /
+``_encode_sync``, src/zarr/abc/codec.py:69-96) form the host stage of a chain
+(``split_host_tail``); hoststage.py runs it, the GPU runs the rest.
 """
 
 from __future__ import annotations
@@ -236,11 +243,193 @@ class ShardingCodec:
         raise NotImplementedError("sharding_indexed output is not fixed-size")
 
 
+@dataclass(frozen=True)
+class GzipCodec:
+    """src/zarr/codecs/gzip.py:31-95 on the host: numcodecs.GZip's stream (a gzip
+    member, mtime 0) for encode; decode takes a gzip member or, as
+    numcodecs.GZip.decode does, a raw zlib stream."""
+
+    level: int = 5
+    is_fixed_size = False
+    host = True
+
+    def __post_init__(self):
+        lv = self.level
+        if isinstance(lv, bool) or not isinstance(lv, int):
+            raise TypeError(f"Expected an integer. Got {lv!r} instead.")
+        if lv not in range(10):
+            raise ValueError(f"Expected an integer from the inclusive range (0, 9). Got {lv} instead.")
+
+    @classmethod
+    def from_dict(cls, data: Any) -> "GzipCodec":
+        conf = _named(data, "gzip")
+        return cls(level=conf.get("level", 5))
+
+    def to_dict(self) -> dict:
+        return {"name": "gzip", "configuration": {"level": self.level}}
+
+    def evolve_from_array_spec(self, spec: ArraySpec) -> "GzipCodec":
+        return self
+
+    def resolve_metadata(self, spec: ArraySpec) -> ArraySpec:
+        return spec
+
+    def compute_encoded_size(self, n: int, spec: ArraySpec | None = None) -> int:
+        raise NotImplementedError  # gzip.py:89-95
+
+    def validate(self, **kw) -> None:
+        return None
+
+    def decode_bytes(self, data, spec: ArraySpec | None = None) -> bytes:
+        import gzip
+        import zlib
+
+        b = bytes(data)
+        if b[:2] == b"\x1f\x8b":
+            return gzip.decompress(b)
+        return zlib.decompress(b)
+
+    def encode_bytes(self, data, spec: ArraySpec | None = None) -> bytes:
+        import gzip
+
+        return gzip.compress(bytes(data), compresslevel=self.level, mtime=0)
+
+
+class _HostBuffer:
+    """The slice of zarr's Buffer API a bytes->bytes codec uses on the host
+    (as_numpy_array / to_bytes / from_bytes, src/zarr/core/buffer/cpu.py), for
+    specs that carry no prototype of their own."""
+
+    def __init__(self, data):
+        self._a = np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray) else \
+            np.ascontiguousarray(data).reshape(-1).view(np.uint8)
+
+    @classmethod
+    def from_bytes(cls, b) -> "_HostBuffer":
+        return cls(b)
+
+    @classmethod
+    def from_array_like(cls, a) -> "_HostBuffer":
+        return cls(np.asarray(a))
+
+    def as_numpy_array(self) -> np.ndarray:
+        return self._a
+
+    def as_array_like(self) -> np.ndarray:
+        return self._a
+
+    def to_bytes(self) -> bytes:
+        return self._a.tobytes()
+
+    def __len__(self) -> int:
+        return int(self._a.size)
+
+
+class _HostPrototype:
+    buffer = _HostBuffer
+    nd_buffer = None
+
+
+HOST_PROTOTYPE = _HostPrototype()
+
+
+@dataclass(frozen=True)
+class HostCodec:
+    """A caller-supplied bytes->bytes codec instance (zarr's GzipCodec,
+    ZstdCodec, BloscCodec, ... -- nothing of zarr or numcodecs is imported
+    here): the pipeline calls its ``_decode_sync`` / ``_encode_sync``
+    (SupportsSyncCodec, src/zarr/abc/codec.py:69-96) on the host with a host
+    Buffer and the chunk's spec, outside the GPU launch."""
+
+    codec: Any
+    is_fixed_size = False
+    host = True
+
+    def to_dict(self) -> dict:
+        return self.codec.to_dict()
+
+    @property
+    def name(self) -> str:
+        d = self.to_dict()
+        return d if isinstance(d, str) else d.get("name", type(self.codec).__name__)
+
+    def evolve_from_array_spec(self, spec: ArraySpec) -> "HostCodec":
+        src = getattr(spec, "source", None)
+        ev = getattr(self.codec, "evolve_from_array_spec", None)
+        if ev is None or src is None:  # only zarr's own spec type is safe to hand it
+            return self
+        new = ev(src)
+        return self if new is self.codec else HostCodec(new)
+
+    def resolve_metadata(self, spec: ArraySpec) -> ArraySpec:
+        return spec
+
+    def compute_encoded_size(self, n: int, spec: ArraySpec | None = None) -> int:
+        fn = getattr(self.codec, "compute_encoded_size", None)
+        if fn is None:
+            raise NotImplementedError
+        return fn(n, getattr(spec, "source", None) or spec)
+
+    def validate(self, **kw) -> None:
+        return None
+
+    def _spec(self, spec: ArraySpec | None):
+        src = getattr(spec, "source", None)
+        if src is not None:
+            return src
+        if spec is None:
+            return ArraySpec((0,), np.dtype("u1"), 0, prototype=HOST_PROTOTYPE)
+        return spec if spec.prototype is not None and hasattr(getattr(spec.prototype, "buffer", None),
+                                                              "from_bytes") else replace(spec, prototype=HOST_PROTOTYPE)
+
+    def decode_bytes(self, data, spec: ArraySpec | None = None) -> bytes:
+        sp = self._spec(spec)
+        out = self.codec._decode_sync(sp.prototype.buffer.from_bytes(bytes(data)), sp)
+        return _to_bytes(out)
+
+    def encode_bytes(self, data, spec: ArraySpec | None = None) -> bytes:
+        sp = self._spec(spec)
+        out = self.codec._encode_sync(sp.prototype.buffer.from_bytes(bytes(data)), sp)
+        if out is None:
+            raise ValueError(f"host codec {self.name!r} returned no bytes")
+        return _to_bytes(out)
+
+
+def _to_bytes(buf) -> bytes:
+    if isinstance(buf, (bytes, bytearray, memoryview)):
+        return bytes(buf)
+    if hasattr(buf, "to_bytes"):
+        return buf.to_bytes()
+    return np.ascontiguousarray(buf.as_numpy_array()).reshape(-1).view(np.uint8).tobytes()
+
+
+def is_host_codec(c) -> bool:
+    return getattr(c, "host", False) is True
+
+
+def split_host_tail(codecs) -> tuple[tuple, tuple]:
+    """(GPU part, host stage) of a chain: the bytes->bytes codecs from the
+    first host codec on run on the host (a crc32c after a compressor checks
+    the compressed bytes, so it stays in that order); every bytes->bytes codec
+    after a sharding codec does too (the GPU path reads shard blobs as stored)."""
+    codecs = tuple(codecs)
+    ab_at = next((i for i, c in enumerate(codecs) if isinstance(c, (BytesCodec, ShardingCodec))), None)
+    if ab_at is None:
+        return codecs, ()
+    cut = len(codecs)
+    for i in range(ab_at + 1, len(codecs)):
+        if is_host_codec(codecs[i]) or isinstance(codecs[ab_at], ShardingCodec):
+            cut = i
+            break
+    return codecs[:cut], codecs[cut:]
+
+
 _REGISTRY = {
     "bytes": BytesCodec,
     "crc32c": Crc32cCodec,
     "transpose": TransposeCodec,
     "sharding_indexed": ShardingCodec,
+    "gzip": GzipCodec,
 }
 
 
@@ -253,15 +442,32 @@ def parse_codecs(codecs) -> list:
     carried over from the instance."""
     out = []
     for c in codecs:
-        if isinstance(c, (BytesCodec, Crc32cCodec, TransposeCodec, ShardingCodec)):
+        if isinstance(c, (BytesCodec, Crc32cCodec, TransposeCodec, ShardingCodec, GzipCodec, HostCodec)):
             out.append(c)
             continue
         conf = c.to_dict() if hasattr(c, "to_dict") and not isinstance(c, dict) else c
         name = conf if isinstance(conf, str) else conf["name"]
+        if name not in ("bytes", "crc32c", "transpose", "sharding_indexed") and not isinstance(c, (dict, str)) \
+                and hasattr(c, "_decode_sync") and hasattr(c, "_encode_sync"):
+            # a compressor instance (zarr's GzipCodec / ZstdCodec / BloscCodec ...):
+            # its own sync methods run the host stage, exactly as the reference does
+            out.append(HostCodec(c))
+            continue
         if name not in _REGISTRY:
             raise NotImplementedError(
-                f"codec {name!r} is not on the GPU fixed-size path (compression stays on the host)")
-        parsed = _REGISTRY[name].from_dict(conf)
+                f"codec {name!r} needs its codec object (compression runs on the host through the "
+                f"instance zarr passes to from_codecs; no built-in {name!r} implementation here)")
+        if name == "sharding_indexed" and not isinstance(c, (dict, str)) and hasattr(c, "codecs"):
+            # zarr's ShardingCodec: keep its inner codec INSTANCES (to_dict would
+            # flatten a compressor to its JSON name and lose the object that
+            # runs it)
+            loc = getattr(c, "index_location", "end")
+            parsed = ShardingCodec(chunk_shape=tuple(c.chunk_shape), codecs=tuple(c.codecs),
+                                   index_codecs=tuple(getattr(c, "index_codecs", None)
+                                                      or (BytesCodec(endian="little"), Crc32cCodec())),
+                                   index_location=str(getattr(loc, "value", loc)))
+        else:
+            parsed = _REGISTRY[name].from_dict(conf)
         order = getattr(c, "subchunk_write_order", None)
         if isinstance(parsed, ShardingCodec) and order is not None and not isinstance(c, dict):
             parsed = replace(parsed, subchunk_write_order=str(order))
@@ -291,7 +497,7 @@ def split_codecs(codecs) -> tuple[tuple, Any, tuple]:
             if ab is not None:
                 raise ValueError("Only one ArrayBytesCodec is allowed.")
             ab = c
-        elif isinstance(c, Crc32cCodec):
+        elif isinstance(c, Crc32cCodec) or is_host_codec(c):
             if ab is None:
                 raise TypeError("BytesBytesCodec must come after the ArrayBytesCodec")
             bb.append(c)

@@ -24,7 +24,7 @@ import numpy as np
 
 from . import _native as N
 from . import staging
-from .codecs import ShardingCodec, evolve_codecs, parse_codecs, split_codecs
+from .codecs import ShardingCodec, evolve_codecs, parse_codecs, split_codecs, split_host_tail
 from .interop import device_tensor, host_array
 from .planner import CHUNK_DT, SEL_DT, STATUS_DT, ChainInfo, Tables, analyze_chain, plan_decode, predict_rows
 from .spec import ArraySpec, GetResult, coerce_spec
@@ -454,6 +454,7 @@ class HipCodecPipeline:
     # per-call plan cache for device-resident reads (read_sync): batch key ->
     # DecodeProgram; entries hold tables, never outs (retargeted per call)
     _read_cache: dict = field(default_factory=dict, compare=False, hash=False, repr=False)
+    _aux: dict = field(default_factory=dict, compare=False, hash=False, repr=False)
 
     @classmethod
     def from_codecs(cls, codecs: Iterable, *, batch_size: int | None = None) -> "HipCodecPipeline":
@@ -488,6 +489,78 @@ class HipCodecPipeline:
 
     def __iter__(self):
         return iter(self.codecs)
+
+    # ---------------------------------------------------------- host stage
+    def _host_split(self):
+        """None for an all-GPU chain, else (outer host stage, inner host stage of
+        the sharding codec, the GPU pipeline for reads -- the chain without the
+        outer stage, its sharding codec still naming the inner stage, which
+        prepare_read runs per inner chunk -- and the GPU pipeline for writes,
+        without either stage: hoststage.TranscodingByteSetter converts).
+        Compression codecs stay on the host (hoststage.py)."""
+        aux = self._aux
+        if "split" not in aux:
+            fixed, outer = split_host_tail(self.codecs)
+            ab = self.array_bytes_codec
+            inner = split_host_tail(ab.codecs)[1] if isinstance(ab, ShardingCodec) else ()
+            if not outer and not inner:
+                aux["split"] = None
+            else:
+                read_pipe = self._sub(fixed) if outer else None
+                wfixed = tuple(replace(c, codecs=split_host_tail(c.codecs)[0]) if isinstance(c, ShardingCodec)
+                               else c for c in fixed)
+                aux["split"] = (outer, inner, read_pipe, self._sub(wfixed))
+        return aux["split"]
+
+    def _sub(self, codecs) -> "HipCodecPipeline":
+        aa, ab, bb = split_codecs(codecs)
+        return type(self)(tuple(codecs), aa, ab, bb, self.batch_size, self.predict_loads)
+
+    def _host_read_batch(self, batch: list, outer: tuple) -> list:
+        """Items whose getters return the stored bytes -> items over the
+        fixed-size bytes the outer host stage yields (decoded once per stored
+        object, on the host-stage pool)."""
+        from . import hoststage
+
+        keys, firsts = {}, []
+        for it in batch:
+            bg = it[0]
+            k = (id(getattr(bg, "store", None)), getattr(bg, "path", None)) if getattr(bg, "path", None) \
+                is not None else ("obj", id(bg))
+            if k not in keys:
+                keys[k] = len(firsts)
+                firsts.append(bg)
+        spec = batch[0][1]
+
+        def one(bg):
+            raw = bg.get_sync(prototype=None) if hasattr(bg, "get_sync") else bg
+            if raw is None:
+                return None
+            return hoststage.decode_tail(staging.staged_host(raw), outer, spec)
+
+        dec = hoststage.map_host(one, firsts)
+        out = []
+        for it in batch:
+            bg = it[0]
+            k = (id(getattr(bg, "store", None)), getattr(bg, "path", None)) if getattr(bg, "path", None) \
+                is not None else ("obj", id(bg))
+            out.append((_Raw(dec[keys[k]]),) + tuple(it[1:]))
+        return out
+
+    def _inner_decoder(self, chain, spec):
+        """The per-inner-chunk host stage of a sharded chain, as the staging
+        hook (list of stored inner-chunk bytes -> fixed-size bytes)."""
+        if not chain.inner_host:
+            return None
+        from . import hoststage
+
+        tail = chain.inner_host
+        ispec = chain.shard.inner_spec(spec)
+
+        def dec(bufs):
+            return hoststage.decode_many(list(bufs), tail, ispec)
+
+        return dec
 
     @property
     def supports_partial_decode(self) -> bool:
@@ -558,6 +631,9 @@ class HipCodecPipeline:
             raise ValueError("empty batch")
         if not isinstance(out, torch.Tensor) or not out.is_cuda:
             raise TypeError("HipCodecPipeline.read needs a device-resident out (torch CUDA tensor)")
+        hs = self._host_split()
+        if hs is not None and hs[0]:
+            return hs[2].prepare_read(self._host_read_batch(batch, hs[0]), out, drop_axes, item_out_extra)
         ss = self._shard_space(batch, out, drop_axes)
         if ss is not None:
             pipe, batch_s, out_s = ss
@@ -571,11 +647,14 @@ class HipCodecPipeline:
         resolved = None
         # host-resident bytes are packed and copied on the stager thread while
         # this thread plans; the launch waits for them (DecodeProgram.pending)
-        if chain.shard is not None and not _device_resident(batch):
+        # (a sharded chain whose inner chunks pass a host stage always reads
+        # through the host: the touched inner chunks are decoded there first)
+        if chain.shard is not None and (chain.inner_host or not _device_resident(batch)):
             sh = chain.shard
             cps = sh.chunks_per_shard(spec.shape)
             src, size, item_missing, resolved, keep, pending = staging.gather_sharded_partial(
-                batch, sh, cps, int(np.prod(cps)), sh.chunk_shape, spec, device, defer=True)
+                batch, sh, cps, int(np.prod(cps)), sh.chunk_shape, spec, device, defer=True,
+                inner_decode=self._inner_decoder(chain, spec))
             srcs = [(0, 0, bool(m)) for m in item_missing]
         else:
             src, size, srcs, keep, pending = staging.gather_sources(batch, device, defer=True)
@@ -617,8 +696,11 @@ class HipCodecPipeline:
         batch = normalize_batch(batch_info)
         if not batch:
             return ()
+        hs = self._host_split()
+        if hs is not None and hs[0]:  # the outer host stage first, then the GPU chain
+            return hs[2].read_sync(self._host_read_batch(batch, hs[0]), out, drop_axes)
         dev_out, host_out = _resolve_out(out, batch, drop_axes)
-        if host_out is None and READ_CACHE_SIZE:
+        if host_out is None and READ_CACHE_SIZE and hs is None:
             key = _read_key(batch, dev_out, drop_axes)
             if key is not None:
                 return self._read_cached(key, batch, dev_out, drop_axes)
@@ -802,6 +884,9 @@ class HipCodecPipeline:
         if not batch:
             return
         value = _resolve_value(value)
+        hs = self._host_split()
+        if hs is not None and (hs[0] or not self.array_array_codecs):
+            return self._host_write(batch, value, drop_axes, partial_encode, hs)
         ss = self._shard_space(batch, value, drop_axes)
         if ss is not None:
             pipe, batch_s, value_s = ss
@@ -817,6 +902,23 @@ class HipCodecPipeline:
         with torch.cuda.device(device):
             w = ChunkWriter(self.codecs, spec, None or spec.shape, device)
             w.write(batch, value, self.codecs, drop_axes, partial_encode=partial_encode)
+
+    def _host_write(self, batch, value, drop_axes, partial_encode, hs) -> None:
+        """Writes through a host stage: the GPU encodes the fixed-size chain;
+        each setter converts between that and the stored form on the host
+        (hoststage.TranscodingByteSetter: the outer stage, and for a sharding
+        codec with an inner stage the shard re-pack)."""
+        from . import hoststage
+
+        outer, inner, _, wpipe = hs
+        spec: ArraySpec = batch[0][1]
+        tr = None
+        if inner:
+            ab = self.array_bytes_codec
+            tr = hoststage.ShardTranscoder(replace(ab, codecs=split_host_tail(ab.codecs)[0]), spec.shape,
+                                           inner, ab.inner_spec(spec))
+        wrapped = [(hoststage.TranscodingByteSetter(it[0], outer, tr, spec),) + tuple(it[1:]) for it in batch]
+        return wpipe._write_sync(wrapped, value, drop_axes, partial_encode)
 
     async def write(self, batch_info: Iterable, value, drop_axes: tuple = ()) -> None:
         await asyncio.to_thread(self.write_sync, list(batch_info), value, drop_axes)

@@ -15,7 +15,8 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from . import _native as N
-from .codecs import BytesCodec, Crc32cCodec, ShardingCodec, TransposeCodec, split_codecs
+from .codecs import BytesCodec, Crc32cCodec, ShardingCodec, TransposeCodec, is_host_codec, split_codecs, \
+    split_host_tail
 from .indexing import basic_projections
 from .indexing import morton_order
 from .spec import ArraySpec
@@ -31,12 +32,19 @@ class ChainInfo:
     swap: bool                    # bytes codec endian != native
     crc: bool                     # trailing crc32c
     endian: str | None
-    shard: ShardingCodec | None = None
+    shard: ShardingCodec | None = None      # the sharding codec with its GPU inner chain
     inner: "ChainInfo | None" = None
+    # the inner chain's host stage (compressors, anything after them): inner
+    # chunks pass through it on the host before their fixed-size part decodes
+    # on the GPU (hoststage.py)
+    inner_host: tuple = ()
 
 
 def analyze_chain(codecs, spec: ArraySpec) -> ChainInfo:
     aa, ab, bb = split_codecs(codecs)
+    if any(is_host_codec(c) for c in bb):
+        raise NotImplementedError("the host stage of this chain must be split off first "
+                                  "(HipCodecPipeline runs it on the host: hoststage.py)")
     if len(bb) > 1 or any(not isinstance(c, Crc32cCodec) for c in bb):
         raise NotImplementedError("only a single trailing crc32c bytes->bytes codec is supported")
     perm = tuple(range(spec.ndim))
@@ -54,14 +62,19 @@ def analyze_chain(codecs, spec: ArraySpec) -> ChainInfo:
             raise NotImplementedError(
                 "bytes->bytes codecs around sharding_indexed are not on the GPU path")
         inner_spec = ab.inner_spec(spec)
-        inner = analyze_chain(ab.codecs, inner_spec)
+        fixed, tail = split_host_tail(ab.codecs)
+        if tail:
+            from dataclasses import replace as _replace
+
+            ab = _replace(ab, codecs=fixed)
+        inner = analyze_chain(fixed, inner_spec)
         if inner.shard is not None:
             raise NotImplementedError("nested sharding is not on the GPU path yet")
         ia, iab, ibb = split_codecs(ab.index_codecs)
         if ia or not isinstance(iab, BytesCodec) or iab.endian not in (None, "little") or \
-                len(ibb) > 1:
+                len(ibb) > 1 or any(not isinstance(c, Crc32cCodec) for c in ibb):
             raise NotImplementedError("shard index codecs must be [bytes(little)] + optional crc32c")
-        return ChainInfo(tuple(perm), False, False, None, ab, inner)
+        return ChainInfo(tuple(perm), False, False, None, ab, inner, tuple(tail))
     assert isinstance(ab, BytesCodec)
     ab = ab.evolve_from_array_spec(spec)
     return ChainInfo(perm, ab.needs_swap(spec.dtype), len(bb) == 1, ab.endian)

@@ -3,7 +3,7 @@ src/zarr/abc/codec.py:40-43)."""
 
 from __future__ import annotations
 
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 from typing import Any, Literal, TypedDict
 
 import numpy as np
@@ -31,6 +31,9 @@ class ArraySpec:
     fill_value: Any
     config: ArrayConfig = ArrayConfig()
     prototype: Any = None
+    # the caller's own spec object (zarr's ArraySpec) this one was made from:
+    # host-stage codec instances are handed that one (HostCodec)
+    source: Any = field(default=None, compare=False, hash=False, repr=False)
 
     def __post_init__(self):
         object.__setattr__(self, "shape", tuple(int(s) for s in self.shape))
@@ -86,4 +89,5 @@ def coerce_spec(spec) -> ArraySpec:
     if hasattr(fv, "item") and not isinstance(fv, np.generic):
         fv = fv.item()
     return ArraySpec(tuple(int(s) for s in spec.shape), native_dtype(spec.dtype), fv,
-                     coerce_config(getattr(spec, "config", None)), getattr(spec, "prototype", None))
+                     coerce_config(getattr(spec, "config", None)), getattr(spec, "prototype", None),
+                     source=spec)

@@ -277,9 +277,12 @@ def _shard_key(bg):
 
 
 def gather_sharded_partial(batch: list, sh, cps, n_inner: int, inner_shape, spec, device,
-                           defer: bool = False):
+                           defer: bool = False, inner_decode=None):
     """Host-sourced sharded batch: index by range request, touched inner chunks
-    by coalesced range requests, staged into one device buffer.
+    by coalesced range requests, staged into one device buffer.  With
+    ``inner_decode`` (a list of inner-chunk bytes -> their fixed-size bytes:
+    the inner chain's host stage, hoststage.py) every fetched inner chunk
+    passes through it on the host before it is staged.
 
     Returns (src, size, item_missing[n_items], resolved, keepalive) where
     resolved[i] = (src_by_slot, len_by_slot, miss_by_slot, index_src_or_-1)."""
@@ -325,7 +328,7 @@ def gather_sharded_partial(batch: list, sh, cps, n_inner: int, inner_shape, spec
                 continue  # missing inner chunk -> fill (sharding.py:700-712)
             reqs.append(Range(int(o), int(o) + int(n)))
             want.append(slot)
-        if reqs and st is not None and hasattr(st, "locate_sync"):
+        if reqs and st is not None and hasattr(st, "locate_sync") and inner_decode is None:
             # a local file: each touched inner chunk is one pread of the shard
             # file by the staging pool (no coalescing needed: no request cost)
             whole = st.locate_sync(bg.path)
@@ -353,9 +356,13 @@ def gather_sharded_partial(batch: list, sh, cps, n_inner: int, inner_shape, spec
                     raise
                 out_of_shard[k] = None
                 continue
-            for j, buf in got:
+            got = list(got)
+            bufs = [staged_host(buf) for _, buf in got]
+            if inner_decode is not None:
+                bufs = inner_decode(bufs)
+            for (j, _), buf in zip(got, bufs):
                 slot = want[j]
-                off, n = lay.add(staged_host(buf))
+                off, n = lay.add(buf)
                 src_by[slot], len_by[slot], miss_by[slot] = off, n, False
         out_of_shard[k] = (src_by, len_by, miss_by, idx_off)
     dev, keep, pending = stage(lay, device, defer=defer)
