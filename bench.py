@@ -15,13 +15,13 @@ working set) steps rotate over 4 independent replicas (inputs + outputs).
 Multi-GPU (one process per GPU, torchrun): chunks are independent, so ONE batch
 is partitioned across the ranks with no collective on the data path (the
 reference's disjoint-output pool map, src/zarr/core/codec_pipeline.py:
-1104-1109, 1169-1171).  The headline's global batch at N ranks is the
-(256N) x 256 x 256 array (8N shards), split round-robin by shard
-(zarr_hip.parallel.rank_batch): every rank stages and decodes only its own 8
-shards, so per-GPU work is fixed (weak scaling) and N=1 is exactly the
-headline.  The C4 (1024^3) and C5 (2048^3, 10 % inner chunks) legs split their
-fixed batch round-robin by shard (strong scaling).  RCCL carries only the
-barrier and the max-over-ranks of the timed wall.
+1104-1109, 1169-1171).  The headline stays BASELINE's array at every N: its 8
+shards are split round-robin over the ranks (zarr_hip.parallel.rank_batch;
+8/N shards per rank, strong scaling).  extra.headline_weak (N > 1) keeps the
+(256N) x 256 x 256 array with 8 shards per rank (weak scaling).  The C4
+(1024^3) and C5 (2048^3, 10 % inner chunks) legs split their fixed batch
+round-robin by shard (strong scaling).  RCCL carries only the barrier and the
+max-over-ranks of the timed wall.
 
 Prints ONE JSON line (rank 0) with the driver's contract fields plus
 "roofline" (dominant kernel vs 8 TB/s HBM, per-launch kernel time from HIP
@@ -824,37 +824,56 @@ def pmc_traffic():
 
 # ------------------------------------------------------------------------ main
 
-def headline(ctx, args):
-    """The headline batch partitioned round-robin by shard (weak scaling: the
-    global array is (256N) x 256 x 256, every rank owns 8 shards = one 256^3
-    array's worth).  Returns (programs, decoded bytes per step on this rank,
-    algorithmic bytes per launch on this rank)."""
+def headline(ctx, args, weak: bool = False):
+    """The headline batch -- BASELINE's 256^3 f32 array in 128^3 shards of 64^3
+    inner chunks -- partitioned round-robin by shard over the ranks (strong
+    scaling: the array is fixed, each of N ranks owns 8/N of its 8 shards).
+    With ``weak`` the global array is (256N) x 256 x 256 and every rank owns 8
+    shards (one 256^3 array's worth; reported under extra at N > 1).  Returns
+    (programs, decoded bytes per step on this rank, algorithmic bytes per
+    launch on this rank)."""
     import torch
 
     g = W.HEADLINE
     shape1, shards, inner = g["shape"], g["shards"], g["inner"]
     data = synthetic(shape1, seed=0)
     src = torch.from_numpy(data).to(ctx.device)
-    if ctx.world > 1:
-        src = src.repeat(ctx.world, 1, 1)
-    shape = (shape1[0] * ctx.world,) + shape1[1:]
+    rep = ctx.world if weak else 1
+    if rep > 1:
+        src = src.repeat(rep, 1, 1)
+    shape = (shape1[0] * rep,) + shape1[1:]
     blob = 8 * (1048576 + 4) + 8 * 16 + 4
+    n_shards = 8 * rep
+    mine_n = len(range(ctx.rank, n_shards, ctx.world))
     progs = []
     for r in range(args.replicas):
         prog, out, mine = build_partitioned(ctx, src, shape, inner, shards, "float32", 0.0,
-                                            8 * (blob + 256) + (1 << 20))
+                                            max(mine_n, 1) * (blob + 256) + (1 << 20))
         if r == 0:  # correctness gate: every decoded byte of this rank's shards
             prog.launch()
             prog.results()
             check_regions(out, src, mine, "headline")
-        assert len(mine) == 8, "every rank owns 8 shards of the headline batch"
+        assert len(mine) == mine_n, "round-robin by shard"
         assert prog.tables.fast and prog.tables.rows, "the headline should take the whole-row kernel"
-        assert prog.index is None and prog.data.n_idx == 8, "index CRC checks should be fused"
+        assert prog.index is None and prog.data.n_idx == mine_n, "index CRC checks should be fused"
         progs.append(prog)
     del src
-    decoded = data.nbytes
-    encoded = 64 * (1048576 + 4) + 8 * (8 * 16 + 4)  # inner chunks + 8 shard indexes
+    decoded = mine_n * int(np.prod(shards)) * 4
+    encoded = mine_n * blob  # this rank's inner chunks + shard indexes
     return progs, decoded, encoded
+
+
+def headline_weak(ctx, args):
+    """extra.headline_weak (N > 1): the (256N) x 256 x 256 array, 8 shards per
+    rank -- per-GPU work fixed as N grows (round 2's headline definition)."""
+    plist, decoded, encoded = headline(ctx, args, weak=True)
+    wall, kern = time_programs(plist, args.steps, args.warmup, ctx.device, ctx)
+    dec = ctx.sum(decoded)
+    del plist
+    return _entry(dec, decoded + encoded, wall, kern, checked="bytes", scaling="weak",
+                  workload=f"({256 * ctx.world})x256x256 f32, 8 shards of 128^3 per rank",
+                  note="decoded_GiBps = all ranks' decoded bytes / max rank step time; "
+                       "kernel_ms / hbm_frac are this rank's")
 
 
 def main():
@@ -908,7 +927,7 @@ def main():
         for p in plist:
             p.results()
 
-    total_decoded = ctx.sum(args.steps * decoded)  # every rank's own shards
+    total_decoded = ctx.sum(args.steps * decoded)  # every rank's own shards of the one array
     value = total_decoded / wall_max / GIB
     # kernel time per launch over the timed region: event span on the launch
     # stream / steps (includes the graph's inter-launch gaps, so it is an upper
@@ -924,20 +943,20 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(wall_max / args.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (seed 0 standard-normal f32, planted NaN payload and -0.0)",
         "config": {
             "workload": "sharded 256^3 float32, 64^3 chunks (128^3 shards of 8 inner chunks; inner "
                         "codecs bytes(little)+crc32c, index bytes+crc32c at end), device-resident "
-                        "decode of the full array per step per GPU (64 inner chunks + 8 index "
-                        "checks, one launch), 4 rotating replicas per GPU; at N GPUs the batch is "
-                        "the (256N)x256x256 array split round-robin by shard (8 shards per rank)",
-            "chunks_per_step": 64 * ctx.world, "shards_per_step": 8 * ctx.world,
-            "decoded_bytes_per_step": decoded * ctx.world,
-            "encoded_bytes_per_step": encoded * ctx.world,
-            "parallelism": f"shard-partitioned x{ctx.world} (weak, no collective on the data path)",
+                        "decode of the full array per step (64 inner chunks + 8 index checks; one "
+                        "launch per GPU), 4 rotating replicas per GPU; at N GPUs the same array's "
+                        "8 shards are split round-robin over the ranks (8/N shards per rank)",
+            "chunks_per_step": 64, "shards_per_step": 8,
+            "decoded_bytes_per_step": int(ctx.sum(decoded)),
+            "encoded_bytes_per_step": int(ctx.sum(encoded)),
+            "parallelism": f"shard-partitioned x{ctx.world} (strong, no collective on the data path)",
         },
         "roofline": {
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -957,6 +976,8 @@ def main():
     if args.extra:
         log("[bench] extra configs " + args.extra)
         res["extra"] = extra_configs(ctx, args)
+        if ctx.world > 1:
+            res["extra"]["headline_weak"] = headline_weak(ctx, args)
     if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu_baseline:
         log("[bench] cpu baseline")
         g = W.HEADLINE

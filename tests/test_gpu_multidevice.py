@@ -1,0 +1,103 @@
+"""GPU tests of the single-process multi-device read (zarr_hip.parallel.
+DeviceGroup): a batch split round-robin by item over a device list, each
+device decoding its sub-batch on its own stream from its own host thread into
+its own out.  On the one-GPU box the list is [0, 0] (two workers on one card,
+the same code path as eight GPUs of a node); the union of the devices' regions
+and the gathered out are compared with the CPU oracle bit for bit."""
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from test_gpu_decode import CRC, LE, SHARD, _data
+
+pytestmark = pytest.mark.gpu
+
+
+def _arr(device, kind, shape, chunks, codecs, shards=None):
+    import zarr_hip
+
+    if shards is not None:
+        meta = O.ArrayMeta(shape, shards, np.dtype("float32"), 0.0, codecs=[SHARD(chunks, codecs)])
+    else:
+        meta = O.ArrayMeta(shape, chunks, np.dtype("float32"), 0.0, codecs=codecs)
+    host: dict = {}
+    O.write(host, meta, (Ellipsis,), _data(shape, "float32"))
+    store = zarr_hip.DeviceStore.from_host(host, device) if kind == "device" else \
+        zarr_hip.PinnedMemoryStore(dict(host)) if kind == "pinned" else zarr_hip.MemoryStore(dict(host))
+    if shards is not None:
+        arr = zarr_hip.Array.create(store, shape, chunks, "float32", 0.0, shards=shards, inner_codecs=codecs)
+    else:
+        arr = zarr_hip.Array.create(store, shape, chunks, "float32", 0.0, codecs=codecs)
+    return arr, host, meta
+
+
+@pytest.mark.parametrize("kind", ["device", "memory", "pinned"])
+@pytest.mark.parametrize("sharded", [False, True])
+@pytest.mark.parametrize("n_dev", [2, 3])
+def test_device_group_matches_oracle(device, kind, sharded, n_dev):
+    import torch
+
+    from zarr_hip.parallel import DeviceGroup, partition
+
+    shape = (128, 96, 64)
+    arr, host, meta = _arr(device, kind, shape, (32, 32, 32), [LE, CRC],
+                           shards=(64, 96, 64) if sharded else None)
+    grp = DeviceGroup([0] * n_dev)
+    for sel in [(Ellipsis,), (slice(5, 120, 3), slice(None), slice(7, 60))]:
+        batch, out_shape = arr.batch_info(sel)
+        outs, res = grp.read_sync(arr.codec_pipeline, batch, out_shape, "float32")
+        assert len(outs) == n_dev and len(res) == len(batch)
+        assert all(r["status"] == "present" for r in res)
+        want = np.ascontiguousarray(O.read(host, meta, sel))
+        # every device holds exactly its own items' regions
+        for r, out in enumerate(outs):
+            o = out.cpu().numpy()
+            for j in partition(len(batch), n_dev, r):
+                osel = tuple(batch[j][3])
+                assert o[osel].tobytes() == want[osel].tobytes()
+        # gathered onto one out: the whole selection
+        into = torch.empty(out_shape, dtype=torch.float32, device=device)
+        prog = grp.prepare_read(arr.codec_pipeline, batch, out_shape, "float32")
+        prog.launch()
+        prog.results()
+        prog.gather(batch, into)
+        assert into.cpu().numpy().tobytes() == want.tobytes()
+
+
+def test_device_group_crc_error_surfaces(device):
+    """A corrupted chunk on any device raises the reference's message."""
+    import zarr_hip
+    from zarr_hip.parallel import DeviceGroup
+
+    meta = O.ArrayMeta((64, 64), (16, 16), np.dtype("float32"), 0.0, codecs=[LE, CRC])
+    host: dict = {}
+    O.write(host, meta, (Ellipsis,), _data((64, 64), "float32"))
+    bad = bytearray(host["c/3/1"])
+    bad[40] ^= 0x04
+    host["c/3/1"] = bytes(bad)
+    with pytest.raises(ValueError) as want:
+        O.read(host, meta)
+    arr = zarr_hip.Array.create(zarr_hip.DeviceStore.from_host(host, device), (64, 64), (16, 16), "float32",
+                                0.0, codecs=[LE, CRC])
+    batch, out_shape = arr.batch_info((Ellipsis,))
+    with pytest.raises(ValueError) as got:
+        DeviceGroup([0, 0]).read_sync(arr.codec_pipeline, batch, out_shape, "float32")
+    assert str(got.value) == str(want.value)
+
+
+def test_device_group_compressed_chain(device):
+    """The host stage runs in each device's thread (gzip inner chunks)."""
+    from zarr_hip.parallel import DeviceGroup
+
+    arr, host, meta = _arr(device, "memory", (64, 48), (16, 16),
+                           [LE, {"name": "gzip", "configuration": {"level": 1}}], shards=(32, 48))
+    batch, out_shape = arr.batch_info((Ellipsis,))
+    prog = DeviceGroup([0, 0]).prepare_read(arr.codec_pipeline, batch, out_shape, "float32")
+    prog.launch()
+    prog.results()
+    import torch
+
+    into = torch.empty(out_shape, dtype=torch.float32, device=device)
+    prog.gather(batch, into)
+    assert into.cpu().numpy().tobytes() == O.read(host, meta).tobytes()

@@ -5,7 +5,8 @@ Restates only what the hot path needs from the reference's Array layer:
   create_codec_pipeline             src/zarr/core/array.py:221-265
   _get_selection                    src/zarr/core/array.py:5393-5514
   _set_selection                    src/zarr/core/array.py:5563-5675
-  default chunk key encoding        src/zarr/core/chunk_key_encodings.py:87-88 ("c/0/0")
+  chunk key encodings               src/zarr/core/chunk_key_encodings.py:87-88 (default, "c/0/0"),
+                                    103-105 (v2, "0.0"; "0" for 0-d)
 """
 
 from __future__ import annotations
@@ -54,13 +55,14 @@ class ArrayMetadata:
     codecs: tuple
     separator: str = "/"
     attributes: dict = field(default_factory=dict)
+    key_encoding: str = "default"  # or "v2"
 
     def to_json(self) -> dict:
         return {
             "zarr_format": 3, "node_type": "array", "shape": list(self.shape),
             "data_type": np.dtype(self.dtype).name,
             "chunk_grid": {"name": "regular", "configuration": {"chunk_shape": list(self.chunk_shape)}},
-            "chunk_key_encoding": {"name": "default", "configuration": {"separator": self.separator}},
+            "chunk_key_encoding": {"name": self.key_encoding, "configuration": {"separator": self.separator}},
             "fill_value": _fill_to_json(self.fill_value, np.dtype(self.dtype)),
             "codecs": [c.to_dict() for c in self.codecs],
             "attributes": self.attributes,
@@ -75,12 +77,18 @@ class ArrayMetadata:
             raise NotImplementedError("only regular chunk grids are on the GPU path")
         dt = np.dtype(d["data_type"])
         cke = d.get("chunk_key_encoding", {"name": "default"})
-        sep = (cke.get("configuration") or {}).get("separator", "/")
+        name = cke.get("name", "default")
+        if name not in ("default", "v2"):
+            raise NotImplementedError(f"chunk key encoding {name!r}")
+        sep = (cke.get("configuration") or {}).get("separator", "/" if name == "default" else ".")
         return cls(tuple(d["shape"]), tuple(grid["configuration"]["chunk_shape"]), dt,
                    _fill_from_json(d["fill_value"], dt), tuple(parse_codecs(d["codecs"])), sep,
-                   d.get("attributes", {}))
+                   d.get("attributes", {}), name)
 
     def chunk_key(self, coords) -> str:
+        if self.key_encoding == "v2":
+            k = self.separator.join(str(int(c)) for c in coords)
+            return k or "0"
         return self.separator.join(map(str, ("c",) + tuple(int(c) for c in coords)))
 
     @property
@@ -153,6 +161,11 @@ class Array:
     def batch_info(self, selection):
         rows, out_shape = chunk_batch(selection, self.metadata.shape, self.metadata.chunk_shape)
         store, spec, sep = self.store_path.store, self.spec, self.metadata.separator
+        if self.metadata.key_encoding == "v2":
+            pre = f"{self.store_path.path}/" if self.store_path.path else ""
+            batch = [(StorePath(store, pre + (sep.join(map(str, co)) or "0")), spec, csel, osel, comp)
+                     for co, csel, osel, comp in rows]
+            return batch, out_shape
         prefix = f"{self.store_path.path}/c" if self.store_path.path else "c"
         batch = [(StorePath(store, sep.join([prefix, *map(str, co)])), spec, csel, osel, comp)
                  for co, csel, osel, comp in rows]

@@ -54,3 +54,135 @@ def owned_regions(array, selection, world: int, rank: int, mode: str = "round_ro
     """Out selections owned by `rank` (for assembling / checking partitioned reads)."""
     batch, _ = array.batch_info(selection)
     return [batch[i][3] for i in partition(len(batch), world, rank, mode)]
+
+
+# ------------------------------------------------------------ one process, N GPUs
+class DeviceGroup:
+    """Several GPUs driven from ONE process (a zarr caller's ``arr[...]`` has no
+    process group): a batch is split round-robin by item (chunk or shard, as
+    BASELINE's C4 wording) over ``devices``; each device stages, plans and
+    decodes its own sub-batch on its own stream from its own host thread into
+    its own ``out`` (full selection shape; only its items' regions are
+    written), so the devices never exchange data.  This is the reference's
+    disjoint-output pool map (src/zarr/core/codec_pipeline.py:1104-1109,
+    1169-1171) with a GPU per worker.  ``gather`` assembles the regions onto
+    one device afterwards (peer copies over xGMI), outside any timed decode.
+
+    Items whose bytes sit in host memory are staged to the device that decodes
+    them (every device's H2D on its own copy stream: the node's PCIe links in
+    parallel); items in a DeviceStore on another device are copied device to
+    device.  A device may be listed twice (devices=[0, 0] runs two workers on
+    one GPU: the test of this path on a one-GPU box)."""
+
+    def __init__(self, devices, mode: str = "round_robin"):
+        import torch
+
+        if not devices:
+            raise ValueError("DeviceGroup needs at least one device")
+        self.devices = [torch.device("cuda", d) if isinstance(d, int) else torch.device(d) for d in devices]
+        self.mode = mode
+        self.streams = []
+        for d in self.devices:
+            with torch.cuda.device(d):
+                self.streams.append(torch.cuda.Stream(d))
+        from concurrent.futures import ThreadPoolExecutor
+
+        self._pool = ThreadPoolExecutor(max_workers=len(self.devices), thread_name_prefix="zarr_hip_dev")
+
+    def _map(self, fn):
+        futs = [self._pool.submit(fn, i) for i in range(len(self.devices))]
+        return [f.result() for f in futs]
+
+    def prepare_read(self, pipeline, batch_info, out_shape, dtype, order: str = "C", outs=None) -> "GroupProgram":
+        """Plan every device's sub-batch (tables uploaded, staging begun).
+        ``outs``: one tensor per device (full selection shape) or None (each
+        allocated on its device)."""
+        import torch
+
+        from . import buffer
+        from .pipeline import normalize_batch
+
+        batch = normalize_batch(batch_info)
+        W = len(self.devices)
+        parts = [partition(len(batch), W, r, self.mode) for r in range(W)]
+
+        def plan(i):
+            dev = self.devices[i]
+            with torch.cuda.device(dev), torch.cuda.stream(self.streams[i]):
+                out = outs[i] if outs is not None else buffer.empty(out_shape, dtype, dev, order)
+                idx = parts[i]
+                prog = pipeline.prepare_read([batch[j] for j in idx], out) if len(idx) else None
+                return prog, out, idx
+
+        return GroupProgram(self, self._map(plan), len(batch))
+
+    def read_sync(self, pipeline, batch_info, out_shape, dtype, order: str = "C", outs=None):
+        """(per-device outs, per-item GetResults in batch order)."""
+        prog = self.prepare_read(pipeline, batch_info, out_shape, dtype, order, outs)
+        prog.launch()
+        return prog.outs, prog.results()
+
+
+class GroupProgram:
+    """Planned per-device reads of a DeviceGroup: launch() starts every
+    device's decode from its own thread on its own stream; results()
+    synchronises all of them and returns statuses in batch order."""
+
+    def __init__(self, group: DeviceGroup, parts: list, n_items: int):
+        self.group = group
+        self.parts = parts  # [(DecodeProgram | None, out, item indices)]
+        self.n_items = n_items
+
+    @property
+    def outs(self) -> list:
+        return [p[1] for p in self.parts]
+
+    def launch(self) -> None:
+        import torch
+
+        g = self.group
+
+        def go(i):
+            prog = self.parts[i][0]
+            if prog is None:
+                return
+            with torch.cuda.device(g.devices[i]):
+                prog.launch(int(g.streams[i].cuda_stream))
+
+        g._map(go)
+
+    def synchronize(self) -> None:
+        for s in self.group.streams:
+            s.synchronize()
+
+    def results(self) -> tuple:
+        import torch
+
+        g = self.group
+        out: list = [None] * self.n_items
+
+        def res(i):
+            prog, _, idx = self.parts[i]
+            if prog is None:
+                return
+            g.streams[i].synchronize()
+            with torch.cuda.device(g.devices[i]), torch.cuda.stream(g.streams[i]):
+                for j, r in zip(idx, prog.results()):
+                    out[j] = r
+
+        g._map(res)
+        return tuple(out)
+
+    def gather(self, batch_info, into) -> None:
+        """Copy every device's item regions into ``into`` (any device): the
+        optional post-step gather, outside the decode."""
+        from .pipeline import normalize_batch
+
+        batch = normalize_batch(batch_info)
+        self.synchronize()
+        for prog, out, idx in self.parts:
+            for j in idx:
+                osel = tuple(batch[j][3])
+                if out.device == into.device and out.data_ptr() == into.data_ptr():
+                    continue
+                into[osel].copy_(out[osel], non_blocking=False)

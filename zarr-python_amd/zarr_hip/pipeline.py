@@ -424,15 +424,28 @@ def _generations(batch: list) -> tuple:
     return tuple(seen.values())
 
 
-def _device_resident(batch: list) -> bool:
-    """True when every ByteGetter reads from a DeviceStore (bytes already in HBM);
-    raw getters holding nothing (absent chunks) go with either."""
+def _same_device(a, b) -> bool:
+    torch = _torch()
+    ia = a.index if a.index is not None else torch.cuda.current_device()
+    ib = b.index if b.index is not None else torch.cuda.current_device()
+    return a.type == b.type and ia == ib
+
+
+def _device_resident(batch: list, device=None) -> bool:
+    """True when every ByteGetter reads from a DeviceStore (bytes already in HBM)
+    -- on `device`, when given: another GPU's bytes are copied, never read
+    across the fabric by the kernel; raw getters holding nothing (absent
+    chunks) go with either."""
     def dev(it):
         bg = it[0]
-        if isinstance(getattr(bg, "store", None), DeviceStore):
-            return True
+        st = getattr(bg, "store", None)
+        if isinstance(st, DeviceStore):
+            return device is None or _same_device(st.device, device)
         if isinstance(bg, _Raw):
-            return bg.value is None or isinstance(bg.value, DeviceRef)
+            if bg.value is None:
+                return True
+            return isinstance(bg.value, DeviceRef) and (device is None or
+                                                        _same_device(bg.value.arena.device, device))
         return False
 
     return all(dev(it) for it in batch) and any(
@@ -649,7 +662,7 @@ class HipCodecPipeline:
         # this thread plans; the launch waits for them (DecodeProgram.pending)
         # (a sharded chain whose inner chunks pass a host stage always reads
         # through the host: the touched inner chunks are decoded there first)
-        if chain.shard is not None and (chain.inner_host or not _device_resident(batch)):
+        if chain.shard is not None and (chain.inner_host or not _device_resident(batch, device)):
             sh = chain.shard
             cps = sh.chunks_per_shard(spec.shape)
             src, size, item_missing, resolved, keep, pending = staging.gather_sharded_partial(
@@ -736,7 +749,7 @@ class HipCodecPipeline:
         if prog is not None and prog.stale():
             prog = None
         if prog is None:
-            if not _device_resident(batch):
+            if not _device_resident(batch, dev_out.device):
                 return self._read_uncached(batch, dev_out, drop_axes)
             prog = self.prepare_read(batch, dev_out, drop_axes)
         prog.retarget(dev_out)

@@ -230,6 +230,10 @@ def gather_sources(batch: list, device, defer: bool = False, start: bool = True)
             raws.append(staged_bytes(bg.get_sync(prototype=None) if hasattr(bg, "get_sync") else bg))
     arenas = {id(r.arena): r.arena for r in raws if isinstance(r, DeviceRef)}
     all_dev = all(r is None or isinstance(r, DeviceRef) for r in raws)
+    tdev = torch.device(device)
+    if arenas and any(a.device.type != tdev.type or (a.device.index or 0) != (tdev.index or 0)
+                      for a in arenas.values()):
+        all_dev = False  # another GPU's arena: its bytes are copied to `device` below
     if all_dev and len(arenas) <= 1:
         if arenas:
             arena = next(iter(arenas.values()))
