@@ -51,7 +51,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # of this same command (scripts/gpu_pmc.sh -> scripts/pmc_summary.py); counters
 # cannot be read from inside the timed process, so the value is labelled with
 # the file it comes from
-TRAFFIC_JSON = os.path.join("profiles", "r02", "pmc_traffic.json")
+TRAFFIC_JSON = os.path.join("profiles", "r03", "pmc_traffic.json")
+LIB_SO = os.path.join("zarr-python_amd", "zarr_hip", "_lib", "libzarrhip.so")
 GIB = float(1 << 30)
 LE, CRC = W.LE, W.CRC
 synthetic = W.synthetic
@@ -813,13 +814,28 @@ def cpu_baseline(data_np, shape, chunks, shards, budget_s=12.0):
                               "cores": 1, "sample": f"{n1} full decodes in {n1 * dt1:.1f}s"}}
 
 
+def lib_sha16() -> str | None:
+    """sha256[:16] of the kernel library this process loads."""
+    import hashlib
+
+    try:
+        with open(os.path.join(ROOT, LIB_SO), "rb") as fh:
+            return hashlib.sha256(fh.read()).hexdigest()[:16]
+    except OSError:
+        return None
+
+
 def pmc_traffic():
-    """HBM bytes per launch measured by the PMC passes (null if not collected)."""
+    """(HBM bytes per launch measured by the PMC passes, the library hash they
+    were measured on).  The bytes are reported only when that hash is the
+    library this run loads: a kernel change leaves them null, not stale."""
     try:
         with open(os.path.join(ROOT, TRAFFIC_JSON)) as fh:
-            return json.load(fh).get("traffic_bytes_per_launch")
+            d = json.load(fh)
     except (OSError, ValueError):
-        return None
+        return None, None
+    sha = d.get("lib_sha16")
+    return (d.get("traffic_bytes_per_launch") if sha is not None and sha == lib_sha16() else None), sha
 
 
 # ------------------------------------------------------------------------ main
@@ -933,6 +949,7 @@ def main():
     # stream / steps (includes the graph's inter-launch gaps, so it is an upper
     # bound on the kernel duration and `achieved` a lower bound)
     avg_kern_s = span_s / args.steps
+    traffic, traffic_sha = pmc_traffic()
     achieved = (encoded + decoded) / avg_kern_s / 1e9
     res = {
         "metric": "decoded GiB/s (device-resident), sharded 256^3 f32 64^3 chunks, 1/2/4/8 GPU",
@@ -960,7 +977,8 @@ def main():
         },
         "roofline": {
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(),
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "traffic_lib_sha16": traffic_sha, "lib_sha16": lib_sha16(),
             "traffic_source": TRAFFIC_JSON + " (FETCH_SIZE x2 + WRITE_SIZE per launch from "
                               "separate rocprofv3 --pmc passes of this command)",
             "kernel": "zhip::k_decode_pair<CRC,4,noswap,2> (zhip_decode_mapped)",

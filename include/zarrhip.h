@@ -345,6 +345,14 @@ int zhip_stage_end(zhip_stage_job *job, void *wait_stream);
  * result buffer can take the D2H DMA directly), else 0. */
 int zhip_host_pinned(const void *p);
 
+/* Read n (<= 16) device words (each launch's 4-byte error flag) after the
+ * work already on `stream`: async copies into page-locked memory, one stream
+ * synchronise, the values into host_out.  The per-call read path's only
+ * device -> host traffic when no chunk failed (FusedCodecPipeline.read_sync
+ * returns statuses, codec_pipeline.py:1095-1172; the full status table is read
+ * only when a flag is set). */
+int zhip_wait_words(const uint32_t *const *words, uint32_t n, uint32_t *host_out, void *stream);
+
 /* memcpy with `nthreads` host threads (pinned result -> a caller's host array). */
 int zhip_host_copy(void *dst, const void *src, uint64_t nbytes, uint32_t nthreads);
 

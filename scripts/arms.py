@@ -74,13 +74,30 @@ def main():
                                ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
         n = int(os.environ.get("SIZE", str(64 << 20)))
         span, K, nt = int(os.environ.get("SPAN", "4096")), int(os.environ.get("K", "1")), int(os.environ.get("NT", "3"))
+        mode = os.environ.get("MODE", "span")  # span (k_copy), wave (k_copy_wave), il (k_copy_il, S = SPAN)
         R = 1 if big else 4
         srcs = [torch.empty(n, dtype=torch.uint8, device=dev).fill_(3) for _ in range(R)]
         dsts = [torch.empty(n, dtype=torch.uint8, device=dev) for _ in range(R)]
         alg = 2 * n
-        launch = lambda i: cb.cb_copy(srcs[i % R].data_ptr(), dsts[i % R].data_ptr(), n, span, K, 1, nt,  # noqa: E731
+        cb.cb_copy_wave.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
+                                    ctypes.c_void_p]
+        cb.cb_copy_il.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_uint32,
+                                  ctypes.c_int, ctypes.c_void_p]
+        if mode == "wave":
+            fn = lambda i: cb.cb_copy_wave(srcs[i % R].data_ptr(), dsts[i % R].data_ptr(), n, K, nt,  # noqa: E731
+                                           ctypes.c_void_p(sh))
+        elif mode == "il":
+            fn = lambda i: cb.cb_copy_il(srcs[i % R].data_ptr(), dsts[i % R].data_ptr(), n, K, span, nt,  # noqa: E731
+                                         ctypes.c_void_p(sh))
+        else:
+            fn = lambda i: cb.cb_copy(srcs[i % R].data_ptr(), dsts[i % R].data_ptr(), n, span, K, 1, nt,  # noqa: E731
                                       ctypes.c_void_p(sh))
-        arm = f"copy_{n >> 20}MiB_span{span}_K{K}_nt{nt}"
+
+        def launch(i):
+            rc = fn(i)
+            if rc != 0:
+                raise SystemExit(f"copy arm {mode}: rc {rc}")
+        arm = f"copy_{mode}_{n >> 20}MiB_span{span}_K{K}_nt{nt}"
     else:
         raise SystemExit(f"unknown ARM {arm}")
     for i in range(4):

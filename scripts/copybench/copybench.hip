@@ -258,3 +258,46 @@ extern "C" int cb_scatter(const void* src, void* dst, uint64_t cstride, int unit
         return -1;
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
+
+// Wave-contiguous spans: a workgroup covers K * 4 KiB; wave w takes the
+// contiguous quarter [w * K KiB, (w + 1) * K KiB), lane l's k-th 16-byte block
+// at 1 KiB * k + 16 l of it (all K loads first, then the stores).  The decode's
+// unit with a per-lane stride of 1 KiB instead of 4 KiB: each wave's loads
+// are one contiguous K KiB burst.
+template <int K, bool NTL, bool NTS>
+__global__ __launch_bounds__(256) void k_copy_wave(const uint4* __restrict__ src, uint4* __restrict__ dst) {
+    const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63u;
+    const uint64_t b0 = (uint64_t)blockIdx.x * 256ull * K + (uint64_t)w * 64ull * K + l;
+    uint4 v[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint64_t i = b0 + 64ull * k;
+        if constexpr (NTL) {
+            const v4u x = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(src) + i);
+            v[k] = make_uint4(x.x, x.y, x.z, x.w);
+        } else v[k] = src[i];
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint64_t i = b0 + 64ull * k;
+        if constexpr (NTS) {
+            v4u x = {v[k].x, v[k].y, v[k].z, v[k].w};
+            __builtin_nontemporal_store(x, reinterpret_cast<v4u*>(dst) + i);
+        } else dst[i] = v[k];
+    }
+}
+
+extern "C" int cb_copy_wave(const void* src, void* dst, uint64_t nbytes, int K, int nt, void* stream) {
+    typedef void (*WFn)(const uint4*, uint4*);
+    WFn fn = nullptr;
+#define WSEL(KK)                                                                                  \
+    if (K == KK) fn = nt == 1 ? (WFn)k_copy_wave<KK, true, true> : nt == 3 ? (WFn)k_copy_wave<KK, false, true> \
+                                                                 : (WFn)k_copy_wave<KK, false, false>;
+    WSEL(2) WSEL(4) WSEL(8) WSEL(16)
+    if (!fn) return -1;
+    const uint64_t per = 4096ull * K;
+    if (nbytes % per) return -3;
+    hipLaunchKernelGGL(fn, dim3((uint32_t)(nbytes / per)), dim3(256), 0, (hipStream_t)stream, (const uint4*)src,
+                       (uint4*)dst);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}

@@ -79,6 +79,21 @@ def main():
     # default-policy loads, nontemporal stores (the better copy policy at 64 MiB)
     arms["copy_8k_ldef"] = graph_of(lambda i, sh: cb.cb_copy(srcs[i % Rc].data_ptr(), dsts[i % Rc].data_ptr(), n,
                                                              8 << 10, 2, 1, 3, ctypes.c_void_p(sh)))
+    # interleaved spans (k_copy_il: workgroup j of a group of S takes steps j,
+    # j + S, ...) and wave-contiguous spans (k_copy_wave), default loads + nt stores
+    cb.cb_copy_il.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_uint32,
+                              ctypes.c_int, ctypes.c_void_p]
+    cb.cb_copy_wave.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
+                                ctypes.c_void_p]
+    for S, K in ((8, 8), (4, 8), (8, 16), (16, 16)):
+        arms[f"copy_il_S{S}_K{K}"] = graph_of(lambda i, sh, S=S, K=K: cb.cb_copy_il(
+            srcs[i % Rc].data_ptr(), dsts[i % Rc].data_ptr(), n, K, S, 3, ctypes.c_void_p(sh)))
+    arms["copy_4k_ldef"] = graph_of(lambda i, sh: cb.cb_copy(srcs[i % Rc].data_ptr(), dsts[i % Rc].data_ptr(), n,
+                                                             4 << 10, 1, 1, 3, ctypes.c_void_p(sh)))
+    arms["copy_32k_k8_ldef"] = graph_of(lambda i, sh: cb.cb_copy(srcs[i % Rc].data_ptr(), dsts[i % Rc].data_ptr(),
+                                                                 n, 32 << 10, 8, 1, 3, ctypes.c_void_p(sh)))
+    arms["copy_wave_k8"] = graph_of(lambda i, sh: cb.cb_copy_wave(srcs[i % Rc].data_ptr(), dsts[i % Rc].data_ptr(),
+                                                                  n, 8, 3, ctypes.c_void_p(sh)))
     # the headline's access pattern without codec work (scripts/copybench k_scatter)
     cb.cb_scatter.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p]
     ssrc = [torch.empty(64 * 1048580 + 64, dtype=torch.uint8, device=dev).fill_(5) for _ in range(R)] \

@@ -32,7 +32,16 @@ def main():
     med = {k: statistics.median(v) for k, v in per.items()}
     fetch = med.get("FETCH_SIZE")
     write = med.get("WRITE_SIZE")
-    res = {"kernel_match": needle, "kernels": sorted(names),
+    lib = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "zarr-python_amd",
+                       "zarr_hip", "_lib", "libzarrhip.so")
+    try:
+        import hashlib
+
+        with open(lib, "rb") as fh:
+            sha = hashlib.sha256(fh.read()).hexdigest()[:16]
+    except OSError:
+        sha = None
+    res = {"kernel_match": needle, "kernels": sorted(names), "lib_sha16": sha,
            "launches": {k: len(v) for k, v in per.items()},
            "median_per_launch_KiB": med,
            "traffic_bytes_per_launch": None if fetch is None or write is None

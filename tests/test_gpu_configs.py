@@ -219,3 +219,30 @@ def test_truncated_shard_on_device_store(device, index_crc):
     store, arr = _device_array(device, meta, host)
     with pytest.raises(ValueError, match="shorter than its index"):
         arr[...]
+
+
+@pytest.mark.parametrize("kind", ["memory", "device"])
+def test_c1_exact_geometry(device, kind):
+    """BASELINE configs[0] at its exact geometry: 1e7 float32 1-D in (2**20,)
+    chunks, bytes codec only (no CRC): 10 chunks, the last a boundary chunk
+    stored at the full 4 MiB (562,816 items in the array, the rest fill).  The
+    GPU write gives the oracle's store byte for byte; the GPU read gives the
+    oracle's values, whole and for a ragged selection."""
+    import zarr_hip
+
+    n, c = 10 ** 7, 2 ** 20
+    meta = O.ArrayMeta((n,), (c,), np.dtype("float32"), 0.0, codecs=[W.LE])
+    data = W.synthetic((n,), seed=0)
+    host = {}
+    O.write(host, meta, (Ellipsis,), data)
+    assert len(host) == 10 and len(host["c/9"]) == 4 * c
+    store = zarr_hip.DeviceStore(device, capacity=48 << 20) if kind == "device" else zarr_hip.MemoryStore()
+    arr = zarr_hip.Array.create(store, (n,), (c,), "float32", 0.0, codecs=[W.LE])
+    arr[...] = data
+    got = {k: bytes(v) for k, v in store.to_dict().items() if not k.endswith("zarr.json")}
+    assert got.keys() == host.keys()
+    for k in host:
+        assert got[k] == host[k], k
+    assert arr[...].tobytes() == data.tobytes()
+    sel = (slice(123457, 9_876_543, 1),)
+    assert arr[sel].tobytes() == np.ascontiguousarray(O.read(host, meta, sel)).tobytes()

@@ -220,15 +220,32 @@ def test_pipeline_parity_outer_transpose_around_sharding(device, direction, shap
             np.testing.assert_array_equal(arr[sel], expected[sel])
 
 
-@pytest.mark.parametrize("codecs", [
-    [{"name": "sharding_indexed", "configuration": {"chunk_shape": [2, 2], "codecs": [LE]}},
-     {"name": "gzip", "configuration": {"level": 1}}],
-])
-def test_outer_codecs_around_sharding_refused(device, codecs):
-    """test_pipeline_parity.py:455-523 (outer gzip around sharding): not on the
-    device path; refused rather than run on the host."""
+@pytest.mark.parametrize("kind", ["memory", "device"])
+def test_outer_gzip_around_sharding(device, kind):
+    """test_pipeline_parity.py:455-523, "outer-gzip-around-sharding": a gzip
+    codec after the sharding serializer compresses whole shards, so partial
+    reads and writes must go through it (the reference's regression: they
+    skipped it).  Here the outer host stage decompresses the whole shard
+    before the GPU reads its index and inner chunks, and recompresses after
+    the GPU re-packs it; full + region write, full + region read, stored bytes
+    equal to the oracle's."""
     import zarr_hip
 
-    with pytest.raises(NotImplementedError):
-        a = zarr_hip.Array.create(zarr_hip.DeviceStore(device), (8, 8), (4, 4), "int32", 0, codecs=codecs)
-        a[:] = np.arange(64, dtype="int32").reshape(8, 8)
+    codecs = [{"name": "sharding_indexed", "configuration": {"chunk_shape": [2, 2], "codecs": [LE]}},
+              {"name": "gzip", "configuration": {"level": 1}}]
+    shape = (8, 8)
+    data = (np.arange(64).reshape(shape) + 1).astype("uint16")
+    store = zarr_hip.MemoryStore() if kind == "memory" else zarr_hip.DeviceStore(device)
+    a = zarr_hip.Array.create(store, shape, (4, 4), "uint16", 0, codecs=codecs)
+    a[...] = data
+    a[2:5, 1:3] = 99
+    expected = data.copy()
+    expected[2:5, 1:3] = 99
+    np.testing.assert_array_equal(a[...], expected)
+    np.testing.assert_array_equal(a[1:3, 2:7], expected[1:3, 2:7])
+    meta = O.ArrayMeta(shape, (4, 4), np.dtype("uint16"), 0, codecs=codecs)
+    host = {}
+    O.write(host, meta, (Ellipsis,), data)
+    O.write(host, meta, (slice(2, 5), slice(1, 3)), np.full((3, 2), 99, "uint16"))
+    got = {k: bytes(v) for k, v in store.to_dict().items() if not k.endswith("zarr.json")}
+    assert got == host

@@ -10,10 +10,12 @@ temp dir, and the HBM-resident DeviceStore -- and checks three things:
 * the stored bytes equal what the CPU oracle writes for the same sequence of
   writes (stronger than the reference suite, which only checks values).
 
-Scenarios that need a host-side compressor (gzip, zstd), zarr v2 or nested
-sharding are out of scope for the device path: they are
-not restated as passing cases; instead the test below pins that the GPU path
-refuses them loudly rather than falling back to the CPU.
+Compressed scenarios run with the compressor on the host (1d-gzip,
+transpose-gzip: the built-in gzip; zstd needs zarr's codec instance, which
+tests/test_gpu_compression.py drives with a caller-supplied codec object).
+zarr v2 and nested sharding are not restated as passing cases; the test below
+pins that the GPU path refuses them (and a zstd named only by JSON) loudly
+rather than falling back to the CPU.
 """
 
 from __future__ import annotations
@@ -76,7 +78,7 @@ def _ar(n, dtype, offset=1):
 _F64 = dict(dtype="float64", fill=0.0)
 _I32 = dict(dtype="int32", fill=-1)
 
-# suite:117-375, minus the compressed / v2 / nested-sharding cases (see module doc)
+# suite:117-375, minus the zstd / v2 / nested-sharding cases (see module doc)
 CASES = (
     Case("1d-unsharded-roundtrip", (100,), (10,), **_F64, writes=((slice(None), _ar(100, "f8")),)),
     Case("1d-sharded-roundtrip", (100,), (10,), shards=(100,), **_F64,
@@ -87,6 +89,8 @@ CASES = (
          writes=((slice(None), np.arange(200, dtype="i4").reshape(10, 20)),)),
     Case("2d-sharded-roundtrip", (20, 20), (5, 5), shards=(10, 10), **_I32,
          writes=((slice(None), np.arange(400, dtype="i4").reshape(20, 20)),)),
+    Case("1d-gzip-roundtrip", (100,), (10,), **_F64, codecs=(LE, {"name": "gzip", "configuration": {"level": 1}}),
+         writes=((slice(None), _ar(100, "f8")),)),
     Case("1d-float32-roundtrip", (50,), (10,), dtype="float32", fill=0.0,
          writes=((slice(None), _ar(50, "f4")),)),
     Case("missing-chunks-fill", (100,), (10,), dtype="float64", fill=-7.0),
@@ -105,6 +109,9 @@ CASES = (
          reads=(np.s_[0, 0], np.s_[10, 10], np.s_[19, 19])),
     Case("transpose", (8, 12), (2, 4), codecs=(_T((1, 0)), LE), **_I32,
          writes=((slice(None), np.arange(96, dtype="i4").reshape(8, 12)),),
+         reads=(slice(None), np.s_[1:7, 2:10])),
+    Case("transpose-gzip", (8, 12), (2, 4), codecs=(_T((1, 0)), LE, {"name": "gzip", "configuration": {"level": 1}}),
+         **_I32, writes=((slice(None), np.arange(96, dtype="i4").reshape(8, 12)),),
          reads=(slice(None), np.s_[1:7, 2:10])),
     Case("partial-shard-overwrite", (40,), (4,), shards=(40,), **_I32, write_empty=True,
          writes=((slice(None), np.arange(40, dtype="i4")), (slice(7, 18), _ar(11, "i4", 700)))),
@@ -289,15 +296,14 @@ def test_read_write_methods_do_not_branch_on_sharding_codec_type():
 
 
 @pytest.mark.parametrize("codecs,shards,why", [
-    ([LE, {"name": "gzip", "configuration": {"level": 1}}], None, "gzip"),
     ([LE, {"name": "zstd", "configuration": {"level": 1}}], None, "zstd"),
     ([{"name": "sharding_indexed", "configuration": {
         "chunk_shape": [10, 10], "codecs": [{"name": "sharding_indexed", "configuration": {
             "chunk_shape": [5, 5], "codecs": [LE]}}]}}], None, "nested sharding"),
 ])
 def test_out_of_scope_chains_refused_loudly(codecs, shards, why, device):
-    """suite:147-226 (compressed, v2) and 274-289 (nested sharding): not on the
-    device path; the pipeline must raise rather than decode on the host."""
+    """suite:147-226 (a zstd without its codec instance, v2) and 274-289
+    (nested sharding): the pipeline must raise rather than decode on the host."""
     import zarr_hip
 
     store = zarr_hip.DeviceStore(device)

@@ -503,7 +503,12 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
         KernelFn fn = nu != 2 ? nullptr
                       : (p.tune & kTuneTrailingCrc) ? select_pair_kernel(crc, p.g.itemsize, swap, 3)
                       : (p.tune & kTuneSplitChain) ? select_pair_kernel(crc, p.g.itemsize, swap, 4)
-                      : (p.tune & kTuneSkipCrc) ? select_pair_kernel(crc, p.g.itemsize, swap, 5) : nullptr;
+                      : (p.tune & kTuneSkipCrc) ? select_pair_kernel(crc, p.g.itemsize, swap, 5)
+                      : (p.tune & (kTunePrio | kTuneDeferB))
+                          ? select_pair_kernel(crc, p.g.itemsize, swap,
+                                               (p.tune & kTunePrio) && (p.tune & kTuneDeferB) ? 8
+                                               : (p.tune & kTunePrio) ? 6 : 7)
+                          : nullptr;
         if (!fn) fn = select_pair_kernel(crc, p.g.itemsize, swap, nu);
         if (!fn) return ZHIP_E_UNSUPPORTED;
         // chunks of more than 32 units (> 1 MiB): one unit per 256-thread half of

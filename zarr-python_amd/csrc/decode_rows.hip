@@ -638,16 +638,45 @@ __device__ __forceinline__ void unit_status_pair(const DecodeParams& p, const Un
     }
 }
 
+// Unit B's loads issued one per stored block of unit A (VARIANT 7 / 8): at
+// most K + 1 loads in flight per thread instead of 2K, so a wave's stores
+// are not queued behind its own second unit's loads.
+template <int ITEM, bool SWAP, int K>
+__device__ __forceinline__ void store_a_load_b(const DecodeParams& p, const Unit& UA, const RowSteps& m,
+                                               uint32_t lane_row, int64_t lane_off, uint8_t* sink,
+                                               const uint4 (&blk)[K], bool crc, const uint32_t* s_tab, Acc4* acc,
+                                               const Unit& UB, bool live_b, int t, uint4 (&nb)[K]) {
+    const bool present = UA.mode == ZHIP_ST_OK;
+    const bool writes = UA.mode == ZHIP_ST_OK || UA.mode == ZHIP_ST_MISSING;
+    uint8_t* const base = p.out + UA.out_off;
+    const uint4 f = make_uint4(p.fill[0], p.fill[1], p.fill[2], p.fill[3]);
+    const bool okb = live_b && UB.mode == ZHIP_ST_OK;
+    const uint8_t* zero = reinterpret_cast<const uint8_t*>(g_rows_zero);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint32_t lo = m.e[k].lo, hi = m.e[k].hi;
+        const bool wr = writes && lane_row - lo < hi - lo;
+        store_nt16(wr ? base + m.e[k].rel + lane_off : sink, present ? swap_block<ITEM, SWAP>(blk[k]) : f);
+        if (crc) crc_block4(s_tab, *acc, blk[k]);
+        const int32_t bb = UB.seg_lo + kWgStride * k;
+        nb[k] = load_stream16_any(okb && bb >= 0 ? UB.cp + bb + 16 * t : zero);
+    }
+}
+
 // VARIANT (tuning arm, headline item type only): 0 production, 3 no CRC
-// lookups (a plain xor; results invalid).  (Round-1 arms 1 -- every store
-// before the lookups -- and 2 -- independent chains for the two units --
-// measured slower and were retired with the single-operator tables.)
+// lookups (a plain xor; results invalid), 6 s_setprio(1) once every load of
+// the wave is issued, 7 unit B's loads interleaved with unit A's stores, 8
+// both.  (Round-1 arms 1 -- every store before the lookups -- and 2 --
+// independent chains for the two units -- measured slower and were retired
+// with the single-operator tables.)
 template <bool CRC, int ITEM, bool SWAP, int NU, int K = 8, int VARIANT = 0>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(NU == 1 ? 8 : 4))) void k_decode_pair(const DecodeParams p) {
     // NU == 1: the lane shift is a VALU multiply (no s_mul), so that eight
     // workgroups fit a CU's LDS
     constexpr bool kLdsMul = CRC && NU == 2;
     constexpr bool SKIP = VARIANT == 3;
+    constexpr bool PRIO = VARIANT == 6 || VARIANT == 8;
+    constexpr bool DEFER_B = NU == 2 && (VARIANT == 7 || VARIANT == 8);
     __shared__ uint32_t s_tab[CRC ? kPairTabWords : 1];
     __shared__ uint32_t s_mul[kLdsMul ? 12 * kThreads : 1];
     __shared__ uint32_t s_red[2][kThreads / 64];
@@ -704,7 +733,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(NU == 
         // predicted addresses: the unit loads go out before the headers arrive
         Unit ga = predict_unit(p, u_a), gb = predict_unit(p, u_b);
         load_unit_rows(ga, has_a, t, A);
-        if constexpr (NU == 2) load_unit_rows(gb, has_b, t, B);
+        if constexpr (NU == 2 && !DEFER_B) load_unit_rows(gb, has_b, t, B);
         ua = resolve_unit(p, u_a, expected);
         ub = ua;
         if constexpr (NU == 2)
@@ -712,7 +741,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(NU == 
         // a wrong prediction (non-default packing, elided inner chunks) reloads
         // from the live index; the full drain keeps every later wait exact
         const bool bad_a = has_a && ua.mode == ZHIP_ST_OK && ua.cp != ga.cp;
-        const bool bad_b = has_b && ub.mode == ZHIP_ST_OK && ub.cp != gb.cp;
+        const bool bad_b = !DEFER_B && has_b && ub.mode == ZHIP_ST_OK && ub.cp != gb.cp;
         if (bad_a || bad_b) {
             if (bad_a) load_unit_rows(ua, true, t, A);
             if constexpr (NU == 2)
@@ -727,8 +756,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(NU == 
             if (has_b) ub = advance_unit(p, ua, u_b, expected);
         if constexpr (CRC) ipre = index_prefetch(p, g, g < p.n_idx, t, zero);
         load_unit_rows(ua, has_a, t, A);
-        if constexpr (NU == 2) load_unit_rows(ub, has_b, t, B);
+        if constexpr (NU == 2 && !DEFER_B) load_unit_rows(ub, has_b, t, B);
     }
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);  // every load of this wave is out
     // destinations of both units' steps (scalar loads, consumed at the stores)
     const RowSteps ma = load_row_steps(p, ua), mb = load_row_steps(p, ub);
     uint32_t stored_a = 0, stored_b = 0;
@@ -766,8 +796,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(NU == 
         const int64_t lane_off = (int64_t)lane_row * p.r_oy + (int64_t)lane_col;
         const bool same = has_b && ub.c == ua.c;
         Acc4 acc_a = {0u, 0u, 0u, 0u}, acc_b = {0u, 0u, 0u, 0u};
-        store_unit_rows<ITEM, SWAP, K, SKIP>(p, ua, ma, true, lane_row, lane_off, sink, A,
-                                             CRC && ua.mode == ZHIP_ST_OK, s_tab, &acc_a);
+        if constexpr (DEFER_B)
+            store_a_load_b<ITEM, SWAP, K>(p, ua, ma, lane_row, lane_off, sink, A, CRC && ua.mode == ZHIP_ST_OK,
+                                          s_tab, &acc_a, ub, has_b, t, B);
+        else
+            store_unit_rows<ITEM, SWAP, K, SKIP>(p, ua, ma, true, lane_row, lane_off, sink, A,
+                                                 CRC && ua.mode == ZHIP_ST_OK, s_tab, &acc_a);
         stamp(p, g, t, 3);
         if constexpr (NU == 2) {
             if (same) acc_b = acc_a;
@@ -825,6 +859,11 @@ KernelFn select_pair_nu(bool crc, int item, bool swap) {
 KernelFn select_pair_kernel(bool crc, int item, bool swap, int nu) {
     if (nu == 5)  // tuning arm (headline item type only): VARIANT 3, no lookups
         return !(crc && item == 4 && !swap) ? nullptr : k_decode_pair<true, 4, false, 2, 8, 3>;
+    if (nu >= 6 && nu <= 8) {  // tuning arms (headline item type only): VARIANT 6 / 7 / 8
+        if (!(crc && item == 4 && !swap)) return nullptr;
+        return nu == 6 ? k_decode_pair<true, 4, false, 2, 8, 6>
+               : nu == 7 ? k_decode_pair<true, 4, false, 2, 8, 7> : k_decode_pair<true, 4, false, 2, 8, 8>;
+    }
     if (nu == 3 || nu == 4) return nullptr;  // retired arms
     return nu == 1 ? select_pair_nu<1>(crc, item, swap) : select_pair_nu<2>(crc, item, swap);
 }

@@ -79,17 +79,48 @@ struct TileMap4 {
     TileEnt e[kTiles];
 };
 
+// The 64-row x 256-byte LDS tile image, XOR-swizzled instead of padded: dword
+// d of row r sits at dword r*64 + (d ^ tile_swz(r)), tile_swz(r) = 2*(r / kPer)
+// (kPer = 16 / ITEM rows per 16-byte out piece).  The column accesses (each
+// lane kPer rows of one element column; a half wave covers 64/kPer pieces of
+// two adjacent columns) then hit 32 distinct banks -- the 260-byte pitch left
+// them 2-way conflicted -- and a thread's 16-byte row block stays one
+// aligned 16-byte slot (one ds_write_b128 / ds_read_b128, its dword pairs
+// swapped when bit 1 of the swizzle is set).
+template <int ITEM>
+__device__ __forceinline__ uint32_t tile_swz(uint32_t r) {
+    return (2u * (r / (16u / ITEM))) & 63u;
+}
+
+template <int ITEM>
+__device__ __forceinline__ uint32_t tile_byte(uint32_t r, uint32_t b) {  // byte b of row r
+    return r * 256u + ((((b >> 2) ^ tile_swz<ITEM>(r)) << 2) | (b & 3u));
+}
+
+template <int ITEM>
+__device__ __forceinline__ void tile_put16(uint8_t* s, uint32_t r, uint32_t b16, uint4 v) {
+    const uint32_t sw = tile_swz<ITEM>(r);
+    uint4* d = reinterpret_cast<uint4*>(s + r * 256u + (((b16 >> 2) ^ (sw & ~3u)) << 2));
+    *d = (sw & 2u) ? make_uint4(v.z, v.w, v.x, v.y) : v;
+}
+
+template <int ITEM>
+__device__ __forceinline__ uint4 tile_get16(const uint8_t* s, uint32_t r, uint32_t b16) {
+    const uint32_t sw = tile_swz<ITEM>(r);
+    const uint4 v = *reinterpret_cast<const uint4*>(s + r * 256u + (((b16 >> 2) ^ (sw & ~3u)) << 2));
+    return (sw & 2u) ? make_uint4(v.z, v.w, v.x, v.y) : v;
+}
+
 }  // namespace
 
 template <bool CRC, int ITEM, bool SWAP>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_decode_tile4(
     const DecodeParams p) {
-    constexpr int kPitch = ITEM == 8 ? 264 : 260;  // bytes per LDS tile row (2-way read conflicts)
     constexpr int kPer = 16 / ITEM;                // rows per 16-byte out piece
     constexpr int kPiecesPerCol = kTileRows / kPer;
     __shared__ uint32_t s_tab[CRC ? 16 * 256 : 1];
     __shared__ uint32_t s_tz[CRC ? 1024 : 1];
-    __shared__ __attribute__((aligned(16))) uint8_t s_tile[kTileRows * kPitch];
+    __shared__ __attribute__((aligned(16))) uint8_t s_tile[kTileRows * 256];
     __shared__ uint32_t s_red[kThreads / 64];
     const int t = threadIdx.x;
     const uint32_t g = blockIdx.x;
@@ -148,11 +179,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
 #pragma unroll
         for (int k = 0; k < kPasses; ++k) {
             const uint4 v = swap_block<ITEM, SWAP>(blk[j][k]);
-            uint32_t* d = reinterpret_cast<uint32_t*>(s_tile + (16 * k + row0) * kPitch + col);
-            d[0] = v.x;
-            d[1] = v.y;
-            d[2] = v.z;
-            d[3] = v.w;
+            tile_put16<ITEM>(s_tile, 16 * k + row0, col, v);
         }
         __syncthreads();  // tile j (and, first time, the tables) in LDS
 #pragma unroll
@@ -163,7 +190,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
             uint32_t w[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
             for (int e = 0; e < kPer; ++e) {
-                const uint8_t* src = s_tile + (r0 + e) * kPitch + jc * ITEM;
+                const uint8_t* src = s_tile + tile_byte<ITEM>(r0 + e, jc * ITEM);
                 if constexpr (ITEM == 8) {
                     const uint2 v = *reinterpret_cast<const uint2*>(src);
                     w[2 * e] = v.x;
@@ -301,12 +328,11 @@ __device__ __forceinline__ bool tileg_arrive(uint32_t* ws, uint32_t n_chunks, ui
 template <bool CRC, int ITEM, bool SWAP>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_decode_tileg(
     const DecodeParams p) {
-    constexpr int kPitch = ITEM == 8 ? 264 : 260;
     constexpr int kPer = 16 / ITEM;
     constexpr int kPiecesPerCol = kTileRows / kPer;
     __shared__ uint32_t s_tab[CRC ? 16 * 256 : 1];
     __shared__ uint32_t s_tz[CRC ? 1024 : 1];
-    __shared__ __attribute__((aligned(16))) uint8_t s_tile[kTileRows * kPitch];
+    __shared__ __attribute__((aligned(16))) uint8_t s_tile[kTileRows * 256];
     __shared__ uint32_t s_red[kThreads / 64];
     const int t = threadIdx.x;
     const uint32_t gpc = p.n_groups;
@@ -366,11 +392,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
 #pragma unroll
         for (int k = 0; k < kPasses; ++k) {
             const uint4 v = swap_block<ITEM, SWAP>(blk[j][k]);
-            uint32_t* d = reinterpret_cast<uint32_t*>(s_tile + (16 * k + row0) * kPitch + col);
-            d[0] = v.x;
-            d[1] = v.y;
-            d[2] = v.z;
-            d[3] = v.w;
+            tile_put16<ITEM>(s_tile, 16 * k + row0, col, v);
         }
         __syncthreads();
 #pragma unroll
@@ -381,7 +403,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
             uint32_t w[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
             for (int e = 0; e < kPer; ++e) {
-                const uint8_t* src = s_tile + (r0 + e) * kPitch + jc * ITEM;
+                const uint8_t* src = s_tile + tile_byte<ITEM>(r0 + e, jc * ITEM);
                 if constexpr (ITEM == 8) {
                     const uint2 v = *reinterpret_cast<const uint2*>(src);
                     w[2 * e] = v.x;
@@ -469,12 +491,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
 template <bool CRC, int ITEM, bool SWAP>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_encode_tile4(
     const EncodeParams p) {
-    constexpr int kPitch = ITEM == 8 ? 264 : 260;
     constexpr int kPer = 16 / ITEM;
     constexpr int kPiecesPerCol = kTileRows / kPer;
     __shared__ uint32_t s_tab[CRC ? 16 * 256 : 1];
     __shared__ uint32_t s_tz[CRC ? 1024 : 1];
-    __shared__ __attribute__((aligned(16))) uint8_t s_tile[kTileRows * kPitch];
+    __shared__ __attribute__((aligned(16))) uint8_t s_tile[kTileRows * 256];
     __shared__ uint32_t s_red[kThreads / 64];
     __shared__ uint32_t s_ne[kThreads / 64];
     const int t = threadIdx.x;
@@ -535,7 +556,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
             const uint32_t w[4] = {pcs[j][k].x, pcs[j][k].y, pcs[j][k].z, pcs[j][k].w};
 #pragma unroll
             for (int e = 0; e < kPer; ++e) {
-                uint8_t* dst = s_tile + (r0 + e) * kPitch + jc * ITEM;
+                uint8_t* dst = s_tile + tile_byte<ITEM>(r0 + e, jc * ITEM);
                 if constexpr (ITEM == 8) {
                     *reinterpret_cast<uint2*>(dst) = make_uint2(w[2 * e], w[2 * e + 1]);
                 } else if constexpr (ITEM == 4) {
@@ -552,8 +573,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
         uint32_t acc = 0;
 #pragma unroll
         for (int k = 0; k < kPasses; ++k) {
-            const uint32_t* sv = reinterpret_cast<const uint32_t*>(s_tile + (16 * k + row0) * kPitch + col);
-            const uint4 v = make_uint4(sv[0], sv[1], sv[2], sv[3]);
+            const uint4 v = tile_get16<ITEM>(s_tile, 16 * k + row0, col);
             eq = eq && block_eq_fill_e<ITEM>(v, p);
             const uint4 e = swap_block<ITEM, SWAP>(v);
             store_nt16_a1(cp + tm.e[j].tbase + (row0 + 16u * k) * sq + col, e);
@@ -654,12 +674,11 @@ __device__ __forceinline__ TileGeo encode_tile_geo(const EncodeParams& p, uint32
 template <bool CRC, int ITEM, bool SWAP>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_encode_tile(
     const EncodeParams p) {
-    constexpr int kPitch = ITEM == 8 ? 264 : 260;
     constexpr int kPer = 16 / ITEM;
     constexpr int kPiecesPerCol = kTileRows / kPer;
     constexpr int G = kTiles;  // tiles per workgroup
     __shared__ uint32_t s_tab[CRC ? 16 * 256 : 1];
-    __shared__ __attribute__((aligned(16))) uint8_t s_tile[kTileRows * kPitch];
+    __shared__ __attribute__((aligned(16))) uint8_t s_tile[kTileRows * 256];
     __shared__ uint32_t s_red[kThreads / 64];
     __shared__ uint32_t s_ne[kThreads / 64];
     struct Counts {
@@ -765,7 +784,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
             }
 #pragma unroll
             for (int e = 0; e < kPer; ++e) {
-                uint8_t* dst = s_tile + (r0 + e) * kPitch + jc * ITEM;
+                uint8_t* dst = s_tile + tile_byte<ITEM>(r0 + e, jc * ITEM);
                 if constexpr (ITEM == 8) {
                     *reinterpret_cast<uint2*>(dst) = make_uint2(w[2 * e], w[2 * e + 1]);
                 } else if constexpr (ITEM == 4) {
@@ -786,8 +805,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
             const uint32_t row = 16u * k + row0;
             uint4 e = make_uint4(0, 0, 0, 0);
             if ((int32_t)row < geo[j].rows_here && (int32_t)col < geo[j].cols_here) {
-                const uint32_t* sv = reinterpret_cast<const uint32_t*>(s_tile + row * kPitch + col);
-                const uint4 v = make_uint4(sv[0], sv[1], sv[2], sv[3]);
+                const uint4 v = tile_get16<ITEM>(s_tile, row, col);
                 eq = eq && block_eq_fill_e<ITEM>(v, p);
                 e = swap_block<ITEM, SWAP>(v);
                 store_nt16_a1(cp + geo[j].tbase + row * sq + col, e);
@@ -851,12 +869,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
 template <bool CRC, int ITEM, bool SWAP>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_encode_tileg(
     const EncodeParams p) {
-    constexpr int kPitch = ITEM == 8 ? 264 : 260;
     constexpr int kPer = 16 / ITEM;
     constexpr int kPiecesPerCol = kTileRows / kPer;
     __shared__ uint32_t s_tab[CRC ? 16 * 256 : 1];
     __shared__ uint32_t s_tz[CRC ? 1024 : 1];
-    __shared__ __attribute__((aligned(16))) uint8_t s_tile[kTileRows * kPitch];
+    __shared__ __attribute__((aligned(16))) uint8_t s_tile[kTileRows * 256];
     __shared__ uint32_t s_red[kThreads / 64];
     __shared__ uint32_t s_ne[kThreads / 64];
     const int t = threadIdx.x;
@@ -920,7 +937,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
             const uint32_t w[4] = {pcs[j][k].x, pcs[j][k].y, pcs[j][k].z, pcs[j][k].w};
 #pragma unroll
             for (int e = 0; e < kPer; ++e) {
-                uint8_t* dst = s_tile + (r0 + e) * kPitch + jc * ITEM;
+                uint8_t* dst = s_tile + tile_byte<ITEM>(r0 + e, jc * ITEM);
                 if constexpr (ITEM == 8) {
                     *reinterpret_cast<uint2*>(dst) = make_uint2(w[2 * e], w[2 * e + 1]);
                 } else if constexpr (ITEM == 4) {
@@ -941,8 +958,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
             const uint32_t row = 16u * k + row0;
             uint4 e = make_uint4(0, 0, 0, 0);
             if ((int32_t)row < rows && (int32_t)col < cols) {
-                const uint32_t* sv = reinterpret_cast<const uint32_t*>(s_tile + row * kPitch + col);
-                const uint4 v = make_uint4(sv[0], sv[1], sv[2], sv[3]);
+                const uint4 v = tile_get16<ITEM>(s_tile, row, col);
                 eq = eq && block_eq_fill_e<ITEM>(v, p);
                 e = swap_block<ITEM, SWAP>(v);
                 store_nt16_a1(cp + (size_t)j * p.g_step_t + row * sq + col, e);

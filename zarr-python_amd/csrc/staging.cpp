@@ -381,6 +381,27 @@ int zhip_host_pinned(const void* p) {
     return a.type == hipMemoryTypeHost ? 1 : 0;
 }
 
+int zhip_wait_words(const uint32_t* const* words, uint32_t n, uint32_t* host_out, void* stream) {
+    // the per-call read's result check: each launch's 4-byte error word, read
+    // back with one async copy per word into a page-locked per-thread buffer
+    // behind the launches on `stream`, then one stream synchronise
+    if (n == 0) return ZHIP_OK;
+    if (!words || !host_out || n > 16) return ZHIP_E_INVALID;
+    thread_local uint32_t* pinned = nullptr;
+    if (!pinned && hipHostMalloc(reinterpret_cast<void**>(&pinned), 16 * sizeof(uint32_t), hipHostMallocDefault) !=
+                       hipSuccess) {
+        pinned = nullptr;
+        return ZHIP_E_HIP;
+    }
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    for (uint32_t i = 0; i < n; ++i)
+        if (hipMemcpyAsync(pinned + i, words[i], sizeof(uint32_t), hipMemcpyDeviceToHost, st) != hipSuccess)
+            return ZHIP_E_HIP;
+    if (hipStreamSynchronize(st) != hipSuccess) return ZHIP_E_HIP;
+    for (uint32_t i = 0; i < n; ++i) host_out[i] = pinned[i];
+    return ZHIP_OK;
+}
+
 int zhip_host_copy(void* dst, const void* src, uint64_t nbytes, uint32_t nthreads) {
     if (nbytes == 0) return ZHIP_OK;
     if (!dst || !src) return ZHIP_E_INVALID;

@@ -136,6 +136,8 @@ constexpr uint32_t kTuneEncNoFlags = 524288u; // k_encode_pair: skip the non-emp
 constexpr uint32_t kTuneNoTile4 = 1048576u;   // transposed layouts: grouped k_*_tileg where k_*_tile4 would run
 constexpr uint32_t kTuneDuo = 2097152u;       // whole-row layouts: k_decode_duo (one unit per half of a 512-thread workgroup)
 constexpr uint32_t kTuneNoXcd = 8388608u;     // k_decode_pair: plain dispatch order (no XCD-contiguous runs)
+constexpr uint32_t kTunePrio = 16777216u;     // k_decode_pair arm: s_setprio(1) once a wave's loads are out
+constexpr uint32_t kTuneDeferB = 33554432u;   // k_decode_pair arm: unit B's loads interleaved with A's stores
 constexpr uint32_t kTuneStamp = 1024u;    // k_decode_pair: per-workgroup phase timestamps (zhip_debug_stamps)
 constexpr uint32_t kStampWG = 8192u;      // workgroups stamped per launch
 constexpr uint32_t kStampSlots = 8u;

@@ -216,6 +216,8 @@ def lib():
     L.zhip_stage_end.restype = ctypes.c_int
     L.zhip_host_pinned.argtypes = [ctypes.c_void_p]
     L.zhip_host_pinned.restype = ctypes.c_int
+    L.zhip_wait_words.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
+    L.zhip_wait_words.restype = ctypes.c_int
     L.zhip_crc32c_host.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
     L.zhip_crc32c_host.restype = ctypes.c_uint32
     L.zhip_host_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32]

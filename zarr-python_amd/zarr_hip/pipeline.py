@@ -284,9 +284,17 @@ class DecodeProgram:
         fused index checks ORs a bit into it); the full status table is read
         only when it is set.  Missing items are known on the host at planning
         (absent keys, absent shards), so the GetResults are prebuilt."""
-        err = self.data.errflag()
-        if self.index is not None:
-            err |= self.index.errflag()
+        w = getattr(self, "_err_words", None)
+        if w is None:
+            import ctypes
+
+            ptrs = [self.data.d_err.data_ptr()] + ([self.index.d_err.data_ptr()] if self.index is not None else [])
+            w = self._err_words = ((ctypes.c_void_p * len(ptrs))(*ptrs), len(ptrs),
+                                   (ctypes.c_uint32 * len(ptrs))())
+        N.check(N.lib().zhip_wait_words(w[0], w[1], w[2], _stream_handle(self.data.device)), "zhip_wait_words")
+        err = 0
+        for x in w[2]:
+            err |= x
         if err:
             self.data.reset_errflag()
             if self.index is not None:
@@ -931,7 +939,10 @@ class HipCodecPipeline:
             tr = hoststage.ShardTranscoder(replace(ab, codecs=split_host_tail(ab.codecs)[0]), spec.shape,
                                            inner, ab.inner_spec(spec))
         wrapped = [(hoststage.TranscodingByteSetter(it[0], outer, tr, spec),) + tuple(it[1:]) for it in batch]
-        return wpipe._write_sync(wrapped, value, drop_axes, partial_encode)
+        # a bytes->bytes codec around a sharding codec hides the index: whole
+        # shards are re-encoded (no partial encode, codec_pipeline.py:1212 with
+        # pipeline_supports_partial_encode false)
+        return wpipe._write_sync(wrapped, value, drop_axes, partial_encode and not outer)
 
     async def write(self, batch_info: Iterable, value, drop_axes: tuple = ()) -> None:
         await asyncio.to_thread(self.write_sync, list(batch_info), value, drop_axes)
