@@ -387,6 +387,10 @@ uint32_t zhip_emulate_chunk_crc(const zhip_plan *plan, const uint8_t *data);
 /* The same for k_decode_pair's scheme (11/11/10-bit tables, four word
  * accumulators per lane, windowed per-lane multiply).  Test hook. */
 uint32_t zhip_emulate_chunk_crc_pair(const zhip_plan *plan, const uint8_t *data);
+/* The same for k_decode_il (a workgroup's eight 4 KiB steps interleaved at a
+ * stride of S steps, A_(4096 S) tables); 0xFFFFFFFF when the plan has no
+ * interleaved layout.  Test hook. */
+uint32_t zhip_emulate_chunk_crc_il(const zhip_plan *plan, const uint8_t *data);
 uint32_t zhip_fdiv_eval(uint32_t n, uint32_t d);
 
 #ifdef __cplusplus

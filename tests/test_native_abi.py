@@ -207,3 +207,27 @@ def test_host_copy_pool(n):
         dst[:] = 0
         assert N.lib().zhip_host_copy(dst.ctypes.data, src.ctypes.data, n, threads) == 0
         assert dst.tobytes() == src.tobytes()
+
+
+@pytest.mark.parametrize("n", [65536, 126976, 131072, 196608, 1048576, 2 ** 21, 4100, 65552])
+def test_emulated_interleaved_crc_matches_oracle(n):
+    """k_decode_il's decomposition (a workgroup's eight 4 KiB steps at a stride
+    of S steps, A_(4096 S) tables, per-workgroup lane constants with negative
+    shifts where the stride outruns the chunk end) reproduces crc32c; layouts
+    whose step count no group of S x 8 steps tiles have no interleaved form."""
+    from zarr_hip import _native as N
+
+    rng = np.random.default_rng(n)
+    data = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+    L = N.Layout()
+    L.ndim, L.itemsize = 1, 1
+    L.shape[0] = n
+    L.nbytes = n
+    L.flags = N.LF_CRC
+    plan = N.Plan(L, upload=False)
+    got = plan.emulate_chunk_crc(data, pair="il")
+    steps = -(-((n + 15) // 16 * 16) // 32768) * 8
+    if steps % 16:
+        assert got == 0xFFFFFFFF
+    else:
+        assert got == O.crc32c(data)

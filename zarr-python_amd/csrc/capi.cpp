@@ -120,10 +120,11 @@ __attribute__((target("sse4.2"))) uint32_t crc_sse42(const uint8_t* p, size_t n)
     return ~(uint32_t)c;
 }
 
-// k_decode_pair tables (kPairTab* layout): A4096 over 11/11/10-bit slices of a
-// word, and the byte slices of A4 that fold the four word accumulators
-void build_pair_tables(uint32_t* tab) {
-    const uint32_t x = xpow8((uint64_t)kWgStride);
+// k_decode_pair tables (kPairTab* layout): A4096 (A_stride) over 11/11/10-bit
+// slices of a word, and the byte slices of A4 that fold the four word
+// accumulators
+void build_pair_tables(uint32_t* tab, uint64_t stride = kWgStride) {
+    const uint32_t x = xpow8(stride);
     for (uint32_t i = 0; i < 2048; ++i) {
         tab[kPairT1 + i] = gf_mul(x, i);
         tab[kPairT2 + i] = gf_mul(x, i << 11);
@@ -236,6 +237,13 @@ int zhip_plan_create(const zhip_layout* layout, zhip_plan** out) {
     if (L.flags & ZHIP_LF_NO_WRITE || !(L.flags & ZHIP_LF_CRC)) p->kblocks = kDefaultBlocks;
     p->seg = (uint32_t)kWgStride * p->kblocks;
     p->nseg = p->E == 0 ? 1u : (p->E + p->seg - 1) / p->seg;
+    // k_decode_il: groups of S x 8 steps must tile the chunk's steps
+    p->il_S = 0;
+    if (p->kblocks == (uint32_t)kDefaultBlocks && (L.flags & ZHIP_LF_CRC) && !(L.flags & ZHIP_LF_NO_WRITE)) {
+        const uint32_t n_steps = p->nseg * (uint32_t)kDefaultBlocks;
+        for (uint32_t S = 8; S >= 2 && !p->il_S; S /= 2)
+            if (n_steps % (S * (uint32_t)kDefaultBlocks) == 0) p->il_S = S;
+    }
     p->R = (uint64_t)p->E + kWgStride;
     p->c_inv = xpow8_inv(p->R - n);
     p->c3 = gf_mul(xpow8(n), 0xFFFFFFFFu);
@@ -320,7 +328,9 @@ int zhip_plan_upload(zhip_plan* p) {
     // per-lane constant kthread[t] * kunit[s] * c_inv of k_decode_pair, whose
     // run ends then need no uniform multiply at all
     const size_t n_old = 4096 + kThreads + p->nseg + (size_t)p->nseg * kThreads;
-    std::vector<uint32_t> h(n_old + kPairTabWords + (size_t)p->nseg * kThreads + kThreads);
+    const size_t n_pair = kPairTabWords + (size_t)p->nseg * kThreads + kThreads;
+    const size_t n_il = p->il_S ? kPairTabWords + (size_t)p->nseg * kThreads + kThreads : 0;
+    std::vector<uint32_t> h(n_old + n_pair + n_il);
     build_horner(h.data());
     for (int t = 0; t < kThreads; ++t) h[4096 + t] = xpow8((uint64_t)kWgStride - 16u * t);
     for (uint32_t s = 0; s < p->nseg; ++s) h[4096 + kThreads + s] = xpow8((uint64_t)s * p->seg);
@@ -338,6 +348,34 @@ int zhip_plan_upload(zhip_plan* p) {
         h[n_old + kPairTabWords + i] = gf_mul(h[4096 + kThreads + p->nseg + i], c96);
     for (int t = 0; t < kThreads; ++t)
         h[n_old + kPairTabWords + (size_t)p->nseg * kThreads + t] = gf_mul(h[4096 + t], c96);
+    p->off_il = 0;
+    if (p->il_S) {
+        // k_decode_il: workgroup r of a chunk (group r / S, offset r % S) takes
+        // steps st_k = (r / S) S 8 + r % S + S k; lane t's chain over them (stride
+        // D = 4096 S) leaves word w of step st_0 multiplied by x^(8 D 8), so the
+        // lane constant x^(8 (E - p_0 + 4096 - 8 D)) c_inv x^(-96) gives every
+        // word at p the pair kernel's x^(8 (E - p + 4096)) c_inv (p_0 = E -
+        // 4096 (n_steps - st_0) + 16 t); exponents may be negative
+        p->off_il = n_old + n_pair;
+        uint32_t* il = h.data() + p->off_il;
+        const uint64_t D = (uint64_t)kWgStride * p->il_S;
+        build_pair_tables(il, D);
+        const int64_t n_steps = (int64_t)p->nseg * kDefaultBlocks, K = kDefaultBlocks, S = p->il_S;
+        for (uint32_t r = 0; r < p->nseg; ++r) {
+            const int64_t st0 = (int64_t)(r / S) * S * K + (int64_t)(r % S);
+            for (int t = 0; t < kThreads; ++t) {
+                const int64_t e = (int64_t)kWgStride * (n_steps - st0 + 1 - S * K) - 16 * t;
+                const uint32_t xe = e >= 0 ? xpow8((uint64_t)e) : xpow8_inv((uint64_t)(-e));
+                il[kPairTabWords + (size_t)r * kThreads + t] = gf_mul(gf_mul(xe, p->c_inv), c96);
+            }
+        }
+        // the fused index check (one 4 KiB step per lane) under A_D: its state
+        // is A_D(w) instead of A4096(w), so kthread11 times x^(-8(D - 4096))
+        const uint32_t back = xpow8_inv(D - (uint64_t)kWgStride);
+        for (int t = 0; t < kThreads; ++t)
+            il[kPairTabWords + (size_t)p->nseg * kThreads + t] =
+                gf_mul(h[n_old + kPairTabWords + (size_t)p->nseg * kThreads + t], back);
+    }
     if (p->d_tables) (void)hipFree(p->d_tables);
     p->d_tables = nullptr;
     HIP_TRY(hipMalloc(&p->d_tables, h.size() * sizeof(uint32_t)));
@@ -595,6 +633,13 @@ int zhip_decode_mapped(const zhip_plan* plan, const void* src, uint64_t src_size
     p.pair_tab = plan->d_tables + plan->off_pair;
     p.kpair11 = p.pair_tab + kPairTabWords;
     p.kthread11 = p.kpair11 + (size_t)plan->nseg * kThreads;
+    // k_decode_il needs its tables, and a fused index check of one step per lane
+    p.il_S = (plan->il_S && (n_index == 0 || plan->idx_E <= (uint32_t)kWgStride)) ? plan->il_S : 0u;
+    if (p.il_S) {
+        p.il_tab = plan->d_tables + plan->off_il;
+        p.il_klane = p.il_tab + kPairTabWords;
+        p.il_kidx = p.il_klane + (size_t)plan->nseg * kThreads;
+    }
     for (int op = 0; op < 4; ++op) p.hx[op] = plan->hx[op];
     for (int i = 0; i < 32; ++i) p.kq[i] = plan->kq[i];
     p.n_chunks = n_chunks;
@@ -945,6 +990,52 @@ uint32_t zhip_emulate_chunk_crc_pair(const zhip_plan* plan, const uint8_t* data)
             const uint32_t S = a4(a4(a4(a[0]) ^ a[1]) ^ a[2]) ^ a[3];
             const uint32_t k11 = gf_mul(gf_mul(xpow8((uint64_t)kWgStride - 16u * t), ku), c96);
             V ^= lanemul3(S, k11);
+        }
+    }
+    return ~(V ^ plan->c3);
+}
+
+// CPU emulation of k_decode_il's CRC for one chunk: workgroup r takes steps
+// (r / S) S 8 + r % S + S k (k < 8); each lane's four word accumulators run
+// through the A_(4096 S) tables, fold with the A4 tables and are multiplied by
+// the workgroup's lane constant (windowed, as the kernel); -1 when the plan
+// has no interleaved layout.  Test hook.
+uint32_t zhip_emulate_chunk_crc_il(const zhip_plan* plan, const uint8_t* data) {
+    std::call_once(g_once, init_tables);
+    if (!plan || !plan->il_S) return 0xFFFFFFFFu;
+    const uint32_t S = plan->il_S, K = kDefaultBlocks;
+    std::vector<uint32_t> tab(kPairTabWords);
+    build_pair_tables(tab.data(), (uint64_t)kWgStride * S);
+    const uint32_t* T = tab.data();
+    auto a11 = [&](uint32_t w) { return T[kPairT1 + (w & 2047u)] ^ T[kPairT2 + ((w >> 11) & 2047u)] ^ T[kPairT3 + (w >> 22)]; };
+    auto a4 = [&](uint32_t w) {
+        const uint32_t* t4 = T + kPairA4;
+        return t4[w & 255u] ^ t4[256 + ((w >> 8) & 255u)] ^ t4[512 + ((w >> 16) & 255u)] ^ t4[768 + (w >> 24)];
+    };
+    const uint32_t N = (uint32_t)plan->layout.nbytes;
+    const uint32_t c96 = xpow8_inv(12);
+    const int64_t n_steps = (int64_t)plan->nseg * K;
+    const int64_t lo_frame = (int64_t)plan->E - n_steps * kWgStride;
+    uint32_t V = 0;
+    for (uint32_t r = 0; r < plan->nseg; ++r) {
+        const int64_t st0 = (int64_t)(r / S) * S * K + (int64_t)(r % S);
+        for (int t = 0; t < kThreads; ++t) {
+            uint32_t a[4] = {0, 0, 0, 0};
+            for (uint32_t k = 0; k < K; ++k) {
+                const int64_t o = lo_frame + (int64_t)kWgStride * (st0 + (int64_t)S * k) + 16 * t;
+                uint8_t b[16] = {0};
+                for (int i = 0; i < 16; ++i) {
+                    const int64_t q = o + i;
+                    if (q >= 0 && q < (int64_t)N) b[i] = data[q];
+                }
+                uint32_t w[4];
+                std::memcpy(w, b, 16);
+                for (int j = 0; j < 4; ++j) a[j] = a11(a[j] ^ w[j]);
+            }
+            const uint32_t Sx = a4(a4(a4(a[0]) ^ a[1]) ^ a[2]) ^ a[3];
+            const int64_t e = (int64_t)kWgStride * (n_steps - st0 + 1 - (int64_t)S * K) - 16 * t;
+            const uint32_t xe = e >= 0 ? xpow8((uint64_t)e) : xpow8_inv((uint64_t)(-e));
+            V ^= gf_mul(Sx, gf_mul(gf_mul(xe, plan->c_inv), c96));
         }
     }
     return ~(V ^ plan->c3);

@@ -491,6 +491,7 @@ static KernelFn select_tile_kernel(bool crc, int item, bool swap) {
 KernelFn select_rows_kernel(bool crc, int item, bool swap, int k);  // decode_rows.hip
 KernelFn select_pair_kernel(bool crc, int item, bool swap, int nu);  // decode_rows.hip
 KernelFn select_duo_kernel(bool crc, int item, bool swap);           // decode_rows.hip
+KernelFn select_il_kernel(bool crc, int item, bool swap);            // decode_rows.hip
 KernelFn select_tile4_kernel(bool crc, int item, bool swap);         // decode_tile.hip
 KernelFn select_tileg_kernel(bool crc, int item, bool swap);         // decode_tile.hip
 
@@ -500,6 +501,20 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
         // one workgroup per pair of units, non-persistent (k_decode_pair)
         const int nu = (p.tune & kTuneSingle) ? 1 : 2;
         const bool crc = (p.lflags & ZHIP_LF_CRC) != 0, swap = (p.lflags & ZHIP_LF_SWAP) != 0;
+        // batches of more than one resident wave of pair workgroups (4 per CU):
+        // interleaved steps (k_decode_il), whose access order keeps the HBM
+        // streaming at 4 GiB (see decode_rows.hip); kTuneIl / kTuneNoIl force
+        const uint32_t resident_pairs = (uint32_t)(max_grid / 8) * 4u;
+        const bool il = p.il_S != 0 && crc && !(p.tune & (kTuneNoIl | kTuneSkipCrc | kTuneSingle | kTuneDuo)) &&
+                        ((p.tune & kTuneIl) || (uint64_t)p.n_units > 2ull * resident_pairs);
+        if (il) {
+            KernelFn ifn = select_il_kernel(crc, p.g.itemsize, swap);
+            if (!ifn) return ZHIP_E_UNSUPPORTED;
+            const uint32_t igrid = p.n_units > p.n_idx ? p.n_units : p.n_idx;
+            if (igrid == 0) return ZHIP_OK;
+            hipLaunchKernelGGL(ifn, dim3(igrid), dim3(kThreads), 0, stream, p);
+            return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
+        }
         KernelFn fn = nu != 2 ? nullptr
                       : (p.tune & kTuneTrailingCrc) ? select_pair_kernel(crc, p.g.itemsize, swap, 3)
                       : (p.tune & kTuneSplitChain) ? select_pair_kernel(crc, p.g.itemsize, swap, 4)

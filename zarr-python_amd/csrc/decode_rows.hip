@@ -955,6 +955,183 @@ __global__ __launch_bounds__(2 * kThreads) __attribute__((amdgpu_waves_per_eu(8,
             verify_index_pair(p, j, tl, kth, s_tab, s_red[2], j == g, ipre, h == 0);
 }
 
+// ---------------------------------------------------------------------------
+// k_decode_il: the whole-row decode with interleaved steps, for batches far
+// larger than one resident wave of workgroups (C4, C5).  A chunk's 4 KiB steps
+// form groups of S x 8; workgroup r of the chunk (group r / S, offset
+// j = r % S) takes steps j, j + S, ..., j + 7S of its group, so the S
+// workgroups of a group -- consecutive in dispatch order -- sweep S x 32 KiB
+// together, 4 KiB each at a time, instead of each streaming its own 64 KiB.
+// At 4 GiB that access order copies at 0.75 of HBM peak where 32 KiB spans
+// reach 0.61-0.67 (profiles/r03/copy_*.jsonl, graphbench arms).  Per lane the
+// eight blocks are D = 4096 S bytes apart: one Horner chain through the
+// A_D 11/11/10 tables (four word accumulators, A4 fold), one windowed lane
+// multiply by the workgroup's host-built constant, one publication per
+// workgroup (arrival bit r; > 32 workgroups per chunk: xor + count).  Same
+// statuses, stores (row map, sink for unselected rows), fused index checks
+// (one step per lane; the constants carry the A_D frame) as k_decode_pair.
+// (CPU emulation: zhip_emulate_chunk_crc_il.)
+__device__ __forceinline__ void publish_il(const DecodeParams& p, uint32_t c, uint32_t r, uint32_t wpc, uint32_t V,
+                                           uint32_t stored, int t) {
+    if (wpc <= 32u) {
+        const uint64_t full = wpc >= 32u ? 0xFFFFFFFFull : ((1ull << wpc) - 1ull);
+        const uint64_t bits = 1ull << r;
+        uint64_t prev = 0;
+        if (t == 0) {
+            uint64_t* w = reinterpret_cast<uint64_t*>(p.ws) + 2ull * c;
+            prev = __hip_atomic_fetch_xor(w, (bits << 32) | V, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)prev);
+        const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(prev >> 32));
+        if ((uint64_t)(hi ^ (uint32_t)bits) == full) {
+            if (t == 0) {
+                uint64_t* w = reinterpret_cast<uint64_t*>(p.ws) + 2ull * c;
+                __hip_atomic_store(w, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            finalize_uniform(p, c, stored, lo ^ V, t, true);
+        }
+    } else {  // more than 32 workgroups per chunk: xor, then count arrivals
+        uint32_t raw = 0, last = 0;
+        if (t == 0) {
+            uint32_t* accw = p.ws + 4ull * c;
+            const uint32_t prev = __hip_atomic_fetch_xor(accw, V, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::"v"(prev) : "memory");
+            const uint32_t tk = __hip_atomic_fetch_add(accw + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (tk + 1u == wpc) {
+                raw = __hip_atomic_exchange(accw, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                asm volatile("s_waitcnt vmcnt(0)" ::"v"(raw) : "memory");
+                __hip_atomic_store(accw + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                last = 1;
+            }
+        }
+        if (__builtin_amdgcn_readfirstlane(last))
+            finalize_uniform(p, c, stored, __builtin_amdgcn_readfirstlane(raw), t, true);
+    }
+}
+
+template <bool CRC, int ITEM, bool SWAP>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_decode_il(const DecodeParams p) {
+    constexpr int K = kDefaultBlocks;
+    __shared__ uint32_t s_tab[CRC ? kPairTabWords : 1];
+    __shared__ uint32_t s_mul[CRC ? 12 * kThreads : 1];
+    __shared__ uint32_t s_red[2][kThreads / 64];
+    const int t = threadIdx.x;
+    const uint32_t G = gridDim.x, g = blockIdx.x;
+    const uint32_t wpc = p.nseg, S = p.il_S;  // workgroups per chunk = its 32 KiB units
+    const uint32_t c = g / wpc, r = g - c * wpc;
+    const bool has = c < p.n_chunks;
+    if (!has && g >= p.n_idx) return;
+    const uint32_t expected = p.g.nbytes + (CRC ? 4u : 0u);
+    const uint8_t* zero = reinterpret_cast<const uint8_t*>(g_rows_zero);
+    // 1. vector loads in a path-independent order and count: [CRC: tables (6),
+    //    the lane constant, the index lane constant, the first index block],
+    //    the K data blocks; headers, row-map entries and the trailer are scalar
+    uint4 tv0, tv1, tv2, tv3, tv4, tv5;
+    uint32_t kl = 0, kix = 0;
+    if constexpr (CRC) {
+        const uint4* gt = reinterpret_cast<const uint4*>(p.il_tab);
+        tv0 = gt[t];
+        tv1 = gt[t + kThreads];
+        tv2 = gt[t + 2 * kThreads];
+        tv3 = gt[t + 3 * kThreads];
+        tv4 = gt[t + 4 * kThreads];
+        tv5 = gt[t + 5 * kThreads];
+        kl = load_u32_any(reinterpret_cast<const uint8_t*>(p.il_klane + (size_t)(has ? r : 0u) * kThreads + t));
+        kix = load_u32_any(reinterpret_cast<const uint8_t*>(p.il_kidx + t));
+    }
+    Unit U;
+    if (has) U = resolve_unit(p, c * p.nseg, expected);
+    else {
+        U.c = 0;
+        U.sidx = 0;
+        U.mode = ZHIP_ST_MISSING;
+        U.cp = zero;
+        U.seg_lo = 0;
+        U.sel = 0;
+        U.out_off = 0;
+    }
+    const bool ok = has && U.mode == ZHIP_ST_OK;
+    const uint32_t st0 = (r / S) * S * (uint32_t)K + (r % S);
+    const int32_t lo_frame = (int32_t)p.E - (int32_t)(p.nseg * p.seg);
+    uint4 ipre = make_uint4(0, 0, 0, 0);
+    if constexpr (CRC) ipre = index_prefetch(p, g, g < p.n_idx, t, zero);
+    uint4 A[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int32_t base = lo_frame + kWgStride * (int32_t)(st0 + S * (uint32_t)k);
+        A[k] = load_stream16_any(ok && base >= 0 ? U.cp + base + 16 * t : zero);
+    }
+    // destinations of the K steps (scalar loads, consumed at the stores)
+    zhip_rowblk m[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint32_t st = st0 + S * (uint32_t)k;
+        const uint32_t sidx = p.nseg - 1u - st / (uint32_t)K;
+        m[k] = load_uniform<zhip_rowblk>(p.rowmap + ((size_t)U.sel * p.nseg + sidx) * K + (st % (uint32_t)K));
+    }
+    uint32_t stored = 0;
+    if (CRC && ok) stored = load_trailer_uniform(U.cp, p.g.nbytes);
+    // 2. tables into LDS, the lane-multiply column
+    if constexpr (CRC) {
+        uint4* stt = reinterpret_cast<uint4*>(s_tab);
+        stt[t] = tv0;
+        stt[t + kThreads] = tv1;
+        stt[t + 2 * kThreads] = tv2;
+        stt[t + 3 * kThreads] = tv3;
+        stt[t + 4 * kThreads] = tv4;
+        stt[t + 5 * kThreads] = tv5;
+        lanemul3_init(s_mul, t, kl);
+        __syncthreads();
+    }
+    if (has) {
+        // 3. stores, each block's Horner step after its store
+        uint8_t* sink = reinterpret_cast<uint8_t*>(g_rows_sink);
+        const uint32_t lane_row = (16u * (uint32_t)t) >> p.row_shift;
+        const uint32_t lane_col = (16u * (uint32_t)t) & ((1u << p.row_shift) - 1u);
+        const int64_t lane_off = (int64_t)lane_row * p.r_oy + (int64_t)lane_col;
+        const bool writes = ok || U.mode == ZHIP_ST_MISSING;
+        uint8_t* const obase = p.out + U.out_off;
+        const uint4 f = make_uint4(p.fill[0], p.fill[1], p.fill[2], p.fill[3]);
+        Acc4 acc = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint32_t lo = m[k].lo, hi = m[k].hi;
+            const bool wr = writes && lane_row - lo < hi - lo;
+            store_nt16(wr ? obase + m[k].rel + lane_off : sink, ok ? swap_block<ITEM, SWAP>(A[k]) : f);
+            if (CRC && ok) crc_block4(s_tab, acc, A[k]);
+        }
+        // 4. run end: one chain per workgroup, one publication
+        if constexpr (CRC) {
+            uint32_t v = ok ? lanemul3(s_mul, t, fold4(s_tab, acc)) : 0u;
+            v = wave_xor(v);
+            if ((t & 63) == 0) s_red[0][t >> 6] = v;
+            __syncthreads();
+            if (ok && t < 64) {
+                const uint32_t V = __builtin_amdgcn_readfirstlane(s_red[0][0] ^ s_red[0][1] ^ s_red[0][2] ^ s_red[0][3]);
+                publish_il(p, c, r, wpc, V, __builtin_amdgcn_readfirstlane(stored), t);
+            }
+        }
+        if (r == 0) unit_status_pair(p, U, CRC, t);
+    }
+    // 5. fused shard-index checks (one step per lane: launch_decode admits
+    //    this kernel only then), the first block prefetched with the data
+    if constexpr (CRC)
+        for (uint32_t j = g; j < p.n_idx; j += G) verify_index_pair(p, j, t, kix, s_tab, s_red[1], j == g, ipre);
+}
+
+KernelFn select_il_kernel(bool crc, int item, bool swap) {
+    switch (item) {
+        case 1: return crc ? k_decode_il<true, 1, false> : k_decode_il<false, 1, false>;
+        case 2: return crc ? (swap ? k_decode_il<true, 2, true> : k_decode_il<true, 2, false>)
+                           : (swap ? k_decode_il<false, 2, true> : k_decode_il<false, 2, false>);
+        case 4: return crc ? (swap ? k_decode_il<true, 4, true> : k_decode_il<true, 4, false>)
+                           : (swap ? k_decode_il<false, 4, true> : k_decode_il<false, 4, false>);
+        case 8: return crc ? (swap ? k_decode_il<true, 8, true> : k_decode_il<true, 8, false>)
+                           : (swap ? k_decode_il<false, 8, true> : k_decode_il<false, 8, false>);
+        default: return nullptr;
+    }
+}
+
 KernelFn select_duo_kernel(bool crc, int item, bool swap) {
     switch (item) {
         case 1: return crc ? k_decode_duo<true, 1, false> : k_decode_duo<false, 1, false>;

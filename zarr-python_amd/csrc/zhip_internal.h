@@ -107,6 +107,12 @@ struct DecodeParams {
     uint32_t rows;             // 1: launch k_decode_rows
     uint32_t xcd_run;          // k_decode_pair: pairs per XCD-contiguous run (0: dispatch order)
     const zhip_rowblk* rowmap; // per (sel, unit, step) destinations (zhip_rows_map); k_decode_pair
+    // k_decode_il: interleave stride (steps), its A_(4096 S) tables, lane
+    // constants per workgroup-in-chunk and for the fused index check
+    uint32_t il_S;
+    const uint32_t* il_tab;
+    const uint32_t* il_klane;
+    const uint32_t* il_kidx;
     // load-address prediction (zhip_predict; k_decode_pair): payload of chunk c
     // predicted at src + pred_base + (c / pred_per) * pred_outer + (c % pred_per) * pred_inner
     uint32_t pred, pred_per;
@@ -138,6 +144,8 @@ constexpr uint32_t kTuneDuo = 2097152u;       // whole-row layouts: k_decode_duo
 constexpr uint32_t kTuneNoXcd = 8388608u;     // k_decode_pair: plain dispatch order (no XCD-contiguous runs)
 constexpr uint32_t kTunePrio = 16777216u;     // k_decode_pair arm: s_setprio(1) once a wave's loads are out
 constexpr uint32_t kTuneDeferB = 33554432u;   // k_decode_pair arm: unit B's loads interleaved with A's stores
+constexpr uint32_t kTuneIl = 67108864u;       // whole-row layouts: k_decode_il wherever the layout admits it
+constexpr uint32_t kTuneNoIl = 134217728u;    // whole-row layouts: never k_decode_il (k_decode_pair)
 constexpr uint32_t kTuneStamp = 1024u;    // k_decode_pair: per-workgroup phase timestamps (zhip_debug_stamps)
 constexpr uint32_t kStampWG = 8192u;      // workgroups stamped per launch
 constexpr uint32_t kStampSlots = 8u;
@@ -259,4 +267,12 @@ struct zhip_plan {
     uint32_t* d_tile_tables;
     // shard index (sharded layouts): payload 16*n_inner, E, CRC constants
     uint32_t idx_nbytes, idx_E, idx_c_inv, idx_c3;  // horner (stride 16*sstride[tq]) | kthread (256) | kunit (t_per_chunk)
+    // k_decode_il (interleaved steps, decode_rows.hip): a workgroup takes K = 8
+    // of the chunk's 4 KiB steps at a stride of il_S steps (il_S = 0: not
+    // available for this layout).  d_tables continues at off_il with the
+    // 11/11/10 tables of A_(4096 il_S) (kPairTabWords) | klane (nseg x 256:
+    // per workgroup-in-chunk lane constants) | kidx (256: the fused index
+    // check's lane constants under those tables)
+    uint32_t il_S;
+    uint64_t off_il;
 };

@@ -224,6 +224,8 @@ def lib():
     L.zhip_host_copy.restype = ctypes.c_int
     L.zhip_emulate_chunk_crc_pair.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
     L.zhip_emulate_chunk_crc_pair.restype = ctypes.c_uint32
+    L.zhip_emulate_chunk_crc_il.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    L.zhip_emulate_chunk_crc_il.restype = ctypes.c_uint32
     L.zhip_fdiv_eval.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
     L.zhip_fdiv_eval.restype = ctypes.c_uint32
     if L.zhip_abi_version() != 1:
@@ -280,7 +282,8 @@ class Plan:
 
     def emulate_chunk_crc(self, data: bytes, pair: bool = False) -> int:
         buf = ctypes.create_string_buffer(bytes(data) + b"\0" * 16)
-        fn = lib().zhip_emulate_chunk_crc_pair if pair else lib().zhip_emulate_chunk_crc
+        fn = lib().zhip_emulate_chunk_crc_il if pair == "il" else \
+            lib().zhip_emulate_chunk_crc_pair if pair else lib().zhip_emulate_chunk_crc
         return int(fn(self._h, buf))
 
     def __del__(self):
