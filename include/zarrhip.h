@@ -391,6 +391,10 @@ uint32_t zhip_emulate_chunk_crc_pair(const zhip_plan *plan, const uint8_t *data)
  * stride of S steps, A_(4096 S) tables); 0xFFFFFFFF when the plan has no
  * interleaved layout.  Test hook. */
 uint32_t zhip_emulate_chunk_crc_il(const zhip_plan *plan, const uint8_t *data);
+/* The same for k_decode_xw (lane l of 8 KiB span r: eight blocks 1 KiB apart,
+ * A_1024 tables, per-(span, lane) constants); 0xFFFFFFFF when the plan has no
+ * xw layout.  Test hook. */
+uint32_t zhip_emulate_chunk_crc_xw(const zhip_plan *plan, const uint8_t *data);
 uint32_t zhip_fdiv_eval(uint32_t n, uint32_t d);
 
 #ifdef __cplusplus

@@ -301,3 +301,96 @@ extern "C" int cb_copy_wave(const void* src, void* dst, uint64_t nbytes, int K, 
                        (uint4*)dst);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
+
+// A sharded decode's access pattern without codec work: cubic chunks of
+// ce^3 f32 (`cstride` bytes apart in src: the shard packing with its 4-byte
+// CRC), cps^3 per shard in (z, y, x) order, sps^3 shards, scattered as
+// 4 ce-byte rows into the (ce cps sps)^3 f32 out.  C4: ce 32, cps 4, sps 8;
+// the headline: ce 64, cps 2, sps 2.  A "step" is 4 KiB of a chunk, one
+// 16-byte block per thread.
+//   MODE 0: workgroup w takes steps [wK, wK + K) (chunk-contiguous spans)
+//   MODE 1: interleaved: workgroup j of a group of S takes steps j + S k
+//   MODE 2: x-quads: 4 consecutive chunks, workgroup takes K/4 consecutive
+//           steps of each of the four
+//   MODE 3: x-quads by wave: wave v on chunk 4 (w / (chunk / 8 KiB)) + v,
+//           8 KiB contiguous per wave at a 1 KiB lane stride
+struct ScatterGeo {
+    uint64_t cstride;
+    uint32_t ce, cps, sps, spc;  // spc: 4 KiB steps per chunk
+};
+template <int MODE, int K, int S>
+__global__ __launch_bounds__(256) void k_scatter_g(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                   const ScatterGeo g) {
+    const uint32_t t = threadIdx.x;
+    const uint32_t w = blockIdx.x;
+    uint4 v[K];
+    uint32_t cc[K], bb[K];  // chunk, byte in the chunk
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        uint32_t c, b;
+        if constexpr (MODE == 3) {
+            const uint32_t per = g.spc / 2;  // 8 KiB spans per chunk
+            c = (w / per) * 4 + (t >> 6);
+            b = (w % per) * 8192 + 1024 * k + 16 * (t & 63);
+        } else {
+            uint32_t q;  // global step: chunk * spc + step
+            if constexpr (MODE == 0) q = w * K + k;
+            else if constexpr (MODE == 1) q = (w / S) * (S * K) + (w % S) + S * k;
+            else {
+                const uint32_t per = g.spc / (K / 4);
+                q = ((w / per) * 4 + (k & 3)) * g.spc + (w % per) * (K / 4) + (k >> 2);
+            }
+            c = q / g.spc;
+            b = (q % g.spc) * 4096 + 16 * t;
+        }
+        cc[k] = c;
+        bb[k] = b;
+        const v4u_a1 x = *reinterpret_cast<const v4u_a1*>(src + (uint64_t)c * g.cstride + b);
+        v[k] = make_uint4(x.x, x.y, x.z, x.w);
+    }
+    const uint32_t row = 4 * g.ce, plane = row * g.ce, c3 = g.cps * g.cps * g.cps;
+    const uint64_t N = (uint64_t)g.ce * g.cps * g.sps;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint32_t c = cc[k], b = bb[k];
+        const uint32_t s = c / c3, i = c % c3;
+        const uint32_t sz = s / (g.sps * g.sps), sy = (s / g.sps) % g.sps, sx = s % g.sps;
+        const uint32_t iz = i / (g.cps * g.cps), iy = (i / g.cps) % g.cps, ix = i % g.cps;
+        const uint32_t z = b / plane, y = (b / row) % g.ce, xb = b % row;
+        const uint64_t o = (((sz * g.cps + iz) * g.ce + z) * N + (sy * g.cps + iy) * g.ce + y) * N * 4 +
+                           (uint64_t)(sx * g.cps + ix) * g.ce * 4 + xb;
+        v4u x = {v[k].x, v[k].y, v[k].z, v[k].w};
+        __builtin_nontemporal_store(x, reinterpret_cast<v4u*>(dst + o));
+    }
+}
+
+// mode: 0 natural (K 1, 2, 4, 8, 16), 1 interleaved (S 4 / 8, K 8), 2 x-quads
+// (K 4, 8, 16), 3 x-quads by wave (K 8); ce 32 = C4, 64 = the headline
+extern "C" int cb_scatter_geo(const void* src, void* dst, uint64_t cstride, int ce, int mode, int K, int S,
+                              void* stream) {
+    ScatterGeo g;
+    g.cstride = cstride;
+    g.ce = ce;
+    g.cps = ce == 32 ? 4 : 2;
+    g.sps = ce == 32 ? 8 : 2;
+    g.spc = ce * ce * ce * 4 / 4096;
+    const uint32_t n_chunks = g.cps * g.cps * g.cps * g.sps * g.sps * g.sps;
+    const uint32_t n_steps = n_chunks * g.spc;
+    typedef void (*SFn)(const uint8_t*, uint8_t*, const ScatterGeo);
+    SFn fn = nullptr;
+    if (mode == 0 && K == 1) fn = k_scatter_g<0, 1, 1>;
+    if (mode == 0 && K == 2) fn = k_scatter_g<0, 2, 1>;
+    if (mode == 0 && K == 4) fn = k_scatter_g<0, 4, 1>;
+    if (mode == 0 && K == 8) fn = k_scatter_g<0, 8, 1>;
+    if (mode == 0 && K == 16) fn = k_scatter_g<0, 16, 1>;
+    if (mode == 1 && K == 8 && S == 4) fn = k_scatter_g<1, 8, 4>;
+    if (mode == 1 && K == 8 && S == 8) fn = k_scatter_g<1, 8, 8>;
+    if (mode == 2 && K == 4) fn = k_scatter_g<2, 4, 1>;
+    if (mode == 2 && K == 8) fn = k_scatter_g<2, 8, 1>;
+    if (mode == 2 && K == 16) fn = k_scatter_g<2, 16, 1>;
+    if (mode == 3 && K == 8) fn = k_scatter_g<3, 8, 1>;
+    if (!fn) return -1;
+    const uint32_t grid = mode == 3 ? n_chunks / 4 * (g.spc / 2) : n_steps / K;
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const uint8_t*)src, (uint8_t*)dst, g);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}

@@ -103,6 +103,22 @@ def main():
             arms[f"scatter_{nm}_u{u}"] = graph_of(
                 lambda i, sh, cs=cs, u=u: cb.cb_scatter(ssrc[i % R].data_ptr(), dsts[i % R].data_ptr(), cs, u,
                                                         ctypes.c_void_p(sh)))
+    # the sharded decode's access pattern without codec work (scripts/copybench
+    # k_scatter_g): source chunks at the shard packing's stride, 4 ce-byte rows
+    cb.cb_scatter_geo.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
+                                  ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    ce = inner[0]
+    cstride = ce ** 3 * 4 + 4
+    Rg = R if cfg == "headline" else 1
+    srcg = [torch.empty(n_inner * cstride + 64, dtype=torch.uint8, device=dev).fill_(5) for _ in range(Rg)]
+    for nm, mode, K, S in (("nat_K1", 0, 1, 1), ("nat_K2", 0, 2, 1), ("nat_K4", 0, 4, 1), ("nat_K8", 0, 8, 1),
+                           ("nat_K16", 0, 16, 1), ("il_S4_K8", 1, 8, 4), ("il_S8_K8", 1, 8, 8),
+                           ("xq_K4", 2, 4, 1), ("xq_K8", 2, 8, 1), ("xq_K16", 2, 16, 1), ("xw_K8", 3, 8, 1)):
+        arms[f"scatterg_{nm}"] = graph_of(lambda i, sh, mode=mode, K=K, S=S: cb.cb_scatter_geo(
+            srcg[i % Rg].data_ptr(), dsts[i % Rg].data_ptr(), cstride, ce, mode, K, S, ctypes.c_void_p(sh)))
+    if os.environ.get("COPIES", "1") == "0":
+        arms = {k: v for k, v in arms.items() if not (k.startswith("copy") or k.startswith("scatter_"))
+                or k in ("copy_4k_ldef", "copy_32k_k8_ldef")}
     res = {k: [] for k in arms}
     for _ in range(int(os.environ.get("ROUNDS", "5"))):
         for k, gr in arms.items():

@@ -231,3 +231,21 @@ def test_emulated_interleaved_crc_matches_oracle(n):
         assert got == 0xFFFFFFFF
     else:
         assert got == O.crc32c(data)
+
+
+@pytest.mark.parametrize("n", [4096, 32768, 65536, 131072, 1048576, 4100, 65552, 2 ** 21 + 4096])
+def test_emulated_xw_crc_matches_oracle(n):
+    """k_decode_xw's decomposition (lane l of 8 KiB span r: eight blocks 1 KiB
+    apart through the A_1024 tables, per-(span, lane) constants, negative
+    shifts for the spans past the chunk end) reproduces crc32c."""
+    from zarr_hip import _native as N
+
+    rng = np.random.default_rng(n)
+    data = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+    L = N.Layout()
+    L.ndim, L.itemsize = 1, 1
+    L.shape[0] = n
+    L.nbytes = n
+    L.flags = N.LF_CRC
+    plan = N.Plan(L, upload=False)
+    assert plan.emulate_chunk_crc(data, pair="xw") == O.crc32c(data)

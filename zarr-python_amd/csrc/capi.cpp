@@ -244,6 +244,13 @@ int zhip_plan_create(const zhip_layout* layout, zhip_plan** out) {
         for (uint32_t S = 8; S >= 2 && !p->il_S; S /= 2)
             if (n_steps % (S * (uint32_t)kDefaultBlocks) == 0) p->il_S = S;
     }
+    // k_decode_xw: 8 KiB spans (whole-row layouts keep E a multiple of 4 KiB)
+    p->xw_P = 0;
+    p->xw_nsub = 0;
+    if (p->kblocks == (uint32_t)kDefaultBlocks && (L.flags & ZHIP_LF_CRC) && !(L.flags & ZHIP_LF_NO_WRITE)) {
+        p->xw_P = p->nseg * 4u;
+        if (p->xw_P > 32u && p->xw_P <= 1024u) p->xw_nsub = (p->xw_P + 31u) / 32u;
+    }
     p->R = (uint64_t)p->E + kWgStride;
     p->c_inv = xpow8_inv(p->R - n);
     p->c3 = gf_mul(xpow8(n), 0xFFFFFFFFu);
@@ -330,7 +337,8 @@ int zhip_plan_upload(zhip_plan* p) {
     const size_t n_old = 4096 + kThreads + p->nseg + (size_t)p->nseg * kThreads;
     const size_t n_pair = kPairTabWords + (size_t)p->nseg * kThreads + kThreads;
     const size_t n_il = p->il_S ? kPairTabWords + (size_t)p->nseg * kThreads + kThreads : 0;
-    std::vector<uint32_t> h(n_old + n_pair + n_il);
+    const size_t n_xw = p->xw_P ? kPairTabWords + (size_t)p->xw_P * 64 + kThreads : 0;
+    std::vector<uint32_t> h(n_old + n_pair + n_il + n_xw);
     build_horner(h.data());
     for (int t = 0; t < kThreads; ++t) h[4096 + t] = xpow8((uint64_t)kWgStride - 16u * t);
     for (uint32_t s = 0; s < p->nseg; ++s) h[4096 + kThreads + s] = xpow8((uint64_t)s * p->seg);
@@ -375,6 +383,28 @@ int zhip_plan_upload(zhip_plan* p) {
         for (int t = 0; t < kThreads; ++t)
             il[kPairTabWords + (size_t)p->nseg * kThreads + t] =
                 gf_mul(h[n_old + kPairTabWords + (size_t)p->nseg * kThreads + t], back);
+    }
+    p->off_xw = 0;
+    if (p->xw_P) {
+        // k_decode_xw: lane l of span r takes blocks p_k = lo + 8192 r + 1024 k
+        // + 16 l (k < 8); its chain (A_1024) leaves block 0 multiplied by
+        // x^(8 8192), so the constant x^(8 (E - p_0 + 4096 - 8192)) c_inv
+        // x^(-96) gives every word the pair kernel's frame
+        p->off_xw = n_old + n_pair + n_il;
+        uint32_t* xw = h.data() + p->off_xw;
+        build_pair_tables(xw, 1024);
+        const int64_t n_steps = (int64_t)p->nseg * kDefaultBlocks;
+        for (uint32_t r = 0; r < p->xw_P; ++r)
+            for (int l = 0; l < 64; ++l) {
+                const int64_t e = (int64_t)kWgStride * (n_steps - 2 * (int64_t)r - 1) - 16 * l;
+                const uint32_t xe = e >= 0 ? xpow8((uint64_t)e) : xpow8_inv((uint64_t)(-e));
+                xw[kPairTabWords + (size_t)r * 64 + l] = gf_mul(gf_mul(xe, p->c_inv), c96);
+            }
+        // the fused index check under A_1024: state A_1024(w) instead of A4096(w)
+        const uint32_t fwd = xpow8((uint64_t)kWgStride - 1024u);
+        for (int t = 0; t < kThreads; ++t)
+            xw[kPairTabWords + (size_t)p->xw_P * 64 + t] =
+                gf_mul(h[n_old + kPairTabWords + (size_t)p->nseg * kThreads + t], fwd);
     }
     if (p->d_tables) (void)hipFree(p->d_tables);
     p->d_tables = nullptr;
@@ -504,7 +534,8 @@ int zhip_plan_kernel_flags(const zhip_plan* p, uint32_t* flags) {
 int zhip_plan_info(const zhip_plan* p, uint32_t* units_per_chunk, uint32_t* workspace_words) {
     if (!p) return set_err(ZHIP_E_INVALID, "null plan");
     if (units_per_chunk) *units_per_chunk = p->nseg;
-    if (workspace_words) *workspace_words = 4 + 2 * p->n_sub;  // + the grouped kernels' subgroup words
+    // + the grouped kernels' / k_decode_xw's arrival subwords
+    if (workspace_words) *workspace_words = 4 + 2 * std::max(p->n_sub, p->xw_nsub);
     return ZHIP_OK;
 }
 
@@ -639,6 +670,13 @@ int zhip_decode_mapped(const zhip_plan* plan, const void* src, uint64_t src_size
         p.il_tab = plan->d_tables + plan->off_il;
         p.il_klane = p.il_tab + kPairTabWords;
         p.il_kidx = p.il_klane + (size_t)plan->nseg * kThreads;
+    }
+    p.xw = (plan->xw_P && (n_index == 0 || plan->idx_E <= (uint32_t)kWgStride)) ? plan->xw_P : 0u;
+    if (p.xw) {
+        p.xw_nsub = plan->xw_nsub;
+        p.xw_tab = plan->d_tables + plan->off_xw;
+        p.xw_klane = p.xw_tab + kPairTabWords;
+        p.xw_kidx = p.xw_klane + (size_t)plan->xw_P * 64;
     }
     for (int op = 0; op < 4; ++op) p.hx[op] = plan->hx[op];
     for (int i = 0; i < 32; ++i) p.kq[i] = plan->kq[i];
@@ -1038,6 +1076,48 @@ uint32_t zhip_emulate_chunk_crc_il(const zhip_plan* plan, const uint8_t* data) {
             V ^= gf_mul(Sx, gf_mul(gf_mul(xe, plan->c_inv), c96));
         }
     }
+    return ~(V ^ plan->c3);
+}
+
+// CPU emulation of k_decode_xw's CRC for one chunk: lane l of span r takes
+// blocks at 8192 r + 1024 k + 16 l (k < 8) through the A_1024 tables, folds
+// with the A4 tables and multiplies by the (r, l) lane constant; -1 when the
+// plan has no xw layout.  Test hook.
+uint32_t zhip_emulate_chunk_crc_xw(const zhip_plan* plan, const uint8_t* data) {
+    std::call_once(g_once, init_tables);
+    if (!plan || !plan->xw_P) return 0xFFFFFFFFu;
+    std::vector<uint32_t> tab(kPairTabWords);
+    build_pair_tables(tab.data(), 1024);
+    const uint32_t* T = tab.data();
+    auto a11 = [&](uint32_t w) { return T[kPairT1 + (w & 2047u)] ^ T[kPairT2 + ((w >> 11) & 2047u)] ^ T[kPairT3 + (w >> 22)]; };
+    auto a4 = [&](uint32_t w) {
+        const uint32_t* t4 = T + kPairA4;
+        return t4[w & 255u] ^ t4[256 + ((w >> 8) & 255u)] ^ t4[512 + ((w >> 16) & 255u)] ^ t4[768 + (w >> 24)];
+    };
+    const uint32_t N = (uint32_t)plan->layout.nbytes;
+    const uint32_t c96 = xpow8_inv(12);
+    const int64_t n_steps = (int64_t)plan->nseg * kDefaultBlocks;
+    const int64_t lo_frame = (int64_t)plan->E - n_steps * kWgStride;
+    uint32_t V = 0;
+    for (uint32_t r = 0; r < plan->xw_P; ++r)
+        for (int l = 0; l < 64; ++l) {
+            uint32_t a[4] = {0, 0, 0, 0};
+            for (int k = 0; k < kDefaultBlocks; ++k) {
+                const int64_t o = lo_frame + 8192 * (int64_t)r + 1024 * k + 16 * l;
+                uint8_t b[16] = {0};
+                for (int i = 0; i < 16; ++i) {
+                    const int64_t q = o + i;
+                    if (q >= 0 && q < (int64_t)N) b[i] = data[q];
+                }
+                uint32_t w[4];
+                std::memcpy(w, b, 16);
+                for (int j = 0; j < 4; ++j) a[j] = a11(a[j] ^ w[j]);
+            }
+            const uint32_t Sx = a4(a4(a4(a[0]) ^ a[1]) ^ a[2]) ^ a[3];
+            const int64_t e = (int64_t)kWgStride * (n_steps - 2 * (int64_t)r - 1) - 16 * l;
+            const uint32_t xe = e >= 0 ? xpow8((uint64_t)e) : xpow8_inv((uint64_t)(-e));
+            V ^= gf_mul(Sx, gf_mul(gf_mul(xe, plan->c_inv), c96));
+        }
     return ~(V ^ plan->c3);
 }
 

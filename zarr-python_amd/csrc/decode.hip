@@ -492,6 +492,7 @@ KernelFn select_rows_kernel(bool crc, int item, bool swap, int k);  // decode_ro
 KernelFn select_pair_kernel(bool crc, int item, bool swap, int nu);  // decode_rows.hip
 KernelFn select_duo_kernel(bool crc, int item, bool swap);           // decode_rows.hip
 KernelFn select_il_kernel(bool crc, int item, bool swap);            // decode_rows.hip
+KernelFn select_xw_kernel(bool crc, int item, bool swap);            // decode_rows.hip
 KernelFn select_tile4_kernel(bool crc, int item, bool swap);         // decode_tile.hip
 KernelFn select_tileg_kernel(bool crc, int item, bool swap);         // decode_tile.hip
 
@@ -501,12 +502,24 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
         // one workgroup per pair of units, non-persistent (k_decode_pair)
         const int nu = (p.tune & kTuneSingle) ? 1 : 2;
         const bool crc = (p.lflags & ZHIP_LF_CRC) != 0, swap = (p.lflags & ZHIP_LF_SWAP) != 0;
-        // batches of more than one resident wave of pair workgroups (4 per CU):
-        // interleaved steps (k_decode_il), whose access order keeps the HBM
-        // streaming at 4 GiB (see decode_rows.hip); kTuneIl / kTuneNoIl force
-        const uint32_t resident_pairs = (uint32_t)(max_grid / 8) * 4u;
+        // chunks of a multiple of 8 x 32 KiB: interleaved steps in groups of
+        // eight workgroups (k_decode_il, see decode_rows.hip) -- graph-timed
+        // 26.4 vs 27.8 us on the headline; groups of four lose to the pair
+        // kernel at C4 (profiles/r03/il/).  kTuneIl / kTuneNoIl force.
         const bool il = p.il_S != 0 && crc && !(p.tune & (kTuneNoIl | kTuneSkipCrc | kTuneSingle | kTuneDuo)) &&
-                        ((p.tune & kTuneIl) || (uint64_t)p.n_units > 2ull * resident_pairs);
+                        ((p.tune & kTuneIl) || p.il_S == 8u);
+        const bool xw = p.xw != 0 && crc && (p.tune & kTuneXw) &&
+                        !(p.tune & (kTuneNoXw | kTuneSkipCrc | kTuneSingle | kTuneDuo | kTuneIl));
+        if (xw) {
+            KernelFn xfn = select_xw_kernel(crc, p.g.itemsize, swap);
+            if (!xfn) return ZHIP_E_UNSUPPORTED;
+            const uint64_t xg = (uint64_t)((p.n_chunks + 3u) / 4u) * p.xw;
+            const uint64_t grid = xg > p.n_idx ? xg : p.n_idx;
+            if (grid == 0) return ZHIP_OK;
+            if (grid > 0x7FFFFFFFull) return ZHIP_E_UNSUPPORTED;
+            hipLaunchKernelGGL(xfn, dim3((uint32_t)grid), dim3(kThreads), 0, stream, p);
+            return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
+        }
         if (il) {
             KernelFn ifn = select_il_kernel(crc, p.g.itemsize, swap);
             if (!ifn) return ZHIP_E_UNSUPPORTED;

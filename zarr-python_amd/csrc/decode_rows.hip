@@ -1106,7 +1106,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))
             v = wave_xor(v);
             if ((t & 63) == 0) s_red[0][t >> 6] = v;
             __syncthreads();
-            if (ok && t < 64) {
+            if (ok && t < 64 && !(p.tune & kTuneNoPub)) {
                 const uint32_t V = __builtin_amdgcn_readfirstlane(s_red[0][0] ^ s_red[0][1] ^ s_red[0][2] ^ s_red[0][3]);
                 publish_il(p, c, r, wpc, V, __builtin_amdgcn_readfirstlane(stored), t);
             }
@@ -1128,6 +1128,160 @@ KernelFn select_il_kernel(bool crc, int item, bool swap) {
                            : (swap ? k_decode_il<false, 4, true> : k_decode_il<false, 4, false>);
         case 8: return crc ? (swap ? k_decode_il<true, 8, true> : k_decode_il<true, 8, false>)
                            : (swap ? k_decode_il<false, 8, true> : k_decode_il<false, 8, false>);
+        default: return nullptr;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_decode_xw: the whole-row decode with the four waves of a workgroup on four
+// consecutive chunks of the batch (a shard's x-adjacent inner chunks), each
+// wave on the same 8 KiB span (r of P = chunk / 8 KiB) of its own chunk: lane
+// l's eight blocks at 1 KiB apart, so one wave streams 8 KiB contiguously and
+// the workgroup's stores are the four chunks' rows side by side in the out
+// (512-byte runs for C4's 128-byte rows).  That access order copies at 0.80 of
+// HBM peak on the headline and 0.68-0.69 at C4, where the pair kernel's 32 KiB
+// per-lane-strided spans reach 0.75 / 0.63 (scripts/copybench k_scatter_g,
+// profiles/r03/xw/).  Per lane one Horner chain through the A_1024 11/11/10
+// tables (four word accumulators, A4 fold), one windowed lane multiply by the
+// host-built constant of (r, l), one publication per WAVE (no workgroup
+// reduction): arrival bit r, two-level for P > 32 (32-bit subwords in the
+// workspace tail), xor + count above 1024.  Statuses, row-map stores and the
+// fused index checks as k_decode_il.  (CPU emulation: zhip_emulate_chunk_crc_xw.)
+__device__ __forceinline__ void publish_xw(const DecodeParams& p, uint32_t c, uint32_t r, uint32_t V,
+                                           uint32_t stored, uint32_t l) {
+    const uint32_t P = p.xw, ns = p.xw_nsub;
+    if (P <= 32u || ns == 0u) {
+        publish_il(p, c, r, P, V, stored, (int)l);
+        return;
+    }
+    const uint32_t sg = r >> 5, in_sg = min(32u, P - (sg << 5));
+    const uint64_t bit = 1ull << (r & 31u);
+    uint64_t* sw = reinterpret_cast<uint64_t*>(p.ws + 4ull * p.n_chunks) + (uint64_t)c * ns + sg;
+    uint64_t prev = 0;
+    if (l == 0) prev = __hip_atomic_fetch_xor(sw, (bit << 32) | V, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)prev);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(prev >> 32));
+    const uint64_t full = in_sg >= 32u ? 0xFFFFFFFFull : ((1ull << in_sg) - 1ull);
+    if ((uint64_t)(hi ^ (uint32_t)bit) != full) return;
+    if (l == 0) __hip_atomic_store(sw, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    publish_il(p, c, sg, ns, V ^ lo, stored, (int)l);
+}
+
+template <bool CRC, int ITEM, bool SWAP>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_decode_xw(const DecodeParams p) {
+    constexpr int K = kDefaultBlocks;
+    __shared__ uint32_t s_tab[CRC ? kPairTabWords : 1];
+    __shared__ uint32_t s_mul[CRC ? 12 * kThreads : 1];
+    __shared__ uint32_t s_red[kThreads / 64];
+    const int t = threadIdx.x;
+    const uint32_t l = (uint32_t)t & 63u;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane((uint32_t)t >> 6);
+    const uint32_t G = gridDim.x, g = blockIdx.x;
+    const uint32_t P = p.xw;  // 8 KiB spans per chunk
+    const uint32_t quad = g / P, r = g - quad * P;
+    if (quad * 4u >= p.n_chunks && g >= p.n_idx) return;  // workgroup-uniform
+    const uint32_t c = quad * 4u + wv;
+    const bool has = c < p.n_chunks;
+    const uint32_t expected = p.g.nbytes + (CRC ? 4u : 0u);
+    const uint8_t* zero = reinterpret_cast<const uint8_t*>(g_rows_zero);
+    // 1. vector loads in a path-independent order: [CRC: tables (6), the lane
+    //    constant, the index lane constant, the first index block], the K data
+    //    blocks; headers, row-map entries and the trailer are scalar (per wave)
+    uint4 tv0, tv1, tv2, tv3, tv4, tv5;
+    uint32_t kl = 0, kix = 0;
+    if constexpr (CRC) {
+        const uint4* gt = reinterpret_cast<const uint4*>(p.xw_tab);
+        tv0 = gt[t];
+        tv1 = gt[t + kThreads];
+        tv2 = gt[t + 2 * kThreads];
+        tv3 = gt[t + 3 * kThreads];
+        tv4 = gt[t + 4 * kThreads];
+        tv5 = gt[t + 5 * kThreads];
+        kl = load_u32_any(reinterpret_cast<const uint8_t*>(p.xw_klane + (size_t)r * 64u + l));
+        kix = load_u32_any(reinterpret_cast<const uint8_t*>(p.xw_kidx + t));
+    }
+    Unit U;
+    if (has) U = resolve_unit(p, c * p.nseg, expected);
+    else {
+        U.c = 0;
+        U.sidx = 0;
+        U.mode = ZHIP_ST_MISSING;
+        U.cp = zero;
+        U.seg_lo = 0;
+        U.sel = 0;
+        U.out_off = 0;
+    }
+    const bool ok = has && U.mode == ZHIP_ST_OK;
+    const int32_t lo_frame = (int32_t)p.E - (int32_t)(p.nseg * p.seg);  // a multiple of 4096 (whole rows)
+    uint4 ipre = make_uint4(0, 0, 0, 0);
+    if constexpr (CRC) ipre = index_prefetch(p, g, g < p.n_idx, t, zero);
+    uint4 A[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int32_t base = lo_frame + 8192 * (int32_t)r + 1024 * k;
+        A[k] = load_stream16_any(ok && base >= 0 ? U.cp + base + 16 * l : zero);
+    }
+    // destinations of the span's two 4 KiB steps (scalar loads)
+    zhip_rowblk m[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const uint32_t st = 2u * r + (uint32_t)h;
+        const uint32_t sidx = p.nseg - 1u - st / (uint32_t)K;
+        m[h] = load_uniform<zhip_rowblk>(p.rowmap + ((size_t)U.sel * p.nseg + sidx) * K + (st % (uint32_t)K));
+    }
+    uint32_t stored = 0;
+    if (CRC && ok) stored = load_trailer_uniform(U.cp, p.g.nbytes);
+    // 2. tables into LDS, the lane-multiply column
+    if constexpr (CRC) {
+        uint4* stt = reinterpret_cast<uint4*>(s_tab);
+        stt[t] = tv0;
+        stt[t + kThreads] = tv1;
+        stt[t + 2 * kThreads] = tv2;
+        stt[t + 3 * kThreads] = tv3;
+        stt[t + 4 * kThreads] = tv4;
+        stt[t + 5 * kThreads] = tv5;
+        lanemul3_init(s_mul, t, kl);
+        __syncthreads();
+    }
+    if (has) {
+        // 3. stores, each block's Horner step after its store
+        uint8_t* sink = reinterpret_cast<uint8_t*>(g_rows_sink);
+        const bool writes = ok || U.mode == ZHIP_ST_MISSING;
+        uint8_t* const obase = p.out + U.out_off;
+        const uint4 f = make_uint4(p.fill[0], p.fill[1], p.fill[2], p.fill[3]);
+        const uint32_t rmask = (1u << p.row_shift) - 1u;
+        Acc4 acc = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const zhip_rowblk& mk = m[k >> 2];
+            const uint32_t o = 1024u * (uint32_t)(k & 3) + 16u * l;  // byte in the 4 KiB step
+            const uint32_t lane_row = o >> p.row_shift;
+            const bool wr = writes && lane_row - mk.lo < mk.hi - mk.lo;
+            const int64_t lane_off = (int64_t)lane_row * p.r_oy + (int64_t)(o & rmask);
+            store_nt16(wr ? obase + mk.rel + lane_off : sink, ok ? swap_block<ITEM, SWAP>(A[k]) : f);
+            if (CRC && ok) crc_block4(s_tab, acc, A[k]);
+        }
+        // 4. run end: one chain per lane, one publication per wave
+        if constexpr (CRC) {
+            uint32_t v = ok ? lanemul3(s_mul, t, fold4(s_tab, acc)) : 0u;
+            v = wave_xor(v);
+            if (ok && !(p.tune & kTuneNoPub))
+                publish_xw(p, c, r, __builtin_amdgcn_readfirstlane(v), __builtin_amdgcn_readfirstlane(stored), l);
+        }
+        if (r == 0) unit_status_pair(p, U, CRC, (int)l);
+    }
+    // 5. fused shard-index checks (one step per lane), the first block prefetched
+    if constexpr (CRC)
+        for (uint32_t j = g; j < p.n_idx; j += G) verify_index_pair(p, j, t, kix, s_tab, s_red, j == g, ipre);
+}
+
+KernelFn select_xw_kernel(bool crc, int item, bool swap) {
+    if (!crc) return nullptr;
+    switch (item) {
+        case 1: return k_decode_xw<true, 1, false>;
+        case 2: return swap ? k_decode_xw<true, 2, true> : k_decode_xw<true, 2, false>;
+        case 4: return swap ? k_decode_xw<true, 4, true> : k_decode_xw<true, 4, false>;
+        case 8: return swap ? k_decode_xw<true, 8, true> : k_decode_xw<true, 8, false>;
         default: return nullptr;
     }
 }

@@ -113,6 +113,13 @@ struct DecodeParams {
     const uint32_t* il_tab;
     const uint32_t* il_klane;
     const uint32_t* il_kidx;
+    // k_decode_xw: 8 KiB spans per chunk (0: not available), arrival subwords
+    // per chunk in the workspace tail (0: one level or xor + count), its A_1024
+    // tables, lane constants per (span, lane) and for the fused index check
+    uint32_t xw, xw_nsub;
+    const uint32_t* xw_tab;
+    const uint32_t* xw_klane;
+    const uint32_t* xw_kidx;
     // load-address prediction (zhip_predict; k_decode_pair): payload of chunk c
     // predicted at src + pred_base + (c / pred_per) * pred_outer + (c % pred_per) * pred_inner
     uint32_t pred, pred_per;
@@ -146,6 +153,9 @@ constexpr uint32_t kTunePrio = 16777216u;     // k_decode_pair arm: s_setprio(1)
 constexpr uint32_t kTuneDeferB = 33554432u;   // k_decode_pair arm: unit B's loads interleaved with A's stores
 constexpr uint32_t kTuneIl = 67108864u;       // whole-row layouts: k_decode_il wherever the layout admits it
 constexpr uint32_t kTuneNoIl = 134217728u;    // whole-row layouts: never k_decode_il (k_decode_pair)
+constexpr uint32_t kTuneXw = 268435456u;      // whole-row layouts: k_decode_xw where admitted
+constexpr uint32_t kTuneNoXw = 536870912u;    // whole-row layouts: never k_decode_xw
+constexpr uint32_t kTuneNoPub = 1073741824u;  // timing arm: k_decode_il / k_decode_xw skip the CRC publication
 constexpr uint32_t kTuneStamp = 1024u;    // k_decode_pair: per-workgroup phase timestamps (zhip_debug_stamps)
 constexpr uint32_t kStampWG = 8192u;      // workgroups stamped per launch
 constexpr uint32_t kStampSlots = 8u;
@@ -275,4 +285,10 @@ struct zhip_plan {
     // check's lane constants under those tables)
     uint32_t il_S;
     uint64_t off_il;
+    // k_decode_xw (decode_rows.hip): xw_P = 8 KiB spans per chunk (0: not
+    // available), xw_nsub = two-level arrival subwords (P > 32, P <= 1024).
+    // d_tables continues at off_xw with the tables of A_1024 | klane (P x 64) |
+    // kidx (256)
+    uint32_t xw_P, xw_nsub;
+    uint64_t off_xw;
 };

@@ -226,6 +226,8 @@ def lib():
     L.zhip_emulate_chunk_crc_pair.restype = ctypes.c_uint32
     L.zhip_emulate_chunk_crc_il.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
     L.zhip_emulate_chunk_crc_il.restype = ctypes.c_uint32
+    L.zhip_emulate_chunk_crc_xw.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    L.zhip_emulate_chunk_crc_xw.restype = ctypes.c_uint32
     L.zhip_fdiv_eval.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
     L.zhip_fdiv_eval.restype = ctypes.c_uint32
     if L.zhip_abi_version() != 1:
@@ -282,7 +284,7 @@ class Plan:
 
     def emulate_chunk_crc(self, data: bytes, pair: bool = False) -> int:
         buf = ctypes.create_string_buffer(bytes(data) + b"\0" * 16)
-        fn = lib().zhip_emulate_chunk_crc_il if pair == "il" else \
+        fn = lib().zhip_emulate_chunk_crc_il if pair == "il" else lib().zhip_emulate_chunk_crc_xw if pair == "xw" else \
             lib().zhip_emulate_chunk_crc_pair if pair else lib().zhip_emulate_chunk_crc
         return int(fn(self._h, buf))
 
