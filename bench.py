@@ -266,6 +266,26 @@ def extra_configs(ctx, args):
         wall, kern = time_programs([p for p, _ in progs], steps, 3, device)
         dec = data.numel() * 4
         out["c2_unsharded_256"] = _entry(dec, dec + 64 * (1048576 + 4), wall, kern, checked="bytes")
+        del progs
+        # the headline array with zarr's DEFAULT sharding codecs (inner chunks
+        # bytes only, index bytes + crc32c: sharding.py:423-427): the index
+        # checks ride in leading workgroups of the data launch (k_decode_lead)
+        progs = []
+        for _ in range(args.replicas):
+            p, o = build_replica(device, data, shape, chunks, [LE], shards=(128, 128, 128)).prepare_read(
+                (Ellipsis,))
+            progs.append((p, o))
+        progs[0][0].launch()
+        progs[0][0].results()
+        if not torch.equal(progs[0][1].view(torch.int32), data.view(torch.int32)):
+            raise SystemExit("bench sharded default chain: decoded bytes differ from the source")
+        fused = progs[0][0].index is None and progs[0][0].data.n_idx == 8
+        wall, kern = time_programs([p for p, _ in progs], steps, 3, device)
+        out["sharded_default_chain_256"] = _entry(
+            dec, dec + 64 * 1048576 + 8 * (8 * 16 + 4), wall, kern, checked="bytes",
+            kernel="k_decode_lead (index checks in 8 leading workgroups)" if fused
+            else "separate index launch + k_decode_pair<noCRC>",
+            note="headline array and shards, zarr's default sharding codecs: inner bytes only, index bytes+crc32c")
         del progs, data
     if single and "c3" in args.extra:
         data = torch.from_numpy(synthetic(shape, seed=0)).to(device)
@@ -312,6 +332,9 @@ def extra_configs(ctx, args):
     if "c5" in args.extra:
         out["c5_partial_2048"] = c5_partial(ctx, args)
         torch.cuda.empty_cache()
+        if single:
+            out["c5_host_coalesced"] = c5_host(ctx, args)
+            torch.cuda.empty_cache()
     if single and "enc" in args.extra:
         out["encode_c2"] = encode_c2(device, args)
         torch.cuda.empty_cache()
@@ -483,6 +506,78 @@ def c5_partial(ctx, args):
                        "decoded_GiBps = all ranks' decoded bytes / max rank step time")
 
 
+def c5_host(ctx, args):
+    """C5 from a HOST store (examples/sharding_coalescing): the same 2048^3
+    int16 array, 256^3 shards of 64^3 inner chunks, in a host MemoryStore; the
+    random 10 % of inner chunks read into a device out through the pipeline's
+    host path -- one index suffix request per touched shard, the touched inner
+    chunks fetched by coalesced range requests (store.get_ranges_sync with the
+    reference's 1 MiB gap / 16 MiB span rules, src/zarr/core/_coalesce.py:61-135),
+    packed into pinned windows and decoded on the GPU.  Reports the requests
+    issued per read next to what an uncoalesced reader would issue, and the
+    host -> HBM decoded rate (PCIe-inclusive: never the headline)."""
+    import torch
+
+    import zarr_hip
+
+    g = W.C5
+    shape, shards, inner = g["shape"], g["shards"], g["inner"]
+    gen = torch.Generator(device=ctx.device).manual_seed(0)
+    data = torch.randint(-2 ** 15, 2 ** 15, shape, generator=gen, device=ctx.device, dtype=torch.int16)
+    n_shards = int(np.prod([s // c for s, c in zip(shape, shards)]))
+    shard_bytes = int(np.prod(shards)) * 2 + 64 * 4 + 64 * 16 + 4
+    dstore = zarr_hip.DeviceStore(ctx.device, capacity=n_shards * (shard_bytes + 256) + (1 << 24))
+    darr = zarr_hip.Array.create(dstore, shape, inner, "int16", 0, shards=shards, inner_codecs=[LE, CRC])
+    sbatch, _ = darr.batch_info((Ellipsis,))
+    for i in range(0, len(sbatch), 64):
+        darr.codec_pipeline.write_sync(sbatch[i:i + 64], data)
+    torch.cuda.synchronize(ctx.device)
+
+    class CountingStore(zarr_hip.MemoryStore):
+        calls = 0
+        fetched = 0
+
+        def get_sync(self, key, byte_range=None, prototype=None):
+            v = super().get_sync(key, byte_range, prototype)
+            if not key.endswith("zarr.json"):
+                CountingStore.calls += 1
+                CountingStore.fetched += 0 if v is None else len(v)
+            return v
+
+    host = CountingStore(dstore.to_dict())
+    del dstore, darr
+    torch.cuda.empty_cache()
+    arr = zarr_hip.Array.open(host)
+    grid = tuple(s // i for s, i in zip(shape, inner))
+    coords = W.partial_selection(grid)
+    batch = W.inner_chunk_batch(arr, host, coords, inner)
+    out = torch.empty(shape, dtype=torch.int16, device=ctx.device)
+    arr.codec_pipeline.read_sync(batch, out)
+    torch.cuda.synchronize(ctx.device)
+    check_regions(out, data, batch, "c5 host")
+    del data
+    ts, calls, fetched = [], [], []
+    for _ in range(5):
+        CountingStore.calls = CountingStore.fetched = 0
+        torch.cuda.synchronize(ctx.device)
+        t0 = time.perf_counter()
+        arr.codec_pipeline.read_sync(batch, out)
+        torch.cuda.synchronize(ctx.device)
+        ts.append(time.perf_counter() - t0)
+        calls.append(CountingStore.calls)
+        fetched.append(CountingStore.fetched)
+    touched = len({it[0].path for it in batch})
+    dec = len(batch) * 64 ** 3 * 2
+    med = float(np.median(ts))
+    return {"host_to_hbm_decoded_GiBps": round(dec / med / GIB, 2), "ms_per_read": round(med * 1e3, 2),
+            "requests": int(calls[-1]), "requests_uncoalesced": touched + len(batch),
+            "fetched_MiB": round(fetched[-1] / 2 ** 20, 1), "inner_chunks": len(batch),
+            "shards_touched": touched, "checked": "bytes",
+            "note": "host MemoryStore; index suffix request per touched shard + coalesced inner-chunk "
+                    "range requests (1 MiB gap, 16 MiB span); requests_uncoalesced = index + one per "
+                    "inner chunk; PCIe-inclusive"}
+
+
 class _EncodeProg:
     """One prepared k_encode launch (what ChunkWriter._encode_chunks issues for
     complete chunks) in the program interface ReadGraph replays."""
@@ -492,6 +587,9 @@ class _EncodeProg:
 
     def launch(self, stream=None):
         self.l.launch(stream)
+
+    def check_fresh(self):
+        return None
 
     def results(self):
         return None
@@ -840,6 +938,9 @@ def pmc_traffic():
 
 # ------------------------------------------------------------------------ main
 
+HEADLINE_KERNEL = ["?"]  # the decode kernel the library launched for the headline (zhip_last_kernel)
+
+
 def headline(ctx, args, weak: bool = False):
     """The headline batch -- BASELINE's 256^3 f32 array in 128^3 shards of 64^3
     inner chunks -- partitioned round-robin by shard over the ranks (strong
@@ -869,6 +970,8 @@ def headline(ctx, args, weak: bool = False):
             prog.launch()
             prog.results()
             check_regions(out, src, mine, "headline")
+            from zarr_hip import _native as N
+            HEADLINE_KERNEL[0] = N.lib().zhip_last_kernel().decode()
         assert len(mine) == mine_n, "round-robin by shard"
         assert prog.tables.fast and prog.tables.rows, "the headline should take the whole-row kernel"
         assert prog.index is None and prog.data.n_idx == mine_n, "index CRC checks should be fused"
@@ -981,7 +1084,7 @@ def main():
             "traffic_lib_sha16": traffic_sha, "lib_sha16": lib_sha16(),
             "traffic_source": TRAFFIC_JSON + " (FETCH_SIZE x2 + WRITE_SIZE per launch from "
                               "separate rocprofv3 --pmc passes of this command)",
-            "kernel": "zhip::k_decode_pair<CRC,4,noswap,2> (zhip_decode_mapped)",
+            "kernel": f"zhip::{HEADLINE_KERNEL[0]}<CRC,4,noswap> (zhip_decode_mapped)",
             "kernel_ms_avg": round(avg_kern_s * 1e3, 5),
             "kernel_ms_eager_mean": round(float(np.mean(kern_s)) * 1e3, 5),
             "timing": "eager launches" if args.eager else

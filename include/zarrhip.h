@@ -269,7 +269,13 @@ int zhip_decode_mapped(const zhip_plan *plan, const void *src, uint64_t src_size
 #define ZHIP_TUNE_ABLATION 2
 #define ZHIP_TUNE_BLOCKS 3   /* blocks/thread per unit for plans created afterwards (4, 8, 16) */
 #define ZHIP_TUNE_STAGE_STREAMS 4  /* host staging: packed windows on 1 (default) or 2 copy streams */
+#define ZHIP_TUNE_STAGE_COPY 5     /* host copies into / out of pinned memory: 1 streaming stores (default), 0 memcpy */
 int zhip_set_tuning(int key, int value);
+
+/* Name of the decode kernel the last zhip_decode* call on this process
+ * launched ("k_decode_il", "k_decode_pair", "k_decode_lead", ...): a
+ * diagnostic for labels and tests; not synchronised across threads. */
+const char *zhip_last_kernel(void);
 
 /* Diagnostics: with ablation bit 1024 set, k_decode_pair records per-workgroup
  * phase timestamps (s_memrealtime, 100 MHz) for the first 8192 workgroups of

@@ -453,6 +453,67 @@ def test_fused_index_crc_mismatch(device, loc):
     assert str(got.value) == str(want.value)
 
 
+# ---- zarr's default sharding codecs (inner bytes only, index bytes + crc32c):
+# the index checks ride in leading workgroups of the pair decode (VARIANT 9)
+
+DEFAULT_SHARD_CASES = [
+    ((128, 128, 128), (64, 64, 64), (32, 32, 32), "float32", (Ellipsis,), LE),
+    ((128, 128, 128), (64, 64, 64), (32, 32, 32), "float32", (slice(3, 120), slice(32, 96), slice(None)), LE),
+    ((128, 128, 128), (64, 64, 64), (32, 32, 32), "float32", (70, slice(None), slice(None)), BE),
+    ((64, 128, 64), (32, 64, 64), (16, 64, 64), "int16", (Ellipsis,), BE),
+    ((32, 64, 128), (16, 64, 128), (8, 32, 128), "float64", (slice(1, 31), slice(None), slice(None)), LE),
+    ((64, 512, 64), (32, 256, 64), (16, 256, 64), "uint8", (Ellipsis,), {"name": "bytes"}),
+]
+
+
+@pytest.mark.parametrize("shape,shards,inner,dtype,sel,endian", DEFAULT_SHARD_CASES)
+@pytest.mark.parametrize("loc", ["end", "start"])
+def test_default_sharding_chain_fused(device, shape, shards, inner, dtype, sel, endian, loc):
+    import zarr_hip
+
+    codecs = [SHARD(inner, [endian], loc)]
+    meta = O.ArrayMeta(shape, shards, np.dtype(dtype), 0, codecs=codecs)
+    data = _data(shape, dtype, seed=3)
+    # one inner chunk of fill (elided: its index entry is the missing marker)
+    data[tuple(slice(0, i) for i in inner)] = 0
+    host = {}
+    O.write(host, meta, (Ellipsis,), data)
+    store = zarr_hip.DeviceStore.from_host(host, device)
+    arr = zarr_hip.Array.create(store, shape, shards, dtype, 0, codecs=codecs)
+    prog, _ = arr.prepare_read(sel)
+    n_shards = int(np.prod([s // c for s, c in zip(shape, shards)]))
+    assert prog.tables.rows and prog.index is None
+    assert 0 < prog.data.n_idx <= n_shards
+    got = arr[sel]
+    from zarr_hip import _native as N
+    assert N.lib().zhip_last_kernel() == b"k_decode_lead"
+    want = O.read(host, meta, sel)
+    assert got.tobytes() == np.ascontiguousarray(want).tobytes()
+
+
+@pytest.mark.parametrize("loc", ["end", "start"])
+def test_default_sharding_chain_index_crc_mismatch(device, loc):
+    import zarr_hip
+
+    codecs = [SHARD((16, 256), [LE], loc)]
+    meta = O.ArrayMeta((32, 512), (16, 512), np.dtype("float32"), 0.0, codecs=codecs)
+    host = {}
+    O.write(host, meta, (Ellipsis,), _data((32, 512), "float32"))
+    bad = bytearray(host["c/1/0"])
+    pos = len(bad) - 3 if loc == "end" else 16 + 9
+    bad[pos] ^= 0x10
+    host["c/1/0"] = bytes(bad)
+    with pytest.raises(ValueError) as want:
+        O.read(host, meta)
+    store = zarr_hip.DeviceStore.from_host(host, device)
+    arr = zarr_hip.Array.create(store, (32, 512), (16, 512), "float32", 0.0, codecs=codecs)
+    prog, _ = arr.prepare_read((Ellipsis,))
+    assert prog.index is None and prog.data.n_idx == 2 and prog.tables.rows
+    with pytest.raises(ValueError) as got:
+        arr[...]
+    assert str(got.value) == str(want.value)
+
+
 # ------------------------------------ affine whole-row decode (ZHIP_DF_ROWS)
 
 ROWS_CASES = [

@@ -13,9 +13,10 @@ temp dir, and the HBM-resident DeviceStore -- and checks three things:
 Compressed scenarios run with the compressor on the host (1d-gzip,
 transpose-gzip: the built-in gzip; zstd needs zarr's codec instance, which
 tests/test_gpu_compression.py drives with a caller-supplied codec object).
-zarr v2 and nested sharding are not restated as passing cases; the test below
-pins that the GPU path refuses them (and a zstd named only by JSON) loudly
-rather than falling back to the CPU.
+Nested sharding (suite:308-320) runs its outer level on the host and its inner
+level on the GPU (zarr_hip/nested.py).  zarr v2 is not restated; the test
+below pins that the GPU path refuses a zstd named only by JSON loudly rather
+than falling back to the CPU.
 """
 
 from __future__ import annotations
@@ -69,6 +70,14 @@ class Case:
         return [{"name": "sharding_indexed", "configuration": {
             "chunk_shape": list(self.chunks), "codecs": list(self.codecs),
             "index_codecs": [LE, {"name": "crc32c"}], "index_location": self.index_location}}]
+
+
+def _NEST(outer, inner, codecs=(LE,), loc="end"):
+    """sharding_indexed(outer) whose inner chain is sharding_indexed(inner)."""
+    return {"name": "sharding_indexed", "configuration": {
+        "chunk_shape": list(outer), "index_location": loc,
+        "codecs": [{"name": "sharding_indexed", "configuration": {
+            "chunk_shape": list(inner), "codecs": list(codecs)}}]}}
 
 
 def _ar(n, dtype, offset=1):
@@ -136,6 +145,19 @@ CASES = (
          writes=((np.s_[2:13, 5:20], np.arange(165, dtype="i4").reshape(11, 15)),
                  (np.s_[13:24, :], 0)),
          reads=(slice(None), np.s_[11:14, 7], np.s_[::7, 3:21:4])),
+    # nested sharding (suite:308-320), then partial writes / strided reads /
+    # empty inner shards / an index at the start over the same two levels
+    Case("nested-sharding", (20, 20), (10, 10), codecs=(_NEST((10, 10), (5, 5)),), dtype="int32", fill=0,
+         writes=((slice(None), np.arange(400, dtype="i4").reshape(20, 20)),)),
+    Case("nested-sharding-partial", (40, 30), (20, 30), codecs=(_NEST((10, 15), (5, 5), (LE, {"name": "crc32c"})),),
+         dtype="int32", fill=-5,
+         writes=((np.s_[3:27, 4:29], np.arange(600, dtype="i4").reshape(24, 25)), (np.s_[10:20, 0:15], -5),
+                 (np.s_[30:40, 20:30], 9)),
+         reads=(slice(None), np.s_[2:39:3, ::4], np.s_[15, 5:25], np.s_[31:37, 22])),
+    Case("nested-sharding-index-start", (16, 16), (16, 16), codecs=(_NEST((8, 8), (4, 4), (LE,), "start"),),
+         dtype="float32", fill=0.0,
+         writes=((np.s_[0:12, 4:16], np.arange(144, dtype="f4").reshape(12, 12)),),
+         reads=(slice(None), np.s_[1:15:2, 3:9])),
     Case("big-endian-crc", (30, 7), (8, 7), dtype="uint16", fill=3,
          codecs=({"name": "bytes", "configuration": {"endian": "big"}}, {"name": "crc32c"}),
          writes=((np.s_[4:25], np.arange(147, dtype="u2").reshape(21, 7)),),
@@ -297,13 +319,10 @@ def test_read_write_methods_do_not_branch_on_sharding_codec_type():
 
 @pytest.mark.parametrize("codecs,shards,why", [
     ([LE, {"name": "zstd", "configuration": {"level": 1}}], None, "zstd"),
-    ([{"name": "sharding_indexed", "configuration": {
-        "chunk_shape": [10, 10], "codecs": [{"name": "sharding_indexed", "configuration": {
-            "chunk_shape": [5, 5], "codecs": [LE]}}]}}], None, "nested sharding"),
 ])
 def test_out_of_scope_chains_refused_loudly(codecs, shards, why, device):
-    """suite:147-226 (a zstd without its codec instance, v2) and 274-289
-    (nested sharding): the pipeline must raise rather than decode on the host."""
+    """suite:147-226 (a zstd without its codec instance, v2): the pipeline must
+    raise rather than decode on the host."""
     import zarr_hip
 
     store = zarr_hip.DeviceStore(device)

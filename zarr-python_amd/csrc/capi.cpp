@@ -87,14 +87,6 @@ void build_horner_stride(uint32_t* tab, uint64_t stride) {  // [op][slice][256],
     }
 }
 
-zhip_fdiv make_fdiv(uint32_t d) {
-    zhip_fdiv f;
-    uint32_t l = 0;
-    while ((1ull << l) < d) ++l;
-    f.s = 31 + l;
-    f.m = (uint32_t)(((1ull << (31 + l)) + d - 1) / d);  // ceil(2^(31+l)/d) <= 2^32-1 for d>=1... (d=1 -> 2^31)
-    return f;
-}
 
 uint32_t crc_bytewise(const uint8_t* p, size_t n) {
     uint32_t c = 0xFFFFFFFFu;
@@ -195,6 +187,7 @@ int zhip_set_tuning(int key, int value) {
         case ZHIP_TUNE_ABLATION: g_tune_bits = (uint32_t)value; return ZHIP_OK;
         case ZHIP_TUNE_BLOCKS: g_tune_blocks = value; return ZHIP_OK;
         case ZHIP_TUNE_STAGE_STREAMS: zhip_stage_set_streams(value >= 2 ? 2u : 1u); return ZHIP_OK;
+        case ZHIP_TUNE_STAGE_COPY: zhip_stage_set_copy(value ? 1u : 0u); return ZHIP_OK;
         default: return set_err(ZHIP_E_INVALID, "unknown tuning key");
     }
 }
@@ -640,7 +633,12 @@ int zhip_decode_mapped(const zhip_plan* plan, const void* src, uint64_t src_size
         return set_err(ZHIP_E_INVALID, "null device pointer");
     if (n_index) {
         if (!d_index_chunks || !d_index_status) return set_err(ZHIP_E_INVALID, "null index pointer");
-        if (!(plan->layout.flags & ZHIP_LF_SHARDED) || !(plan->layout.flags & ZHIP_LF_CRC) ||
+        // inner chunks without a CRC: only the mapped pair decode carries the
+        // index checks (k_decode_lead, leading workgroups)
+        const bool lead_ok = d_rowmap && (decode_flags & ZHIP_DF_ROWS) && (decode_flags & ZHIP_DF_FAST_ROWS) &&
+                             plan->nseg <= 32u && plan->seg == (uint32_t)kWgStride * kDefaultBlocks &&
+                             !(g_tune_bits & zhip::kTunePersist);
+        if (!(plan->layout.flags & ZHIP_LF_SHARDED) || (!(plan->layout.flags & ZHIP_LF_CRC) && !lead_ok) ||
             (decode_flags & ZHIP_DF_TILE) || plan->idx_nbytes == 0)
             return set_err(ZHIP_E_UNSUPPORTED, "index check cannot be fused for this plan");
     }
@@ -771,6 +769,8 @@ int zhip_decode_mapped(const zhip_plan* plan, const void* src, uint64_t src_size
         p.n_units = (uint32_t)tunits;
         p.fast = 0;
     }
+    if (p.rows && units >= (1ull << 31)) return set_err(ZHIP_E_UNSUPPORTED, "too many units for a row decode");
+    fill_pair_hot(p);
     int rc = launch_decode(p, static_cast<hipStream_t>(stream), plan->max_grid);
     if (rc == ZHIP_E_UNSUPPORTED) return set_err(rc, "no kernel for this layout");
     if (rc != ZHIP_OK) return set_err(rc, std::string("launch failed: ") + hipGetErrorString(hipGetLastError()));

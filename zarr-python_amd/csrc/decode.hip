@@ -492,9 +492,14 @@ KernelFn select_rows_kernel(bool crc, int item, bool swap, int k);  // decode_ro
 KernelFn select_pair_kernel(bool crc, int item, bool swap, int nu);  // decode_rows.hip
 KernelFn select_duo_kernel(bool crc, int item, bool swap);           // decode_rows.hip
 KernelFn select_il_kernel(bool crc, int item, bool swap);            // decode_rows.hip
+KernelFn select_il_kernel_lean(bool crc, int item, bool swap);       // decode_rows.hip
 KernelFn select_xw_kernel(bool crc, int item, bool swap);            // decode_rows.hip
 KernelFn select_tile4_kernel(bool crc, int item, bool swap);         // decode_tile.hip
 KernelFn select_tileg_kernel(bool crc, int item, bool swap);         // decode_tile.hip
+
+// name of the kernel the last launch_decode chose (zhip_last_kernel: bench
+// labels and tests; the selection depends on layout, plan and tuning bits)
+static const char* g_last_kernel = "";
 
 int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
     if (g_tune_max_grid > 0) max_grid = g_tune_max_grid;
@@ -502,6 +507,25 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
         // one workgroup per pair of units, non-persistent (k_decode_pair)
         const int nu = (p.tune & kTuneSingle) ? 1 : 2;
         const bool crc = (p.lflags & ZHIP_LF_CRC) != 0, swap = (p.lflags & ZHIP_LF_SWAP) != 0;
+        if (!crc && p.n_idx) {
+            // inner chunks without a CRC, shard indexes with one (zarr's default
+            // sharding codecs): leading index-check workgroups, then the pairs
+            // (k_decode_lead); > 32 units per chunk is not fused
+            if (p.nseg > 32u) return ZHIP_E_UNSUPPORTED;
+            KernelFn lfn = select_pair_kernel(false, p.g.itemsize, swap, 9);
+            if (!lfn) return ZHIP_E_UNSUPPORTED;
+            const uint32_t pairs = (uint32_t)(((uint64_t)p.n_units + 1u) / 2u);
+            const uint32_t lead = (p.n_idx + 7u) & ~7u;
+            if ((uint64_t)pairs + lead > 0x7FFFFFFFull) return ZHIP_E_UNSUPPORTED;
+            DecodeParams q = p;
+            q.xcd_run = (!(p.tune & kTuneNoXcd) && pairs % 8u == 0u && pairs <= (uint32_t)(max_grid / 8) * 4u)
+                            ? pairs / 8u : 0u;
+            q.h.xcd_run = q.xcd_run;
+            q.h.d_xcd = make_fdiv(q.xcd_run ? q.xcd_run : 1u);
+            g_last_kernel = "k_decode_lead";
+            hipLaunchKernelGGL(lfn, dim3(pairs + lead), dim3(kThreads), 0, stream, q);
+            return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
+        }
         // chunks of a multiple of 8 x 32 KiB: interleaved steps in groups of
         // eight workgroups (k_decode_il, see decode_rows.hip) -- graph-timed
         // 26.4 vs 27.8 us on the headline; groups of four lose to the pair
@@ -517,14 +541,17 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
             const uint64_t grid = xg > p.n_idx ? xg : p.n_idx;
             if (grid == 0) return ZHIP_OK;
             if (grid > 0x7FFFFFFFull) return ZHIP_E_UNSUPPORTED;
+            g_last_kernel = "k_decode_xw";
             hipLaunchKernelGGL(xfn, dim3((uint32_t)grid), dim3(kThreads), 0, stream, p);
             return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
         }
         if (il) {
-            KernelFn ifn = select_il_kernel(crc, p.g.itemsize, swap);
+            KernelFn ifn = (p.tune & kTuneIlLean) ? select_il_kernel_lean(crc, p.g.itemsize, swap)
+                                                  : select_il_kernel(crc, p.g.itemsize, swap);
             if (!ifn) return ZHIP_E_UNSUPPORTED;
             const uint32_t igrid = p.n_units > p.n_idx ? p.n_units : p.n_idx;
             if (igrid == 0) return ZHIP_OK;
+            g_last_kernel = "k_decode_il";
             hipLaunchKernelGGL(ifn, dim3(igrid), dim3(kThreads), 0, stream, p);
             return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
         }
@@ -548,6 +575,7 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
             const uint32_t duos = (uint32_t)(((uint64_t)p.n_units + 1u) / 2u);
             const uint32_t dgrid = duos > p.n_idx ? duos : p.n_idx;
             if (dgrid == 0) return ZHIP_OK;
+            g_last_kernel = "k_decode_duo";
             hipLaunchKernelGGL(dfn, dim3(dgrid), dim3(2 * kThreads), 0, stream, p);
             return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
         }
@@ -559,7 +587,10 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
         DecodeParams q = p;
         q.xcd_run = (nu == 2 && !(p.tune & kTuneNoXcd) && grid % 8u == 0u &&
                      grid <= (uint32_t)(max_grid / 8) * 4u) ? grid / 8u : 0u;
-        hipLaunchKernelGGL(fn, dim3(grid), dim3(kThreads), 0, stream, q);
+        q.h.xcd_run = q.xcd_run;
+        q.h.d_xcd = make_fdiv(q.xcd_run ? q.xcd_run : 1u);
+        g_last_kernel = "k_decode_pair";
+            hipLaunchKernelGGL(fn, dim3(grid), dim3(kThreads), 0, stream, q);
         return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
     }
     if (p.rows) {
@@ -574,6 +605,7 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
                 max_grid = (max_grid / 8) * per_cu;
         }
         const uint32_t grid = p.n_units < (uint32_t)max_grid ? p.n_units : (uint32_t)max_grid;
+        g_last_kernel = "k_decode_rows";
         hipLaunchKernelGGL(fn, dim3(grid), dim3(kThreads), 0, stream, p);
         return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
     }
@@ -582,6 +614,7 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
         KernelFn fn = select_tile4_kernel((p.lflags & ZHIP_LF_CRC) != 0, p.g.itemsize, (p.lflags & ZHIP_LF_SWAP) != 0);
         if (!fn) return ZHIP_E_UNSUPPORTED;
         if (p.n_units == 0) return ZHIP_OK;
+        g_last_kernel = "k_decode_tile4";
         hipLaunchKernelGGL(fn, dim3(p.n_units / 4u), dim3(kThreads), 0, stream, p);
         return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
     }
@@ -591,6 +624,7 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
         if (!fn) return ZHIP_E_UNSUPPORTED;
         if (p.n_chunks == 0) return ZHIP_OK;
         if ((uint64_t)p.n_chunks * p.n_groups >= (1ull << 31)) return ZHIP_E_UNSUPPORTED;
+        g_last_kernel = "k_decode_tileg";
         hipLaunchKernelGGL(fn, dim3(p.n_chunks * p.n_groups), dim3(kThreads), 0, stream, p);
         return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
     }
@@ -605,6 +639,7 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
                 max_grid = (max_grid / 8) * per_cu;
         }
         const uint32_t grid = p.n_units < (uint32_t)max_grid ? p.n_units : (uint32_t)max_grid;
+        g_last_kernel = "k_decode_tile";
         hipLaunchKernelGGL(fn, dim3(grid), dim3(kThreads), 0, stream, p);
         return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
     }
@@ -621,8 +656,11 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
             max_grid = (max_grid / 8) * per_cu;  // max_grid arrives as CUs * 8
     }
     const uint32_t grid = p.n_units < (uint32_t)max_grid ? p.n_units : (uint32_t)max_grid;
+    g_last_kernel = "k_decode";
     hipLaunchKernelGGL(fn, dim3(grid), dim3(kThreads), 0, stream, p);
     return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
 }
 
 }  // namespace zhip
+
+extern "C" const char* zhip_last_kernel(void) { return zhip::g_last_kernel; }

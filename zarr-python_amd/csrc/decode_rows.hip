@@ -58,8 +58,8 @@ __device__ __forceinline__ uint4 load_stream16_any(const uint8_t* a) {  // any a
 // phase timestamps (diagnostics, kTuneStamp): [wg][slot]
 __device__ uint64_t g_stamps[kStampWG * kStampSlots];
 
-__device__ __forceinline__ void stamp(const DecodeParams& p, uint32_t g, int t, int slot) {
-    if ((p.tune & kTuneStamp) && t == 0 && g < kStampWG) {
+__device__ __forceinline__ void stamp(uint32_t tune, uint32_t g, int t, int slot) {
+    if ((tune & kTuneStamp) && t == 0 && g < kStampWG) {
         uint64_t v = __builtin_amdgcn_s_memrealtime();
         if (slot == 0) {  // slot 0 also carries the hardware id (XCC / SE / CU) in the top bits
             uint32_t hw;
@@ -71,6 +71,8 @@ __device__ __forceinline__ void stamp(const DecodeParams& p, uint32_t g, int t, 
         g_stamps[g * kStampSlots + slot] = v;
     }
 }
+
+__device__ __forceinline__ void stamp(const DecodeParams& p, uint32_t g, int t, int slot) { stamp(p.tune, g, t, slot); }
 
 // zeros: blocks outside the chunk and units that are not present read here
 __device__ uint4 g_rows_zero[kThreads];
@@ -99,6 +101,38 @@ __device__ __forceinline__ Unit predict_unit(const DecodeParams& p, uint32_t u) 
     const uint64_t off = p.pred_base + (uint64_t)grp * p.pred_outer + (uint64_t)(U.c - grp * p.pred_per) * p.pred_inner;
     U.cp = p.src + off;
     U.seg_lo = (int32_t)p.E - (int32_t)((U.sidx + 1u) * p.seg);
+    U.sel = 0;
+    U.out_off = 0;
+    return U;
+}
+
+// The kernel arguments k_decode_pair needs before its first loads (PairHot),
+// forced into SGPRs at one point: every s_load of the batch is issued before
+// a single wait, instead of one dependent round trip per branch that first
+// uses a field.
+__device__ __forceinline__ void pair_hot(PairHot& h) {
+    asm volatile("" : "+s"(h.n_units), "+s"(h.nseg), "+s"(h.n_idx), "+s"(h.xcd_run), "+s"(h.d_nseg.m),
+                 "+s"(h.d_nseg.s), "+s"(h.d_xcd.m), "+s"(h.d_xcd.s), "+s"(h.d_per.m), "+s"(h.d_per.s), "+s"(h.pred),
+                 "+s"(h.pred_per), "+s"(h.E), "+s"(h.seg), "+s"(h.tune));
+    asm volatile("" : "+s"(h.pred_base), "+s"(h.pred_outer), "+s"(h.pred_inner), "+s"(h.src), "+s"(h.pair_tab),
+                 "+s"(h.kpair11), "+s"(h.kthread11));
+}
+
+// k_decode_il's part of the batch (with pair_hot)
+__device__ __forceinline__ void il_hot(PairHot& h) {
+    asm volatile("" : "+s"(h.il_S), "+s"(h.n_chunks), "+s"(h.il_tab), "+s"(h.il_klane), "+s"(h.il_kidx));
+}
+
+// predict_unit from the PairHot batch (magic divisions, no kernarg reloads)
+__device__ __forceinline__ Unit predict_unit_h(const PairHot& h, uint32_t u) {
+    Unit U;
+    U.c = fdiv_apply(u, h.d_nseg.m, h.d_nseg.s);
+    U.sidx = u - U.c * h.nseg;
+    U.mode = ZHIP_ST_OK;
+    const uint32_t grp = fdiv_apply(U.c, h.d_per.m, h.d_per.s);
+    const uint64_t off = h.pred_base + (uint64_t)grp * h.pred_outer + (uint64_t)(U.c - grp * h.pred_per) * h.pred_inner;
+    U.cp = reinterpret_cast<const uint8_t*>(h.src) + off;
+    U.seg_lo = (int32_t)h.E - (int32_t)((U.sidx + 1u) * h.seg);
     U.sel = 0;
     U.out_off = 0;
     return U;
@@ -663,6 +697,24 @@ __device__ __forceinline__ void store_a_load_b(const DecodeParams& p, const Unit
     }
 }
 
+// Shard-index check by a leading workgroup of a decode whose inner chunks carry
+// no CRC (zarr's default sharding codecs: inner bytes only, index
+// bytes + crc32c, sharding.py:423-427): the pair tables go into LDS for this
+// workgroup alone, then verify_index_pair's chain.
+__device__ __forceinline__ void index_lead(const DecodeParams& p, uint32_t j, int t, uint32_t* s_tab,
+                                           uint32_t* red) {
+    const uint4* gt = reinterpret_cast<const uint4*>(p.pair_tab);
+    uint4 v[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) v[i] = gt[t + i * kThreads];
+    const uint32_t kth = load_u32_any(reinterpret_cast<const uint8_t*>(p.kthread11 + t));
+    uint4* st = reinterpret_cast<uint4*>(s_tab);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) st[t + i * kThreads] = v[i];
+    __syncthreads();
+    verify_index_pair(p, j, t, kth, s_tab, red, false, make_uint4(0, 0, 0, 0));
+}
+
 // VARIANT (tuning arm, headline item type only): 0 production, 3 no CRC
 // lookups (a plain xor; results invalid), 6 s_setprio(1) once every load of
 // the wave is issued, 7 unit B's loads interleaved with unit A's stores, 8
@@ -834,6 +886,82 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(NU == 
     stamp(p, g, t, 7);
 }
 
+// ---------------------------------------------------------------------------
+// k_decode_lead: k_decode_pair for chains whose inner chunks carry no CRC but
+// whose shard indexes do (zarr's default sharding codecs: inner bytes only,
+// index bytes + crc32c, sharding.py:423-427).  The first round_up(n_idx, 8)
+// workgroups each verify one shard index (index_lead: pair tables in LDS) and
+// return; the rest decode two units each with no tables at all -- one launch
+// instead of an index launch ahead of the data.  With nothing to compute but
+// addresses, the prologue is lean: the PairHot batch (one scalar round trip),
+// magic divisions, and the unit loads at the addresses the default shard
+// packing predicts (zhip_predict) before the header chain resolves; a wrong
+// guess reloads.  (The same prologue measured slower in the CRC kernels, whose
+// 24 KiB table loads then queue behind every workgroup's data loads:
+// profiles/r03/lean/.)
+template <int ITEM, bool SWAP, int K = kDefaultBlocks>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_decode_lead(const DecodeParams p) {
+    __shared__ uint32_t s_tab[kPairTabWords];
+    __shared__ uint32_t s_red[kThreads / 64];
+    const int t = threadIdx.x;
+    PairHot h = p.h;
+    pair_hot(h);
+    uint32_t bx = blockIdx.x;
+    // a multiple of 8 leading workgroups keeps bx % 8 the dispatch XCD
+    const uint32_t lead = (h.n_idx + 7u) & ~7u;
+    if (bx < lead) {
+        if (bx < h.n_idx) index_lead(p, bx, t, s_tab, s_red);
+        return;
+    }
+    bx -= lead;
+    uint32_t g = bx;
+    {
+        const uint32_t x = bx & 7u, slot = bx >> 3;
+        const uint32_t r = fdiv_apply(slot, h.d_xcd.m, h.d_xcd.s);
+        const uint32_t gx = (r * 8u + x) * h.xcd_run + (slot - r * h.xcd_run);
+        g = h.xcd_run ? gx : bx;
+    }
+    const uint32_t q0 = 2u * g;
+    const bool has_a = q0 < h.n_units, has_b = q0 + 1u < h.n_units;
+    if (!has_a) return;
+    auto unit_of = [&](uint32_t q) {
+        const uint32_t c = fdiv_apply(q, h.d_nseg.m, h.d_nseg.s);
+        return c * h.nseg + (h.nseg - 1u - (q - c * h.nseg));
+    };
+    const uint32_t u_a = unit_of(q0), u_b = has_b ? unit_of(q0 + 1u) : u_a;
+    const uint32_t expected = p.g.nbytes;
+    uint4 A[K], B[K];
+    Unit ua, ub;
+    if (h.pred) {
+        const Unit ga = predict_unit_h(h, u_a), gb = predict_unit_h(h, u_b);
+        load_unit_rows(ga, true, t, A);
+        load_unit_rows(gb, has_b, t, B);
+        ua = resolve_unit(p, u_a, expected);
+        ub = has_b ? advance_unit(p, ua, u_b, expected) : ua;
+        const bool bad_a = ua.mode == ZHIP_ST_OK && ua.cp != ga.cp;
+        const bool bad_b = has_b && ub.mode == ZHIP_ST_OK && ub.cp != gb.cp;
+        if (bad_a || bad_b) {  // a wrong guess reloads from the live index; the full drain keeps later waits exact
+            if (bad_a) load_unit_rows(ua, true, t, A);
+            if (bad_b) load_unit_rows(ub, true, t, B);
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+        }
+    } else {
+        ua = resolve_unit(p, u_a, expected);
+        ub = has_b ? advance_unit(p, ua, u_b, expected) : ua;
+        load_unit_rows(ua, true, t, A);
+        load_unit_rows(ub, has_b, t, B);
+    }
+    const RowSteps ma = load_row_steps(p, ua), mb = load_row_steps(p, ub);
+    uint8_t* sink = reinterpret_cast<uint8_t*>(g_rows_sink);
+    const uint32_t lane_row = (16u * (uint32_t)t) >> p.row_shift;
+    const uint32_t lane_col = (16u * (uint32_t)t) & ((1u << p.row_shift) - 1u);
+    const int64_t lane_off = (int64_t)lane_row * p.r_oy + (int64_t)lane_col;
+    store_unit_rows<ITEM, SWAP, K>(p, ua, ma, true, lane_row, lane_off, sink, A);
+    store_unit_rows<ITEM, SWAP, K>(p, ub, mb, has_b, lane_row, lane_off, sink, B);
+    unit_status_pair(p, ua, false, t);
+    if (has_b) unit_status_pair(p, ub, false, t);
+}
+
 int debug_stamps(uint64_t* host_out, uint32_t n_wg) {
     if (n_wg > kStampWG) n_wg = kStampWG;
     return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_stamps), (size_t)n_wg * kStampSlots * sizeof(uint64_t), 0,
@@ -857,6 +985,16 @@ KernelFn select_pair_nu(bool crc, int item, bool swap) {
 }
 
 KernelFn select_pair_kernel(bool crc, int item, bool swap, int nu) {
+    if (nu == 9) {  // no data CRC, leading index-check workgroups (k_decode_lead)
+        if (crc) return nullptr;
+        switch (item) {
+            case 1: return k_decode_lead<1, false>;
+            case 2: return swap ? k_decode_lead<2, true> : k_decode_lead<2, false>;
+            case 4: return swap ? k_decode_lead<4, true> : k_decode_lead<4, false>;
+            case 8: return swap ? k_decode_lead<8, true> : k_decode_lead<8, false>;
+            default: return nullptr;
+        }
+    }
     if (nu == 5)  // tuning arm (headline item type only): VARIANT 3, no lookups
         return !(crc && item == 4 && !swap) ? nullptr : k_decode_pair<true, 4, false, 2, 8, 3>;
     if (nu >= 6 && nu <= 8) {  // tuning arms (headline item type only): VARIANT 6 / 7 / 8
@@ -1009,7 +1147,14 @@ __device__ __forceinline__ void publish_il(const DecodeParams& p, uint32_t c, ui
     }
 }
 
-template <bool CRC, int ITEM, bool SWAP>
+// LEAN (tuning arm kTuneIlLean): the PairHot batch, then tables, constants
+// and -- at the addresses the default shard packing predicts (zhip_predict) --
+// the data loads, all before the header chain (chunk record -> index entry)
+// resolves; a wrong prediction reloads.  Measured 1.5 us SLOWER on the
+// headline than the production order (data loads after the resolved header:
+// the tables, L2 hits, are in LDS before the data flood;
+// profiles/r03/lean/).
+template <bool CRC, int ITEM, bool SWAP, bool LEAN = false>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_decode_il(const DecodeParams p) {
     constexpr int K = kDefaultBlocks;
     __shared__ uint32_t s_tab[CRC ? kPairTabWords : 1];
@@ -1017,17 +1162,88 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))
     __shared__ uint32_t s_red[2][kThreads / 64];
     const int t = threadIdx.x;
     const uint32_t G = gridDim.x, g = blockIdx.x;
-    const uint32_t wpc = p.nseg, S = p.il_S;  // workgroups per chunk = its 32 KiB units
-    const uint32_t c = g / wpc, r = g - c * wpc;
-    const bool has = c < p.n_chunks;
-    if (!has && g >= p.n_idx) return;
     const uint32_t expected = p.g.nbytes + (CRC ? 4u : 0u);
     const uint8_t* zero = reinterpret_cast<const uint8_t*>(g_rows_zero);
+    uint32_t c, r, st0;
+    bool has, ok;
+    Unit U;
+    int32_t lo_frame;
+    uint4 ipre = make_uint4(0, 0, 0, 0);
+    uint4 tv0, tv1, tv2, tv3, tv4, tv5;
+    uint32_t kl = 0, kix = 0;
+    uint4 A[K];
+    if constexpr (LEAN) {
+        PairHot h = p.h;
+        pair_hot(h);
+        il_hot(h);
+        const uint32_t wpc = h.nseg, S = h.il_S;  // S in {2, 4, 8}
+        const uint32_t ls = (uint32_t)__builtin_ctz(S);
+        c = fdiv_apply(g, h.d_nseg.m, h.d_nseg.s);
+        r = g - c * wpc;
+        has = c < h.n_chunks;
+        if (!has && g >= h.n_idx) return;
+        if constexpr (CRC) {
+            const uint4* gt = reinterpret_cast<const uint4*>(h.il_tab);
+            tv0 = gt[t];
+            tv1 = gt[t + kThreads];
+            tv2 = gt[t + 2 * kThreads];
+            tv3 = gt[t + 3 * kThreads];
+            tv4 = gt[t + 4 * kThreads];
+            tv5 = gt[t + 5 * kThreads];
+            kl = load_u32_any(reinterpret_cast<const uint8_t*>(reinterpret_cast<const uint32_t*>(h.il_klane) +
+                                                               (size_t)(has ? r : 0u) * kThreads + t));
+            kix = load_u32_any(reinterpret_cast<const uint8_t*>(reinterpret_cast<const uint32_t*>(h.il_kidx) + t));
+        }
+        st0 = ((r >> ls) << ls) * (uint32_t)K + (r & (S - 1u));
+        lo_frame = (int32_t)h.E - (int32_t)(h.nseg * h.seg);
+        if (h.pred) {
+            const uint32_t grp = fdiv_apply(c, h.d_per.m, h.d_per.s);
+            const uint8_t* cpp = reinterpret_cast<const uint8_t*>(h.src) + h.pred_base + (uint64_t)grp * h.pred_outer +
+                                 (uint64_t)(c - grp * h.pred_per) * h.pred_inner;
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int32_t base = lo_frame + kWgStride * (int32_t)(st0 + S * (uint32_t)k);
+                A[k] = load_stream16_any(has && base >= 0 ? cpp + base + 16 * t : zero);
+            }
+            if (has) U = resolve_unit(p, c * h.nseg, expected);
+            ok = has && U.mode == ZHIP_ST_OK;
+            if (ok && U.cp != cpp) {  // a wrong guess: reload from the live index, full drain
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    const int32_t base = lo_frame + kWgStride * (int32_t)(st0 + S * (uint32_t)k);
+                    A[k] = load_stream16_any(base >= 0 ? U.cp + base + 16 * t : zero);
+                }
+                __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+            }
+            if constexpr (CRC) ipre = index_prefetch(p, g, g < h.n_idx, t, zero);
+        } else {
+            if (has) U = resolve_unit(p, c * h.nseg, expected);
+            ok = has && U.mode == ZHIP_ST_OK;
+            if constexpr (CRC) ipre = index_prefetch(p, g, g < h.n_idx, t, zero);
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int32_t base = lo_frame + kWgStride * (int32_t)(st0 + S * (uint32_t)k);
+                A[k] = load_stream16_any(ok && base >= 0 ? U.cp + base + 16 * t : zero);
+            }
+        }
+        if (!has) {
+            U.c = 0;
+            U.sidx = 0;
+            U.mode = ZHIP_ST_MISSING;
+            U.cp = zero;
+            U.seg_lo = 0;
+            U.sel = 0;
+            U.out_off = 0;
+        }
+    } else {
+    const uint32_t wpc = p.nseg, S = p.il_S;  // workgroups per chunk = its 32 KiB units
+    c = g / wpc;
+    r = g - c * wpc;
+    has = c < p.n_chunks;
+    if (!has && g >= p.n_idx) return;
     // 1. vector loads in a path-independent order and count: [CRC: tables (6),
     //    the lane constant, the index lane constant, the first index block],
     //    the K data blocks; headers, row-map entries and the trailer are scalar
-    uint4 tv0, tv1, tv2, tv3, tv4, tv5;
-    uint32_t kl = 0, kix = 0;
     if constexpr (CRC) {
         const uint4* gt = reinterpret_cast<const uint4*>(p.il_tab);
         tv0 = gt[t];
@@ -1039,7 +1255,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))
         kl = load_u32_any(reinterpret_cast<const uint8_t*>(p.il_klane + (size_t)(has ? r : 0u) * kThreads + t));
         kix = load_u32_any(reinterpret_cast<const uint8_t*>(p.il_kidx + t));
     }
-    Unit U;
     if (has) U = resolve_unit(p, c * p.nseg, expected);
     else {
         U.c = 0;
@@ -1050,17 +1265,17 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))
         U.sel = 0;
         U.out_off = 0;
     }
-    const bool ok = has && U.mode == ZHIP_ST_OK;
-    const uint32_t st0 = (r / S) * S * (uint32_t)K + (r % S);
-    const int32_t lo_frame = (int32_t)p.E - (int32_t)(p.nseg * p.seg);
-    uint4 ipre = make_uint4(0, 0, 0, 0);
+    ok = has && U.mode == ZHIP_ST_OK;
+    st0 = (r / S) * S * (uint32_t)K + (r % S);
+    lo_frame = (int32_t)p.E - (int32_t)(p.nseg * p.seg);
     if constexpr (CRC) ipre = index_prefetch(p, g, g < p.n_idx, t, zero);
-    uint4 A[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-        const int32_t base = lo_frame + kWgStride * (int32_t)(st0 + S * (uint32_t)k);
+        const int32_t base = lo_frame + kWgStride * (int32_t)(st0 + p.il_S * (uint32_t)k);
         A[k] = load_stream16_any(ok && base >= 0 ? U.cp + base + 16 * t : zero);
     }
+    }
+    const uint32_t S = p.il_S, wpc = p.nseg;
     // destinations of the K steps (scalar loads, consumed at the stores)
     zhip_rowblk m[K];
 #pragma unroll
@@ -1117,6 +1332,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))
     //    this kernel only then), the first block prefetched with the data
     if constexpr (CRC)
         for (uint32_t j = g; j < p.n_idx; j += G) verify_index_pair(p, j, t, kix, s_tab, s_red[1], j == g, ipre);
+}
+
+KernelFn select_il_kernel_lean(bool crc, int item, bool swap) {  // kTuneIlLean (4-byte LE CRC item type only)
+    return (crc && item == 4 && !swap) ? k_decode_il<true, 4, false, true> : nullptr;
 }
 
 KernelFn select_il_kernel(bool crc, int item, bool swap) {

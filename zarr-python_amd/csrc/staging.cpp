@@ -7,6 +7,7 @@
 // transfer and the caller's planning all overlap, with no per-window work in
 // Python.  A parallel host memcpy serves the way back (pinned result -> a
 // caller's host array).
+#include <emmintrin.h>
 #include <fcntl.h>
 #include <hip/hip_runtime.h>
 #include <unistd.h>
@@ -84,6 +85,38 @@ class Pool {
 Pool& pool() {
     static Pool* p = new Pool();  // never destroyed: detached workers outlive static teardown
     return *p;
+}
+
+// Host copies into page-locked windows (and back out of them): 1 = streaming
+// (non-temporal) 16-byte stores, which skip the read-for-ownership of every
+// destination line that a cached store pays -- the packed bytes are read next
+// by the DMA engine, not by this core; 0 = memcpy.  zhip_set_tuning(
+// ZHIP_TUNE_STAGE_COPY, v) selects (measurement arms).
+static uint32_t g_copy_nt = 1;
+
+static void copy_bytes(uint8_t* dst, const uint8_t* src, uint64_t n) {
+    if (!g_copy_nt || n < 4096) {
+        std::memcpy(dst, src, n);
+        return;
+    }
+    const uint64_t head = (16u - (reinterpret_cast<uintptr_t>(dst) & 15u)) & 15u;
+    std::memcpy(dst, src, head);
+    dst += head;
+    src += head;
+    n -= head;
+    const uint64_t nb = n / 64u;
+    for (uint64_t i = 0; i < nb; ++i, dst += 64, src += 64) {
+        const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src));
+        const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + 16));
+        const __m128i c = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + 32));
+        const __m128i d = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + 48));
+        _mm_stream_si128(reinterpret_cast<__m128i*>(dst), a);
+        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + 16), b);
+        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + 32), c);
+        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + 48), d);
+    }
+    std::memcpy(dst, src, n - nb * 64u);
+    _mm_sfence();  // the streamed lines are visible (to the DMA engine) before the copy is enqueued
 }
 
 // Page-locked pieces: straight DMA, merged while both the host and the
@@ -220,7 +253,7 @@ static int pack_windows(const zhip_piece* pieces, uint32_t n_pieces, uint8_t* pi
                                          pinned + s, e - s))
                         rc.store(ZHIP_E_IO);
                 } else {
-                    std::memcpy(pinned + s, reinterpret_cast<const uint8_t*>(pc.host) + (s - pc.dst_off), e - s);
+                    copy_bytes(pinned + s, reinterpret_cast<const uint8_t*>(pc.host) + (s - pc.dst_off), e - s);
                 }
                 if (run_e > run_s && s - run_e >= 256) flush();  // a real gap: leave it alone
                 if (run_e == run_s) run_s = s;
@@ -370,6 +403,7 @@ int zhip_stage_end(zhip_stage_job* j, void* wait_stream) {
 }
 
 void zhip_stage_set_streams(uint32_t n) { g_stage_streams = n; }
+void zhip_stage_set_copy(uint32_t nt) { g_copy_nt = nt ? 1u : 0u; }
 
 int zhip_host_pinned(const void* p) {
     if (!p) return 0;
@@ -413,7 +447,7 @@ int zhip_host_copy(void* dst, const void* src, uint64_t nbytes, uint32_t nthread
             const uint64_t i = next.fetch_add(1);
             if (i >= n) return;
             const uint64_t a = i * piece, b = a + piece < nbytes ? a + piece : nbytes;
-            std::memcpy(static_cast<uint8_t*>(dst) + a, static_cast<const uint8_t*>(src) + a, b - a);
+            copy_bytes(static_cast<uint8_t*>(dst) + a, static_cast<const uint8_t*>(src) + a, b - a);
         }
     };
     const uint32_t nt = nthreads == 0 ? 1u : (nthreads > 64 ? 64u : nthreads);

@@ -46,7 +46,25 @@ struct GroupEnt {
 constexpr int kPairT1 = 0, kPairT2 = 2048, kPairT3 = 4096, kPairA4 = 5120;
 constexpr int kPairTabWords = 6144;
 
+// What k_decode_lead (and the k_decode_il arm) need before their first vector loads,
+// FIRST in the kernel arguments and read as one scalar batch (pair_hot): the
+// lazily scheduled kernarg loads of the full struct put five to seven
+// dependent round trips (and software divisions) between the kernel start and
+// the first data load.  Divisors are host-built magic numbers (zhip_fdiv).
+struct PairHot {
+    uint32_t n_units, nseg, n_idx, xcd_run;
+    zhip_fdiv d_nseg, d_xcd, d_per;
+    uint32_t pred, pred_per, E, seg;
+    uint32_t tune, pad;
+    uint64_t pred_base, pred_outer, pred_inner;
+    uint64_t src, pair_tab, kpair11, kthread11;
+    // k_decode_il
+    uint32_t il_S, n_chunks;
+    uint64_t il_tab, il_klane, il_kidx;
+};
+
 struct DecodeParams {
+    PairHot h;
     const uint8_t* src;
     uint64_t src_size;
     uint8_t* out;
@@ -126,6 +144,47 @@ struct DecodeParams {
     uint64_t pred_base, pred_outer, pred_inner;
 };
 
+// n / d == (n * m) >> s for 0 <= n < 2^31 (host side; fdiv_apply on the device)
+inline zhip_fdiv make_fdiv(uint32_t d) {
+    zhip_fdiv f;
+    uint32_t l = 0;
+    while ((1ull << l) < d) ++l;
+    f.s = 31 + l;
+    f.m = (uint32_t)(((1ull << (31 + l)) + d - 1) / d);  // ceil(2^(31+l) / d) < 2^32 for d >= 1
+    return f;
+}
+
+// PairHot from the full parameters (after every field is final); xcd_run and
+// its divisor are set again by launch_decode
+inline void fill_pair_hot(DecodeParams& p) {
+    PairHot& h = p.h;
+    h.n_units = p.n_units;
+    h.nseg = p.nseg;
+    h.n_idx = p.n_idx;
+    h.xcd_run = p.xcd_run;
+    h.d_nseg = make_fdiv(p.nseg ? p.nseg : 1u);
+    h.d_xcd = make_fdiv(p.xcd_run ? p.xcd_run : 1u);
+    h.d_per = make_fdiv(p.pred_per ? p.pred_per : 1u);
+    h.pred = p.pred;
+    h.pred_per = p.pred_per;
+    h.E = p.E;
+    h.seg = p.seg;
+    h.tune = p.tune;
+    h.pad = 0;
+    h.pred_base = p.pred_base;
+    h.pred_outer = p.pred_outer;
+    h.pred_inner = p.pred_inner;
+    h.src = reinterpret_cast<uint64_t>(p.src);
+    h.pair_tab = reinterpret_cast<uint64_t>(p.pair_tab);
+    h.kpair11 = reinterpret_cast<uint64_t>(p.kpair11);
+    h.kthread11 = reinterpret_cast<uint64_t>(p.kthread11);
+    h.il_S = p.il_S;
+    h.n_chunks = p.n_chunks;
+    h.il_tab = reinterpret_cast<uint64_t>(p.il_tab);
+    h.il_klane = reinterpret_cast<uint64_t>(p.il_klane);
+    h.il_kidx = reinterpret_cast<uint64_t>(p.il_kidx);
+}
+
 constexpr int kTileRows = 64;    // rows of the contiguous-in-out dim per tile
 constexpr int kTileCols = 256;   // bytes of the innermost stored row per tile
 
@@ -156,12 +215,14 @@ constexpr uint32_t kTuneNoIl = 134217728u;    // whole-row layouts: never k_deco
 constexpr uint32_t kTuneXw = 268435456u;      // whole-row layouts: k_decode_xw where admitted
 constexpr uint32_t kTuneNoXw = 536870912u;    // whole-row layouts: never k_decode_xw
 constexpr uint32_t kTuneNoPub = 1073741824u;  // timing arm: k_decode_il / k_decode_xw skip the CRC publication
+constexpr uint32_t kTuneIlLean = 16384u;    // k_decode_il arm: lean predicted prologue (data loads before the header chain)
 constexpr uint32_t kTuneStamp = 1024u;    // k_decode_pair: per-workgroup phase timestamps (zhip_debug_stamps)
 constexpr uint32_t kStampWG = 8192u;      // workgroups stamped per launch
 constexpr uint32_t kStampSlots = 8u;
 extern int g_tune_max_grid;
 }  // namespace zhip
 extern "C" void zhip_stage_set_streams(uint32_t n);  // staging.cpp (ZHIP_TUNE_STAGE_STREAMS)
+extern "C" void zhip_stage_set_copy(uint32_t nt);     // staging.cpp (ZHIP_TUNE_STAGE_COPY)
 namespace zhip {
 extern int g_tune_blocks;
 extern uint32_t g_tune_bits;

@@ -202,6 +202,8 @@ def lib():
     L.zhip_shard_pack.restype = ctypes.c_int
     L.zhip_set_tuning.argtypes = [ctypes.c_int, ctypes.c_int]
     L.zhip_set_tuning.restype = ctypes.c_int
+    L.zhip_last_kernel.argtypes = []
+    L.zhip_last_kernel.restype = ctypes.c_char_p
     L.zhip_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
     L.zhip_debug_stamps.restype = ctypes.c_int
     L.zhip_selftest.restype = ctypes.c_int

@@ -371,7 +371,9 @@ class ReadGraph:
 
     def replay(self) -> None:
         for p in self.programs:  # the graph holds the programs' planned offsets
-            p.check_fresh()
+            chk = getattr(p, "check_fresh", None)  # (any object with launch / results replays)
+            if chk is not None:
+                chk()
         self.graph.replay()
 
     def results(self) -> list:
@@ -533,6 +535,15 @@ class HipCodecPipeline:
                 aux["split"] = (outer, inner, read_pipe, self._sub(wfixed))
         return aux["split"]
 
+    def _nested(self):
+        """The outer ShardingCodec of a nested-sharding chain, else None."""
+        aux = self._aux
+        if "nested" not in aux:
+            from . import nested
+
+            aux["nested"] = nested.nested_split(self)
+        return aux["nested"]
+
     def _sub(self, codecs) -> "HipCodecPipeline":
         aa, ab, bb = split_codecs(codecs)
         return type(self)(tuple(codecs), aa, ab, bb, self.batch_size, self.predict_loads)
@@ -652,6 +663,12 @@ class HipCodecPipeline:
             raise ValueError("empty batch")
         if not isinstance(out, torch.Tensor) or not out.is_cuda:
             raise TypeError("HipCodecPipeline.read needs a device-resident out (torch CUDA tensor)")
+        ns = self._nested()
+        if ns is not None:  # the inner pipeline's program over the touched inner shards
+            from . import nested
+
+            inner, items, _, _ = nested.read_batch(self, ns, batch)
+            return inner.prepare_read(items, out, drop_axes, item_out_extra)
         hs = self._host_split()
         if hs is not None and hs[0]:
             return hs[2].prepare_read(self._host_read_batch(batch, hs[0]), out, drop_axes, item_out_extra)
@@ -691,8 +708,19 @@ class HipCodecPipeline:
                 # the non-tiled kernel); else a second NO_WRITE launch
                 fuse = (t.index_layout is not None and resolved is None and chain.inner.crc
                         and not t.tile)
+                # inner chunks without a CRC (zarr's default sharding codecs):
+                # leading index-check workgroups of the mapped pair decode
+                # (k_decode_lead), whole-row layouts of <= 1 MiB chunks
+                lead = (t.index_layout is not None and resolved is None and not chain.inner.crc
+                        and not t.tile and t.fast and t.rows
+                        and get_plan(t.layout).units_per_chunk <= 32)
                 data = DecodeLaunch(t.layout, t.chunks, t.sels, src, size, out, t.fast, device, t.tile,
-                                    t.index_chunks if fuse else None, t.rows, t.predict)
+                                    t.index_chunks if (fuse or lead) else None, t.rows, t.predict)
+                if lead and data.d_rowmap is None:  # the library declined the row map
+                    data = DecodeLaunch(t.layout, t.chunks, t.sels, src, size, out, t.fast, device, t.tile,
+                                        None, t.rows, t.predict)
+                    lead = False
+                fuse = fuse or lead
                 index = None
                 if t.index_layout is not None and not fuse:
                     index = DecodeLaunch(t.index_layout, t.index_chunks, np.zeros(1, SEL_DT), src, size,
@@ -717,6 +745,11 @@ class HipCodecPipeline:
         batch = normalize_batch(batch_info)
         if not batch:
             return ()
+        ns = self._nested()
+        if ns is not None:  # nested sharding: outer level routed on the host (nested.py)
+            from . import nested
+
+            return nested.read_sync(self, ns, batch, out, drop_axes)
         hs = self._host_split()
         if hs is not None and hs[0]:  # the outer host stage first, then the GPU chain
             return hs[2].read_sync(self._host_read_batch(batch, hs[0]), out, drop_axes)
@@ -905,6 +938,11 @@ class HipCodecPipeline:
         if not batch:
             return
         value = _resolve_value(value)
+        ns = self._nested()
+        if ns is not None:  # nested sharding: outer level assembled on the host (nested.py)
+            from . import nested
+
+            return nested.write_sync(self, ns, batch, value, drop_axes)
         hs = self._host_split()
         if hs is not None and (hs[0] or not self.array_array_codecs):
             return self._host_write(batch, value, drop_axes, partial_encode, hs)

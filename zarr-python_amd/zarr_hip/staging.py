@@ -22,6 +22,7 @@ launch), so errors surface with the reference's message.
 
 from __future__ import annotations
 
+import ctypes
 import os
 
 import numpy as np
@@ -170,11 +171,14 @@ def stage(layout: StagingLayout, device, post=(), defer: bool = False):
     from . import _native as N
 
     total = max(layout.top, 16)
-    # file pieces carry an encoded path (kept alive with the job) and an offset
-    views = [np.frombuffer(buf.path.encode() + b"\0", np.uint8) if isinstance(buf, FileRef) else _host_view(buf)
-             for buf, _, _ in layout.pieces]
+    # file pieces carry an encoded path (kept alive with the job) and an offset;
+    # bytes objects are addressed in place (ctypes.cast: a third of the cost
+    # of a numpy view's .ctypes per piece, which adds up over a batch)
+    views = [np.frombuffer(buf.path.encode() + b"\0", np.uint8) if isinstance(buf, FileRef)
+             else buf if type(buf) is bytes else _host_view(buf) for buf, _, _ in layout.pieces]
     pieces = np.zeros(len(views), N.PIECE_DT)
-    addrs = [v.ctypes.data for v in views]
+    _cast, _vp = ctypes.cast, ctypes.c_void_p
+    addrs = [_cast(v, _vp).value if type(v) is bytes else v.ctypes.data for v in views]
     pieces["host"] = addrs
     pieces["nbytes"] = [n for _, _, n in layout.pieces]
     pieces["dst_off"] = [off for _, off, _ in layout.pieces]
