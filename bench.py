@@ -228,11 +228,21 @@ def time_programs(progs, steps, warmup, device, ctx=None):
     return wall_max / steps, min(float(np.median(kern)), span / steps)
 
 
+def _last_kernel() -> str:
+    from zarr_hip import _native as N
+
+    return N.lib().zhip_last_kernel().decode()
+
+
 def _entry(dec, alg, wall, kern, **kw):
+    """One extra's line; decode legs are labelled with the kernel the library
+    launched last (zhip_last_kernel: the timed program's data launch)."""
     d = {"decoded_GiBps": round(dec / wall / GIB, 1), "step_ms": round(wall * 1e3, 4),
          "kernel_ms": round(kern * 1e3, 4), "algorithmic_bytes": int(alg),
          "hbm_frac": round(alg / kern / 1e9 / HBM_PEAK_GBS, 4)}
     d.update(kw)
+    if "kernel" not in d:
+        d["kernel"] = _last_kernel()
     return d
 
 
@@ -248,6 +258,12 @@ def extra_configs(ctx, args):
     out = {}
     steps = max(10, args.steps // 2)
     single = ctx.world == 1
+    # the host-memory legs first: after the 4-16 GiB legs below the same reads
+    # measured up to 2x slower in one process (caching-allocator and host
+    # memory state), so they run while the process is fresh
+    if single and "e2e" in args.extra:
+        out["e2e_c2_host"] = e2e_host(ctx.device, args)
+        torch.cuda.empty_cache()
     if single and "c1" in args.extra:
         out["c1_1d_bytes"] = c1_plumbing(device, args)
         torch.cuda.empty_cache()
@@ -283,8 +299,8 @@ def extra_configs(ctx, args):
         wall, kern = time_programs([p for p, _ in progs], steps, 3, device)
         out["sharded_default_chain_256"] = _entry(
             dec, dec + 64 * 1048576 + 8 * (8 * 16 + 4), wall, kern, checked="bytes",
-            kernel="k_decode_lead (index checks in 8 leading workgroups)" if fused
-            else "separate index launch + k_decode_pair<noCRC>",
+            kernel=_last_kernel() + (" (index checks in 8 leading workgroups)" if fused
+                                     else " (after a separate index launch)"),
             note="headline array and shards, zarr's default sharding codecs: inner bytes only, index bytes+crc32c")
         del progs, data
     if single and "c3" in args.extra:
@@ -304,9 +320,8 @@ def extra_configs(ctx, args):
             not (args.tune & 65536)
         wall, kern = time_programs([p for p, _ in progs], steps, 3, device)
         dec = data.numel() * 4
-        out["c3_transpose_210"] = _entry(dec, dec + 64 * (1048576 + 4), wall, kern,
-                                         kernel="k_decode_tile4" if tile4 else "k_decode_tile",
-                                         checked="bytes")
+        out["c3_transpose_210"] = _entry(dec, dec + 64 * (1048576 + 4), wall, kern, checked="bytes",
+                                         tile4_eligible=tile4)
         del progs
         # the same array in 128^3 chunks: k_decode_tile4 declines (512 tiles per
         # chunk, two different steps between consecutive tiles) -> k_decode_tileg
@@ -323,7 +338,7 @@ def extra_configs(ctx, args):
         wall, kern = time_programs([p for p, _ in progs], steps, 3, device)
         out["c3_transpose_210_chunks128"] = _entry(
             dec, dec + 8 * (128 ** 3 * 4 + 4), wall, kern, checked="bytes",
-            kernel="k_decode_tile" if (args.tune & 65536) or not (kf & N.PK_TILEG) else "k_decode_tileg",
+            tileg_eligible=bool(kf & N.PK_TILEG),
             note="8 chunks of 128^3: no k_decode_tile4 (round 1: persistent k_decode_tile)")
         del progs, data
     if "c4" in args.extra:
@@ -341,9 +356,6 @@ def extra_configs(ctx, args):
         out["encode_c3"] = encode_c3(device, args)
         torch.cuda.empty_cache()
         out["encode_c3_chunks128"] = encode_c3_general(device, args)
-        torch.cuda.empty_cache()
-    if single and "e2e" in args.extra:
-        out["e2e_c2_host"] = e2e_host(device, args)
         torch.cuda.empty_cache()
     if single and "call" in args.extra:
         out["device_read_call"] = device_read_call(device, args)
@@ -717,7 +729,7 @@ def c1_plumbing(device, args):
         t_rt.append(time.perf_counter() - t0)
     return _entry(dec, dec + 10 * ck * 4, wall, kern, checked="bytes",
                   host_roundtrip_GiBps=round(dec / float(np.median(t_rt)) / GIB, 2),
-                  note="device decode via k_decode_duo (1-D chunks viewed as whole 512-byte rows, planner._split_1d; 128 units per chunk); host_roundtrip = MemoryStore -> HBM -> numpy")
+                  note="device decode of 1-D chunks viewed as whole 512-byte rows (planner._split_1d; 128 units per chunk); host_roundtrip = MemoryStore -> HBM -> numpy")
 
 
 def e2e_host(device, args):

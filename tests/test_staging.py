@@ -149,3 +149,32 @@ def test_slab_groups_declines():
     assert _slab_groups(batch, torch.empty(out_shape, dtype=torch.float32).transpose(0, 1)) is None  # strided
     one_row, shp = _batch_for((64, 512, 512), (64, 64, 64))  # a single chunk row along dim 0
     assert _slab_groups(one_row, torch.empty(shp, dtype=torch.float32)) is None
+
+
+def test_touched_slots_matches_projection():
+    """staging._touched_slots (interval arithmetic for ints and unit-step
+    slices) names exactly the inner chunks basic_projections touches; other
+    selection forms return None (the caller projects)."""
+    import numpy as np
+
+    from zarr_hip.indexing import basic_projections
+    from zarr_hip.staging import _touched_slots
+
+    rng = np.random.default_rng(7)
+    shape, inner = (12, 20, 9), (4, 5, 3)
+    cps = [s // c for s, c in zip(shape, inner)]
+    strides = np.array([int(np.prod(cps[d + 1:])) for d in range(3)])
+    for _ in range(500):
+        sel = []
+        for n in shape:
+            r = rng.integers(0, 3)
+            if r == 0:
+                sel.append(int(rng.integers(-n, n)))
+            else:
+                a = int(rng.integers(0, n))
+                b = int(rng.integers(a, n + 1))
+                sel.append(slice(a, b, None if r == 1 else 1))
+        sel = tuple(sel)
+        want = {int(x) for x in (basic_projections(sel, shape, inner).coords * strides).sum(axis=1)}
+        assert set(_touched_slots(sel, shape, inner, strides).tolist()) == want, sel
+    assert _touched_slots((slice(0, 12, 2), slice(None), slice(None)), shape, inner, strides) is None

@@ -46,6 +46,25 @@ def _fill_to_json(v, dtype: np.dtype):
     return int(a)
 
 
+def _selection_key(selection):
+    """A hashable image of a basic selection (ints, unit or strided slices,
+    Ellipsis), None for anything else (arrays, masks: not memoised)."""
+    sel = selection if isinstance(selection, tuple) else (selection,)
+    out = []
+    for s in sel:
+        if s is Ellipsis:
+            out.append("...")
+        elif isinstance(s, slice):
+            if not all(v is None or isinstance(v, (int, np.integer)) for v in (s.start, s.stop, s.step)):
+                return None
+            out.append(("s", s.start, s.stop, s.step))
+        elif isinstance(s, (int, np.integer)) and not isinstance(s, bool):
+            out.append(int(s))
+        else:
+            return None
+    return tuple(out)
+
+
 @dataclass
 class ArrayMetadata:
     shape: tuple[int, ...]
@@ -159,6 +178,24 @@ class Array:
         return f"{self.store_path.path}/{k}" if self.store_path.path else k
 
     def batch_info(self, selection):
+        """The CodecPipeline batch of a selection (BasicIndexer's chunk
+        projections, src/zarr/core/indexing.py:365-621).  Depends only on the
+        metadata and the selection, so basic selections are memoised per array
+        (a repeated read skips the indexer: the per-call path)."""
+        key = _selection_key(selection)
+        cache = self.__dict__.setdefault("_batches", {})
+        if key is not None:
+            hit = cache.get(key)
+            if hit is not None:
+                return list(hit[0]), hit[1]
+        batch, out_shape = self._batch_info(selection)
+        if key is not None:
+            if len(cache) >= 64:
+                cache.pop(next(iter(cache)))
+            cache[key] = (tuple(batch), out_shape)
+        return batch, out_shape
+
+    def _batch_info(self, selection):
         rows, out_shape = chunk_batch(selection, self.metadata.shape, self.metadata.chunk_shape)
         store, spec, sep = self.store_path.store, self.spec, self.metadata.separator
         if self.metadata.key_encoding == "v2":

@@ -36,6 +36,20 @@ WINDOW = int(os.environ.get("ZARR_HIP_STAGE_WINDOW", str(4 << 20)))
 MAX_U64 = np.uint64(0xFFFFFFFFFFFFFFFF)
 
 _COPY_STREAMS: dict = {}
+_COPY_MODE_SET = [False]
+
+
+def _copy_mode() -> None:
+    """ZARR_HIP_STAGE_COPY=memcpy selects plain memcpy packing (measurement
+    arm; the library default is streaming stores, ZHIP_TUNE_STAGE_COPY)."""
+    if _COPY_MODE_SET[0]:
+        return
+    _COPY_MODE_SET[0] = True
+    mode = os.environ.get("ZARR_HIP_STAGE_COPY", "")
+    if mode:
+        from . import _native as N
+
+        N.lib().zhip_set_tuning(5, 0 if mode == "memcpy" else 1)
 
 
 def _workers() -> int:
@@ -170,6 +184,7 @@ def stage(layout: StagingLayout, device, post=(), defer: bool = False):
 
     from . import _native as N
 
+    _copy_mode()
     total = max(layout.top, 16)
     # file pieces carry an encoded path (kept alive with the job) and an offset;
     # bytes objects are addressed in place (ctypes.cast: a third of the cost
@@ -284,6 +299,28 @@ def _shard_key(bg):
     return (id(st), getattr(bg, "path", id(bg)))
 
 
+def _touched_slots(csel, shard_shape, inner_shape, strides):
+    """Linear inner-chunk slots a chunk selection of ints and unit-step slices
+    touches, by interval arithmetic; None for other forms (the caller then
+    projects: strided slices may skip inner chunks)."""
+    slots = np.zeros(1, np.int64)
+    for s, n, c, st in zip(csel, shard_shape, inner_shape, strides):
+        if isinstance(s, (int, np.integer)):
+            i = int(s) + (int(n) if int(s) < 0 else 0)
+            lo, hi = i // c, i // c + 1
+        elif isinstance(s, slice):
+            a, b, step = s.indices(int(n))
+            if step != 1:
+                return None
+            if a >= b:
+                return np.zeros(0, np.int64)
+            lo, hi = a // c, (b - 1) // c + 1
+        else:
+            return None
+        slots = (slots[:, None] + np.arange(lo, hi, dtype=np.int64)[None, :] * int(st)).reshape(-1)
+    return slots
+
+
 def gather_sharded_partial(batch: list, sh, cps, n_inner: int, inner_shape, spec, device,
                            defer: bool = False, inner_decode=None):
     """Host-sourced sharded batch: index by range request, touched inner chunks
@@ -305,9 +342,12 @@ def gather_sharded_partial(batch: list, sh, cps, n_inner: int, inner_shape, spec
         k = _shard_key(item[0])
         if k not in shards:
             shards[k] = {"bg": item[0], "slots": set()}
-        csel = item[2]
-        pr = basic_projections(tuple(csel), spec.shape, inner_shape)
-        shards[k]["slots"].update(int(s) for s in (pr.coords * cps_strides[None, :]).sum(axis=1))
+        csel = tuple(item[2])
+        sl = _touched_slots(csel, spec.shape, inner_shape, cps_strides) if len(csel) == len(spec.shape) else None
+        if sl is None:
+            pr = basic_projections(csel, spec.shape, inner_shape)
+            sl = (pr.coords * cps_strides[None, :]).sum(axis=1)
+        shards[k]["slots"].update(sl.tolist())
         item_shard.append(k)
     out_of_shard = {}
     for k, s in shards.items():
