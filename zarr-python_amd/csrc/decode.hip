@@ -493,6 +493,7 @@ KernelFn select_pair_kernel(bool crc, int item, bool swap, int nu);  // decode_r
 KernelFn select_duo_kernel(bool crc, int item, bool swap);           // decode_rows.hip
 KernelFn select_il_kernel(bool crc, int item, bool swap);            // decode_rows.hip
 KernelFn select_il_kernel_lean(bool crc, int item, bool swap);       // decode_rows.hip
+KernelFn select_il_kernel_cf(bool crc, int item, bool swap);         // decode_rows.hip
 KernelFn select_xw_kernel(bool crc, int item, bool swap);            // decode_rows.hip
 KernelFn select_tile4_kernel(bool crc, int item, bool swap);         // decode_tile.hip
 KernelFn select_tileg_kernel(bool crc, int item, bool swap);         // decode_tile.hip
@@ -546,8 +547,9 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
             return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
         }
         if (il) {
-            KernelFn ifn = (p.tune & kTuneIlLean) ? select_il_kernel_lean(crc, p.g.itemsize, swap)
-                                                  : select_il_kernel(crc, p.g.itemsize, swap);
+            KernelFn ifn = (p.tune & kTuneCfLookup) ? select_il_kernel_cf(crc, p.g.itemsize, swap)
+                           : (p.tune & kTuneIlLean) ? select_il_kernel_lean(crc, p.g.itemsize, swap)
+                                                    : select_il_kernel(crc, p.g.itemsize, swap);
             if (!ifn) return ZHIP_E_UNSUPPORTED;
             const uint32_t igrid = p.n_units > p.n_idx ? p.n_units : p.n_idx;
             if (igrid == 0) return ZHIP_OK;

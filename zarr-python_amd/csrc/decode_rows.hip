@@ -463,6 +463,22 @@ __device__ __forceinline__ void crc_block4(const uint32_t* s, Acc4& a, const uin
     a.a3 = t11(s, a.a3 ^ v.w);
 }
 
+// Timing arm (kTuneCfLookup): the same three lookups per word at addresses
+// whose bank is the lane's own (index bits << 5 | lane % 32), so no ds_read_b32
+// group conflicts -- the cost of the CRC lookups without bank conflicts.
+// Results invalid.
+__device__ __forceinline__ uint32_t t11_cf(const uint32_t* s, uint32_t w, uint32_t ln) {
+    return s[kPairT1 + (((w & 63u) << 5) | ln)] ^ s[kPairT2 + ((((w >> 11) & 63u) << 5) | ln)] ^
+           s[kPairT3 + ((((w >> 22) & 31u) << 5) | ln)];
+}
+
+__device__ __forceinline__ void crc_block4_cf(const uint32_t* s, Acc4& a, const uint4 v, uint32_t ln) {
+    a.a0 = t11_cf(s, a.a0 ^ v.x, ln);
+    a.a1 = t11_cf(s, a.a1 ^ v.y, ln);
+    a.a2 = t11_cf(s, a.a2 ^ v.z, ln);
+    a.a3 = t11_cf(s, a.a3 ^ v.w, ln);
+}
+
 __device__ __forceinline__ uint32_t fold4(const uint32_t* s, const Acc4& a) {
     const uint32_t* t4 = s + kPairA4;
     return tab_apply(t4, tab_apply(t4, tab_apply(t4, a.a0) ^ a.a1) ^ a.a2) ^ a.a3;
@@ -1154,7 +1170,7 @@ __device__ __forceinline__ void publish_il(const DecodeParams& p, uint32_t c, ui
 // headline than the production order (data loads after the resolved header:
 // the tables, L2 hits, are in LDS before the data flood;
 // profiles/r03/lean/).
-template <bool CRC, int ITEM, bool SWAP, bool LEAN = false>
+template <bool CRC, int ITEM, bool SWAP, bool LEAN = false, bool CF = false>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_decode_il(const DecodeParams p) {
     constexpr int K = kDefaultBlocks;
     __shared__ uint32_t s_tab[CRC ? kPairTabWords : 1];
@@ -1313,7 +1329,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))
             const uint32_t lo = m[k].lo, hi = m[k].hi;
             const bool wr = writes && lane_row - lo < hi - lo;
             store_nt16(wr ? obase + m[k].rel + lane_off : sink, ok ? swap_block<ITEM, SWAP>(A[k]) : f);
-            if (CRC && ok) crc_block4(s_tab, acc, A[k]);
+            if constexpr (CF) {  // timing arm: the lookups at lane-owned banks (results invalid)
+                if (CRC && ok) crc_block4_cf(s_tab, acc, A[k], (uint32_t)t & 31u);
+            } else {
+                if (CRC && ok) crc_block4(s_tab, acc, A[k]);
+            }
         }
         // 4. run end: one chain per workgroup, one publication
         if constexpr (CRC) {
@@ -1336,6 +1356,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))
 
 KernelFn select_il_kernel_lean(bool crc, int item, bool swap) {  // kTuneIlLean (4-byte LE CRC item type only)
     return (crc && item == 4 && !swap) ? k_decode_il<true, 4, false, true> : nullptr;
+}
+
+KernelFn select_il_kernel_cf(bool crc, int item, bool swap) {  // kTuneCfLookup timing arm (results invalid)
+    return (crc && item == 4 && !swap) ? k_decode_il<true, 4, false, false, true> : nullptr;
 }
 
 KernelFn select_il_kernel(bool crc, int item, bool swap) {
