@@ -1261,13 +1261,18 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))
     //    the lane constant, the index lane constant, the first index block],
     //    the K data blocks; headers, row-map entries and the trailer are scalar
     if constexpr (CRC) {
-        const uint4* gt = reinterpret_cast<const uint4*>(p.il_tab);
-        tv0 = gt[t];
-        tv1 = gt[t + kThreads];
-        tv2 = gt[t + 2 * kThreads];
-        tv3 = gt[t + 3 * kThreads];
-        tv4 = gt[t + 4 * kThreads];
-        tv5 = gt[t + 5 * kThreads];
+        // (timing arm kTuneNoTables: every lane reads one zero line instead of
+        // the 24 KiB of tables; results invalid)
+        const bool ntab = (p.tune & kTuneNoTables) != 0;
+        const uint4* gt = ntab ? reinterpret_cast<const uint4*>(g_rows_zero)
+                               : reinterpret_cast<const uint4*>(p.il_tab);
+        const int ti = ntab ? 0 : t, ts = ntab ? 0 : kThreads;
+        tv0 = gt[ti];
+        tv1 = gt[ti + ts];
+        tv2 = gt[ti + 2 * ts];
+        tv3 = gt[ti + 3 * ts];
+        tv4 = gt[ti + 4 * ts];
+        tv5 = gt[ti + 5 * ts];
         kl = load_u32_any(reinterpret_cast<const uint8_t*>(p.il_klane + (size_t)(has ? r : 0u) * kThreads + t));
         kix = load_u32_any(reinterpret_cast<const uint8_t*>(p.il_kidx + t));
     }
@@ -1337,7 +1342,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))
         }
         // 4. run end: one chain per workgroup, one publication
         if constexpr (CRC) {
-            uint32_t v = ok ? lanemul3(s_mul, t, fold4(s_tab, acc)) : 0u;
+            uint32_t v = ok ? ((p.tune & kTuneNoRunEnd) ? acc.a0 ^ acc.a1 ^ acc.a2 ^ acc.a3  // timing arm
+                                                         : lanemul3(s_mul, t, fold4(s_tab, acc)))
+                            : 0u;
             v = wave_xor(v);
             if ((t & 63) == 0) s_red[0][t >> 6] = v;
             __syncthreads();
