@@ -246,3 +246,97 @@ def test_c1_exact_geometry(device, kind):
     assert arr[...].tobytes() == data.tobytes()
     sel = (slice(123457, 9_876_543, 1),)
     assert arr[sel].tobytes() == np.ascontiguousarray(O.read(host, meta, sel)).tobytes()
+
+
+# --------------------------------------------- C4 / C5 at their FULL sizes
+# The oracle cannot decode 4 GiB in seconds, so the full-size checks are the
+# size-independent properties the domain offers: the GPU encode -> GPU decode
+# round trip is the source bit for bit, a sample of the stored shards is
+# byte-identical to what the oracle encodes from the same source region and
+# decodes back to it, and a corrupted inner chunk is caught with the
+# reference's message.
+
+def _full(device, g, dtype):
+    import torch
+
+    import zarr_hip
+
+    gen = torch.Generator(device=device).manual_seed(11)
+    if dtype == "int16":
+        src = torch.randint(-2 ** 15, 2 ** 15, g["shape"], generator=gen, device=device, dtype=torch.int16)
+    else:
+        src = torch.randn(g["shape"], generator=gen, device=device, dtype=torch.float32)
+    n_shards = int(np.prod([s // c for s, c in zip(g["shape"], g["shards"])]))
+    per = int(np.prod(g["shards"])) * src.element_size() + int(np.prod(
+        [s // i for s, i in zip(g["shards"], g["inner"])])) * (4 + 16) + 4
+    store = zarr_hip.DeviceStore(device, capacity=n_shards * (per + 256) + (1 << 24))
+    arr = zarr_hip.Array.create(store, g["shape"], g["inner"], dtype, 0, shards=g["shards"],
+                                inner_codecs=[W.LE, W.CRC])
+    sb, _ = arr.batch_info((Ellipsis,))
+    for i in range(0, len(sb), 64):
+        arr.codec_pipeline.write_sync(sb[i:i + 64], src)
+    torch.cuda.synchronize(device)
+    return src, store, arr
+
+
+def _oracle_shard_check(store, g, dtype, src, key, coords):
+    meta = O.ArrayMeta(tuple(g["shards"]), tuple(g["shards"]), np.dtype(dtype), 0,
+                       codecs=[SHARD(g["inner"], [W.LE, W.CRC])])
+    region = tuple(slice(c * s, (c + 1) * s) for c, s in zip(coords, g["shards"]))
+    want_vals = src[region].cpu().numpy()
+    host = {}
+    O.write(host, meta, (Ellipsis,), want_vals)
+    got = store.get_sync(key).to_bytes()
+    assert got == host["c/0/0/0"], f"stored shard {key} differs from the oracle's encoding"
+    back = O.read({"c/0/0/0": got}, meta)
+    assert back.tobytes() == want_vals.tobytes()
+
+
+@pytest.mark.parametrize("which", ["c4", "c5"])
+def test_full_size_roundtrip_and_oracle_sample(device, which):
+    import torch
+
+    g = W.C4 if which == "c4" else W.C5
+    dtype = "float32" if which == "c4" else "int16"
+    src, store, arr = _full(device, g, dtype)
+    try:
+        if which == "c4":
+            out = arr.get((Ellipsis,))
+            assert torch.equal(out.view(torch.int32), src.view(torch.int32))
+            del out
+        else:  # bench.py's C5 batch: rng(1) 10 % of the inner chunks into a full-shape out
+            grid = tuple(s // i for s, i in zip(g["shape"], g["inner"]))
+            coords = W.partial_selection(grid)
+            batch = W.inner_chunk_batch(arr, store, coords, g["inner"])
+            out = torch.zeros(g["shape"], dtype=torch.int16, device=device)
+            arr.codec_pipeline.read_sync(batch, out)
+            for it in batch[::97]:
+                osel = tuple(it[3])
+                assert torch.equal(out[osel], src[osel])
+            del out
+        grid = [s // c for s, c in zip(g["shape"], g["shards"])]
+        for coords in [(0, 0, 0), tuple(x - 1 for x in grid), (grid[0] // 2, 1, grid[2] - 2)]:
+            key = "c/" + "/".join(str(c) for c in coords)
+            _oracle_shard_check(store, g, dtype, src, key, coords)
+    finally:
+        del src, store, arr
+        torch.cuda.empty_cache()
+
+
+def test_full_size_c4_corruption_caught(device):
+    """One flipped bit in one inner chunk of the 4 GiB C4 array: the full read
+    raises the reference's checksum message (crc32c_.py:46-49)."""
+    import torch
+
+    g = W.C4
+    src, store, arr = _full(device, g, "float32")
+    try:
+        key = "c/3/5/7"
+        ref = store.get_sync(key)
+        off = ref.offset + 123457
+        store.arena.buf[off] ^= 0x10
+        with pytest.raises(ValueError, match="Stored and computed checksum do not match"):
+            arr.get((Ellipsis,))
+    finally:
+        del src, store, arr
+        torch.cuda.empty_cache()
