@@ -765,7 +765,7 @@ class HipCodecPipeline:
                 return self._read_slabs(batch, groups, dev_out, host_out, direct)
         prog = self.prepare_read(batch, dev_out, drop_axes)
         prog.launch()
-        res = prog.results()
+        res = prog.results_fast()  # one 4-byte error word back (the statuses only on an error)
         if direct:
             _d2h(dev_out, host_out, 0, dev_out.numel() * dev_out.element_size())
             _torch().cuda.current_stream(dev_out.device).synchronize()
@@ -807,7 +807,7 @@ class HipCodecPipeline:
     def _read_uncached(self, batch, dev_out, drop_axes) -> tuple[GetResult, ...]:
         prog = self.prepare_read(batch, dev_out, drop_axes)
         prog.launch()
-        return prog.results()
+        return prog.results_fast()
 
     def _read_slabs_one_plan(self, batch, groups, dev_out, host_out, direct: bool):
         """_read_slabs for unsharded chains: the batch is planned ONCE (in slab

@@ -28,7 +28,7 @@ import os
 import numpy as np
 
 from .interop import byte_payload, is_missing_key_error, request_classes, staged_bytes
-from .store import ALIGN, TAIL_SLACK, DeviceRef, FileRef, pinned_spans
+from .store import ALIGN, TAIL_SLACK, DeviceRef, FileRef, MemoryStore, StorePath, pinned_spans
 
 # 4 MiB windows: smaller ones pay ~10 us per hipMemcpyAsync, larger ones start
 # the DMA late (scripts/stage_micro.py)
@@ -239,16 +239,19 @@ def gather_sources(batch: list, device, defer: bool = False, start: bool = True)
     (deferred) and returns (src, keepalive, pending)."""
     import torch
 
-    raws = []
-    for item in batch:
-        bg = item[0]
-        loc = getattr(getattr(bg, "store", None), "locate_sync", None)
-        if loc is not None:  # a local file: the staging pool preads it (ZHIP_PIECE_FILE)
-            raws.append(loc(bg.path))
-        else:
-            raws.append(staged_bytes(bg.get_sync(prototype=None) if hasattr(bg, "get_sync") else bg))
-    arenas = {id(r.arena): r.arena for r in raws if isinstance(r, DeviceRef)}
-    all_dev = all(r is None or isinstance(r, DeviceRef) for r in raws)
+    raws = _memory_values(batch)
+    host_only = raws is not None  # bytes / None only: no device pieces to look for
+    if raws is None:
+        raws = []
+        for item in batch:
+            bg = item[0]
+            loc = getattr(getattr(bg, "store", None), "locate_sync", None)
+            if loc is not None:  # a local file: the staging pool preads it (ZHIP_PIECE_FILE)
+                raws.append(loc(bg.path))
+            else:
+                raws.append(staged_bytes(bg.get_sync(prototype=None) if hasattr(bg, "get_sync") else bg))
+    arenas = {} if host_only else {id(r.arena): r.arena for r in raws if isinstance(r, DeviceRef)}
+    all_dev = not host_only and all(r is None or isinstance(r, DeviceRef) for r in raws)
     tdev = torch.device(device)
     if arenas and any(a.device.type != tdev.type or (a.device.index or 0) != (tdev.index or 0)
                       for a in arenas.values()):
@@ -265,17 +268,21 @@ def gather_sources(batch: list, device, defer: bool = False, start: bool = True)
     lay = StagingLayout()
     srcs = []
     dev_refs = []
-    for r in raws:
+    pieces, top, A = lay.pieces, 0, ALIGN - 1
+    for r in raws:  # StagingLayout.add / reserve inlined (one pass per batch item)
         if r is None:
             srcs.append((0, 0, True))
-        elif isinstance(r, (DeviceRef, torch.Tensor)):  # device bytes elsewhere: D2D copy below
+            continue
+        if not host_only and isinstance(r, (DeviceRef, torch.Tensor)):  # device bytes elsewhere: D2D below
             n = r.length if isinstance(r, DeviceRef) else r.numel()
-            off = lay.reserve(n)
-            dev_refs.append((r, off))
-            srcs.append((off, n, False))
+            dev_refs.append((r, top))
         else:
-            off, n = lay.add(r)
-            srcs.append((off, n, False))
+            n = len(r)
+            if n:
+                pieces.append((r, top, n))
+        srcs.append((top, n, False))
+        top = (top + n + A) & ~A
+    lay.top = top
     def d2d(dev):  # after the H2D windows (which also cover the reserved gaps)
         for r, off in dev_refs:
             v = r.arena.view(r.offset, r.length) if isinstance(r, DeviceRef) else r
@@ -285,6 +292,25 @@ def gather_sources(batch: list, device, defer: bool = False, start: bool = True)
         return None, lay.top, srcs, [], lambda: stage(lay, device, post=[d2d] if dev_refs else [], defer=True)
     dev, keep, pending = stage(lay, device, post=[d2d] if dev_refs else [], defer=defer)
     return dev, lay.top, srcs, keep, pending
+
+
+def _memory_values(batch: list):
+    """Whole values of a batch whose getters are all StorePaths into ONE of this
+    package's MemoryStores (the class itself: a subclass may override
+    get_sync), read from its dict in one pass: the per-item getter chain
+    (StorePath.get_sync -> MemoryStore.get_sync -> memoryview -> staging view)
+    is most of a host read's Python cost before the first DMA.  The bytes
+    objects go to the packer as they are (addressed in place).  None when the
+    batch is anything else."""
+    bg0 = batch[0][0]
+    if type(bg0) is not StorePath or type(bg0.store) is not MemoryStore:
+        return None
+    st = bg0.store
+    if not all(type(it[0]) is StorePath and it[0].store is st for it in batch):
+        return None
+    get = st._d.get
+    vals = [get(it[0].path) for it in batch]
+    return [v if v is None or type(v) is bytes else staged_bytes(memoryview(v)) for v in vals]
 
 
 def staged_host(buf):
