@@ -31,10 +31,20 @@ def main():
     data = torch.from_numpy(bench.synthetic(shape)).to(dev)
     tune = int(os.environ.get("TUNE", "0"))
     progs = []
+    # WORLD=n: only rank 0's shards of an n-way round-robin split (the bench's
+    # strong-scaled headline at n GPUs), decoded into a full-shape out
+    world = int(os.environ.get("WORLD", "1"))
+    from zarr_hip import buffer, parallel
+
     for _ in range(4):
         codecs = [bench.LE] if os.environ.get("NOCRC") else [bench.LE, bench.CRC]
         arr = bench.build_replica(dev, data, shape, chunks, codecs, shards=shards)
-        progs.append(arr.prepare_read((Ellipsis,))[0])
+        if world == 1:
+            progs.append(arr.prepare_read((Ellipsis,))[0])
+        else:
+            batch, out_shape = arr.batch_info((Ellipsis,))
+            out = buffer.empty(out_shape, "float32", dev)
+            progs.append(arr.codec_pipeline.prepare_read(parallel.rank_batch(batch, world, 0), out))
     sh = int(torch.cuda.current_stream(dev).cuda_stream)
     N.lib().zhip_set_tuning(2, 1024 | tune)
     for i in range(8):
@@ -43,7 +53,7 @@ def main():
     N.lib().zhip_set_tuning(2, 0)
     for p in progs:
         p.results()
-    n_wg = 2048 if tune & 128 else 1024
+    n_wg = (2048 if tune & 128 else 1024) // world
     buf = np.zeros(n_wg * 8, np.uint64)
     N.check(N.lib().zhip_debug_stamps(buf.ctypes.data, n_wg), "zhip_debug_stamps")
     st = buf.reshape(n_wg, 8)
