@@ -14,9 +14,11 @@ Compressed scenarios run with the compressor on the host (1d-gzip,
 transpose-gzip: the built-in gzip; zstd needs zarr's codec instance, which
 tests/test_gpu_compression.py drives with a caller-supplied codec object).
 Nested sharding (suite:308-320) runs its outer level on the host and its inner
-level on the GPU (zarr_hip/nested.py).  zarr v2 is not restated; the test
-below pins that the GPU path refuses a zstd named only by JSON loudly rather
-than falling back to the CPU.
+level on the GPU (zarr_hip/nested.py).  zarr v2 (suite:178-221) runs through
+the V2Codec wrapper's mapping: the caller's numcodecs compressor and filters on
+the host, the raw chunk bytes on the GPU (restated numcodecs fakes,
+tests/zarr_fakes.py).  The last test pins that the GPU path refuses a zstd
+named only by JSON loudly rather than falling back to the CPU.
 """
 
 from __future__ import annotations
@@ -305,6 +307,83 @@ def test_empty_shard_deleted_after_overwrite_to_fill(kind, tmp_path, device):
     np.testing.assert_array_equal(arr[:], np.zeros(16))
 
 
+def _v2_array(store, shape, chunks, dtype, fill, codec, order="C"):
+    """An array as zarr v2 hands its pipeline: one V2Codec(filters, compressor)
+    (src/zarr/codecs/_v2.py), "." chunk keys, the chunk order from the array."""
+    from zarr_hip.array import Array, ArrayMetadata
+    from zarr_hip.spec import ArrayConfig
+    from zarr_hip.store import StorePath
+
+    md = ArrayMetadata(tuple(shape), tuple(chunks), np.dtype(dtype), np.array(fill, dtype)[()], (codec,),
+                       ".", {}, "v2")
+    return Array(StorePath(store, ""), md, ArrayConfig(order=order))
+
+
+def _v2_expected(ref, chunks, fill, filters, comp, order) -> dict:
+    """Stored bytes per v2 key: the whole chunk (edges padded with the fill)
+    in the array's order -> filters -> compressor (_v2.py:72-93); chunks equal
+    to the fill are not written (write_empty_chunks=False)."""
+    grid = [-(-s // c) for s, c in zip(ref.shape, chunks)]
+    out = {}
+    for co in np.ndindex(*grid):
+        blk = np.full(chunks, fill, ref.dtype)
+        src = ref[tuple(slice(i * c, min((i + 1) * c, s)) for i, c, s in zip(co, chunks, ref.shape))]
+        blk[tuple(slice(0, n) for n in src.shape)] = src
+        if np.array_equal(blk, np.full(chunks, fill, ref.dtype)):
+            continue
+        chunk = np.asarray(blk, order=order)
+        for f in filters or ():
+            chunk = f.encode(chunk)
+        data = comp.encode(chunk) if comp is not None else \
+            np.ascontiguousarray(np.asarray(chunk).reshape(-1, order="A")).view(np.uint8).tobytes()
+        out[".".join(map(str, co))] = bytes(data)
+    return out
+
+
+def _v2_cases():
+    from zarr_fakes import NumDelta, NumGZip
+
+    return [
+        # suite:182-221, as written there
+        ("v2-roundtrip", (100,), (10,), "C", None, None, ((slice(None), _ar(100, "f8")),), (slice(None),)),
+        ("v2-gzip-roundtrip", (100,), (10,), "C", None, NumGZip(1), ((slice(None), _ar(100, "f8")),),
+         (slice(None),)),
+        ("v2-filter-gzip-roundtrip", (100,), (10,), "C", (NumDelta("float64"),), NumGZip(1),
+         ((slice(None), _ar(100, "f8")),), (slice(None),)),
+        # additions: 2-d, ragged edges, F order, partial writes, strided reads
+        ("v2-2d-F-filter-gzip", (12, 10), (5, 4), "F", (NumDelta("float64"),), NumGZip(1),
+         ((np.s_[1:11, 2:9], np.arange(70, dtype="f8").reshape(10, 7) + 0.5), (np.s_[0:3, :], 2.0)),
+         (slice(None), np.s_[::3, 1:10:4], np.s_[11, 9])),
+        ("v2-2d-C-raw-partial", (12, 10), (5, 4), "C", None, None,
+         ((np.s_[4:12, 3:7], np.arange(32, dtype="f8").reshape(8, 4)),), (slice(None), np.s_[5:7, ::2])),
+    ]
+
+
+@pytest.mark.parametrize("kind", STORES)
+@pytest.mark.parametrize("case", _v2_cases(), ids=lambda c: c[0])
+def test_v2_scenario(case, kind, tmp_path, device):
+    """The suite's zarr v2 scenarios (suite:178-221): reads equal the numpy
+    reference, stored bytes equal the wrapper's (filters, compressor) over the
+    raw chunks."""
+    from zarr_fakes import V2Codec
+
+    vid, shape, chunks, order, filters, comp, writes, reads = case
+    store = _make_store(kind, tmp_path, device)
+    arr = _v2_array(store, shape, chunks, "float64", 0.0, V2Codec(filters, comp), order)
+    ref = np.zeros(shape, "f8")
+    for sel, value in writes:
+        arr[sel] = value
+        ref[sel] = value
+    for sel in reads:
+        got = arr[sel]
+        np.testing.assert_array_equal(got, ref[sel], err_msg=f"{vid}: read {sel!r}")
+    exp = _v2_expected(ref, chunks, 0.0, filters, comp, order)
+    got = {k: bytes(v) for k, v in store.to_dict().items()}
+    assert sorted(got) == sorted(exp), vid
+    for k in exp:
+        assert got[k] == exp[k], f"{vid}: bytes differ for {k}"
+
+
 def test_read_write_methods_do_not_branch_on_sharding_codec_type():
     """suite:555-583: read/write dispatch on supports_partial_decode/encode, not
     isinstance(ShardingCodec)."""
@@ -321,8 +400,8 @@ def test_read_write_methods_do_not_branch_on_sharding_codec_type():
     ([LE, {"name": "zstd", "configuration": {"level": 1}}], None, "zstd"),
 ])
 def test_out_of_scope_chains_refused_loudly(codecs, shards, why, device):
-    """suite:147-226 (a zstd without its codec instance, v2): the pipeline must
-    raise rather than decode on the host."""
+    """suite:156-165 (a zstd named by JSON, without its codec instance): the
+    pipeline must raise rather than decode on the host."""
     import zarr_hip
 
     store = zarr_hip.DeviceStore(device)

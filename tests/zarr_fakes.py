@@ -21,6 +21,13 @@ HipCodecPipeline the way zarr's Array layer would:
                   (src/zarr/storage/_common.py:247-272)
   RangeByteRequest / SuffixByteRequest  (src/zarr/abc/store.py)
   ArrayV3Metadata codecs / chunk_grid.chunk_shape / data_type / fill_value
+  V2Codec         filters + compressor (src/zarr/codecs/_v2.py:19-23), holding
+                  numcodecs objects restated from numcodecs' published
+                  algorithms (numcodecs is not installed here):
+  NumGZip         numcodecs.GZip(level): a gzip member (mtime 0 here, so the
+                  bytes are reproducible), decode of a gzip member
+  NumDelta        numcodecs.Delta(dtype, astype): out[0] = a[0], out[i] =
+                  a[i] - a[i-1] in astype; decode = cumulative sum in dtype
 """
 
 from __future__ import annotations
@@ -324,3 +331,57 @@ class ShardingCodec:
         return {"name": "sharding_indexed", "configuration": {
             "chunk_shape": list(self.chunk_shape), "codecs": [c.to_dict() for c in self.codecs],
             "index_codecs": [c.to_dict() for c in self.index_codecs], "index_location": self.index_location}}
+
+
+class NumGZip:
+    """numcodecs.GZip (level): encode -> a gzip member, decode -> its payload."""
+
+    codec_id = "gzip"
+
+    def __init__(self, level: int = 1):
+        self.level = level
+
+    def encode(self, buf):
+        import gzip
+
+        # ensure_contiguous_ndarray: the bytes in memory order (reshape order "A")
+        data = np.ascontiguousarray(buf.reshape(-1, order="A")).view(np.uint8).tobytes() \
+            if isinstance(buf, np.ndarray) else bytes(buf)
+        return gzip.compress(data, compresslevel=self.level, mtime=0)
+
+    def decode(self, buf, out=None):
+        import gzip
+
+        return gzip.decompress(bytes(buf))
+
+
+class NumDelta:
+    """numcodecs.Delta (dtype, astype)."""
+
+    codec_id = "delta"
+
+    def __init__(self, dtype, astype=None):
+        self.dtype = np.dtype(dtype)
+        self.astype = np.dtype(astype) if astype is not None else self.dtype
+
+    def encode(self, buf):
+        a = np.asarray(buf).reshape(-1, order="A")  # memory order, as ensure_ndarray + reshape
+        a = np.ascontiguousarray(a).view(self.dtype)
+        enc = np.empty_like(a, dtype=self.astype)
+        if a.size:
+            enc[0] = a[0]
+            enc[1:] = np.diff(a).astype(self.astype)
+        return enc
+
+    def decode(self, buf, out=None):
+        enc = np.frombuffer(bytes(buf), self.astype) if not isinstance(buf, np.ndarray) else \
+            np.ascontiguousarray(buf).reshape(-1).view(self.astype)
+        return np.cumsum(enc, dtype=self.dtype)
+
+
+class V2Codec:
+    """zarr's V2Codec (src/zarr/codecs/_v2.py:19-23): filters + compressor."""
+
+    def __init__(self, filters=None, compressor=None):
+        self.filters = tuple(filters) if filters else None
+        self.compressor = compressor

@@ -395,6 +395,85 @@ class HostCodec:
         return _to_bytes(out)
 
 
+@dataclass(frozen=True)
+class V2Stage:
+    """The host half of zarr v2's codec wrapper (V2Codec, src/zarr/codecs/_v2.py:
+    19-96): the numcodecs compressor and filters the caller's V2Codec holds run
+    on the host, in the reference's order; the raw chunk bytes they produce or
+    consume are the fixed-size part the GPU decodes / encodes as a little-endian
+    ``bytes`` codec (plus a reversing transpose for ``order="F"``, added when the
+    pipeline is evolved against the chunk spec).  Nothing of numcodecs is
+    imported: the objects are the caller's."""
+
+    filters: tuple
+    compressor: Any
+    is_fixed_size = False
+    host = True
+
+    def to_dict(self) -> dict:
+        return {"name": "v2", "configuration": {"filters": [repr(f) for f in self.filters],
+                                                "compressor": repr(self.compressor)}}
+
+    @property
+    def name(self) -> str:
+        return "v2"
+
+    def evolve_from_array_spec(self, spec: ArraySpec) -> "V2Stage":
+        return self
+
+    def resolve_metadata(self, spec: ArraySpec) -> ArraySpec:
+        return spec
+
+    def compute_encoded_size(self, n: int, spec: ArraySpec | None = None) -> int:
+        raise NotImplementedError  # _v2.py:95-96
+
+    def validate(self, **kw) -> None:
+        return None
+
+    def decode_bytes(self, data, spec: ArraySpec | None = None) -> bytes:
+        """_v2.py:25-70 up to the reinterpretation: decompress, filters in reverse,
+        then the chunk's bytes in memory order (reshape(-1, order="A"))."""
+        chunk = self.compressor.decode(bytes(data)) if self.compressor else data
+        for f in reversed(self.filters):
+            chunk = f.decode(chunk)
+        if isinstance(chunk, (bytes, bytearray, memoryview)):
+            return bytes(chunk)
+        a = np.asarray(chunk)
+        if a.dtype == object:
+            raise RuntimeError("cannot read object array without object codec")
+        return a.reshape(-1, order="A").view(np.uint8).tobytes()
+
+    def encode_bytes(self, data, spec: ArraySpec | None = None) -> bytes:
+        """_v2.py:72-93: the chunk as an array of the native dtype in the spec's
+        shape and order, filters, compressor."""
+        raw = np.frombuffer(bytes(data), np.uint8)
+        chunk = raw
+        if spec is not None and raw.size == int(np.prod(spec.shape)) * spec.dtype.itemsize:
+            chunk = raw.view(spec.dtype).reshape(spec.shape, order=spec.order)
+        for f in self.filters:
+            chunk = f.encode(chunk)
+        if np.asarray(chunk).dtype == object:
+            raise RuntimeError("cannot write object array without object codec")
+        cdata = self.compressor.encode(chunk) if self.compressor else chunk
+        return _to_bytes(cdata) if not isinstance(cdata, np.ndarray) else \
+            np.ascontiguousarray(cdata).reshape(-1).view(np.uint8).tobytes()
+
+
+def is_v2_codec(c) -> bool:
+    """zarr's V2Codec instance (duck-typed: no zarr import)."""
+    return type(c).__name__ == "V2Codec" and hasattr(c, "filters") and hasattr(c, "compressor")
+
+
+def v2_chain(c) -> list:
+    """V2Codec(filters, compressor) -> [bytes(little), V2Stage] (the stage only
+    when there is something to run on the host)."""
+    filters = tuple(c.filters or ())
+    out = [BytesCodec(endian="little")]
+    if filters or c.compressor is not None:
+        out.append(V2Stage(filters, c.compressor))
+    return out
+
+
 def _to_bytes(buf) -> bytes:
     if isinstance(buf, (bytes, bytearray, memoryview)):
         return bytes(buf)
@@ -442,8 +521,11 @@ def parse_codecs(codecs) -> list:
     carried over from the instance."""
     out = []
     for c in codecs:
-        if isinstance(c, (BytesCodec, Crc32cCodec, TransposeCodec, ShardingCodec, GzipCodec, HostCodec)):
+        if isinstance(c, (BytesCodec, Crc32cCodec, TransposeCodec, ShardingCodec, GzipCodec, HostCodec, V2Stage)):
             out.append(c)
+            continue
+        if is_v2_codec(c):  # zarr v2's filters + compressor wrapper (an ArrayBytesCodec)
+            out.extend(v2_chain(c))
             continue
         conf = c.to_dict() if hasattr(c, "to_dict") and not isinstance(c, dict) else c
         name = conf if isinstance(conf, str) else conf["name"]

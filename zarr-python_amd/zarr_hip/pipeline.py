@@ -24,7 +24,8 @@ import numpy as np
 
 from . import _native as N
 from . import staging
-from .codecs import ShardingCodec, evolve_codecs, parse_codecs, split_codecs, split_host_tail
+from .codecs import (ShardingCodec, TransposeCodec, evolve_codecs, is_v2_codec, parse_codecs, split_codecs,
+                     split_host_tail)
 from .interop import device_tensor, host_array
 from .planner import CHUNK_DT, SEL_DT, STATUS_DT, ChainInfo, Tables, analyze_chain, plan_decode, predict_rows
 from .spec import ArraySpec, GetResult, coerce_spec
@@ -481,9 +482,13 @@ class HipCodecPipeline:
 
     @classmethod
     def from_codecs(cls, codecs: Iterable, *, batch_size: int | None = None) -> "HipCodecPipeline":
+        codecs = tuple(codecs)
         cl = tuple(parse_codecs(codecs))
         aa, ab, bb = split_codecs(cl)
-        return cls(cl, aa, ab, bb, batch_size or (1 << 30))
+        p = cls(cl, aa, ab, bb, batch_size or (1 << 30))
+        if any(is_v2_codec(c) for c in codecs):
+            p._aux["v2"] = True  # the chunk spec's order decides the stored layout (evolve)
+        return p
 
     @classmethod
     def from_array_metadata_and_store(cls, array_metadata, store) -> "HipCodecPipeline":
@@ -506,7 +511,15 @@ class HipCodecPipeline:
 
     def evolve_from_array_spec(self, array_spec) -> "HipCodecPipeline":
         array_spec = coerce_spec(array_spec)
-        ev = evolve_codecs(self.codecs, array_spec)
+        codecs = self.codecs
+        if self._aux.get("v2"):
+            # zarr v2 (V2Codec): the raw chunk is the array in the spec's order
+            # (_v2.py:66-68); F order is the v3 chain with a reversing transpose
+            if array_spec.dtype.byteorder == ">":
+                raise NotImplementedError("zarr v2 big-endian dtypes")
+            if array_spec.order == "F" and array_spec.ndim > 1:
+                codecs = (TransposeCodec(order=tuple(reversed(range(array_spec.ndim)))),) + codecs
+        ev = evolve_codecs(codecs, array_spec)
         aa, ab, bb = split_codecs(ev)
         return type(self)(ev, aa, ab, bb, self.batch_size, self.predict_loads)
 
