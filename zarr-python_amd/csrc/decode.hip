@@ -494,6 +494,7 @@ KernelFn select_duo_kernel(bool crc, int item, bool swap);           // decode_r
 KernelFn select_il_kernel(bool crc, int item, bool swap);            // decode_rows.hip
 KernelFn select_il_kernel_lean(bool crc, int item, bool swap);       // decode_rows.hip
 KernelFn select_il_kernel_cf(bool crc, int item, bool swap);         // decode_rows.hip
+KernelFn select_il_kernel_regmul(bool crc, int item, bool swap, bool occ6);  // decode_rows.hip
 KernelFn select_xw_kernel(bool crc, int item, bool swap);            // decode_rows.hip
 KernelFn select_tile4_kernel(bool crc, int item, bool swap);         // decode_tile.hip
 KernelFn select_tileg_kernel(bool crc, int item, bool swap);         // decode_tile.hip
@@ -549,7 +550,9 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
         if (il) {
             KernelFn ifn = (p.tune & kTuneCfLookup) ? select_il_kernel_cf(crc, p.g.itemsize, swap)
                            : (p.tune & kTuneIlLean) ? select_il_kernel_lean(crc, p.g.itemsize, swap)
-                                                    : select_il_kernel(crc, p.g.itemsize, swap);
+                           : (p.tune & (kTuneIlRegMul | kTuneIlOcc6))
+                               ? select_il_kernel_regmul(crc, p.g.itemsize, swap, (p.tune & kTuneIlOcc6) != 0)
+                               : select_il_kernel(crc, p.g.itemsize, swap);
             if (!ifn) return ZHIP_E_UNSUPPORTED;
             const uint32_t igrid = p.n_units > p.n_idx ? p.n_units : p.n_idx;
             if (igrid == 0) return ZHIP_OK;

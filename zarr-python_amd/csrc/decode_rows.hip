@@ -521,6 +521,21 @@ __device__ __forceinline__ uint32_t lanemul3(const uint32_t* s_mul, int t, uint3
     return (q >> 2) ^ r2(q & 3u) ^ m[10];
 }
 
+// lanemul3 with the lane's 8 + 4 window products selected in registers from
+// k, kx, kx^2 (no LDS column): ~130 VALU instructions once per run end instead
+// of 11 LDS reads, and 12 KiB less LDS per workgroup (k_decode_il arm LM = 1/2).
+__device__ __forceinline__ uint32_t lanemul_reg(uint32_t k, uint32_t a) {
+    const uint32_t k1 = mulx1(k), k2 = mulx1(k1);
+    auto sel3 = [&](uint32_t w) {
+        return (k & (0u - ((w >> 2) & 1u))) ^ (k1 & (0u - ((w >> 1) & 1u))) ^ (k2 & (0u - (w & 1u)));
+    };
+    uint32_t q = sel3(a & 7u);
+#pragma unroll
+    for (int j = 1; j < 10; ++j) q = (q >> 3) ^ r3(q & 7u) ^ sel3((a >> (3 * j)) & 7u);
+    const uint32_t w = a >> 30;
+    return (q >> 2) ^ r2(q & 3u) ^ (k & (0u - ((w >> 1) & 1u))) ^ (k1 & (0u - (w & 1u)));
+}
+
 // Shard-index CRC check by one workgroup with the pair tables (verify_index's
 // chain, four accumulators, folded, shifted by kthread11).
 // (`active` false: a second half-workgroup that only joins the barriers)
@@ -1170,11 +1185,15 @@ __device__ __forceinline__ void publish_il(const DecodeParams& p, uint32_t c, ui
 // headline than the production order (data loads after the resolved header:
 // the tables, L2 hits, are in LDS before the data flood;
 // profiles/r03/lean/).
-template <bool CRC, int ITEM, bool SWAP, bool LEAN = false, bool CF = false>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_decode_il(const DecodeParams p) {
+// LM (arms kTuneIlRegMul / kTuneIlOcc6): 0 = lane multiply from the LDS
+// column (production); 1 = in registers (lanemul_reg), 4 workgroups per CU;
+// 2 = in registers with 24 KiB of LDS and 6 workgroups per CU.
+template <bool CRC, int ITEM, bool SWAP, bool LEAN = false, bool CF = false, int LM = 0>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(LM == 2 ? 6 : 4, LM == 2 ? 6 : 4)))
+void k_decode_il(const DecodeParams p) {
     constexpr int K = kDefaultBlocks;
     __shared__ uint32_t s_tab[CRC ? kPairTabWords : 1];
-    __shared__ uint32_t s_mul[CRC ? 12 * kThreads : 1];
+    __shared__ uint32_t s_mul[CRC && LM == 0 ? 12 * kThreads : 1];
     __shared__ uint32_t s_red[2][kThreads / 64];
     const int t = threadIdx.x;
     const uint32_t G = gridDim.x, g = blockIdx.x;
@@ -1316,7 +1335,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))
         stt[t + 3 * kThreads] = tv3;
         stt[t + 4 * kThreads] = tv4;
         stt[t + 5 * kThreads] = tv5;
-        lanemul3_init(s_mul, t, kl);
+        if constexpr (LM == 0) lanemul3_init(s_mul, t, kl);
         __syncthreads();
     }
     if (has) {
@@ -1343,7 +1362,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))
         // 4. run end: one chain per workgroup, one publication
         if constexpr (CRC) {
             uint32_t v = ok ? ((p.tune & kTuneNoRunEnd) ? acc.a0 ^ acc.a1 ^ acc.a2 ^ acc.a3  // timing arm
-                                                         : lanemul3(s_mul, t, fold4(s_tab, acc)))
+                               : LM == 0 ? lanemul3(s_mul, t, fold4(s_tab, acc))
+                                         : lanemul_reg(kl, fold4(s_tab, acc)))
                             : 0u;
             v = wave_xor(v);
             if ((t & 63) == 0) s_red[0][t >> 6] = v;
@@ -1367,6 +1387,11 @@ KernelFn select_il_kernel_lean(bool crc, int item, bool swap) {  // kTuneIlLean 
 
 KernelFn select_il_kernel_cf(bool crc, int item, bool swap) {  // kTuneCfLookup timing arm (results invalid)
     return (crc && item == 4 && !swap) ? k_decode_il<true, 4, false, false, true> : nullptr;
+}
+
+KernelFn select_il_kernel_regmul(bool crc, int item, bool swap, bool occ6) {  // kTuneIlRegMul / kTuneIlOcc6 arms
+    if (!(crc && item == 4 && !swap)) return nullptr;
+    return occ6 ? k_decode_il<true, 4, false, false, false, 2> : k_decode_il<true, 4, false, false, false, 1>;
 }
 
 KernelFn select_il_kernel(bool crc, int item, bool swap) {

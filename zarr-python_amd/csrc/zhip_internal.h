@@ -216,6 +216,8 @@ constexpr uint32_t kTuneXw = 268435456u;      // whole-row layouts: k_decode_xw 
 constexpr uint32_t kTuneNoXw = 536870912u;    // whole-row layouts: never k_decode_xw
 constexpr uint32_t kTuneNoPub = 1073741824u;  // timing arm: k_decode_il / k_decode_xw skip the CRC publication
 constexpr uint32_t kTuneIlLean = 16384u;    // k_decode_il arm: lean predicted prologue (data loads before the header chain)
+constexpr uint32_t kTuneIlRegMul = 32u;      // k_decode_il arm: lane multiply in registers (no LDS column)
+constexpr uint32_t kTuneIlOcc6 = 4194304u;   // k_decode_il arm: register lane multiply, 6 workgroups per CU
 constexpr uint32_t kTuneCfLookup = 131072u;  // k_decode_il timing arm: conflict-free lookup addresses (results invalid)
 constexpr uint32_t kTuneStamp = 1024u;    // k_decode_pair: per-workgroup phase timestamps (zhip_debug_stamps)
 constexpr uint32_t kStampWG = 8192u;      // workgroups stamped per launch
