@@ -1243,6 +1243,8 @@ void k_decode_il(const DecodeParams p) {
             if (has) U = resolve_unit(p, c * h.nseg, expected);
             ok = has && U.mode == ZHIP_ST_OK;
             if (ok && U.cp != cpp) {  // a wrong guess: reload from the live index, full drain
+                // (diagnostics: counted in the last stamp slot, zhip_debug_stamps)
+                if (t == 0) atomicAdd(reinterpret_cast<unsigned long long*>(&g_stamps[kStampWG * kStampSlots - 1]), 1ull);
 #pragma unroll
                 for (int k = 0; k < K; ++k) {
                     const int32_t base = lo_frame + kWgStride * (int32_t)(st0 + S * (uint32_t)k);
