@@ -405,6 +405,34 @@ def test_transpose_tile4_crc_mismatch(device):
     with pytest.raises(ValueError) as got:
         arr[...]
     assert str(got.value) == str(want.value)
+    from zarr_hip import _native as N
+
+    N.lib().zhip_set_tuning(2, -(1 << 31))  # the same mismatch through the k_decode_tile4f arm
+    try:
+        with pytest.raises(ValueError) as got_f:
+            zarr_hip.Array.create(store, (128, 64, 64), (64, 64, 64), "float32", 0.0, codecs=codecs)[...]
+        assert N.lib().zhip_last_kernel() == b"k_decode_tile4f"
+    finally:
+        N.lib().zhip_set_tuning(2, 0)
+    assert str(got_f.value) == str(want.value)
+
+
+@pytest.mark.parametrize("dtype,endian,chunks,shape", TILE4_CASES)
+def test_transpose_tile4f_chain(device, dtype, endian, chunks, shape):
+    """The k_decode_tile4f arm (kTuneTile4F, bit 31: the four tiles of a
+    workgroup are 1 KiB of every stored row, one A_64 chain per thread) decodes
+    exactly what the oracle wrote; without the bit k_decode_tile4 runs."""
+    from zarr_hip import _native as N
+
+    _roundtrip(device, shape, chunks, dtype, [T((2, 1, 0)), endian, CRC])
+    assert N.lib().zhip_last_kernel() == b"k_decode_tile4"
+    N.lib().zhip_set_tuning(2, -(1 << 31))
+    try:
+        # every case: 256-byte stored rows, one 64-row tile along the transposed dim
+        _roundtrip(device, shape, chunks, dtype, [T((2, 1, 0)), endian, CRC])
+        assert N.lib().zhip_last_kernel() == b"k_decode_tile4f"
+    finally:
+        N.lib().zhip_set_tuning(2, 0)
 
 
 def test_tile_mode_engaged(device):

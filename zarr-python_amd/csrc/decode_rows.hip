@@ -447,21 +447,9 @@ __device__ __forceinline__ uint32_t crc_block(const uint32_t* s_tab, uint32_t ac
 // into one state with the A4 byte tables, a3 ^ A4(a2 ^ A4(a1 ^ A4(a0))), which
 // sits 12 bytes after the single-chain state of the other kernels; the lane
 // constants kpair11 / kthread11 carry the x^(-96) that undoes it.  (The CPU
-// emulation zhip_emulate_chunk_crc_pair checks this decomposition.)
-struct Acc4 {
-    uint32_t a0, a1, a2, a3;
-};
-
-__device__ __forceinline__ uint32_t t11(const uint32_t* s, uint32_t w) {
-    return s[kPairT1 + (w & 2047u)] ^ s[kPairT2 + ((w >> 11) & 2047u)] ^ s[kPairT3 + (w >> 22)];
-}
-
-__device__ __forceinline__ void crc_block4(const uint32_t* s, Acc4& a, const uint4 v) {
-    a.a0 = t11(s, a.a0 ^ v.x);
-    a.a1 = t11(s, a.a1 ^ v.y);
-    a.a2 = t11(s, a.a2 ^ v.z);
-    a.a3 = t11(s, a.a3 ^ v.w);
-}
+// emulation zhip_emulate_chunk_crc_pair checks this decomposition.)  The step
+// (Acc4, t11, crc_block4, fold4) lives in zhip_decode_common.h, shared with
+// k_decode_tile4f.
 
 // Timing arm (kTuneCfLookup): the same three lookups per word at addresses
 // whose bank is the lane's own (index bits << 5 | lane % 32), so no ds_read_b32
@@ -479,28 +467,8 @@ __device__ __forceinline__ void crc_block4_cf(const uint32_t* s, Acc4& a, const 
     a.a3 = t11_cf(s, a.a3 ^ v.w, ln);
 }
 
-__device__ __forceinline__ uint32_t fold4(const uint32_t* s, const Acc4& a) {
-    const uint32_t* t4 = s + kPairA4;
-    return tab_apply(t4, tab_apply(t4, tab_apply(t4, a.a0) ^ a.a1) ^ a.a2) ^ a.a3;
-}
-
-// Per-lane multiply by the lane's constant k from a 12-entry LDS column: 3-bit
-// windows of the operand (bits 0..29, entries 0..7) and a 2-bit top window
-// (bits 30..31, entries 8..11); Horner over the windows with x^3 / x^2 steps
-// whose reductions are VALU.  12 KiB for 256 lanes (the 4-bit form needs 16).
-constexpr uint32_t rbasis(uint32_t n, int steps) {
-    for (int i = 0; i < steps; ++i) n = (n >> 1) ^ (kPoly & (0u - (n & 1u)));
-    return n;
-}
-
-__device__ __forceinline__ uint32_t r3(uint32_t n) {
-    return ((n & 1u) ? rbasis(1, 3) : 0u) ^ ((n & 2u) ? rbasis(2, 3) : 0u) ^ ((n & 4u) ? rbasis(4, 3) : 0u);
-}
-
-__device__ __forceinline__ uint32_t r2(uint32_t n) {
-    return ((n & 1u) ? rbasis(1, 2) : 0u) ^ ((n & 2u) ? rbasis(2, 2) : 0u);
-}
-
+// The lane's 12-entry window column of k in LDS (12 KiB for 256 lanes; the
+// 4-bit form needs 16), and the multiply over it (windows: zhip_decode_common.h).
 __device__ __forceinline__ void lanemul3_init(uint32_t* s_mul, int t, uint32_t k) {
     const uint32_t k1 = mulx1(k), k2 = mulx1(k1);
 #pragma unroll
@@ -521,20 +489,6 @@ __device__ __forceinline__ uint32_t lanemul3(const uint32_t* s_mul, int t, uint3
     return (q >> 2) ^ r2(q & 3u) ^ m[10];
 }
 
-// lanemul3 with the lane's 8 + 4 window products selected in registers from
-// k, kx, kx^2 (no LDS column): ~130 VALU instructions once per run end instead
-// of 11 LDS reads, and 12 KiB less LDS per workgroup (k_decode_il arm LM = 1/2).
-__device__ __forceinline__ uint32_t lanemul_reg(uint32_t k, uint32_t a) {
-    const uint32_t k1 = mulx1(k), k2 = mulx1(k1);
-    auto sel3 = [&](uint32_t w) {
-        return (k & (0u - ((w >> 2) & 1u))) ^ (k1 & (0u - ((w >> 1) & 1u))) ^ (k2 & (0u - (w & 1u)));
-    };
-    uint32_t q = sel3(a & 7u);
-#pragma unroll
-    for (int j = 1; j < 10; ++j) q = (q >> 3) ^ r3(q & 7u) ^ sel3((a >> (3 * j)) & 7u);
-    const uint32_t w = a >> 30;
-    return (q >> 2) ^ r2(q & 3u) ^ (k & (0u - ((w >> 1) & 1u))) ^ (k1 & (0u - (w & 1u)));
-}
 
 // Shard-index CRC check by one workgroup with the pair tables (verify_index's
 // chain, four accumulators, folded, shifted by kthread11).

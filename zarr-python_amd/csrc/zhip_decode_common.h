@@ -306,4 +306,59 @@ __device__ __forceinline__ void retire(const DecodeParams& p, Pending& q, uint64
     }
 }
 
+// ---- the pair kernel's CRC step (k_decode_pair / k_decode_il / k_decode_tile4f;
+// tables in the kPairTab* layout, built by capi.cpp build_pair_tables) ----
+struct Acc4 {
+    uint32_t a0, a1, a2, a3;
+};
+
+__device__ __forceinline__ uint32_t t11(const uint32_t* s, uint32_t w) {
+    return s[kPairT1 + (w & 2047u)] ^ s[kPairT2 + ((w >> 11) & 2047u)] ^ s[kPairT3 + (w >> 22)];
+}
+
+__device__ __forceinline__ void crc_block4(const uint32_t* s, Acc4& a, const uint4 v) {
+    a.a0 = t11(s, a.a0 ^ v.x);
+    a.a1 = t11(s, a.a1 ^ v.y);
+    a.a2 = t11(s, a.a2 ^ v.z);
+    a.a3 = t11(s, a.a3 ^ v.w);
+}
+
+__device__ __forceinline__ uint32_t fold4(const uint32_t* s, const Acc4& a) {
+    const uint32_t* t4 = s + kPairA4;
+    return tab_apply(t4, tab_apply(t4, tab_apply(t4, a.a0) ^ a.a1) ^ a.a2) ^ a.a3;
+}
+
+// Per-lane multiply by a lane constant k over 3-bit windows of the operand
+// (bits 0..29) and a 2-bit top window (bits 30..31), Horner over the windows
+// with x^3 / x^2 steps whose reductions (r3 / r2) are VALU; the window products
+// come from a 12-entry LDS column (lanemul3, decode_rows.hip) or from
+// registers (lanemul_reg).
+constexpr uint32_t rbasis(uint32_t n, int steps) {
+    for (int i = 0; i < steps; ++i) n = (n >> 1) ^ (kPoly & (0u - (n & 1u)));
+    return n;
+}
+
+__device__ __forceinline__ uint32_t r3(uint32_t n) {
+    return ((n & 1u) ? rbasis(1, 3) : 0u) ^ ((n & 2u) ? rbasis(2, 3) : 0u) ^ ((n & 4u) ? rbasis(4, 3) : 0u);
+}
+
+__device__ __forceinline__ uint32_t r2(uint32_t n) {
+    return ((n & 1u) ? rbasis(1, 2) : 0u) ^ ((n & 2u) ? rbasis(2, 2) : 0u);
+}
+
+// The window products selected in registers from k, kx, kx^2 (no LDS column):
+// ~130 VALU instructions once per run end instead of 11 LDS reads
+// (k_decode_il arms LM = 1 / 2, k_decode_tile4f).
+__device__ __forceinline__ uint32_t lanemul_reg(uint32_t k, uint32_t a) {
+    const uint32_t k1 = mulx1_u(k), k2 = mulx1_u(k1);
+    auto sel3 = [&](uint32_t w) {
+        return (k & (0u - ((w >> 2) & 1u))) ^ (k1 & (0u - ((w >> 1) & 1u))) ^ (k2 & (0u - (w & 1u)));
+    };
+    uint32_t q = sel3(a & 7u);
+#pragma unroll
+    for (int j = 1; j < 10; ++j) q = (q >> 3) ^ r3(q & 7u) ^ sel3((a >> (3 * j)) & 7u);
+    const uint32_t w = a >> 30;
+    return (q >> 2) ^ r2(q & 3u) ^ (k & (0u - ((w >> 1) & 1u))) ^ (k1 & (0u - (w & 1u)));
+}
+
 }  // namespace zhip

@@ -106,6 +106,9 @@ struct DecodeParams {
     const uint32_t* tz;
     const uint32_t* kq4;
     const struct TileEnt* tmap;
+    // k_decode_tile4f (non-null: the layout qualifies): A_64 pair tables, lane constants
+    const uint32_t* t4f_tab;
+    const uint32_t* t4f_kq;
     // k_decode_tileg (tileg != 0): group map, step multiply table, steps
     uint32_t tileg;
     const struct GroupEnt* gmap;
@@ -216,6 +219,7 @@ constexpr uint32_t kTuneXw = 268435456u;      // whole-row layouts: k_decode_xw 
 constexpr uint32_t kTuneNoXw = 536870912u;    // whole-row layouts: never k_decode_xw
 constexpr uint32_t kTuneNoPub = 1073741824u;  // timing arm: k_decode_il / k_decode_xw skip the CRC publication
 constexpr uint32_t kTuneIlLean = 16384u;    // k_decode_il arm: lean predicted prologue (data loads before the header chain)
+constexpr uint32_t kTuneTile4F = 2147483648u;   // transposed layouts arm: k_decode_tile4f where the layout admits it
 constexpr uint32_t kTuneIlRegMul = 32u;      // k_decode_il arm: lane multiply in registers (no LDS column)
 constexpr uint32_t kTuneIlOcc6 = 4194304u;   // k_decode_il arm: register lane multiply, 6 workgroups per CU
 constexpr uint32_t kTuneCfLookup = 131072u;  // k_decode_il timing arm: conflict-free lookup addresses (results invalid)
@@ -330,6 +334,10 @@ struct zhip_plan {
     uint32_t tile4;
     uint64_t tile4_step;                                 // base step between consecutive tiles
     uint64_t tile4_off_tz, tile4_off_kq, tile4_off_map;  // u32 offsets in d_tile_tables
+    // k_decode_tile4f (tile step 256 B, CRC): A_64 tables in the kPairTab*
+    // layout | lane constants [T/4][kThreads], at tile4f_off in d_tile_tables
+    uint32_t tile4f;
+    uint64_t tile4f_off;
     // k_encode_tileg (full selections): tiles grouped by four along the
     // innermost other stored dim gd with shape[gd] % 4 == 0 (uniform step
     // sstride[gd] inside every group, whatever the natural tile order); tables
