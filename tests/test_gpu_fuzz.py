@@ -7,6 +7,8 @@ array and two random selections.  The store's bytes are compared with the
 oracle's after every write, and every read as raw bytes -- through whichever
 kernels the planner picks for that geometry."""
 
+import os
+
 import numpy as np
 import pytest
 
@@ -76,7 +78,13 @@ def _case(seed):
     return rng, shape, chunks, dtype, codecs, fill
 
 
-@pytest.mark.parametrize("seed", range(160))
+# ZARR_HIP_FUZZ_FIRST / ZARR_HIP_FUZZ_SEEDS widen the sweep for stress runs
+# (profiles/r03/fuzz_stress.log); the default suite runs seeds 0..159
+_FIRST = int(os.environ.get("ZARR_HIP_FUZZ_FIRST", "0"))
+_SEEDS = int(os.environ.get("ZARR_HIP_FUZZ_SEEDS", "160"))
+
+
+@pytest.mark.parametrize("seed", range(_FIRST, _FIRST + _SEEDS))
 def test_random_roundtrip(device, seed):
     import zarr_hip
     from zarr_hip.spec import ArrayConfig
