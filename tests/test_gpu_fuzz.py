@@ -127,7 +127,10 @@ def test_random_roundtrip(device, seed):
         assert got.tobytes() == np.ascontiguousarray(want).tobytes(), (sel, shape, chunks, codecs)
 
 
-@pytest.mark.parametrize("seed", range(8))
+_LARGE = int(os.environ.get("ZARR_HIP_FUZZ_LARGE", "8"))
+
+
+@pytest.mark.parametrize("seed", range(_LARGE))
 def test_random_host_reads_large(device, tmp_path, seed):
     """Host-sourced reads big enough for the slab pipeline (>= 16 MiB outs):
     random chunking (sharded or not, transposed or not), host stores of the
