@@ -130,6 +130,33 @@ def test_compressed_crc_mismatch_message(device):
     assert str(got.value) == str(want.value)
 
 
+@pytest.mark.parametrize("where", ["offset", "crc"])
+def test_sharded_compressed_corrupt_index_message(where, device):
+    """A corrupted shard index in front of compressed inner chunks raises the
+    reference's checksum message (the index CRC is checked before its
+    offsets drive the host decompression, as _decode_shard_index_sync does,
+    sharding.py:624-631), not the decompressor's error."""
+    import zarr_hip
+
+    inner = [LE, GZ(1)]
+    shape, shards, ichunks = (40, 36), (20, 36), (10, 12)
+    meta = O.ArrayMeta(shape, shards, np.dtype("float32"), 0.0, codecs=[SHARD(ichunks, inner)])
+    host: dict = {}
+    O.write(host, meta, (Ellipsis,), _data(shape, "float32"))
+    bad = bytearray(host["c/1/0"])
+    isz = 16 * 6 + 4  # 2 x 3 inner chunks per shard
+    bad[len(bad) - isz + (3 if where == "offset" else isz - 3)] ^= 0x40  # an offset byte / the CRC
+    host["c/1/0"] = bytes(bad)
+    with pytest.raises(ValueError) as want:
+        O.read(host, meta)
+    arr = zarr_hip.Array.create(zarr_hip.MemoryStore(dict(host)), shape, ichunks, "float32", 0.0,
+                                shards=shards, inner_codecs=inner)
+    with pytest.raises(ValueError) as got:
+        arr[...]
+    assert str(got.value) == str(want.value)
+    assert str(got.value).startswith("Stored and computed checksum do not match")
+
+
 def _zarr_batch(meta_shape, chunk_shape, sel, store, dtype, fill, prototype=None):
     spec = Z.ArraySpec(tuple(chunk_shape), Z.ZDType(dtype), fill, Z.ArrayConfig(), prototype or Z.cpu_prototype)
     return Z.batch_for(meta_shape, chunk_shape, sel, store, spec)

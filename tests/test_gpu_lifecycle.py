@@ -172,6 +172,37 @@ def test_cached_read_sees_overwrite_and_delete(device, sharded):
     assert out2.cpu().numpy().tobytes() == O.read(host, meta).tobytes()
 
 
+def test_cached_read_new_store_same_keys(device):
+    """One pipeline reads store A, A is dropped, store B with different bytes
+    at the same keys is read through the same pipeline: the result is B's
+    (the cache keys on the store object, not its address), and A's program
+    -- holding A's HBM arena -- leaves the cache."""
+    import gc
+
+    import torch
+
+    import zarr_hip
+
+    shape, chunks = (64, 64, 64), (32, 32, 32)
+    arr, store, host, meta = _device_array(device, shape, chunks, [LE, CRC])
+    pipe = arr.codec_pipeline
+    batch, _ = arr.batch_info((Ellipsis,))
+    out = torch.empty(shape, dtype=torch.float32, device=device)
+    pipe.read_sync(batch, out)
+    assert len(pipe._read_cache) == 1
+    for _round in range(3):
+        host2 = {}
+        O.write(host2, meta, (Ellipsis,), _data(shape, "float32", seed=11 + _round))
+        del arr, store, batch
+        gc.collect()
+        store = zarr_hip.DeviceStore.from_host(host2, device)
+        arr = zarr_hip.Array.create(store, shape, chunks, "float32", 0.0, codecs=[LE, CRC])
+        batch, _ = arr.batch_info((Ellipsis,))
+        pipe.read_sync(batch, out)
+        assert out.cpu().numpy().tobytes() == O.read(host2, meta).tobytes()
+        assert len(pipe._read_cache) == 1  # the dead store's program was dropped
+
+
 def test_cached_read_crc_error_then_recovery(device):
     """A cached program re-verifies every CRC: bytes corrupted in HBM after
     the first read raise the reference's message, restored bytes read clean."""

@@ -659,8 +659,7 @@ int zhip_decode_mapped(const zhip_plan* plan, const void* src, uint64_t src_size
         // inner chunks without a CRC: only the mapped pair decode carries the
         // index checks (k_decode_lead, leading workgroups)
         const bool lead_ok = d_rowmap && (decode_flags & ZHIP_DF_ROWS) && (decode_flags & ZHIP_DF_FAST_ROWS) &&
-                             plan->nseg <= 32u && plan->seg == (uint32_t)kWgStride * kDefaultBlocks &&
-                             !(g_tune_bits & zhip::kTunePersist);
+                             plan->nseg <= 32u && plan->seg == (uint32_t)kWgStride * kDefaultBlocks;
         if (!(plan->layout.flags & ZHIP_LF_SHARDED) || (!(plan->layout.flags & ZHIP_LF_CRC) && !lead_ok) ||
             (decode_flags & ZHIP_DF_TILE) || plan->idx_nbytes == 0)
             return set_err(ZHIP_E_UNSUPPORTED, "index check cannot be fused for this plan");

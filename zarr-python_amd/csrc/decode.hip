@@ -506,7 +506,11 @@ static const char* g_last_kernel = "";
 
 int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
     if (g_tune_max_grid > 0) max_grid = g_tune_max_grid;
-    if (p.rows && p.rowmap && p.seg == (uint32_t)kWgStride * kDefaultBlocks && !(p.tune & kTunePersist)) {
+    // (the kTunePersist arm never applies to a launch carrying fused index
+    // checks of CRC-free inner chunks: only k_decode_lead carries those)
+    const bool lead_launch = !(p.lflags & ZHIP_LF_CRC) && p.n_idx != 0;
+    if (p.rows && p.rowmap && p.seg == (uint32_t)kWgStride * kDefaultBlocks &&
+        (!(p.tune & kTunePersist) || lead_launch)) {
         // one workgroup per pair of units, non-persistent (k_decode_pair)
         const int nu = (p.tune & kTuneSingle) ? 1 : 2;
         const bool crc = (p.lflags & ZHIP_LF_CRC) != 0, swap = (p.lflags & ZHIP_LF_SWAP) != 0;

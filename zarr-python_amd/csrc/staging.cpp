@@ -447,7 +447,9 @@ int zhip_host_copy(void* dst, const void* src, uint64_t nbytes, uint32_t nthread
             const uint64_t i = next.fetch_add(1);
             if (i >= n) return;
             const uint64_t a = i * piece, b = a + piece < nbytes ? a + piece : nbytes;
-            copy_bytes(static_cast<uint8_t*>(dst) + a, static_cast<const uint8_t*>(src) + a, b - a);
+            // plain memcpy: the CPU reads the caller's array next, so the lines
+            // stay cached (streaming stores serve the DMA packing direction)
+            std::memcpy(static_cast<uint8_t*>(dst) + a, static_cast<const uint8_t*>(src) + a, b - a);
         }
     };
     const uint32_t nt = nthreads == 0 ? 1u : (nthreads > 64 ? 64u : nthreads);

@@ -47,6 +47,7 @@ class BytesCodec:
 
     endian: str | None = sys.byteorder
     is_fixed_size = True
+    kind = "AB"
 
     def __post_init__(self):
         if self.endian is not None and self.endian not in ("little", "big"):
@@ -93,6 +94,7 @@ class Crc32cCodec:
     """crc32c_.py:20-78: 4-byte little-endian CRC-32C trailer."""
 
     is_fixed_size = True
+    kind = "BB"
 
     @classmethod
     def from_dict(cls, data: Any) -> "Crc32cCodec":
@@ -121,6 +123,7 @@ class TransposeCodec:
 
     order: tuple[int, ...]
     is_fixed_size = True
+    kind = "AA"
 
     def __post_init__(self):
         object.__setattr__(self, "order", tuple(int(i) for i in self.order))
@@ -170,6 +173,7 @@ class ShardingCodec:
     index_location: str = "end"
     subchunk_write_order: str = "morton"
     is_fixed_size = False
+    kind = "AB"
 
     def __post_init__(self):
         object.__setattr__(self, "chunk_shape", tuple(int(c) for c in self.chunk_shape))
@@ -252,6 +256,7 @@ class GzipCodec:
     level: int = 5
     is_fixed_size = False
     host = True
+    kind = "BB"
 
     def __post_init__(self):
         lv = self.level
@@ -344,6 +349,7 @@ class HostCodec:
     codec: Any
     is_fixed_size = False
     host = True
+    kind = "BB"
 
     def to_dict(self) -> dict:
         return self.codec.to_dict()
@@ -396,6 +402,50 @@ class HostCodec:
 
 
 @dataclass(frozen=True)
+class ForeignArrayCodec:
+    """A caller's array->array codec instance other than ``transpose`` (e.g. a
+    cast or scale filter).  The pipeline accepts it in a chain and threads the
+    chunk spec through it exactly as the reference does
+    (``evolve_from_array_spec`` forwards each codec's ``resolve_metadata``,
+    chunk_utils.py:18-40; regression test
+    tests/test_codec_pipeline.py:189-261), but its compute is not on the GPU
+    path: a read or write through such a chain raises NotImplementedError
+    (planner.analyze_chain)."""
+
+    codec: Any
+    is_fixed_size = True
+    kind = "AA"
+
+    def to_dict(self) -> dict:
+        return self.codec.to_dict()
+
+    @property
+    def name(self) -> str:
+        d = self.to_dict()
+        return d if isinstance(d, str) else d.get("name", type(self.codec).__name__)
+
+    def evolve_from_array_spec(self, spec: ArraySpec) -> "ForeignArrayCodec":
+        ev = getattr(self.codec, "evolve_from_array_spec", None)
+        if ev is None:
+            return self
+        new = ev(getattr(spec, "source", None) or spec)
+        return self if new is self.codec else ForeignArrayCodec(new)
+
+    def resolve_metadata(self, spec: ArraySpec) -> ArraySpec:
+        from .spec import coerce_spec
+
+        return coerce_spec(self.codec.resolve_metadata(getattr(spec, "source", None) or spec))
+
+    def compute_encoded_size(self, n: int, spec: ArraySpec | None = None) -> int:
+        return self.codec.compute_encoded_size(n, getattr(spec, "source", None) or spec)
+
+    def validate(self, **kw) -> None:
+        fn = getattr(self.codec, "validate", None)
+        if fn is not None:
+            fn(**kw)
+
+
+@dataclass(frozen=True)
 class V2Stage:
     """The host half of zarr v2's codec wrapper (V2Codec, src/zarr/codecs/_v2.py:
     19-96): the numcodecs compressor and filters the caller's V2Codec holds run
@@ -409,6 +459,7 @@ class V2Stage:
     compressor: Any
     is_fixed_size = False
     host = True
+    kind = "BB"
 
     def to_dict(self) -> dict:
         return {"name": "v2", "configuration": {"filters": [repr(f) for f in self.filters],
@@ -521,7 +572,8 @@ def parse_codecs(codecs) -> list:
     carried over from the instance."""
     out = []
     for c in codecs:
-        if isinstance(c, (BytesCodec, Crc32cCodec, TransposeCodec, ShardingCodec, GzipCodec, HostCodec, V2Stage)):
+        if isinstance(c, (BytesCodec, Crc32cCodec, TransposeCodec, ShardingCodec, GzipCodec, HostCodec, V2Stage,
+                          ForeignArrayCodec)):
             out.append(c)
             continue
         if is_v2_codec(c):  # zarr v2's filters + compressor wrapper (an ArrayBytesCodec)
@@ -529,6 +581,9 @@ def parse_codecs(codecs) -> list:
             continue
         conf = c.to_dict() if hasattr(c, "to_dict") and not isinstance(c, dict) else c
         name = conf if isinstance(conf, str) else conf["name"]
+        if name != "transpose" and not isinstance(c, (dict, str)) and codec_kind(c) == "AA":
+            out.append(ForeignArrayCodec(c))  # spec threading only; not on the GPU path
+            continue
         if name not in ("bytes", "crc32c", "transpose", "sharding_indexed") and not isinstance(c, (dict, str)) \
                 and hasattr(c, "_decode_sync") and hasattr(c, "_encode_sync"):
             # a compressor instance (zarr's GzipCodec / ZstdCodec / BloscCodec ...):
@@ -567,24 +622,58 @@ def evolve_codecs(codecs, spec: ArraySpec) -> tuple:
     return tuple(out)
 
 
+def codec_kind(c) -> str | None:
+    """"AA" / "AB" / "BB" for this package's codecs (their ``kind``) and for a
+    zarr Codec instance (its base class: ArrayArrayCodec / ArrayBytesCodec /
+    BytesBytesCodec, src/zarr/abc/codec.py:228-262, matched by name -- zarr is
+    not imported); None for anything else."""
+    k = getattr(c, "kind", None)
+    if k in ("AA", "AB", "BB"):
+        return k
+    for base in type(c).__mro__:
+        n = base.__name__
+        if n == "ArrayArrayCodec":
+            return "AA"
+        if n == "ArrayBytesCodec":
+            return "AB"
+        if n == "BytesBytesCodec":
+            return "BB"
+    return None
+
+
 def split_codecs(codecs) -> tuple[tuple, Any, tuple]:
-    """codecs_from_list (codec_pipeline.py:859-944): AA*, exactly one AB, BB*."""
+    """codecs_from_list_unchecked (codec_pipeline.py:886-944): one left-to-right
+    scan over adjacent pairs, so the first structural violation decides the
+    error -- an array->array codec after an array->bytes or bytes->bytes one,
+    an array->bytes codec right after a bytes->bytes one, and a bytes->bytes
+    codec right after an array->array one are TypeErrors; a second
+    array->bytes codec, or none at all, is a ValueError."""
     aa, ab, bb = [], None, []
+    prev = None
     for c in codecs:
-        if isinstance(c, TransposeCodec):
-            if ab is not None:
-                raise TypeError("ArrayArrayCodec must come before the ArrayBytesCodec")
+        k = codec_kind(c)
+        pk = None if prev is None else codec_kind(prev)
+        if k == "AA":
+            if pk in ("AB", "BB"):
+                raise TypeError(f"Invalid codec order. ArrayArrayCodec {c} must be preceded by another "
+                                f"ArrayArrayCodec. Got {type(prev)} instead.")
             aa.append(c)
-        elif isinstance(c, (BytesCodec, ShardingCodec)):
+        elif k == "AB":
+            if pk == "BB":
+                raise TypeError(f"Invalid codec order. ArrayBytes codec {c} must be preceded by an "
+                                f"ArrayArrayCodec. Got {type(prev)} instead.")
             if ab is not None:
-                raise ValueError("Only one ArrayBytesCodec is allowed.")
+                raise ValueError(f"Got two instances of ArrayBytesCodec: {ab} and {c}. "
+                                 "Only one array-to-bytes codec is allowed.")
             ab = c
-        elif isinstance(c, Crc32cCodec) or is_host_codec(c):
-            if ab is None:
-                raise TypeError("BytesBytesCodec must come after the ArrayBytesCodec")
+        elif k == "BB":
+            if pk == "AA":
+                raise TypeError(f"Invalid codec order. BytesBytesCodec {c} must be preceded by either "
+                                f"another BytesBytesCodec, or an ArrayBytesCodec. Got {type(prev)} instead.")
             bb.append(c)
         else:
-            raise NotImplementedError(type(c).__name__)
+            raise TypeError(f"not a codec: {c!r}")
+        prev = c
     if ab is None:
         raise ValueError("Required ArrayBytesCodec was not found.")
     return tuple(aa), ab, tuple(bb)

@@ -17,6 +17,9 @@ from __future__ import annotations
 
 import asyncio
 import os
+import threading
+import warnings
+import weakref
 from dataclasses import dataclass, field, replace
 from typing import Any, Iterable
 
@@ -418,8 +421,26 @@ def _read_key(batch: list, dev_out, drop_axes):
         cs, os_ = _sel_key(it[2]), _sel_key(it[3])
         if cs is None or os_ is None or it[1] is not spec and it[1] != spec:
             return None
-        parts.append((id(st), bg.path, cs, os_, bool(it[4])))
+        # the store enters by weak reference: a dead store's key never matches a
+        # new store that happens to reuse its address (dead weakrefs compare by
+        # identity), and _read_cached drops entries whose store died
+        parts.append((_store_ref(st), bg.path, cs, os_, bool(it[4])))
     return tuple(parts)
+
+
+def _store_ref(st):
+    r = getattr(st, "_zhip_wref", None)
+    if r is None or r() is not st:
+        r = weakref.ref(st)
+        try:
+            st._zhip_wref = r
+        except AttributeError:
+            pass
+    return r
+
+
+def _key_alive(key) -> bool:
+    return all(p[0]() is not None for p in key[11:])
 
 
 def _generations(batch: list) -> tuple:
@@ -433,6 +454,14 @@ def _generations(batch: list) -> tuple:
         if arena is not None and id(arena) not in seen:
             seen[id(arena)] = (arena, arena.gen)
     return tuple(seen.values())
+
+
+def _same_arenas(prog, batch: list) -> bool:
+    """The arenas a cached program was planned against are the batch's arenas
+    now (object identity, not addresses)."""
+    now = _generations(batch)
+    return len(now) == len(prog.generations) and all(
+        a is b for (a, _), (b, _) in zip(now, prog.generations))
 
 
 def _same_device(a, b) -> bool:
@@ -484,6 +513,10 @@ class HipCodecPipeline:
     def from_codecs(cls, codecs: Iterable, *, batch_size: int | None = None) -> "HipCodecPipeline":
         codecs = tuple(codecs)
         cl = tuple(parse_codecs(codecs))
+        if any(isinstance(c, ShardingCodec) for c in cl) and len(cl) > 1:
+            # codecs_from_list's advisory (codec_pipeline.py:859-883)
+            warnings.warn("Combining a `sharding_indexed` codec disables partial reads and writes, which "
+                          "may lead to inefficient performance.", UserWarning, stacklevel=2)
         aa, ab, bb = split_codecs(cl)
         p = cls(cl, aa, ab, bb, batch_size or (1 << 30))
         if any(is_v2_codec(c) for c in codecs):
@@ -796,11 +829,13 @@ class HipCodecPipeline:
         reference re-plans every read (codec_pipeline.py:1257-1319); its
         plans are Python objects, these are device tables."""
         cache = self._read_cache
+        lock = self._aux.setdefault("cache_lock", threading.Lock())
         # checked out while in use: a concurrent read of the same key (another
         # thread, another stream) plans its own program instead of sharing
         # this one's status and arrival workspace
-        prog = cache.pop(key, None)
-        if prog is not None and prog.stale():
+        with lock:
+            prog = cache.pop(key, None)
+        if prog is not None and (prog.stale() or not _same_arenas(prog, batch)):
             prog = None
         if prog is None:
             if not _device_resident(batch, dev_out.device):
@@ -812,9 +847,12 @@ class HipCodecPipeline:
             res = prog.results_fast()
         finally:
             prog.retarget(None)
-        while len(cache) >= READ_CACHE_SIZE:  # oldest first (insertion order = LRU)
-            cache.pop(next(iter(cache)), None)
-        cache[key] = prog
+        with lock:
+            for k in [k for k in cache if not _key_alive(k)]:  # stores gone: free their programs
+                del cache[k]
+            while len(cache) >= READ_CACHE_SIZE:  # oldest first (insertion order = LRU)
+                del cache[next(iter(cache))]
+            cache[key] = prog
         return res
 
     def _read_uncached(self, batch, dev_out, drop_axes) -> tuple[GetResult, ...]:

@@ -49,7 +49,9 @@ def analyze_chain(codecs, spec: ArraySpec) -> ChainInfo:
         raise NotImplementedError("only a single trailing crc32c bytes->bytes codec is supported")
     perm = tuple(range(spec.ndim))
     for t in aa:
-        assert isinstance(t, TransposeCodec)
+        if not isinstance(t, TransposeCodec):
+            raise NotImplementedError(f"array->array codec {getattr(t, 'name', t)!r} is not on the GPU path "
+                                      "(transpose is the only array->array codec it runs)")
         t.evolve_from_array_spec(ArraySpec(tuple(spec.shape[p] for p in perm), spec.dtype,
                                            spec.fill_value))
         perm = tuple(perm[t.order[i]] for i in range(len(perm)))

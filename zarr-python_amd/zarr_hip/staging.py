@@ -389,6 +389,19 @@ def gather_sharded_partial(batch: list, sh, cps, n_inner: int, inner_shape, spec
         if len(raw) < isz:
             raise ValueError("shard blob is shorter than its index")
         idx = np.frombuffer(raw, dtype="<u8", count=2 * n_inner).reshape(n_inner, 2)
+        if inner_decode is not None and sh.index_has_crc:
+            # the offsets drive host decompression before the GPU sees the
+            # index: verify it here first, as _decode_shard_index_sync does
+            # (sharding.py:624-631), so a corrupted index raises the checksum
+            # message, not the decompressor's error
+            from .hoststage import host_crc32c
+            from .pipeline import crc_error_message
+
+            body = np.frombuffer(raw, np.uint8, count=isz - 4)
+            stored = int(np.frombuffer(raw, "<u4", count=1, offset=isz - 4)[0])
+            computed = host_crc32c(body)
+            if stored != computed:
+                raise ValueError(crc_error_message(stored, computed))
         idx_off, _ = lay.add(raw) if sh.index_has_crc else (-1, 0)
         src_by = np.zeros(n_inner, np.int64)
         len_by = np.zeros(n_inner, np.int64)
