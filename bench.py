@@ -1007,6 +1007,46 @@ def headline_weak(ctx, args):
                        "kernel_ms / hbm_frac are this rank's")
 
 
+def free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return int(so.getsockname()[1])
+
+
+def launcher_cmd(argv: list, n: int, port: int) -> list:
+    """The torchrun command that runs this bench as n ranks on one node (the
+    driver's own form: --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def launch_ranks(n: int, argv: list, env=None) -> int:
+    """`python bench.py --gpus N` with no WORLD_SIZE in the environment: start
+    the N ranks as ONE child torchrun (nothing here has touched the GPU -- a
+    process that has must never exec another program on this pool) and
+    return its exit code; rank 0 of the child prints the JSON line."""
+    import subprocess
+
+    e = dict(os.environ if env is None else env)
+    e.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    log(f"[bench] launching {n} ranks: " + " ".join(launcher_cmd(argv, n, 0)[:6]))
+    return subprocess.call(launcher_cmd(argv, n, free_port()), env=e)
+
+
+def rank_plan(gpus: int, env) -> str:
+    """'launch' (start N ranks), 'run' (this process is a rank or the only
+    one) -- or ValueError when the launcher's world size disagrees with
+    --gpus."""
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        return "launch" if gpus > 1 else "run"
+    if int(ws) != gpus:
+        raise ValueError(f"--gpus {gpus} but WORLD_SIZE={ws}: launch with matching sizes")
+    return "run"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -1023,6 +1063,12 @@ def main():
                     help="extra configs (subset of c1,c2,c3,c4,c5,enc,e2e,call, or ''); c4/c5 run "
                          "partitioned at every N, the others at N=1")
     args = ap.parse_args()
+    if rank_plan(args.gpus, os.environ) == "launch":
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if os.environ.get("ZHIP_BENCH_DRY") == "1":  # launcher test hook (tests/test_bench_launcher.py)
+        if int(os.environ.get("RANK", "0")) == 0:
+            print(json.dumps({"n_gpus": int(os.environ.get("WORLD_SIZE", "1")), "gpus_arg": args.gpus}))
+        return
 
     import torch
 
