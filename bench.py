@@ -114,7 +114,7 @@ class Ctx:
         return self._reduce(x, self.dist.ReduceOp.SUM)
 
 
-def build_replica(device, data_dev, shape, chunks, codecs, shards=None):
+def build_replica(device, data_dev, shape, chunks, codecs, shards=None, dtype="float32", fill=0.0):
     """Encode a device array into a fresh DeviceStore with zarr_hip's own GPU
     encode path (setup, not timed)."""
     import torch
@@ -124,9 +124,9 @@ def build_replica(device, data_dev, shape, chunks, codecs, shards=None):
     n_enc = int(np.prod(shape)) * data_dev.element_size() * 1.02 + (1 << 24)
     store = zarr_hip.DeviceStore(device, capacity=int(n_enc))
     if shards is None:
-        arr = zarr_hip.Array.create(store, shape, chunks, "float32", 0.0, codecs=codecs)
+        arr = zarr_hip.Array.create(store, shape, chunks, dtype, fill, codecs=codecs)
     else:
-        arr = zarr_hip.Array.create(store, shape, chunks, "float32", 0.0, shards=shards,
+        arr = zarr_hip.Array.create(store, shape, chunks, dtype, fill, shards=shards,
                                     inner_codecs=codecs)
     arr.set((Ellipsis,), data_dev)
     torch.cuda.synchronize(device)
@@ -263,6 +263,9 @@ def extra_configs(ctx, args):
     # memory state), so they run while the process is fresh
     if single and "e2e" in args.extra:
         out["e2e_c2_host"] = e2e_host(ctx.device, args)
+        torch.cuda.empty_cache()
+    if single and "cpp" in args.extra:
+        out["cpp_example_4096"] = cpp_example(device, args)
         torch.cuda.empty_cache()
     if single and "c1" in args.extra:
         out["c1_1d_bytes"] = c1_plumbing(device, args)
@@ -840,6 +843,125 @@ def box_cores() -> int:
     return max(1, min(n, cap) if cap else n)
 
 
+def _median_s(fn, repeat=3):
+    ts = []
+    for _ in range(repeat):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    return float(np.median(ts))
+
+
+def cpp_example(device, args):
+    """extra.cpp_example_4096: the reference's own timing harness for this
+    boundary (examples/codec_pipeline_performance/codec_pipeline_performance.py:
+    67-80, 95-130) -- 4096^2 int32 (64 MiB), 16 shards of 1024^2, 256 inner
+    chunks of 64^2 (16 KiB, 256-byte rows) per shard, zarr's default sharding
+    codecs, compressors None (arange data) or gzip-6 (noisy data).
+
+    * device: the uncompressed array resident in HBM, one full decode per step
+      (one launch: 4096 inner chunks, 16 index CRCs), graph-timed;
+    * host: as the example does, the median of 3 full writes and of 3 full
+      reads through zarr_hip.Array on a MemoryStore and a LocalStore (host ->
+      HBM -> host; compression on the host stage);
+    * cpu_port: the oracle's restatement of FusedCodecPipeline's per-shard
+      pool map (codec_pipeline.py:1095-1172, 1174-1255) over the same bytes in
+      host memory, at 1 worker and at the box's worker share, write and read."""
+    import tempfile
+    from concurrent.futures import ThreadPoolExecutor
+
+    import torch
+
+    import zarr_hip
+    from oracle import oracle as O
+
+    g = W.CPP_EXAMPLE
+    shape, shards, inner = g["shape"], g["shards"], g["inner"]
+    res = {"workload": "4096^2 int32, 16 shards of 1024^2, 64^2 inner chunks (codec_pipeline_performance.py)"}
+    plain = W.cpp_example_data("plain")
+    noisy = W.cpp_example_data("noisy")
+    dec = plain.nbytes
+    n_inner = (shape[0] // inner[0]) * (shape[1] // inner[1])
+    # 1. device-resident decode of the uncompressed chain
+    data = torch.from_numpy(plain).to(device)
+    progs = []
+    for _ in range(args.replicas):
+        arr = build_replica(device, data, shape, inner, [LE], shards=shards, dtype="int32", fill=0)
+        progs.append(arr.prepare_read((Ellipsis,)))
+    progs[0][0].launch()
+    progs[0][0].results()
+    if not torch.equal(progs[0][1], data):
+        raise SystemExit("bench cpp_example: decoded bytes differ from the source")
+    wall, kern = time_programs([p for p, _ in progs], max(10, args.steps // 2), 3, device)
+    alg = 2 * dec + 16 * (256 * 16 + 4)
+    res["device_uncompressed"] = _entry(dec, alg, wall, kern, checked="bytes",
+                                        note=f"{n_inner} inner chunks of 16 KiB + 16 index CRCs per launch")
+    del progs, data, arr
+    torch.cuda.empty_cache()
+    # 2. host stores, full write + full read (the example's measure())
+    host = {}
+    with tempfile.TemporaryDirectory() as tmp:
+        for kind in ("memory", "local"):
+            for label, codecs, src in (("uncompressed", [LE], plain), ("gzip6", [LE, W.GZIP6], noisy)):
+                def mk(kind=kind, label=label):
+                    return zarr_hip.MemoryStore() if kind == "memory" else \
+                        zarr_hip.LocalStore(os.path.join(tmp, f"{kind}_{label}_{time.perf_counter_ns()}"))
+
+                holder = {}
+
+                def write_once(codecs=codecs, src=src, mk=mk, holder=holder):
+                    st = mk()
+                    a = zarr_hip.Array.create(st, shape, inner, "int32", 0, shards=shards, inner_codecs=codecs)
+                    a[...] = src
+                    holder["a"] = a
+
+                w = _median_s(write_once)
+                r = _median_s(lambda holder=holder: holder["a"][...])
+                if not np.array_equal(holder["a"][...], src):
+                    raise SystemExit(f"bench cpp_example: {kind}/{label} round trip mismatch")
+                host[f"{kind}_{label}"] = {"write_s": round(w, 4), "read_s": round(r, 4),
+                                           "write_GiBps": round(dec / w / GIB, 2),
+                                           "read_GiBps": round(dec / r / GIB, 2)}
+    res["host"] = host
+    # 3. the CPU port: per-shard pool map over the same bytes
+    workers = min(16, os.cpu_count() or 1)
+    port = {"workers": workers}
+    for label, codecs, src in (("uncompressed", [LE], plain), ("gzip6", [LE, W.GZIP6], noisy)):
+        meta = O.ArrayMeta(shape, shards, np.dtype("int32"), 0, codecs=[
+            {"name": "sharding_indexed", "configuration": {"chunk_shape": list(inner), "codecs": codecs,
+                                                           "index_location": "end"}}])
+        chain, spec = meta.chain, meta.spec()
+        grid = [(i, j) for i in range(shape[0] // shards[0]) for j in range(shape[1] // shards[1])]
+        store = {}
+
+        def enc(c, src=src, chain=chain, spec=spec, store=store):
+            sl = tuple(slice(x * s, (x + 1) * s) for x, s in zip(c, shards))
+            b = O.chain_encode(np.ascontiguousarray(src[sl]), chain, spec)
+            if b is not None:
+                store["c/%d/%d" % c] = bytes(b)
+
+        out = np.empty(shape, np.int32)
+
+        def decs(c, chain=chain, spec=spec, store=store, out=out):
+            sl = tuple(slice(x * s, (x + 1) * s) for x, s in zip(c, shards))
+            out[sl] = O.chain_decode(np.frombuffer(store["c/%d/%d" % c], np.uint8), chain, spec)
+
+        for nw in (1, workers):
+            with ThreadPoolExecutor(max_workers=nw) as pool:
+                t0 = time.perf_counter()
+                list(pool.map(enc, grid))
+                tw = time.perf_counter() - t0
+                t0 = time.perf_counter()
+                list(pool.map(decs, grid))
+                tr = time.perf_counter() - t0
+            if not np.array_equal(out, src):
+                raise SystemExit("bench cpp_example: cpu port round trip mismatch")
+            port[f"{label}_w{nw}"] = {"write_s": round(tw, 4), "read_s": round(tr, 4),
+                                      "read_GiBps": round(dec / tr / GIB, 2)}
+    res["cpu_port"] = port
+    return res
+
+
 def cpu_baseline(data_np, shape, chunks, shards, budget_s=12.0):
     """The reference's FusedCodecPipeline.read_sync restated on the host for the
     headline config (oracle port): one pool task per shard
@@ -1059,8 +1181,8 @@ def main():
     ap.add_argument("--eager", action="store_true",
                     help="time one host launch per step instead of a hipGraph replay")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
-    ap.add_argument("--extra", default="c1,c2,c3,c4,c5,enc,e2e,call",
-                    help="extra configs (subset of c1,c2,c3,c4,c5,enc,e2e,call, or ''); c4/c5 run "
+    ap.add_argument("--extra", default="c1,c2,c3,c4,c5,enc,e2e,call,cpp",
+                    help="extra configs (subset of c1,c2,c3,c4,c5,enc,e2e,call,cpp, or ''); c4/c5 run "
                          "partitioned at every N, the others at N=1")
     args = ap.parse_args()
     if rank_plan(args.gpus, os.environ) == "launch":

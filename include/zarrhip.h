@@ -270,6 +270,7 @@ int zhip_decode_mapped(const zhip_plan *plan, const void *src, uint64_t src_size
 #define ZHIP_TUNE_BLOCKS 3   /* blocks/thread per unit for plans created afterwards (4, 8, 16) */
 #define ZHIP_TUNE_STAGE_STREAMS 4  /* host staging: packed windows on 1 (default) or 2 copy streams */
 #define ZHIP_TUNE_STAGE_COPY 5     /* host copies into / out of pinned memory: 1 streaming stores (default), 0 memcpy */
+#define ZHIP_TUNE_ARM 6            /* experimental kernel variant for timing arms (0 = production) */
 int zhip_set_tuning(int key, int value);
 
 /* Name of the decode kernel the last zhip_decode* call on this process

@@ -22,6 +22,22 @@ CRC = {"name": "crc32c"}
 HEADLINE = dict(shape=(256, 256, 256), shards=(128, 128, 128), inner=(64, 64, 64), dtype="float32")
 C4 = dict(shape=(1024, 1024, 1024), shards=(128, 128, 128), inner=(32, 32, 32), dtype="float32")
 C5 = dict(shape=(2048, 2048, 2048), shards=(256, 256, 256), inner=(64, 64, 64), dtype="int16")
+# the reference's own timing harness for this boundary
+# (examples/codec_pipeline_performance/codec_pipeline_performance.py:67-80):
+# 4096^2 int32 = 64 MiB, 16 shards of 1024^2, 256 inner chunks of 64^2 each,
+# zarr's default sharding codecs (inner: bytes + the compressors, index:
+# bytes + crc32c at the end), compressors None or gzip-6, fill 0
+CPP_EXAMPLE = dict(shape=(4096, 4096), shards=(1024, 1024), inner=(64, 64), dtype="int32")
+GZIP6 = {"name": "gzip", "configuration": {"level": 6}}
+
+
+def cpp_example_data(kind: str) -> np.ndarray:
+    """The example's inputs (codec_pipeline_performance.py:149-156): `plain` =
+    arange (uncompressed runs), `noisy` = rng(0) integers in [0, 2**24) (gzip)."""
+    shape = CPP_EXAMPLE["shape"]
+    if kind == "plain":
+        return np.arange(int(np.prod(shape)), dtype=np.int32).reshape(shape)
+    return np.random.default_rng(0).integers(0, 2**24, size=shape, dtype=np.int32)
 
 
 def synthetic(shape, seed=0) -> np.ndarray:

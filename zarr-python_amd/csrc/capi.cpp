@@ -177,6 +177,7 @@ void fill_geom(Geom& g, const zhip_plan& plan) {
 
 uint32_t g_tune_bits = 0;
 int g_tune_blocks = 0;
+int g_tune_arm = 0;
 }
 
 extern "C" {
@@ -188,6 +189,7 @@ int zhip_set_tuning(int key, int value) {
         case ZHIP_TUNE_BLOCKS: g_tune_blocks = value; return ZHIP_OK;
         case ZHIP_TUNE_STAGE_STREAMS: zhip_stage_set_streams(value >= 2 ? 2u : 1u); return ZHIP_OK;
         case ZHIP_TUNE_STAGE_COPY: zhip_stage_set_copy(value ? 1u : 0u); return ZHIP_OK;
+        case ZHIP_TUNE_ARM: g_tune_arm = value; return ZHIP_OK;
         default: return set_err(ZHIP_E_INVALID, "unknown tuning key");
     }
 }

@@ -493,6 +493,8 @@ KernelFn select_pair_kernel(bool crc, int item, bool swap, int nu);  // decode_r
 KernelFn select_duo_kernel(bool crc, int item, bool swap);           // decode_rows.hip
 KernelFn select_il_kernel(bool crc, int item, bool swap);            // decode_rows.hip
 KernelFn select_il_kernel_lean(bool crc, int item, bool swap);       // decode_rows.hip
+KernelFn select_il_kernel_tuned(bool crc, int item, bool swap);      // decode_rows.hip
+KernelFn select_il_kernel_arm(bool crc, int item, bool swap, int arm);  // decode_rows.hip
 KernelFn select_il_kernel_cf(bool crc, int item, bool swap);         // decode_rows.hip
 KernelFn select_il_kernel_regmul(bool crc, int item, bool swap, bool occ6);  // decode_rows.hip
 KernelFn select_xw_kernel(bool crc, int item, bool swap);            // decode_rows.hip
@@ -553,11 +555,14 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
             return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
         }
         if (il) {
-            KernelFn ifn = (p.tune & kTuneCfLookup) ? select_il_kernel_cf(crc, p.g.itemsize, swap)
+            KernelFn ifn = g_tune_arm ? select_il_kernel_arm(crc, p.g.itemsize, swap, g_tune_arm)
+                           : (p.tune & kTuneCfLookup) ? select_il_kernel_cf(crc, p.g.itemsize, swap)
                            : (p.tune & kTuneIlLean) ? select_il_kernel_lean(crc, p.g.itemsize, swap)
                            : (p.tune & (kTuneIlRegMul | kTuneIlOcc6))
                                ? select_il_kernel_regmul(crc, p.g.itemsize, swap, (p.tune & kTuneIlOcc6) != 0)
-                               : select_il_kernel(crc, p.g.itemsize, swap);
+                               : (p.tune & (kTuneNoTables | kTuneNoRunEnd | kTuneNoPub))
+                                   ? select_il_kernel_tuned(crc, p.g.itemsize, swap)
+                                   : select_il_kernel(crc, p.g.itemsize, swap);
             if (!ifn) return ZHIP_E_UNSUPPORTED;
             const uint32_t igrid = p.n_units > p.n_idx ? p.n_units : p.n_idx;
             if (igrid == 0) return ZHIP_OK;

@@ -1142,7 +1142,13 @@ __device__ __forceinline__ void publish_il(const DecodeParams& p, uint32_t c, ui
 // LM (arms kTuneIlRegMul / kTuneIlOcc6): 0 = lane multiply from the LDS
 // column (production); 1 = in registers (lanemul_reg), 4 workgroups per CU;
 // 2 = in registers with 24 KiB of LDS and 6 workgroups per CU.
-template <bool CRC, int ITEM, bool SWAP, bool LEAN = false, bool CF = false, int LM = 0>
+// TUNE: the timing arms that read p.tune at run time (kTuneNoTables,
+// kTuneNoRunEnd, kTuneNoPub) are compiled in; the production instantiation has
+// TUNE = false and no such branch.  PUB (arm ZHIP_TUNE_ARM = 1, timing only):
+// 1 = a NON-returning atomic xor of the contribution (no arrival bits, no
+// finalize; results invalid) -- the price of the returning publication.
+template <bool CRC, int ITEM, bool SWAP, bool LEAN = false, bool CF = false, int LM = 0, bool TUNE = false,
+          int PUB = 0>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(LM == 2 ? 6 : 4, LM == 2 ? 6 : 4)))
 void k_decode_il(const DecodeParams p) {
     constexpr int K = kDefaultBlocks;
@@ -1238,7 +1244,7 @@ void k_decode_il(const DecodeParams p) {
     if constexpr (CRC) {
         // (timing arm kTuneNoTables: every lane reads one zero line instead of
         // the 24 KiB of tables; results invalid)
-        const bool ntab = (p.tune & kTuneNoTables) != 0;
+        const bool ntab = TUNE && (p.tune & kTuneNoTables) != 0;
         const uint4* gt = ntab ? reinterpret_cast<const uint4*>(g_rows_zero)
                                : reinterpret_cast<const uint4*>(p.il_tab);
         const int ti = ntab ? 0 : t, ts = ntab ? 0 : kThreads;
@@ -1317,16 +1323,24 @@ void k_decode_il(const DecodeParams p) {
         }
         // 4. run end: one chain per workgroup, one publication
         if constexpr (CRC) {
-            uint32_t v = ok ? ((p.tune & kTuneNoRunEnd) ? acc.a0 ^ acc.a1 ^ acc.a2 ^ acc.a3  // timing arm
+            uint32_t v = ok ? ((TUNE && (p.tune & kTuneNoRunEnd)) ? acc.a0 ^ acc.a1 ^ acc.a2 ^ acc.a3  // timing arm
                                : LM == 0 ? lanemul3(s_mul, t, fold4(s_tab, acc))
                                          : lanemul_reg(kl, fold4(s_tab, acc)))
                             : 0u;
             v = wave_xor(v);
             if ((t & 63) == 0) s_red[0][t >> 6] = v;
             __syncthreads();
-            if (ok && t < 64 && !(p.tune & kTuneNoPub)) {
+            if (ok && t < 64 && !(TUNE && (p.tune & kTuneNoPub))) {
                 const uint32_t V = __builtin_amdgcn_readfirstlane(s_red[0][0] ^ s_red[0][1] ^ s_red[0][2] ^ s_red[0][3]);
-                publish_il(p, c, r, wpc, V, __builtin_amdgcn_readfirstlane(stored), t);
+                if constexpr (PUB == 1) {
+                    if (t == 0) {  // timing arm: fire and forget (the third workspace dword)
+                        const uint32_t fin = r == 0 ? (p.c3 ^ ~__builtin_amdgcn_readfirstlane(stored)) : 0u;
+                        __hip_atomic_fetch_xor(p.ws + 4ull * c + 2, V ^ fin, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                } else {
+                    publish_il(p, c, r, wpc, V, __builtin_amdgcn_readfirstlane(stored), t);
+                }
             }
         }
         if (r == 0) unit_status_pair(p, U, CRC, t);
@@ -1335,6 +1349,18 @@ void k_decode_il(const DecodeParams p) {
     //    this kernel only then), the first block prefetched with the data
     if constexpr (CRC)
         for (uint32_t j = g; j < p.n_idx; j += G) verify_index_pair(p, j, t, kix, s_tab, s_red[1], j == g, ipre);
+}
+
+KernelFn select_il_kernel_tuned(bool crc, int item, bool swap) {  // runtime timing arms (p.tune)
+    return (crc && item == 4 && !swap) ? k_decode_il<true, 4, false, false, false, 0, true> : nullptr;
+}
+
+KernelFn select_il_kernel_arm(bool crc, int item, bool swap, int arm) {  // ZHIP_TUNE_ARM experiments
+    if (!(crc && item == 4 && !swap)) return nullptr;
+    switch (arm) {
+        case 1: return k_decode_il<true, 4, false, false, false, 0, false, 1>;
+        default: return nullptr;
+    }
 }
 
 KernelFn select_il_kernel_lean(bool crc, int item, bool swap) {  // kTuneIlLean (4-byte LE CRC item type only)

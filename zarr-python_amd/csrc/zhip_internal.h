@@ -233,6 +233,7 @@ extern "C" void zhip_stage_set_copy(uint32_t nt);     // staging.cpp (ZHIP_TUNE_
 namespace zhip {
 extern int g_tune_blocks;
 extern uint32_t g_tune_bits;
+extern int g_tune_arm;  // ZHIP_TUNE_ARM: experimental kernel variant (0 = production)
 
 struct EncodeParams {
     const uint8_t* arr;   // source array base (device)
