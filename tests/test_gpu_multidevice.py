@@ -101,3 +101,67 @@ def test_device_group_compressed_chain(device):
     into = torch.empty(out_shape, dtype=torch.float32, device=device)
     prog.gather(batch, into)
     assert into.cpu().numpy().tobytes() == O.read(host, meta).tobytes()
+
+
+# ------------------------------------------------- HipCodecPipeline(devices=...)
+@pytest.mark.parametrize("kind", ["memory", "device"])
+@pytest.mark.parametrize("sharded", [False, True])
+@pytest.mark.parametrize("devs", ["0,0", "0,0,0"])
+def test_pipeline_devices_through_array(device, monkeypatch, kind, sharded, devs):
+    """A zarr caller's arr[...] / arr[...] = v with a device list (zarr config
+    "hip.devices", env ZARR_HIP__DEVICES): the items split into bands of the
+    out over the devices, every band decoded / encoded on its device; reads
+    into host and device outs and the written store compared with the oracle."""
+    import torch
+
+    import zarr_hip
+
+    monkeypatch.setenv("ZARR_HIP__DEVICES", devs)
+    shape, chunks = (128, 96, 64), (32, 32, 32)
+    shards = (64, 96, 64) if sharded else None
+    if shards is not None:
+        meta = O.ArrayMeta(shape, shards, np.dtype("float32"), 0.0, codecs=[SHARD(chunks, [LE, CRC])])
+    else:
+        meta = O.ArrayMeta(shape, chunks, np.dtype("float32"), 0.0, codecs=[LE, CRC])
+    store = zarr_hip.DeviceStore(device) if kind == "device" else zarr_hip.MemoryStore()
+    if shards is not None:
+        arr = zarr_hip.Array.create(store, shape, chunks, "float32", 0.0, shards=shards, inner_codecs=[LE, CRC])
+    else:
+        arr = zarr_hip.Array.create(store, shape, chunks, "float32", 0.0, codecs=[LE, CRC])
+    assert arr.codec_pipeline.devices == tuple(int(d) for d in devs.split(","))
+    host: dict = {}
+    data = _data(shape, "float32")
+    for sel, val in [((Ellipsis,), data), ((slice(10, 100), slice(5, 90), slice(3, 60)), _data((90, 85, 57), "float32", seed=4)),
+                     ((slice(64, 128),), np.float32(2.5))]:
+        arr[sel] = val
+        O.write(host, meta, sel, val)
+        stored = {k: bytes(v) for k, v in store.to_dict().items() if not k.endswith("zarr.json")}
+        assert stored == host
+    for sel in [(Ellipsis,), (slice(5, 120, 3), slice(None), slice(7, 60)), (slice(30, 31), slice(None), 5)]:
+        want = np.ascontiguousarray(O.read(host, meta, sel))
+        assert np.asarray(arr[sel]).tobytes() == want.tobytes()
+    out = torch.empty(shape, dtype=torch.float32, device=device)
+    arr.get((Ellipsis,), out=out)
+    assert out.cpu().numpy().tobytes() == O.read(host, meta).tobytes()
+    outf = torch.empty(tuple(reversed(shape)), dtype=torch.float32, device=device).permute(2, 1, 0)  # F order
+    arr.get((Ellipsis,), out=outf)
+    assert outf.cpu().numpy().tobytes() == O.read(host, meta).tobytes()
+
+
+def test_pipeline_devices_crc_error(device, monkeypatch):
+    import zarr_hip
+
+    monkeypatch.setenv("ZARR_HIP__DEVICES", "0,0")
+    meta = O.ArrayMeta((64, 64), (16, 16), np.dtype("float32"), 0.0, codecs=[LE, CRC])
+    host: dict = {}
+    O.write(host, meta, (Ellipsis,), _data((64, 64), "float32"))
+    bad = bytearray(host["c/3/1"])
+    bad[40] ^= 0x04
+    host["c/3/1"] = bytes(bad)
+    with pytest.raises(ValueError) as want:
+        O.read(host, meta)
+    arr = zarr_hip.Array.create(zarr_hip.MemoryStore(dict(host)), (64, 64), (16, 16), "float32", 0.0,
+                                codecs=[LE, CRC])
+    with pytest.raises(ValueError) as got:
+        arr[...]
+    assert str(got.value) == str(want.value)

@@ -385,6 +385,46 @@ class ReadGraph:
         return [p.results() for p in self.programs]
 
 
+def _parse_devices(devices) -> tuple:
+    """A device list (ints, "cuda:i" strings or torch devices, or a comma
+    string "0,1,2") -> tuple of device indices."""
+    if devices is None or devices == "" or devices == ():
+        return ()
+    if isinstance(devices, str):
+        devices = [d for d in devices.replace(" ", "").split(",") if d]
+    out = []
+    for d in devices:
+        if isinstance(d, str):
+            out.append(int(d.split(":")[-1]))
+        elif isinstance(d, (int, np.integer)):
+            out.append(int(d))
+        else:  # a torch.device
+            out.append(int(d.index or 0))
+    return tuple(out)
+
+
+def _config_devices() -> tuple:
+    """zarr's config key "hip.devices" when zarr is importable, else its
+    environment form ZARR_HIP__DEVICES (donfig's mapping of nested keys)."""
+    v = os.environ.get("ZARR_HIP__DEVICES")
+    z = _ZARR_CONFIG.get("z", 0)
+    if z == 0:  # import once (absent on this image's Python)
+        try:
+            import zarr as z
+        except Exception:
+            z = None
+        _ZARR_CONFIG["z"] = z
+    if z is not None:
+        try:
+            v = z.config.get("hip.devices", v)
+        except Exception:
+            pass
+    return _parse_devices(v)
+
+
+_ZARR_CONFIG: dict = {}
+
+
 # entries of the per-call plan cache (per pipeline instance); 0 disables it
 READ_CACHE_SIZE = int(os.environ.get("ZARR_HIP_READ_CACHE", "16"))
 
@@ -504,13 +544,18 @@ class HipCodecPipeline:
     # load-address prediction for whole-row batches (planner.predict_rows);
     # ZARR_HIP_PREDICT=0 turns it off (measurements only)
     predict_loads: bool = field(default_factory=lambda: os.environ.get("ZARR_HIP_PREDICT", "1") != "0")
+    # GPUs a read / write is split over (parallel.read_multi / write_multi):
+    # () = one device (the out's, the store's or the current one).  Default
+    # from zarr's config key "hip.devices" (env ZARR_HIP__DEVICES="0,1,...")
+    devices: tuple = field(default_factory=lambda: _config_devices())
     # per-call plan cache for device-resident reads (read_sync): batch key ->
     # DecodeProgram; entries hold tables, never outs (retargeted per call)
     _read_cache: dict = field(default_factory=dict, compare=False, hash=False, repr=False)
     _aux: dict = field(default_factory=dict, compare=False, hash=False, repr=False)
 
     @classmethod
-    def from_codecs(cls, codecs: Iterable, *, batch_size: int | None = None) -> "HipCodecPipeline":
+    def from_codecs(cls, codecs: Iterable, *, batch_size: int | None = None,
+                    devices=None) -> "HipCodecPipeline":
         codecs = tuple(codecs)
         cl = tuple(parse_codecs(codecs))
         if any(isinstance(c, ShardingCodec) for c in cl) and len(cl) > 1:
@@ -519,6 +564,8 @@ class HipCodecPipeline:
                           "may lead to inefficient performance.", UserWarning, stacklevel=2)
         aa, ab, bb = split_codecs(cl)
         p = cls(cl, aa, ab, bb, batch_size or (1 << 30))
+        if devices is not None:
+            p = replace(p, devices=_parse_devices(devices), _read_cache={}, _aux={})
         if any(is_v2_codec(c) for c in codecs):
             p._aux["v2"] = True  # the chunk spec's order decides the stored layout (evolve)
         return p
@@ -554,7 +601,7 @@ class HipCodecPipeline:
                 codecs = (TransposeCodec(order=tuple(reversed(range(array_spec.ndim)))),) + codecs
         ev = evolve_codecs(codecs, array_spec)
         aa, ab, bb = split_codecs(ev)
-        return type(self)(ev, aa, ab, bb, self.batch_size, self.predict_loads)
+        return type(self)(ev, aa, ab, bb, self.batch_size, self.predict_loads, self.devices)
 
     def __iter__(self):
         return iter(self.codecs)
@@ -592,7 +639,7 @@ class HipCodecPipeline:
 
     def _sub(self, codecs) -> "HipCodecPipeline":
         aa, ab, bb = split_codecs(codecs)
-        return type(self)(tuple(codecs), aa, ab, bb, self.batch_size, self.predict_loads)
+        return type(self)(tuple(codecs), aa, ab, bb, self.batch_size, self.predict_loads, ())
 
     def _host_read_batch(self, batch: list, outer: tuple) -> list:
         """Items whose getters return the stored bytes -> items over the
@@ -791,6 +838,12 @@ class HipCodecPipeline:
         batch = normalize_batch(batch_info)
         if not batch:
             return ()
+        if len(self.devices) > 1:  # items split over several GPUs (parallel.read_multi)
+            from . import parallel
+
+            res = parallel.read_multi(self, batch, out, drop_axes)
+            if res is not None:
+                return res
         ns = self._nested()
         if ns is not None:  # nested sharding: outer level routed on the host (nested.py)
             from . import nested
@@ -989,6 +1042,11 @@ class HipCodecPipeline:
         if not batch:
             return
         value = _resolve_value(value)
+        if len(self.devices) > 1:  # items split over several GPUs (parallel.write_multi)
+            from . import parallel
+
+            if parallel.write_multi(self, batch, value, drop_axes, partial_encode):
+                return
         ns = self._nested()
         if ns is not None:  # nested sharding: outer level assembled on the host (nested.py)
             from . import nested
