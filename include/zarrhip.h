@@ -175,6 +175,37 @@ int zhip_plan_kernel_flags(const zhip_plan *plan, uint32_t *flags);
                                  steps, innermost rows are 2^k <= 4096 bytes and
                                  shape[ndim-2] is a multiple of 4096/row_bytes
                                  (ndim >= 2): affine per-step addressing */
+#define ZHIP_DF_BANK1 16u     /* deferred CRC verdicts (below): this launch publishes
+                                 into workspace bank 1 and checks bank 0 (else the
+                                 reverse); the caller alternates it per launch */
+
+/* Deferred CRC verdicts.  The headline kernel (k_decode_il) publishes each
+ * workgroup's CRC contribution with a NON-returning atomic xor into the
+ * chunk's workspace word of the launch's bank (4 words per chunk:
+ * {w0, w1, s0, s1}); the chunk's first workgroup also folds in the stored
+ * trailer, so after the launch w_b = computed ^ stored: 0 for a matching
+ * chunk, and s_b holds the stored trailer.  The verdict is read, and a
+ * nonzero word cleared, by the next launch (its first workgroup per chunk
+ * checks the other bank: status CRC_MISMATCH + errflag, sticky across graph
+ * replays), by zhip_dv_check, or by the host after synchronising (a nonzero
+ * w_b is Crc32cCodec's mismatch with stored s_b, computed w_b ^ s_b).  Every
+ * other kernel leaves w0 and w1 zero once its launch completes. */
+typedef struct zhip_dv_ref {
+    uint32_t *workspace;   /* a launch's d_workspace (4 words per chunk first) */
+    zhip_status *status;   /* its d_status */
+    uint32_t *errflag;     /* its d_errflag */
+    uint32_t n_chunks, pad;
+} zhip_dv_ref;
+/* Fold the deferred verdicts of n_refs launches' workspaces (a device array
+ * of zhip_dv_ref) into their statuses and error words and clear them: one
+ * small kernel, e.g. the last node of a captured read loop. */
+int zhip_dv_check(const zhip_dv_ref *d_refs, uint32_t n_refs, void *stream);
+
+/* The per-call read's result check, generalised: n device ranges (srcs[i],
+ * sizes[i] bytes) copied back behind the launches on `stream` into one
+ * page-locked buffer, one stream synchronise, then concatenated into
+ * host_out. */
+int zhip_wait_ranges(const void *const *srcs, const uint64_t *sizes, uint32_t n, void *host_out, void *stream);
 
 /* Upload the plan's constant tables to the current HIP device (once). */
 int zhip_plan_upload(zhip_plan *plan);

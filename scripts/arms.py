@@ -6,6 +6,8 @@ rocprofv3 --pmc pass over this process attributes every counter to one arm.
             4 replicas rotated (512 MiB working set)
   ARM=c2    the unsharded 256^3 / 64^3 decode
   ARM=c4    C4 (1024^3 f32, 128^3 shards of 32^3), 2 replicas
+  ARM=c3 / c3g  C3: transpose(2,1,0) + bytes (+ crc32c unless NOCRC=1) on the
+            256^3 array in 64^3 (k_decode_tile4) / 128^3 (k_decode_tileg) chunks
   ARM=copy  scripts/copybench k_copy: SIZE bytes (default 64 MiB), SPAN bytes
             per workgroup, K loads in flight per thread, NT policy (0 default,
             1 nt loads+stores, 2 nt loads, 3 nt stores), 4 replicas at 64 MiB,
@@ -43,17 +45,22 @@ def main():
     reps = int(os.environ.get("REPS", "8" if big else "40"))
     stream = torch.cuda.current_stream(dev)
     sh = int(stream.cuda_stream)
-    if arm in ("hl", "c2", "c4"):
+    if arm in ("hl", "c2", "c4", "c3", "c3g"):
         g = W.C4 if arm == "c4" else W.HEADLINE
         shape, inner = g["shape"], g["inner"]
-        shards = None if arm == "c2" else g["shards"]
+        shards = None if arm in ("c2", "c3", "c3g") else g["shards"]
+        codecs = [W.LE] if os.environ.get("NOCRC") == "1" else [W.LE, W.CRC]
+        if arm in ("c3", "c3g"):
+            codecs = [{"name": "transpose", "configuration": {"order": [2, 1, 0]}}] + codecs
+            inner = (128, 128, 128) if arm == "c3g" else inner
+            arm = arm + ("_nocrc" if os.environ.get("NOCRC") == "1" else "")
         if arm == "c4":
             gen = torch.Generator(device=dev).manual_seed(0)
             data = torch.randn(shape, generator=gen, device=dev, dtype=torch.float32)
         else:
             data = torch.from_numpy(W.synthetic(shape)).to(dev)
         R = 2 if arm == "c4" else 4
-        progs = [bench.build_replica(dev, data, shape, inner, [W.LE, W.CRC], shards=shards).prepare_read((Ellipsis,))
+        progs = [bench.build_replica(dev, data, shape, inner, codecs, shards=shards).prepare_read((Ellipsis,))
                  for _ in range(R)]
         for p, out in progs:
             p.launch()
@@ -61,7 +68,8 @@ def main():
             if not torch.equal(out.view(torch.int32), data.view(torch.int32)):
                 raise SystemExit(f"arms {arm}: decode differs from the source")
         n_inner = int(np.prod([s // i for s, i in zip(shape, inner)]))
-        alg = n_inner * (int(np.prod(inner)) * 4 + 4) + data.numel() * 4
+        alg = n_inner * (int(np.prod(inner)) * 4 + (4 if len(codecs) > 1 and codecs[-1] == W.CRC else 0)) + \
+            data.numel() * 4
         if shards is not None:
             n_shards = int(np.prod([s // i for s, i in zip(shape, shards)]))
             alg += n_shards * ((n_inner // n_shards) * 16 + 4)
@@ -112,7 +120,8 @@ def main():
     us = [a.elapsed_time(b) * 1e3 for a, b in ev]
     N.lib().zhip_set_tuning(2, 0)
     med = float(np.median(us))
-    print(json.dumps({"arm": arm, "tune": tune, "reps": reps, "us_med": round(med, 2), "us_min": round(min(us), 2),
+    kern = N.lib().zhip_last_kernel().decode() if not arm.startswith("copy") else "copybench"
+    print(json.dumps({"arm": arm, "kernel": kern, "tune": tune, "reps": reps, "us_med": round(med, 2), "us_min": round(min(us), 2),
                       "alg_bytes": int(alg), "hbm_frac_med": round(alg / (med * 1e-6) / 8e12, 4)}), flush=True)
 
 

@@ -8,7 +8,7 @@ for i in $(seq 1 12); do
   /usr/local/graft/bin/gpurun "$@" > "$out" 2>&1
   rc=$?
   if [ $rc -eq 3 ]; then echo "[retry $i: no box]" >> "$out.retries"; sleep 150; continue; fi
-  if grep -q 'status=transient' "$out" && grep -q 'charged=0.0s' "$out"; then
+  if grep -q 'status=transient' "$out" && grep -qE 'charged=(0.0s|Nones)' "$out"; then
     echo "[retry $i: transient]" >> "$out.retries"; sleep 150; continue
   fi
   exit $rc

@@ -735,3 +735,110 @@ def test_transpose_tileg_many_groups(device):
         warr[...] = O.read(host, meta)
         got = {k: v for k, v in st.to_dict().items() if not k.endswith("zarr.json")}
         assert got == host
+
+
+# ------------------------------------------- deferred CRC verdicts (k_decode_il)
+def _il_array(device, fill=0.0):
+    """The headline geometry's chunk shape (64^3 f32 = 1 MiB: eight-workgroup
+    groups, k_decode_il with deferred verdicts) on a small array."""
+    import zarr_hip
+
+    shape, chunks = (128, 64, 64), (64, 64, 64)
+    meta = O.ArrayMeta(shape, chunks, np.dtype("float32"), fill, codecs=[LE, CRC])
+    host = {}
+    O.write(host, meta, (Ellipsis,), _data(shape, "float32"))
+    store = zarr_hip.DeviceStore.from_host(host, device)
+    arr = zarr_hip.Array.create(store, shape, chunks, "float32", fill, codecs=[LE, CRC])
+    return arr, store, host, meta
+
+
+def _corrupt(store, host, key, at=4321):
+    ref = store.get_sync(key)
+    ref.arena.buf[ref.offset + at] ^= 0x10
+    b = bytearray(host[key])
+    b[at] ^= 0x10
+    host[key] = bytes(b)
+
+
+def test_deferred_verdict_sticky_over_eager_launches(device):
+    """Launches without a result check in between: a chunk corrupted before an
+    even number of launches still raises (consecutive launches publish into
+    alternate banks and each checks the previous one), with the reference's
+    message; then the restored bytes read clean."""
+    from zarr_hip import _native as N
+
+    arr, store, host, meta = _il_array(device)
+    prog, out = arr.prepare_read((Ellipsis,))
+    prog.launch()
+    prog.results()
+    assert N.lib().zhip_last_kernel().decode() == "k_decode_il"
+    clean = dict(host)
+    _corrupt(store, host, "c/1/0/0")
+    with pytest.raises(ValueError) as want:
+        O.read(host, meta)
+    for n in (2, 3, 4):
+        for _ in range(n):
+            prog.launch()
+        with pytest.raises(ValueError) as got:
+            prog.results()
+        assert str(got.value) == str(want.value)
+    _corrupt(store, host, "c/1/0/0")  # flips the same bit back
+    assert host == clean
+    for _ in range(2):
+        prog.launch()
+        prog.results()
+    assert out.cpu().numpy().tobytes() == O.read(host, meta).tobytes()
+
+
+@pytest.mark.parametrize("repeats", [1, 2, 3])
+def test_deferred_verdict_graph_replays(device, repeats):
+    """A captured read loop with 1, 2 or 3 launches of one program, replayed
+    twice between result checks: corruption after capture raises (an odd
+    count ends the graph with a zhip_dv_check node), clean data does not."""
+    import zarr_hip
+
+    arr, store, host, meta = _il_array(device)
+    prog, out = arr.prepare_read((Ellipsis,))
+    g = zarr_hip.ReadGraph([prog], repeats, device)
+    assert (g._dv_refs is not None) == (repeats % 2 == 1)
+    g.replay()
+    g.replay()
+    g.results()
+    _corrupt(store, host, "c/0/0/0", at=77)
+    with pytest.raises(ValueError) as want:
+        O.read(host, meta)
+    g.replay()
+    g.replay()
+    with pytest.raises(ValueError) as got:
+        g.results()
+    assert str(got.value) == str(want.value)
+    _corrupt(store, host, "c/0/0/0", at=77)
+    g.replay()
+    g.results()
+    g.replay()
+    g.results()
+    assert out.cpu().numpy().tobytes() == O.read(host, meta).tobytes()
+
+
+def test_deferred_verdict_host_slabs(device):
+    """A host-sourced read through the slab pipeline (range launches of one
+    plan) reports a mismatch in any slab, and the next clean read passes."""
+    import zarr_hip
+
+    shape, chunks = (512, 64, 64), (64, 64, 64)
+    meta = O.ArrayMeta(shape, chunks, np.dtype("float32"), 0.0, codecs=[LE, CRC])
+    host = {}
+    O.write(host, meta, (Ellipsis,), _data(shape, "float32"))
+    bad = dict(host)
+    b = bytearray(bad["c/6/0/0"])
+    b[999] ^= 0x02
+    bad["c/6/0/0"] = bytes(b)
+    with pytest.raises(ValueError) as want:
+        O.read(bad, meta)
+    arr = zarr_hip.Array.create(zarr_hip.MemoryStore(bad), shape, chunks, "float32", 0.0, codecs=[LE, CRC])
+    with pytest.raises(ValueError) as got:
+        arr[...]
+    assert str(got.value) == str(want.value)
+    arr2 = zarr_hip.Array.create(zarr_hip.MemoryStore(dict(host)), shape, chunks, "float32", 0.0, codecs=[LE, CRC])
+    for _ in range(2):
+        assert arr2[...].tobytes() == O.read(host, meta).tobytes()

@@ -194,6 +194,14 @@ int zhip_set_tuning(int key, int value) {
     }
 }
 
+int zhip_dv_check(const zhip_dv_ref* d_refs, uint32_t n_refs, void* stream) {
+    if (n_refs && !d_refs) return set_err(ZHIP_E_INVALID, "null argument");
+    if (n_refs > 65535u) return set_err(ZHIP_E_INVALID, "too many launches in one check");
+    if (zhip::launch_dv_check(d_refs, n_refs, static_cast<hipStream_t>(stream)) != ZHIP_OK)
+        return set_err(ZHIP_E_HIP, "k_dv_check launch failed");
+    return ZHIP_OK;
+}
+
 int zhip_abi_version(void) { return ZHIP_ABI_VERSION; }
 
 int zhip_debug_stamps(uint64_t* host_out, uint32_t n_wg) {
@@ -722,6 +730,7 @@ int zhip_decode_mapped(const zhip_plan* plan, const void* src, uint64_t src_size
     p.n_inner = L.n_inner;
     std::memcpy(p.fill, plan->fill, sizeof(p.fill));
     p.fast = (decode_flags & ZHIP_DF_FAST_ROWS) ? 1u : 0u;
+    p.dv_bank = (decode_flags & ZHIP_DF_BANK1) ? 1u : 0u;
     p.tune = g_tune_bits;
     p.tq = -1;
     p.rows = 0;

@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cerrno>
 #include <condition_variable>
@@ -433,6 +434,38 @@ int zhip_wait_words(const uint32_t* const* words, uint32_t n, uint32_t* host_out
             return ZHIP_E_HIP;
     if (hipStreamSynchronize(st) != hipSuccess) return ZHIP_E_HIP;
     for (uint32_t i = 0; i < n; ++i) host_out[i] = pinned[i];
+    return ZHIP_OK;
+}
+
+int zhip_wait_ranges(const void* const* srcs, const uint64_t* sizes, uint32_t n, void* host_out, void* stream) {
+    // zhip_wait_words for ranges: every range copied back behind the launches
+    // on `stream` into one page-locked per-thread buffer, one synchronise
+    if (n == 0) return ZHIP_OK;
+    if (!srcs || !sizes || !host_out) return ZHIP_E_INVALID;
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < n; ++i) total += sizes[i];
+    thread_local uint8_t* pinned = nullptr;
+    thread_local uint64_t cap = 0;
+    if (total > cap) {
+        if (pinned) (void)hipHostFree(pinned);
+        pinned = nullptr;
+        cap = 0;
+        const uint64_t want = std::max<uint64_t>(total, 4096);
+        if (hipHostMalloc(reinterpret_cast<void**>(&pinned), want, hipHostMallocDefault) != hipSuccess) {
+            pinned = nullptr;
+            return ZHIP_E_HIP;
+        }
+        cap = want;
+    }
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    uint64_t at = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        if (sizes[i] && hipMemcpyAsync(pinned + at, srcs[i], sizes[i], hipMemcpyDeviceToHost, st) != hipSuccess)
+            return ZHIP_E_HIP;
+        at += sizes[i];
+    }
+    if (hipStreamSynchronize(st) != hipSuccess) return ZHIP_E_HIP;
+    std::memcpy(host_out, pinned, total);
     return ZHIP_OK;
 }
 

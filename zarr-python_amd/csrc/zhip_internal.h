@@ -134,6 +134,7 @@ struct DecodeParams {
     const uint32_t* il_tab;
     const uint32_t* il_klane;
     const uint32_t* il_kidx;
+    uint32_t dv_bank;  // deferred CRC verdicts: bank this launch publishes into (ZHIP_DF_BANK1)
     // k_decode_xw: 8 KiB spans per chunk (0: not available), arrival subwords
     // per chunk in the workspace tail (0: one level or xor + count), its A_1024
     // tables, lane constants per (span, lane) and for the fused index check
@@ -296,6 +297,7 @@ struct PackParams {
 int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid);
 int launch_encode(const EncodeParams& p, hipStream_t stream, int max_grid);
 int launch_shard_pack(const PackParams& p, uint32_t n_shards, hipStream_t stream);
+int launch_dv_check(const zhip_dv_ref* d_refs, uint32_t n_refs, hipStream_t stream);
 int debug_stamps(uint64_t* host_out, uint32_t n_wg);
 
 }  // namespace zhip

@@ -38,6 +38,7 @@ DF_FAST_ROWS = 1
 DF_TILE = 2
 DF_ROWS = 4
 DF_TILE_PREFIX = 8
+DF_BANK1 = 16  # deferred CRC verdicts: publish into workspace bank 1, check bank 0
 
 PK_TILE4 = 1
 PK_TILE4_ENCODE = 2
@@ -220,6 +221,11 @@ def lib():
     L.zhip_host_pinned.restype = ctypes.c_int
     L.zhip_wait_words.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
     L.zhip_wait_words.restype = ctypes.c_int
+    L.zhip_wait_ranges.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                                   ctypes.c_void_p]
+    L.zhip_wait_ranges.restype = ctypes.c_int
+    L.zhip_dv_check.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
+    L.zhip_dv_check.restype = ctypes.c_int
     L.zhip_crc32c_host.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
     L.zhip_crc32c_host.restype = ctypes.c_uint32
     L.zhip_host_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32]

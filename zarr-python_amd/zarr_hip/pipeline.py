@@ -164,12 +164,19 @@ class DecodeLaunch:
         nw = max(self.n, 1) * 4
         nws = max(self.n, 1) * max(4, self.plan.workspace_words)  # zhip_plan_info
         ni = self.n_idx * 4
-        z = torch.zeros(nw + nws + 64 + ni, dtype=torch.int32, device=device)
+        # [statuses][error word, pad to 256 B][workspace][index statuses]: the
+        # error word and the chunks' deferred-verdict words (the first 4 words
+        # per chunk of the workspace, zarrhip.h) are one contiguous range, read
+        # back with one copy after a launch
+        z = torch.zeros(nw + 64 + nws + ni, dtype=torch.int32, device=device)
         self.d_status = z[:nw]
-        self.d_ws = z[nw: nw + nws]
-        self.d_err = z[nw + nws: nw + nws + 4]
+        self.d_err = z[nw: nw + 4]
+        self.d_ws = z[nw + 64: nw + 64 + nws]
+        self.d_verdict = z[nw: nw + 64 + 4 * self.n]  # error word .. last chunk's verdict words
         if self.n_idx:
-            self.d_idx_status = z[nw + nws + 64: nw + nws + 64 + ni]
+            self.d_idx_status = z[nw + 64 + nws: nw + 64 + nws + ni]
+        self._bank = 0  # deferred-verdict bank of the next launch (alternates)
+        self._ranges: list = []  # (first, count) of launch_range calls since the last statuses()
 
     def launch(self, stream: int | None = None) -> None:
         if self.n == 0:
@@ -177,12 +184,14 @@ class DecodeLaunch:
         s = _stream_handle(self.device) if stream is None else stream
         out_ptr = self.out.data_ptr() if self.out is not None else None
         if self.d_rowmap is not None:
+            bank = self._bank
+            self._bank ^= 1  # consecutive launches publish into alternate banks (also while captured)
             N.check(N.lib().zhip_decode_mapped(
                 self.plan.handle, self.src.data_ptr(), self.src_size, out_ptr, self.d_chunks.data_ptr(),
                 self.n, self.d_sels.data_ptr(), self.d_status.data_ptr(), self.d_ws.data_ptr(),
                 self.d_err.data_ptr(), self.d_idx_chunks.data_ptr() if self.n_idx else None, self.n_idx,
-                self.d_idx_status.data_ptr() if self.n_idx else None, self.flags, self.predict,
-                self.d_rowmap.data_ptr(), s), "zhip_decode_mapped")
+                self.d_idx_status.data_ptr() if self.n_idx else None, self.flags | (N.DF_BANK1 if bank else 0),
+                self.predict, self.d_rowmap.data_ptr(), s), "zhip_decode_mapped")
             return
         if self.predict is not None:
             N.check(N.lib().zhip_decode_predicted(
@@ -212,6 +221,7 @@ class DecodeLaunch:
         if count == 0:
             return
         assert self.n_idx == 0 and self.predict is None
+        self._ranges.append((first, count))  # where this range's verdict words live (statuses())
         s = _stream_handle(self.device) if stream is None else stream
         out_ptr = self.out.data_ptr() if self.out is not None else None
         wsw = max(4, self.plan.workspace_words)
@@ -221,15 +231,45 @@ class DecodeLaunch:
         if self.d_rowmap is not None:
             N.check(N.lib().zhip_decode_mapped(
                 self.plan.handle, src.data_ptr(), src_size, out_ptr, chunks, count, self.d_sels.data_ptr(),
-                status, ws, self.d_err.data_ptr(), None, 0, None, self.flags, None, self.d_rowmap.data_ptr(), s),
-                "zhip_decode_mapped")
+                status, ws, self.d_err.data_ptr(), None, 0, None, self.flags | (N.DF_BANK1 if self._bank else 0),
+                None, self.d_rowmap.data_ptr(), s), "zhip_decode_mapped")
             return
         N.check(N.lib().zhip_decode(self.plan.handle, src.data_ptr(), src_size, out_ptr, chunks, count,
                                     self.d_sels.data_ptr(), status, ws, self.d_err.data_ptr(), self.flags, s),
                 "zhip_decode")
 
     def statuses(self) -> np.ndarray:
-        return self.d_status[: self.n * 4].cpu().numpy().view(STATUS_DT)
+        """Per-chunk statuses with the deferred CRC verdicts merged in: a
+        nonzero verdict word w of bank b is a mismatch with stored trailer s_b,
+        computed w ^ s_b (zarrhip.h); such words are cleared, so the next
+        launch starts clean."""
+        st = self.d_status[: self.n * 4].cpu().numpy().view(STATUS_DT).copy()
+        if self._ranges:  # range launches: chunk first + c's words at first * wsw + 4 c
+            wsw = max(4, self.plan.workspace_words)
+            for first, count in self._ranges:
+                self.merge_verdicts(st[first: first + count],
+                                    self.d_ws[first * wsw: first * wsw + 4 * count].cpu().numpy().view(np.uint32),
+                                    self.d_ws[first * wsw: first * wsw + 4 * count])
+            self._ranges = []
+        else:
+            self.merge_verdicts(st, self.d_ws[: self.n * 4].cpu().numpy().view(np.uint32))
+        return st
+
+    def merge_verdicts(self, st: np.ndarray, ws: np.ndarray, dev_ws=None) -> bool:
+        """Fold verdict words (the workspace's first 4 words per chunk, host
+        copy) into host statuses; True (and the device words cleared) when one
+        was set."""
+        w = ws.reshape(-1, 4)
+        bad = (w[:, 0] != 0) | (w[:, 2] != 0)
+        if not bad.any():
+            return False
+        for c in np.nonzero(bad)[0]:
+            b = 0 if w[c, 0] != 0 else 2
+            st[c]["code"] = N.ST_CRC_MISMATCH
+            st[c]["stored"] = w[c, b + 1]
+            st[c]["computed"] = w[c, b] ^ w[c, b + 1]
+        (self.d_ws[: self.n * 4] if dev_ws is None else dev_ws).view(-1, 4)[:, 0::2].zero_()
+        return True
 
     def index_statuses(self) -> np.ndarray:
         return self.d_idx_status[: self.n_idx * 4].cpu().numpy().view(STATUS_DT)
@@ -283,23 +323,30 @@ class DecodeProgram:
         self.data.out = out
 
     def results_fast(self) -> tuple[GetResult, ...]:
-        """results() for the per-call path: synchronise on ONE 4-byte error
-        word per launch (every non-OK, non-missing status of the data and the
-        fused index checks ORs a bit into it); the full status table is read
-        only when it is set.  Missing items are known on the host at planning
-        (absent keys, absent shards), so the GetResults are prebuilt."""
-        w = getattr(self, "_err_words", None)
+        """results() for the per-call path: synchronise on ONE copy back per
+        launch -- the data launch's error word and its chunks' deferred CRC
+        verdict words (one contiguous range, zarrhip.h), the index launch's
+        error word -- and read the full status table only when one is set.
+        Missing items are known on the host at planning (absent keys, absent
+        shards), so the GetResults are prebuilt."""
+        w = getattr(self, "_err_ranges", None)
         if w is None:
             import ctypes
 
-            ptrs = [self.data.d_err.data_ptr()] + ([self.index.d_err.data_ptr()] if self.index is not None else [])
-            w = self._err_words = ((ctypes.c_void_p * len(ptrs))(*ptrs), len(ptrs),
-                                   (ctypes.c_uint32 * len(ptrs))())
-        N.check(N.lib().zhip_wait_words(w[0], w[1], w[2], _stream_handle(self.data.device)), "zhip_wait_words")
-        err = 0
-        for x in w[2]:
-            err |= x
-        if err:
+            rngs = [(self.data.d_verdict.data_ptr(), self.data.d_verdict.numel() * 4)]
+            if self.index is not None:
+                rngs.append((self.index.d_err.data_ptr(), 4))
+            n = len(rngs)
+            host = np.zeros(sum(r[1] for r in rngs) // 4, np.uint32)
+            w = self._err_ranges = ((ctypes.c_void_p * n)(*[r[0] for r in rngs]),
+                                    (ctypes.c_uint64 * n)(*[r[1] for r in rngs]), n, host)
+        host = w[3]
+        N.check(N.lib().zhip_wait_ranges(w[0], w[1], w[2], host.ctypes.data, _stream_handle(self.data.device)),
+                "zhip_wait_ranges")
+        nv = self.data.d_verdict.numel()
+        err = int(host[0]) | (int(host[nv]) if self.index is not None else 0)
+        dv = host[64:nv]
+        if err or (dv.size and (dv[0::2].any())):
             self.data.reset_errflag()
             if self.index is not None:
                 self.index.reset_errflag()
@@ -312,6 +359,7 @@ class DecodeProgram:
 
     def results(self) -> tuple[GetResult, ...]:
         """Synchronise, then raise like the reference or return per-item statuses."""
+        data_st = self.data.statuses()  # first: consumes (clears) the deferred verdicts
         st = None
         if self.index is not None:
             st = self.index.statuses()
@@ -322,7 +370,7 @@ class DecodeProgram:
             if len(bad):
                 r = st[bad[0]]
                 raise ValueError(crc_error_message(int(r["stored"]), int(r["computed"])))
-        st = self.data.statuses()
+        st = data_st
         codes = st["code"]
         bad = np.nonzero((codes != N.ST_OK) & (codes != N.ST_MISSING))[0]
         if len(bad):
@@ -344,6 +392,16 @@ class DecodeProgram:
             for i in range(self.n_items):
                 out.append(GetResult(status="missing" if by_item[i] == N.ST_MISSING else "present"))
         return tuple(out)
+
+
+def _dv_refs(launches: list, device):
+    """A device array of zhip_dv_ref (zarrhip.h) for DecodeLaunches."""
+    torch = _torch()
+    dt = np.dtype([("ws", "<u8"), ("status", "<u8"), ("err", "<u8"), ("n", "<u4"), ("pad", "<u4")])
+    a = np.zeros(len(launches), dt)
+    for i, d in enumerate(launches):
+        a[i] = (d.d_ws.data_ptr(), d.d_status.data_ptr(), d.d_err.data_ptr(), d.n, 0)
+    return torch.from_numpy(a.view(np.uint8).copy()).to(device)
 
 
 class ReadGraph:
@@ -368,10 +426,22 @@ class ReadGraph:
         self.graph = torch.cuda.CUDAGraph()
         self.stream = torch.cuda.Stream(self.device)
         self.stream.wait_stream(torch.cuda.current_stream(self.device))
+        # deferred CRC verdicts (zarrhip.h): consecutive launches of a program
+        # alternate banks and each checks the previous one; a program launched
+        # an odd number of times would start the next replay in the bank its
+        # last launch left unchecked, so the graph then ends with one
+        # zhip_dv_check node over every program's workspace
+        counts = [len(range(j, self.repeats, len(self.programs))) for j in range(len(self.programs))]
+        launches = [getattr(p, "data", None) for p in self.programs]
+        odd = any(c % 2 for c, d in zip(counts, launches) if d is not None and getattr(d, "d_rowmap", None) is not None)
+        self._dv_refs = _dv_refs([d for d in launches if d is not None], self.device) if odd else None
         with torch.cuda.device(self.device):
             with torch.cuda.graph(self.graph, stream=self.stream):
                 for i in range(self.repeats):
                     self.programs[i % len(self.programs)].launch()
+                if self._dv_refs is not None:
+                    N.check(N.lib().zhip_dv_check(self._dv_refs.data_ptr(), self._dv_refs.numel() // 32,
+                                                  int(self.stream.cuda_stream)), "zhip_dv_check")
 
     def replay(self) -> None:
         for p in self.programs:  # the graph holds the programs' planned offsets
