@@ -58,6 +58,8 @@ extern "C" {
 #define ZHIP_E_HIP -2
 #define ZHIP_E_UNSUPPORTED -3
 #define ZHIP_E_IO -4          /* a file piece could not be read in full (zhip_stage_*) */
+#define ZHIP_E_BOUNDS -5      /* an output table is too small (the counts are still returned),
+                                 or a shard blob is shorter than its index */
 
 /* per-chunk status codes (zhip_status.code) */
 #define ZHIP_ST_OK 0u
@@ -206,6 +208,53 @@ int zhip_dv_check(const zhip_dv_ref *d_refs, uint32_t n_refs, void *stream);
  * page-locked buffer, one stream synchronise, then concatenated into
  * host_out. */
 int zhip_wait_ranges(const void *const *srcs, const uint64_t *sizes, uint32_t n, void *host_out, void *stream);
+
+/* Host planner for a batch of basic selections (zhip_plan_batch).  One item
+ * of a CodecPipeline batch: its chunk (or shard) bytes, its chunk selection
+ * per DECODED dim (step 0: an integer index `start`; slices normalised to
+ * the chunk shape, step >= 1) and the byte offset of its out selection's
+ * first element.  Replaces BasicIndexer's per-chunk projections
+ * (src/zarr/core/indexing.py:390-468, 571-621) and, for sharded items,
+ * ShardingCodec._decode_partial_sync's inner-chunk expansion
+ * (src/zarr/codecs/sharding.py:1222-1309). */
+typedef struct zhip_item {
+    uint64_t src;
+    uint64_t src_len;
+    int64_t out_off;
+    uint32_t missing, _pad;
+    int64_t start[ZHIP_MAX_DIMS];
+    int64_t stop[ZHIP_MAX_DIMS];
+    int64_t step[ZHIP_MAX_DIMS];
+} zhip_item;
+
+typedef struct zhip_batch_geom {
+    int32_t ndim;
+    int32_t perm[ZHIP_MAX_DIMS];   /* stored dim s is decoded dim perm[s]                  */
+    int64_t shape[ZHIP_MAX_DIMS];  /* decoded chunk (shard) shape                          */
+    int64_t ost[ZHIP_MAX_DIMS];    /* out byte stride per decoded dim (0: absent from out) */
+    int64_t inner[ZHIP_MAX_DIMS];  /* sharded: inner chunk shape; inner[0] == 0: unsharded */
+    uint32_t index_size;           /* sharded: encoded index bytes                          */
+    uint32_t index_start;          /* sharded: index_location == "start"                   */
+    uint32_t index_crc;            /* sharded: the index chain ends in crc32c               */
+    uint32_t _pad;
+} zhip_batch_geom;
+
+/* aggregate flags over the planned entries (layout-independent halves of the
+ * kernel choice) */
+#define ZHIP_AGG_LAST_FULL 1u    /* every entry selects whole innermost stored rows        */
+#define ZHIP_AGG_OUT_ALIGNED 2u  /* every entry's out offset is a multiple of 16 bytes     */
+#define ZHIP_AGG_UNIT_STEPS 4u   /* every stored dim has step 1 or selects one index       */
+#define ZHIP_AGG_ALL_FULL 8u     /* every entry selects its whole chunk                    */
+
+/* Plan a batch: chunk entries (inner chunks of sharded items, in item order,
+ * C order within an item) with their deduplicated selections (sorted rows),
+ * the item of each entry, and for sharded items with a CRC'd index one index
+ * check entry per distinct shard.  Capacities too small: ZHIP_E_BOUNDS with
+ * *n_chunks / *n_sels / *n_idx set to the sizes needed. */
+int zhip_plan_batch(const zhip_batch_geom *g, const zhip_item *items, uint32_t n_items, zhip_chunk *chunks,
+                    uint64_t chunks_cap, uint64_t *n_chunks, zhip_sel *sels, uint32_t sels_cap,
+                    uint32_t *n_sels, uint32_t *item_of, zhip_chunk *idx_chunks, uint32_t *idx_item,
+                    uint32_t *n_idx, uint32_t *agg);
 
 /* Upload the plan's constant tables to the current HIP device (once). */
 int zhip_plan_upload(zhip_plan *plan);

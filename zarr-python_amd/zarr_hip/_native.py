@@ -129,6 +129,15 @@ PIECE_DT = np.dtype([("host", "<u8"), ("nbytes", "<u8"), ("dst_off", "<u8"), ("f
 PIECE_PINNED = 1
 PIECE_FILE = 2
 
+# zhip_item / zhip_batch_geom (include/zarrhip.h): the native host planner's input
+ITEM_DT = np.dtype([("src", "<u8"), ("src_len", "<u8"), ("out_off", "<i8"), ("missing", "<u4"), ("_pad", "<u4"),
+                    ("start", "<i8", (MAX_DIMS,)), ("stop", "<i8", (MAX_DIMS,)), ("step", "<i8", (MAX_DIMS,))])
+GEOM_DT = np.dtype([("ndim", "<i4"), ("perm", "<i4", (MAX_DIMS,)), ("_pad0", "<i4"),
+                    ("shape", "<i8", (MAX_DIMS,)), ("ost", "<i8", (MAX_DIMS,)), ("inner", "<i8", (MAX_DIMS,)),
+                    ("index_size", "<u4"), ("index_start", "<u4"), ("index_crc", "<u4"), ("_pad", "<u4")])
+AGG_LAST_FULL, AGG_OUT_ALIGNED, AGG_UNIT_STEPS, AGG_ALL_FULL = 1, 2, 4, 8
+E_BOUNDS = -5
+
 # zhip_rowblk (include/zarrhip.h)
 ROWBLK_DT = np.dtype([("rel", "<i4"), ("lo", "<u2"), ("hi", "<u2")])
 
@@ -226,6 +235,9 @@ def lib():
     L.zhip_wait_ranges.restype = ctypes.c_int
     L.zhip_dv_check.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
     L.zhip_dv_check.restype = ctypes.c_int
+    vp, u32, u64 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64
+    L.zhip_plan_batch.argtypes = [vp, vp, u32, vp, u64, vp, vp, u32, vp, vp, vp, vp, vp, vp]
+    L.zhip_plan_batch.restype = ctypes.c_int
     L.zhip_crc32c_host.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
     L.zhip_crc32c_host.restype = ctypes.c_uint32
     L.zhip_host_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32]

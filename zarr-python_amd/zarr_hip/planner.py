@@ -329,6 +329,10 @@ def plan_decode(chain: ChainInfo, spec: ArraySpec, items: list, out_strides_byte
         raise ValueError("empty batch")
     _, _, _, is_int0 = _sel_fields(items[0][3], ndim)
     ost_dec = out_dim_strides(ndim, is_int0, drop_axes, out_strides_bytes)
+    if NATIVE_PLANNER and resolved is None and (ndim > 1 or chain.shard is not None):
+        t = _plan_native(chain, spec, items, out_strides_bytes, out_base_ptr, ost_dec, item_out_extra, fill)
+        if t is not None:
+            return t
 
     if chain.shard is None:
         perm = chain.perm
@@ -460,6 +464,152 @@ def plan_decode(chain: ChainInfo, spec: ArraySpec, items: list, out_strides_byte
         t.index_layout = L2
         t.index_chunks = ic
         t.index_item = np.array([r[0] for r in idx_rows], np.int64)
+    return t
+
+
+# the native host planner (zhip_plan_batch) for basic-selection batches;
+# ZARR_HIP_NATIVE_PLANNER=0 keeps the Python loop (tests compare the two)
+NATIVE_PLANNER = __import__("os").environ.get("ZARR_HIP_NATIVE_PLANNER", "1") != "0"
+
+
+_NATIVE_CTX: dict = {}
+
+
+def _native_ctx(chain: ChainInfo, spec: ArraySpec, ost_dec, fill):
+    """Per-geometry constants of the native planner (layouts, the
+    zhip_batch_geom record, the layout halves of the kernel choice), built
+    once per (chain, chunk spec, out strides)."""
+    key = (chain, spec.shape, spec.dtype.str, fill, tuple(int(x) for x in ost_dec))
+    try:
+        ctx = _NATIVE_CTX.get(key)
+    except TypeError:  # an unhashable codec object in the chain: no caching
+        key, ctx = None, None
+    if ctx is not None:
+        return ctx
+    ndim = spec.ndim
+    shape = spec.shape
+    g = np.zeros(1, N.GEOM_DT)
+    g["ndim"] = ndim
+    sh = chain.shard
+    inner = chain.inner if sh is not None else chain
+    perm = list(inner.perm)
+    g["perm"][0, :ndim] = perm
+    g["shape"][0, :ndim] = shape
+    g["ost"][0, :ndim] = ost_dec
+    flags = (N.LF_CRC if inner.crc else 0) | (N.LF_SWAP if inner.swap else 0)
+    n_inner, index_layout = 1, None
+    if sh is not None:
+        inner_shape = sh.chunk_shape
+        n_inner = int(np.prod(sh.chunks_per_shard(shape)))
+        index_size = sh.shard_index_size(n_inner)
+        g["inner"][0, :ndim] = inner_shape
+        g["index_size"] = index_size
+        g["index_start"] = 1 if sh.index_location == "start" else 0
+        g["index_crc"] = 1 if sh.index_has_crc else 0
+        flags |= N.LF_SHARDED | (N.LF_INDEX_START if sh.index_location == "start" else 0)
+        layout = _make_layout([inner_shape[p] for p in perm], spec.dtype.itemsize, [ost_dec[p] for p in perm],
+                              flags, fill, n_inner, index_size)
+        index_layout = _make_layout([16 * n_inner], 1, [0], N.LF_CRC | N.LF_NO_WRITE, b"\0")
+    else:
+        layout = _make_layout([shape[p] for p in perm], spec.dtype.itemsize, [ost_dec[p] for p in perm],
+                              flags, fill)
+    # the layout halves of _fast_ok / _rows_ok / _tile_ok
+    nd, isz, last = layout.ndim, layout.itemsize, layout.ndim - 1
+    fast_l = (layout.out_stride[last] == isz and (layout.shape[last] * isz) % 16 == 0
+              and all(layout.out_stride[d] % 16 == 0 for d in range(last)))
+    tile_l = False
+    if nd >= 2 and layout.out_stride[last] != isz and (layout.shape[last] * isz) % 16 == 0:
+        tq = [d for d in range(last) if layout.out_stride[d] == isz and layout.shape[d] > 1]
+        tile_l = bool(tq) and all(layout.out_stride[d] % 16 == 0 for d in range(nd) if d != tq[0])
+    rows_l = False
+    if nd >= 2:
+        rb = layout.shape[last] * isz
+        rows_l = 16 <= rb <= 4096 and not rb & (rb - 1) and layout.shape[nd - 2] % (4096 // rb) == 0
+    ctx = (g, g.ctypes.data, layout, index_layout, n_inner, fast_l, tile_l, rows_l)
+    if key is not None:
+        if len(_NATIVE_CTX) > 256:
+            _NATIVE_CTX.clear()
+        _NATIVE_CTX[key] = ctx
+    return ctx
+
+
+_CH_SZ, _SEL_SZ = CHUNK_DT.itemsize, SEL_DT.itemsize
+
+
+def _plan_native(chain: ChainInfo, spec: ArraySpec, items: list, out_strides_bytes, out_base_ptr: int,
+                 ost_dec, item_out_extra, fill) -> "Tables | None":
+    """plan_decode through zhip_plan_batch: the per-item projections, inner-chunk
+    expansion, selection dedup and index list in one native call; the kernel
+    choice from the layout (cached per geometry) and the call's aggregate
+    flags.  None when an item is not a basic selection (the Python loop then
+    plans)."""
+    ndim = spec.ndim
+    n = len(items)
+    shape = spec.shape
+    ostr = [int(x) for x in out_strides_bytes]
+    S, E, K, OO = [], [], [], []
+    for so, sl, miss, csel, osel in items:
+        if len(csel) != ndim:
+            return None
+        for d, s in enumerate(csel):
+            if type(s) is slice:
+                a, b, k = s.indices(shape[d])
+                if k < 1:
+                    return None
+                S.append(a)
+                E.append(b)
+                K.append(k)
+            elif isinstance(s, (int, np.integer)):
+                v = int(s)
+                S.append(v + shape[d] if v < 0 else v)
+                E.append(0)
+                K.append(0)
+            else:
+                return None
+        oo = 0
+        for o, w in zip(osel, ostr):
+            oo += (o.start or 0) * w if type(o) is slice else int(o) * w
+        OO.append(oo)
+    g, gp, layout, index_layout, n_inner, fast_l, tile_l, rows_l = _native_ctx(chain, spec, ost_dec, fill)
+    it = np.zeros(n, N.ITEM_DT)
+    it["start"][:, :ndim] = np.array(S, np.int64).reshape(n, ndim)
+    it["stop"][:, :ndim] = np.array(E, np.int64).reshape(n, ndim)
+    it["step"][:, :ndim] = np.array(K, np.int64).reshape(n, ndim)
+    it["out_off"] = OO
+    it["src"] = [x[0] for x in items]
+    it["src_len"] = [x[1] for x in items]
+    it["missing"] = [1 if x[2] else 0 for x in items]
+    if item_out_extra is not None:
+        it["out_off"] += np.asarray(item_out_extra, np.int64)
+    cap = n * n_inner
+    ni = n if chain.shard is not None else 0
+    # one buffer: [counts 32 B][chunks cap][sels cap][item_of cap][index chunks ni][index items ni]
+    o_ch = 32
+    o_se = o_ch + cap * _CH_SZ
+    o_io = o_se + cap * _SEL_SZ
+    o_ix = o_io + 4 * cap + (-(4 * cap) % 16)
+    o_ii = o_ix + ni * _CH_SZ
+    buf = np.zeros(o_ii + 4 * ni + 16, np.uint8)
+    b = buf.ctypes.data
+    rc = N.lib().zhip_plan_batch(gp, it.ctypes.data, n, b + o_ch, cap, b, b + o_se, cap, b + 8, b + o_io,
+                                 b + o_ix, b + o_ii, b + 12, b + 16)
+    cnt = buf[:32].view(np.uint32)
+    if rc == N.E_BOUNDS and cnt[0] == 0 and cnt[1] == 0 and chain.shard is not None:
+        raise ValueError("shard blob is shorter than its index")
+    N.check(rc, "zhip_plan_batch")
+    nc, n_sels, n_idx, agg = int(cnt[0]), int(cnt[2]), int(cnt[3]), int(cnt[4])
+    chunks = buf[o_ch: o_ch + nc * _CH_SZ].view(CHUNK_DT)
+    sels = buf[o_se: o_se + n_sels * _SEL_SZ].view(SEL_DT)
+    item_of = buf[o_io: o_io + 4 * nc].view(np.uint32).astype(np.int64)
+    al = out_base_ptr % 16 == 0 and bool(agg & N.AGG_OUT_ALIGNED)
+    fast = fast_l and al and bool(agg & N.AGG_LAST_FULL)
+    tile = not fast and tile_l and al and bool(agg & N.AGG_ALL_FULL)
+    rows = fast and rows_l and bool(agg & N.AGG_UNIT_STEPS)
+    t = Tables(layout, chunks, sels, fast, item_of, tile=tile, rows=rows)
+    if n_idx:
+        t.index_layout = index_layout
+        t.index_chunks = buf[o_ix: o_ix + n_idx * _CH_SZ].view(CHUNK_DT)
+        t.index_item = buf[o_ii: o_ii + 4 * n_idx].view(np.uint32).astype(np.int64)
     return t
 
 
