@@ -18,4 +18,13 @@ rc=$?; echo "bench cpp rc=$rc"; cat $O/bench_cpp.json; tail -3 $O/bench_cpp.err
 [ $rc -ne 0 ] && exit $rc
 timeout -k 10 200 python scripts/prof_uncached.py > $O/prof_uncached.jsonl 2> $O/prof_uncached.err
 rc=$?; echo "prof rc=$rc"; head -c 600 $O/prof_uncached.jsonl
+[ $rc -ne 0 ] && exit $rc
+for w in 8 1; do
+  WORLD=$w timeout -k 10 200 python scripts/stamps.py > $O/stamps_il_w$w.jsonl 2> $O/stamps_il_w$w.err
+  rc=$?; echo "stamps w=$w rc=$rc"; [ $rc -ne 0 ] && { tail -5 $O/stamps_il_w$w.err; exit $rc; }
+done
+for cfg in share8 share4; do
+  CONFIG=$cfg ARMS="prod=0:0,ret=0:1" timeout -k 10 300 python scripts/armbench.py > $O/arms_$cfg.jsonl 2> $O/arms_$cfg.err
+  rc=$?; echo "arms $cfg rc=$rc"; cat $O/arms_$cfg.jsonl; [ $rc -ne 0 ] && { tail -5 $O/arms_$cfg.err; exit $rc; }
+done
 exit $rc

@@ -4,7 +4,7 @@
 # "transient", nothing charged).  Never retries a command that ran.
 out=$1; shift
 rc=0
-for i in $(seq 1 12); do
+for i in $(seq 1 ${GPU_RETRIES:-30}); do
   /usr/local/graft/bin/gpurun "$@" > "$out" 2>&1
   rc=$?
   if [ $rc -eq 3 ]; then echo "[retry $i: no box]" >> "$out.retries"; sleep 150; continue; fi

@@ -7,6 +7,9 @@ workgroups resident per CU over time.
 
 Slots: 0 start, 1 loads issued, 2 tables + barrier, 3 unit A stored,
 4 unit B stored, 5 CRC lookups done, 6 run end (atomic returned), 7 exit.
+k_decode_il (the default since round 3): 0 start, 1 loads issued, 2 tables
++ barrier, 3 stores and Horner steps done, 4 reduced contribution ready
+(publication issued right after), 7 exit.
 """
 import json
 import os
@@ -53,7 +56,8 @@ def main():
     N.lib().zhip_set_tuning(2, 0)
     for p in progs:
         p.results()
-    n_wg = (2048 if tune & 128 else 1024) // world
+    il = N.lib().zhip_last_kernel().decode() == "k_decode_il"
+    n_wg = (2048 if (tune & 128 or il) else 1024) // world
     buf = np.zeros(n_wg * 8, np.uint64)
     N.check(N.lib().zhip_debug_stamps(buf.ctypes.data, n_wg), "zhip_debug_stamps")
     st = buf.reshape(n_wg, 8)
@@ -62,6 +66,8 @@ def main():
     t0 = t[:, 0].min()
     rel = (t - t0) * 0.01  # 100 MHz -> us
     names = ["start", "loads_issued", "tables_barrier", "A_stored", "B_stored", "runend_barrier", "V_ready", "exit"]
+    if il:  # k_decode_il's slots (TUNE variant)
+        names = ["start", "loads_issued", "tables_barrier", "stored_hornered", "V_ready", "-", "-", "exit"]
     for i, nm in enumerate(names):
         if rel[:, i].min() < -1e3:
             continue  # slot not recorded by this variant

@@ -560,7 +560,7 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
                            : (p.tune & kTuneIlLean) ? select_il_kernel_lean(crc, p.g.itemsize, swap)
                            : (p.tune & (kTuneIlRegMul | kTuneIlOcc6))
                                ? select_il_kernel_regmul(crc, p.g.itemsize, swap, (p.tune & kTuneIlOcc6) != 0)
-                               : (p.tune & (kTuneNoTables | kTuneNoRunEnd | kTuneNoPub))
+                               : (p.tune & (kTuneNoTables | kTuneNoRunEnd | kTuneNoPub | kTuneStamp))
                                    ? select_il_kernel_tuned(crc, p.g.itemsize, swap)
                                    : select_il_kernel(crc, p.g.itemsize, swap);
             if (!ifn) return ZHIP_E_UNSUPPORTED;

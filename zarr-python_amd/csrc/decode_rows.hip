@@ -1246,6 +1246,7 @@ void k_decode_il(const DecodeParams p) {
     r = g - c * wpc;
     has = c < p.n_chunks;
     if (!has && g >= p.n_idx) return;
+    if constexpr (TUNE) stamp(p, g, t, 0);
     // 1. vector loads in a path-independent order and count: [CRC: tables (6),
     //    the lane constant, the index lane constant, the first index block],
     //    the K data blocks; headers, row-map entries and the trailer are scalar
@@ -1294,6 +1295,7 @@ void k_decode_il(const DecodeParams p) {
         const int32_t base = lo_frame + kWgStride * (int32_t)(st0 + p.il_S * (uint32_t)k);
         A[k] = load_stream16_any(ok && base >= 0 ? U.cp + base + 16 * t : zero);
     }
+    if constexpr (TUNE) stamp(p, g, t, 1);
     }
     const uint32_t S = p.il_S, wpc = p.nseg;
     // destinations of the K steps (scalar loads, consumed at the stores)
@@ -1317,6 +1319,7 @@ void k_decode_il(const DecodeParams p) {
         stt[t + 5 * kThreads] = tv5;
         if constexpr (LM == 0) lanemul3_init(s_mul, t, kl);
         __syncthreads();
+        if constexpr (TUNE) stamp(p, g, t, 2);
     }
     if (has) {
         // 3. stores, each block's Horner step after its store
@@ -1340,6 +1343,7 @@ void k_decode_il(const DecodeParams p) {
             }
         }
         // 4. run end: one chain per workgroup, one publication
+        if constexpr (TUNE) stamp(p, g, t, 3);
         if constexpr (CRC) {
             uint32_t v = ok ? ((TUNE && (p.tune & kTuneNoRunEnd)) ? acc.a0 ^ acc.a1 ^ acc.a2 ^ acc.a3  // timing arm
                                : LM == 0 ? lanemul3(s_mul, t, fold4(s_tab, acc))
@@ -1350,6 +1354,7 @@ void k_decode_il(const DecodeParams p) {
             __syncthreads();
             if (ok && t < 64 && !(TUNE && (p.tune & kTuneNoPub))) {
                 const uint32_t V = __builtin_amdgcn_readfirstlane(s_red[0][0] ^ s_red[0][1] ^ s_red[0][2] ^ s_red[0][3]);
+                if constexpr (TUNE) stamp(p, g, t, 4);
                 if constexpr (PUB == 2) {
                     if (t == 0) {  // fire and forget: nobody waits for this atomic
                         const uint32_t st = __builtin_amdgcn_readfirstlane(stored);
@@ -1377,6 +1382,7 @@ void k_decode_il(const DecodeParams p) {
             }
         }
     }
+    if constexpr (TUNE) stamp(p, g, t, 7);
     // 5. fused shard-index checks (one step per lane: launch_decode admits
     //    this kernel only then), the first block prefetched with the data
     if constexpr (CRC)
