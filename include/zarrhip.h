@@ -221,7 +221,8 @@ typedef struct zhip_item {
     uint64_t src;
     uint64_t src_len;
     int64_t out_off;
-    uint32_t missing, _pad;
+    uint32_t missing;
+    int32_t res;       /* with a zhip_resolved table: the item's shard row (-1: shard absent) */
     int64_t start[ZHIP_MAX_DIMS];
     int64_t stop[ZHIP_MAX_DIMS];
     int64_t step[ZHIP_MAX_DIMS];
@@ -239,6 +240,20 @@ typedef struct zhip_batch_geom {
     uint32_t _pad;
 } zhip_batch_geom;
 
+/* Host-staged partial shard reads (the touched inner chunks already fetched
+ * and staged by the host, staging.gather_sharded_partial): per shard row r
+ * and inner slot j, the staged offset / length / absence of the inner chunk
+ * (row-major [n_rows][n_inner]) and the staged offset of the row's index
+ * bytes (-1: no index check).  Entries then read src[r][slot] directly (an
+ * unsharded layout); index check entries are one per distinct index offset. */
+typedef struct zhip_resolved {
+    const uint64_t *src;
+    const uint64_t *len;
+    const uint8_t *missing;
+    const int64_t *index_src;
+    uint32_t n_rows, n_inner;
+} zhip_resolved;
+
 /* aggregate flags over the planned entries (layout-independent halves of the
  * kernel choice) */
 #define ZHIP_AGG_LAST_FULL 1u    /* every entry selects whole innermost stored rows        */
@@ -249,12 +264,13 @@ typedef struct zhip_batch_geom {
 /* Plan a batch: chunk entries (inner chunks of sharded items, in item order,
  * C order within an item) with their deduplicated selections (sorted rows),
  * the item of each entry, and for sharded items with a CRC'd index one index
- * check entry per distinct shard.  Capacities too small: ZHIP_E_BOUNDS with
+ * check entry per distinct shard.  `res` (NULL: none) plans host-staged
+ * partial shard reads (zhip_resolved).  Capacities too small: ZHIP_E_BOUNDS with
  * *n_chunks / *n_sels / *n_idx set to the sizes needed. */
-int zhip_plan_batch(const zhip_batch_geom *g, const zhip_item *items, uint32_t n_items, zhip_chunk *chunks,
-                    uint64_t chunks_cap, uint64_t *n_chunks, zhip_sel *sels, uint32_t sels_cap,
-                    uint32_t *n_sels, uint32_t *item_of, zhip_chunk *idx_chunks, uint32_t *idx_item,
-                    uint32_t *n_idx, uint32_t *agg);
+int zhip_plan_batch(const zhip_batch_geom *g, const zhip_item *items, uint32_t n_items,
+                    const zhip_resolved *res, zhip_chunk *chunks, uint64_t chunks_cap, uint64_t *n_chunks,
+                    zhip_sel *sels, uint32_t sels_cap, uint32_t *n_sels, uint32_t *item_of,
+                    zhip_chunk *idx_chunks, uint32_t *idx_item, uint32_t *n_idx, uint32_t *agg);
 
 /* Upload the plan's constant tables to the current HIP device (once). */
 int zhip_plan_upload(zhip_plan *plan);

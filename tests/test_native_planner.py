@@ -137,3 +137,72 @@ def test_native_planner_headline_and_short_blob():
     for native in (True, False):
         with pytest.raises(ValueError, match="shorter than its index"):
             _tables(native, chain, spec, short, ostr, 0)
+
+
+@pytest.mark.parametrize("seed", range(30))
+def test_native_planner_host_staged_matches_python(seed):
+    """Host-staged partial shard reads (plan_decode's `resolved`: inner chunks
+    fetched and staged by staging.gather_sharded_partial): items are inner-chunk
+    selections sharing their shards' staged tables, some shards absent, some
+    inner chunks absent, with and without an index check."""
+    from zarr_hip import HipCodecPipeline, planner
+    from zarr_hip.spec import ArraySpec
+
+    rng = np.random.default_rng(1000 + seed)
+    ndim = int(rng.integers(2, 4))
+    inner = tuple(int(rng.choice([2, 4, 8])) for _ in range(ndim))
+    cps = tuple(int(rng.integers(1, 4)) for _ in range(ndim))
+    shard = tuple(i * c for i, c in zip(inner, cps))
+    n_inner = int(np.prod(cps))
+    crc_ix = bool(rng.random() < 0.7)
+    codecs = [{"name": "sharding_indexed", "configuration": {
+        "chunk_shape": list(inner), "codecs": [{"name": "bytes", "configuration": {"endian": "little"}},
+                                               {"name": "crc32c"}],
+        "index_codecs": [{"name": "bytes", "configuration": {"endian": "little"}}]
+        + ([{"name": "crc32c"}] if crc_ix else [])}}]
+    spec = ArraySpec(shard, np.dtype("<f4"), 0.0)
+    pipe = HipCodecPipeline.from_codecs(codecs).evolve_from_array_spec(spec)
+    chain = planner.analyze_chain(pipe.codecs, spec)
+    n_shards = int(rng.integers(1, 6))
+    tables = []
+    top = 0
+    for s in range(n_shards):
+        if rng.random() < 0.15:
+            tables.append(None)
+            continue
+        src_by = np.zeros(n_inner, np.int64)
+        len_by = np.zeros(n_inner, np.int64)
+        miss_by = rng.random(n_inner) < 0.2
+        for j in range(n_inner):
+            if not miss_by[j]:
+                src_by[j], len_by[j] = top, 4 * int(np.prod(inner)) + 4
+                top += int(len_by[j]) + 16
+        tables.append((src_by, len_by, miss_by, top if crc_ix else -1))
+        top += 256
+    items, resolved = [], []
+    out_rows = 0
+    for k in range(int(rng.integers(3, 20))):
+        s = int(rng.integers(0, n_shards))
+        c = [int(rng.integers(0, x)) for x in cps]
+        csel = tuple(slice(ci * i, ci * i + i, 1) for ci, i in zip(c, inner))
+        osel = (slice(out_rows, out_rows + inner[0]),) + tuple(slice(0, i) for i in inner[1:])
+        out_rows += inner[0]
+        items.append((0, 0, tables[s] is None, csel, osel))
+        resolved.append(tables[s])
+    isz = 4
+    ostr = []
+    acc = isz
+    oshape = (out_rows,) + inner[1:]
+    for d in reversed(range(ndim)):
+        ostr.append(acc)
+        acc *= oshape[d]
+    ostr = list(reversed(ostr))
+    keep = planner.NATIVE_PLANNER
+    try:
+        planner.NATIVE_PLANNER = True
+        a = planner.plan_decode(chain, spec, items, ostr, 0, (), resolved, None)
+        planner.NATIVE_PLANNER = False
+        b = planner.plan_decode(chain, spec, items, ostr, 0, (), resolved, None)
+    finally:
+        planner.NATIVE_PLANNER = keep
+    _same(a, b)

@@ -176,5 +176,5 @@ def test_touched_slots_matches_projection():
                 sel.append(slice(a, b, None if r == 1 else 1))
         sel = tuple(sel)
         want = {int(x) for x in (basic_projections(sel, shape, inner).coords * strides).sum(axis=1)}
-        assert set(_touched_slots(sel, shape, inner, strides).tolist()) == want, sel
+        assert set(_touched_slots(sel, shape, inner, strides)) == want, sel
     assert _touched_slots((slice(0, 12, 2), slice(None), slice(None)), shape, inner, strides) is None

@@ -15,6 +15,7 @@
 #include <cstdint>
 #include <cstring>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "../../include/zarrhip.h"
@@ -102,16 +103,17 @@ zhip_fdiv fdiv_of(uint32_t d) {
 
 extern "C" {
 
-int zhip_plan_batch(const zhip_batch_geom* g, const zhip_item* items, uint32_t n_items, zhip_chunk* chunks,
-                    uint64_t chunks_cap, uint64_t* n_chunks, zhip_sel* sels, uint32_t sels_cap,
-                    uint32_t* n_sels, uint32_t* item_of, zhip_chunk* idx_chunks, uint32_t* idx_item,
-                    uint32_t* n_idx, uint32_t* agg) {
+int zhip_plan_batch(const zhip_batch_geom* g, const zhip_item* items, uint32_t n_items, const zhip_resolved* res,
+                    zhip_chunk* chunks, uint64_t chunks_cap, uint64_t* n_chunks, zhip_sel* sels,
+                    uint32_t sels_cap, uint32_t* n_sels, uint32_t* item_of, zhip_chunk* idx_chunks,
+                    uint32_t* idx_item, uint32_t* n_idx, uint32_t* agg) {
     if (!g || (!items && n_items) || !n_chunks || !n_sels || !n_idx || !agg) return ZHIP_E_INVALID;
     const int nd = g->ndim;
     if (nd < 1 || nd > ZHIP_MAX_DIMS) return ZHIP_E_INVALID;
     for (int s = 0; s < nd; ++s)
         if (g->perm[s] < 0 || g->perm[s] >= nd) return ZHIP_E_INVALID;
     const bool sharded = g->inner[0] > 0;
+    if (res && (!sharded || !res->src || !res->len || !res->missing || !res->index_src)) return ZHIP_E_INVALID;
     // the projection grid: inner chunks of the shard, or the chunk itself
     int64_t grid_chunk[ZHIP_MAX_DIMS], cps[ZHIP_MAX_DIMS], cps_stride[ZHIP_MAX_DIMS];
     for (int d = 0; d < nd; ++d) {
@@ -128,13 +130,15 @@ int zhip_plan_batch(const zhip_batch_geom* g, const zhip_item* items, uint32_t n
     std::unordered_map<SelKey, uint32_t, KeyHash> sel_ix;
     std::vector<SelKey> keys;
     std::vector<uint32_t> sel_of;  // per chunk entry: index into keys (insertion order)
-    std::vector<uint64_t> idx_seen;
+    std::unordered_set<uint64_t> idx_set;
     // aggregates for the layout-level kernel choice (planner._fast_ok / _rows_ok / _tile_ok)
     bool last_full = true, out_al16 = true, unit_or_single = true, all_full = true;
     const int last = nd - 1;
     for (uint32_t i = 0; i < n_items; ++i) {
         const zhip_item& it = items[i];
-        if (sharded && !it.missing && it.src_len < g->index_size) {
+        const int64_t row = res ? (int64_t)it.res : -1;
+        if (res && row >= (int64_t)res->n_rows) return ZHIP_E_INVALID;
+        if (sharded && !res && !it.missing && it.src_len < g->index_size) {
             *n_chunks = 0;
             *n_sels = 0;
             *n_idx = 0;
@@ -181,11 +185,20 @@ int zhip_plan_batch(const zhip_batch_geom* g, const zhip_item* items, uint32_t n
                 key[ZHIP_MAX_DIMS + s] = dp[d].cnt[pos[d]];
                 key[2 * ZHIP_MAX_DIMS + s] = dp[d].step;
             }
-            ch.src = it.src;
-            ch.src_len = it.src_len;
             ch.out_off = oo;
-            ch.flags = it.missing ? ZHIP_CF_MISSING : 0u;
             ch.slot = sharded ? (uint32_t)slot : 0u;
+            if (!res) {
+                ch.src = it.src;
+                ch.src_len = it.src_len;
+                ch.flags = it.missing ? ZHIP_CF_MISSING : 0u;
+            } else if (row < 0 || it.missing || (uint64_t)slot >= res->n_inner) {
+                ch.flags = ZHIP_CF_MISSING;  // src / src_len stay 0
+            } else {
+                const size_t at = (size_t)row * res->n_inner + (size_t)slot;
+                ch.src = res->src[at];
+                ch.src_len = res->len[at];
+                ch.flags = res->missing[at] ? ZHIP_CF_MISSING : 0u;
+            }
             auto f = sel_ix.find(key);
             uint32_t k;
             if (f == sel_ix.end()) {
@@ -213,13 +226,17 @@ int zhip_plan_batch(const zhip_batch_geom* g, const zhip_item* items, uint32_t n
                 pos[d] = 0;
             }
         }
-        if (sharded && !it.missing && g->index_crc &&
-            std::find(idx_seen.begin(), idx_seen.end(), it.src) == idx_seen.end()) {
-            idx_seen.push_back(it.src);
+        // one index check per distinct shard (host-staged: per distinct staged
+        // index copy, which only CRC'd indexes have)
+        const bool has_ix = res ? (row >= 0 && !it.missing && res->index_src[row] >= 0)
+                                : (sharded && !it.missing && g->index_crc);
+        const uint64_t ix_src = res ? (has_ix ? (uint64_t)res->index_src[row] : 0)
+                                    : it.src + (g->index_start ? 0 : it.src_len - g->index_size);
+        if (has_ix && idx_set.insert(ix_src).second) {
             if (idx_chunks && n_ix < n_items) {
                 zhip_chunk& ic = idx_chunks[n_ix];
                 std::memset(&ic, 0, sizeof(ic));
-                ic.src = it.src + (g->index_start ? 0 : it.src_len - g->index_size);
+                ic.src = ix_src;
                 ic.src_len = g->index_size;
                 if (idx_item) idx_item[n_ix] = i;
             }

@@ -130,11 +130,13 @@ PIECE_PINNED = 1
 PIECE_FILE = 2
 
 # zhip_item / zhip_batch_geom (include/zarrhip.h): the native host planner's input
-ITEM_DT = np.dtype([("src", "<u8"), ("src_len", "<u8"), ("out_off", "<i8"), ("missing", "<u4"), ("_pad", "<u4"),
+ITEM_DT = np.dtype([("src", "<u8"), ("src_len", "<u8"), ("out_off", "<i8"), ("missing", "<u4"), ("res", "<i4"),
                     ("start", "<i8", (MAX_DIMS,)), ("stop", "<i8", (MAX_DIMS,)), ("step", "<i8", (MAX_DIMS,))])
 GEOM_DT = np.dtype([("ndim", "<i4"), ("perm", "<i4", (MAX_DIMS,)), ("_pad0", "<i4"),
                     ("shape", "<i8", (MAX_DIMS,)), ("ost", "<i8", (MAX_DIMS,)), ("inner", "<i8", (MAX_DIMS,)),
                     ("index_size", "<u4"), ("index_start", "<u4"), ("index_crc", "<u4"), ("_pad", "<u4")])
+RESOLVED_DT = np.dtype([("src", "<u8"), ("len", "<u8"), ("missing", "<u8"), ("index_src", "<u8"),
+                        ("n_rows", "<u4"), ("n_inner", "<u4")])
 AGG_LAST_FULL, AGG_OUT_ALIGNED, AGG_UNIT_STEPS, AGG_ALL_FULL = 1, 2, 4, 8
 E_BOUNDS = -5
 
@@ -236,7 +238,7 @@ def lib():
     L.zhip_dv_check.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
     L.zhip_dv_check.restype = ctypes.c_int
     vp, u32, u64 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64
-    L.zhip_plan_batch.argtypes = [vp, vp, u32, vp, u64, vp, vp, u32, vp, vp, vp, vp, vp, vp]
+    L.zhip_plan_batch.argtypes = [vp, vp, u32, vp, vp, u64, vp, vp, u32, vp, vp, vp, vp, vp, vp]
     L.zhip_plan_batch.restype = ctypes.c_int
     L.zhip_crc32c_host.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
     L.zhip_crc32c_host.restype = ctypes.c_uint32

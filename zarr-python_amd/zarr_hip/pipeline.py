@@ -814,6 +814,18 @@ class HipCodecPipeline:
             arr = arr.transpose(order)
         return pipe, batch_s, arr
 
+    def _chain(self, spec: ArraySpec) -> ChainInfo:
+        """analyze_chain of this pipeline's codecs for a chunk spec (memoised per
+        shape and dtype: the per-call read path)."""
+        key = (spec.shape, spec.dtype.str)
+        cache = self._aux.setdefault("chains", {})
+        c = cache.get(key)
+        if c is None:
+            c = analyze_chain(self.codecs, spec)
+            if len(cache) < 64:
+                cache[key] = c
+        return c
+
     # ---------------------------------------------------------------- read
     def prepare_read(self, batch_info: Iterable, out, drop_axes: tuple = (),
                      item_out_extra=None) -> DecodeProgram:
@@ -844,7 +856,7 @@ class HipCodecPipeline:
         itemsize = out.element_size()
         if np.dtype(spec.dtype).itemsize != itemsize:
             raise TypeError("out dtype itemsize does not match the array dtype")
-        chain: ChainInfo = analyze_chain(self.codecs, spec)
+        chain: ChainInfo = self._chain(spec)
         resolved = None
         # host-resident bytes are packed and copied on the stager thread while
         # this thread plans; the launch waits for them (DecodeProgram.pending)

@@ -329,8 +329,9 @@ def plan_decode(chain: ChainInfo, spec: ArraySpec, items: list, out_strides_byte
         raise ValueError("empty batch")
     _, _, _, is_int0 = _sel_fields(items[0][3], ndim)
     ost_dec = out_dim_strides(ndim, is_int0, drop_axes, out_strides_bytes)
-    if NATIVE_PLANNER and resolved is None and (ndim > 1 or chain.shard is not None):
-        t = _plan_native(chain, spec, items, out_strides_bytes, out_base_ptr, ost_dec, item_out_extra, fill)
+    if NATIVE_PLANNER and (ndim > 1 or chain.shard is not None) and (resolved is None or chain.shard is not None):
+        t = _plan_native(chain, spec, items, out_strides_bytes, out_base_ptr, ost_dec, item_out_extra, fill,
+                         resolved)
         if t is not None:
             return t
 
@@ -475,11 +476,11 @@ NATIVE_PLANNER = __import__("os").environ.get("ZARR_HIP_NATIVE_PLANNER", "1") !=
 _NATIVE_CTX: dict = {}
 
 
-def _native_ctx(chain: ChainInfo, spec: ArraySpec, ost_dec, fill):
+def _native_ctx(chain: ChainInfo, spec: ArraySpec, ost_dec, fill, staged: bool = False):
     """Per-geometry constants of the native planner (layouts, the
     zhip_batch_geom record, the layout halves of the kernel choice), built
     once per (chain, chunk spec, out strides)."""
-    key = (chain, spec.shape, spec.dtype.str, fill, tuple(int(x) for x in ost_dec))
+    key = (chain, spec.shape, spec.dtype.str, fill, tuple(int(x) for x in ost_dec), staged)
     try:
         ctx = _NATIVE_CTX.get(key)
     except TypeError:  # an unhashable codec object in the chain: no caching
@@ -506,9 +507,13 @@ def _native_ctx(chain: ChainInfo, spec: ArraySpec, ost_dec, fill):
         g["index_size"] = index_size
         g["index_start"] = 1 if sh.index_location == "start" else 0
         g["index_crc"] = 1 if sh.index_has_crc else 0
-        flags |= N.LF_SHARDED | (N.LF_INDEX_START if sh.index_location == "start" else 0)
-        layout = _make_layout([inner_shape[p] for p in perm], spec.dtype.itemsize, [ost_dec[p] for p in perm],
-                              flags, fill, n_inner, index_size)
+        if staged:  # host-staged inner chunks: a plain launch over them (plan_decode's `resolved`)
+            layout = _make_layout([inner_shape[p] for p in perm], spec.dtype.itemsize,
+                                  [ost_dec[p] for p in perm], flags, fill)
+        else:
+            flags |= N.LF_SHARDED | (N.LF_INDEX_START if sh.index_location == "start" else 0)
+            layout = _make_layout([inner_shape[p] for p in perm], spec.dtype.itemsize,
+                                  [ost_dec[p] for p in perm], flags, fill, n_inner, index_size)
         index_layout = _make_layout([16 * n_inner], 1, [0], N.LF_CRC | N.LF_NO_WRITE, b"\0")
     else:
         layout = _make_layout([shape[p] for p in perm], spec.dtype.itemsize, [ost_dec[p] for p in perm],
@@ -537,7 +542,7 @@ _CH_SZ, _SEL_SZ = CHUNK_DT.itemsize, SEL_DT.itemsize
 
 
 def _plan_native(chain: ChainInfo, spec: ArraySpec, items: list, out_strides_bytes, out_base_ptr: int,
-                 ost_dec, item_out_extra, fill) -> "Tables | None":
+                 ost_dec, item_out_extra, fill, resolved=None) -> "Tables | None":
     """plan_decode through zhip_plan_batch: the per-item projections, inner-chunk
     expansion, selection dedup and index list in one native call; the kernel
     choice from the layout (cached per geometry) and the call's aggregate
@@ -570,7 +575,36 @@ def _plan_native(chain: ChainInfo, spec: ArraySpec, items: list, out_strides_byt
         for o, w in zip(osel, ostr):
             oo += (o.start or 0) * w if type(o) is slice else int(o) * w
         OO.append(oo)
-    g, gp, layout, index_layout, n_inner, fast_l, tile_l, rows_l = _native_ctx(chain, spec, ost_dec, fill)
+    g, gp, layout, index_layout, n_inner, fast_l, tile_l, rows_l = _native_ctx(chain, spec, ost_dec, fill,
+                                                                               resolved is not None)
+    res_p, keep = None, None
+    if resolved is not None:  # one zhip_resolved row per distinct staged shard
+        rows, row_of = [], {}
+        rix = []
+        for r in resolved:
+            if r is None:
+                rix.append(-1)
+                continue
+            j = row_of.get(id(r))
+            if j is None:
+                j = row_of[id(r)] = len(rows)
+                rows.append(r)
+            rix.append(j)
+        R = max(len(rows), 1)
+        rs = np.zeros((R, n_inner), np.uint64)
+        rl = np.zeros((R, n_inner), np.uint64)
+        rm = np.ones((R, n_inner), np.uint8)
+        ri = np.full(R, -1, np.int64)
+        for j, (src_by, len_by, miss_by, isrc) in enumerate(rows):
+            rs[j] = src_by
+            rl[j] = len_by
+            rm[j] = miss_by
+            ri[j] = isrc
+        rr = np.zeros(1, N.RESOLVED_DT)
+        rr["src"], rr["len"], rr["missing"], rr["index_src"] = rs.ctypes.data, rl.ctypes.data, rm.ctypes.data, \
+            ri.ctypes.data
+        rr["n_rows"], rr["n_inner"] = len(rows), n_inner
+        res_p, keep = rr.ctypes.data, (rs, rl, rm, ri, rr)
     it = np.zeros(n, N.ITEM_DT)
     it["start"][:, :ndim] = np.array(S, np.int64).reshape(n, ndim)
     it["stop"][:, :ndim] = np.array(E, np.int64).reshape(n, ndim)
@@ -581,6 +615,8 @@ def _plan_native(chain: ChainInfo, spec: ArraySpec, items: list, out_strides_byt
     it["missing"] = [1 if x[2] else 0 for x in items]
     if item_out_extra is not None:
         it["out_off"] += np.asarray(item_out_extra, np.int64)
+    if resolved is not None:
+        it["res"] = rix
     cap = n * n_inner
     ni = n if chain.shard is not None else 0
     # one buffer: [counts 32 B][chunks cap][sels cap][item_of cap][index chunks ni][index items ni]
@@ -591,10 +627,11 @@ def _plan_native(chain: ChainInfo, spec: ArraySpec, items: list, out_strides_byt
     o_ii = o_ix + ni * _CH_SZ
     buf = np.zeros(o_ii + 4 * ni + 16, np.uint8)
     b = buf.ctypes.data
-    rc = N.lib().zhip_plan_batch(gp, it.ctypes.data, n, b + o_ch, cap, b, b + o_se, cap, b + 8, b + o_io,
-                                 b + o_ix, b + o_ii, b + 12, b + 16)
+    rc = N.lib().zhip_plan_batch(gp, it.ctypes.data, n, res_p, b + o_ch, cap, b, b + o_se, cap, b + 8,
+                                 b + o_io, b + o_ix, b + o_ii, b + 12, b + 16)
+    del keep
     cnt = buf[:32].view(np.uint32)
-    if rc == N.E_BOUNDS and cnt[0] == 0 and cnt[1] == 0 and chain.shard is not None:
+    if rc == N.E_BOUNDS and cnt[0] == 0 and cnt[1] == 0 and chain.shard is not None and resolved is None:
         raise ValueError("shard blob is shorter than its index")
     N.check(rc, "zhip_plan_batch")
     nc, n_sels, n_idx, agg = int(cnt[0]), int(cnt[2]), int(cnt[3]), int(cnt[4])

@@ -328,22 +328,30 @@ def _shard_key(bg):
 def _touched_slots(csel, shard_shape, inner_shape, strides):
     """Linear inner-chunk slots a chunk selection of ints and unit-step slices
     touches, by interval arithmetic; None for other forms (the caller then
-    projects: strided slices may skip inner chunks)."""
-    slots = np.zeros(1, np.int64)
-    for s, n, c, st in zip(csel, shard_shape, inner_shape, strides):
-        if isinstance(s, (int, np.integer)):
-            i = int(s) + (int(n) if int(s) < 0 else 0)
-            lo, hi = i // c, i // c + 1
-        elif isinstance(s, slice):
-            a, b, step = s.indices(int(n))
+    projects: strided slices may skip inner chunks).  A list of ints."""
+    los, his = [], []
+    for s, n, c in zip(csel, shard_shape, inner_shape):
+        if type(s) is slice:
+            a, b, step = s.indices(n)
             if step != 1:
                 return None
             if a >= b:
-                return np.zeros(0, np.int64)
-            lo, hi = a // c, (b - 1) // c + 1
+                return []
+            los.append(a // c)
+            his.append((b - 1) // c + 1)
+        elif isinstance(s, (int, np.integer)):
+            i = int(s) + (n if int(s) < 0 else 0)
+            los.append(i // c)
+            his.append(i // c + 1)
         else:
             return None
-        slots = (slots[:, None] + np.arange(lo, hi, dtype=np.int64)[None, :] * int(st)).reshape(-1)
+    slots = [0]
+    for lo, hi, st in zip(los, his, strides):
+        if hi - lo == 1:
+            off = lo * st
+            slots = [x + off for x in slots]
+        else:
+            slots = [x + k * st for x in slots for k in range(lo, hi)]
     return slots
 
 
@@ -362,6 +370,9 @@ def gather_sharded_partial(batch: list, sh, cps, n_inner: int, inner_shape, spec
     isz = sh.shard_index_size(n_inner)
     lay = StagingLayout()
     cps_strides = np.array([int(np.prod(cps[d + 1:])) for d in range(len(cps))], np.int64)
+    st_list = [int(x) for x in cps_strides]
+    sshape = tuple(int(x) for x in spec.shape)
+    ishape = tuple(int(x) for x in inner_shape)
     shards: dict = {}
     item_shard = []
     for item in batch:
@@ -369,11 +380,11 @@ def gather_sharded_partial(batch: list, sh, cps, n_inner: int, inner_shape, spec
         if k not in shards:
             shards[k] = {"bg": item[0], "slots": set()}
         csel = tuple(item[2])
-        sl = _touched_slots(csel, spec.shape, inner_shape, cps_strides) if len(csel) == len(spec.shape) else None
+        sl = _touched_slots(csel, sshape, ishape, st_list) if len(csel) == len(sshape) else None
         if sl is None:
             pr = basic_projections(csel, spec.shape, inner_shape)
-            sl = (pr.coords * cps_strides[None, :]).sum(axis=1)
-        shards[k]["slots"].update(sl.tolist())
+            sl = (pr.coords * cps_strides[None, :]).sum(axis=1).tolist()
+        shards[k]["slots"].update(sl)
         item_shard.append(k)
     out_of_shard = {}
     for k, s in shards.items():
