@@ -1265,16 +1265,8 @@ void k_decode_il(const DecodeParams p) {
         tv5 = gt[ti + 5 * ts];
         kl = load_u32_any(reinterpret_cast<const uint8_t*>(p.il_klane + (size_t)(has ? r : 0u) * kThreads + t));
         kix = load_u32_any(reinterpret_cast<const uint8_t*>(p.il_kidx + t));
-        if constexpr (PUB == 2) {
-            // the previous launch's verdict of this chunk (the other bank),
-            // read by its first workgroup; one address for every lane, and
-            // the same load on every path (static vmcnt)
-            const bool chk = has && r == 0;
-            dvprev = __hip_atomic_load(reinterpret_cast<const uint64_t*>(
-                                           chk ? p.ws + 4ull * c + 2u * (p.dv_bank ^ 1u)
-                                               : reinterpret_cast<const uint32_t*>(g_rows_zero)),
-                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        // the previous launch's verdict of this chunk (deferred verdicts)
+        if constexpr (PUB == 2) dvprev = dv_prev(p, c, has && r == 0, g_rows_zero);
     }
     if (has) U = resolve_unit(p, c * p.nseg, expected);
     else {
@@ -1356,13 +1348,7 @@ void k_decode_il(const DecodeParams p) {
                 const uint32_t V = __builtin_amdgcn_readfirstlane(s_red[0][0] ^ s_red[0][1] ^ s_red[0][2] ^ s_red[0][3]);
                 if constexpr (TUNE) stamp(p, g, t, 4);
                 if constexpr (PUB == 2) {
-                    if (t == 0) {  // fire and forget: nobody waits for this atomic
-                        const uint32_t st = __builtin_amdgcn_readfirstlane(stored);
-                        uint32_t* w = p.ws + 4ull * c + 2u * p.dv_bank;
-                        __hip_atomic_fetch_xor(w, V ^ (r == 0 ? (p.c3 ^ ~st) : 0u), __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
-                        if (r == 0) __hip_atomic_store(w + 1, st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    }
+                    if (t == 0) dv_publish(p, c, r == 0, V, __builtin_amdgcn_readfirstlane(stored));
                 } else {
                     publish_il(p, c, r, wpc, V, __builtin_amdgcn_readfirstlane(stored), t);
                 }
@@ -1371,16 +1357,8 @@ void k_decode_il(const DecodeParams p) {
         // (deferred verdicts: the status of a present chunk is OK here; a
         // mismatch is reported from its bank word)
         if (r == 0) unit_status_pair(p, U, CRC && PUB != 2, t);
-        if constexpr (CRC && PUB == 2) {
-            const uint32_t pw = (uint32_t)dvprev, ps = (uint32_t)(dvprev >> 32);
-            if (r == 0 && t == 0 && pw != 0u) {  // the previous launch's mismatch: sticky
-                zhip_status st = {ZHIP_ST_CRC_MISMATCH, ps, pw ^ ps, 0u};
-                p.status[c] = st;
-                atomicOr(p.errflag, 1u << ZHIP_ST_CRC_MISMATCH);
-                __hip_atomic_store(p.ws + 4ull * c + 2u * (p.dv_bank ^ 1u), 0u, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
+        if constexpr (CRC && PUB == 2)
+            if (r == 0 && t == 0) dv_settle(p, c, dvprev);  // the previous launch's mismatch: sticky
     }
     if constexpr (TUNE) stamp(p, g, t, 7);
     // 5. fused shard-index checks (one step per lane: launch_decode admits

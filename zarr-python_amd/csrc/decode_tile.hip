@@ -113,7 +113,11 @@ __device__ __forceinline__ uint4 tile_get16(const uint8_t* s, uint32_t r, uint32
 
 }  // namespace
 
-template <bool CRC, int ITEM, bool SWAP>
+// PUB: 2 = deferred CRC verdicts (zarrhip.h; production since round 4: a
+// non-returning xor per workgroup, the first workgroup of a chunk checks the
+// previous launch's verdict); 0 = round 3's returning publication with
+// arrival bits (arm ZHIP_TUNE_ARM = 2).
+template <bool CRC, int ITEM, bool SWAP, int PUB = 2>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_decode_tile4(
     const DecodeParams p) {
     constexpr int kPer = 16 / ITEM;                // rows per 16-byte out piece
@@ -141,6 +145,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
         tzv = reinterpret_cast<const uint4*>(p.tz)[t];
         kq = p.kq4[(size_t)grp * kThreads + t];
     }
+    uint64_t dvprev = 0;
+    if constexpr (CRC && PUB == 2) dvprev = dv_prev(p, c, grp == 0, g_tile_zero);
     const Unit U = resolve_unit(p, c * p.nseg, expected);
     const TileMap4 tm = load_uniform<TileMap4>(p.tmap + (size_t)grp * kTiles);
     const bool ok = U.mode == ZHIP_ST_OK;
@@ -231,7 +237,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
         if (t < 64) {
             const uint32_t V = __builtin_amdgcn_readfirstlane(s_red[0] ^ s_red[1] ^ s_red[2] ^ s_red[3]);
             uint32_t raw = 0, last_arrival = 0;
-            if (t == 0) {
+            if (PUB == 2) {
+                if (t == 0) dv_publish(p, c, grp == 0, V, __builtin_amdgcn_readfirstlane(stored));
+            } else if (t == 0) {
                 if (gpc <= 32) {
                     const uint64_t full = gpc == 32 ? 0xFFFFFFFFull : ((1ull << gpc) - 1ull);
                     const uint64_t bits = 1ull << grp;
@@ -264,10 +272,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
             }
         }
     }
-    // statuses not produced by the CRC finalize
+    // statuses not produced by the CRC finalize (deferred verdicts: a present
+    // chunk is OK here, a mismatch is reported from its bank word)
     if (grp == 0 && t == 0) {
         if (ok) {
-            if (!CRC) {
+            if (!CRC || PUB == 2) {
                 zhip_status st = {ZHIP_ST_OK, 0u, 0u, 0u};
                 p.status[c] = st;
             }
@@ -276,6 +285,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
             p.status[c] = st;
             if (U.mode != ZHIP_ST_MISSING) atomicOr(p.errflag, 1u << U.mode);
         }
+        if constexpr (CRC && PUB == 2) dv_settle(p, c, dvprev);
     }
 }
 
@@ -479,8 +489,9 @@ __device__ __forceinline__ bool tileg_arrive(uint32_t* ws, uint32_t n_chunks, ui
 // image -> out pieces -> 16-byte stores (failed chunks to a sink, a static
 // count) -> Horner steps, the state carried by one table multiply -- and one
 // lane multiply, one reduction and one XOR + arrival pair per workgroup (any
-// number of groups per chunk).
-template <bool CRC, int ITEM, bool SWAP>
+// number of groups per chunk).  PUB as in k_decode_tile4 (2: deferred CRC
+// verdicts, production; 0: the returning two-level arrival, arm 2).
+template <bool CRC, int ITEM, bool SWAP, int PUB = 2>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_decode_tileg(
     const DecodeParams p) {
     constexpr int kPer = 16 / ITEM;
@@ -505,6 +516,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
         tzv = reinterpret_cast<const uint4*>(p.gtz)[t];
         kth = p.kthread[t];
     }
+    uint64_t dvprev = 0;
+    if constexpr (CRC && PUB == 2) dvprev = dv_prev(p, c, grp == 0, g_tile_zero);
     const Unit U = resolve_unit(p, c * p.nseg, expected);
     const GroupEnt ge = load_uniform<GroupEnt>(p.gmap + grp);
     const bool ok = U.mode == ZHIP_ST_OK;
@@ -593,7 +606,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
         uint32_t v = wave_xor(gf_mul(S, kth));
         if ((t & 63) == 0) s_red[t >> 6] = v;
         __syncthreads();
-        if (t == 0) {
+        if (t == 0 && PUB == 2) {
+            dv_publish(p, c, grp == 0, gf_mul(s_red[0] ^ s_red[1] ^ s_red[2] ^ s_red[3], ge.ku), stored);
+        } else if (t == 0) {
             const uint32_t V = gf_mul(s_red[0] ^ s_red[1] ^ s_red[2] ^ s_red[3], ge.ku);
             uint32_t raw = 0;
             bool last_one = false;
@@ -622,7 +637,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     }
     if (grp == 0 && t == 0) {
         if (ok) {
-            if (!CRC) {
+            if (!CRC || PUB == 2) {
                 zhip_status st = {ZHIP_ST_OK, 0u, 0u, 0u};
                 p.status[c] = st;
             }
@@ -631,6 +646,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
             p.status[c] = st;
             if (U.mode != ZHIP_ST_MISSING) atomicOr(p.errflag, 1u << U.mode);
         }
+        if constexpr (CRC && PUB == 2) dv_settle(p, c, dvprev);
     }
 }
 
@@ -1214,6 +1230,7 @@ EncodeFn select_encode_tile4_kernel(bool crc, int item, bool swap) {
 }
 
 KernelFn select_tileg_kernel(bool crc, int item, bool swap) {
+    if (g_tune_arm == 2 && crc && item == 4 && !swap) return k_decode_tileg<true, 4, false, 0>;  // returning arm
     switch (item) {
         case 1: return crc ? k_decode_tileg<true, 1, false> : k_decode_tileg<false, 1, false>;
         case 2: return crc ? (swap ? k_decode_tileg<true, 2, true> : k_decode_tileg<true, 2, false>)
@@ -1237,6 +1254,7 @@ KernelFn select_tile4f_kernel(int item, bool swap) {  // CRC chains only
 }
 
 KernelFn select_tile4_kernel(bool crc, int item, bool swap) {
+    if (g_tune_arm == 2 && crc && item == 4 && !swap) return k_decode_tile4<true, 4, false, 0>;  // returning arm
     switch (item) {
         case 1: return crc ? k_decode_tile4<true, 1, false> : k_decode_tile4<false, 1, false>;
         case 2: return crc ? (swap ? k_decode_tile4<true, 2, true> : k_decode_tile4<true, 2, false>)

@@ -230,6 +230,41 @@ __device__ __forceinline__ uint32_t load_trailer(const uint8_t* cp, uint32_t n) 
     return (uint32_t)tr[0] | ((uint32_t)tr[1] << 8) | ((uint32_t)tr[2] << 16) | ((uint32_t)tr[3] << 24);
 }
 
+// ---- deferred CRC verdicts (zarrhip.h), shared by the decode kernels that
+// publish without a returning atomic ----
+// {word, stored} of chunk c in the OTHER bank (the previous launch's verdict),
+// read by the chunk's first workgroup; one address for every lane (`zero`
+// otherwise), so every path issues the same vector load.
+__device__ __forceinline__ uint64_t dv_prev(const DecodeParams& p, uint32_t c, bool first, const void* zero) {
+    return __hip_atomic_load(reinterpret_cast<const uint64_t*>(
+                                 first ? p.ws + 4ull * c + 2u * (p.dv_bank ^ 1u) : static_cast<const uint32_t*>(zero)),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// One lane: xor the workgroup's (chunk-referenced) contribution into this
+// launch's bank word -- the first workgroup also folds in c3 ^ ~stored, so
+// the word ends as computed ^ stored -- and record the trailer.  The atomic's
+// result is unused: nobody waits for its round trip.
+__device__ __forceinline__ void dv_publish(const DecodeParams& p, uint32_t c, bool first, uint32_t V,
+                                           uint32_t stored) {
+    uint32_t* w = p.ws + 4ull * c + 2u * p.dv_bank;
+    __hip_atomic_fetch_xor(w, V ^ (first ? (p.c3 ^ ~stored) : 0u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (first) __hip_atomic_store(w + 1, stored, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// One lane of the first workgroup, after the chunk's own status: a nonzero
+// previous verdict is the previous launch's mismatch (sticky status + error
+// bit); its word is cleared for the launch after this one.
+__device__ __forceinline__ void dv_settle(const DecodeParams& p, uint32_t c, uint64_t prev) {
+    const uint32_t pw = (uint32_t)prev, ps = (uint32_t)(prev >> 32);
+    if (pw != 0u) {
+        zhip_status st = {ZHIP_ST_CRC_MISMATCH, ps, pw ^ ps, 0u};
+        p.status[c] = st;
+        atomicOr(p.errflag, 1u << ZHIP_ST_CRC_MISMATCH);
+        __hip_atomic_store(p.ws + 4ull * c + 2u * (p.dv_bank ^ 1u), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 // CRC-32C check of one shard index (payload idx_nbytes + LE trailer) by one
 // workgroup: the same per-thread Horner chain as a data unit ending at idx_E
 // (reference point idx_E + 4096), reduced over the workgroup.  `red` is a

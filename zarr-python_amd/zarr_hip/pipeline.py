@@ -183,14 +183,16 @@ class DecodeLaunch:
             return
         s = _stream_handle(self.device) if stream is None else stream
         out_ptr = self.out.data_ptr() if self.out is not None else None
+        # deferred CRC verdicts (zarrhip.h): consecutive launches publish into
+        # alternate workspace banks (also while captured into a graph)
+        flags = self.flags | (N.DF_BANK1 if self._bank else 0)
+        self._bank ^= 1
         if self.d_rowmap is not None:
-            bank = self._bank
-            self._bank ^= 1  # consecutive launches publish into alternate banks (also while captured)
             N.check(N.lib().zhip_decode_mapped(
                 self.plan.handle, self.src.data_ptr(), self.src_size, out_ptr, self.d_chunks.data_ptr(),
                 self.n, self.d_sels.data_ptr(), self.d_status.data_ptr(), self.d_ws.data_ptr(),
                 self.d_err.data_ptr(), self.d_idx_chunks.data_ptr() if self.n_idx else None, self.n_idx,
-                self.d_idx_status.data_ptr() if self.n_idx else None, self.flags | (N.DF_BANK1 if bank else 0),
+                self.d_idx_status.data_ptr() if self.n_idx else None, flags,
                 self.predict, self.d_rowmap.data_ptr(), s), "zhip_decode_mapped")
             return
         if self.predict is not None:
@@ -198,7 +200,7 @@ class DecodeLaunch:
                 self.plan.handle, self.src.data_ptr(), self.src_size, out_ptr, self.d_chunks.data_ptr(),
                 self.n, self.d_sels.data_ptr(), self.d_status.data_ptr(), self.d_ws.data_ptr(),
                 self.d_err.data_ptr(), self.d_idx_chunks.data_ptr() if self.n_idx else None, self.n_idx,
-                self.d_idx_status.data_ptr() if self.n_idx else None, self.flags, self.predict, s),
+                self.d_idx_status.data_ptr() if self.n_idx else None, flags, self.predict, s),
                 "zhip_decode_predicted")
             return
         if self.n_idx:
@@ -206,12 +208,12 @@ class DecodeLaunch:
                 self.plan.handle, self.src.data_ptr(), self.src_size, out_ptr, self.d_chunks.data_ptr(),
                 self.n, self.d_sels.data_ptr(), self.d_status.data_ptr(), self.d_ws.data_ptr(),
                 self.d_err.data_ptr(), self.d_idx_chunks.data_ptr(), self.n_idx,
-                self.d_idx_status.data_ptr(), self.flags, s), "zhip_decode_indexed")
+                self.d_idx_status.data_ptr(), flags, s), "zhip_decode_indexed")
             return
         N.check(N.lib().zhip_decode(self.plan.handle, self.src.data_ptr(), self.src_size, out_ptr,
                                     self.d_chunks.data_ptr(), self.n, self.d_sels.data_ptr(),
                                     self.d_status.data_ptr(), self.d_ws.data_ptr(),
-                                    self.d_err.data_ptr(), self.flags, s), "zhip_decode")
+                                    self.d_err.data_ptr(), flags, s), "zhip_decode")
 
     def launch_range(self, first: int, count: int, src, src_size: int, stream: int | None = None) -> None:
         """Chunks [first, first + count) of the table, reading from `src` (the
@@ -235,8 +237,8 @@ class DecodeLaunch:
                 None, self.d_rowmap.data_ptr(), s), "zhip_decode_mapped")
             return
         N.check(N.lib().zhip_decode(self.plan.handle, src.data_ptr(), src_size, out_ptr, chunks, count,
-                                    self.d_sels.data_ptr(), status, ws, self.d_err.data_ptr(), self.flags, s),
-                "zhip_decode")
+                                    self.d_sels.data_ptr(), status, ws, self.d_err.data_ptr(),
+                                    self.flags | (N.DF_BANK1 if self._bank else 0), s), "zhip_decode")
 
     def statuses(self) -> np.ndarray:
         """Per-chunk statuses with the deferred CRC verdicts merged in: a
@@ -433,7 +435,7 @@ class ReadGraph:
         # zhip_dv_check node over every program's workspace
         counts = [len(range(j, self.repeats, len(self.programs))) for j in range(len(self.programs))]
         launches = [getattr(p, "data", None) for p in self.programs]
-        odd = any(c % 2 for c, d in zip(counts, launches) if d is not None and getattr(d, "d_rowmap", None) is not None)
+        odd = any(c % 2 for c, d in zip(counts, launches) if d is not None and hasattr(d, "d_ws"))
         self._dv_refs = _dv_refs([d for d in launches if d is not None], self.device) if odd else None
         with torch.cuda.device(self.device):
             with torch.cuda.graph(self.graph, stream=self.stream):
