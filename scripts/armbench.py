@@ -5,7 +5,8 @@ ARMS: comma list of name=bits:arm (bits = zhip_set_tuning(ABLATION), arm =
 zhip_set_tuning(ARM)); each arm is a hipGraph of REPS launches rotating over
 4 replicas (the Infinity Cache cannot serve re-reads), replayed ROUNDS times,
 interleaved with the other arms in ONE process.  CONFIG = headline | c4 |
-share8 (rank 0's 1-shard share of the headline at N = 8) | share4.  Also
+share8 (rank 0's 1-shard share of the headline at N = 8) | share4 | c3 | c3g
+(transpose (2,1,0) in 64^3 / 128^3 chunks).  Also
 the no-CRC twin (zarr's default sharding codecs, k_decode_lead) for the
 headline.  One JSON line per arm: min / median us per launch and the HBM
 fraction of the algorithmic bytes.  After timing, the production arm's
@@ -43,16 +44,24 @@ def main():
         keep = 8 // int(cfg[5:])
         shape = {1: (128, 128, 128), 2: (128, 128, 256), 4: (128, 256, 256)}[keep]
         data = data[: shape[0], : shape[1], : shape[2]].contiguous()
+    aa = []
+    if cfg in ("c3", "c3g"):  # C3: transpose (2,1,0) + bytes + crc32c, unsharded 64^3 / 128^3 chunks
+        aa = [{"name": "transpose", "configuration": {"order": [2, 1, 0]}}]
+        inner = (128, 128, 128) if cfg == "c3g" else (64, 64, 64)
+        shards = None
     R = 2 if cfg == "c4" else 4
     reps = int(os.environ.get("REPS", "4" if cfg == "c4" else "20"))
-    crc = [bench.build_replica(dev, data, shape, inner, [W.LE, W.CRC], shards=shards).prepare_read((Ellipsis,))
+    crc = [bench.build_replica(dev, data, shape, inner, aa + [W.LE, W.CRC], shards=shards).prepare_read((Ellipsis,))
            for _ in range(R)]
-    nocrc = [bench.build_replica(dev, data, shape, inner, [W.LE], shards=shards).prepare_read((Ellipsis,))
+    nocrc = [bench.build_replica(dev, data, shape, inner, aa + [W.LE], shards=shards).prepare_read((Ellipsis,))
              for _ in range(R)] if cfg != "c4" else []
     n_inner = int(np.prod([s // i for s, i in zip(shape, inner)]))
-    n_shards = int(np.prod([s // i for s, i in zip(shape, shards)]))
-    cps = n_inner // n_shards
-    alg = n_inner * (int(np.prod(inner)) * 4 + 4) + n_shards * (cps * 16 + 4) + data.numel() * 4
+    if shards is not None:
+        n_shards = int(np.prod([s // i for s, i in zip(shape, shards)]))
+        cps = n_inner // n_shards
+        alg = n_inner * (int(np.prod(inner)) * 4 + 4) + n_shards * (cps * 16 + 4) + data.numel() * 4
+    else:
+        alg = n_inner * (int(np.prod(inner)) * 4 + 4) + data.numel() * 4
 
     def graph_of(progs):
         s = torch.cuda.Stream(dev)
