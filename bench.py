@@ -419,6 +419,28 @@ def device_read_call(device, args):
     for i in range(R):
         if not torch.equal(outs[i].view(torch.int32), src.view(torch.int32)):
             raise SystemExit("bench device_read_call: decoded bytes differ from the source")
+    # a data loader walking the array: a DIFFERENT selection every call (128-row
+    # windows at 8 offsets, crossing shard boundaries), plan cache off
+    sels = [(slice(16 * i + 8, 16 * i + 136), slice(None), slice(None)) for i in range(8)]
+    wouts = [torch.empty((128,) + tuple(shape[1:]), dtype=torch.float32, device=device) for _ in sels]
+    wb = [arrs[0].batch_info(sl)[0] for sl in sels]
+    wprogs = [arrs[0].codec_pipeline.prepare_read(b, o) for b, o in zip(wb, wouts)]
+    wkern = float(np.median(eager_kernel_times(wprogs, max(16, args.steps), device)))
+    del wprogs
+    keep, P.READ_CACHE_SIZE = P.READ_CACHE_SIZE, 0
+    try:
+        ctr = [0]
+
+        def walk(_i):
+            j = ctr[0] = (ctr[0] + 1) % 8
+            arrs[0].codec_pipeline.read_sync(wb[j], wouts[j])
+
+        varying = timed(walk)
+    finally:
+        P.READ_CACHE_SIZE = keep
+    for i in range(8):
+        if not torch.equal(wouts[i].view(torch.int32), src[sels[i]].contiguous().view(torch.int32)):
+            raise SystemExit("bench device_read_call: a window read differs from the source")
     dec = src.numel() * 4
 
     def line(w):
@@ -428,6 +450,11 @@ def device_read_call(device, args):
     return {"kernel_ms": round(kern * 1e3, 4), "calls": n, "first_call_ms": round(first_ms, 3),
             "read_sync_cached": line(cached), "array_get_cached": line(get),
             "read_sync_uncached": line(uncached), "checked": "bytes",
+            "read_sync_uncached_varying": {
+                "ms_per_call": round(varying * 1e3, 4), "kernel_ms": round(wkern * 1e3, 4),
+                "host_overhead_ms": round((varying - wkern) * 1e3, 4),
+                "decoded_GiBps": round(128 * 256 * 256 * 4 / varying / GIB, 1),
+                "note": "a different 128-row window (16 MiB) every call, plan cache off"},
             "note": "headline config; eager per-call reads, each synchronised; kernel_ms = median "
                     "event-timed eager launch of the same program"}
 
