@@ -161,6 +161,10 @@ int zhip_plan_info(const zhip_plan *plan, uint32_t *units_per_chunk, uint32_t *w
                             (whole 16-byte pieces along the out-contiguous dim): where
                             k_decode_tile4 / k_encode_tile4 do not apply, full-selection
                             batches run k_decode_tileg / k_encode_tileg */
+#define ZHIP_PK_IL 16u   /* whole-row layout whose chunks decode in k_decode_il by default
+                            (groups of eight 32 KiB workgroups, a trailing crc32c): that
+                            kernel resolves its units itself, a load-address prediction
+                            (zhip_predict) is not used */
 int zhip_plan_kernel_flags(const zhip_plan *plan, uint32_t *flags);
 
 /* decode flags (zhip_decode decode_flags) */

@@ -661,11 +661,13 @@ def test_predicted_loads_engaged_and_exact(device, loc):
     """Default Morton packing: the load-address prediction fits (one 2-level
     progression) and the decode is bit-exact; a missing inner chunk turns the
     prediction off for its batch."""
+    # 128 KiB inner chunks (four units: the pair kernel, which uses the
+    # prediction; k_decode_il's layouts resolve their own units, no prediction)
     arr, host, meta = _roundtrip(device, (128, 128, 64), (64, 64, 64), "float32",
-                                 [SHARD((32, 32, 64), [LE, CRC], loc)])
+                                 [SHARD((32, 32, 32), [LE, CRC], loc)])
     prog, out = arr.prepare_read((Ellipsis,))
     assert prog.tables.rows and prog.tables.predict is not None
-    assert prog.tables.predict.per == 4
+    assert prog.tables.predict.per == 8
     prog.launch()
     prog.results()
     from zarr_hip.buffer import to_numpy

@@ -553,7 +553,8 @@ int zhip_plan_kernel_flags(const zhip_plan* p, uint32_t* flags) {
     if (!p || !flags) return set_err(ZHIP_E_INVALID, "null argument");
     *flags = (p->tile4 ? ZHIP_PK_TILE4 : 0u) | (p->tile4 && p->t_per_chunk <= 64 ? ZHIP_PK_TILE4_ENCODE : 0u) |
              (p->tq >= 0 ? ZHIP_PK_TILE : 0u) |
-             (p->gd >= 0 && p->layout.shape[p->tq] % (16 / p->layout.itemsize) == 0 ? ZHIP_PK_TILEG : 0u);
+             (p->gd >= 0 && p->layout.shape[p->tq] % (16 / p->layout.itemsize) == 0 ? ZHIP_PK_TILEG : 0u) |
+             (p->il_S == 8u && (p->layout.flags & ZHIP_LF_CRC) ? ZHIP_PK_IL : 0u);
     return ZHIP_OK;
 }
 

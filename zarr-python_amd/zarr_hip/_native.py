@@ -44,6 +44,7 @@ PK_TILE4 = 1
 PK_TILE4_ENCODE = 2
 PK_TILE = 4
 PK_TILEG = 8
+PK_IL = 16
 
 PF_INDEX_START = 1
 PF_INDEX_CRC = 2

@@ -104,6 +104,15 @@ def get_plan(layout: N.Layout) -> N.Plan:
     return p
 
 
+def _kernel_flags(layout: N.Layout) -> int:
+    """zhip_plan_kernel_flags of the layout's plan, memoised on the plan."""
+    p = get_plan(layout)
+    f = getattr(p, "_pk", None)
+    if f is None:
+        f = p._pk = p.kernel_flags
+    return f
+
+
 def _rows_map_host(plan, sels: np.ndarray):
     """zhip_rows_map over the host copy of the selections; None when the
     library declines the layout (then the launch takes the persistent row
@@ -878,7 +887,8 @@ class HipCodecPipeline:
             ostr = [int(s) * itemsize for s in out.stride()]
             with torch.cuda.device(device):
                 t = plan_decode(chain, spec, items, ostr, out.data_ptr(), drop_axes, resolved, item_out_extra)
-                if self.predict_loads:
+                # (k_decode_il resolves its own units: no prediction to build)
+                if self.predict_loads and t.rows and not (_kernel_flags(t.layout) & N.PK_IL):
                     predict_rows(t, chain, spec, size)
                 # fuse the shard-index CRC checks into the data launch
                 # (zhip_decode_indexed: needs the CRC tables, i.e. an inner crc32c, and

@@ -650,6 +650,22 @@ def _plan_native(chain: ChainInfo, spec: ArraySpec, items: list, out_strides_byt
     return t
 
 
+_MORTON_RANK: dict = {}
+
+
+def _morton_rank(cps: tuple) -> np.ndarray:
+    """Morton rank of every C-order inner-chunk slot of a shard (memoised)."""
+    r = _MORTON_RANK.get(cps)
+    if r is None:
+        morton = morton_order(cps)
+        cstr = np.array([int(np.prod(cps[d + 1:])) for d in range(len(cps))], np.int64)
+        r = np.zeros(int(np.prod(cps)), np.int64)
+        r[(morton * cstr[None, :]).sum(axis=1)] = np.arange(len(morton))
+        if len(_MORTON_RANK) < 64:
+            _MORTON_RANK[cps] = r
+    return r
+
+
 def predict_rows(t: Tables, chain: ChainInfo, spec: ArraySpec, src_size: int) -> None:
     """Load-address prediction for a whole-row batch (zhip_decode_predicted).
 
@@ -674,10 +690,7 @@ def predict_rows(t: Tables, chain: ChainInfo, spec: ArraySpec, src_size: int) ->
     if L.flags & N.LF_SHARDED:
         sh = chain.shard
         cps = tuple(int(c) for c in sh.chunks_per_shard(spec.shape))
-        morton = morton_order(cps)
-        cstr = np.array([int(np.prod(cps[d + 1:])) for d in range(len(cps))], np.int64)
-        rank_of_slot = np.zeros(int(np.prod(cps)), np.int64)
-        rank_of_slot[(morton * cstr[None, :]).sum(axis=1)] = np.arange(len(morton))
+        rank_of_slot = _morton_rank(cps)
         elen = nbytes + (4 if chain.inner.crc else 0)
         start = int(L.index_size) if L.flags & N.LF_INDEX_START else 0
         pred = ch["src"].astype(np.int64) + start + rank_of_slot[ch["slot"].astype(np.int64)] * elen
