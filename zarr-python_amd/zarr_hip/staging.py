@@ -420,11 +420,12 @@ def gather_sharded_partial(batch: list, sh, cps, n_inner: int, inner_shape, spec
         slots = sorted(s["slots"])
         reqs = []
         want = []
+        ent = idx.reshape(-1).tolist()  # plain ints: (offset, length) per slot
         for slot in slots:
-            o, n = idx[slot]
+            o, n = ent[2 * slot], ent[2 * slot + 1]
             if o == MAX_U64 and n == MAX_U64:
                 continue  # missing inner chunk -> fill (sharding.py:700-712)
-            reqs.append(Range(int(o), int(o) + int(n)))
+            reqs.append(Range(o, o + n))
             want.append(slot)
         if reqs and st is not None and hasattr(st, "locate_sync") and inner_decode is None:
             # a local file: each touched inner chunk is one pread of the shard
