@@ -24,7 +24,7 @@ for w in 8 1; do
   rc=$?; echo "stamps w=$w rc=$rc"; [ $rc -ne 0 ] && { tail -5 $O/stamps_il_w$w.err; exit $rc; }
 done
 for cfg in share8 share4 c3 c3g c4; do
-  A="prod=0:0,ret=0:1"; case $cfg in c3*) A="prod=0:0,ret=0:2";; c4) A="prod=0:0,il=67108864:0,il_ret=67108864:1";; esac
+  A="prod=0:0,ret=0:1,lean=16384:0"; case $cfg in c3*) A="prod=0:0,ret=0:2";; c4) A="prod=0:0,il=67108864:0,il_ret=67108864:1";; esac
   CONFIG=$cfg ARMS="$A" timeout -k 10 300 python scripts/armbench.py > $O/arms_$cfg.jsonl 2> $O/arms_$cfg.err
   rc=$?; echo "arms $cfg rc=$rc"; cat $O/arms_$cfg.jsonl; [ $rc -ne 0 ] && { tail -5 $O/arms_$cfg.err; exit $rc; }
 done
