@@ -1094,23 +1094,23 @@ __global__ __launch_bounds__(2 * kThreads) __attribute__((amdgpu_waves_per_eu(8,
 // statuses, stores (row map, sink for unselected rows), fused index checks
 // (one step per lane; the constants carry the A_D frame) as k_decode_pair.
 // (CPU emulation: zhip_emulate_chunk_crc_il.)
+// timing arms of the publication's placement (ZHIP_TUNE_ARM 3-5; chunks < 64):
+// chunk words 128 B apart instead of 16 B (eight chunks per line), and a
+// per-workgroup line for a plain store of the contribution
+__device__ uint32_t g_ws_spread[64 * 32 + 64 * 32 * 32];
+
 __device__ __forceinline__ void publish_il(const DecodeParams& p, uint32_t c, uint32_t r, uint32_t wpc, uint32_t V,
-                                           uint32_t stored, int t) {
+                                           uint32_t stored, int t, uint64_t* wsw = nullptr) {
     if (wpc <= 32u) {
         const uint64_t full = wpc >= 32u ? 0xFFFFFFFFull : ((1ull << wpc) - 1ull);
         const uint64_t bits = 1ull << r;
         uint64_t prev = 0;
-        if (t == 0) {
-            uint64_t* w = reinterpret_cast<uint64_t*>(p.ws) + 2ull * c;
-            prev = __hip_atomic_fetch_xor(w, (bits << 32) | V, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        uint64_t* const w = wsw ? wsw : reinterpret_cast<uint64_t*>(p.ws) + 2ull * c;
+        if (t == 0) prev = __hip_atomic_fetch_xor(w, (bits << 32) | V, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)prev);
         const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(prev >> 32));
         if ((uint64_t)(hi ^ (uint32_t)bits) == full) {
-            if (t == 0) {
-                uint64_t* w = reinterpret_cast<uint64_t*>(p.ws) + 2ull * c;
-                __hip_atomic_store(w, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
+            if (t == 0) __hip_atomic_store(w, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             finalize_uniform(p, c, stored, lo ^ V, t, true);
         }
     } else {  // more than 32 workgroups per chunk: xor, then count arrivals
@@ -1349,6 +1349,17 @@ void k_decode_il(const DecodeParams p) {
                 if constexpr (TUNE) stamp(p, g, t, 4);
                 if constexpr (PUB == 2) {
                     if (t == 0) dv_publish(p, c, r == 0, V, __builtin_amdgcn_readfirstlane(stored));
+                } else if constexpr (PUB == 3) {  // arm: returning protocol, chunk words 128 B apart
+                    publish_il(p, c, r, wpc, V, __builtin_amdgcn_readfirstlane(stored), t,
+                               reinterpret_cast<uint64_t*>(g_ws_spread + 32u * (c & 63u)));
+                } else if constexpr (PUB == 4) {  // arm: non-returning xor, chunk words 128 B apart
+                    if (t == 0)
+                        __hip_atomic_fetch_xor(g_ws_spread + 32u * (c & 63u) + 2u * p.dv_bank, V, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+                } else if constexpr (PUB == 5) {  // arm: plain store to a line of the workgroup's own
+                    if (t == 0)
+                        __hip_atomic_store(g_ws_spread + 64u * 32u + ((c & 63u) * 32u + (r & 31u)) * 32u, V,
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 } else {
                     publish_il(p, c, r, wpc, V, __builtin_amdgcn_readfirstlane(stored), t);
                 }
@@ -1375,6 +1386,9 @@ KernelFn select_il_kernel_arm(bool crc, int item, bool swap, int arm) {  // ZHIP
     if (!(crc && item == 4 && !swap)) return nullptr;
     switch (arm) {
         case 1: return k_decode_il<true, 4, false, false, false, 0, false, 0>;  // round 3: returning publication
+        case 3: return k_decode_il<true, 4, false, false, false, 0, false, 3>;  // returning, words spread
+        case 4: return k_decode_il<true, 4, false, false, false, 0, false, 4>;  // non-returning, spread (timing)
+        case 5: return k_decode_il<true, 4, false, false, false, 0, false, 5>;  // per-WG plain store (timing)
         default: return nullptr;
     }
 }

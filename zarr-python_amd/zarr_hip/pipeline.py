@@ -55,14 +55,42 @@ def _upload(arr: np.ndarray, device):
     return t
 
 
+# device buffers of per-call reads, reused (read_sync with the plan cache off
+# or missed): table blocks by power-of-two size, zeroed status / workspace
+# blocks by exact size -- returned only after a launch whose results came back
+# clean, so a reused workspace is zero and its error word clear
+_BUF_POOL: dict = {}
+_BUF_POOL_MAX = 8
+
+
+def _pool_take(kind: str, n: int, device, dtype):
+    torch = _torch()
+    key = (kind, n, str(device))
+    lst = _BUF_POOL.get(key)
+    if lst:
+        return lst.pop()
+    if kind == "z":
+        return torch.zeros(n, dtype=dtype, device=device)
+    return torch.empty(n, dtype=dtype, device=device)
+
+
+def _pool_give(kind: str, t) -> None:
+    key = (kind, t.numel(), str(t.device))
+    lst = _BUF_POOL.setdefault(key, [])
+    if len(lst) < _BUF_POOL_MAX:
+        lst.append(t)
+
+
 class _Upload:
     """Several host tables in ONE pinned host -> device copy (256-byte aligned
     slices of one device buffer), instead of one pageable copy each."""
 
-    def __init__(self, device):
+    def __init__(self, device, pooled: bool = False):
         self.device = device
         self.parts: list = []
         self.top = 0
+        self.pooled = pooled
+        self.dev = None
 
     def add(self, arr: np.ndarray) -> int:
         b = np.ascontiguousarray(arr).view(np.uint8).reshape(-1)
@@ -77,7 +105,12 @@ class _Upload:
         hv = host.numpy()
         for off, b in self.parts:
             hv[off: off + b.size] = b
-        dev = torch.empty(max(self.top, 16), dtype=torch.uint8, device=self.device)
+        if self.pooled:
+            cap = 1 << max(12, (max(self.top, 16) - 1).bit_length())
+            self.dev = _pool_take("t", cap, self.device, torch.uint8)
+            dev = self.dev[: max(self.top, 16)]
+        else:
+            dev = torch.empty(max(self.top, 16), dtype=torch.uint8, device=self.device)
         dev.copy_(host, non_blocking=True)  # torch keeps the pinned block until the copy is done
         return [dev[off: off + max(b.size, 16)] for off, b in self.parts]
 
@@ -143,9 +176,10 @@ class DecodeLaunch:
 
     def __init__(self, layout: N.Layout, chunks: np.ndarray, sels: np.ndarray, src, src_size: int,
                  out, fast: bool, device, tile: bool = False, index_chunks: np.ndarray | None = None,
-                 rows: bool = False, predict: "N.Predict | None" = None):
+                 rows: bool = False, predict: "N.Predict | None" = None, pooled: bool = False):
         torch = _torch()
         self.plan = get_plan(layout)
+        self.pooled = pooled
         self.n = len(chunks)
         self.device = device
         # shard-index CRC checks fused into this launch (zhip_decode_indexed)
@@ -161,7 +195,7 @@ class DecodeLaunch:
         rowmap = _rows_map_host(self.plan, sels) if fast and rows else None
         # every table in one host -> device copy; statuses and workspaces in
         # one zeroed buffer
-        up = _Upload(device)
+        up = _Upload(device, pooled)
         i_ch = up.add(chunks)
         i_sel = up.add(sels if len(sels) else np.zeros(1, SEL_DT))
         i_idx = up.add(index_chunks) if self.n_idx else None
@@ -177,7 +211,9 @@ class DecodeLaunch:
         # error word and the chunks' deferred-verdict words (the first 4 words
         # per chunk of the workspace, zarrhip.h) are one contiguous range, read
         # back with one copy after a launch
-        z = torch.zeros(nw + 64 + nws + ni, dtype=torch.int32, device=device)
+        z = _pool_take("z", nw + 64 + nws + ni, device, torch.int32) if pooled else \
+            torch.zeros(nw + 64 + nws + ni, dtype=torch.int32, device=device)
+        self._bufs = (up.dev, z) if pooled else None
         self.d_status = z[:nw]
         self.d_err = z[nw: nw + 4]
         self.d_ws = z[nw + 64: nw + 64 + nws]
@@ -249,6 +285,16 @@ class DecodeLaunch:
                                     self.d_sels.data_ptr(), status, ws, self.d_err.data_ptr(),
                                     self.flags | (N.DF_BANK1 if self._bank else 0), s), "zhip_decode")
 
+    def release(self) -> None:
+        """Give pooled buffers back (after a clean result check; the launch
+        must not be used again)."""
+        if self._bufs is not None:
+            tb, z = self._bufs
+            self._bufs = None
+            if tb is not None:
+                _pool_give("t", tb)
+            _pool_give("z", z)
+
     def statuses(self) -> np.ndarray:
         """Per-chunk statuses with the deferred CRC verdicts merged in: a
         nonzero verdict word w of bank b is a mismatch with stored trailer s_b,
@@ -304,6 +350,7 @@ class DecodeProgram:
     item_missing: np.ndarray
     keepalive: list = field(default_factory=list)
     pending: Any = None  # staging.Pending: host bytes still on their way to HBM
+    clean: bool = False  # the last results_fast found no error
     # ((DeviceArena, gen), ...) of the device stores the batch reads: a launch
     # after any of them changed placements would read moved or reused bytes
     generations: tuple = ()
@@ -366,7 +413,14 @@ class DecodeProgram:
         if ok is None:
             ok = tuple(GetResult(status="missing" if m else "present") for m in self.item_missing)
             self._ok_results = ok
+        self.clean = True
         return ok
+
+    def release(self) -> None:
+        """Pooled buffers back to the per-call pool (the program is done)."""
+        self.data.release()
+        if self.index is not None:
+            self.index.release()
 
     def results(self) -> tuple[GetResult, ...]:
         """Synchronise, then raise like the reference or return per-item statuses."""
@@ -839,7 +893,7 @@ class HipCodecPipeline:
 
     # ---------------------------------------------------------------- read
     def prepare_read(self, batch_info: Iterable, out, drop_axes: tuple = (),
-                     item_out_extra=None) -> DecodeProgram:
+                     item_out_extra=None, pooled: bool = False) -> DecodeProgram:
         """Plan a batch once: tables uploaded, launches ready.  `out` is a device
         tensor; item_out_extra (bytes per item) shifts each item's out position,
         so one launch can decode a batch into the slices of a stacked out."""
@@ -901,8 +955,10 @@ class HipCodecPipeline:
                 lead = (t.index_layout is not None and resolved is None and not chain.inner.crc
                         and not t.tile and t.fast and t.rows
                         and get_plan(t.layout).units_per_chunk <= 32)
+                # (pooled: the per-call read hands the buffers back after a clean check)
+                pooled = pooled and pending is None
                 data = DecodeLaunch(t.layout, t.chunks, t.sels, src, size, out, t.fast, device, t.tile,
-                                    t.index_chunks if (fuse or lead) else None, t.rows, t.predict)
+                                    t.index_chunks if (fuse or lead) else None, t.rows, t.predict, pooled)
                 if lead and data.d_rowmap is None:  # the library declined the row map
                     data = DecodeLaunch(t.layout, t.chunks, t.sels, src, size, out, t.fast, device, t.tile,
                                         None, t.rows, t.predict)
@@ -1003,9 +1059,12 @@ class HipCodecPipeline:
         return res
 
     def _read_uncached(self, batch, dev_out, drop_axes) -> tuple[GetResult, ...]:
-        prog = self.prepare_read(batch, dev_out, drop_axes)
+        prog = self.prepare_read(batch, dev_out, drop_axes, pooled=True)
         prog.launch()
-        return prog.results_fast()
+        res = prog.results_fast()
+        if prog.clean:  # nothing raised or flagged: the buffers are zero again
+            prog.release()
+        return res
 
     def _read_slabs_one_plan(self, batch, groups, dev_out, host_out, direct: bool):
         """_read_slabs for unsharded chains: the batch is planned ONCE (in slab
