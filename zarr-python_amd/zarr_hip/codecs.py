@@ -247,6 +247,44 @@ class ShardingCodec:
         raise NotImplementedError("sharding_indexed output is not fixed-size")
 
 
+def gzip_member(data, level: int) -> bytes:
+    """The bytes ``gzip.compress(data, compresslevel=level, mtime=0)`` returns
+    (one member as GzipFile writes it: no name, mtime 0, XFL by level, OS 255,
+    raw deflate, CRC-32, ISIZE), built on zlib directly: the deflate runs
+    without the GIL, so the host stage's threads compress in parallel
+    (gzip.compress in Python 3.10 drives a GzipFile object per call)."""
+    import struct
+    import zlib
+
+    mv = memoryview(data).cast("B") if not isinstance(data, (bytes, bytearray)) else data
+    co = zlib.compressobj(level, zlib.DEFLATED, -zlib.MAX_WBITS, zlib.DEF_MEM_LEVEL, 0)
+    body = co.compress(mv) + co.flush()
+    xfl = b"\002" if level == 9 else b"\004" if level == 1 else b"\000"
+    return b"\037\213\010\000\000\000\000\000" + xfl + b"\377" + body + \
+        struct.pack("<II", zlib.crc32(mv) & 0xFFFFFFFF, len(mv) & 0xFFFFFFFF)
+
+
+def gzip_decode(data) -> bytes:
+    """numcodecs.GZip.decode over zlib: a gzip member (several members are
+    concatenated, as gzip.decompress reads them) or a raw zlib stream; the
+    inflate runs without the GIL."""
+    import zlib
+
+    b = data if isinstance(data, (bytes, bytearray)) else bytes(data)
+    if b[:2] != b"\x1f\x8b":
+        return zlib.decompress(b)
+    out = []
+    while b:
+        d = zlib.decompressobj(31)
+        out.append(d.decompress(b))
+        if not d.eof:
+            raise EOFError("Compressed file ended before the end-of-stream marker was reached")
+        b = d.unused_data
+        if b and b[:2] != b"\x1f\x8b":
+            break  # trailing garbage after the last member (gzip.decompress ignores zero padding)
+    return b"".join(out)
+
+
 @dataclass(frozen=True)
 class GzipCodec:
     """src/zarr/codecs/gzip.py:31-95 on the host: numcodecs.GZip's stream (a gzip
@@ -286,18 +324,10 @@ class GzipCodec:
         return None
 
     def decode_bytes(self, data, spec: ArraySpec | None = None) -> bytes:
-        import gzip
-        import zlib
-
-        b = bytes(data)
-        if b[:2] == b"\x1f\x8b":
-            return gzip.decompress(b)
-        return zlib.decompress(b)
+        return gzip_decode(data)
 
     def encode_bytes(self, data, spec: ArraySpec | None = None) -> bytes:
-        import gzip
-
-        return gzip.compress(bytes(data), compresslevel=self.level, mtime=0)
+        return gzip_member(data, self.level)
 
 
 class _HostBuffer:
