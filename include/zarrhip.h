@@ -147,7 +147,8 @@ int zhip_device_count(void);
  * current device).  Not for the timed path: cache the plan per array. */
 int zhip_plan_create(const zhip_layout *layout, zhip_plan **plan);
 int zhip_plan_destroy(zhip_plan *plan);
-/* Units (workgroup work items) per chunk and workspace words per chunk. */
+/* Units (workgroup work items) per chunk and workspace words per chunk
+ * (>= 32 for layouts with a crc32c: one 128-byte publication line per chunk). */
 int zhip_plan_info(const zhip_plan *plan, uint32_t *units_per_chunk, uint32_t *workspace_words);
 /* Which specialised kernels the plan's layout admits (ZHIP_PK_* bits). */
 #define ZHIP_PK_TILE4 1u  /* transposed layout with full 64 x 256-byte tiles: k_decode_tile4 */
@@ -185,7 +186,8 @@ int zhip_plan_kernel_flags(const zhip_plan *plan, uint32_t *flags);
                                  into workspace bank 1 and checks bank 0 (else the
                                  reverse); the caller alternates it per launch */
 
-/* Deferred CRC verdicts.  The headline kernel (k_decode_il) publishes each
+/* Deferred CRC verdicts.  k_decode_tileg (the transposing decode of chunks
+ * larger than 64 tiles) publishes each
  * workgroup's CRC contribution with a NON-returning atomic xor into the
  * chunk's workspace word of the launch's bank (4 words per chunk:
  * {w0, w1, s0, s1}); the chunk's first workgroup also folds in the stored
@@ -195,7 +197,10 @@ int zhip_plan_kernel_flags(const zhip_plan *plan, uint32_t *flags);
  * checks the other bank: status CRC_MISMATCH + errflag, sticky across graph
  * replays), by zhip_dv_check, or by the host after synchronising (a nonzero
  * w_b is Crc32cCodec's mismatch with stored s_b, computed w_b ^ s_b).  Every
- * other kernel leaves w0 and w1 zero once its launch completes. */
+ * other kernel leaves w0 and w1 zero once its launch completes (the returning
+ * publications of k_decode_il / k_decode_tile4 use word 32 c of the
+ * workspace, zhip_plan_info's >= 32 words per chunk of CRC layouts, and
+ * clear it when the chunk's last workgroup arrives). */
 typedef struct zhip_dv_ref {
     uint32_t *workspace;   /* a launch's d_workspace (4 words per chunk first) */
     zhip_status *status;   /* its d_status */
@@ -212,6 +217,14 @@ int zhip_dv_check(const zhip_dv_ref *d_refs, uint32_t n_refs, void *stream);
  * page-locked buffer, one stream synchronise, then concatenated into
  * host_out. */
 int zhip_wait_ranges(const void *const *srcs, const uint64_t *sizes, uint32_t n, void *host_out, void *stream);
+
+/* A launch's host tables in ONE host -> device copy on `stream`: part i
+ * (sizes[i] bytes at parts[i]) lands at dev + offsets[i] (each part inside
+ * [0, total)).  The parts are packed into a page-locked per-thread buffer of
+ * the current device, reused once its previous copy has finished; the host
+ * parts may be freed when the call returns. */
+int zhip_upload(const void *const *parts, const uint64_t *sizes, const uint64_t *offsets, uint32_t n, void *dev,
+                uint64_t total, void *stream);
 
 /* Host planner for a batch of basic selections (zhip_plan_batch).  One item
  * of a CodecPipeline batch: its chunk (or shard) bytes, its chunk selection

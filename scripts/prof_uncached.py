@@ -1,19 +1,19 @@
 #!/usr/bin/env python
 """Where an uncached per-call read spends its host time (measurement only):
 the headline array in HBM, read_sync with the plan cache off, a DIFFERENT
-selection every call (a data loader walking the array), under cProfile.
-Prints the per-call wall, then the top functions by cumulative and by own
-time as JSON lines."""
+selection every call (a data loader walking the array).  Prints the per-call
+wall, then each stage's inclusive mean (perf_counter wrappers around the
+read path's functions; a wrapper costs ~0.3 us), then a cProfile top list,
+as JSON lines."""
 
 import cProfile
+import functools
 import io
 import json
 import os
 import pstats
 import sys
 import time
-
-import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -22,11 +22,31 @@ sys.path.insert(0, os.path.join(ROOT, "zarr-python_amd"))
 import bench  # noqa: E402
 import workloads as W  # noqa: E402
 
+_T: dict = {}
+
+
+def _wrap(owner, name, label):
+    fn = getattr(owner, name)
+
+    @functools.wraps(fn)
+    def w(*a, **k):
+        t0 = time.perf_counter()
+        try:
+            return fn(*a, **k)
+        finally:
+            e = _T.setdefault(label, [0, 0.0])
+            e[0] += 1
+            e[1] += time.perf_counter() - t0
+    setattr(owner, name, w)
+    return fn
+
 
 def main():
     import torch
 
     from zarr_hip import pipeline as P
+    from zarr_hip import planner as PL
+    from zarr_hip import staging as ST
 
     dev = torch.device("cuda:0")
     g = W.HEADLINE
@@ -41,21 +61,45 @@ def main():
     for i in range(16):
         pipe.read_sync(batches[i % 8][0], outs[i % 8])
     torch.cuda.synchronize(dev)
-    n = int(os.environ.get("CALLS", "200"))
+    n = int(os.environ.get("CALLS", "400"))
     t0 = time.perf_counter()
     for i in range(n):
         pipe.read_sync(batches[i % 8][0], outs[i % 8])
     wall = (time.perf_counter() - t0) / n
     print(json.dumps({"uncached_ms_per_call": round(wall * 1e3, 4), "calls": n}), flush=True)
-    pr = cProfile.Profile()
-    pr.enable()
+    H = P.HipCodecPipeline
+    stages = [
+        (P, "normalize_batch", "normalize_batch"), (P, "_resolve_out", "_resolve_out"),
+        (H, "prepare_read", "prepare_read"), (H, "_shard_space", "_shard_space"), (H, "_chain", "_chain"),
+        (P, "_device_resident", "_device_resident"), (ST, "gather_sources", "gather_sources"),
+        (P, "plan_decode", "plan_decode"), (PL, "_plan_native", "_plan_native"),
+        (PL, "_native_ctx", "_native_ctx"), (P, "_kernel_flags", "_kernel_flags"),
+        (P.DecodeLaunch, "__init__", "DecodeLaunch.__init__"), (P, "_rows_map_host", "_rows_map_host"),
+        (P._Upload, "commit", "_Upload.commit"), (P, "_pool_take", "_pool_take"),
+        (P, "_generations", "_generations"), (P.DecodeProgram, "launch", "DecodeProgram.launch"),
+        (P.DecodeLaunch, "launch", "DecodeLaunch.launch"), (P.DecodeProgram, "results_fast", "results_fast"),
+        (P.DecodeProgram, "release", "release"), (P, "_stream_handle", "_stream_handle"),
+    ]
+    for owner, name, label in stages:
+        if hasattr(owner, name):
+            _wrap(owner, name, label)
+    _T.clear()
+    t0 = time.perf_counter()
     for i in range(n):
         pipe.read_sync(batches[i % 8][0], outs[i % 8])
+    wall_w = (time.perf_counter() - t0) / n
+    print(json.dumps({"wrapped_ms_per_call": round(wall_w * 1e3, 4),
+                      "stages_us_per_call": {k: round(v[1] / n * 1e6, 2) for k, v in
+                                             sorted(_T.items(), key=lambda kv: -kv[1][1])},
+                      "stage_calls_per_read": {k: round(v[0] / n, 2) for k, v in _T.items()}}), flush=True)
+    pr = cProfile.Profile()
+    pr.enable()
+    for i in range(n // 2):
+        pipe.read_sync(batches[i % 8][0], outs[i % 8])
     pr.disable()
-    for key in ("cumulative", "tottime"):
-        s = io.StringIO()
-        pstats.Stats(pr, stream=s).sort_stats(key).print_stats(30)
-        print(json.dumps({"sort": key, "stats": s.getvalue()}), flush=True)
+    s = io.StringIO()
+    pstats.Stats(pr, stream=s).sort_stats("tottime").print_stats(25)
+    print(json.dumps({"sort": "tottime", "stats": s.getvalue()}), flush=True)
     for i in range(8):
         pipe.read_sync(batches[i][0], outs[i])
         want = src[sels[i]]

@@ -562,7 +562,10 @@ int zhip_plan_info(const zhip_plan* p, uint32_t* units_per_chunk, uint32_t* work
     if (!p) return set_err(ZHIP_E_INVALID, "null plan");
     if (units_per_chunk) *units_per_chunk = p->nseg;
     // + the grouped kernels' / k_decode_xw's arrival subwords
-    if (workspace_words) *workspace_words = 4 + 2 * std::max(p->n_sub, p->xw_nsub);
+    // (CRC layouts: >= kPubLine, the il / tile4 publication lines)
+    if (workspace_words)
+        *workspace_words = std::max(4 + 2 * std::max(p->n_sub, p->xw_nsub),
+                                    (p->layout.flags & ZHIP_LF_CRC) ? kPubLine : 0u);
     return ZHIP_OK;
 }
 

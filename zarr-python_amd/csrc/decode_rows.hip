@@ -1094,18 +1094,18 @@ __global__ __launch_bounds__(2 * kThreads) __attribute__((amdgpu_waves_per_eu(8,
 // statuses, stores (row map, sink for unselected rows), fused index checks
 // (one step per lane; the constants carry the A_D frame) as k_decode_pair.
 // (CPU emulation: zhip_emulate_chunk_crc_il.)
-// timing arms of the publication's placement (ZHIP_TUNE_ARM 3-5; chunks < 64):
-// chunk words 128 B apart instead of 16 B (eight chunks per line), and a
-// per-workgroup line for a plain store of the contribution
-__device__ uint32_t g_ws_spread[64 * 32 + 64 * 32 * 32];
-
+//
+// wstride: 64-bit words between chunks' publication words; default 2 (16 B
+// per chunk, eight chunks per 128-byte line).  k_decode_il / k_decode_tile4
+// pass kPubLine / 2 instead, one line per chunk (zhip_plan_info reports
+// >= kPubLine workspace words per chunk for CRC layouts).
 __device__ __forceinline__ void publish_il(const DecodeParams& p, uint32_t c, uint32_t r, uint32_t wpc, uint32_t V,
-                                           uint32_t stored, int t, uint64_t* wsw = nullptr) {
+                                           uint32_t stored, int t, uint32_t wstride = 2u) {
     if (wpc <= 32u) {
         const uint64_t full = wpc >= 32u ? 0xFFFFFFFFull : ((1ull << wpc) - 1ull);
         const uint64_t bits = 1ull << r;
         uint64_t prev = 0;
-        uint64_t* const w = wsw ? wsw : reinterpret_cast<uint64_t*>(p.ws) + 2ull * c;
+        uint64_t* const w = reinterpret_cast<uint64_t*>(p.ws) + (uint64_t)wstride * c;
         if (t == 0) prev = __hip_atomic_fetch_xor(w, (bits << 32) | V, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)prev);
         const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(prev >> 32));
@@ -1146,16 +1146,21 @@ __device__ __forceinline__ void publish_il(const DecodeParams& p, uint32_t c, ui
 // kTuneNoRunEnd, kTuneNoPub) are compiled in; the production instantiation has
 // TUNE = false and no such branch.
 // PUB: how a workgroup's CRC contribution reaches the chunk's verdict.
-//   2 (production, round 4): deferred verdicts (zarrhip.h) -- a NON-returning
-//     atomic xor into the chunk's word of this launch's bank (the chunk's
-//     first workgroup also folds in c3 ^ ~stored and records the trailer), so
-//     no workgroup waits for an atomic's round trip or finalizes; the first
-//     workgroup of each chunk checks the other bank (the previous launch's
-//     verdict) and clears it.
-//   0 (arm ZHIP_TUNE_ARM = 1): round 3's returning 64-bit publication with
-//     arrival bits; the last arriver compares with the trailer.
+//   3 (production, round 4): the returning 64-bit publication with arrival
+//     bits (publish_il), the chunk's word alone in its 128-byte line
+//     (p.ws + kPubLine c); the last arriver compares with the trailer.
+//   0 (arm ZHIP_TUNE_ARM = 1): the same at p.ws + 4 c (round 3: eight
+//     chunks' words share a line).
+//   2 (arm ZHIP_TUNE_ARM = 2): deferred verdicts (zarrhip.h) -- a
+//     NON-returning atomic xor into the chunk's word of this launch's bank
+//     (the chunk's first workgroup also folds in c3 ^ ~stored and records the
+//     trailer); the first workgroup of each chunk checks the other bank (the
+//     previous launch's verdict) and clears it.
+//   Graph-timed on one box (profiles/r04/c/arms_*.jsonl), headline / N = 8
+//   share: 3: 26.01 / 9.45 us, 0: 26.22 / 9.62, 2: 26.38 / 10.14, no
+//   publication at all 25.48 / 9.17.
 template <bool CRC, int ITEM, bool SWAP, bool LEAN = false, bool CF = false, int LM = 0, bool TUNE = false,
-          int PUB = 2>
+          int PUB = 3>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(LM == 2 ? 6 : 4, LM == 2 ? 6 : 4)))
 void k_decode_il(const DecodeParams p) {
     constexpr int K = kDefaultBlocks;
@@ -1349,17 +1354,8 @@ void k_decode_il(const DecodeParams p) {
                 if constexpr (TUNE) stamp(p, g, t, 4);
                 if constexpr (PUB == 2) {
                     if (t == 0) dv_publish(p, c, r == 0, V, __builtin_amdgcn_readfirstlane(stored));
-                } else if constexpr (PUB == 3) {  // arm: returning protocol, chunk words 128 B apart
-                    publish_il(p, c, r, wpc, V, __builtin_amdgcn_readfirstlane(stored), t,
-                               reinterpret_cast<uint64_t*>(g_ws_spread + 32u * (c & 63u)));
-                } else if constexpr (PUB == 4) {  // arm: non-returning xor, chunk words 128 B apart
-                    if (t == 0)
-                        __hip_atomic_fetch_xor(g_ws_spread + 32u * (c & 63u) + 2u * p.dv_bank, V, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
-                } else if constexpr (PUB == 5) {  // arm: plain store to a line of the workgroup's own
-                    if (t == 0)
-                        __hip_atomic_store(g_ws_spread + 64u * 32u + ((c & 63u) * 32u + (r & 31u)) * 32u, V,
-                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                } else if constexpr (PUB == 3) {  // the chunk's word alone in its line
+                    publish_il(p, c, r, wpc, V, __builtin_amdgcn_readfirstlane(stored), t, kPubLine / 2u);
                 } else {
                     publish_il(p, c, r, wpc, V, __builtin_amdgcn_readfirstlane(stored), t);
                 }
@@ -1379,16 +1375,14 @@ void k_decode_il(const DecodeParams p) {
 }
 
 KernelFn select_il_kernel_tuned(bool crc, int item, bool swap) {  // runtime timing arms (p.tune)
-    return (crc && item == 4 && !swap) ? k_decode_il<true, 4, false, false, false, 0, true, 2> : nullptr;
+    return (crc && item == 4 && !swap) ? k_decode_il<true, 4, false, false, false, 0, true> : nullptr;
 }
 
 KernelFn select_il_kernel_arm(bool crc, int item, bool swap, int arm) {  // ZHIP_TUNE_ARM experiments
     if (!(crc && item == 4 && !swap)) return nullptr;
     switch (arm) {
-        case 1: return k_decode_il<true, 4, false, false, false, 0, false, 0>;  // round 3: returning publication
-        case 3: return k_decode_il<true, 4, false, false, false, 0, false, 3>;  // returning, words spread
-        case 4: return k_decode_il<true, 4, false, false, false, 0, false, 4>;  // non-returning, spread (timing)
-        case 5: return k_decode_il<true, 4, false, false, false, 0, false, 5>;  // per-WG plain store (timing)
+        case 1: return k_decode_il<true, 4, false, false, false, 0, false, 0>;  // round 3: words 16 B apart
+        case 2: return k_decode_il<true, 4, false, false, false, 0, false, 2>;  // deferred verdicts
         default: return nullptr;
     }
 }

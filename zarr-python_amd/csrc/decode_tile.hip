@@ -113,11 +113,13 @@ __device__ __forceinline__ uint4 tile_get16(const uint8_t* s, uint32_t r, uint32
 
 }  // namespace
 
-// PUB: 2 = deferred CRC verdicts (zarrhip.h; production since round 4: a
-// non-returning xor per workgroup, the first workgroup of a chunk checks the
-// previous launch's verdict); 0 = round 3's returning publication with
-// arrival bits (arm ZHIP_TUNE_ARM = 2).
-template <bool CRC, int ITEM, bool SWAP, int PUB = 2>
+// PUB: 3 (production) = the returning publication with arrival bits, the
+// chunk's word alone in its 128-byte line (p.ws + kPubLine c); 0 (arm
+// ZHIP_TUNE_ARM = 1) = the same at p.ws + 4 c (round 3); 2 (arm 2) = deferred
+// CRC verdicts (zarrhip.h: a non-returning xor per workgroup, the first
+// workgroup of a chunk checks the previous launch's verdict).  Graph-timed on
+// C3 (profiles/r04/b/arms_c3.jsonl): returning 29.30 us, deferred 29.85.
+template <bool CRC, int ITEM, bool SWAP, int PUB = 3>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_decode_tile4(
     const DecodeParams p) {
     constexpr int kPer = 16 / ITEM;                // rows per 16-byte out piece
@@ -243,7 +245,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
                 if (gpc <= 32) {
                     const uint64_t full = gpc == 32 ? 0xFFFFFFFFull : ((1ull << gpc) - 1ull);
                     const uint64_t bits = 1ull << grp;
-                    uint64_t* w = reinterpret_cast<uint64_t*>(p.ws) + 2ull * c;
+                    uint64_t* w = reinterpret_cast<uint64_t*>(p.ws + (PUB == 3 ? (uint64_t)kPubLine * c : 4ull * c));
                     const uint64_t prev = __hip_atomic_fetch_xor(w, (bits << 32) | V, __ATOMIC_RELAXED,
                                                                  __HIP_MEMORY_SCOPE_AGENT);
                     if (((prev >> 32) ^ bits) == full) {
@@ -1254,7 +1256,8 @@ KernelFn select_tile4f_kernel(int item, bool swap) {  // CRC chains only
 }
 
 KernelFn select_tile4_kernel(bool crc, int item, bool swap) {
-    if (g_tune_arm == 2 && crc && item == 4 && !swap) return k_decode_tile4<true, 4, false, 0>;  // returning arm
+    if (g_tune_arm == 1 && crc && item == 4 && !swap) return k_decode_tile4<true, 4, false, 0>;  // words 16 B apart
+    if (g_tune_arm == 2 && crc && item == 4 && !swap) return k_decode_tile4<true, 4, false, 2>;  // deferred arm
     switch (item) {
         case 1: return crc ? k_decode_tile4<true, 1, false> : k_decode_tile4<false, 1, false>;
         case 2: return crc ? (swap ? k_decode_tile4<true, 2, true> : k_decode_tile4<true, 2, false>)

@@ -469,6 +469,54 @@ int zhip_wait_ranges(const void* const* srcs, const uint64_t* sizes, uint32_t n,
     return ZHIP_OK;
 }
 
+int zhip_upload(const void* const* parts, const uint64_t* sizes, const uint64_t* offsets, uint32_t n, void* dev,
+                uint64_t total, void* stream) {
+    // a launch's host tables in one H2D copy: packed into a page-locked
+    // per-thread, per-device buffer, whose previous copy (an event behind it)
+    // has finished before it is overwritten
+    if (total == 0) return ZHIP_OK;
+    if (!dev || (n && (!parts || !sizes || !offsets))) return ZHIP_E_INVALID;
+    for (uint32_t i = 0; i < n; ++i)
+        if (offsets[i] > total || sizes[i] > total - offsets[i] || (sizes[i] && !parts[i])) return ZHIP_E_INVALID;
+    int d = 0;
+    if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= 64) return ZHIP_E_HIP;
+    struct Slot {
+        uint8_t* pinned = nullptr;
+        uint64_t cap = 0;
+        hipEvent_t ev = nullptr;
+        bool pending = false;
+    };
+    thread_local Slot slots[64];
+    Slot& s = slots[d];
+    if (s.pending) {
+        if (hipEventSynchronize(s.ev) != hipSuccess) return ZHIP_E_HIP;
+        s.pending = false;
+    }
+    if (!s.ev && hipEventCreateWithFlags(&s.ev, hipEventDisableTiming) != hipSuccess) {
+        s.ev = nullptr;
+        return ZHIP_E_HIP;
+    }
+    if (total > s.cap) {
+        if (s.pinned) (void)hipHostFree(s.pinned);
+        s.pinned = nullptr;
+        s.cap = 0;
+        uint64_t want = 1ull << 16;
+        while (want < total) want <<= 1;
+        if (hipHostMalloc(reinterpret_cast<void**>(&s.pinned), want, hipHostMallocDefault) != hipSuccess) {
+            s.pinned = nullptr;
+            return ZHIP_E_HIP;
+        }
+        s.cap = want;
+    }
+    for (uint32_t i = 0; i < n; ++i)
+        if (sizes[i]) std::memcpy(s.pinned + offsets[i], parts[i], sizes[i]);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (hipMemcpyAsync(dev, s.pinned, total, hipMemcpyHostToDevice, st) != hipSuccess) return ZHIP_E_HIP;
+    if (hipEventRecord(s.ev, st) != hipSuccess) return ZHIP_E_HIP;
+    s.pending = true;
+    return ZHIP_OK;
+}
+
 int zhip_host_copy(void* dst, const void* src, uint64_t nbytes, uint32_t nthreads) {
     if (nbytes == 0) return ZHIP_OK;
     if (!dst || !src) return ZHIP_E_INVALID;

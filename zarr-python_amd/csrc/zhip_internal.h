@@ -10,6 +10,10 @@ namespace zhip {
 constexpr int kThreads = 256;                            // one workgroup = 4 waves
 constexpr int kWgStride = kThreads * 16;                 // 4 KiB per workgroup step
 constexpr int kDefaultBlocks = 8;                        // 16-byte blocks per thread per unit
+// workspace words per chunk of CRC layouts (zhip_plan_info): k_decode_il /
+// k_decode_tile4 publish into word kPubLine * c, one 128-byte line per chunk
+// (32 workgroups' returning atomics per line instead of 8 chunks' 256)
+constexpr uint32_t kPubLine = 32;
 
 // Stored-chunk geometry + out mapping (shared by decode and encode).
 struct Geom {

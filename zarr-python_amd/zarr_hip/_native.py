@@ -236,6 +236,9 @@ def lib():
     L.zhip_wait_ranges.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
                                    ctypes.c_void_p]
     L.zhip_wait_ranges.restype = ctypes.c_int
+    L.zhip_upload.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                              ctypes.c_uint64, ctypes.c_void_p]
+    L.zhip_upload.restype = ctypes.c_int
     L.zhip_dv_check.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
     L.zhip_dv_check.restype = ctypes.c_int
     vp, u32, u64 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64

@@ -42,8 +42,13 @@ def _torch():
 
 
 def _stream_handle(device) -> int:
+    """The raw HIP stream torch treats as current on `device`."""
     torch = _torch()
-    return int(torch.cuda.current_stream(device).cuda_stream)
+    raw = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+    if raw is None:
+        return int(torch.cuda.current_stream(device).cuda_stream)
+    idx = device if isinstance(device, int) else getattr(device, "index", None)
+    return int(raw(torch.cuda.current_device() if idx is None else idx))
 
 
 def _upload(arr: np.ndarray, device):
@@ -82,8 +87,9 @@ def _pool_give(kind: str, t) -> None:
 
 
 class _Upload:
-    """Several host tables in ONE pinned host -> device copy (256-byte aligned
-    slices of one device buffer), instead of one pageable copy each."""
+    """Several host tables in ONE host -> device copy (256-byte aligned parts
+    of one device buffer): zhip_upload packs them into a page-locked buffer
+    of the library's, instead of one pageable copy each."""
 
     def __init__(self, device, pooled: bool = False):
         self.device = device
@@ -93,26 +99,30 @@ class _Upload:
         self.dev = None
 
     def add(self, arr: np.ndarray) -> int:
-        b = np.ascontiguousarray(arr).view(np.uint8).reshape(-1)
+        b = arr if arr.flags.c_contiguous else np.ascontiguousarray(arr)
         off = self.top
         self.parts.append((off, b))
-        self.top = (off + max(b.size, 16) + 255) // 256 * 256
+        self.top = (off + max(b.nbytes, 16) + 255) // 256 * 256
         return len(self.parts) - 1
 
-    def commit(self) -> list:
+    def commit(self, stream: int) -> list:
+        """Device addresses of the parts (the device buffer is self.dev)."""
+        import ctypes
+
         torch = _torch()
-        host = torch.empty(max(self.top, 16), dtype=torch.uint8, pin_memory=True)
-        hv = host.numpy()
-        for off, b in self.parts:
-            hv[off: off + b.size] = b
+        total = max(self.top, 16)
         if self.pooled:
-            cap = 1 << max(12, (max(self.top, 16) - 1).bit_length())
+            cap = 1 << max(12, (total - 1).bit_length())
             self.dev = _pool_take("t", cap, self.device, torch.uint8)
-            dev = self.dev[: max(self.top, 16)]
         else:
-            dev = torch.empty(max(self.top, 16), dtype=torch.uint8, device=self.device)
-        dev.copy_(host, non_blocking=True)  # torch keeps the pinned block until the copy is done
-        return [dev[off: off + max(b.size, 16)] for off, b in self.parts]
+            self.dev = torch.empty(total, dtype=torch.uint8, device=self.device)
+        n = len(self.parts)
+        ptrs = (ctypes.c_void_p * n)(*[b.ctypes.data for _, b in self.parts])
+        sizes = (ctypes.c_uint64 * n)(*[b.nbytes for _, b in self.parts])
+        offs = (ctypes.c_uint64 * n)(*[o for o, _ in self.parts])
+        base = self.dev.data_ptr()
+        N.check(N.lib().zhip_upload(ptrs, sizes, offs, n, base, total, stream), "zhip_upload")
+        return [base + o for o, _ in self.parts]
 
 
 def crc_error_message(stored: int, computed: int) -> str:
@@ -194,18 +204,27 @@ class DecodeLaunch:
         # two-unit row decode; None when the layout does not admit one
         rowmap = _rows_map_host(self.plan, sels) if fast and rows else None
         # every table in one host -> device copy; statuses and workspaces in
-        # one zeroed buffer
+        # one zeroed buffer.  The launches take plain addresses (p_*); the d_*
+        # tensor views are built on demand (result checks, tests, tools).
         up = _Upload(device, pooled)
+        sels = sels if len(sels) else np.zeros(1, SEL_DT)
         i_ch = up.add(chunks)
-        i_sel = up.add(sels if len(sels) else np.zeros(1, SEL_DT))
+        i_sel = up.add(sels)
         i_idx = up.add(index_chunks) if self.n_idx else None
         i_map = up.add(rowmap) if rowmap is not None else None
-        views = up.commit()
-        self.d_chunks, self.d_sels = views[i_ch], views[i_sel]
-        self.d_idx_chunks = views[i_idx] if i_idx is not None else None
-        self.d_rowmap = views[i_map] if i_map is not None else None
+        ptrs = up.commit(_stream_handle(device))
+        self._tb = up.dev
+        self._tparts = {"chunks": (ptrs[i_ch], chunks.nbytes), "sels": (ptrs[i_sel], sels.nbytes)}
+        self.p_chunks, self.p_sels = ptrs[i_ch], ptrs[i_sel]
+        self.p_idx_chunks = ptrs[i_idx] if i_idx is not None else None
+        self.p_rowmap = ptrs[i_map] if i_map is not None else None
+        if i_idx is not None:
+            self._tparts["idx_chunks"] = (ptrs[i_idx], index_chunks.nbytes)
+        if i_map is not None:
+            self._tparts["rowmap"] = (ptrs[i_map], rowmap.nbytes)
         nw = max(self.n, 1) * 4
-        nws = max(self.n, 1) * max(4, self.plan.workspace_words)  # zhip_plan_info
+        self.ws_words = max(4, self.plan.workspace_words)  # zhip_plan_info
+        nws = max(self.n, 1) * self.ws_words
         ni = self.n_idx * 4
         # [statuses][error word, pad to 256 B][workspace][index statuses]: the
         # error word and the chunks' deferred-verdict words (the first 4 words
@@ -213,15 +232,34 @@ class DecodeLaunch:
         # back with one copy after a launch
         z = _pool_take("z", nw + 64 + nws + ni, device, torch.int32) if pooled else \
             torch.zeros(nw + 64 + nws + ni, dtype=torch.int32, device=device)
+        self._z = z
+        self._zl = (nw, nws, ni)
         self._bufs = (up.dev, z) if pooled else None
-        self.d_status = z[:nw]
-        self.d_err = z[nw: nw + 4]
-        self.d_ws = z[nw + 64: nw + 64 + nws]
-        self.d_verdict = z[nw: nw + 64 + 4 * self.n]  # error word .. last chunk's verdict words
-        if self.n_idx:
-            self.d_idx_status = z[nw + 64 + nws: nw + 64 + nws + ni]
+        zp = z.data_ptr()
+        self.p_status, self.p_err, self.p_ws = zp, zp + 4 * nw, zp + 4 * (nw + 64)
+        self.p_idx_status = zp + 4 * (nw + 64 + nws) if self.n_idx else None
+        # error word .. last chunk's verdict words
+        self.verdict_range = (self.p_err, 4 * (64 + 4 * self.n))
         self._bank = 0  # deferred-verdict bank of the next launch (alternates)
         self._ranges: list = []  # (first, count) of launch_range calls since the last statuses()
+
+    def _tview(self, name: str):
+        part = self._tparts.get(name)
+        if part is None:
+            return None
+        off = part[0] - self._tb.data_ptr()
+        return self._tb[off: off + max(part[1], 16)]
+
+    d_chunks = property(lambda self: self._tview("chunks"))
+    d_sels = property(lambda self: self._tview("sels"))
+    d_idx_chunks = property(lambda self: self._tview("idx_chunks"))
+    d_rowmap = property(lambda self: self._tview("rowmap"))
+    d_status = property(lambda self: self._z[: self._zl[0]])
+    d_err = property(lambda self: self._z[self._zl[0]: self._zl[0] + 4])
+    d_ws = property(lambda self: self._z[self._zl[0] + 64: self._zl[0] + 64 + self._zl[1]])
+    d_verdict = property(lambda self: self._z[self._zl[0]: self._zl[0] + 64 + 4 * self.n])
+    d_idx_status = property(lambda self: self._z[self._zl[0] + 64 + self._zl[1]:
+                                                 self._zl[0] + 64 + self._zl[1] + self._zl[2]])
 
     def launch(self, stream: int | None = None) -> None:
         if self.n == 0:
@@ -232,33 +270,27 @@ class DecodeLaunch:
         # alternate workspace banks (also while captured into a graph)
         flags = self.flags | (N.DF_BANK1 if self._bank else 0)
         self._bank ^= 1
-        if self.d_rowmap is not None:
+        src = self.src.data_ptr()
+        if self.p_rowmap is not None:
             N.check(N.lib().zhip_decode_mapped(
-                self.plan.handle, self.src.data_ptr(), self.src_size, out_ptr, self.d_chunks.data_ptr(),
-                self.n, self.d_sels.data_ptr(), self.d_status.data_ptr(), self.d_ws.data_ptr(),
-                self.d_err.data_ptr(), self.d_idx_chunks.data_ptr() if self.n_idx else None, self.n_idx,
-                self.d_idx_status.data_ptr() if self.n_idx else None, flags,
-                self.predict, self.d_rowmap.data_ptr(), s), "zhip_decode_mapped")
+                self.plan.handle, src, self.src_size, out_ptr, self.p_chunks, self.n, self.p_sels,
+                self.p_status, self.p_ws, self.p_err, self.p_idx_chunks, self.n_idx, self.p_idx_status, flags,
+                self.predict, self.p_rowmap, s), "zhip_decode_mapped")
             return
         if self.predict is not None:
             N.check(N.lib().zhip_decode_predicted(
-                self.plan.handle, self.src.data_ptr(), self.src_size, out_ptr, self.d_chunks.data_ptr(),
-                self.n, self.d_sels.data_ptr(), self.d_status.data_ptr(), self.d_ws.data_ptr(),
-                self.d_err.data_ptr(), self.d_idx_chunks.data_ptr() if self.n_idx else None, self.n_idx,
-                self.d_idx_status.data_ptr() if self.n_idx else None, flags, self.predict, s),
-                "zhip_decode_predicted")
+                self.plan.handle, src, self.src_size, out_ptr, self.p_chunks, self.n, self.p_sels,
+                self.p_status, self.p_ws, self.p_err, self.p_idx_chunks, self.n_idx, self.p_idx_status, flags,
+                self.predict, s), "zhip_decode_predicted")
             return
         if self.n_idx:
             N.check(N.lib().zhip_decode_indexed(
-                self.plan.handle, self.src.data_ptr(), self.src_size, out_ptr, self.d_chunks.data_ptr(),
-                self.n, self.d_sels.data_ptr(), self.d_status.data_ptr(), self.d_ws.data_ptr(),
-                self.d_err.data_ptr(), self.d_idx_chunks.data_ptr(), self.n_idx,
-                self.d_idx_status.data_ptr(), flags, s), "zhip_decode_indexed")
+                self.plan.handle, src, self.src_size, out_ptr, self.p_chunks, self.n, self.p_sels,
+                self.p_status, self.p_ws, self.p_err, self.p_idx_chunks, self.n_idx, self.p_idx_status, flags,
+                s), "zhip_decode_indexed")
             return
-        N.check(N.lib().zhip_decode(self.plan.handle, self.src.data_ptr(), self.src_size, out_ptr,
-                                    self.d_chunks.data_ptr(), self.n, self.d_sels.data_ptr(),
-                                    self.d_status.data_ptr(), self.d_ws.data_ptr(),
-                                    self.d_err.data_ptr(), flags, s), "zhip_decode")
+        N.check(N.lib().zhip_decode(self.plan.handle, src, self.src_size, out_ptr, self.p_chunks, self.n,
+                                    self.p_sels, self.p_status, self.p_ws, self.p_err, flags, s), "zhip_decode")
 
     def launch_range(self, first: int, count: int, src, src_size: int, stream: int | None = None) -> None:
         """Chunks [first, first + count) of the table, reading from `src` (the
@@ -271,19 +303,17 @@ class DecodeLaunch:
         self._ranges.append((first, count))  # where this range's verdict words live (statuses())
         s = _stream_handle(self.device) if stream is None else stream
         out_ptr = self.out.data_ptr() if self.out is not None else None
-        wsw = max(4, self.plan.workspace_words)
-        chunks = self.d_chunks.data_ptr() + first * CHUNK_DT.itemsize
-        status = self.d_status.data_ptr() + first * 16
-        ws = self.d_ws.data_ptr() + first * wsw * 4
-        if self.d_rowmap is not None:
+        chunks = self.p_chunks + first * CHUNK_DT.itemsize
+        status = self.p_status + first * 16
+        ws = self.p_ws + first * self.ws_words * 4
+        flags = self.flags | (N.DF_BANK1 if self._bank else 0)
+        if self.p_rowmap is not None:
             N.check(N.lib().zhip_decode_mapped(
-                self.plan.handle, src.data_ptr(), src_size, out_ptr, chunks, count, self.d_sels.data_ptr(),
-                status, ws, self.d_err.data_ptr(), None, 0, None, self.flags | (N.DF_BANK1 if self._bank else 0),
-                None, self.d_rowmap.data_ptr(), s), "zhip_decode_mapped")
+                self.plan.handle, src.data_ptr(), src_size, out_ptr, chunks, count, self.p_sels,
+                status, ws, self.p_err, None, 0, None, flags, None, self.p_rowmap, s), "zhip_decode_mapped")
             return
         N.check(N.lib().zhip_decode(self.plan.handle, src.data_ptr(), src_size, out_ptr, chunks, count,
-                                    self.d_sels.data_ptr(), status, ws, self.d_err.data_ptr(),
-                                    self.flags | (N.DF_BANK1 if self._bank else 0), s), "zhip_decode")
+                                    self.p_sels, status, ws, self.p_err, flags, s), "zhip_decode")
 
     def release(self) -> None:
         """Give pooled buffers back (after a clean result check; the launch
@@ -302,7 +332,7 @@ class DecodeLaunch:
         launch starts clean."""
         st = self.d_status[: self.n * 4].cpu().numpy().view(STATUS_DT).copy()
         if self._ranges:  # range launches: chunk first + c's words at first * wsw + 4 c
-            wsw = max(4, self.plan.workspace_words)
+            wsw = self.ws_words
             for first, count in self._ranges:
                 self.merge_verdicts(st[first: first + count],
                                     self.d_ws[first * wsw: first * wsw + 4 * count].cpu().numpy().view(np.uint32),
@@ -391,9 +421,9 @@ class DecodeProgram:
         if w is None:
             import ctypes
 
-            rngs = [(self.data.d_verdict.data_ptr(), self.data.d_verdict.numel() * 4)]
+            rngs = [self.data.verdict_range]
             if self.index is not None:
-                rngs.append((self.index.d_err.data_ptr(), 4))
+                rngs.append((self.index.p_err, 4))
             n = len(rngs)
             host = np.zeros(sum(r[1] for r in rngs) // 4, np.uint32)
             w = self._err_ranges = ((ctypes.c_void_p * n)(*[r[0] for r in rngs]),
@@ -401,7 +431,7 @@ class DecodeProgram:
         host = w[3]
         N.check(N.lib().zhip_wait_ranges(w[0], w[1], w[2], host.ctypes.data, _stream_handle(self.data.device)),
                 "zhip_wait_ranges")
-        nv = self.data.d_verdict.numel()
+        nv = self.data.verdict_range[1] // 4
         err = int(host[0]) | (int(host[nv]) if self.index is not None else 0)
         dv = host[64:nv]
         if err or (dv.size and (dv[0::2].any())):
@@ -465,7 +495,7 @@ def _dv_refs(launches: list, device):
     dt = np.dtype([("ws", "<u8"), ("status", "<u8"), ("err", "<u8"), ("n", "<u4"), ("pad", "<u4")])
     a = np.zeros(len(launches), dt)
     for i, d in enumerate(launches):
-        a[i] = (d.d_ws.data_ptr(), d.d_status.data_ptr(), d.d_err.data_ptr(), d.n, 0)
+        a[i] = (d.p_ws, d.p_status, d.p_err, d.n, 0)
     return torch.from_numpy(a.view(np.uint8).copy()).to(device)
 
 
@@ -959,7 +989,7 @@ class HipCodecPipeline:
                 pooled = pooled and pending is None
                 data = DecodeLaunch(t.layout, t.chunks, t.sels, src, size, out, t.fast, device, t.tile,
                                     t.index_chunks if (fuse or lead) else None, t.rows, t.predict, pooled)
-                if lead and data.d_rowmap is None:  # the library declined the row map
+                if lead and data.p_rowmap is None:  # the library declined the row map
                     data = DecodeLaunch(t.layout, t.chunks, t.sels, src, size, out, t.fast, device, t.tile,
                                         None, t.rows, t.predict)
                     lead = False

@@ -12,6 +12,8 @@ from __future__ import annotations
 import ctypes
 from dataclasses import dataclass, field
 
+import struct as _struct
+
 import numpy as np
 
 from . import _native as N
@@ -115,16 +117,17 @@ def _sel_lists(csel):
     return st, ct, sp
 
 
-def out_dim_strides(ndim: int, is_int: np.ndarray, drop_axes, out_strides_bytes) -> np.ndarray:
+def out_dim_strides(ndim: int, is_int, drop_axes, out_strides_bytes) -> list:
     """Per decoded dim: the out byte stride (0 for dims absent from out)."""
     kept = [d for d in range(ndim) if not is_int[d]]
-    drop = set(int(a) for a in drop_axes)
-    kept = [d for k, d in enumerate(kept) if k not in drop]
-    st = np.zeros(ndim, np.int64)
+    if drop_axes:
+        drop = set(int(a) for a in drop_axes)
+        kept = [d for k, d in enumerate(kept) if k not in drop]
+    st = [0] * ndim
     if len(kept) != len(out_strides_bytes):
         raise ValueError(f"selection has {len(kept)} output dims, out has {len(out_strides_bytes)}")
     for j, d in enumerate(kept):
-        st[d] = out_strides_bytes[j]
+        st[d] = int(out_strides_bytes[j])
     return st
 
 
@@ -327,7 +330,7 @@ def plan_decode(chain: ChainInfo, spec: ArraySpec, items: list, out_strides_byte
     fill = spec.fill_bytes()
     if not items:
         raise ValueError("empty batch")
-    _, _, _, is_int0 = _sel_fields(items[0][3], ndim)
+    is_int0 = [not isinstance(s, slice) for s in items[0][3]]
     ost_dec = out_dim_strides(ndim, is_int0, drop_axes, out_strides_bytes)
     if NATIVE_PLANNER and (ndim > 1 or chain.shard is not None) and (resolved is None or chain.shard is not None):
         t = _plan_native(chain, spec, items, out_strides_bytes, out_base_ptr, ost_dec, item_out_extra, fill,
@@ -409,7 +412,7 @@ def plan_decode(chain: ChainInfo, spec: ArraySpec, items: list, out_strides_byte
         base = _out_offset(osel, out_strides_bytes) + \
             (0 if item_out_extra is None else int(item_out_extra[i]))
         m = len(pr.coords)
-        oo = base + (pr.out_start * ost_dec[None, :]).sum(axis=1)
+        oo = base + (pr.out_start * np.asarray(ost_dec, np.int64)[None, :]).sum(axis=1)
         parts.append((i, so, sl, miss, pr, oo, m))
     total = sum(p[-1] for p in parts)
     chunks = np.zeros(total, CHUNK_DT)
@@ -552,29 +555,33 @@ def _plan_native(chain: ChainInfo, spec: ArraySpec, items: list, out_strides_byt
     n = len(items)
     shape = spec.shape
     ostr = [int(x) for x in out_strides_bytes]
-    S, E, K, OO = [], [], [], []
+    # zhip_item records as int64 rows: src, src_len, out_off, missing | res << 32,
+    # start[MAX_DIMS], stop[MAX_DIMS], step[MAX_DIMS]
+    MD = N.MAX_DIMS
+    o_st, o_sp, o_sk = 4, 4 + MD, 4 + 2 * MD
+    blank = [0] * (4 + 3 * MD)
+    recs = []
     for so, sl, miss, csel, osel in items:
         if len(csel) != ndim:
             return None
+        row = blank.copy()
+        row[0], row[1], row[3] = so, sl, 1 if miss else 0
         for d, s in enumerate(csel):
             if type(s) is slice:
                 a, b, k = s.indices(shape[d])
                 if k < 1:
                     return None
-                S.append(a)
-                E.append(b)
-                K.append(k)
+                row[o_st + d], row[o_sp + d], row[o_sk + d] = a, b, k
             elif isinstance(s, (int, np.integer)):
                 v = int(s)
-                S.append(v + shape[d] if v < 0 else v)
-                E.append(0)
-                K.append(0)
+                row[o_st + d] = v + shape[d] if v < 0 else v  # stop = step = 0: an integer index
             else:
                 return None
         oo = 0
         for o, w in zip(osel, ostr):
             oo += (o.start or 0) * w if type(o) is slice else int(o) * w
-        OO.append(oo)
+        row[2] = oo
+        recs.append(row)
     g, gp, layout, index_layout, n_inner, fast_l, tile_l, rows_l = _native_ctx(chain, spec, ost_dec, fill,
                                                                                resolved is not None)
     res_p, keep = None, None
@@ -605,14 +612,7 @@ def _plan_native(chain: ChainInfo, spec: ArraySpec, items: list, out_strides_byt
             ri.ctypes.data
         rr["n_rows"], rr["n_inner"] = len(rows), n_inner
         res_p, keep = rr.ctypes.data, (rs, rl, rm, ri, rr)
-    it = np.zeros(n, N.ITEM_DT)
-    it["start"][:, :ndim] = np.array(S, np.int64).reshape(n, ndim)
-    it["stop"][:, :ndim] = np.array(E, np.int64).reshape(n, ndim)
-    it["step"][:, :ndim] = np.array(K, np.int64).reshape(n, ndim)
-    it["out_off"] = OO
-    it["src"] = [x[0] for x in items]
-    it["src_len"] = [x[1] for x in items]
-    it["missing"] = [1 if x[2] else 0 for x in items]
+    it = np.array(recs, np.int64).view(N.ITEM_DT).reshape(n)
     if item_out_extra is not None:
         it["out_off"] += np.asarray(item_out_extra, np.int64)
     if resolved is not None:
@@ -625,19 +625,19 @@ def _plan_native(chain: ChainInfo, spec: ArraySpec, items: list, out_strides_byt
     o_io = o_se + cap * _SEL_SZ
     o_ix = o_io + 4 * cap + (-(4 * cap) % 16)
     o_ii = o_ix + ni * _CH_SZ
-    buf = np.zeros(o_ii + 4 * ni + 16, np.uint8)
+    buf = np.empty(o_ii + 4 * ni + 16, np.uint8)
+    buf[:32] = 0
     b = buf.ctypes.data
     rc = N.lib().zhip_plan_batch(gp, it.ctypes.data, n, res_p, b + o_ch, cap, b, b + o_se, cap, b + 8,
                                  b + o_io, b + o_ix, b + o_ii, b + 12, b + 16)
     del keep
-    cnt = buf[:32].view(np.uint32)
-    if rc == N.E_BOUNDS and cnt[0] == 0 and cnt[1] == 0 and chain.shard is not None and resolved is None:
+    nc, c1, n_sels, n_idx, agg = _struct.unpack_from("<5I", buf, 0)
+    if rc == N.E_BOUNDS and nc == 0 and c1 == 0 and chain.shard is not None and resolved is None:
         raise ValueError("shard blob is shorter than its index")
     N.check(rc, "zhip_plan_batch")
-    nc, n_sels, n_idx, agg = int(cnt[0]), int(cnt[2]), int(cnt[3]), int(cnt[4])
-    chunks = buf[o_ch: o_ch + nc * _CH_SZ].view(CHUNK_DT)
-    sels = buf[o_se: o_se + n_sels * _SEL_SZ].view(SEL_DT)
-    item_of = buf[o_io: o_io + 4 * nc].view(np.uint32).astype(np.int64)
+    chunks = np.frombuffer(buf, CHUNK_DT, nc, o_ch)
+    sels = np.frombuffer(buf, SEL_DT, n_sels, o_se)
+    item_of = np.frombuffer(buf, np.uint32, nc, o_io).astype(np.int64)
     al = out_base_ptr % 16 == 0 and bool(agg & N.AGG_OUT_ALIGNED)
     fast = fast_l and al and bool(agg & N.AGG_LAST_FULL)
     tile = not fast and tile_l and al and bool(agg & N.AGG_ALL_FULL)
@@ -645,8 +645,8 @@ def _plan_native(chain: ChainInfo, spec: ArraySpec, items: list, out_strides_byt
     t = Tables(layout, chunks, sels, fast, item_of, tile=tile, rows=rows)
     if n_idx:
         t.index_layout = index_layout
-        t.index_chunks = buf[o_ix: o_ix + n_idx * _CH_SZ].view(CHUNK_DT)
-        t.index_item = buf[o_ii: o_ii + 4 * n_idx].view(np.uint32).astype(np.int64)
+        t.index_chunks = np.frombuffer(buf, CHUNK_DT, n_idx, o_ix)
+        t.index_item = np.frombuffer(buf, np.uint32, n_idx, o_ii).astype(np.int64)
     return t
 
 

@@ -53,10 +53,14 @@ class ArraySpec:
     def fill_bytes(self) -> bytes:
         """The fill value as native-order item bytes (fill_value_or_default,
         chunk_utils.py:61-71)."""
-        fv = self.fill_value
-        if fv is None:
-            fv = 0
-        return np.asarray(fv, dtype=self.dtype).astype(self.dtype.newbyteorder("=")).tobytes()
+        b = self.__dict__.get("_fill_b")
+        if b is None:  # memoised: the spec is frozen
+            fv = self.fill_value
+            if fv is None:
+                fv = 0
+            b = np.asarray(fv, dtype=self.dtype).astype(self.dtype.newbyteorder("=")).tobytes()
+            object.__setattr__(self, "_fill_b", b)
+        return b
 
 
 def coerce_config(config) -> ArrayConfig:
