@@ -33,6 +33,9 @@ from .store import ALIGN, TAIL_SLACK, DeviceRef, FileRef, MemoryStore, StorePath
 # 4 MiB windows: smaller ones pay ~10 us per hipMemcpyAsync, larger ones start
 # the DMA late (scripts/stage_micro.py)
 WINDOW = int(os.environ.get("ZARR_HIP_STAGE_WINDOW", str(4 << 20)))
+# partial shard reads: shards are staged in runs of this many bytes, each run
+# one packing job begun as soon as its bytes are fetched
+GROUP = int(os.environ.get("ZARR_HIP_STAGE_GROUP", str(64 << 20)))
 MAX_U64 = np.uint64(0xFFFFFFFFFFFFFFFF)
 
 _COPY_STREAMS: dict = {}
@@ -176,56 +179,100 @@ class Pending:
             self.abort()
 
 
-def stage(layout: StagingLayout, device, post=(), defer: bool = False):
-    """Copy every piece to one new device buffer.  Returns (dev, keepalive,
-    pending); with defer the packing job keeps running when this returns and
-    the caller must ``pending.finish()`` before the first use of dev."""
-    import torch
-
+def _piece_table(pieces: list):
+    """zhip_piece records of (buffer-like, dst_off, nbytes) pieces; returns
+    (table, views to keep alive, all pieces page-locked)."""
     from . import _native as N
 
-    _copy_mode()
-    total = max(layout.top, 16)
     # file pieces carry an encoded path (kept alive with the job) and an offset;
     # bytes objects are addressed in place (ctypes.cast: a third of the cost
     # of a numpy view's .ctypes per piece, which adds up over a batch)
     views = [np.frombuffer(buf.path.encode() + b"\0", np.uint8) if isinstance(buf, FileRef)
-             else buf if type(buf) is bytes else _host_view(buf) for buf, _, _ in layout.pieces]
-    pieces = np.zeros(len(views), N.PIECE_DT)
+             else buf if type(buf) is bytes else _host_view(buf) for buf, _, _ in pieces]
+    table = np.zeros(len(views), N.PIECE_DT)
     _cast, _vp = ctypes.cast, ctypes.c_void_p
     addrs = [_cast(v, _vp).value if type(v) is bytes else v.ctypes.data for v in views]
-    pieces["host"] = addrs
-    pieces["nbytes"] = [n for _, _, n in layout.pieces]
-    pieces["dst_off"] = [off for _, off, _ in layout.pieces]
-    files = [isinstance(buf, FileRef) for buf, _, _ in layout.pieces]
+    table["host"] = addrs
+    table["nbytes"] = [n for _, _, n in pieces]
+    table["dst_off"] = [off for _, off, _ in pieces]
+    files = [isinstance(buf, FileRef) for buf, _, _ in pieces]
     flags = [N.PIECE_FILE if f else 0 for f in files]
     if any(files):
-        pieces["file_off"] = [buf.offset if f else 0 for f, (buf, _, _) in zip(files, layout.pieces)]
+        table["file_off"] = [buf.offset if f else 0 for f, (buf, _, _) in zip(files, pieces)]
     spans = pinned_spans()
     if spans:
         flags = [fl or (N.PIECE_PINNED if any(lo <= a and a + n <= hi for lo, hi in spans) else 0)
-                 for fl, a, (_, _, n) in zip(flags, addrs, layout.pieces)]
-    pieces["flags"] = flags
-    all_pinned = bool(flags) and all(fl == N.PIECE_PINNED for fl in flags)
+                 for fl, a, (_, _, n) in zip(flags, addrs, pieces)]
+    table["flags"] = flags
+    return table, views, bool(flags) and all(fl == N.PIECE_PINNED for fl in flags)
+
+
+def _begin_job(pieces: list, dev, dev_off: int, total: int, cs, post=()):
+    """One library packing job: `pieces` (dst offsets relative to dev_off)
+    into dev[dev_off: dev_off + total] on copy stream cs.  Returns its Pending."""
+    import torch
+
+    from . import _native as N
+
+    table, views, all_pinned = _piece_table(pieces)
     # the packing buffer (pinned, reused through torch's caching host allocator)
     host = torch.empty(16 if all_pinned else total + TAIL_SLACK, dtype=torch.uint8, pin_memory=True)
-    dev = torch.empty(total + TAIL_SLACK, dtype=torch.uint8, device=device)
-    compute = torch.cuda.current_stream(device)
-    cs = _copy_stream(device)
-    cs.wait_stream(compute)
-    dev.record_stream(cs)
-    job = N.lib().zhip_stage_begin(pieces.ctypes.data, len(pieces), host.data_ptr(), dev.data_ptr(), total,
-                                   WINDOW, _workers(), cs.cuda_stream)
+    job = N.lib().zhip_stage_begin(table.ctypes.data, len(table), host.data_ptr(), dev.data_ptr() + dev_off,
+                                   total, WINDOW, _workers(), cs.cuda_stream)
     if not job:
         raise N.NativeError("zhip_stage_begin: out of memory")
     # the pinned block and the host views must outlive the copies: the job
     # holds them until it is finished or aborted, the program afterwards
     # (dropped after its results() synchronised)
-    keep = [dev, host, views]
-    pending = Pending(dev, job, cs, list(post), keep)
+    return Pending(dev, job, cs, list(post), [dev, host, views])
+
+
+def _stage_target(total: int, device):
+    """A new device buffer for staged bytes and the copy stream that fills it
+    (after the compute stream's earlier work)."""
+    import torch
+
+    _copy_mode()
+    dev = torch.empty(max(total, 16) + TAIL_SLACK, dtype=torch.uint8, device=device)
+    compute = torch.cuda.current_stream(device)
+    cs = _copy_stream(device)
+    cs.wait_stream(compute)
+    dev.record_stream(cs)
+    return dev, cs
+
+
+def stage(layout: StagingLayout, device, post=(), defer: bool = False):
+    """Copy every piece to one new device buffer.  Returns (dev, keepalive,
+    pending); with defer the packing job keeps running when this returns and
+    the caller must ``pending.finish()`` before the first use of dev."""
+    total = max(layout.top, 16)
+    dev, cs = _stage_target(total, device)
+    pending = _begin_job(layout.pieces, dev, 0, total, cs, post)
     if not defer:
         pending.finish()
-    return dev, keep, pending
+    return dev, pending.keepalive, pending
+
+
+class PendingGroup:
+    """Several packing jobs filling one device buffer, begun as their bytes
+    arrived (Pending's interface: finish / abort / active / keepalive)."""
+
+    def __init__(self, dev, parts: list):
+        self.dev = dev
+        self.parts = parts
+        self.keepalive = [p.keepalive for p in parts]
+
+    @property
+    def active(self) -> bool:
+        return any(p.active for p in self.parts)
+
+    def finish(self, stream: int | None = None) -> None:
+        for p in self.parts:
+            p.finish(stream)
+
+    def abort(self) -> None:
+        for p in self.parts:
+            p.abort()
 
 
 def gather_sources(batch: list, device, defer: bool = False, start: bool = True):
@@ -368,7 +415,6 @@ def gather_sharded_partial(batch: list, sh, cps, n_inner: int, inner_shape, spec
     from .indexing import basic_projections
 
     isz = sh.shard_index_size(n_inner)
-    lay = StagingLayout()
     cps_strides = np.array([int(np.prod(cps[d + 1:])) for d in range(len(cps))], np.int64)
     st_list = [int(x) for x in cps_strides]
     sshape = tuple(int(x) for x in spec.shape)
@@ -386,7 +432,29 @@ def gather_sharded_partial(batch: list, sh, cps, n_inner: int, inner_shape, spec
             sl = (pr.coords * cps_strides[None, :]).sum(axis=1).tolist()
         shards[k]["slots"].update(sl)
         item_shard.append(k)
+    # 1. every touched shard's index (one range request each) and the layout:
+    #    [index bytes][touched inner chunks] per shard, each chunk's size known
+    #    from its index entry (a host-stage chain: the decoded chunk size)
     out_of_shard = {}
+    plans = []
+    top, A = 0, ALIGN - 1
+    cfg = spec.config  # forwarded like sharding.py:1695-1752
+    cap = int(np.prod(ishape)) * spec.dtype.itemsize + 4  # the largest encoded inner chunk of a GPU chain
+
+    def fetch_ranges(bg, st, reqs):
+        """(request index, bytes) of every range, or None when the shard
+        vanished between the index and data reads."""
+        try:
+            if st is not None and hasattr(st, "get_ranges_sync"):
+                return list(st.get_ranges_sync(bg.path, reqs, prototype=spec.prototype,
+                                               max_gap_bytes=cfg.sharding_coalesce_max_gap_bytes,
+                                               max_coalesced_bytes=cfg.sharding_coalesce_max_bytes))
+            return [(j, bg.get_sync(prototype=None, byte_range=r)) for j, r in enumerate(reqs)]
+        except Exception as e:
+            if not is_missing_key_error(e):
+                raise
+            return None
+
     for k, s in shards.items():
         bg = s["bg"]
         st = getattr(bg, "store", None)
@@ -413,58 +481,107 @@ def gather_sharded_partial(batch: list, sh, cps, n_inner: int, inner_shape, spec
             computed = host_crc32c(body)
             if stored != computed:
                 raise ValueError(crc_error_message(stored, computed))
-        idx_off, _ = lay.add(raw) if sh.index_has_crc else (-1, 0)
+        lo = top
+        pieces = []
+        idx_off = -1
+        if sh.index_has_crc:
+            idx_off = top
+            pieces.append((raw, top, len(raw)))
+            top = (top + len(raw) + A) & ~A
         src_by = np.zeros(n_inner, np.int64)
         len_by = np.zeros(n_inner, np.int64)
         miss_by = np.ones(n_inner, bool)
-        slots = sorted(s["slots"])
-        reqs = []
-        want = []
+        reqs, fetch = [], []
+        eager = False
         ent = idx.reshape(-1).tolist()  # plain ints: (offset, length) per slot
-        for slot in slots:
-            o, n = ent[2 * slot], ent[2 * slot + 1]
-            if o == MAX_U64 and n == MAX_U64:
-                continue  # missing inner chunk -> fill (sharding.py:700-712)
-            reqs.append(Range(o, o + n))
-            want.append(slot)
-        if reqs and st is not None and hasattr(st, "locate_sync") and inner_decode is None:
+        whole = None
+        if st is not None and hasattr(st, "locate_sync") and inner_decode is None:
             # a local file: each touched inner chunk is one pread of the shard
             # file by the staging pool (no coalescing needed: no request cost)
             whole = st.locate_sync(bg.path)
             if whole is None:
                 out_of_shard[k] = None
                 continue
-            for slot, r in zip(want, reqs):
-                if r.end > whole.length:
+        for slot in sorted(s["slots"]):
+            o, n = ent[2 * slot], ent[2 * slot + 1]
+            if o == MAX_U64 and n == MAX_U64:
+                continue  # missing inner chunk -> fill (sharding.py:700-712)
+            if whole is not None:
+                if o + n > whole.length:
                     raise ValueError("shard index entry points outside the shard blob")
-                off, n = lay.add(FileRef(whole.path, r.start, r.end - r.start))
-                src_by[slot], len_by[slot], miss_by[slot] = off, n, False
-            out_of_shard[k] = (src_by, len_by, miss_by, idx_off)
-            continue
-        if reqs:
-            cfg = spec.config  # forwarded like sharding.py:1695-1752
-            try:
-                if st is not None and hasattr(st, "get_ranges_sync"):
-                    got = st.get_ranges_sync(bg.path, reqs, prototype=spec.prototype,
-                                             max_gap_bytes=cfg.sharding_coalesce_max_gap_bytes,
-                                             max_coalesced_bytes=cfg.sharding_coalesce_max_bytes)
-                else:
-                    got = [(j, bg.get_sync(prototype=None, byte_range=r)) for j, r in enumerate(reqs)]
-            except Exception as e:  # the shard vanished between the index and data reads
-                if not is_missing_key_error(e):
-                    raise
+                pieces.append((FileRef(whole.path, o, n), top, n))
+                src_by[slot], len_by[slot], miss_by[slot] = top, n, False
+                top = (top + n + A) & ~A
+                continue
+            reqs.append(Range(o, o + n))
+            fetch.append((slot, top, n))
+            top = (top + n + A) & ~A
+            eager = eager or n > cap
+        if reqs and (inner_decode is not None or eager):
+            # a host stage first (its output size is the GPU chain's), or an
+            # index entry longer than any encoded inner chunk (a corrupted
+            # index; the GPU's index check reports it): fetched now, laid out
+            # at the sizes that arrive
+            got = fetch_ranges(bg, st, reqs)
+            if got is None:
                 out_of_shard[k] = None
                 continue
-            got = list(got)
             bufs = [staged_host(buf) for _, buf in got]
             if inner_decode is not None:
                 bufs = inner_decode(bufs)
+            top = pieces[-1][1] + ((pieces[-1][2] + A) & ~A) if pieces else lo
             for (j, _), buf in zip(got, bufs):
-                slot = want[j]
-                off, n = lay.add(buf)
-                src_by[slot], len_by[slot], miss_by[slot] = off, n, False
+                slot = fetch[j][0]
+                pieces.append((buf, top, len(buf)))
+                src_by[slot], len_by[slot], miss_by[slot] = top, len(buf), False
+                top = (top + len(buf) + A) & ~A
+            reqs, fetch = [], []
         out_of_shard[k] = (src_by, len_by, miss_by, idx_off)
-    dev, keep, pending = stage(lay, device, defer=defer)
+        plans.append((k, bg, st, lo, top, pieces, reqs, fetch))
+    # 2. the chunk bytes, shard by shard: each run of shards reaching GROUP
+    #    bytes becomes its own packing job into its slice of the buffer, begun
+    #    as soon as its bytes are fetched, so the copies of early shards overlap
+    #    the requests (and the Python) of later ones
+    dev, cs = _stage_target(top, device)
+    parts: list = []
+    run: list = []
+    run_lo = run_hi = 0
+
+    def emit():
+        if run:
+            parts.append(_begin_job([(b, off - run_lo, n) for b, off, n in run], dev, run_lo, run_hi - run_lo, cs))
+    try:
+        for k, bg, st, lo, hi, pieces, reqs, fetch in plans:
+            if reqs:
+                got = fetch_ranges(bg, st, reqs)
+                if got is None:  # the shard vanished between the index and data reads
+                    out_of_shard[k] = None
+                    continue
+                src_by, len_by, miss_by, _ = out_of_shard[k]
+                for j, buf in got:
+                    buf = staged_host(buf)
+                    slot, off, size = fetch[j]
+                    m = len(buf)
+                    if m > size:
+                        raise ValueError("an inner chunk is larger than its index entry")
+                    pieces.append((buf, off, m))
+                    src_by[slot], len_by[slot], miss_by[slot] = off, m, False
+                pieces.sort(key=lambda x: x[1])  # packing jobs take pieces in destination order
+            if not run:
+                run_lo = lo
+            run.extend(pieces)
+            run_hi = hi
+            if run_hi - run_lo >= GROUP:
+                emit()
+                run = []
+        emit()
+    except BaseException:
+        for p in parts:  # begun jobs must not outlive the buffers they fill
+            p.abort()
+        raise
+    pending = PendingGroup(dev, parts)
+    if not defer:
+        pending.finish()
     missing = np.array([out_of_shard[k] is None for k in item_shard], bool)
     resolved = [out_of_shard[k] for k in item_shard]
-    return dev, lay.top, missing, resolved, keep, pending
+    return dev, top, missing, resolved, pending.keepalive, pending
