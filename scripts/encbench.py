@@ -1,8 +1,9 @@
 #!/usr/bin/env python
 """Encode-only timing for PMC / rocprof passes (measurement only): the C3
 transposed encode on 64^3 chunks (k_encode_tile4, or k_encode_tile with
-TUNE=65536) and on 128^3 chunks (k_encode_tile), graph-timed as bench.py
-does; one JSON line per arm."""
+TUNE=65536), on 128^3 chunks (k_encode_tile) and the C2 encode
+(k_encode_pair), graph-timed as bench.py does, each config with an optional
+ZHIP_TUNE_ARM; one JSON line per arm."""
 
 import json
 import os
@@ -25,12 +26,17 @@ def main():
         N.lib().zhip_set_tuning(2, tune)
     args = type("A", (), {"steps": int(os.environ.get("STEPS", "20")), "tune": tune})()
     dev = torch.device("cuda:0")
-    codecs = [{"name": "transpose", "configuration": {"order": [2, 1, 0]}}, bench.LE, bench.CRC]
-    for name, chunks, want in (("c3_64", (64, 64, 64), "tile4"), ("c3_128", (128, 128, 128), "tile")):
-        if name not in os.environ.get("ARMS", "c3_64,c3_128"):
-            continue
-        src, wall, kern = bench._encode_bench(dev, args, codecs, want, chunks=chunks)
-        print(json.dumps({"arm": name, "tune": tune, "us_graph": round(wall * 1e6, 2),
+    tr = [{"name": "transpose", "configuration": {"order": [2, 1, 0]}}]
+    cfgs = {"c3_64": (tr, (64, 64, 64), "tile4"), "c3_128": (tr, (128, 128, 128), "tile"),
+            "c2": ([], (64, 64, 64), "rows")}
+    # ARMS: comma list of config[:arm] (arm = zhip_set_tuning(ARM), e.g. c2:1)
+    for item in os.environ.get("ARMS", "c3_64,c3_128").split(","):
+        name, _, arm = item.partition(":")
+        aa, chunks, want = cfgs[name]
+        N.lib().zhip_set_tuning(6, int(arm or 0))
+        src, wall, kern = bench._encode_bench(dev, args, aa + [bench.LE, bench.CRC], want, chunks=chunks)
+        N.lib().zhip_set_tuning(6, 0)
+        print(json.dumps({"arm": item, "tune": tune, "us_graph": round(wall * 1e6, 2),
                           "us_eager": round(kern * 1e6, 2),
                           "hbm_frac": round(2 * src / wall / 8e12, 4)}), flush=True)
         torch.cuda.empty_cache()

@@ -925,6 +925,8 @@ int zhip_encode_mapped(const zhip_plan* plan, const void* arr, void* dst, const 
             return set_err(ZHIP_E_INVALID, "row map given for a layout without whole-row encode");
         p.rowmap = d_rowmap;
         p.kpair = plan->d_tables + 4096 + kThreads + plan->nseg;
+        p.pair_tab = plan->d_tables + plan->off_pair;
+        p.kpair11 = p.pair_tab + kPairTabWords;
         p.row_shift = (uint32_t)__builtin_ctz(rb);
         p.r_oy = L.out_stride[nd - 2];
     }

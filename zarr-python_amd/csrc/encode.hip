@@ -20,6 +20,8 @@
 // thread t of a unit owns the 16-byte blocks at lo + 16t + 4096k.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "../../include/zarrhip.h"
 #include "zhip_device.h"
 #include "zhip_gf2.h"
@@ -260,10 +262,14 @@ struct EncRowSteps {
     zhip_rowblk e[kDefaultBlocks];
 };
 
-template <bool CRC, int ITEM, bool SWAP>
+// ACC: uint32_t (one chain, the 16 byte-position tables: p.horner) or Acc4
+// (one accumulator per word through A4096, the 11/11/10 pair tables: 12
+// lookups per block instead of 16, folded at the run end -- k_decode_pair's
+// CRC, zhip_decode_common.h)
+template <bool CRC, int ITEM, bool SWAP, typename ACC>
 __device__ __forceinline__ void enc_unit(const EncodeParams& p, const zhip_chunk& ch, uint32_t sidx, bool live,
                                         const EncRowSteps& m, uint32_t lane_row, const uint4 (&blk)[kDefaultBlocks],
-                                        const uint32_t* s_tab, uint32_t& acc, bool& alleq, int t) {
+                                        const uint32_t* s_tab, ACC& acc, bool& alleq, int t) {
     const uint4 f = make_uint4(p.fill[0], p.fill[1], p.fill[2], p.fill[3]);
     const int32_t seg_lo = (int32_t)p.E - (int32_t)((sidx + 1u) * p.seg);
     uint8_t* const cp = p.dst + ch.src;
@@ -277,11 +283,20 @@ __device__ __forceinline__ void enc_unit(const EncodeParams& p, const zhip_chunk
         const uint4 e = swap_block<ITEM, SWAP>(v);
         enc_store16(live && o >= 0 ? cp + o + 16 * t : sink, e);  // every path stores: static count
         if constexpr (CRC) {
-            if (live && o >= 0)
-                acc = tab_apply(s_tab, acc ^ e.x) ^ tab_apply(s_tab + 1024, e.y) ^ tab_apply(s_tab + 2048, e.z) ^
-                      tab_apply(s_tab + 3072, e.w);
+            if (live && o >= 0) {
+                if constexpr (sizeof(ACC) == sizeof(Acc4)) crc_block4(s_tab, acc, e);
+                else
+                    acc = tab_apply(s_tab, acc ^ e.x) ^ tab_apply(s_tab + 1024, e.y) ^
+                          tab_apply(s_tab + 2048, e.z) ^ tab_apply(s_tab + 3072, e.w);
+            }
         }
     }
+}
+
+template <typename ACC>
+__device__ __forceinline__ uint32_t enc_state(const uint32_t* s_tab, const ACC& acc) {
+    if constexpr (sizeof(ACC) == sizeof(Acc4)) return fold4(s_tab, acc);
+    else return acc;
 }
 
 template <bool CRC>
@@ -364,10 +379,15 @@ __device__ __forceinline__ void enc_run_end_pair(const EncodeParams& p, const zh
     p.status[c] = st;
 }
 
-template <bool CRC, int ITEM, bool SWAP>
+// T11: the CRC through the 11/11/10 pair tables (arm ZHIP_TUNE_ARM = 1)
+// instead of the byte-position tables: 12 lookups per block instead of 16,
+// graph-timed on C2 30.7-30.9 vs 30.5-30.6 us (profiles/r04/g/enc_arms.jsonl):
+// the encode is not bound by its lookups
+template <bool CRC, int ITEM, bool SWAP, bool T11 = false>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_encode_pair(const EncodeParams p) {
     constexpr int K = kDefaultBlocks;
-    __shared__ uint32_t s_tab[CRC ? 16 * 256 : 1];
+    using ACC = typename std::conditional<T11, Acc4, uint32_t>::type;
+    __shared__ uint32_t s_tab[CRC ? (T11 ? kPairTabWords : 16 * 256) : 1];
     __shared__ uint32_t s_red[2][kThreads / 64];
     const int t = threadIdx.x;
     // XCD-contiguous runs for a one-wave grid (launch_encode's xcd_run, as k_decode_pair)
@@ -382,16 +402,21 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     };
     const uint32_t u_a = unit_of(q0), u_b = has_b ? unit_of(q0 + 1u) : u_a;
     const uint32_t ca = u_a / p.nseg, sa = u_a - ca * p.nseg, cb = u_b / p.nseg, sb = u_b - cb * p.nseg;
-    uint4 tv0, tv1, tv2, tv3;
+    uint4 tv0, tv1, tv2, tv3, tv4, tv5;
     uint32_t ka = 0, kb = 0;
     if constexpr (CRC) {
-        const uint4* gt = reinterpret_cast<const uint4*>(p.horner);
+        const uint4* gt = reinterpret_cast<const uint4*>(T11 ? p.pair_tab : p.horner);
         tv0 = gt[t];
         tv1 = gt[t + kThreads];
         tv2 = gt[t + 2 * kThreads];
         tv3 = gt[t + 3 * kThreads];
-        ka = p.kpair[(size_t)sa * kThreads + t];
-        kb = p.kpair[(size_t)sb * kThreads + t];
+        if constexpr (T11) {
+            tv4 = gt[t + 4 * kThreads];
+            tv5 = gt[t + 5 * kThreads];
+        }
+        const uint32_t* kp = T11 ? p.kpair11 : p.kpair;
+        ka = kp[(size_t)sa * kThreads + t];
+        kb = kp[(size_t)sb * kThreads + t];
     }
     const zhip_chunk cha = load_uniform<zhip_chunk>(p.chunks + ca);
     const zhip_chunk chb = load_uniform<zhip_chunk>(p.chunks + cb);
@@ -419,11 +444,15 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
         st[t + kThreads] = tv1;
         st[t + 2 * kThreads] = tv2;
         st[t + 3 * kThreads] = tv3;
+        if constexpr (T11) {
+            st[t + 4 * kThreads] = tv4;
+            st[t + 5 * kThreads] = tv5;
+        }
         __syncthreads();
     }
     // 2. per block: fill test, byteswap, store, Horner step
     const bool same = has_b && cb == ca;
-    uint32_t acc_a = 0, acc_b = 0;
+    ACC acc_a{}, acc_b{};
     bool eq_a = true, eq_b = true;
     enc_unit<CRC, ITEM, SWAP>(p, cha, sa, true, ma, lane_row, A, s_tab, acc_a, eq_a, t);
     if (same) {
@@ -437,7 +466,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     //    the last arrival writes trailer, status and the chunk's non-empty flag
     //    (so the flags need no zeroing and no same-address atomic storm)
     if (p.nseg % 2u == 0u && p.nseg <= 32u) {
-        enc_run_end_pair<CRC>(p, chb, cb, acc_b, kb, (p.nseg - 1u - sb) >> 1, __any(!eq_b), s_red[1], t);
+        enc_run_end_pair<CRC>(p, chb, cb, CRC ? enc_state(s_tab, acc_b) : 0u, kb, (p.nseg - 1u - sb) >> 1,
+                              __any(!eq_b), s_red[1], t);
         return;
     }
     // 3. chunk_is_empty (chunk_utils.py:74-85): any element != fill -> non-empty
@@ -446,10 +476,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
         if (has_b && __any(!eq_b) && (t & 63) == 0) atomicOr(p.nonempty + cb, 1u);
     }
     // 4. run ends: A alone when B starts another chunk, then B (or A+B)
-    if (!same) enc_run_end<CRC>(p, cha, ca, acc_a, ka, 1u << (sa & 31u), 1u, s_red[0], t);
+    if (!same) enc_run_end<CRC>(p, cha, ca, CRC ? enc_state(s_tab, acc_a) : 0u, ka, 1u << (sa & 31u), 1u, s_red[0], t);
     if (has_b)
-        enc_run_end<CRC>(p, chb, cb, acc_b, kb, (same ? 1u << (sa & 31u) : 0u) | (1u << (sb & 31u)), same ? 2u : 1u,
-                         s_red[1], t);
+        enc_run_end<CRC>(p, chb, cb, CRC ? enc_state(s_tab, acc_b) : 0u, kb,
+                         (same ? 1u << (sa & 31u) : 0u) | (1u << (sb & 31u)), same ? 2u : 1u, s_red[1], t);
 }
 
 using EncodeFn = void (*)(const EncodeParams);
@@ -466,6 +496,7 @@ static EncodeFn pick_encode(int item, bool swap) {
 }
 
 static EncodeFn pick_encode_pair(bool crc, int item, bool swap) {
+    if (g_tune_arm == 1 && crc && item == 4 && !swap) return k_encode_pair<true, 4, false, true>;  // 11/11/10 tables
     switch (item) {
         case 1: return crc ? k_encode_pair<true, 1, false> : k_encode_pair<false, 1, false>;
         case 2: return crc ? (swap ? k_encode_pair<true, 2, true> : k_encode_pair<true, 2, false>)

@@ -263,6 +263,8 @@ struct EncodeParams {
     // the two-unit decode; rows of 2^row_shift bytes, r_oy = arr stride of dim ndim-2
     const zhip_rowblk* rowmap;
     const uint32_t* kpair;
+    const uint32_t* pair_tab;  // k_encode_pair: the 11/11/10 tables and their lane constants (kpair11)
+    const uint32_t* kpair11;
     uint32_t row_shift;
     int64_t r_oy;
     uint32_t tune;
