@@ -53,7 +53,12 @@ def main():
     shape, shards, inner = g["shape"], g["shards"], g["inner"]
     src = torch.from_numpy(W.synthetic(shape)).to(dev)
     arr = bench.build_replica(dev, src, shape, inner, [W.LE, W.CRC], shards=shards)
-    sels = [(slice(64 * (i % 4), 64 * (i % 4) + 128 + 64 * (i % 2)), slice(None), slice(None)) for i in range(8)]
+    if os.environ.get("SEL") == "full":  # bench.device_read_call's read_sync_uncached: the whole array
+        sels = [(slice(None), slice(None), slice(None))] * 8
+    elif os.environ.get("SEL") == "bench":  # its varying leg: unaligned 128-row windows
+        sels = [(slice(16 * i + 8, 16 * i + 136), slice(None), slice(None)) for i in range(8)]
+    else:
+        sels = [(slice(64 * (i % 4), 64 * (i % 4) + 128 + 64 * (i % 2)), slice(None), slice(None)) for i in range(8)]
     batches = [arr.batch_info(s) for s in sels]
     outs = [torch.empty(b[1], dtype=torch.float32, device=dev) for b in batches]
     P.READ_CACHE_SIZE = 0

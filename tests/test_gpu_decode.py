@@ -739,19 +739,38 @@ def test_transpose_tileg_many_groups(device):
         assert got == host
 
 
-# ------------------------------------------- deferred CRC verdicts (k_decode_il)
-def _il_array(device, fill=0.0):
+# ------------------------------------------- CRC verdicts across launches
+def _il_array(device, fill=0.0, kind="il"):
     """The headline geometry's chunk shape (64^3 f32 = 1 MiB: eight-workgroup
-    groups, k_decode_il with deferred verdicts) on a small array."""
+    groups, k_decode_il) on a small array; kind "tileg": 96 x 80 x 80 chunks
+    through transpose (2, 1, 0) (k_decode_tileg, whose production publication
+    is the deferred verdicts)."""
     import zarr_hip
 
-    shape, chunks = (128, 64, 64), (64, 64, 64)
-    meta = O.ArrayMeta(shape, chunks, np.dtype("float32"), fill, codecs=[LE, CRC])
+    shape, chunks, codecs = (128, 64, 64), (64, 64, 64), [LE, CRC]
+    if kind == "tileg":
+        shape, chunks, codecs = (192, 80, 80), (96, 80, 80), [T((2, 1, 0)), LE, CRC]
+    meta = O.ArrayMeta(shape, chunks, np.dtype("float32"), fill, codecs=codecs)
     host = {}
     O.write(host, meta, (Ellipsis,), _data(shape, "float32"))
     store = zarr_hip.DeviceStore.from_host(host, device)
-    arr = zarr_hip.Array.create(store, shape, chunks, "float32", fill, codecs=[LE, CRC])
+    arr = zarr_hip.Array.create(store, shape, chunks, "float32", fill, codecs=codecs)
     return arr, store, host, meta
+
+
+# (kind, ZHIP_TUNE_ARM): k_decode_il's returning publication (production),
+# its deferred-verdict arm, and k_decode_tileg's deferred verdicts
+VERDICT_CASES = [("il", 0), ("il", 2), ("tileg", 0)]
+
+
+@pytest.fixture
+def verdict_case(request):
+    from zarr_hip import _native as N
+
+    kind, arm = request.param
+    N.lib().zhip_set_tuning(6, arm)
+    yield kind
+    N.lib().zhip_set_tuning(6, 0)
 
 
 def _corrupt(store, host, key, at=4321):
@@ -762,18 +781,19 @@ def _corrupt(store, host, key, at=4321):
     host[key] = bytes(b)
 
 
-def test_deferred_verdict_sticky_over_eager_launches(device):
+@pytest.mark.parametrize("verdict_case", VERDICT_CASES, indirect=True)
+def test_deferred_verdict_sticky_over_eager_launches(device, verdict_case):
     """Launches without a result check in between: a chunk corrupted before an
-    even number of launches still raises (consecutive launches publish into
-    alternate banks and each checks the previous one), with the reference's
-    message; then the restored bytes read clean."""
+    even number of launches still raises (deferred verdicts: consecutive
+    launches publish into alternate banks and each checks the previous one),
+    with the reference's message; then the restored bytes read clean."""
     from zarr_hip import _native as N
 
-    arr, store, host, meta = _il_array(device)
+    arr, store, host, meta = _il_array(device, kind=verdict_case)
     prog, out = arr.prepare_read((Ellipsis,))
     prog.launch()
     prog.results()
-    assert N.lib().zhip_last_kernel().decode() == "k_decode_il"
+    assert N.lib().zhip_last_kernel().decode() == "k_decode_" + verdict_case
     clean = dict(host)
     _corrupt(store, host, "c/1/0/0")
     with pytest.raises(ValueError) as want:
@@ -792,14 +812,15 @@ def test_deferred_verdict_sticky_over_eager_launches(device):
     assert out.cpu().numpy().tobytes() == O.read(host, meta).tobytes()
 
 
+@pytest.mark.parametrize("verdict_case", VERDICT_CASES, indirect=True)
 @pytest.mark.parametrize("repeats", [1, 2, 3])
-def test_deferred_verdict_graph_replays(device, repeats):
+def test_deferred_verdict_graph_replays(device, repeats, verdict_case):
     """A captured read loop with 1, 2 or 3 launches of one program, replayed
     twice between result checks: corruption after capture raises (an odd
     count ends the graph with a zhip_dv_check node), clean data does not."""
     import zarr_hip
 
-    arr, store, host, meta = _il_array(device)
+    arr, store, host, meta = _il_array(device, kind=verdict_case)
     prog, out = arr.prepare_read((Ellipsis,))
     g = zarr_hip.ReadGraph([prog], repeats, device)
     assert (g._dv_refs is not None) == (repeats % 2 == 1)

@@ -68,9 +68,14 @@ _BUF_POOL: dict = {}
 _BUF_POOL_MAX = 8
 
 
+def _dev_key(device) -> int:
+    idx = getattr(device, "index", device)
+    return _torch().cuda.current_device() if idx is None else int(idx)
+
+
 def _pool_take(kind: str, n: int, device, dtype):
     torch = _torch()
-    key = (kind, n, str(device))
+    key = (kind, n, _dev_key(device))
     lst = _BUF_POOL.get(key)
     if lst:
         return lst.pop()
@@ -80,7 +85,7 @@ def _pool_take(kind: str, n: int, device, dtype):
 
 
 def _pool_give(kind: str, t) -> None:
-    key = (kind, t.numel(), str(t.device))
+    key = (kind, t.numel(), t.device.index)
     lst = _BUF_POOL.setdefault(key, [])
     if len(lst) < _BUF_POOL_MAX:
         lst.append(t)
@@ -117,11 +122,12 @@ class _Upload:
         else:
             self.dev = torch.empty(total, dtype=torch.uint8, device=self.device)
         n = len(self.parts)
-        ptrs = (ctypes.c_void_p * n)(*[b.ctypes.data for _, b in self.parts])
-        sizes = (ctypes.c_uint64 * n)(*[b.nbytes for _, b in self.parts])
-        offs = (ctypes.c_uint64 * n)(*[o for o, _ in self.parts])
+        # one ctypes block: [host pointers][sizes][offsets]
+        arg = (ctypes.c_uint64 * (3 * n))(*([b.ctypes.data for _, b in self.parts] +
+                                           [b.nbytes for _, b in self.parts] + [o for o, _ in self.parts]))
+        a = ctypes.addressof(arg)
         base = self.dev.data_ptr()
-        N.check(N.lib().zhip_upload(ptrs, sizes, offs, n, base, total, stream), "zhip_upload")
+        N.check(N.lib().zhip_upload(a, a + 8 * n, a + 16 * n, n, base, total, stream), "zhip_upload")
         return [base + o for o, _ in self.parts]
 
 
@@ -137,13 +143,24 @@ _PLAN_CACHE: dict = {}
 
 def get_plan(layout: N.Layout) -> N.Plan:
     """Plans are cached per (layout bytes, device): building them is host math +
-    one small upload, kept off the timed path."""
+    one small upload, kept off the timed path.  A layout object also keeps its
+    plans (the per-geometry layouts of the native planner are reused across
+    calls: no key bytes to build)."""
     torch = _torch()
-    key = (bytes(layout), torch.cuda.current_device())
+    dev = torch.cuda.current_device()
+    mine = layout.__dict__.get("_zplans")
+    if mine is not None:
+        p = mine.get(dev)
+        if p is not None:
+            return p
+    key = (bytes(layout), dev)
     p = _PLAN_CACHE.get(key)
     if p is None:
         p = N.Plan(layout, upload=True)
         _PLAN_CACHE[key] = p
+    if mine is None:
+        mine = layout.__dict__.setdefault("_zplans", {})
+    mine[dev] = p
     return p
 
 
@@ -633,6 +650,31 @@ def _read_key(batch: list, dev_out, drop_axes):
     return tuple(parts)
 
 
+def _one_device_store(batch: list, device):
+    """(store, srcs) when every item is a StorePath into ONE DeviceStore on
+    `device` (the per-call read of a device-resident array): the placements
+    straight from its index, no per-item getter chain; else None."""
+    from .store import StorePath
+
+    bg0 = batch[0][0]
+    if type(bg0) is not StorePath:
+        return None
+    st = bg0.store
+    if type(st) is not DeviceStore or not _same_device(st.device, device):
+        return None
+    idx = st._index
+    srcs = []
+    for it in batch:
+        bg = it[0]
+        if type(bg) is not StorePath or bg.store is not st:
+            return None
+        v = idx.get(bg.path)
+        srcs.append((0, 0, True) if v is None else (v[0], v[1], False))
+    if all(s[2] for s in srcs):
+        return None  # nothing present: the general path's zero-source handling
+    return st, srcs
+
+
 def _store_ref(st):
     r = getattr(st, "_zhip_wref", None)
     if r is None or r() is not st:
@@ -953,11 +995,15 @@ class HipCodecPipeline:
             raise TypeError("out dtype itemsize does not match the array dtype")
         chain: ChainInfo = self._chain(spec)
         resolved = None
+        one = None if chain.inner_host else _one_device_store(batch, device)
         # host-resident bytes are packed and copied on the stager thread while
         # this thread plans; the launch waits for them (DecodeProgram.pending)
         # (a sharded chain whose inner chunks pass a host stage always reads
         # through the host: the touched inner chunks are decoded there first)
-        if chain.shard is not None and (chain.inner_host or not _device_resident(batch, device)):
+        if one is not None:  # one DeviceStore: its arena is the source
+            arena = one[0].arena
+            src, size, srcs, keep, pending = arena.buf, arena.top, one[1], [arena.buf], None
+        elif chain.shard is not None and (chain.inner_host or not _device_resident(batch, device)):
             sh = chain.shard
             cps = sh.chunks_per_shard(spec.shape)
             src, size, item_missing, resolved, keep, pending = staging.gather_sharded_partial(
@@ -1004,7 +1050,8 @@ class HipCodecPipeline:
             raise
         return DecodeProgram(t, data, index, len(batch), chain.shard is not None,
                              np.array([s[2] for s in srcs], bool), keepalive=keep, pending=pending,
-                             generations=_generations(batch))
+                             generations=((one[0].arena, one[0].arena.gen),) if one is not None
+                             else _generations(batch))
 
     def read_sync(self, batch_info: Iterable, out, drop_axes: tuple = (),
                   max_workers: int = 1) -> tuple[GetResult, ...]:

@@ -483,13 +483,12 @@ def _native_ctx(chain: ChainInfo, spec: ArraySpec, ost_dec, fill, staged: bool =
     """Per-geometry constants of the native planner (layouts, the
     zhip_batch_geom record, the layout halves of the kernel choice), built
     once per (chain, chunk spec, out strides)."""
-    key = (chain, spec.shape, spec.dtype.str, fill, tuple(int(x) for x in ost_dec), staged)
-    try:
-        ctx = _NATIVE_CTX.get(key)
-    except TypeError:  # an unhashable codec object in the chain: no caching
-        key, ctx = None, None
-    if ctx is not None:
-        return ctx
+    # (the chain by identity, held by the entry: pipelines memoise their
+    # chains, and hashing one walks its codecs)
+    key = (id(chain), spec.shape, spec.dtype.str, fill, tuple(ost_dec), staged)
+    hit = _NATIVE_CTX.get(key)
+    if hit is not None and hit[0] is chain:
+        return hit[1]
     ndim = spec.ndim
     shape = spec.shape
     g = np.zeros(1, N.GEOM_DT)
@@ -534,10 +533,9 @@ def _native_ctx(chain: ChainInfo, spec: ArraySpec, ost_dec, fill, staged: bool =
         rb = layout.shape[last] * isz
         rows_l = 16 <= rb <= 4096 and not rb & (rb - 1) and layout.shape[nd - 2] % (4096 // rb) == 0
     ctx = (g, g.ctypes.data, layout, index_layout, n_inner, fast_l, tile_l, rows_l)
-    if key is not None:
-        if len(_NATIVE_CTX) > 256:
-            _NATIVE_CTX.clear()
-        _NATIVE_CTX[key] = ctx
+    if len(_NATIVE_CTX) > 256:
+        _NATIVE_CTX.clear()
+    _NATIVE_CTX[key] = (chain, ctx)
     return ctx
 
 
