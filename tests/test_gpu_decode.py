@@ -421,11 +421,11 @@ def test_transpose_tile4_crc_mismatch(device):
 def test_transpose_tile4f_chain(device, dtype, endian, chunks, shape):
     """The k_decode_tile4f arm (kTuneTile4F, bit 31: the four tiles of a
     workgroup are 1 KiB of every stored row, one A_64 chain per thread) decodes
-    exactly what the oracle wrote; without the bit k_decode_tile4 runs."""
+    exactly what the oracle wrote; without the bit k_decode_tile4w runs."""
     from zarr_hip import _native as N
 
     _roundtrip(device, shape, chunks, dtype, [T((2, 1, 0)), endian, CRC])
-    assert N.lib().zhip_last_kernel() == b"k_decode_tile4"
+    assert N.lib().zhip_last_kernel() == b"k_decode_tile4w"
     N.lib().zhip_set_tuning(2, -(1 << 31))
     try:
         # every case: 256-byte stored rows, one 64-row tile along the transposed dim
@@ -895,5 +895,40 @@ def test_il_arms_exact_and_crc(device, arm):
             prog.launch()
             prog.results()
         assert out.cpu().numpy().tobytes() == O.read(host, meta).tobytes()
+    finally:
+        N.lib().zhip_set_tuning(6, 0)
+
+
+@pytest.mark.parametrize("arm", [0, 5])
+@pytest.mark.parametrize("dtype,endian,chunks,shape", TILE4_CASES)
+def test_transpose_tile4w_and_tile4(device, dtype, endian, chunks, shape, arm):
+    """k_decode_tile4w (production for CRC layouts: a wave per tile, one
+    A_(4 sq) chain per lane) and k_decode_tile4 (ZHIP_TUNE_ARM = 5) decode
+    exactly what the oracle wrote and report a corrupted chunk with the
+    reference's message."""
+    import zarr_hip
+    from zarr_hip import _native as N
+
+    codecs = [T((2, 1, 0)), endian, CRC]
+    kernel = b"k_decode_tile4" if arm else b"k_decode_tile4w"
+    N.lib().zhip_set_tuning(6, arm)
+    try:
+        _roundtrip(device, shape, chunks, dtype, codecs)
+        assert N.lib().zhip_last_kernel() == kernel
+        meta = O.ArrayMeta(shape, chunks, np.dtype(dtype), 0, codecs=codecs)
+        host = {}
+        O.write(host, meta, (Ellipsis,), _data(shape, dtype))
+        key = sorted(k for k in host if not k.endswith("zarr.json"))[-1]
+        bad = bytearray(host[key])
+        bad[len(bad) // 3] ^= 0x20
+        host[key] = bytes(bad)
+        with pytest.raises(ValueError) as want:
+            O.read(host, meta)
+        arr = zarr_hip.Array.create(zarr_hip.DeviceStore.from_host(host, device), shape, chunks, dtype, 0,
+                                    codecs=codecs)
+        with pytest.raises(ValueError) as got:
+            arr[...]
+        assert str(got.value) == str(want.value)
+        assert N.lib().zhip_last_kernel() == kernel
     finally:
         N.lib().zhip_set_tuning(6, 0)

@@ -434,7 +434,11 @@ int zhip_plan_upload(zhip_plan* p) {
         // 16 (t%4) + 64 n, n < 16) form one chain of stride 64 B
         const bool t4f = t4 && step == (uint64_t)kTileCols && (L.flags & ZHIP_LF_CRC);
         const size_t n_t4f = t4f ? kPairTabWords + (size_t)(T / 4) * kThreads : 0;
-        std::vector<uint32_t> ht(n_base + n_t4 + n_g + n_t4f);
+        // k_decode_tile4w: wave w of a workgroup owns tile w; lane l its rows
+        // l/16 + 4 m (m < 16) at column block l % 16: one chain of stride 4 sq
+        const bool t4w = t4 && (L.flags & ZHIP_LF_CRC);
+        const size_t n_t4w = t4w ? kPairTabWords + (size_t)(T / 4) * kThreads : 0;
+        std::vector<uint32_t> ht(n_base + n_t4 + n_g + n_t4f + n_t4w);
         build_horner_stride(ht.data(), 16ull * sq);
         for (int t = 0; t < kThreads; ++t) {
             const uint64_t rel = (uint64_t)(kTileRows + t / 16) * sq + 16u * (t % 16);
@@ -525,6 +529,25 @@ int zhip_plan_upload(zhip_plan* p) {
                 for (int t = 0; t < kThreads; ++t) {
                     const int64_t p0 = (int64_t)base[4 * g4] + (int64_t)(t / 4) * (int64_t)sq + 16 * (t % 4);
                     const int64_t e = (int64_t)p->E - p0 + kWgStride - 16 * 64;
+                    const uint32_t xe = e >= 0 ? xpow8((uint64_t)e) : xpow8_inv((uint64_t)(-e));
+                    f[kPairTabWords + (size_t)g4 * kThreads + t] = gf_mul(gf_mul(xe, p->c_inv), c96);
+                }
+        }
+        p->tile4w = t4w ? 1u : 0u;
+        p->tile4w_off = n_base + n_t4 + n_g + n_t4f;
+        if (t4w) {
+            // A_(4 sq); lane constant (the il frame, D = 4 sq, 16 blocks)
+            // x^(8 (E - p_0 + 4096 - 16 D)) c_inv x^(-96), p_0 = base[4 g + w] +
+            // (l / 16) sq + 16 (l % 16) for thread t = 64 w + l
+            uint32_t* f = &ht[p->tile4w_off];
+            const uint64_t D = 4ull * sq;
+            build_pair_tables(f, D);
+            const uint32_t c96 = xpow8_inv(12);
+            for (uint32_t g4 = 0; g4 < T / 4; ++g4)
+                for (int t = 0; t < kThreads; ++t) {
+                    const int w = t / 64, l = t % 64;
+                    const int64_t p0 = (int64_t)base[4 * g4 + w] + (int64_t)(l / 16) * (int64_t)sq + 16 * (l % 16);
+                    const int64_t e = (int64_t)p->E - p0 + kWgStride - 16 * (int64_t)D;
                     const uint32_t xe = e >= 0 ? xpow8((uint64_t)e) : xpow8_inv((uint64_t)(-e));
                     f[kPairTabWords + (size_t)g4 * kThreads + t] = gf_mul(gf_mul(xe, p->c_inv), c96);
                 }
@@ -793,6 +816,11 @@ int zhip_decode_mapped(const zhip_plan* plan, const void* src, uint64_t src_size
             if (plan->tile4f && (g_tune_bits & kTuneTile4F)) {  // arm: measured 0.3-0.4 us slower on C3
                 p.t4f_tab = plan->d_tile_tables + plan->tile4f_off;
                 p.t4f_kq = p.t4f_tab + kPairTabWords;
+            } else if (plan->tile4w && g_tune_arm != 1 && g_tune_arm != 2 && g_tune_arm != 5) {
+                // production for CRC layouts: a wave per tile, one chain per lane (k_decode_tile4w:
+                // C3 28.9 vs 30.3-30.6 us, profiles/r04/k); arms 1 / 2 / 5: k_decode_tile4
+                p.t4w_tab = plan->d_tile_tables + plan->tile4w_off;
+                p.t4w_kq = p.t4w_tab + kPairTabWords;
             }
         } else if (plan->gd >= 0 && !(g_tune_bits & kTuneTile1) &&
                    L.shape[plan->tq] % (16 / L.itemsize) == 0) {

@@ -500,6 +500,7 @@ KernelFn select_il_kernel_regmul(bool crc, int item, bool swap, bool occ6);  // 
 KernelFn select_xw_kernel(bool crc, int item, bool swap);            // decode_rows.hip
 KernelFn select_tile4_kernel(bool crc, int item, bool swap);         // decode_tile.hip
 KernelFn select_tile4f_kernel(int item, bool swap);                  // decode_tile.hip
+KernelFn select_tile4w_kernel(int item, bool swap);                  // decode_tile.hip
 KernelFn select_tileg_kernel(bool crc, int item, bool swap);         // decode_tile.hip
 
 // name of the kernel the last launch_decode chose (zhip_last_kernel: bench
@@ -629,11 +630,14 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
         // (arm kTuneTile4F: one A_64 chain per thread when the layout's tile step is
         // 256 B, k_decode_tile4f -- exact, measured 0.3-0.4 us slower on C3)
         const bool f4 = p.t4f_tab != nullptr && (p.lflags & ZHIP_LF_CRC) != 0;
-        KernelFn fn = f4 ? select_tile4f_kernel(p.g.itemsize, (p.lflags & ZHIP_LF_SWAP) != 0)
-                         : select_tile4_kernel((p.lflags & ZHIP_LF_CRC) != 0, p.g.itemsize, (p.lflags & ZHIP_LF_SWAP) != 0);
+        const bool w4 = !f4 && p.t4w_tab != nullptr && (p.lflags & ZHIP_LF_CRC) != 0;
+        const bool swp = (p.lflags & ZHIP_LF_SWAP) != 0;
+        KernelFn fn = f4 ? select_tile4f_kernel(p.g.itemsize, swp)
+                      : w4 ? select_tile4w_kernel(p.g.itemsize, swp)
+                           : select_tile4_kernel((p.lflags & ZHIP_LF_CRC) != 0, p.g.itemsize, swp);
         if (!fn) return ZHIP_E_UNSUPPORTED;
         if (p.n_units == 0) return ZHIP_OK;
-        g_last_kernel = f4 ? "k_decode_tile4f" : "k_decode_tile4";
+        g_last_kernel = f4 ? "k_decode_tile4f" : w4 ? "k_decode_tile4w" : "k_decode_tile4";
         hipLaunchKernelGGL(fn, dim3(p.n_units / 4u), dim3(kThreads), 0, stream, p);
         return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
     }

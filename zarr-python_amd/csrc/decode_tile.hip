@@ -446,6 +446,166 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     }
 }
 
+// k_decode_tile4w: k_decode_tile4 with one CRC chain per lane and one wave
+// per tile.  Wave w of a workgroup loads tile w (of its four): lane l takes
+// rows l/16 + 4 m (m < 16) at column block l % 16, so a wave instruction
+// still loads four whole 256-byte rows (k_decode_tile4's width; k_decode_tile4f
+// lost on its 64-byte pieces) and the lane's 16 blocks are 4 sq apart in the
+// stored stream: ONE Horner chain through A_(4 sq) in the pair kernel's
+// 11/11/10 layout (12 LDS lookups per block instead of 16, no tile-to-tile
+// carry), one fold, one lane multiply by a host-built constant in the il
+// frame (capi.cpp), one publication (a 128-byte line per chunk).  In tile
+// iteration j wave j writes the whole 16 KiB image of tile j; every wave then
+// reads it back in out order and stores, and takes four Horner steps of its
+// own chain.  24 KiB of tables + the 16 KiB image: four workgroups per CU.
+// Production for transposed layouts with a CRC since round 4: C3 28.9 vs
+// 30.3-30.6 us graph-timed (profiles/r04/k/arms_c3.jsonl); ZHIP_TUNE_ARM 5
+// (or 1 / 2, its publication arms) takes k_decode_tile4.
+template <int ITEM, bool SWAP>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_decode_tile4w(
+    const DecodeParams p) {
+    constexpr int kPer = 16 / ITEM;
+    constexpr int kPiecesPerCol = kTileRows / kPer;
+    constexpr int KB = kTileRows / 4;  // blocks per lane
+    __shared__ __attribute__((aligned(16))) uint32_t s_mem[kPairTabWords + kTileRows * 64];
+    uint32_t* const s_tab = s_mem;
+    uint8_t* const s_tile = reinterpret_cast<uint8_t*>(s_mem + kPairTabWords);
+    uint32_t* const s_red = s_mem + kPairTabWords;  // after the last out-order pass
+    const int t = threadIdx.x;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane((uint32_t)t >> 6);  // this wave's tile
+    const uint32_t ln = (uint32_t)t & 63u, rg = ln >> 4, cl = 16u * (ln & 15u);
+    const uint32_t g = blockIdx.x;
+    const uint32_t gpc = p.t_per_chunk / kTiles;
+    const uint32_t c = g / gpc;
+    const uint32_t grp = g - c * gpc;
+    const uint32_t expected = p.g.nbytes + 4u;
+    // 1. tables and the lane constant (L2 hits), the chunk header, 16 data blocks
+    const uint4* gt = reinterpret_cast<const uint4*>(p.t4w_tab);
+    const uint4 tv0 = gt[t], tv1 = gt[t + kThreads], tv2 = gt[t + 2 * kThreads], tv3 = gt[t + 3 * kThreads],
+                tv4 = gt[t + 4 * kThreads], tv5 = gt[t + 5 * kThreads];
+    const uint32_t kq = p.t4w_kq[(size_t)grp * kThreads + t];
+    const Unit U = resolve_unit(p, c * p.nseg, expected);
+    const TileMap4 tm = load_uniform<TileMap4>(p.tmap + (size_t)grp * kTiles);
+    const TileEnt mine = load_uniform<TileEnt>(p.tmap + (size_t)grp * kTiles + wv);
+    const bool ok = U.mode == ZHIP_ST_OK;
+    const uint32_t sq = p.sstride[p.tq];
+    const uint8_t* zero = reinterpret_cast<const uint8_t*>(g_tile_zero);
+    uint4 blk[KB];
+#pragma unroll
+    for (int m = 0; m < KB; ++m)
+        blk[m] = load_stream16_a1(ok ? U.cp + mine.tbase + (rg + 4u * (uint32_t)m) * sq + cl : zero);
+    uint32_t stored = 0;
+    if (ok) stored = load_trailer_uniform(U.cp, p.g.nbytes);
+    {
+        uint4* st = reinterpret_cast<uint4*>(s_tab);
+        st[t] = tv0;
+        st[t + kThreads] = tv1;
+        st[t + 2 * kThreads] = tv2;
+        st[t + 3 * kThreads] = tv3;
+        st[t + 4 * kThreads] = tv4;
+        st[t + 5 * kThreads] = tv5;
+    }
+    // 2. per tile: wave j writes tile j into LDS in stored order, every wave
+    //    reads it back in out order and stores 16-byte pieces, then takes four
+    //    Horner steps of its own chain
+    const bool writes = ok || U.mode == ZHIP_ST_MISSING;
+    const uint4 f = make_uint4(p.fill[0], p.fill[1], p.fill[2], p.fill[3]);
+    const int32_t last = p.g.ndim - 1;
+    const int64_t oq = p.g.ostride[p.tq];
+    const int64_t ocol = p.g.ostride[last];
+    uint8_t* const obase = p.out + U.out_off;
+    uint8_t* const sink = reinterpret_cast<uint8_t*>(g_tile_sink) + 16 * t;
+    Acc4 acc = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int j = 0; j < kTiles; ++j) {
+        if (j > 0) __syncthreads();  // the previous tile's LDS reads are done
+        if (wv == (uint32_t)j) {
+#pragma unroll
+            for (int m = 0; m < KB; ++m)
+                tile_put16<ITEM>(s_tile, rg + 4u * (uint32_t)m, cl, swap_block<ITEM, SWAP>(blk[m]));
+        }
+        __syncthreads();  // tile j (and, first time, the tables) in LDS
+#pragma unroll
+        for (int k = 0; k < kPasses; ++k) {
+            const uint32_t pc = (uint32_t)(k * kThreads + t);
+            const uint32_t jc = pc / kPiecesPerCol;
+            const uint32_t r0 = (pc % kPiecesPerCol) * kPer;
+            uint32_t w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int e = 0; e < kPer; ++e) {
+                const uint8_t* src = s_tile + tile_byte<ITEM>(r0 + e, jc * ITEM);
+                if constexpr (ITEM == 8) {
+                    const uint2 v = *reinterpret_cast<const uint2*>(src);
+                    w[2 * e] = v.x;
+                    w[2 * e + 1] = v.y;
+                } else if constexpr (ITEM == 4) {
+                    w[e] = *reinterpret_cast<const uint32_t*>(src);
+                } else if constexpr (ITEM == 2) {
+                    w[e / 2] |= (uint32_t)(*reinterpret_cast<const uint16_t*>(src)) << (16 * (e & 1));
+                } else {
+                    w[e / 4] |= (uint32_t)(*src) << (8 * (e & 3));
+                }
+            }
+            uint8_t* dst = writes ? obase + tm.e[j].orel + (int64_t)jc * ocol + (int64_t)r0 * oq : sink;
+            store_nt16(dst, ok ? make_uint4(w[0], w[1], w[2], w[3]) : f);
+        }
+        if (ok) {
+#pragma unroll
+            for (int m = 4 * j; m < 4 * j + 4; ++m) crc_block4(s_tab, acc, blk[m]);
+        }
+    }
+    // 3. run end: fold, lane multiply, reduce, publish (returning, the chunk's
+    //    word alone in its 128-byte line); the arrival completing the chunk
+    //    compares with the trailer
+    if (ok) {
+        const uint32_t v = wave_xor(lanemul_reg(kq, fold4(s_tab, acc)));
+        __syncthreads();  // every out-order read of the last tile is done: s_red reuses the image
+        if ((t & 63) == 0) s_red[t >> 6] = v;
+        __syncthreads();
+        if (t < 64) {
+            const uint32_t V = __builtin_amdgcn_readfirstlane(s_red[0] ^ s_red[1] ^ s_red[2] ^ s_red[3]);
+            uint32_t raw = 0, last_arrival = 0;
+            if (t == 0) {
+                if (gpc <= 32) {
+                    const uint64_t full = gpc == 32 ? 0xFFFFFFFFull : ((1ull << gpc) - 1ull);
+                    const uint64_t bits = 1ull << grp;
+                    uint64_t* w = reinterpret_cast<uint64_t*>(p.ws) + (uint64_t)(kPubLine / 2u) * c;
+                    const uint64_t prev = __hip_atomic_fetch_xor(w, (bits << 32) | V, __ATOMIC_RELAXED,
+                                                                 __HIP_MEMORY_SCOPE_AGENT);
+                    if (((prev >> 32) ^ bits) == full) {
+                        __hip_atomic_store(w, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        raw = (uint32_t)prev ^ V;
+                        last_arrival = 1;
+                    }
+                } else {  // more than 32 workgroups per chunk: xor, then count arrivals
+                    uint32_t* accw = p.ws + 4ull * c;
+                    const uint32_t prev = __hip_atomic_fetch_xor(accw, V, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    asm volatile("s_waitcnt vmcnt(0)" ::"v"(prev) : "memory");
+                    const uint32_t tk = __hip_atomic_fetch_add(accw + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (tk + 1u == gpc) {
+                        raw = __hip_atomic_exchange(accw, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store(accw + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        last_arrival = 1;
+                    }
+                }
+                if (last_arrival) {
+                    const uint32_t computed = ~(raw ^ p.c3);  // the lane constants carry c_inv
+                    const uint32_t code = computed == stored ? ZHIP_ST_OK : ZHIP_ST_CRC_MISMATCH;
+                    zhip_status st = {code, stored, computed, 0u};
+                    p.status[c] = st;
+                    if (code != ZHIP_ST_OK) atomicOr(p.errflag, 1u << code);
+                }
+            }
+        }
+    }
+    // statuses not produced by the CRC finalize
+    if (grp == 0 && t == 0 && !ok) {
+        zhip_status st = {U.mode, 0u, 0u, 0u};
+        p.status[c] = st;
+        if (U.mode != ZHIP_ST_MISSING) atomicOr(p.errflag, 1u << U.mode);
+    }
+}
+
 // Arrival of one workgroup of a grouped tile kernel (k_decode_tileg /
 // k_encode_tileg) with its CRC contribution v and non-empty bit: 64-bit words
 // CRC (low 32) | arrival bits (32..47) | non-empty bits (48..63), one relaxed
@@ -1241,6 +1401,16 @@ KernelFn select_tileg_kernel(bool crc, int item, bool swap) {
                            : (swap ? k_decode_tileg<false, 4, true> : k_decode_tileg<false, 4, false>);
         case 8: return crc ? (swap ? k_decode_tileg<true, 8, true> : k_decode_tileg<true, 8, false>)
                            : (swap ? k_decode_tileg<false, 8, true> : k_decode_tileg<false, 8, false>);
+        default: return nullptr;
+    }
+}
+
+KernelFn select_tile4w_kernel(int item, bool swap) {  // CRC chains only
+    switch (item) {
+        case 1: return k_decode_tile4w<1, false>;
+        case 2: return swap ? k_decode_tile4w<2, true> : k_decode_tile4w<2, false>;
+        case 4: return swap ? k_decode_tile4w<4, true> : k_decode_tile4w<4, false>;
+        case 8: return swap ? k_decode_tile4w<8, true> : k_decode_tile4w<8, false>;
         default: return nullptr;
     }
 }

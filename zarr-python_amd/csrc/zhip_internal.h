@@ -113,6 +113,9 @@ struct DecodeParams {
     // k_decode_tile4f (non-null: the layout qualifies): A_64 pair tables, lane constants
     const uint32_t* t4f_tab;
     const uint32_t* t4f_kq;
+    // k_decode_tile4w (non-null: taken): A_(4 sq) pair tables, lane constants
+    const uint32_t* t4w_tab;
+    const uint32_t* t4w_kq;
     // k_decode_tileg (tileg != 0): group map, step multiply table, steps
     uint32_t tileg;
     const struct GroupEnt* gmap;
@@ -347,6 +350,10 @@ struct zhip_plan {
     // layout | lane constants [T/4][kThreads], at tile4f_off in d_tile_tables
     uint32_t tile4f;
     uint64_t tile4f_off;
+    // k_decode_tile4w (tile4 layouts with a CRC): A_(4 sq) tables in the
+    // kPairTab* layout | lane constants [T/4][kThreads], at tile4w_off
+    uint32_t tile4w;
+    uint64_t tile4w_off;
     // k_encode_tileg (full selections): tiles grouped by four along the
     // innermost other stored dim gd with shape[gd] % 4 == 0 (uniform step
     // sstride[gd] inside every group, whatever the natural tile order); tables
