@@ -748,7 +748,7 @@ def _il_array(device, fill=0.0, kind="il"):
     import zarr_hip
 
     shape, chunks, codecs = (128, 64, 64), (64, 64, 64), [LE, CRC]
-    if kind == "tileg":
+    if kind.startswith("tileg"):
         shape, chunks, codecs = (192, 80, 80), (96, 80, 80), [T((2, 1, 0)), LE, CRC]
     meta = O.ArrayMeta(shape, chunks, np.dtype("float32"), fill, codecs=codecs)
     host = {}
@@ -759,8 +759,9 @@ def _il_array(device, fill=0.0, kind="il"):
 
 
 # (kind, ZHIP_TUNE_ARM): k_decode_il's returning publication (production),
-# its deferred-verdict arm, and k_decode_tileg's deferred verdicts
-VERDICT_CASES = [("il", 0), ("il", 2), ("tileg", 0)]
+# its deferred-verdict arm, and the deferred verdicts of k_decode_tilegw
+# (production) and k_decode_tileg (arm 5)
+VERDICT_CASES = [("il", 0), ("il", 2), ("tilegw", 0), ("tileg", 5)]
 
 
 @pytest.fixture
@@ -922,6 +923,43 @@ def test_transpose_tile4w_and_tile4(device, dtype, endian, chunks, shape, arm):
         bad = bytearray(host[key])
         bad[len(bad) // 3] ^= 0x20
         host[key] = bytes(bad)
+        with pytest.raises(ValueError) as want:
+            O.read(host, meta)
+        arr = zarr_hip.Array.create(zarr_hip.DeviceStore.from_host(host, device), shape, chunks, dtype, 0,
+                                    codecs=codecs)
+        with pytest.raises(ValueError) as got:
+            arr[...]
+        assert str(got.value) == str(want.value)
+        assert N.lib().zhip_last_kernel() == kernel
+    finally:
+        N.lib().zhip_set_tuning(6, 0)
+
+
+@pytest.mark.parametrize("arm", [0, 5])
+@pytest.mark.parametrize("order", [(2, 1, 0), (1, 2, 0), (0, 2, 1)])
+@pytest.mark.parametrize("dtype,endian", [("float32", LE), ("int16", BE), ("float64", LE), ("uint8", LE)])
+def test_transpose_tilegw_and_tileg(device, order, dtype, endian, arm):
+    """k_decode_tilegw (production for grouped CRC layouts: k_decode_tileg
+    with a wave per tile and one A_(4 sq) chain per lane; partial tiles load
+    zeros) and k_decode_tileg (ZHIP_TUNE_ARM = 5) decode exactly what the
+    oracle wrote, fill missing chunks and report a corrupted chunk with the
+    reference's message."""
+    import zarr_hip
+    from zarr_hip import _native as N
+
+    codecs = [T(order), endian, CRC]
+    kernel = b"k_decode_tileg" if arm else b"k_decode_tilegw"
+    N.lib().zhip_set_tuning(6, arm)
+    try:
+        _roundtrip(device, (96, 160, 160), (96, 80, 80), dtype, codecs, fill=3, drop=["c/0/1/0"])
+        assert N.lib().zhip_last_kernel() == kernel
+        shape, chunks = (96, 80, 160), (96, 80, 80)
+        meta = O.ArrayMeta(shape, chunks, np.dtype(dtype), 0, codecs=codecs)
+        host = {}
+        O.write(host, meta, (Ellipsis,), _data(shape, dtype))
+        bad = bytearray(host["c/0/0/1"])
+        bad[len(bad) // 2 + 5] ^= 0x40
+        host["c/0/0/1"] = bytes(bad)
         with pytest.raises(ValueError) as want:
             O.read(host, meta)
         arr = zarr_hip.Array.create(zarr_hip.DeviceStore.from_host(host, device), shape, chunks, dtype, 0,

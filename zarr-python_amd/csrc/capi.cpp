@@ -438,7 +438,10 @@ int zhip_plan_upload(zhip_plan* p) {
         // l/16 + 4 m (m < 16) at column block l % 16: one chain of stride 4 sq
         const bool t4w = t4 && (L.flags & ZHIP_LF_CRC);
         const size_t n_t4w = t4w ? kPairTabWords + (size_t)(T / 4) * kThreads : 0;
-        std::vector<uint32_t> ht(n_base + n_t4 + n_g + n_t4f + n_t4w);
+        // k_decode_tilegw: the same chains for the four tiles of a group
+        const bool tgw = p->gd >= 0 && (L.flags & ZHIP_LF_CRC);
+        const size_t n_tgw = tgw ? kPairTabWords + (size_t)p->n_groups * kThreads : 0;
+        std::vector<uint32_t> ht(n_base + n_t4 + n_g + n_t4f + n_t4w + n_tgw);
         build_horner_stride(ht.data(), 16ull * sq);
         for (int t = 0; t < kThreads; ++t) {
             const uint64_t rel = (uint64_t)(kTileRows + t / 16) * sq + 16u * (t % 16);
@@ -550,6 +553,26 @@ int zhip_plan_upload(zhip_plan* p) {
                     const int64_t e = (int64_t)p->E - p0 + kWgStride - 16 * (int64_t)D;
                     const uint32_t xe = e >= 0 ? xpow8((uint64_t)e) : xpow8_inv((uint64_t)(-e));
                     f[kPairTabWords + (size_t)g4 * kThreads + t] = gf_mul(gf_mul(xe, p->c_inv), c96);
+                }
+        }
+        p->tilegw = tgw ? 1u : 0u;
+        p->tilegw_off = n_base + n_t4 + n_g + n_t4f + n_t4w;
+        if (tgw) {
+            // as k_decode_tile4w, tile w of group g at gm[g].tbase + w step(gd)
+            uint32_t* f = &ht[p->tilegw_off];
+            const uint64_t D = 4ull * sq;
+            build_pair_tables(f, D);
+            const uint32_t c96 = xpow8_inv(12);
+            const GroupEnt* gm = reinterpret_cast<const GroupEnt*>(&ht[p->g_off_map]);
+            const int64_t gstep = (int64_t)p->sstride[p->gd];
+            for (uint32_t g = 0; g < p->n_groups; ++g)
+                for (int t = 0; t < kThreads; ++t) {
+                    const int w = t / 64, l = t % 64;
+                    const int64_t p0 = (int64_t)gm[g].tbase + w * gstep + (int64_t)(l / 16) * (int64_t)sq +
+                                       16 * (l % 16);
+                    const int64_t e = (int64_t)p->E - p0 + kWgStride - 16 * (int64_t)D;
+                    const uint32_t xe = e >= 0 ? xpow8((uint64_t)e) : xpow8_inv((uint64_t)(-e));
+                    f[kPairTabWords + (size_t)g * kThreads + t] = gf_mul(gf_mul(xe, p->c_inv), c96);
                 }
         }
         if (p->d_tile_tables) (void)hipFree(p->d_tile_tables);
@@ -832,6 +855,10 @@ int zhip_decode_mapped(const zhip_plan* plan, const void* src, uint64_t src_size
             p.n_sub = plan->n_sub;
             p.g_step_t = plan->sstride[plan->gd];
             p.g_step_o = L.out_stride[plan->gd];
+            if (plan->tilegw && g_tune_arm != 2 && g_tune_arm != 5) {  // a wave per tile, one chain per lane
+                p.t4w_tab = plan->d_tile_tables + plan->tilegw_off;
+                p.t4w_kq = p.t4w_tab + kPairTabWords;
+            }
         }
         const uint64_t tunits = (uint64_t)n_chunks * plan->t_per_chunk;
         if (tunits >= (1ull << 32)) return set_err(ZHIP_E_UNSUPPORTED, "too many tiles in one batch");

@@ -501,6 +501,7 @@ KernelFn select_xw_kernel(bool crc, int item, bool swap);            // decode_r
 KernelFn select_tile4_kernel(bool crc, int item, bool swap);         // decode_tile.hip
 KernelFn select_tile4f_kernel(int item, bool swap);                  // decode_tile.hip
 KernelFn select_tile4w_kernel(int item, bool swap);                  // decode_tile.hip
+KernelFn select_tilegw_kernel(int item, bool swap);                  // decode_tile.hip
 KernelFn select_tileg_kernel(bool crc, int item, bool swap);         // decode_tile.hip
 
 // name of the kernel the last launch_decode chose (zhip_last_kernel: bench
@@ -643,11 +644,15 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
     }
     if (p.tq >= 0 && p.tileg) {
         // tiles grouped by four along a stored dim (k_decode_tileg, decode_tile.hip)
-        KernelFn fn = select_tileg_kernel((p.lflags & ZHIP_LF_CRC) != 0, p.g.itemsize, (p.lflags & ZHIP_LF_SWAP) != 0);
+        // (k_decode_tilegw when the plan's wave-per-tile chains are selected)
+        const bool gw = p.t4w_tab != nullptr && (p.lflags & ZHIP_LF_CRC) != 0;
+        KernelFn fn = gw ? select_tilegw_kernel(p.g.itemsize, (p.lflags & ZHIP_LF_SWAP) != 0)
+                         : select_tileg_kernel((p.lflags & ZHIP_LF_CRC) != 0, p.g.itemsize,
+                                               (p.lflags & ZHIP_LF_SWAP) != 0);
         if (!fn) return ZHIP_E_UNSUPPORTED;
         if (p.n_chunks == 0) return ZHIP_OK;
         if ((uint64_t)p.n_chunks * p.n_groups >= (1ull << 31)) return ZHIP_E_UNSUPPORTED;
-        g_last_kernel = "k_decode_tileg";
+        g_last_kernel = gw ? "k_decode_tilegw" : "k_decode_tileg";
         hipLaunchKernelGGL(fn, dim3(p.n_chunks * p.n_groups), dim3(kThreads), 0, stream, p);
         return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
     }

@@ -812,6 +812,130 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     }
 }
 
+// k_decode_tilegw: k_decode_tileg with k_decode_tile4w's chains: wave w owns
+// tile w of its group (lane l: rows l/16 + 4 m, column block l % 16; rows
+// and columns past a partial tile load zeros, which the chain steps over like
+// absent bytes), one A_(4 sq) chain per lane, the group's and lane's frame in
+// the host-built lane constant; the publication of k_decode_tileg (deferred
+// verdicts).  Production for grouped CRC layouts since round 4: C3 in 128^3
+// chunks 28.7-28.9 vs 30.2-30.3 us graph-timed (profiles/r04/l/); arms 2 / 5
+// take k_decode_tileg.  (Taking the previous tile's Horner steps before the
+// barrier, while one wave writes the image, measured the same in
+// k_decode_tile4w.)
+template <int ITEM, bool SWAP>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_decode_tilegw(
+    const DecodeParams p) {
+    constexpr int kPer = 16 / ITEM;
+    constexpr int kPiecesPerCol = kTileRows / kPer;
+    constexpr int KB = kTileRows / 4;  // blocks per lane
+    __shared__ __attribute__((aligned(16))) uint32_t s_mem[kPairTabWords + kTileRows * 64];
+    uint32_t* const s_tab = s_mem;
+    uint8_t* const s_tile = reinterpret_cast<uint8_t*>(s_mem + kPairTabWords);
+    uint32_t* const s_red = s_mem + kPairTabWords;  // after the last out-order pass
+    const int t = threadIdx.x;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane((uint32_t)t >> 6);
+    const uint32_t ln = (uint32_t)t & 63u, rg = ln >> 4, cl = 16u * (ln & 15u);
+    const uint32_t gpc = p.n_groups;
+    const uint32_t c = blockIdx.x / gpc;
+    const uint32_t grp = blockIdx.x - c * gpc;
+    const uint32_t expected = p.g.nbytes + 4u;
+    const uint4* gt = reinterpret_cast<const uint4*>(p.t4w_tab);
+    const uint4 tv0 = gt[t], tv1 = gt[t + kThreads], tv2 = gt[t + 2 * kThreads], tv3 = gt[t + 3 * kThreads],
+                tv4 = gt[t + 4 * kThreads], tv5 = gt[t + 5 * kThreads];
+    const uint32_t kq = p.t4w_kq[(size_t)grp * kThreads + t];
+    const uint64_t dvprev = dv_prev(p, c, grp == 0, g_tile_zero);
+    const Unit U = resolve_unit(p, c * p.nseg, expected);
+    const GroupEnt ge = load_uniform<GroupEnt>(p.gmap + grp);
+    const bool ok = U.mode == ZHIP_ST_OK;
+    const uint32_t sq = p.sstride[p.tq];
+    const int32_t rows = ge.rows, cols = ge.cols;
+    const uint8_t* zero = reinterpret_cast<const uint8_t*>(g_tile_zero);
+    const bool lane_in = (int32_t)cl < cols;
+    const uint8_t* const tb = U.cp + ge.tbase + (size_t)wv * p.g_step_t;
+    uint4 blk[KB];
+#pragma unroll
+    for (int m = 0; m < KB; ++m) {
+        const uint32_t row = rg + 4u * (uint32_t)m;
+        blk[m] = load_stream16_a1(ok && lane_in && (int32_t)row < rows ? tb + row * sq + cl : zero);
+    }
+    uint32_t stored = 0;
+    if (ok) stored = load_trailer_uniform(U.cp, p.g.nbytes);
+    {
+        uint4* st = reinterpret_cast<uint4*>(s_tab);
+        st[t] = tv0;
+        st[t + kThreads] = tv1;
+        st[t + 2 * kThreads] = tv2;
+        st[t + 3 * kThreads] = tv3;
+        st[t + 4 * kThreads] = tv4;
+        st[t + 5 * kThreads] = tv5;
+    }
+    const bool writes = ok || U.mode == ZHIP_ST_MISSING;
+    const uint4 f = make_uint4(p.fill[0], p.fill[1], p.fill[2], p.fill[3]);
+    const int32_t last = p.g.ndim - 1;
+    const int64_t oq = p.g.ostride[p.tq];
+    const int64_t ocol = p.g.ostride[last];
+    uint8_t* const obase = p.out + U.out_off + ge.orel;
+    uint8_t* const sink = reinterpret_cast<uint8_t*>(g_tile_sink) + 16 * t;
+    Acc4 acc = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int j = 0; j < kTiles; ++j) {
+        if (j > 0) __syncthreads();
+        if (wv == (uint32_t)j) {
+#pragma unroll
+            for (int m = 0; m < KB; ++m)
+                tile_put16<ITEM>(s_tile, rg + 4u * (uint32_t)m, cl, swap_block<ITEM, SWAP>(blk[m]));
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kPasses; ++k) {
+            const uint32_t pc = (uint32_t)(k * kThreads + t);
+            const uint32_t jc = pc / kPiecesPerCol;
+            const uint32_t r0 = (pc % kPiecesPerCol) * kPer;
+            uint32_t w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int e = 0; e < kPer; ++e) {
+                const uint8_t* src = s_tile + tile_byte<ITEM>(r0 + e, jc * ITEM);
+                if constexpr (ITEM == 8) {
+                    const uint2 v = *reinterpret_cast<const uint2*>(src);
+                    w[2 * e] = v.x;
+                    w[2 * e + 1] = v.y;
+                } else if constexpr (ITEM == 4) {
+                    w[e] = *reinterpret_cast<const uint32_t*>(src);
+                } else if constexpr (ITEM == 2) {
+                    w[e / 2] |= (uint32_t)(*reinterpret_cast<const uint16_t*>(src)) << (16 * (e & 1));
+                } else {
+                    w[e / 4] |= (uint32_t)(*src) << (8 * (e & 3));
+                }
+            }
+            const bool in = writes && (int32_t)(jc * ITEM) < cols && (int32_t)r0 < rows;
+            uint8_t* dst = in ? obase + (int64_t)j * p.g_step_o + (int64_t)jc * ocol + (int64_t)r0 * oq : sink;
+            store_nt16(dst, ok ? make_uint4(w[0], w[1], w[2], w[3]) : f);
+        }
+        if (ok) {
+#pragma unroll
+            for (int m = 4 * j; m < 4 * j + 4; ++m) crc_block4(s_tab, acc, blk[m]);
+        }
+    }
+    if (ok) {
+        const uint32_t v = wave_xor(lanemul_reg(kq, fold4(s_tab, acc)));
+        __syncthreads();  // every out-order read of the last tile is done: s_red reuses the image
+        if ((t & 63) == 0) s_red[t >> 6] = v;
+        __syncthreads();
+        if (t == 0) dv_publish(p, c, grp == 0, s_red[0] ^ s_red[1] ^ s_red[2] ^ s_red[3], stored);
+    }
+    if (grp == 0 && t == 0) {
+        if (ok) {
+            zhip_status st = {ZHIP_ST_OK, 0u, 0u, 0u};
+            p.status[c] = st;
+        } else {
+            zhip_status st = {U.mode, 0u, 0u, 0u};
+            p.status[c] = st;
+            if (U.mode != ZHIP_ST_MISSING) atomicOr(p.errflag, 1u << U.mode);
+        }
+        dv_settle(p, c, dvprev);
+    }
+}
+
 // k_encode_tile4: the same four tiles per workgroup in reverse (TransposeCodec
 // _encode_sync, transpose.py:113-118): 16-byte pieces of the source array's
 // out-contiguous rows are gathered (all 16 per thread issued first), written
@@ -1401,6 +1525,16 @@ KernelFn select_tileg_kernel(bool crc, int item, bool swap) {
                            : (swap ? k_decode_tileg<false, 4, true> : k_decode_tileg<false, 4, false>);
         case 8: return crc ? (swap ? k_decode_tileg<true, 8, true> : k_decode_tileg<true, 8, false>)
                            : (swap ? k_decode_tileg<false, 8, true> : k_decode_tileg<false, 8, false>);
+        default: return nullptr;
+    }
+}
+
+KernelFn select_tilegw_kernel(int item, bool swap) {  // CRC chains only
+    switch (item) {
+        case 1: return k_decode_tilegw<1, false>;
+        case 2: return swap ? k_decode_tilegw<2, true> : k_decode_tilegw<2, false>;
+        case 4: return swap ? k_decode_tilegw<4, true> : k_decode_tilegw<4, false>;
+        case 8: return swap ? k_decode_tilegw<8, true> : k_decode_tilegw<8, false>;
         default: return nullptr;
     }
 }

@@ -113,7 +113,8 @@ struct DecodeParams {
     // k_decode_tile4f (non-null: the layout qualifies): A_64 pair tables, lane constants
     const uint32_t* t4f_tab;
     const uint32_t* t4f_kq;
-    // k_decode_tile4w (non-null: taken): A_(4 sq) pair tables, lane constants
+    // k_decode_tile4w / k_decode_tilegw (non-null: taken): A_(4 sq) pair
+    // tables, lane constants [T/4 or n_groups][kThreads]
     const uint32_t* t4w_tab;
     const uint32_t* t4w_kq;
     // k_decode_tileg (tileg != 0): group map, step multiply table, steps
@@ -354,6 +355,9 @@ struct zhip_plan {
     // kPairTab* layout | lane constants [T/4][kThreads], at tile4w_off
     uint32_t tile4w;
     uint64_t tile4w_off;
+    // k_decode_tilegw (grouped tile layouts with a CRC): the same for groups
+    uint32_t tilegw;
+    uint64_t tilegw_off;
     // k_encode_tileg (full selections): tiles grouped by four along the
     // innermost other stored dim gd with shape[gd] % 4 == 0 (uniform step
     // sstride[gd] inside every group, whatever the natural tile order); tables
