@@ -893,6 +893,9 @@ int zhip_encode_mapped(const zhip_plan* plan, const void* arr, void* dst, const 
     const uint64_t units = (uint64_t)n_chunks * plan->nseg;
     if (units >= (1ull << 32)) return set_err(ZHIP_E_UNSUPPORTED, "too many units in one batch");
     EncodeParams p{};
+    // chunks' publication words a 128-byte line apart (zhip_plan_info's >= kPubLine
+    // workspace words for CRC layouts); arm ZHIP_TUNE_ARM = 9: 16 bytes apart
+    p.pub_stride = ((plan->layout.flags & ZHIP_LF_CRC) && g_tune_arm != 9) ? kPubLine / 2u : 2u;
     p.arr = static_cast<const uint8_t*>(arr);
     p.dst = static_cast<uint8_t*>(dst);
     p.chunks = d_chunks;

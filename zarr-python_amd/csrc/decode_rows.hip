@@ -1383,7 +1383,7 @@ KernelFn select_il_kernel_arm(bool crc, int item, bool swap, int arm) {  // ZHIP
     switch (arm) {
         case 1: return k_decode_il<true, 4, false, false, false, 0, false, 0>;  // round 3: words 16 B apart
         case 2: return k_decode_il<true, 4, false, false, false, 0, false, 2>;  // deferred verdicts
-        default: return nullptr;
+        default: return k_decode_il<true, 4, false>;  // arms of other kernels: production
     }
 }
 

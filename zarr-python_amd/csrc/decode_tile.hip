@@ -1054,7 +1054,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     const bool ne = (s_ne[0] | s_ne[1] | s_ne[2] | s_ne[3]) != 0u;
     const uint64_t pb = 1ull << grp;
     const uint64_t full = (1ull << gpc) - 1ull;
-    uint64_t* w = reinterpret_cast<uint64_t*>(p.ws) + 2ull * c;
+    uint64_t* w = reinterpret_cast<uint64_t*>(p.ws) + (uint64_t)p.pub_stride * c;
     const uint64_t prev = __hip_atomic_fetch_xor(w, (pb << 32) | (ne ? pb << 48 : 0ull) | V, __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_AGENT);
     if ((((prev >> 32) & 0xFFFFull) ^ pb) != full) return;

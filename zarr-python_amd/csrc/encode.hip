@@ -318,7 +318,7 @@ __device__ __forceinline__ void enc_run_end(const EncodeParams& p, const zhip_ch
         uint32_t raw = 0, last = 0;
         if (p.nseg <= 32) {
             const uint64_t full = p.nseg >= 32 ? 0xFFFFFFFFull : ((1ull << p.nseg) - 1ull);
-            uint64_t* w = reinterpret_cast<uint64_t*>(p.ws) + 2ull * c;
+            uint64_t* w = reinterpret_cast<uint64_t*>(p.ws) + (uint64_t)p.pub_stride * c;
             const uint64_t prev =
                 __hip_atomic_fetch_xor(w, ((uint64_t)bits << 32) | V, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (((prev >> 32) ^ bits) == full) {
@@ -364,7 +364,7 @@ __device__ __forceinline__ void enc_run_end_pair(const EncodeParams& p, const zh
     const bool ne = (s_ne[0] | s_ne[1] | s_ne[2] | s_ne[3]) != 0u;
     const uint64_t pb = 1ull << pr;
     const uint64_t full = (1ull << (p.nseg >> 1)) - 1ull;
-    uint64_t* w = reinterpret_cast<uint64_t*>(p.ws) + 2ull * c;
+    uint64_t* w = reinterpret_cast<uint64_t*>(p.ws) + (uint64_t)p.pub_stride * c;
     const uint64_t word = (pb << 32) | (ne ? pb << 48 : 0ull) | V;
     const uint64_t prev = __hip_atomic_fetch_xor(w, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if ((((prev >> 32) & 0xFFFFull) ^ pb) != full) return;

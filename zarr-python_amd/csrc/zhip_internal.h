@@ -289,6 +289,9 @@ struct EncodeParams {
     uint32_t n_groups, g_step_t, n_sub;
     int64_t g_step_o;
     uint32_t xcd_run;     // k_encode_pair: pairs per XCD-contiguous run (0: dispatch order)
+    // 64-bit words between chunks' publication words (k_encode_pair / k_encode_tile4):
+    // kPubLine / 2 for CRC layouts (a 128-byte line per chunk), else 2
+    uint32_t pub_stride;
 };
 
 struct PackParams {
