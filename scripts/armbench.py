@@ -6,7 +6,8 @@ zhip_set_tuning(ARM)); each arm is a hipGraph of REPS launches rotating over
 4 replicas (the Infinity Cache cannot serve re-reads), replayed ROUNDS times,
 interleaved with the other arms in ONE process.  CONFIG = headline | c4 |
 share8 (rank 0's 1-shard share of the headline at N = 8) | share4 | c3 | c3g
-(transpose (2,1,0) in 64^3 / 128^3 chunks).  Also
+(transpose (2,1,0) in 64^3 / 128^3 chunks) | cpp (the reference's
+codec_pipeline_performance array, zarr's default sharding codecs).  Also
 the no-CRC twin (zarr's default sharding codecs, k_decode_lead) for the
 headline.  One JSON line per arm: min / median us per launch and the HBM
 fraction of the algorithmic bytes.  After timing, the production arm's
@@ -33,9 +34,11 @@ def main():
 
     dev = torch.device("cuda:0")
     cfg = os.environ.get("CONFIG", "headline")
-    g = W.C4 if cfg == "c4" else W.HEADLINE
+    g = W.C4 if cfg == "c4" else W.CPP_EXAMPLE if cfg == "cpp" else W.HEADLINE
     shape, shards, inner = g["shape"], g["shards"], g["inner"]
-    if cfg == "c4":
+    if cfg == "cpp":  # the reference's example: int32, zarr's default sharding codecs (k_decode_lead)
+        data = torch.from_numpy(W.cpp_example_data("plain")).to(dev)
+    elif cfg == "c4":
         gen = torch.Generator(device=dev).manual_seed(0)
         data = torch.randn(shape, generator=gen, device=dev, dtype=torch.float32)
     else:
@@ -51,12 +54,21 @@ def main():
         shards = None
     R = 2 if cfg == "c4" else 4
     reps = int(os.environ.get("REPS", "4" if cfg == "c4" else "20"))
-    crc = [bench.build_replica(dev, data, shape, inner, aa + [W.LE, W.CRC], shards=shards).prepare_read((Ellipsis,))
-           for _ in range(R)]
-    nocrc = [bench.build_replica(dev, data, shape, inner, aa + [W.LE], shards=shards).prepare_read((Ellipsis,))
-             for _ in range(R)] if cfg != "c4" else []
+    if cfg == "cpp":
+        crc = [bench.build_replica(dev, data, shape, inner, [W.LE], shards=shards, dtype="int32", fill=0)
+               .prepare_read((Ellipsis,)) for _ in range(R)]
+        nocrc = []
+    else:
+        crc = [bench.build_replica(dev, data, shape, inner, aa + [W.LE, W.CRC], shards=shards)
+               .prepare_read((Ellipsis,)) for _ in range(R)]
+        nocrc = [bench.build_replica(dev, data, shape, inner, aa + [W.LE], shards=shards).prepare_read((Ellipsis,))
+                 for _ in range(R)] if cfg != "c4" else []
     n_inner = int(np.prod([s // i for s, i in zip(shape, inner)]))
-    if shards is not None:
+    if cfg == "cpp":  # inner chunks without a trailer, one index CRC per shard
+        n_shards = int(np.prod([s // i for s, i in zip(shape, shards)]))
+        cps = n_inner // n_shards
+        alg = n_inner * int(np.prod(inner)) * 4 + n_shards * (cps * 16 + 4) + data.numel() * 4
+    elif shards is not None:
         n_shards = int(np.prod([s // i for s, i in zip(shape, shards)]))
         cps = n_inner // n_shards
         alg = n_inner * (int(np.prod(inner)) * 4 + 4) + n_shards * (cps * 16 + 4) + data.numel() * 4
