@@ -82,6 +82,8 @@ def test_cpp_example_device_resident_kernel(oracle_stores, device):
     prog, out = arr.prepare_read((Ellipsis,), out=out)
     prog.launch()
     prog.results()
+    from zarr_hip import _native as N
+    assert N.lib().zhip_last_kernel() == b"k_decode_lead4", "16 KiB inner chunks: four per workgroup"
     assert prog.index is None and prog.data.n_idx == 16, "index checks fused into the data launch"
     assert out.cpu().numpy().tobytes() == data.tobytes()
     bad = dict(host)

@@ -491,6 +491,14 @@ DEFAULT_SHARD_CASES = [
     ((64, 128, 64), (32, 64, 64), (16, 64, 64), "int16", (Ellipsis,), BE),
     ((32, 64, 128), (16, 64, 128), (8, 32, 128), "float64", (slice(1, 31), slice(None), slice(None)), LE),
     ((64, 512, 64), (32, 256, 64), (16, 256, 64), "uint8", (Ellipsis,), {"name": "bytes"}),
+    # inner chunks of <= 16 KiB: four per workgroup (k_decode_lead4) -- the
+    # reference example's 64 x 64 int32, one live step (4 KiB), a 12 KiB chunk
+    # (an empty head step), a partial last quad (6 chunks), 8-byte items
+    ((256, 256), (128, 128), (64, 64), "int32", (Ellipsis,), LE),
+    ((96, 256), (48, 128), (16, 64), "float32", (slice(5, 90), slice(64, 256)), BE),
+    ((12, 32, 64), (6, 32, 64), (3, 16, 64), "float32", (slice(1, 11), slice(2, 30), slice(None)), LE),
+    ((96, 128), (32, 128), (16, 128), "int16", (Ellipsis,), BE),
+    ((16, 64, 32), (8, 32, 32), (4, 16, 32), "float64", (slice(1, 15), slice(2, 60), slice(None)), BE),
 ]
 
 
@@ -514,9 +522,18 @@ def test_default_sharding_chain_fused(device, shape, shards, inner, dtype, sel, 
     assert 0 < prog.data.n_idx <= n_shards
     got = arr[sel]
     from zarr_hip import _native as N
-    assert N.lib().zhip_last_kernel() == b"k_decode_lead"
+    small = int(np.prod(inner)) * np.dtype(dtype).itemsize <= 16384
+    assert N.lib().zhip_last_kernel() == (b"k_decode_lead4" if small else b"k_decode_lead")
     want = O.read(host, meta, sel)
     assert got.tobytes() == np.ascontiguousarray(want).tobytes()
+    if small:  # ZHIP_TUNE_ARM 11: the pair kernel for the same layout, same bytes
+        N.lib().zhip_set_tuning(6, 11)
+        try:
+            got2 = arr[sel]
+            assert N.lib().zhip_last_kernel() == b"k_decode_lead"
+        finally:
+            N.lib().zhip_set_tuning(6, 0)
+        assert got2.tobytes() == got.tobytes()
 
 
 @pytest.mark.parametrize("loc", ["end", "start"])

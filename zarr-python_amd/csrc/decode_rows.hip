@@ -947,6 +947,94 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     if (has_b) unit_status_pair(p, ub, false, t);
 }
 
+// k_decode_lead4: k_decode_lead for chunks of at most 16 KiB (one unit per
+// chunk; the reference's example array has 64 x 64 float32 inner chunks).  Such
+// a unit's first four 4 KiB steps lie before the chunk start (seg_lo =
+// E - 32 KiB <= -16 KiB), so the pair kernel spends half its loads on the zero
+// line and half its stores on the sink.  Here a workgroup decodes four chunks
+// with only the last four steps of each: 16 loads and 16 stores per lane, all
+// live except the whole empty head steps of a chunk under 16 KiB.  The row map
+// is zhip_rows_map's, unchanged (entries 4..7 of each unit); no XCD remap (four
+// consecutive chunks per workgroup already keep a shard's chunks together).
+template <int ITEM, bool SWAP>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_decode_lead4(const DecodeParams p) {
+    constexpr int NQ = 4, KS = kDefaultBlocks / 2, K0 = kDefaultBlocks - KS;
+    __shared__ uint32_t s_tab[kPairTabWords];
+    __shared__ uint32_t s_red[kThreads / 64];
+    const int t = threadIdx.x;
+    PairHot h = p.h;
+    pair_hot(h);
+    uint32_t bx = blockIdx.x;
+    const uint32_t lead = (h.n_idx + 7u) & ~7u;
+    if (bx < lead) {
+        if (bx < h.n_idx) index_lead(p, bx, t, s_tab, s_red);
+        return;
+    }
+    const uint32_t q0 = (uint32_t)NQ * (bx - lead);  // nseg == 1: unit = chunk
+    if (q0 >= h.n_units) return;
+    const uint32_t expected = p.g.nbytes;
+    const uint8_t* zero = reinterpret_cast<const uint8_t*>(g_rows_zero);
+    auto load_tail = [&](const Unit& u, bool live, uint4 (&b)[KS]) {
+        const bool ok = live && u.mode == ZHIP_ST_OK;
+#pragma unroll
+        for (int k = 0; k < KS; ++k) {
+            const int32_t base = u.seg_lo + kWgStride * (K0 + k);
+            b[k] = load_stream16_any(ok && base >= 0 ? u.cp + base + 16 * t : zero);
+        }
+    };
+    bool live[NQ];
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) live[i] = q0 + (uint32_t)i < h.n_units;
+    Unit U[NQ];
+    uint4 blk[NQ][KS];
+    if (h.pred) {
+        Unit gs[NQ];
+#pragma unroll
+        for (int i = 0; i < NQ; ++i) {
+            gs[i] = predict_unit_h(h, live[i] ? q0 + i : q0);
+            load_tail(gs[i], live[i], blk[i]);
+        }
+        bool bad = false;
+#pragma unroll
+        for (int i = 0; i < NQ; ++i) {
+            U[i] = live[i] ? resolve_unit(p, q0 + i, expected) : U[0];
+            const bool b = live[i] && U[i].mode == ZHIP_ST_OK && U[i].cp != gs[i].cp;
+            if (b) load_tail(U[i], true, blk[i]);
+            bad = bad || b;
+        }
+        if (bad) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): later waits stay exact
+    } else {
+#pragma unroll
+        for (int i = 0; i < NQ; ++i) U[i] = live[i] ? resolve_unit(p, q0 + i, expected) : U[0];
+#pragma unroll
+        for (int i = 0; i < NQ; ++i) load_tail(U[i], live[i], blk[i]);
+    }
+    RowSteps m[NQ];
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) m[i] = load_row_steps(p, U[i]);
+    uint8_t* sink = reinterpret_cast<uint8_t*>(g_rows_sink);
+    const uint32_t lane_row = (16u * (uint32_t)t) >> p.row_shift;
+    const uint32_t lane_col = (16u * (uint32_t)t) & ((1u << p.row_shift) - 1u);
+    const int64_t lane_off = (int64_t)lane_row * p.r_oy + (int64_t)lane_col;
+    const uint4 f = make_uint4(p.fill[0], p.fill[1], p.fill[2], p.fill[3]);
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) {
+        const bool present = live[i] && U[i].mode == ZHIP_ST_OK;
+        const bool writes = live[i] && (U[i].mode == ZHIP_ST_OK || U[i].mode == ZHIP_ST_MISSING);
+        uint8_t* const base = p.out + U[i].out_off;
+#pragma unroll
+        for (int k = 0; k < KS; ++k) {
+            const zhip_rowblk& e = m[i].e[K0 + k];
+            const uint32_t lo = e.lo, hi = e.hi;
+            const bool wr = writes && lane_row - lo < hi - lo;  // unsigned: lo <= lane_row < hi
+            store_nt16(wr ? base + e.rel + lane_off : sink, present ? swap_block<ITEM, SWAP>(blk[i][k]) : f);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < NQ; ++i)
+        if (live[i]) unit_status_pair(p, U[i], false, t);
+}
+
 int debug_stamps(uint64_t* host_out, uint32_t n_wg) {
     if (n_wg > kStampWG) n_wg = kStampWG;
     return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_stamps), (size_t)n_wg * kStampSlots * sizeof(uint64_t), 0,
@@ -977,6 +1065,16 @@ KernelFn select_pair_kernel(bool crc, int item, bool swap, int nu) {
             case 2: return swap ? k_decode_lead<2, true> : k_decode_lead<2, false>;
             case 4: return swap ? k_decode_lead<4, true> : k_decode_lead<4, false>;
             case 8: return swap ? k_decode_lead<8, true> : k_decode_lead<8, false>;
+            default: return nullptr;
+        }
+    }
+    if (nu == 10) {  // no data CRC, chunks of <= 16 KiB: four per workgroup (k_decode_lead4)
+        if (crc) return nullptr;
+        switch (item) {
+            case 1: return k_decode_lead4<1, false>;
+            case 2: return swap ? k_decode_lead4<2, true> : k_decode_lead4<2, false>;
+            case 4: return swap ? k_decode_lead4<4, true> : k_decode_lead4<4, false>;
+            case 8: return swap ? k_decode_lead4<8, true> : k_decode_lead4<8, false>;
             default: return nullptr;
         }
     }
