@@ -2,7 +2,7 @@
 """Encode-only timing for PMC / rocprof passes (measurement only): the C3
 transposed encode on 64^3 chunks (k_encode_tile4, or k_encode_tile with
 TUNE=65536), on 128^3 chunks (k_encode_tile) and the C2 encode
-(k_encode_pair), graph-timed as bench.py does, each config with an optional
+(k_encode_pair), 16 KiB chunks (k_encode_quad), graph-timed as bench.py does, each config with an optional
 ZHIP_TUNE_ARM; one JSON line per arm."""
 
 import json
@@ -28,7 +28,9 @@ def main():
     dev = torch.device("cuda:0")
     tr = [{"name": "transpose", "configuration": {"order": [2, 1, 0]}}]
     cfgs = {"c3_64": (tr, (64, 64, 64), "tile4"), "c3_128": (tr, (128, 128, 128), "tile"),
-            "c2": ([], (64, 64, 64), "rows")}
+            "c2": ([], (64, 64, 64), "rows"),
+            # 16 KiB chunks (the reference example's chunk size): k_encode_quad, arm 11 k_encode_pair
+            "q16": ([], (1, 64, 64), "rows")}
     # ARMS: comma list of config[:arm] (arm = zhip_set_tuning(ARM), e.g. c2:1)
     for item in os.environ.get("ARMS", "c3_64,c3_128").split(","):
         name, _, arm = item.partition(":")

@@ -186,6 +186,37 @@ def test_encode_pair_sharded_empty_inner(device):
          [((Ellipsis,), d), ((slice(0, 8),), 0.0), ((slice(2, 30, 3), slice(1, 63)), 5.0)])
 
 
+# ---- k_encode_quad: chunks of <= 16 KiB, four per workgroup (trailer, status
+#      and non-empty flag written by the workgroup that owns the chunk);
+#      ZHIP_TUNE_ARM 11 runs k_encode_pair on the same writes
+
+QUAD_CASES = [
+    ((256, 256), (64, 64), "int32", [LE, CRC], 0),                    # the reference example's inner chunk
+    ((48, 32, 64), (3, 16, 64), "float32", [LE, CRC], np.nan),        # 12 KiB: an empty head step
+    ((16, 64, 32), (4, 16, 32), "float64", [BE, CRC], 0.0),
+    ((96, 128), (16, 128), "int16", [BE], 0),                         # 4 KiB, 6 chunks: a partial quad
+    ((256, 256), (128, 128), "int32", [SHARD((64, 64), [LE])], 0),     # zarr's default sharding codecs
+]
+
+
+@pytest.mark.parametrize("arm", [0, 11])
+@pytest.mark.parametrize("shape,chunks,dtype,codecs,fill", QUAD_CASES)
+def test_encode_quad_small_chunks(device, arm, shape, chunks, dtype, codecs, fill):
+    from zarr_hip import _native as N
+
+    d = _data(shape, dtype)
+    d[tuple(slice(0, c) for c in chunks)] = fill   # first chunk all fill -> elided
+    sub = tuple(slice(1, s - 2) for s in shape[:-1]) + (slice(None),)
+    w = [((Ellipsis,), d),
+         (sub, _data(tuple(s - 3 for s in shape[:-1]) + (shape[-1],), dtype, 4)),   # merges with fill
+         (tuple(slice(c, 2 * c) for c in chunks), fill)]                          # a chunk back to fill
+    N.lib().zhip_set_tuning(6, arm)
+    try:
+        _run(device, shape, chunks, dtype, codecs, fill, w)
+    finally:
+        N.lib().zhip_set_tuning(6, 0)
+
+
 # ---- k_encode_tile4: transposed chunks with full 64-row x 256-byte tiles
 
 @pytest.mark.parametrize("dtype,endian,chunks,shape", [

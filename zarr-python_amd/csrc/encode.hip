@@ -482,7 +482,122 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
                          (same ? 1u << (sa & 31u) : 0u) | (1u << (sb & 31u)), same ? 2u : 1u, s_red[1], t);
 }
 
+// k_encode_quad: k_encode_pair for chunks of at most 16 KiB (one unit per
+// chunk; the reference example's 64 x 64 int32 inner chunks).  Such a unit's
+// first four steps lie before the chunk start, so the pair kernel gathers and
+// stores half its blocks for nothing; here a workgroup encodes four chunks with
+// only the last four steps of each.  The workgroup owns its chunks whole: CRC
+// and non-empty bit reduce in LDS and lanes 0..3 write trailer, status and flag
+// of one chunk each (no publication word, no zeroed flags).
+template <bool CRC, int ITEM, bool SWAP>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_encode_quad(const EncodeParams p) {
+    constexpr int NQ = 4, KS = kDefaultBlocks / 2, K0 = kDefaultBlocks - KS;
+    __shared__ uint32_t s_tab[CRC ? 16 * 256 : 1];
+    __shared__ uint32_t s_red[NQ][kThreads / 64];
+    __shared__ uint32_t s_ne[NQ][kThreads / 64];
+    const int t = threadIdx.x;
+    const uint32_t c0 = (uint32_t)NQ * blockIdx.x;  // nseg == 1: unit = chunk
+    uint4 tv0, tv1, tv2, tv3;
+    uint32_t kl = 0;
+    if constexpr (CRC) {
+        const uint4* gt = reinterpret_cast<const uint4*>(p.horner);
+        tv0 = gt[t];
+        tv1 = gt[t + kThreads];
+        tv2 = gt[t + 2 * kThreads];
+        tv3 = gt[t + 3 * kThreads];
+        kl = p.kpair[t];  // unit 0's lane constants
+    }
+    bool live[NQ];
+    zhip_chunk ch[NQ];
+    EncRowSteps m[NQ];
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) {
+        live[i] = c0 + (uint32_t)i < p.n_units;
+        ch[i] = load_uniform<zhip_chunk>(p.chunks + (live[i] ? c0 + i : c0));
+    }
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) m[i] = load_uniform<EncRowSteps>(p.rowmap + (size_t)ch[i].sel * kDefaultBlocks);
+    const uint32_t lane_row = (16u * (uint32_t)t) >> p.row_shift;
+    const uint32_t lane_col = (16u * (uint32_t)t) & ((1u << p.row_shift) - 1u);
+    const int64_t lane_off = (int64_t)lane_row * p.r_oy + (int64_t)lane_col;
+    const uint8_t* zero = reinterpret_cast<const uint8_t*>(g_enc_zero);
+    uint4 blk[NQ][KS];
+#pragma unroll
+    for (int i = 0; i < NQ; ++i)
+#pragma unroll
+        for (int k = 0; k < KS; ++k) {
+            const zhip_rowblk& e = m[i].e[K0 + k];
+            const bool in = live[i] && lane_row - e.lo < (uint32_t)(e.hi - e.lo);
+            blk[i][k] = enc_load16(in ? p.arr + ch[i].out_off + e.rel + lane_off : zero);
+        }
+    if constexpr (CRC) {
+        uint4* st = reinterpret_cast<uint4*>(s_tab);
+        st[t] = tv0;
+        st[t + kThreads] = tv1;
+        st[t + 2 * kThreads] = tv2;
+        st[t + 3 * kThreads] = tv3;
+        __syncthreads();
+    }
+    const uint4 f = make_uint4(p.fill[0], p.fill[1], p.fill[2], p.fill[3]);
+    const int32_t seg_lo = (int32_t)p.E - (int32_t)p.seg;
+    uint8_t* const sink = reinterpret_cast<uint8_t*>(g_enc_sink) + 16 * t;
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) {
+        uint8_t* const cp = p.dst + ch[i].src;
+        uint32_t acc = 0;
+        bool eq = true;
+#pragma unroll
+        for (int k = 0; k < KS; ++k) {
+            const zhip_rowblk& e = m[i].e[K0 + k];
+            const int32_t o = seg_lo + kWgStride * (K0 + k);
+            const bool in_sel = lane_row - e.lo < (uint32_t)(e.hi - e.lo);
+            const uint4 v = in_sel ? blk[i][k] : f;  // _merge_chunk_array: outside the selection = fill
+            eq = eq && block_eq_fill<ITEM>(v, 16u, p);
+            const uint4 w = swap_block<ITEM, SWAP>(v);
+            enc_store16(live[i] && o >= 0 ? cp + o + 16 * t : sink, w);
+            if constexpr (CRC)
+                if (o >= 0)
+                    acc = tab_apply(s_tab, acc ^ w.x) ^ tab_apply(s_tab + 1024, w.y) ^ tab_apply(s_tab + 2048, w.z) ^
+                          tab_apply(s_tab + 3072, w.w);
+        }
+        const uint32_t v = CRC ? wave_xor(gf_mul(acc, kl)) : 0u;
+        const bool ne = __any(!eq);
+        if ((t & 63) == 0) {
+            s_red[i][t >> 6] = v;
+            s_ne[i][t >> 6] = ne ? 1u : 0u;
+        }
+    }
+    __syncthreads();
+    if (t < NQ && c0 + (uint32_t)t < p.n_units) {  // lane i: chunk c0 + i
+        const uint32_t c = c0 + (uint32_t)t;
+        p.nonempty[c] = (s_ne[t][0] | s_ne[t][1] | s_ne[t][2] | s_ne[t][3]) != 0u ? 1u : 0u;
+        uint32_t crc = 0;
+        if constexpr (CRC) {
+            crc = ~((s_red[t][0] ^ s_red[t][1] ^ s_red[t][2] ^ s_red[t][3]) ^ p.c3);  // kpair carries c_inv
+            put_le_u32(p.dst + p.chunks[c].src + p.g.nbytes, crc);  // LE trailer (crc32c_.py:64-68)
+        }
+        zhip_status st = {ZHIP_ST_OK, crc, crc, 0u};
+        p.status[c] = st;
+    }
+}
+
 using EncodeFn = void (*)(const EncodeParams);
+
+template <bool CRC, int ITEM>
+static EncodeFn pick_encode_quad_item(bool swap) {
+    if constexpr (ITEM == 1) return k_encode_quad<CRC, 1, false>;
+    else return swap ? k_encode_quad<CRC, ITEM, true> : k_encode_quad<CRC, ITEM, false>;
+}
+
+static EncodeFn pick_encode_quad(bool crc, int item, bool swap) {
+    switch (item) {
+        case 1: return crc ? pick_encode_quad_item<true, 1>(swap) : pick_encode_quad_item<false, 1>(swap);
+        case 2: return crc ? pick_encode_quad_item<true, 2>(swap) : pick_encode_quad_item<false, 2>(swap);
+        case 4: return crc ? pick_encode_quad_item<true, 4>(swap) : pick_encode_quad_item<false, 4>(swap);
+        case 8: return crc ? pick_encode_quad_item<true, 8>(swap) : pick_encode_quad_item<false, 8>(swap);
+        default: return nullptr;
+    }
+}
 
 template <bool CRC, bool FAST>
 static EncodeFn pick_encode(int item, bool swap) {
@@ -540,6 +655,14 @@ int launch_encode(const EncodeParams& p, hipStream_t stream, int max_grid) {
         if ((uint64_t)p.n_chunks * gpc >= (1ull << 31) || gpc >= 65536u) return ZHIP_E_UNSUPPORTED;
         // (the last arrival of each chunk writes its non-empty flag)
         hipLaunchKernelGGL(fn, dim3((uint32_t)(p.n_chunks * gpc)), dim3(kThreads), 0, stream, p);
+        return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
+    }
+    if (p.rowmap && p.seg == (uint32_t)kWgStride * kDefaultBlocks && !(p.tune & kTunePersist) && p.nseg == 1u &&
+        p.E <= 4u * kWgStride && g_tune_arm != 11) {  // chunks of <= 16 KiB: four per workgroup (arm 11: pairs)
+        EncodeFn fn = pick_encode_quad(crc, p.g.itemsize, swap);
+        if (!fn) return ZHIP_E_UNSUPPORTED;
+        if (p.n_units == 0) return ZHIP_OK;
+        hipLaunchKernelGGL(fn, dim3((p.n_units + 3u) / 4u), dim3(kThreads), 0, stream, p);
         return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
     }
     if (p.rowmap && p.seg == (uint32_t)kWgStride * kDefaultBlocks && !(p.tune & kTunePersist)) {
