@@ -30,13 +30,17 @@ def main():
     cfgs = {"c3_64": (tr, (64, 64, 64), "tile4"), "c3_128": (tr, (128, 128, 128), "tile"),
             "c2": ([], (64, 64, 64), "rows"),
             # 16 KiB chunks (the reference example's chunk size): k_encode_quad, arm 11 k_encode_pair
-            "q16": ([], (1, 64, 64), "rows")}
-    # ARMS: comma list of config[:arm] (arm = zhip_set_tuning(ARM), e.g. c2:1)
+            "q16": ([], (1, 64, 64), "rows"), "q16n": ([], (1, 64, 64), "rows", False),
+            "c2n": ([], (64, 64, 64), "rows", False)}
+    # ARMS: comma list of config[:arm] (arm = zhip_set_tuning(ARM), e.g. c2:1);
+    # NOCHECK: the same items for ablation arms whose output is not a valid store
     for item in os.environ.get("ARMS", "c3_64,c3_128").split(","):
         name, _, arm = item.partition(":")
-        aa, chunks, want = cfgs[name]
+        aa, chunks, want, *crc = cfgs[name]  # q16n: no CRC codec
+        tail = [bench.LE, bench.CRC] if not crc or crc[0] else [bench.LE]
         N.lib().zhip_set_tuning(6, int(arm or 0))
-        src, wall, kern = bench._encode_bench(dev, args, aa + [bench.LE, bench.CRC], want, chunks=chunks)
+        src, wall, kern = bench._encode_bench(dev, args, aa + tail, want, chunks=chunks,
+                                              check=item not in os.environ.get("NOCHECK", "").split(","))
         N.lib().zhip_set_tuning(6, 0)
         print(json.dumps({"arm": item, "tune": tune, "us_graph": round(wall * 1e6, 2),
                           "us_eager": round(kern * 1e6, 2),

@@ -169,6 +169,7 @@ def test_encode_pair_elision_and_merges(device, codecs, fill):
     d = _data(shape, "float32")
     d[0:8, :, 0:64] = fill        # one chunk entirely fill -> elided
     d[16:24, :, 64:128] = fill    # another
+    d[24, 3, 70] = -0.0 if fill == 0.0 else d[24, 3, 70]   # bitwise != fill: that chunk is kept
     w = [((Ellipsis,), d),
          ((slice(8, 16), slice(None), slice(64, 128)), fill),             # a full chunk back to fill
          ((slice(3, 29), slice(5, 60), slice(10, 100)), _data((26, 55, 90), "float32", 3))]
