@@ -536,6 +536,41 @@ def test_default_sharding_chain_fused(device, shape, shards, inner, dtype, sel, 
         assert got2.tobytes() == got.tobytes()
 
 
+# unsharded chunks of <= 16 KiB without a CRC (zarr's default v3 codecs,
+# bytes only) take k_decode_lead4 too, with no leading workgroups
+PLAIN_SMALL_CASES = [
+    ((256, 256), (64, 64), "int32", (Ellipsis,), LE),
+    ((96, 256), (16, 64), "float32", (slice(5, 90), slice(64, 256)), BE),
+    ((12, 32, 64), (3, 16, 64), "float32", (slice(1, 11), slice(2, 30), slice(None)), LE),
+    ((96, 128), (16, 128), "int16", (Ellipsis,), BE),
+    ((16, 64, 32), (4, 16, 32), "float64", (slice(1, 15), slice(2, 60), slice(None)), LE),
+]
+
+
+@pytest.mark.parametrize("shape,chunks,dtype,sel,endian", PLAIN_SMALL_CASES)
+def test_plain_small_chunks_lead4(device, shape, chunks, dtype, sel, endian):
+    import zarr_hip
+    from zarr_hip import _native as N
+
+    codecs = [endian]
+    meta = O.ArrayMeta(shape, chunks, np.dtype(dtype), 0, codecs=codecs)
+    host = {}
+    O.write(host, meta, (Ellipsis,), _data(shape, dtype, seed=5))
+    del host[[k for k in sorted(host) if k.startswith("c/")][1]]  # a missing chunk: fill
+    store = zarr_hip.DeviceStore.from_host(host, device)
+    arr = zarr_hip.Array.create(store, shape, chunks, dtype, 0, codecs=codecs)
+    got = arr[sel]
+    assert N.lib().zhip_last_kernel() == b"k_decode_lead4"
+    assert got.tobytes() == np.ascontiguousarray(O.read(host, meta, sel)).tobytes()
+    N.lib().zhip_set_tuning(6, 11)  # the pair kernel on the same layout
+    try:
+        got2 = arr[sel]
+        assert N.lib().zhip_last_kernel() == b"k_decode_pair"
+    finally:
+        N.lib().zhip_set_tuning(6, 0)
+    assert got2.tobytes() == got.tobytes()
+
+
 @pytest.mark.parametrize("loc", ["end", "start"])
 def test_default_sharding_chain_index_crc_mismatch(device, loc):
     import zarr_hip
