@@ -8,7 +8,8 @@ interleaved with the other arms in ONE process.  CONFIG = headline | c4 |
 share8 (rank 0's 1-shard share of the headline at N = 8) | share4 | c3 | c3g
 (transpose (2,1,0) in 64^3 / 128^3 chunks) | cpp (the reference's
 codec_pipeline_performance array, zarr's default sharding codecs) | cppu (the
-same array unsharded, bytes only: 64^2 chunks of 16 KiB).  Also
+same array unsharded, bytes only: 64^2 chunks of 16 KiB) | cppuc (the same
+with crc32c).  Also
 the no-CRC twin (zarr's default sharding codecs, k_decode_lead) for the
 headline.  One JSON line per arm: min / median us per launch and the HBM
 fraction of the algorithmic bytes.  After timing, the production arm's
@@ -35,9 +36,9 @@ def main():
 
     dev = torch.device("cuda:0")
     cfg = os.environ.get("CONFIG", "headline")
-    g = W.C4 if cfg == "c4" else W.CPP_EXAMPLE if cfg in ("cpp", "cppu") else W.HEADLINE
+    g = W.C4 if cfg == "c4" else W.CPP_EXAMPLE if cfg in ("cpp", "cppu", "cppuc") else W.HEADLINE
     shape, shards, inner = g["shape"], g["shards"], g["inner"]
-    if cfg in ("cpp", "cppu"):  # the reference's example: int32, zarr's default sharding codecs (cppu: unsharded)
+    if cfg in ("cpp", "cppu", "cppuc"):  # the reference's example array (cppu: unsharded; cppuc: + crc32c)
         data = torch.from_numpy(W.cpp_example_data("plain")).to(dev)
     elif cfg == "c4":
         gen = torch.Generator(device=dev).manual_seed(0)
@@ -55,10 +56,11 @@ def main():
         shards = None
     R = 2 if cfg == "c4" else 4
     reps = int(os.environ.get("REPS", "4" if cfg == "c4" else "20"))
-    if cfg == "cppu":
+    if cfg in ("cppu", "cppuc"):
         shards = None
-    if cfg in ("cpp", "cppu"):
-        crc = [bench.build_replica(dev, data, shape, inner, [W.LE], shards=shards, dtype="int32", fill=0)
+    if cfg in ("cpp", "cppu", "cppuc"):
+        cc = [W.LE, W.CRC] if cfg == "cppuc" else [W.LE]
+        crc = [bench.build_replica(dev, data, shape, inner, cc, shards=shards, dtype="int32", fill=0)
                .prepare_read((Ellipsis,)) for _ in range(R)]
         nocrc = []
     else:
@@ -69,6 +71,8 @@ def main():
     n_inner = int(np.prod([s // i for s, i in zip(shape, inner)]))
     if cfg == "cppu":  # bytes only: no trailer, no index
         alg = n_inner * int(np.prod(inner)) * 4 + data.numel() * 4
+    elif cfg == "cppuc":  # + a 4-byte trailer per chunk
+        alg = n_inner * (int(np.prod(inner)) * 4 + 4) + data.numel() * 4
     elif cfg == "cpp":  # inner chunks without a trailer, one index CRC per shard
         n_shards = int(np.prod([s // i for s, i in zip(shape, shards)]))
         cps = n_inner // n_shards

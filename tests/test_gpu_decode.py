@@ -571,6 +571,58 @@ def test_plain_small_chunks_lead4(device, shape, chunks, dtype, sel, endian):
     assert got2.tobytes() == got.tobytes()
 
 
+# chunks of <= 16 KiB WITH a crc32c trailer (unsharded, or inner chunks of a
+# shard): k_decode_lead4's CRC form, one verdict per chunk in its workgroup
+CRC_SMALL_CASES = [
+    ((256, 256), (64, 64), "int32", (Ellipsis,), [LE, CRC], None),
+    ((96, 256), (16, 64), "float32", (slice(5, 90), slice(64, 256)), [BE, CRC], None),
+    ((12, 32, 64), (3, 16, 64), "float32", (Ellipsis,), [LE, CRC], None),
+    ((96, 128), (16, 128), "int16", (Ellipsis,), [BE, CRC], None),
+    ((256, 256), (128, 128), "int32", (Ellipsis,), None, (64, 64)),
+    ((64, 64, 32), (16, 32, 32), "float64", (slice(1, 60), slice(None), slice(None)), None, (4, 16, 32)),
+]
+
+
+@pytest.mark.parametrize("shape,chunks,dtype,sel,codecs,inner", CRC_SMALL_CASES)
+def test_crc_small_chunks_lead4(device, shape, chunks, dtype, sel, codecs, inner):
+    import zarr_hip
+    from zarr_hip import _native as N
+
+    if inner is not None:
+        codecs = [SHARD(inner, [LE, CRC])]
+    meta = O.ArrayMeta(shape, chunks, np.dtype(dtype), 0, codecs=codecs)
+    host = {}
+    data = _data(shape, dtype, seed=7)
+    if inner is not None:
+        data[tuple(slice(0, i) for i in inner)] = 0  # an elided inner chunk
+    O.write(host, meta, (Ellipsis,), data)
+    keys = [k for k in sorted(host) if k.startswith("c/")]
+    if inner is None:
+        del host[keys[1]]  # a missing chunk: fill
+    arr = zarr_hip.Array.create(zarr_hip.DeviceStore.from_host(host, device), shape, chunks, dtype, 0, codecs=codecs)
+    got = arr[sel]
+    assert N.lib().zhip_last_kernel() == b"k_decode_lead4"
+    assert got.tobytes() == np.ascontiguousarray(O.read(host, meta, sel)).tobytes()
+    N.lib().zhip_set_tuning(6, 11)  # the pair kernels on the same layout
+    try:
+        got2 = arr[sel]
+        assert N.lib().zhip_last_kernel() != b"k_decode_lead4"
+    finally:
+        N.lib().zhip_set_tuning(6, 0)
+    assert got2.tobytes() == got.tobytes()
+    bad = dict(host)
+    b = bytearray(bad[keys[-1]])
+    b[len(b) // 3] ^= 0x01  # inside a chunk's payload
+    bad[keys[-1]] = bytes(b)
+    with pytest.raises(ValueError) as want:
+        O.read(bad, meta)
+    arr2 = zarr_hip.Array.create(zarr_hip.DeviceStore.from_host(bad, device), shape, chunks, dtype, 0, codecs=codecs)
+    with pytest.raises(ValueError) as err:
+        arr2[...]
+    assert N.lib().zhip_last_kernel() == b"k_decode_lead4"
+    assert str(err.value) == str(want.value)
+
+
 @pytest.mark.parametrize("loc", ["end", "start"])
 def test_default_sharding_chain_index_crc_mismatch(device, loc):
     import zarr_hip

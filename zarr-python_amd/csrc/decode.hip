@@ -518,11 +518,11 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
         // one workgroup per pair of units, non-persistent (k_decode_pair)
         const int nu = (p.tune & kTuneSingle) ? 1 : 2;
         const bool crc = (p.lflags & ZHIP_LF_CRC) != 0, swap = (p.lflags & ZHIP_LF_SWAP) != 0;
-        if (!crc && p.nseg == 1u && p.E <= 4u * kWgStride && g_tune_arm != 11) {
-            // chunks of <= 16 KiB without a CRC (sharded or not): four per
+        if (p.nseg == 1u && p.E <= 4u * kWgStride && g_tune_arm != 11) {
+            // chunks of <= 16 KiB (sharded or not, with a CRC or not): four per
             // workgroup over their live steps, after the leading index-check
             // workgroups if any (k_decode_lead4; arm 11 keeps the pair kernels)
-            KernelFn qfn = select_pair_kernel(false, p.g.itemsize, swap, 10);
+            KernelFn qfn = select_pair_kernel(crc, p.g.itemsize, swap, 10);
             if (!qfn) return ZHIP_E_UNSUPPORTED;
             const uint32_t quads = (uint32_t)(((uint64_t)p.n_units + 3u) / 4u);
             const uint32_t lead = (p.n_idx + 7u) & ~7u;

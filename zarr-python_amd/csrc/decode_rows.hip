@@ -956,11 +956,16 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
 // live except the whole empty head steps of a chunk under 16 KiB.  The row map
 // is zhip_rows_map's, unchanged (entries 4..7 of each unit); no XCD remap (four
 // consecutive chunks per workgroup already keep a shard's chunks together).
-template <int ITEM, bool SWAP>
+// CRC: inner chunks with a crc32c trailer.  A workgroup owns its four chunks
+// whole, so each one's Horner state (four accumulators through the 11/11/10
+// tables, as k_decode_pair) folds, takes unit 0's lane constant, reduces in
+// LDS and is compared with the trailer by lane i of wave 0: no publication.
+template <int ITEM, bool SWAP, bool CRC = false>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_decode_lead4(const DecodeParams p) {
     constexpr int NQ = 4, KS = kDefaultBlocks / 2, K0 = kDefaultBlocks - KS;
     __shared__ uint32_t s_tab[kPairTabWords];
     __shared__ uint32_t s_red[kThreads / 64];
+    __shared__ uint32_t s_crc[CRC ? NQ : 1][kThreads / 64];
     const int t = threadIdx.x;
     PairHot h = p.h;
     pair_hot(h);
@@ -972,8 +977,22 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     }
     const uint32_t q0 = (uint32_t)NQ * (bx - lead);  // nseg == 1: unit = chunk
     if (q0 >= h.n_units) return;
-    const uint32_t expected = p.g.nbytes;
+    const uint32_t expected = p.g.nbytes + (CRC ? 4u : 0u);
     const uint8_t* zero = reinterpret_cast<const uint8_t*>(g_rows_zero);
+    // CRC: the pair tables and unit 0's lane constants first (L2 hits, back
+    // before the chunk data)
+    uint4 tv0, tv1, tv2, tv3, tv4, tv5;
+    uint32_t kl = 0;
+    if constexpr (CRC) {
+        const uint4* gt = reinterpret_cast<const uint4*>(p.pair_tab);
+        tv0 = gt[t];
+        tv1 = gt[t + kThreads];
+        tv2 = gt[t + 2 * kThreads];
+        tv3 = gt[t + 3 * kThreads];
+        tv4 = gt[t + 4 * kThreads];
+        tv5 = gt[t + 5 * kThreads];
+        kl = load_u32_any(reinterpret_cast<const uint8_t*>(p.kpair11 + t));
+    }
     auto load_tail = [&](const Unit& u, bool live, uint4 (&b)[KS]) {
         const bool ok = live && u.mode == ZHIP_ST_OK;
 #pragma unroll
@@ -1012,6 +1031,20 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     RowSteps m[NQ];
 #pragma unroll
     for (int i = 0; i < NQ; ++i) m[i] = load_row_steps(p, U[i]);
+    uint32_t stored[NQ];
+    if constexpr (CRC) {
+#pragma unroll
+        for (int i = 0; i < NQ; ++i)
+            stored[i] = (live[i] && U[i].mode == ZHIP_ST_OK) ? load_trailer_uniform(U[i].cp, p.g.nbytes) : 0u;
+        uint4* st = reinterpret_cast<uint4*>(s_tab);
+        st[t] = tv0;
+        st[t + kThreads] = tv1;
+        st[t + 2 * kThreads] = tv2;
+        st[t + 3 * kThreads] = tv3;
+        st[t + 4 * kThreads] = tv4;
+        st[t + 5 * kThreads] = tv5;
+        __syncthreads();
+    }
     uint8_t* sink = reinterpret_cast<uint8_t*>(g_rows_sink);
     const uint32_t lane_row = (16u * (uint32_t)t) >> p.row_shift;
     const uint32_t lane_col = (16u * (uint32_t)t) & ((1u << p.row_shift) - 1u);
@@ -1022,20 +1055,37 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
         const bool present = live[i] && U[i].mode == ZHIP_ST_OK;
         const bool writes = live[i] && (U[i].mode == ZHIP_ST_OK || U[i].mode == ZHIP_ST_MISSING);
         uint8_t* const base = p.out + U[i].out_off;
+        Acc4 acc = {0u, 0u, 0u, 0u};
 #pragma unroll
         for (int k = 0; k < KS; ++k) {
             const zhip_rowblk& e = m[i].e[K0 + k];
             const uint32_t lo = e.lo, hi = e.hi;
             const bool wr = writes && lane_row - lo < hi - lo;  // unsigned: lo <= lane_row < hi
             store_nt16(wr ? base + e.rel + lane_off : sink, present ? swap_block<ITEM, SWAP>(blk[i][k]) : f);
+            // (zero head blocks of a chunk under 16 KiB leave the state at 0)
+            if constexpr (CRC) crc_block4(s_tab, acc, blk[i][k]);
+        }
+        if constexpr (CRC) {
+            const uint32_t v = wave_xor(present ? lanemul_reg(kl, fold4(s_tab, acc)) : 0u);
+            if ((t & 63) == 0) s_crc[i][t >> 6] = v;
+        }
+    }
+    if constexpr (CRC) {
+        __syncthreads();
+        if (t < 64) {  // wave 0: one verdict per chunk against its trailer
+#pragma unroll
+            for (int i = 0; i < NQ; ++i)
+                if (live[i] && U[i].mode == ZHIP_ST_OK)
+                    finalize_uniform(p, U[i].c, __builtin_amdgcn_readfirstlane(stored[i]),
+                                     __builtin_amdgcn_readfirstlane(s_crc[i][0] ^ s_crc[i][1] ^ s_crc[i][2] ^
+                                                                    s_crc[i][3]),
+                                     t, true);
         }
     }
 #pragma unroll
     for (int i = 0; i < NQ; ++i)
-        if (live[i]) unit_status_pair(p, U[i], false, t);
-}
-
-int debug_stamps(uint64_t* host_out, uint32_t n_wg) {
+        if (live[i]) unit_status_pair(p, U[i], CRC, t);
+}int debug_stamps(uint64_t* host_out, uint32_t n_wg) {
     if (n_wg > kStampWG) n_wg = kStampWG;
     return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_stamps), (size_t)n_wg * kStampSlots * sizeof(uint64_t), 0,
                                hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
@@ -1068,13 +1118,15 @@ KernelFn select_pair_kernel(bool crc, int item, bool swap, int nu) {
             default: return nullptr;
         }
     }
-    if (nu == 10) {  // no data CRC, chunks of <= 16 KiB: four per workgroup (k_decode_lead4)
-        if (crc) return nullptr;
+    if (nu == 10) {  // chunks of <= 16 KiB: four per workgroup (k_decode_lead4)
         switch (item) {
-            case 1: return k_decode_lead4<1, false>;
-            case 2: return swap ? k_decode_lead4<2, true> : k_decode_lead4<2, false>;
-            case 4: return swap ? k_decode_lead4<4, true> : k_decode_lead4<4, false>;
-            case 8: return swap ? k_decode_lead4<8, true> : k_decode_lead4<8, false>;
+            case 1: return crc ? k_decode_lead4<1, false, true> : k_decode_lead4<1, false>;
+            case 2: return crc ? (swap ? k_decode_lead4<2, true, true> : k_decode_lead4<2, false, true>)
+                               : (swap ? k_decode_lead4<2, true> : k_decode_lead4<2, false>);
+            case 4: return crc ? (swap ? k_decode_lead4<4, true, true> : k_decode_lead4<4, false, true>)
+                               : (swap ? k_decode_lead4<4, true> : k_decode_lead4<4, false>);
+            case 8: return crc ? (swap ? k_decode_lead4<8, true, true> : k_decode_lead4<8, false, true>)
+                               : (swap ? k_decode_lead4<8, true> : k_decode_lead4<8, false>);
             default: return nullptr;
         }
     }
