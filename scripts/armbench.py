@@ -9,7 +9,7 @@ share8 (rank 0's 1-shard share of the headline at N = 8) | share4 | c3 | c3g
 (transpose (2,1,0) in 64^3 / 128^3 chunks) | cpp (the reference's
 codec_pipeline_performance array, zarr's default sharding codecs) | cppu (the
 same array unsharded, bytes only: 64^2 chunks of 16 KiB) | cppuc (the same
-with crc32c).  Also
+with crc32c) | cppu8 / cppu4 (unsharded, 8 / 4 KiB chunks).  Also
 the no-CRC twin (zarr's default sharding codecs, k_decode_lead) for the
 headline.  One JSON line per arm: min / median us per launch and the HBM
 fraction of the algorithmic bytes.  After timing, the production arm's
@@ -36,9 +36,9 @@ def main():
 
     dev = torch.device("cuda:0")
     cfg = os.environ.get("CONFIG", "headline")
-    g = W.C4 if cfg == "c4" else W.CPP_EXAMPLE if cfg in ("cpp", "cppu", "cppuc") else W.HEADLINE
+    g = W.C4 if cfg == "c4" else W.CPP_EXAMPLE if cfg.startswith("cpp") else W.HEADLINE
     shape, shards, inner = g["shape"], g["shards"], g["inner"]
-    if cfg in ("cpp", "cppu", "cppuc"):  # the reference's example array (cppu: unsharded; cppuc: + crc32c)
+    if cfg.startswith("cpp"):  # the reference's example array (cppu: unsharded; cppuc: + crc32c; cppu8 / cppu4: 8 / 4 KiB chunks)
         data = torch.from_numpy(W.cpp_example_data("plain")).to(dev)
     elif cfg == "c4":
         gen = torch.Generator(device=dev).manual_seed(0)
@@ -56,9 +56,10 @@ def main():
         shards = None
     R = 2 if cfg == "c4" else 4
     reps = int(os.environ.get("REPS", "4" if cfg == "c4" else "20"))
-    if cfg in ("cppu", "cppuc"):
+    if cfg in ("cppu", "cppuc", "cppu8", "cppu4"):
         shards = None
-    if cfg in ("cpp", "cppu", "cppuc"):
+        inner = {"cppu8": (32, 64), "cppu4": (16, 64)}.get(cfg, inner)
+    if cfg.startswith("cpp"):
         cc = [W.LE, W.CRC] if cfg == "cppuc" else [W.LE]
         crc = [bench.build_replica(dev, data, shape, inner, cc, shards=shards, dtype="int32", fill=0)
                .prepare_read((Ellipsis,)) for _ in range(R)]
@@ -69,7 +70,7 @@ def main():
         nocrc = [bench.build_replica(dev, data, shape, inner, aa + [W.LE], shards=shards).prepare_read((Ellipsis,))
                  for _ in range(R)] if cfg != "c4" else []
     n_inner = int(np.prod([s // i for s, i in zip(shape, inner)]))
-    if cfg == "cppu":  # bytes only: no trailer, no index
+    if cfg in ("cppu", "cppu8", "cppu4"):  # bytes only: no trailer, no index
         alg = n_inner * int(np.prod(inner)) * 4 + data.numel() * 4
     elif cfg == "cppuc":  # + a 4-byte trailer per chunk
         alg = n_inner * (int(np.prod(inner)) * 4 + 4) + data.numel() * 4

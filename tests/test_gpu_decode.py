@@ -522,8 +522,12 @@ def test_default_sharding_chain_fused(device, shape, shards, inner, dtype, sel, 
     assert 0 < prog.data.n_idx <= n_shards
     got = arr[sel]
     from zarr_hip import _native as N
-    small = int(np.prod(inner)) * np.dtype(dtype).itemsize <= 16384
-    assert N.lib().zhip_last_kernel() == (b"k_decode_lead4" if small else b"k_decode_lead")
+    nb = int(np.prod(inner)) * np.dtype(dtype).itemsize
+    small = nb <= 16384
+    if small:
+        _check_small_kernel(nb)
+    else:
+        assert N.lib().zhip_last_kernel() == b"k_decode_lead"
     want = O.read(host, meta, sel)
     assert got.tobytes() == np.ascontiguousarray(want).tobytes()
     if small:  # ZHIP_TUNE_ARM 11: the pair kernel for the same layout, same bytes
@@ -536,9 +540,26 @@ def test_default_sharding_chain_fused(device, shape, shards, inner, dtype, sel, 
         assert got2.tobytes() == got.tobytes()
 
 
+def _small_kernel(nbytes):
+    """k_decode_lead4 runs four chunks of <= 16 KiB per workgroup, eight of
+    4-8 KiB (launched as k_decode_lead8)."""
+    return b"k_decode_lead8" if 4096 < nbytes <= 8192 else b"k_decode_lead4"
+
+
+def _check_small_kernel(nbytes):
+    from zarr_hip import _native as N
+
+    k, want = N.lib().zhip_last_kernel(), _small_kernel(nbytes)
+    if want is None:
+        assert k not in (b"k_decode_lead4", b"k_decode_lead8"), k
+    else:
+        assert k == want, k
+
+
 # unsharded chunks of <= 16 KiB without a CRC (zarr's default v3 codecs,
 # bytes only) take k_decode_lead4 too, with no leading workgroups
 PLAIN_SMALL_CASES = [
+    ((8, 32, 64), (2, 16, 64), "float32", (Ellipsis,), LE),
     ((256, 256), (64, 64), "int32", (Ellipsis,), LE),
     ((96, 256), (16, 64), "float32", (slice(5, 90), slice(64, 256)), BE),
     ((12, 32, 64), (3, 16, 64), "float32", (slice(1, 11), slice(2, 30), slice(None)), LE),
@@ -560,7 +581,7 @@ def test_plain_small_chunks_lead4(device, shape, chunks, dtype, sel, endian):
     store = zarr_hip.DeviceStore.from_host(host, device)
     arr = zarr_hip.Array.create(store, shape, chunks, dtype, 0, codecs=codecs)
     got = arr[sel]
-    assert N.lib().zhip_last_kernel() == b"k_decode_lead4"
+    _check_small_kernel(int(np.prod(chunks)) * np.dtype(dtype).itemsize)
     assert got.tobytes() == np.ascontiguousarray(O.read(host, meta, sel)).tobytes()
     N.lib().zhip_set_tuning(6, 11)  # the pair kernel on the same layout
     try:
@@ -569,6 +590,15 @@ def test_plain_small_chunks_lead4(device, shape, chunks, dtype, sel, endian):
     finally:
         N.lib().zhip_set_tuning(6, 0)
     assert got2.tobytes() == got.tobytes()
+    if int(np.prod(chunks)) * np.dtype(dtype).itemsize <= 8192:  # arms 12 / 13: four / eight per workgroup
+        for arm, k in ((12, b"k_decode_lead4"), (13, b"k_decode_lead8")):
+            N.lib().zhip_set_tuning(6, arm)
+            try:
+                got3 = arr[sel]
+                assert N.lib().zhip_last_kernel() == k
+            finally:
+                N.lib().zhip_set_tuning(6, 0)
+            assert got3.tobytes() == got.tobytes()
 
 
 # chunks of <= 16 KiB WITH a crc32c trailer (unsharded, or inner chunks of a
@@ -600,13 +630,14 @@ def test_crc_small_chunks_lead4(device, shape, chunks, dtype, sel, codecs, inner
     if inner is None:
         del host[keys[1]]  # a missing chunk: fill
     arr = zarr_hip.Array.create(zarr_hip.DeviceStore.from_host(host, device), shape, chunks, dtype, 0, codecs=codecs)
+    nb = int(np.prod(inner if inner is not None else chunks)) * np.dtype(dtype).itemsize
     got = arr[sel]
-    assert N.lib().zhip_last_kernel() == b"k_decode_lead4"
+    _check_small_kernel(nb)
     assert got.tobytes() == np.ascontiguousarray(O.read(host, meta, sel)).tobytes()
     N.lib().zhip_set_tuning(6, 11)  # the pair kernels on the same layout
     try:
         got2 = arr[sel]
-        assert N.lib().zhip_last_kernel() != b"k_decode_lead4"
+        assert N.lib().zhip_last_kernel() not in (b"k_decode_lead4", b"k_decode_lead8")
     finally:
         N.lib().zhip_set_tuning(6, 0)
     assert got2.tobytes() == got.tobytes()
@@ -619,7 +650,7 @@ def test_crc_small_chunks_lead4(device, shape, chunks, dtype, sel, codecs, inner
     arr2 = zarr_hip.Array.create(zarr_hip.DeviceStore.from_host(bad, device), shape, chunks, dtype, 0, codecs=codecs)
     with pytest.raises(ValueError) as err:
         arr2[...]
-    assert N.lib().zhip_last_kernel() == b"k_decode_lead4"
+    _check_small_kernel(nb)
     assert str(err.value) == str(want.value)
 
 

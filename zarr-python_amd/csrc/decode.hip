@@ -522,12 +522,20 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
             // chunks of <= 16 KiB (sharded or not, with a CRC or not): four per
             // workgroup over their live steps, after the leading index-check
             // workgroups if any (k_decode_lead4; arm 11 keeps the pair kernels)
-            KernelFn qfn = select_pair_kernel(crc, p.g.itemsize, swap, 10);
+            // (chunks of 4-8 KiB: eight per workgroup over their last two steps;
+            // graph-timed on the example array unsharded, profiles/r04/lead8/:
+            // 8 KiB chunks 25.3-25.6 us vs 37.1 with four per workgroup and 30.8
+            // with the pair kernel; 4 KiB chunks 37.2 with four, 52.4 with eight,
+            // 41.4 with the pair kernel.  Arms 12 / 13 force four / eight.)
+            const bool e8 = g_tune_arm == 13 ||
+                            (g_tune_arm != 12 && p.E > (uint32_t)kWgStride && p.E <= 2u * kWgStride);
+            KernelFn qfn = select_pair_kernel(crc, p.g.itemsize, swap, e8 ? 11 : 10);
             if (!qfn) return ZHIP_E_UNSUPPORTED;
-            const uint32_t quads = (uint32_t)(((uint64_t)p.n_units + 3u) / 4u);
+            const uint32_t per = e8 ? 8u : 4u;
+            const uint32_t quads = (uint32_t)(((uint64_t)p.n_units + per - 1u) / per);
             const uint32_t lead = (p.n_idx + 7u) & ~7u;
             if ((uint64_t)quads + lead > 0x7FFFFFFFull) return ZHIP_E_UNSUPPORTED;
-            g_last_kernel = "k_decode_lead4";
+            g_last_kernel = e8 ? "k_decode_lead8" : "k_decode_lead4";
             hipLaunchKernelGGL(qfn, dim3(quads + lead), dim3(kThreads), 0, stream, p);
             return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
         }

@@ -960,9 +960,17 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
 // whole, so each one's Horner state (four accumulators through the 11/11/10
 // tables, as k_decode_pair) folds, takes unit 0's lane constant, reduces in
 // LDS and is compared with the trailer by lane i of wave 0: no publication.
-template <int ITEM, bool SWAP, bool CRC = false>
+// NQ = 8 (launched as "k_decode_lead8"): chunks of <= 8 KiB, eight per
+// workgroup over their last two steps.
+template <int KS>
+struct RowTail {
+    zhip_rowblk e[KS];
+};
+
+template <int ITEM, bool SWAP, bool CRC = false, int NQ = 4>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_decode_lead4(const DecodeParams p) {
-    constexpr int NQ = 4, KS = kDefaultBlocks / 2, K0 = kDefaultBlocks - KS;
+    static_assert(NQ == 4 || NQ == 8, "four or eight chunks per workgroup");
+    constexpr int KS = 16 / NQ, K0 = kDefaultBlocks - KS;  // 16 blocks per lane either way
     __shared__ uint32_t s_tab[kPairTabWords];
     __shared__ uint32_t s_red[kThreads / 64];
     __shared__ uint32_t s_crc[CRC ? NQ : 1][kThreads / 64];
@@ -1028,9 +1036,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
 #pragma unroll
         for (int i = 0; i < NQ; ++i) load_tail(U[i], live[i], blk[i]);
     }
-    RowSteps m[NQ];
+    RowTail<KS> m[NQ];  // the live row-map entries K0..7 of each unit
 #pragma unroll
-    for (int i = 0; i < NQ; ++i) m[i] = load_row_steps(p, U[i]);
+    for (int i = 0; i < NQ; ++i)
+        m[i] = load_uniform<RowTail<KS>>(p.rowmap + ((size_t)U[i].sel * p.nseg + U[i].sidx) * kDefaultBlocks + K0);
     uint32_t stored[NQ];
     if constexpr (CRC) {
 #pragma unroll
@@ -1058,7 +1067,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
         Acc4 acc = {0u, 0u, 0u, 0u};
 #pragma unroll
         for (int k = 0; k < KS; ++k) {
-            const zhip_rowblk& e = m[i].e[K0 + k];
+            const zhip_rowblk& e = m[i].e[k];
             const uint32_t lo = e.lo, hi = e.hi;
             const bool wr = writes && lane_row - lo < hi - lo;  // unsigned: lo <= lane_row < hi
             store_nt16(wr ? base + e.rel + lane_off : sink, present ? swap_block<ITEM, SWAP>(blk[i][k]) : f);
@@ -1118,15 +1127,23 @@ KernelFn select_pair_kernel(bool crc, int item, bool swap, int nu) {
             default: return nullptr;
         }
     }
-    if (nu == 10) {  // chunks of <= 16 KiB: four per workgroup (k_decode_lead4)
+    if (nu == 10 || nu == 11) {  // chunks of <= 16 / 8 KiB: four / eight per workgroup (k_decode_lead4)
+        const bool e8 = nu == 11;
         switch (item) {
-            case 1: return crc ? k_decode_lead4<1, false, true> : k_decode_lead4<1, false>;
-            case 2: return crc ? (swap ? k_decode_lead4<2, true, true> : k_decode_lead4<2, false, true>)
-                               : (swap ? k_decode_lead4<2, true> : k_decode_lead4<2, false>);
-            case 4: return crc ? (swap ? k_decode_lead4<4, true, true> : k_decode_lead4<4, false, true>)
-                               : (swap ? k_decode_lead4<4, true> : k_decode_lead4<4, false>);
-            case 8: return crc ? (swap ? k_decode_lead4<8, true, true> : k_decode_lead4<8, false, true>)
-                               : (swap ? k_decode_lead4<8, true> : k_decode_lead4<8, false>);
+            case 1: return crc ? (e8 ? k_decode_lead4<1, false, true, 8> : k_decode_lead4<1, false, true>)
+                               : (e8 ? k_decode_lead4<1, false, false, 8> : k_decode_lead4<1, false>);
+            case 2: return crc ? (swap ? (e8 ? k_decode_lead4<2, true, true, 8> : k_decode_lead4<2, true, true>)
+                                       : (e8 ? k_decode_lead4<2, false, true, 8> : k_decode_lead4<2, false, true>))
+                               : (swap ? (e8 ? k_decode_lead4<2, true, false, 8> : k_decode_lead4<2, true>)
+                                       : (e8 ? k_decode_lead4<2, false, false, 8> : k_decode_lead4<2, false>));
+            case 4: return crc ? (swap ? (e8 ? k_decode_lead4<4, true, true, 8> : k_decode_lead4<4, true, true>)
+                                       : (e8 ? k_decode_lead4<4, false, true, 8> : k_decode_lead4<4, false, true>))
+                               : (swap ? (e8 ? k_decode_lead4<4, true, false, 8> : k_decode_lead4<4, true>)
+                                       : (e8 ? k_decode_lead4<4, false, false, 8> : k_decode_lead4<4, false>));
+            case 8: return crc ? (swap ? (e8 ? k_decode_lead4<8, true, true, 8> : k_decode_lead4<8, true, true>)
+                                       : (e8 ? k_decode_lead4<8, false, true, 8> : k_decode_lead4<8, false, true>))
+                               : (swap ? (e8 ? k_decode_lead4<8, true, false, 8> : k_decode_lead4<8, true>)
+                                       : (e8 ? k_decode_lead4<8, false, false, 8> : k_decode_lead4<8, false>));
             default: return nullptr;
         }
     }
