@@ -499,9 +499,102 @@ def _ceildiv(a: int, b: int) -> int:
     return -(-a // b)
 
 
-def dim_projections(sel: Any, dim_len: int, chunk_len: int):
-    """IntDimIndexer / SliceDimIndexer.__iter__ (indexing.py:365-468) for a regular grid.
+# ---------------------------------------------------------------------------
+# Chunk grids (src/zarr/core/chunk_grids.py): FixedDimension 73-164,
+# VaryingDimension 167-293, ChunkGrid.from_sizes 448-487, __getitem__ 528-546
+# ---------------------------------------------------------------------------
+
+
+class VaryingDim:
+    """VaryingDimension (chunk_grids.py:167-293): explicit edges; data_size
+    clips the last chunk at the extent, chunk_size (the codec shape) does not."""
+
+    def __init__(self, edges, extent: int):
+        self.edges = tuple(int(e) for e in edges)
+        if not self.edges:
+            raise ValueError("VaryingDimension edges must not be empty")
+        if any(e <= 0 for e in self.edges):
+            raise ValueError(f"All edge lengths must be > 0, got {self.edges}")
+        self.cumulative = tuple(itertools.accumulate(self.edges))
+        if extent > self.cumulative[-1]:
+            raise ValueError(f"VaryingDimension extent {extent} exceeds sum of edges {self.cumulative[-1]}")
+        self.extent = int(extent)
+        # chunks overlapping [0, extent): bisect_left(cumulative, extent) + 1
+        self.nchunks = 0 if extent == 0 else sum(1 for c in self.cumulative if c < extent) + 1
+
+    def index_to_chunk(self, idx: int) -> int:
+        if idx < 0 or idx >= self.extent:
+            raise IndexError(f"Index {idx} out of bounds for dimension with extent {self.extent}")
+        return sum(1 for c in self.cumulative if c <= idx)  # bisect_right
+
+    def chunk_offset(self, ix: int) -> int:
+        return self.cumulative[ix - 1] if ix > 0 else 0
+
+    def chunk_size(self, ix: int) -> int:
+        return self.edges[ix]
+
+    def data_size(self, ix: int) -> int:
+        return max(0, min(self.edges[ix], self.extent - self.chunk_offset(ix)))
+
+
+class FixedDim:
+    """FixedDimension (chunk_grids.py:73-130)."""
+
+    def __init__(self, size: int, extent: int):
+        self.size, self.extent = int(size), int(extent)
+        self.nchunks = 0 if self.size == 0 else _ceildiv(self.extent, self.size)
+
+    def index_to_chunk(self, idx: int) -> int:
+        return 0 if self.size == 0 else idx // self.size
+
+    def chunk_offset(self, ix: int) -> int:
+        return ix * self.size
+
+    def chunk_size(self, ix: int) -> int:
+        return self.size
+
+    def data_size(self, ix: int) -> int:
+        return 0 if self.size == 0 else max(0, min(self.size, self.extent - ix * self.size))
+
+
+def grid_dims(shape: tuple[int, ...], chunk_sizes) -> list:
+    """ChunkGrid.from_sizes (chunk_grids.py:448-487): an int per dim is
+    regular; an edge list is regular when its edges are equal and cover the
+    extent, else varying."""
+    dims = []
+    for spec, extent in zip(chunk_sizes, shape):
+        if isinstance(spec, (int, np.integer)):
+            dims.append(FixedDim(int(spec), extent))
+            continue
+        edges = [int(e) for e in spec]
+        if edges and edges[0] > 0 and all(e == edges[0] for e in edges) and (
+                extent == sum(edges) or len(edges) == _ceildiv(extent, edges[0])):
+            dims.append(FixedDim(edges[0], extent))
+        else:
+            dims.append(VaryingDim(edges, extent))
+    return dims
+
+
+def grid_getitem(dims: list, coords: tuple[int, ...]):
+    """ChunkGrid.__getitem__ (chunk_grids.py:528-546): (slices, codec_shape),
+    None out of bounds."""
+    slices, cshape = [], []
+    for d, ix in zip(dims, coords):
+        if ix < 0 or ix >= d.nchunks:
+            return None
+        off = d.chunk_offset(ix)
+        slices.append(slice(off, off + d.data_size(ix), 1))
+        cshape.append(d.chunk_size(ix))
+    return tuple(slices), tuple(cshape)
+
+
+def dim_projections(sel: Any, dim_len: int, chunk_len):
+    """IntDimIndexer / SliceDimIndexer.__iter__ (indexing.py:369-468) over a
+    regular chunk length or a dimension grid (FixedDim / VaryingDim).
     Yields (chunk_ix, chunk_sel, out_sel|None, is_complete)."""
+    if not isinstance(chunk_len, (int, np.integer)):
+        yield from _dim_projections_grid(sel, dim_len, chunk_len)
+        return
     nchunks = _ceildiv(dim_len, chunk_len)
     if isinstance(sel, (int, np.integer)):
         i = int(sel)
@@ -541,7 +634,47 @@ def dim_projections(sel: Any, dim_len: int, chunk_len: int):
         yield ix, slice(s0, s1, step), slice(out_off, out_off + nitems), complete
 
 
-def basic_indexer(selection: tuple, shape: tuple[int, ...], chunk_shape: tuple[int, ...]):
+def _dim_projections_grid(sel: Any, dim_len: int, g):
+    """indexing.py:369-468 with the DimensionGrid protocol (index_to_chunk,
+    chunk_offset, data_size)."""
+    if isinstance(sel, (int, np.integer)):
+        i = int(sel)
+        if i < 0:
+            i += dim_len
+        if not 0 <= i < dim_len:
+            raise IndexError(f"index out of bounds for dimension with length {dim_len}")
+        ix = g.index_to_chunk(i)
+        yield ix, i - g.chunk_offset(ix), None, g.data_size(ix) == 1
+        return
+    start, stop, step = sel.indices(dim_len)
+    if step < 1:
+        raise IndexError("only slices with step >= 1 are supported.")
+    if start >= stop:
+        return
+    ix_from = g.index_to_chunk(start) if start > 0 else 0
+    ix_to = g.index_to_chunk(stop - 1) + 1 if stop > 0 else 0
+    for ix in range(ix_from, ix_to):
+        off = g.chunk_offset(ix)
+        clen = g.data_size(ix)
+        limit = off + clen
+        if start < off:
+            s0 = 0
+            rem = (off - start) % step
+            if rem:
+                s0 += step - rem
+            out_off = _ceildiv(off - start, step)
+        else:
+            s0 = start - off
+            out_off = 0
+        s1 = clen if stop > limit else stop - off
+        nitems = _ceildiv(s1 - s0, step)
+        if nitems <= 0:
+            continue
+        complete = s0 == 0 and stop >= limit and step == 1
+        yield ix, slice(s0, s1, step), slice(out_off, out_off + nitems), complete
+
+
+def basic_indexer(selection: tuple, shape: tuple[int, ...], chunk_shape):
     """BasicIndexer (indexing.py:571-621): list of ChunkProjection + output shape."""
     if not isinstance(selection, tuple):
         selection = (selection,)
@@ -583,6 +716,27 @@ class ArrayMeta:
                                                    "configuration": {"endian": "little"}}])
     write_empty_chunks: bool = False
 
+    def __post_init__(self):
+        # chunk_shape may name a rectilinear grid: per dim an int or an edge list
+        self.chunk_shape = tuple(c if isinstance(c, (int, np.integer)) else tuple(int(e) for e in c)
+                                 for c in self.chunk_shape)
+
+    @property
+    def regular(self) -> bool:
+        return all(isinstance(c, (int, np.integer)) for c in self.chunk_shape)
+
+    def dims(self) -> list:
+        return grid_dims(self.shape, self.chunk_shape)
+
+    def chunk_spec(self, coords: tuple[int, ...]) -> Spec:
+        """_get_chunk_spec (array.py:5373-5390): the chunk's codec shape."""
+        if self.regular:
+            return self.spec()
+        got = grid_getitem(self.dims(), coords)
+        if got is None:
+            raise IndexError(f"Chunk coordinates {coords} are out of bounds.")
+        return Spec(got[1], np.dtype(self.dtype), self.fill_value, self.write_empty_chunks)
+
     @property
     def chain(self) -> Chain:
         return Chain.from_json(self.codecs)
@@ -598,17 +752,17 @@ class ArrayMeta:
 
 def read(store: dict, meta: ArrayMeta, selection: Any = Ellipsis) -> np.ndarray:
     """Array._get_selection + FusedCodecPipeline.read_sync (per-chunk decode & scatter)."""
+    grid = meta.chunk_shape if meta.regular else meta.dims()
     projections, out_shape = basic_indexer(selection if isinstance(selection, tuple)
-                                           else (selection,), meta.shape, meta.chunk_shape)
+                                           else (selection,), meta.shape, grid)
     out = np.empty(out_shape, dtype=meta.dtype)
     chain = meta.chain
-    spec = meta.spec()
     for coords, csel, osel, _ in projections:
         raw = store.get(meta.chunk_key(coords))
         if raw is None:
             out[osel] = meta.fill_value  # scatter_chunk(None, ...) (chunk_utils.py:106-108)
             continue
-        chunk = chain_decode(_as_u8(raw), chain, spec)
+        chunk = chain_decode(_as_u8(raw), chain, meta.chunk_spec(coords))
         out[osel] = chunk[csel]
     return out
 
@@ -659,28 +813,30 @@ def shard_encode_partial(store: dict, key: str, chunk_value: np.ndarray, selecti
 def write(store: dict, meta: ArrayMeta, selection: Any, value: Any) -> None:
     """Array._set_selection + FusedCodecPipeline.write_sync + merge_and_encode_chunk
     (partial shard encode when the chain is a sharding codec alone)."""
+    grid = meta.chunk_shape if meta.regular else meta.dims()
     projections, out_shape = basic_indexer(selection if isinstance(selection, tuple)
-                                           else (selection,), meta.shape, meta.chunk_shape)
+                                           else (selection,), meta.shape, grid)
     value = np.asarray(value, dtype=meta.dtype)
     chain = meta.chain
-    spec = meta.spec()
     if chain.shard is not None and not chain.aa and not chain.bb:
         for coords, csel, osel, complete in projections:
             chunk_value = value if value.shape == () else value[osel]
-            shard_encode_partial(store, meta.chunk_key(coords), chunk_value, csel, chain.shard, spec)
+            shard_encode_partial(store, meta.chunk_key(coords), chunk_value, csel, chain.shard,
+                                 meta.chunk_spec(coords))
         return
     for coords, csel, osel, complete in projections:
         key = meta.chunk_key(coords)
+        spec = meta.chunk_spec(coords)
         if complete and value.shape != ():
             merged = value[osel]
-            if merged.shape != tuple(meta.chunk_shape):
+            if merged.shape != tuple(spec.shape):
                 merged = None
         else:
             merged = None
         if merged is None:
             raw = None if complete else store.get(key)
             if raw is None:
-                merged = np.full(meta.chunk_shape, meta.fill_value, dtype=meta.dtype)
+                merged = np.full(spec.shape, meta.fill_value, dtype=meta.dtype)
             else:
                 merged = chain_decode(_as_u8(raw), chain, spec).copy()
             merged[csel] = value if value.shape == () else value[osel].reshape(

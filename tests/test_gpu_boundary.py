@@ -196,6 +196,56 @@ def test_encode_decode_batch_api(device):
     assert isinstance(e2[0], Buffer) and e2[0].to_bytes() == enc[0].to_bytes()
 
 
+@pytest.mark.parametrize("codecs", [[LE, CRC], [{"name": "transpose", "configuration": {"order": [2, 0, 1]}}, BE, CRC],
+                                    [SHARD((8, 8, 16), [LE, CRC])]])
+def test_decode_encode_64_chunks_one_launch(device, codecs):
+    """pipeline.decode / encode over a list of chunks plan the whole list as
+    one batch per spec (BatchedCodecPipeline.decode_batch / encode_batch,
+    codec_pipeline.py:679-745): 64 chunks decode in ONE decode launch (plus
+    the shard-index check launch of a sharded chain, fused where it can be)
+    and agree with the oracle; None entries stay None; a second spec in the
+    same list is its own group."""
+    from zarr_hip import pipeline as P
+    from zarr_hip.buffer import NDBuffer
+
+    shape = (16, 16, 16)
+    meta, spec, pipe = _setup(shape, shape, codecs)
+    chain = O.Chain.from_json(codecs)
+    arrs = [_data(shape, seed=s) for s in range(64)]
+    arrs[9] = np.zeros(shape, np.float32)  # all fill: elided
+    n0 = P.LAUNCHES[0]
+    enc = pipe.encode_sync([(NDBuffer(a), spec) for a in arrs] + [(None, spec)])
+    assert enc[64] is None and enc[9] is None
+    for a, e in zip(arrs, enc):
+        if e is not None:
+            assert e.to_bytes() == bytes(O.chain_encode(a, chain, meta.spec()))
+    items = [(e, spec) for e in enc]
+    n0 = P.LAUNCHES[0]
+    dec = pipe.decode_sync(items)
+    launches = P.LAUNCHES[0] - n0
+    # (a sharded chain read from host bytes may add its shard-index check launch)
+    assert launches == 1 or ("sharding_indexed" in str(codecs) and launches == 2)
+    assert dec[9] is None and dec[64] is None
+    for a, d in zip(arrs, dec):
+        if d is not None:
+            assert d.as_numpy_array().tobytes() == a.tobytes()
+    # a second chunk shape in the same list: one more group, one more launch
+    spec_b = Z.ArraySpec((8, 16, 16), Z.ZDType("float32"), np.float32(0), Z.ArrayConfig(), Z.cpu_prototype)
+    meta_b = O.ArrayMeta((8, 16, 16), (8, 16, 16), np.dtype("float32"), 0.0, codecs=codecs)
+    b = _data((8, 16, 16), seed=99)
+    eb = bytes(O.chain_encode(b, chain, meta_b.spec()))
+    from zarr_hip.buffer import Buffer
+
+    n0 = P.LAUNCHES[0]
+    mixed = pipe.decode_sync([(enc[0], spec), (Buffer.from_bytes(eb), spec_b), (enc[1], spec)])
+    assert P.LAUNCHES[0] - n0 == 2 * launches
+    assert mixed[0].as_numpy_array().tobytes() == arrs[0].tobytes()
+    assert mixed[1].as_numpy_array().tobytes() == b.tobytes()
+    assert mixed[2].as_numpy_array().tobytes() == arrs[1].tobytes()
+    eb2 = pipe.encode_sync([(NDBuffer(b), spec_b), (NDBuffer(arrs[2]), spec)])
+    assert eb2[0].to_bytes() == eb and eb2[1].to_bytes() == enc[2].to_bytes()
+
+
 def test_rocm_buffer_prototype(device):
     from zarr_hip.buffer import Buffer, NDBuffer, buffer_prototype
 

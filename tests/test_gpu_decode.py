@@ -1035,6 +1035,56 @@ def test_il_arms_exact_and_crc(device, arm):
         N.lib().zhip_set_tuning(6, 0)
 
 
+ILQ_ARMS = {20: "k_decode_ilq2", 21: "k_decode_ilq4", 22: "k_decode_ilq1_glds", 23: "k_decode_ilq2_glds",
+            24: "k_decode_ilq4_glds"}
+
+
+@pytest.mark.parametrize("sharded", [False, True])
+@pytest.mark.parametrize("arm", sorted(ILQ_ARMS))
+def test_ilq_arms_exact_and_crc(device, arm, sharded):
+    """k_decode_ilq (NQ units of one chunk per workgroup, tables by registers
+    or LDS-DMA) decodes the headline chunk geometry bit-exactly -- whole
+    array, a partial window, a missing chunk filled -- and reports a corrupted
+    chunk (and, sharded, a corrupted index) with the reference's message."""
+    import zarr_hip
+    from zarr_hip import _native as N
+
+    shape, chunks = (128, 128, 64), (64, 64, 64)
+    codecs = [SHARD((64, 64, 64), [LE, CRC])] if sharded else [LE, CRC]
+    cshape = (128, 128, 64) if sharded else chunks
+    meta = O.ArrayMeta(shape, cshape, np.dtype("float32"), 1.5, codecs=codecs)
+    host = {}
+    O.write(host, meta, (Ellipsis,), _data(shape, "float32"))
+    if not sharded:
+        host.pop("c/1/0/0")
+    store = zarr_hip.DeviceStore.from_host(host, device)
+    arr = zarr_hip.Array.create(store, shape, cshape, "float32", 1.5, codecs=codecs)
+    N.lib().zhip_set_tuning(6, arm)
+    try:
+        for sel in [(Ellipsis,), (slice(16, 100), slice(0, 128), slice(0, 64))]:
+            prog, out = arr.prepare_read(sel)
+            prog.launch()
+            prog.results()
+            assert N.lib().zhip_last_kernel().decode() == ILQ_ARMS[arm]
+            assert out.cpu().numpy().tobytes() == np.ascontiguousarray(O.read(host, meta, sel)).tobytes()
+        key = "c/0/0/0" if sharded else "c/0/1/0"
+        for at in ([700001, len(host[key]) - 40] if sharded else [700001]):
+            _corrupt(store, host, key, at=at)
+            with pytest.raises(ValueError) as want:
+                O.read(host, meta)
+            prog, out = arr.prepare_read((Ellipsis,))
+            prog.launch()
+            with pytest.raises(ValueError) as got:
+                prog.results()
+            assert str(got.value) == str(want.value)
+            _corrupt(store, host, key, at=at)
+            prog.launch()
+            prog.results()
+            assert out.cpu().numpy().tobytes() == O.read(host, meta).tobytes()
+    finally:
+        N.lib().zhip_set_tuning(6, 0)
+
+
 @pytest.mark.parametrize("arm", [0, 5])
 @pytest.mark.parametrize("dtype,endian,chunks,shape", TILE4_CASES)
 def test_transpose_tile4w_and_tile4(device, dtype, endian, chunks, shape, arm):

@@ -80,7 +80,6 @@ def test_fixture_details():
 @pytest.mark.parametrize("name,exc,what", [
     ("zstd_codec", NotImplementedError, "zstd"),
     ("blosc_codec", NotImplementedError, "blosc"),
-    ("rectilinear_grid", NotImplementedError, "regular"),
 ])
 def test_fixture_off_the_path_is_refused(name, exc, what):
     from zarr_hip import ArrayMetadata

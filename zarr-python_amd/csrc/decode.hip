@@ -498,6 +498,7 @@ KernelFn select_il_kernel_arm(bool crc, int item, bool swap, int arm);  // decod
 KernelFn select_il_kernel_cf(bool crc, int item, bool swap);         // decode_rows.hip
 KernelFn select_il_kernel_regmul(bool crc, int item, bool swap, bool occ6);  // decode_rows.hip
 KernelFn select_xw_kernel(bool crc, int item, bool swap);            // decode_rows.hip
+KernelFn select_ilq_kernel(int item, bool swap, int nq, bool glds);  // decode_rows.hip
 KernelFn select_tile4_kernel(bool crc, int item, bool swap);         // decode_tile.hip
 KernelFn select_tile4f_kernel(int item, bool swap);                  // decode_tile.hip
 KernelFn select_tile4w_kernel(int item, bool swap);                  // decode_tile.hip
@@ -575,6 +576,23 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
             if (grid > 0x7FFFFFFFull) return ZHIP_E_UNSUPPORTED;
             g_last_kernel = "k_decode_xw";
             hipLaunchKernelGGL(xfn, dim3((uint32_t)grid), dim3(kThreads), 0, stream, p);
+            return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
+        }
+        if (il && g_tune_arm >= 20 && g_tune_arm <= 24) {
+            // k_decode_ilq arms: NQ units per workgroup, tables by registers or LDS-DMA
+            static const char* names[] = {"k_decode_ilq2", "k_decode_ilq4", "k_decode_ilq1_glds",
+                                          "k_decode_ilq2_glds", "k_decode_ilq4_glds"};
+            const int a = g_tune_arm - 20;
+            const int nq = (a == 0 || a == 3) ? 2 : (a == 1 || a == 4) ? 4 : 1;
+            if (p.nseg % (uint32_t)nq) return ZHIP_E_UNSUPPORTED;
+            KernelFn qfn = select_ilq_kernel(p.g.itemsize, swap, nq, a >= 2);
+            if (!qfn) return ZHIP_E_UNSUPPORTED;
+            const uint32_t ug = (uint32_t)(((uint64_t)p.n_units + nq - 1u) / nq);
+            const uint32_t xg = (p.n_idx + (uint32_t)nq - 1u) / (uint32_t)nq;
+            const uint32_t qgrid = ug > xg ? ug : xg;
+            if (qgrid == 0) return ZHIP_OK;
+            g_last_kernel = names[a];
+            hipLaunchKernelGGL(qfn, dim3(qgrid), dim3(nq * kThreads), 0, stream, p);
             return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
         }
         if (il) {

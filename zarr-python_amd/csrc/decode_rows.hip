@@ -1606,6 +1606,202 @@ KernelFn select_il_kernel(bool crc, int item, bool swap) {
 }
 
 // ---------------------------------------------------------------------------
+// k_decode_ilq: k_decode_il with NQ consecutive units of one chunk per
+// workgroup (NQ x 256 threads).  Quarter q = threadIdx.x / 256 runs unit
+// r0 + q exactly as k_decode_il's workgroup r0 + q would (same loads, row-map
+// stores, one 8-step Horner chain per lane through the A_(4096 S) tables, the
+// same host-built lane constants), but the NQ units share one 24 KiB table
+// fill, one workgroup reduction and one publication (arrival bits
+// ((1 << NQ) - 1) << r0), so per byte decoded the table traffic, the run-end
+// barrier and the returning atomics drop by NQ.  GLDS: the tables go global
+// -> LDS by LDS-DMA (global_load_lds_dwordx4, issued in inline asm ahead of
+// every compiler-visible data load, so the compiler's counted vmcnt waits
+// stay exact; one manual vmcnt before the table barrier), which frees the
+// staging VGPRs and the ds_write_b128 transfers.  CPU emulation of the CRC
+// algebra: zhip_emulate_chunk_crc_il (the chains are k_decode_il's).
+__device__ __forceinline__ uint32_t lds_addr32(const void* a) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)a;
+}
+
+// One LDS-DMA piece: lane i's 16 bytes at g land at LDS byte lds + 16 i (lds
+// wave-uniform).  M0 is saved and restored around it.
+__device__ __forceinline__ void glds16(const void* g, uint32_t lds) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(g), "s"(lds)
+                 : "memory");
+}
+
+// publish_il for a workgroup carrying several arrival bits of chunk c
+__device__ __forceinline__ void publish_ilq(const DecodeParams& p, uint32_t c, uint32_t r0, uint32_t nq, uint32_t wpc,
+                                            uint32_t V, uint32_t stored, int t) {
+    if (wpc <= 32u) {
+        const uint64_t full = wpc >= 32u ? 0xFFFFFFFFull : ((1ull << wpc) - 1ull);
+        const uint32_t bits = ((1u << nq) - 1u) << r0;
+        uint64_t prev = 0;
+        uint64_t* const w = reinterpret_cast<uint64_t*>(p.ws) + (uint64_t)(kPubLine / 2u) * c;
+        if (t == 0) prev = __hip_atomic_fetch_xor(w, ((uint64_t)bits << 32) | V, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)prev);
+        const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(prev >> 32));
+        if ((uint64_t)(hi ^ bits) == full) {
+            if (t == 0) __hip_atomic_store(w, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            finalize_uniform(p, c, stored, lo ^ V, t, true);
+        }
+    } else {  // more than 32 units per chunk: xor, then count arrivals
+        uint32_t raw = 0, last = 0;
+        if (t == 0) {
+            uint32_t* accw = p.ws + 4ull * c;
+            const uint32_t prev = __hip_atomic_fetch_xor(accw, V, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::"v"(prev) : "memory");
+            const uint32_t tk = __hip_atomic_fetch_add(accw + 2, nq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (tk + nq == wpc) {
+                raw = __hip_atomic_exchange(accw, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                asm volatile("s_waitcnt vmcnt(0)" ::"v"(raw) : "memory");
+                __hip_atomic_store(accw + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                last = 1;
+            }
+        }
+        if (__builtin_amdgcn_readfirstlane(last))
+            finalize_uniform(p, c, stored, __builtin_amdgcn_readfirstlane(raw), t, true);
+    }
+}
+
+template <int ITEM, bool SWAP, int NQ, bool GLDS>
+__global__ __launch_bounds__(NQ * kThreads) __attribute__((amdgpu_waves_per_eu(NQ == 4 ? 8 : NQ == 2 ? 6 : 4)))
+void k_decode_ilq(const DecodeParams p) {
+    constexpr int K = kDefaultBlocks;
+    constexpr int NT = NQ * kThreads;
+    constexpr int NTV = kPairTabWords / 4;  // 16-byte table pieces
+    constexpr int NL = (NTV + NT - 1) / NT;
+    static_assert(K == 8, "the manual table wait below counts K + 1 younger loads");
+    __shared__ uint32_t s_tab[kPairTabWords];
+    __shared__ uint32_t s_mul[12 * NT];
+    __shared__ uint32_t s_red[NT / 64];
+    __shared__ uint32_t s_ridx[4 * NQ];
+    const int T = threadIdx.x;
+    const int q = T >> 8, t = T & (kThreads - 1);
+    const uint32_t G = gridDim.x, g = blockIdx.x;
+    const uint32_t wpc = p.nseg, S = p.il_S;
+    const uint32_t u0 = g * (uint32_t)NQ;
+    const uint32_t c = u0 / wpc;
+    const uint32_t r0 = u0 - c * wpc, r = r0 + (uint32_t)q;
+    const bool has = c < p.n_chunks;
+    if (!has && u0 >= p.n_idx) return;  // workgroup-uniform
+    const uint32_t expected = p.g.nbytes + 4u;
+    const uint8_t* zero = reinterpret_cast<const uint8_t*>(g_rows_zero);
+    // 1. vector loads: the lane constants, [GLDS: the table pieces], the K data
+    //    blocks, the first index block; headers, row map, trailer are scalar
+    const uint32_t kl = load_u32_any(reinterpret_cast<const uint8_t*>(p.il_klane + (size_t)(has ? r : 0u) * kThreads + t));
+    const uint32_t kix = load_u32_any(reinterpret_cast<const uint8_t*>(p.il_kidx + t));
+    const uint4* gt = reinterpret_cast<const uint4*>(p.il_tab);
+    uint4 tv[GLDS ? 1 : NL];
+    if constexpr (GLDS) {
+        const uint32_t wv = (uint32_t)T & ~63u;
+        const uint32_t lb = __builtin_amdgcn_readfirstlane(lds_addr32(s_tab) + 16u * wv);
+#pragma unroll
+        for (int i = 0; i < NL; ++i)
+            if ((uint32_t)(i * NT) + wv < (uint32_t)NTV) glds16(gt + i * NT + T, lb + 16u * (uint32_t)(i * NT));
+    } else {
+#pragma unroll
+        for (int i = 0; i < NL; ++i) tv[i] = gt[min(i * NT + T, NTV - 1)];
+    }
+    Unit U;
+    if (has) U = resolve_unit(p, c * wpc, expected);
+    else {
+        U.c = 0;
+        U.sidx = 0;
+        U.mode = ZHIP_ST_MISSING;
+        U.cp = zero;
+        U.seg_lo = 0;
+        U.sel = 0;
+        U.out_off = 0;
+    }
+    const bool ok = has && U.mode == ZHIP_ST_OK;
+    const uint32_t st0 = (r / S) * S * (uint32_t)K + (r % S);
+    const int32_t lo_frame = (int32_t)p.E - (int32_t)(p.nseg * p.seg);
+    uint4 A[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int32_t base = lo_frame + kWgStride * (int32_t)(st0 + S * (uint32_t)k);
+        A[k] = load_stream16_any(ok && base >= 0 ? U.cp + base + 16 * t : zero);
+    }
+    const uint32_t jq = u0 + (uint32_t)q;
+    const uint4 ipre = index_prefetch(p, jq, jq < p.n_idx, t, zero);
+    zhip_rowblk m[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint32_t st = st0 + S * (uint32_t)k;
+        const uint32_t sidx = p.nseg - 1u - st / (uint32_t)K;
+        m[k] = load_uniform<zhip_rowblk>(p.rowmap + ((size_t)U.sel * p.nseg + sidx) * K + (st % (uint32_t)K));
+    }
+    uint32_t stored = 0;
+    if (ok) stored = load_trailer_uniform(U.cp, p.g.nbytes);
+    // 2. tables into LDS, the lane-multiply column of this quarter
+    uint32_t* const smq = s_mul + q * 12 * kThreads;
+    if constexpr (GLDS) {
+        asm volatile("s_waitcnt vmcnt(9)" ::: "memory");  // all but the K data loads and the index block
+    } else {
+        uint4* stt = reinterpret_cast<uint4*>(s_tab);
+#pragma unroll
+        for (int i = 0; i < NL; ++i)
+            if (i * NT + T < NTV) stt[i * NT + T] = tv[i];
+    }
+    lanemul3_init(smq, t, kl);
+    __syncthreads();
+    if (has) {
+        // 3. stores, each block's Horner step after its store
+        uint8_t* sink = reinterpret_cast<uint8_t*>(g_rows_sink);
+        const uint32_t lane_row = (16u * (uint32_t)t) >> p.row_shift;
+        const uint32_t lane_col = (16u * (uint32_t)t) & ((1u << p.row_shift) - 1u);
+        const int64_t lane_off = (int64_t)lane_row * p.r_oy + (int64_t)lane_col;
+        const bool writes = ok || U.mode == ZHIP_ST_MISSING;
+        uint8_t* const obase = p.out + U.out_off;
+        const uint4 f = make_uint4(p.fill[0], p.fill[1], p.fill[2], p.fill[3]);
+        Acc4 acc = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint32_t lo = m[k].lo, hi = m[k].hi;
+            const bool wr = writes && lane_row - lo < hi - lo;
+            store_nt16(wr ? obase + m[k].rel + lane_off : sink, ok ? swap_block<ITEM, SWAP>(A[k]) : f);
+            if (ok) crc_block4(s_tab, acc, A[k]);
+        }
+        // 4. run end: one reduction and one publication for the NQ units
+        uint32_t v = ok ? lanemul3(smq, t, fold4(s_tab, acc)) : 0u;
+        v = wave_xor(v);
+        if ((T & 63) == 0) s_red[T >> 6] = v;
+        __syncthreads();
+        if (ok && T < 64) {
+            uint32_t V = 0;
+#pragma unroll
+            for (int w = 0; w < NT / 64; ++w) V ^= s_red[w];
+            publish_ilq(p, c, r0, (uint32_t)NQ, wpc, __builtin_amdgcn_readfirstlane(V),
+                        __builtin_amdgcn_readfirstlane(stored), T);
+        }
+        if (r == 0) unit_status_pair(p, U, true, t);
+    }
+    // 5. fused shard-index checks: quarter q checks index jj NQ + q (one step
+    //    per lane), every quarter joins every barrier
+    for (uint32_t jj = g; jj * (uint32_t)NQ < p.n_idx; jj += G) {
+        const uint32_t j = jj * (uint32_t)NQ + (uint32_t)q;
+        const bool act = j < p.n_idx;
+        verify_index_pair(p, act ? j : 0u, t, kix, s_tab, s_ridx + 4 * q, act && jj == g, ipre, act);
+    }
+}
+
+KernelFn select_ilq_kernel(int item, bool swap, int nq, bool glds) {  // CRC chains only
+#define ZHIP_ILQ(I, W) \
+    (nq == 4 ? (glds ? k_decode_ilq<I, W, 4, true> : k_decode_ilq<I, W, 4, false>) \
+             : nq == 2 ? (glds ? k_decode_ilq<I, W, 2, true> : k_decode_ilq<I, W, 2, false>) \
+                       : (glds ? k_decode_ilq<I, W, 1, true> : k_decode_ilq<I, W, 1, false>))
+    switch (item) {
+        case 4: return swap ? ZHIP_ILQ(4, true) : ZHIP_ILQ(4, false);
+        default: return nullptr;
+    }
+#undef ZHIP_ILQ
+}
+
+// ---------------------------------------------------------------------------
 // k_decode_xw: the whole-row decode with the four waves of a workgroup on four
 // consecutive chunks of the batch (a shard's x-adjacent inner chunks), each
 // wave on the same 8 KiB span (r of P = chunk / 8 KiB) of its own chunk: lane

@@ -20,6 +20,7 @@ import numpy as np
 
 from . import buffer
 from .codecs import BytesCodec, Crc32cCodec, ShardingCodec, parse_codecs
+from .grid import ChunkGrid
 from .indexing import basic_projections, chunk_batch
 from .pipeline import DecodeProgram, HipCodecPipeline
 from .spec import ArrayConfig, ArraySpec
@@ -75,12 +76,27 @@ class ArrayMetadata:
     separator: str = "/"
     attributes: dict = field(default_factory=dict)
     key_encoding: str = "default"  # or "v2"
+    # a rectilinear grid (chunk_grids.py:399-546); None: the regular grid of
+    # chunk_shape.  With a rectilinear grid chunk_shape is the placeholder
+    # (1,) * ndim zarr evolves the pipeline with (array.py:237-247)
+    grid: ChunkGrid | None = None
+
+    @property
+    def chunk_grid(self) -> ChunkGrid:
+        if self.grid is not None:
+            return self.grid
+        return ChunkGrid.from_sizes(self.shape, tuple(self.chunk_shape))
+
+    @property
+    def is_regular(self) -> bool:
+        return self.grid is None or self.grid.is_regular
 
     def to_json(self) -> dict:
         return {
             "zarr_format": 3, "node_type": "array", "shape": list(self.shape),
             "data_type": np.dtype(self.dtype).name,
-            "chunk_grid": {"name": "regular", "configuration": {"chunk_shape": list(self.chunk_shape)}},
+            "chunk_grid": self.chunk_grid.to_json() if self.grid is not None else
+            {"name": "regular", "configuration": {"chunk_shape": list(self.chunk_shape)}},
             "chunk_key_encoding": {"name": self.key_encoding, "configuration": {"separator": self.separator}},
             "fill_value": _fill_to_json(self.fill_value, np.dtype(self.dtype)),
             "codecs": [c.to_dict() for c in self.codecs],
@@ -91,18 +107,17 @@ class ArrayMetadata:
     def from_json(cls, d: dict) -> "ArrayMetadata":
         if d.get("zarr_format") != 3 or d.get("node_type") != "array":
             raise ValueError("not a zarr v3 array")
-        grid = d["chunk_grid"]
-        if grid["name"] != "regular":
-            raise NotImplementedError("only regular chunk grids are on the GPU path")
+        g = ChunkGrid.from_json(tuple(d["shape"]), d["chunk_grid"])
         dt = np.dtype(d["data_type"])
         cke = d.get("chunk_key_encoding", {"name": "default"})
         name = cke.get("name", "default")
         if name not in ("default", "v2"):
             raise NotImplementedError(f"chunk key encoding {name!r}")
         sep = (cke.get("configuration") or {}).get("separator", "/" if name == "default" else ".")
-        return cls(tuple(d["shape"]), tuple(grid["configuration"]["chunk_shape"]), dt,
-                   _fill_from_json(d["fill_value"], dt), tuple(parse_codecs(d["codecs"])), sep,
-                   d.get("attributes", {}), name)
+        chunk_shape = g.chunk_shape if g.is_regular else (1,) * g.ndim
+        return cls(tuple(d["shape"]), chunk_shape, dt, _fill_from_json(d["fill_value"], dt),
+                   tuple(parse_codecs(d["codecs"])), sep, d.get("attributes", {}), name,
+                   None if g.is_regular else g)
 
     def chunk_key(self, coords) -> str:
         if self.key_encoding == "v2":
@@ -112,6 +127,8 @@ class ArrayMetadata:
 
     @property
     def grid_shape(self) -> tuple[int, ...]:
+        if self.grid is not None:
+            return self.grid.grid_shape
         return tuple(-(-s // c) for s, c in zip(self.shape, self.chunk_shape))
 
 
@@ -123,10 +140,16 @@ class Array:
         self.store_path = store_path
         self.metadata = metadata
         self.config = config
+        # (rectilinear grids: the pipeline is evolved with the placeholder
+        # shape, every chunk then carries its own spec -- array.py:237-247,
+        # 5373-5390)
         self.spec = ArraySpec(metadata.chunk_shape, metadata.dtype, metadata.fill_value, config)
         self.codec_pipeline = HipCodecPipeline.from_codecs(metadata.codecs).evolve_from_array_spec(
             self.spec)
-        self.codec_pipeline.validate(shape=metadata.shape, chunk_shape=metadata.chunk_shape)
+        if metadata.is_regular:
+            self.codec_pipeline.validate(shape=metadata.shape, chunk_shape=metadata.chunk_shape)
+        else:
+            self.codec_pipeline.validate(shape=metadata.shape, chunk_grid=metadata.grid)
         self._programs: dict = {}
 
     # ------------------------------------------------------------ construction
@@ -138,14 +161,20 @@ class Array:
         if codecs is None:
             codecs = (BytesCodec(endian="little" if dtype.itemsize > 1 else None),)
         codecs = tuple(parse_codecs(codecs))
-        chunk_shape = tuple(chunks)
+        chunk_shape = tuple(c if isinstance(c, int) else tuple(c) for c in chunks)
         if shards is not None:
             inner = tuple(parse_codecs(inner_codecs)) if inner_codecs is not None else codecs
             codecs = (ShardingCodec(chunk_shape=chunk_shape, codecs=inner,
                                     index_location=index_location),)
-            chunk_shape = tuple(shards)
+            chunk_shape = tuple(c if isinstance(c, int) else tuple(c) for c in shards)
+        # nested edge lists: a rectilinear grid (regular when they reduce to one)
+        grid = None
+        if any(not isinstance(c, int) for c in chunk_shape):
+            grid = ChunkGrid.from_sizes(tuple(shape), chunk_shape)
+            chunk_shape = grid.chunk_shape if grid.is_regular else (1,) * len(chunk_shape)
+            grid = None if grid.is_regular else grid
         md = ArrayMetadata(tuple(shape), chunk_shape, dtype, np.array(fill_value, dtype)[()],
-                           codecs)
+                           codecs, grid=grid)
         sp = StorePath(store, path)
         key = f"{path}/zarr.json" if path else "zarr.json"
         store.set_sync(key, json.dumps(md.to_json()).encode())
@@ -196,6 +225,9 @@ class Array:
         return batch, out_shape
 
     def _batch_info(self, selection):
+        md = self.metadata
+        if not md.is_regular:
+            return self._batch_info_rectilinear(selection)
         rows, out_shape = chunk_batch(selection, self.metadata.shape, self.metadata.chunk_shape)
         store, spec, sep = self.store_path.store, self.spec, self.metadata.separator
         if self.metadata.key_encoding == "v2":
@@ -206,6 +238,24 @@ class Array:
         prefix = f"{self.store_path.path}/c" if self.store_path.path else "c"
         batch = [(StorePath(store, sep.join([prefix, *map(str, co)])), spec, csel, osel, comp)
                  for co, csel, osel, comp in rows]
+        return batch, out_shape
+
+    def _batch_info_rectilinear(self, selection):
+        """_get_selection's batch for a rectilinear grid: one ArraySpec per
+        chunk, shape = ChunkGrid[coords].codec_shape (_get_chunk_spec,
+        array.py:5373-5390, 5469-5486); specs of equal shape are shared."""
+        md = self.metadata
+        g = md.grid
+        rows, out_shape = chunk_batch(selection, md.shape, g)
+        store, sep = self.store_path.store, md.separator
+        specs: dict = {}
+        batch = []
+        for co, csel, osel, comp in rows:
+            cs = g.codec_shape(co)
+            sp = specs.get(cs)
+            if sp is None:
+                sp = specs[cs] = ArraySpec(cs, md.dtype, md.fill_value, self.config)
+            batch.append((StorePath(store, self._key(co)), sp, csel, osel, comp))
         return batch, out_shape
 
     # ------------------------------------------------------------------- read

@@ -205,13 +205,28 @@ class ShardingCodec:
             "index_codecs": tuple(c.to_dict() for c in self.index_codecs),
             "index_location": self.index_location}}
 
-    def validate(self, *, shape, chunk_shape=None, **kw) -> None:
-        """sharding.py:558-590 (regular grid)."""
+    def validate(self, *, shape, chunk_shape=None, chunk_grid=None, **kw) -> None:
+        """sharding.py:567-593: every distinct edge of the (regular or
+        rectilinear) outer grid divisible by the inner chunk size."""
         if len(self.chunk_shape) != len(shape):
             raise ValueError("The shard's `chunk_shape` and array's `shape` need to have the same "
                              "number of dimensions.")
+        edges_per_dim = None
         if chunk_shape is not None:
-            for i, (edge, inner) in enumerate(zip(chunk_shape, self.chunk_shape)):
+            edges_per_dim = tuple((int(e),) for e in chunk_shape)
+        elif chunk_grid is not None:
+            dims = getattr(chunk_grid, "dimensions", None)
+            if dims is not None:  # zarr_hip.grid.ChunkGrid
+                edges_per_dim = tuple(tuple(d.unique_edge_lengths) for d in dims)
+            else:  # zarr's Regular / RectilinearChunkGridMetadata
+                cs = getattr(chunk_grid, "chunk_shape", None)
+                shapes = getattr(chunk_grid, "chunk_shapes", None)
+                if cs is not None:
+                    edges_per_dim = tuple((int(e),) for e in cs)
+                elif shapes is not None:
+                    edges_per_dim = tuple((int(s),) if isinstance(s, int) else tuple(s) for s in shapes)
+        for i, (edges, inner) in enumerate(zip(edges_per_dim or (), self.chunk_shape)):
+            for edge in dict.fromkeys(edges):
                 if edge % inner != 0:
                     raise ValueError(f"Chunk edge length {edge} in dimension {i} is not divisible "
                                      f"by the shard's inner chunk size {inner}.")

@@ -188,18 +188,63 @@ def _project_dim_lists(sel, dim_len: int, chunk_len: int):
     return ixs, s0s, cnts, oos, cps, step, False, nitems
 
 
-def chunk_batch(selection, shape: tuple[int, ...], chunk_shape: tuple[int, ...]):
+def _project_dim_grid(sel, dim_len: int, g):
+    """IntDimIndexer / SliceDimIndexer.__iter__ over any dimension grid
+    (indexing.py:369-468 with DimensionGrid's index_to_chunk / chunk_offset /
+    data_size): a VaryingDimension of a rectilinear grid (zarr_hip.grid)."""
+    if isinstance(sel, int):
+        ix = g.index_to_chunk(sel)
+        return [ix], [sel - g.chunk_offset(ix)], [1], [0], [g.data_size(ix) == 1], 1, True, 1
+    start, stop, step = sel.start, sel.stop, sel.step
+    nitems = max(0, -((start - stop) // step))
+    if start >= stop:
+        return [], [], [], [], [], step, False, 0
+    ix_from = g.index_to_chunk(start) if start > 0 else 0
+    ix_to = g.index_to_chunk(stop - 1) + 1 if stop > 0 else 0
+    ixs, s0s, cnts, oos, cps = [], [], [], [], []
+    for ix in range(ix_from, ix_to):
+        off = g.chunk_offset(ix)
+        clen = g.data_size(ix)
+        limit = off + clen
+        if start < off:
+            rem = (off - start) % step
+            s0 = step - rem if rem else 0
+            oo = -((start - off) // step)
+        else:
+            s0, oo = start - off, 0
+        s1 = clen if stop > limit else stop - off
+        cnt = max(0, -((s0 - s1) // step))
+        if cnt > 0:
+            ixs.append(ix)
+            s0s.append(s0)
+            cnts.append(cnt)
+            oos.append(oo)
+            cps.append(s0 == 0 and stop >= limit and step == 1)
+    return ixs, s0s, cnts, oos, cps, step, False, nitems
+
+
+def chunk_batch(selection, shape: tuple[int, ...], chunk_shape):
     """basic_projections + chunk_selections for a batch: per-dim projections,
     then their Cartesian product (C order over chunk coordinates, as
     basic_projections) built from Python lists.  Returns
-    ([(coords, chunk_selection, out_selection, complete)], out_shape)."""
+    ([(coords, chunk_selection, out_selection, complete)], out_shape).
+    `chunk_shape` is a regular chunk shape or a zarr_hip.grid.ChunkGrid
+    (rectilinear grids: per-dim projections over the varying edges)."""
     import itertools
 
+    from .grid import ChunkGrid, FixedDimension
+
     sel = normalize_selection(selection, shape)
+    if isinstance(chunk_shape, ChunkGrid):
+        dims = chunk_shape.dimensions
+        chunk_shape = tuple(d.size if isinstance(d, FixedDimension) else d for d in dims)
     ixs, csels, osels, cps = [], [], [], []
     out_shape = []
     for s, n, c in zip(sel, shape, chunk_shape):
-        ix, s0, cnt, oo, cp, st, dropped, nitems = _project_dim_lists(s, n, c)
+        if isinstance(c, int):
+            ix, s0, cnt, oo, cp, st, dropped, nitems = _project_dim_lists(s, n, c)
+        else:
+            ix, s0, cnt, oo, cp, st, dropped, nitems = _project_dim_grid(s, n, c)
         ixs.append(ix)
         cps.append(cp)
         if dropped:

@@ -281,6 +281,7 @@ class DecodeLaunch:
     def launch(self, stream: int | None = None) -> None:
         if self.n == 0:
             return
+        LAUNCHES[0] += 1
         s = _stream_handle(self.device) if stream is None else stream
         out_ptr = self.out.data_ptr() if self.out is not None else None
         # deferred CRC verdicts (zarrhip.h): consecutive launches publish into
@@ -316,6 +317,7 @@ class DecodeLaunch:
         launches only (no fused index checks, no load prediction)."""
         if count == 0:
             return
+        LAUNCHES[0] += 1
         assert self.n_idx == 0 and self.predict is None
         self._ranges.append((first, count))  # where this range's verdict words live (statuses())
         s = _stream_handle(self.device) if stream is None else stream
@@ -506,6 +508,67 @@ class DecodeProgram:
         return tuple(out)
 
 
+class ProgramGroup:
+    """The planned read of a batch whose items carry different chunk specs
+    (spec_groups): one DecodeProgram per spec group, all over the same out
+    (the groups' out selections are disjoint), launched back to back on one
+    stream; results come back in the batch's item order."""
+
+    def __init__(self, programs: list, groups: list, n_items: int):
+        self.programs = programs
+        self.groups = groups
+        self.n_items = n_items
+
+    @property
+    def data_launches(self) -> list:
+        return [d for p in self.programs for d in getattr(p, "data_launches", [p.data])]
+
+    @property
+    def data(self):
+        return self.programs[0].data
+
+    @property
+    def clean(self) -> bool:
+        return all(p.clean for p in self.programs)
+
+    def stale(self) -> bool:
+        return any(p.stale() for p in self.programs)
+
+    def check_fresh(self) -> None:
+        for p in self.programs:
+            p.check_fresh()
+
+    def launch(self, stream: int | None = None) -> None:
+        for p in self.programs:
+            p.launch(stream)
+
+    def retarget(self, out) -> None:
+        for p in self.programs:
+            p.retarget(out)
+
+    def release(self) -> None:
+        for p in self.programs:
+            p.release()
+
+    def _merge(self, per_group) -> tuple:
+        out = [None] * self.n_items
+        for idx, res in zip(self.groups, per_group):
+            for i, r in zip(idx, res):
+                out[i] = r
+        return tuple(out)
+
+    def results(self) -> tuple[GetResult, ...]:
+        return self._merge([p.results() for p in self.programs])
+
+    def results_fast(self) -> tuple[GetResult, ...]:
+        return self._merge([p.results_fast() for p in self.programs])
+
+
+# host-side count of decode launches issued (DecodeLaunch.launch /
+# launch_range): tests check that a batch costs one launch per spec group
+LAUNCHES = [0]
+
+
 def _dv_refs(launches: list, device):
     """A device array of zhip_dv_ref (zarrhip.h) for DecodeLaunches."""
     torch = _torch()
@@ -544,9 +607,10 @@ class ReadGraph:
         # last launch left unchecked, so the graph then ends with one
         # zhip_dv_check node over every program's workspace
         counts = [len(range(j, self.repeats, len(self.programs))) for j in range(len(self.programs))]
-        launches = [getattr(p, "data", None) for p in self.programs]
-        odd = any(c % 2 for c, d in zip(counts, launches) if d is not None and hasattr(d, "d_ws"))
-        self._dv_refs = _dv_refs([d for d in launches if d is not None], self.device) if odd else None
+        launches = [getattr(p, "data_launches", None) or [getattr(p, "data", None)] for p in self.programs]
+        odd = any(c % 2 for c, ds in zip(counts, launches) for d in ds if d is not None and hasattr(d, "d_ws"))
+        self._dv_refs = _dv_refs([d for ds in launches for d in ds if d is not None], self.device) if odd \
+            else None
         with torch.cuda.device(self.device):
             with torch.cuda.graph(self.graph, stream=self.stream):
                 for i in range(self.repeats):
@@ -905,8 +969,8 @@ class HipCodecPipeline:
         return self.supports_partial_decode
 
     def validate(self, *, shape, dtype=None, chunk_grid=None, chunk_shape=None) -> None:
-        if chunk_shape is None and chunk_grid is not None:
-            chunk_shape = getattr(chunk_grid, "chunk_shape", None)
+        if chunk_shape is None and chunk_grid is not None and getattr(chunk_grid, "is_regular", True):
+            chunk_shape = getattr(chunk_grid, "chunk_shape", None)  # (rectilinear grids: per edge)
         for c in self.codecs:
             c.validate(shape=shape, dtype=dtype, chunk_grid=chunk_grid, chunk_shape=chunk_shape)
 
@@ -975,6 +1039,12 @@ class HipCodecPipeline:
             raise ValueError("empty batch")
         if not isinstance(out, torch.Tensor) or not out.is_cuda:
             raise TypeError("HipCodecPipeline.read needs a device-resident out (torch CUDA tensor)")
+        groups = spec_groups(batch)
+        if groups is not None:  # chunks of different specs (rectilinear grids): a program per spec
+            progs = [self.prepare_read([batch[i] for i in idx], out, drop_axes,
+                                       None if item_out_extra is None else np.asarray(item_out_extra)[idx],
+                                       pooled) for idx in groups]
+            return ProgramGroup(progs, groups, len(batch))
         ns = self._nested()
         if ns is not None:  # the inner pipeline's program over the touched inner shards
             from . import nested
@@ -1065,6 +1135,9 @@ class HipCodecPipeline:
         batch = normalize_batch(batch_info)
         if not batch:
             return ()
+        groups = spec_groups(batch)
+        if groups is not None:  # chunks of different specs (rectilinear grids)
+            return self._read_groups(batch, groups, out, drop_axes)
         if len(self.devices) > 1:  # items split over several GPUs (parallel.read_multi)
             from . import parallel
 
@@ -1100,6 +1173,22 @@ class HipCodecPipeline:
 
             copy_to_host(dev_out, host_out)
         return res
+
+    def _read_groups(self, batch, groups, out, drop_axes) -> tuple[GetResult, ...]:
+        """read_sync of a batch whose items carry different chunk specs: each
+        spec group is read on its own (its own plan, tables and launch) into
+        the same device out, whose regions the groups split between them; a
+        host out is copied back once, after the last group."""
+        dev_out, host_out = _resolve_out(out, batch, drop_axes)
+        res: list = [None] * len(batch)
+        for idx in groups:
+            for i, r in zip(idx, self.read_sync([batch[i] for i in idx], dev_out, drop_axes)):
+                res[i] = r
+        if host_out is not None:
+            from .buffer import copy_to_host
+
+            copy_to_host(dev_out, host_out)
+        return tuple(res)
 
     def _read_cached(self, key, batch, dev_out, drop_axes) -> tuple[GetResult, ...]:
         """A device-resident read through the per-call plan cache: a repeated
@@ -1272,6 +1361,11 @@ class HipCodecPipeline:
         if not batch:
             return
         value = _resolve_value(value)
+        groups = spec_groups(batch)
+        if groups is not None:  # chunks of different specs (rectilinear grids): one write per spec
+            for idx in groups:
+                self._write_sync([batch[i] for i in idx], value, drop_axes, partial_encode)
+            return
         if len(self.devices) > 1:  # items split over several GPUs (parallel.write_multi)
             from . import parallel
 
@@ -1326,26 +1420,48 @@ class HipCodecPipeline:
 
     def decode_sync(self, chunk_bytes_and_specs: Iterable) -> list:
         """Decode standalone chunks (Buffer | None, ArraySpec) -> NDBuffer | None
-        (abc/codec.py:417-434): one GPU decode per chunk into a device array,
-        returned as an NDBuffer of the spec's prototype (this package's device
-        NDBuffer when the spec names none)."""
+        (abc/codec.py:417-434; BatchedCodecPipeline.decode_batch,
+        codec_pipeline.py:679-706, decodes the whole list per call).  The
+        chunks of one spec are ONE read: stacked along axis 0 of one device
+        array (chunk i is rows [i s0, (i + 1) s0)), one plan, one launch; each
+        result is an NDBuffer view of its rows (this package's device NDBuffer
+        when the spec names no prototype)."""
         torch = _torch()
         from .buffer import torch_dtype
 
-        res = []
-        for raw, spec in chunk_bytes_and_specs:
-            if raw is None:
-                res.append(None)
+        items = list(chunk_bytes_and_specs)
+        res: list = [None] * len(items)
+        groups: dict = {}
+        for i, (raw, spec) in enumerate(items):
+            if raw is not None:
+                spec = coerce_spec(spec)
+                groups.setdefault(_spec_key(spec), (spec, []))[1].append(i)
+        for spec, idx in groups.values():
+            raws = []
+            dev = None
+            for i in idx:
+                raw = items[i][0]
+                raw = raw if isinstance(raw, (DeviceRef, bytes, bytearray, memoryview)) else \
+                    staging.staged_bytes(raw)
+                if dev is None:
+                    dev = raw.arena.device if isinstance(raw, DeviceRef) else (
+                        raw.device if isinstance(raw, torch.Tensor) else None)
+                raws.append(raw)
+            dev = dev or torch.device("cuda", torch.cuda.current_device())
+            full = tuple(slice(0, s, 1) for s in spec.shape)
+            if spec.ndim == 0:  # 0-d chunks cannot stack along an axis: one read each
+                for i, raw in zip(idx, raws):
+                    out = torch.empty((), dtype=torch_dtype(spec.dtype), device=dev)
+                    self.read_sync([(_Raw(raw), spec, (), (), True)], out)
+                    res[i] = _as_nd_buffer(out, spec)
                 continue
-            spec = coerce_spec(spec)
-            raw = raw if isinstance(raw, (DeviceRef, bytes, bytearray, memoryview)) else \
-                staging.staged_bytes(raw)
-            dev = raw.arena.device if isinstance(raw, DeviceRef) else (
-                raw.device if isinstance(raw, torch.Tensor) else torch.device("cuda", torch.cuda.current_device()))
-            out = torch.empty(spec.shape, dtype=torch_dtype(spec.dtype), device=dev)
-            sel = tuple(slice(0, s, 1) for s in spec.shape)
-            self.read_sync([(_Raw(raw), spec, sel, sel, True)], out)
-            res.append(_as_nd_buffer(out, spec))
+            s0 = spec.shape[0]
+            out = torch.empty((len(idx) * s0,) + tuple(spec.shape[1:]), dtype=torch_dtype(spec.dtype), device=dev)
+            batch = [(_Raw(raw), spec, full, (slice(j * s0, (j + 1) * s0),) + full[1:], True)
+                     for j, raw in enumerate(raws)]
+            self.read_sync(batch, out)
+            for j, i in enumerate(idx):
+                res[i] = _as_nd_buffer(out[j * s0:(j + 1) * s0], spec)
         return res
 
     async def decode(self, chunk_bytes_and_specs: Iterable) -> list:
@@ -1353,20 +1469,42 @@ class HipCodecPipeline:
 
     def encode_sync(self, chunk_arrays_and_specs: Iterable) -> list:
         """Encode standalone chunks (NDBuffer | None, ArraySpec) -> Buffer | None
-        (abc/codec.py:436-453): the GPU encode of each chunk (empty chunks are
-        None unless write_empty_chunks, chunk_utils.py:43-58), returned as a
-        Buffer of the spec's prototype (this package's device Buffer when the
-        spec names none).  The encoded bytes stay in HBM for device Buffers."""
-        res = []
-        for arr, spec in chunk_arrays_and_specs:
-            if arr is None:
-                res.append(None)
-                continue
-            spec = coerce_spec(spec)
-            sink = _CollectSetter()
+        (abc/codec.py:436-453; BatchedCodecPipeline.encode_batch,
+        codec_pipeline.py:716-745, encodes the whole list per call).  The
+        chunks of one spec are ONE write: stacked along axis 0 of one device
+        array, each chunk a complete chunk region of it, one GPU encode.  Empty
+        chunks are None unless write_empty_chunks (chunk_utils.py:43-58); each
+        result is a Buffer of the spec's prototype (this package's device
+        Buffer when the spec names none: the encoded bytes stay in HBM)."""
+        torch = _torch()
+        from .writer import _value_tensor
+
+        items = list(chunk_arrays_and_specs)
+        res: list = [None] * len(items)
+        groups: dict = {}
+        for i, (arr, spec) in enumerate(items):
+            if arr is not None:
+                spec = coerce_spec(spec)
+                groups.setdefault(_spec_key(spec), (spec, []))[1].append(i)
+        for spec, idx in groups.values():
             full = tuple(slice(0, s, 1) for s in spec.shape)
-            self._write_sync([(sink, spec, full, full, True)], arr, partial_encode=False)
-            res.append(None if sink.value is None else _as_buffer(sink.value, spec))
+            vals = [_resolve_value(items[i][0]) for i in idx]
+            dev = next((v.device for v in vals if isinstance(v, torch.Tensor) and v.is_cuda), None) or \
+                torch.device("cuda", torch.cuda.current_device())
+            if spec.ndim == 0:
+                for i, v in zip(idx, vals):
+                    sink = _CollectSetter()
+                    self._write_sync([(sink, spec, (), (), True)], v, partial_encode=False)
+                    res[i] = None if sink.value is None else _as_buffer(sink.value, spec)
+                continue
+            s0 = spec.shape[0]
+            stacked = torch.cat([_value_tensor(v, spec.dtype, dev).reshape(spec.shape) for v in vals], 0)
+            sinks = [_CollectSetter() for _ in idx]
+            batch = [(sink, spec, full, (slice(j * s0, (j + 1) * s0),) + full[1:], True)
+                     for j, sink in enumerate(sinks)]
+            self._write_sync(batch, stacked, partial_encode=False)
+            for i, sink in zip(idx, sinks):
+                res[i] = None if sink.value is None else _as_buffer(sink.value, spec)
         return res
 
     async def encode(self, chunk_arrays_and_specs: Iterable) -> list:
@@ -1380,10 +1518,38 @@ def normalize_batch(batch_info: Iterable) -> list:
     if all(type(it) is tuple and type(it[1]) is ArraySpec for it in items):
         return items  # already normalized (read_sync -> prepare_read)
     out = []
+    seen: dict = {}  # one coerced spec per caller spec object (a regular grid shares one)
     for it in items:
         it = tuple(it)
-        out.append((it[0], coerce_spec(it[1])) + it[2:])
+        sp = seen.get(id(it[1]))
+        if sp is None:
+            sp = seen[id(it[1])] = coerce_spec(it[1])
+        out.append((it[0], sp) + it[2:])
     return out
+
+
+def _spec_key(spec: ArraySpec) -> tuple:
+    return (spec.shape, spec.dtype.str, spec.fill_bytes(), spec.config)
+
+
+def spec_groups(batch: list) -> list | None:
+    """Item indices grouped by chunk spec (shape, dtype, fill, config), in
+    first-seen order, or None when every item shares the first item's spec.
+    zarr hands a batch one ArraySpec per chunk, and on a rectilinear grid
+    their shapes differ (_get_chunk_spec, src/zarr/core/array.py:5373-5390,
+    5469-5486): each group is planned and launched with its own spec."""
+    s0 = batch[0][1]
+    for it in batch:
+        if it[1] is not s0:
+            break
+    else:
+        return None
+    k0 = _spec_key(s0)
+    groups: dict = {}
+    for i, it in enumerate(batch):
+        sp = it[1]
+        groups.setdefault(k0 if sp is s0 else _spec_key(sp), []).append(i)
+    return None if len(groups) == 1 else list(groups.values())
 
 
 def _selection_items(osel) -> int:
