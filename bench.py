@@ -1229,7 +1229,10 @@ def main():
     if args.tune:
         from zarr_hip import _native as N
 
-        N.lib().zhip_set_tuning(2, args.tune)
+        if not N.tuning_build():
+            raise SystemExit("--tune needs the tuning build (make -C zarr-python_amd tune; "
+                             "ZHIP_LIB=zarr-python_amd/zarr_hip/_lib/libzarrhip_tune.so)")
+        N.check(N.lib().zhip_set_tuning(2, args.tune), "zhip_set_tuning")
     log(f"[bench] building {args.replicas} replicas of the headline batch on {device} "
         f"(rank {ctx.rank} of {ctx.world})")
     plist, decoded, encoded = headline(ctx, args, weak=True)
@@ -1284,7 +1287,10 @@ def main():
                         "launch per GPU), 4 rotating replicas per GPU; at N GPUs the batch is the "
                         "(256N)x256x256 array of 8N shards split round-robin by shard (8 shards "
                         "per rank: weak scaling; the strong split is extra.headline_strong)",
-            "chunks_per_step": 64, "shards_per_step": 8,
+            "chunks_per_step": 64 * ctx.world, "shards_per_step": 8 * ctx.world,
+            "headline_scaling": "weak since round 4: each of the N ranks decodes its own 8 shards "
+                                "(extra.headline_strong splits BASELINE's one 256^3 array 8/N shards "
+                                "per rank, the round-3 definition)",
             "decoded_bytes_per_step": int(ctx.sum(decoded)),
             "encoded_bytes_per_step": int(ctx.sum(encoded)),
             "parallelism": f"shard-partitioned x{ctx.world} (weak, no collective on the data path)",

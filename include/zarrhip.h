@@ -185,12 +185,17 @@ int zhip_plan_kernel_flags(const zhip_plan *plan, uint32_t *flags);
 #define ZHIP_DF_BANK1 16u     /* deferred CRC verdicts (below): this launch publishes
                                  into workspace bank 1 and checks bank 0 (else the
                                  reverse); the caller alternates it per launch */
+#define ZHIP_DF_DEFER 32u     /* opt in to deferred CRC verdicts (below).  Without it
+                                 every decode reports a chunk's CRC mismatch in its own
+                                 launch (d_status + d_errflag), as zhip_decode documents */
 
-/* Deferred CRC verdicts.  k_decode_tileg (the transposing decode of chunks
- * larger than 64 tiles) publishes each
+/* Deferred CRC verdicts (opt-in: ZHIP_DF_DEFER).  With the flag,
+ * k_decode_tileg / k_decode_tilegw (the transposing decodes of chunks
+ * larger than 64 tiles) publish each
  * workgroup's CRC contribution with a NON-returning atomic xor into the
- * chunk's workspace word of the launch's bank (4 words per chunk:
- * {w0, w1, s0, s1}); the chunk's first workgroup also folds in the stored
+ * chunk's workspace word of the launch's bank (4 words per chunk: bank b's
+ * word at 4c + 2b, its stored trailer at 4c + 2b + 1, i.e.
+ * {w0, s0, w1, s1}); the chunk's first workgroup also folds in the stored
  * trailer, so after the launch w_b = computed ^ stored: 0 for a matching
  * chunk, and s_b holds the stored trailer.  The verdict is read, and a
  * nonzero word cleared, by the next launch (its first workgroup per chunk
@@ -300,7 +305,10 @@ int zhip_plan_upload(zhip_plan *plan);
  * for the next call).  *d_errflag gets the OR of (1 << status code) over all
  * chunks whose status is an error (not OK, not MISSING).  `stream` is a
  * hipStream_t (NULL = default stream).  Asynchronous.  With ZHIP_LF_NO_WRITE
- * (shard-index CRC verification, itemsize 1) `out` may be NULL. */
+ * (shard-index CRC verification, itemsize 1) `out` may be NULL.  A CRC
+ * mismatch is in d_status / d_errflag once the launch completes, unless the
+ * caller opts in to deferred verdicts (ZHIP_DF_DEFER: then read them from the
+ * workspace bank words, zhip_dv_check or the next launch). */
 int zhip_decode(const zhip_plan *plan, const void *src, uint64_t src_size, void *out,
                 const zhip_chunk *d_chunks, uint32_t n_chunks, const zhip_sel *d_sels,
                 zhip_status *d_status, uint32_t *d_workspace, uint32_t *d_errflag,
@@ -384,6 +392,11 @@ int zhip_decode_mapped(const zhip_plan *plan, const void *src, uint64_t src_size
 #define ZHIP_TUNE_STAGE_STREAMS 4  /* host staging: packed windows on 1 (default) or 2 copy streams */
 #define ZHIP_TUNE_STAGE_COPY 5     /* host copies into / out of pinned memory: 1 streaming stores (default), 0 memcpy */
 #define ZHIP_TUNE_ARM 6            /* experimental kernel variant for timing arms (0 = production) */
+/* MAX_GRID / ABLATION / BLOCKS / ARM exist in the tuning build only
+ * (libzarrhip_tune.so, -DZHIP_TUNING=1); the shipped library accepts 0 and
+ * returns ZHIP_E_UNSUPPORTED for anything else.  1 when this library is the
+ * tuning build. */
+int zhip_tuning_build(void);
 int zhip_set_tuning(int key, int value);
 
 /* Name of the decode kernel the last zhip_decode* call on this process

@@ -13,6 +13,9 @@ k_decode_il (the default since round 3): 0 start, 1 loads issued, 2 tables
 """
 import json
 import os
+# kernel arms and knobs exist only in the tuning build (make -C zarr-python_amd tune)
+os.environ.setdefault("ZHIP_LIB", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                               "zarr-python_amd", "zarr_hip", "_lib", "libzarrhip_tune.so"))
 import sys
 
 import numpy as np
@@ -65,6 +68,8 @@ def main():
     t = (st & np.uint64(0xFFFFFFFF)).astype(np.int64)
     t0 = t[:, 0].min()
     rel = (t - t0) * 0.01  # 100 MHz -> us
+    if os.environ.get("STAMPS_OUT"):  # every workgroup's stamps and hardware ids, for offline analysis
+        np.savez(os.environ["STAMPS_OUT"], rel=rel, hw=(st[:, 0] >> np.uint64(32)).astype(np.int64))
     names = ["start", "loads_issued", "tables_barrier", "A_stored", "B_stored", "runend_barrier", "V_ready", "exit"]
     if il:  # k_decode_il's slots (TUNE variant)
         names = ["start", "loads_issued", "tables_barrier", "stored_hornered", "V_ready", "-", "-", "exit"]

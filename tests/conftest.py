@@ -12,6 +12,21 @@ for p in (ROOT, PKG_DIR):
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through the HIP C-ABI)")
+    config.addinivalue_line("markers", "tuning: forces a kernel arm (the tuning build, libzarrhip_tune.so; "
+                                       "tests/test_gpu_tuning_build.py runs these there)")
+
+
+def set_tuning(key: int, value: int) -> None:
+    """zhip_set_tuning for a test that forces a kernel arm or ablation: the
+    knobs and the arm kernels exist only in the tuning build, so in the
+    shipped library's process the test skips (test_gpu_tuning_build.py runs
+    the `tuning` tests in a child process on libzarrhip_tune.so).  Setting 0
+    (the production choice) always works."""
+    from zarr_hip import _native as N
+
+    if value and not N.lib().zhip_tuning_build():
+        pytest.skip("kernel arm: tuning build only (tests/test_gpu_tuning_build.py)")
+    N.check(N.lib().zhip_set_tuning(key, value), "zhip_set_tuning")
 
 
 def gpu_available() -> bool:

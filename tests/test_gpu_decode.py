@@ -8,6 +8,7 @@ import numpy as np
 import pytest
 
 from oracle import oracle as O
+from conftest import set_tuning
 
 pytestmark = pytest.mark.gpu
 
@@ -98,6 +99,7 @@ def test_1d_row_decode(device, shape, chunks, dtype, codecs, sel):
     assert prog.tables.rows and prog.tables.layout.ndim == 2
 
 
+@pytest.mark.tuning
 @pytest.mark.parametrize("tune", [64, 65536 | 64, 128, 2097152])
 def test_rows_fallback_kernels(device, tune):
     """Whole-row batches without a row map (zhip_decode_predicted, or a map the
@@ -107,16 +109,17 @@ def test_rows_fallback_kernels(device, tune):
     the kernel chunks of > 32 units take by default).  All stay exact."""
     from zarr_hip import _native as N
 
-    N.lib().zhip_set_tuning(2, tune)
+    set_tuning(2, tune)
     try:
         _roundtrip(device, (128, 128, 128), (64, 64, 64), "float32", [LE, CRC])
         _roundtrip(device, (128, 128, 64), (64, 64, 64), "float32",
                    [SHARD((32, 32, 64), [LE, CRC])])
         _roundtrip(device, (128, 128, 128), (64, 64, 64), "float32", [T((2, 1, 0)), LE, CRC])
     finally:
-        N.lib().zhip_set_tuning(2, 0)
+        set_tuning(2, 0)
 
 
+@pytest.mark.tuning
 @pytest.mark.parametrize("case", ["missing", "partial", "sharded_missing_inner", "odd_units", "big_endian"])
 def test_duo_kernel_cases(device, case):
     """k_decode_duo forced on whole-row layouts it does not take by default
@@ -126,7 +129,7 @@ def test_duo_kernel_cases(device, case):
     with the oracle."""
     from zarr_hip import _native as N
 
-    N.lib().zhip_set_tuning(2, 2097152)
+    set_tuning(2, 2097152)
     try:
         if case == "missing":
             _roundtrip(device, (128, 128, 128), (64, 64, 64), "float32", [LE, CRC], fill=7,
@@ -143,7 +146,7 @@ def test_duo_kernel_cases(device, case):
         else:
             _roundtrip(device, (128, 64, 64), (64, 64, 64), "int16", [BE, CRC])
     finally:
-        N.lib().zhip_set_tuning(2, 0)
+        set_tuning(2, 0)
 
 
 def test_duo_crc_mismatch(device):
@@ -387,6 +390,7 @@ def test_transpose_tile4_no_crc_missing_and_sharded(device, dtype, endian, chunk
     _roundtrip(device, shard, shard, dtype, [SHARD(chunks, [T((2, 1, 0)), endian, CRC])])
 
 
+@pytest.mark.tuning
 def test_transpose_tile4_crc_mismatch(device):
     import zarr_hip
 
@@ -407,16 +411,17 @@ def test_transpose_tile4_crc_mismatch(device):
     assert str(got.value) == str(want.value)
     from zarr_hip import _native as N
 
-    N.lib().zhip_set_tuning(2, -(1 << 31))  # the same mismatch through the k_decode_tile4f arm
+    set_tuning(2, -(1 << 31))  # the same mismatch through the k_decode_tile4f arm
     try:
         with pytest.raises(ValueError) as got_f:
             zarr_hip.Array.create(store, (128, 64, 64), (64, 64, 64), "float32", 0.0, codecs=codecs)[...]
         assert N.lib().zhip_last_kernel() == b"k_decode_tile4f"
     finally:
-        N.lib().zhip_set_tuning(2, 0)
+        set_tuning(2, 0)
     assert str(got_f.value) == str(want.value)
 
 
+@pytest.mark.tuning
 @pytest.mark.parametrize("dtype,endian,chunks,shape", TILE4_CASES)
 def test_transpose_tile4f_chain(device, dtype, endian, chunks, shape):
     """The k_decode_tile4f arm (kTuneTile4F, bit 31: the four tiles of a
@@ -426,13 +431,13 @@ def test_transpose_tile4f_chain(device, dtype, endian, chunks, shape):
 
     _roundtrip(device, shape, chunks, dtype, [T((2, 1, 0)), endian, CRC])
     assert N.lib().zhip_last_kernel() == b"k_decode_tile4w"
-    N.lib().zhip_set_tuning(2, -(1 << 31))
+    set_tuning(2, -(1 << 31))
     try:
         # every case: 256-byte stored rows, one 64-row tile along the transposed dim
         _roundtrip(device, shape, chunks, dtype, [T((2, 1, 0)), endian, CRC])
         assert N.lib().zhip_last_kernel() == b"k_decode_tile4f"
     finally:
-        N.lib().zhip_set_tuning(2, 0)
+        set_tuning(2, 0)
 
 
 def test_tile_mode_engaged(device):
@@ -502,6 +507,7 @@ DEFAULT_SHARD_CASES = [
 ]
 
 
+@pytest.mark.tuning
 @pytest.mark.parametrize("shape,shards,inner,dtype,sel,endian", DEFAULT_SHARD_CASES)
 @pytest.mark.parametrize("loc", ["end", "start"])
 def test_default_sharding_chain_fused(device, shape, shards, inner, dtype, sel, endian, loc):
@@ -531,12 +537,12 @@ def test_default_sharding_chain_fused(device, shape, shards, inner, dtype, sel, 
     want = O.read(host, meta, sel)
     assert got.tobytes() == np.ascontiguousarray(want).tobytes()
     if small:  # ZHIP_TUNE_ARM 11: the pair kernel for the same layout, same bytes
-        N.lib().zhip_set_tuning(6, 11)
+        set_tuning(6, 11)
         try:
             got2 = arr[sel]
             assert N.lib().zhip_last_kernel() == b"k_decode_lead"
         finally:
-            N.lib().zhip_set_tuning(6, 0)
+            set_tuning(6, 0)
         assert got2.tobytes() == got.tobytes()
 
 
@@ -568,6 +574,7 @@ PLAIN_SMALL_CASES = [
 ]
 
 
+@pytest.mark.tuning
 @pytest.mark.parametrize("shape,chunks,dtype,sel,endian", PLAIN_SMALL_CASES)
 def test_plain_small_chunks_lead4(device, shape, chunks, dtype, sel, endian):
     import zarr_hip
@@ -583,21 +590,21 @@ def test_plain_small_chunks_lead4(device, shape, chunks, dtype, sel, endian):
     got = arr[sel]
     _check_small_kernel(int(np.prod(chunks)) * np.dtype(dtype).itemsize)
     assert got.tobytes() == np.ascontiguousarray(O.read(host, meta, sel)).tobytes()
-    N.lib().zhip_set_tuning(6, 11)  # the pair kernel on the same layout
+    set_tuning(6, 11)  # the pair kernel on the same layout
     try:
         got2 = arr[sel]
         assert N.lib().zhip_last_kernel() == b"k_decode_pair"
     finally:
-        N.lib().zhip_set_tuning(6, 0)
+        set_tuning(6, 0)
     assert got2.tobytes() == got.tobytes()
     if int(np.prod(chunks)) * np.dtype(dtype).itemsize <= 8192:  # arms 12 / 13: four / eight per workgroup
         for arm, k in ((12, b"k_decode_lead4"), (13, b"k_decode_lead8")):
-            N.lib().zhip_set_tuning(6, arm)
+            set_tuning(6, arm)
             try:
                 got3 = arr[sel]
                 assert N.lib().zhip_last_kernel() == k
             finally:
-                N.lib().zhip_set_tuning(6, 0)
+                set_tuning(6, 0)
             assert got3.tobytes() == got.tobytes()
 
 
@@ -613,6 +620,7 @@ CRC_SMALL_CASES = [
 ]
 
 
+@pytest.mark.tuning
 @pytest.mark.parametrize("shape,chunks,dtype,sel,codecs,inner", CRC_SMALL_CASES)
 def test_crc_small_chunks_lead4(device, shape, chunks, dtype, sel, codecs, inner):
     import zarr_hip
@@ -634,12 +642,12 @@ def test_crc_small_chunks_lead4(device, shape, chunks, dtype, sel, codecs, inner
     got = arr[sel]
     _check_small_kernel(nb)
     assert got.tobytes() == np.ascontiguousarray(O.read(host, meta, sel)).tobytes()
-    N.lib().zhip_set_tuning(6, 11)  # the pair kernels on the same layout
+    set_tuning(6, 11)  # the pair kernels on the same layout
     try:
         got2 = arr[sel]
         assert N.lib().zhip_last_kernel() not in (b"k_decode_lead4", b"k_decode_lead8")
     finally:
-        N.lib().zhip_set_tuning(6, 0)
+        set_tuning(6, 0)
     assert got2.tobytes() == got.tobytes()
     bad = dict(host)
     b = bytearray(bad[keys[-1]])
@@ -904,9 +912,9 @@ def verdict_case(request):
     from zarr_hip import _native as N
 
     kind, arm = request.param
-    N.lib().zhip_set_tuning(6, arm)
+    set_tuning(6, arm)
     yield kind
-    N.lib().zhip_set_tuning(6, 0)
+    set_tuning(6, 0)
 
 
 def _corrupt(store, host, key, at=4321):
@@ -917,6 +925,7 @@ def _corrupt(store, host, key, at=4321):
     host[key] = bytes(b)
 
 
+@pytest.mark.tuning
 @pytest.mark.parametrize("verdict_case", VERDICT_CASES, indirect=True)
 def test_deferred_verdict_sticky_over_eager_launches(device, verdict_case):
     """Launches without a result check in between: a chunk corrupted before an
@@ -948,6 +957,7 @@ def test_deferred_verdict_sticky_over_eager_launches(device, verdict_case):
     assert out.cpu().numpy().tobytes() == O.read(host, meta).tobytes()
 
 
+@pytest.mark.tuning
 @pytest.mark.parametrize("verdict_case", VERDICT_CASES, indirect=True)
 @pytest.mark.parametrize("repeats", [1, 2, 3])
 def test_deferred_verdict_graph_replays(device, repeats, verdict_case):
@@ -1003,6 +1013,7 @@ def test_deferred_verdict_host_slabs(device):
         assert arr2[...].tobytes() == O.read(host, meta).tobytes()
 
 
+@pytest.mark.tuning
 @pytest.mark.parametrize("arm", [1, 2])
 def test_il_arms_exact_and_crc(device, arm):
     """k_decode_il's timing arms (ZHIP_TUNE_ARM 1: the round-3 publication
@@ -1012,7 +1023,7 @@ def test_il_arms_exact_and_crc(device, arm):
     from zarr_hip import _native as N
 
     arr, store, host, meta = _il_array(device)
-    N.lib().zhip_set_tuning(6, arm)
+    set_tuning(6, arm)
     try:
         prog, out = arr.prepare_read((Ellipsis,))
         prog.launch()
@@ -1032,13 +1043,60 @@ def test_il_arms_exact_and_crc(device, arm):
             prog.results()
         assert out.cpu().numpy().tobytes() == O.read(host, meta).tobytes()
     finally:
-        N.lib().zhip_set_tuning(6, 0)
+        set_tuning(6, 0)
+
+
+@pytest.mark.tuning
+@pytest.mark.parametrize("kind", ["tilegw", "tileg"])
+def test_c_abi_default_reports_mismatch_each_launch(device, kind):
+    """A C caller that does not opt in to deferred verdicts (no ZHIP_DF_DEFER,
+    never ZHIP_DF_BANK1) gets the documented zhip_decode contract from the
+    transposing grouped decodes too: every launch over a corrupted chunk sets
+    its status and the error word itself, two back-to-back launches alike, and
+    the restored bytes then read clean (nothing stale left in a bank word)."""
+    from zarr_hip import _native as N
+
+    arr, store, host, meta = _il_array(device, kind="tileg")
+    set_tuning(6, 5 if kind == "tileg" else 0)
+    try:
+        prog, out = arr.prepare_read((Ellipsis,))
+        d = prog.data
+        d.flags &= ~N.DF_DEFER
+        d._bank = 0
+        prog.launch()
+        prog.results()
+        assert N.lib().zhip_last_kernel().decode() == "k_decode_" + kind
+        _corrupt(store, host, "c/1/0/0")
+        with pytest.raises(ValueError) as want:
+            O.read(host, meta)
+        from zarr_hip.pipeline import STATUS_DT
+
+        for _ in range(2):
+            d._bank = 0  # a C caller that never sets ZHIP_DF_BANK1
+            d.reset_errflag()
+            d.d_status.zero_()
+            d.launch()
+            assert d.errflag() & (1 << N.ST_CRC_MISMATCH)
+            st = d.d_status[: d.n * 4].cpu().numpy().view(STATUS_DT)
+            assert (st["code"] == N.ST_CRC_MISMATCH).sum() == 1
+            with pytest.raises(ValueError) as got:
+                prog.results()
+            assert str(got.value) == str(want.value)
+        _corrupt(store, host, "c/1/0/0")
+        for _ in range(2):
+            d._bank = 0
+            prog.launch()
+            prog.results()
+        assert out.cpu().numpy().tobytes() == O.read(host, meta).tobytes()
+    finally:
+        set_tuning(6, 0)
 
 
 ILQ_ARMS = {20: "k_decode_ilq2", 21: "k_decode_ilq4", 22: "k_decode_ilq1_glds", 23: "k_decode_ilq2_glds",
             24: "k_decode_ilq4_glds"}
 
 
+@pytest.mark.tuning
 @pytest.mark.parametrize("sharded", [False, True])
 @pytest.mark.parametrize("arm", sorted(ILQ_ARMS))
 def test_ilq_arms_exact_and_crc(device, arm, sharded):
@@ -1059,7 +1117,7 @@ def test_ilq_arms_exact_and_crc(device, arm, sharded):
         host.pop("c/1/0/0")
     store = zarr_hip.DeviceStore.from_host(host, device)
     arr = zarr_hip.Array.create(store, shape, cshape, "float32", 1.5, codecs=codecs)
-    N.lib().zhip_set_tuning(6, arm)
+    set_tuning(6, arm)
     try:
         for sel in [(Ellipsis,), (slice(16, 100), slice(0, 128), slice(0, 64))]:
             prog, out = arr.prepare_read(sel)
@@ -1082,9 +1140,10 @@ def test_ilq_arms_exact_and_crc(device, arm, sharded):
             prog.results()
             assert out.cpu().numpy().tobytes() == O.read(host, meta).tobytes()
     finally:
-        N.lib().zhip_set_tuning(6, 0)
+        set_tuning(6, 0)
 
 
+@pytest.mark.tuning
 @pytest.mark.parametrize("arm", [0, 5])
 @pytest.mark.parametrize("dtype,endian,chunks,shape", TILE4_CASES)
 def test_transpose_tile4w_and_tile4(device, dtype, endian, chunks, shape, arm):
@@ -1097,7 +1156,7 @@ def test_transpose_tile4w_and_tile4(device, dtype, endian, chunks, shape, arm):
 
     codecs = [T((2, 1, 0)), endian, CRC]
     kernel = b"k_decode_tile4" if arm else b"k_decode_tile4w"
-    N.lib().zhip_set_tuning(6, arm)
+    set_tuning(6, arm)
     try:
         _roundtrip(device, shape, chunks, dtype, codecs)
         assert N.lib().zhip_last_kernel() == kernel
@@ -1117,9 +1176,10 @@ def test_transpose_tile4w_and_tile4(device, dtype, endian, chunks, shape, arm):
         assert str(got.value) == str(want.value)
         assert N.lib().zhip_last_kernel() == kernel
     finally:
-        N.lib().zhip_set_tuning(6, 0)
+        set_tuning(6, 0)
 
 
+@pytest.mark.tuning
 @pytest.mark.parametrize("arm", [0, 5])
 @pytest.mark.parametrize("order", [(2, 1, 0), (1, 2, 0), (0, 2, 1)])
 @pytest.mark.parametrize("dtype,endian", [("float32", LE), ("int16", BE), ("float64", LE), ("uint8", LE)])
@@ -1134,7 +1194,7 @@ def test_transpose_tilegw_and_tileg(device, order, dtype, endian, arm):
 
     codecs = [T(order), endian, CRC]
     kernel = b"k_decode_tileg" if arm else b"k_decode_tilegw"
-    N.lib().zhip_set_tuning(6, arm)
+    set_tuning(6, arm)
     try:
         _roundtrip(device, (96, 160, 160), (96, 80, 80), dtype, codecs, fill=3, drop=["c/0/1/0"])
         assert N.lib().zhip_last_kernel() == kernel
@@ -1154,4 +1214,4 @@ def test_transpose_tilegw_and_tileg(device, order, dtype, endian, arm):
         assert str(got.value) == str(want.value)
         assert N.lib().zhip_last_kernel() == kernel
     finally:
-        N.lib().zhip_set_tuning(6, 0)
+        set_tuning(6, 0)

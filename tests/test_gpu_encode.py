@@ -7,6 +7,7 @@ import numpy as np
 import pytest
 
 from oracle import oracle as O
+from conftest import set_tuning
 
 pytestmark = pytest.mark.gpu
 
@@ -200,6 +201,7 @@ QUAD_CASES = [
 ]
 
 
+@pytest.mark.tuning
 @pytest.mark.parametrize("arm", [0, 11])
 @pytest.mark.parametrize("shape,chunks,dtype,codecs,fill", QUAD_CASES)
 def test_encode_quad_small_chunks(device, arm, shape, chunks, dtype, codecs, fill):
@@ -211,11 +213,11 @@ def test_encode_quad_small_chunks(device, arm, shape, chunks, dtype, codecs, fil
     w = [((Ellipsis,), d),
          (sub, _data(tuple(s - 3 for s in shape[:-1]) + (shape[-1],), dtype, 4)),   # merges with fill
          (tuple(slice(c, 2 * c) for c in chunks), fill)]                          # a chunk back to fill
-    N.lib().zhip_set_tuning(6, arm)
+    set_tuning(6, arm)
     try:
         _run(device, shape, chunks, dtype, codecs, fill, w)
     finally:
-        N.lib().zhip_set_tuning(6, 0)
+        set_tuning(6, 0)
 
 
 # ---- k_encode_tile4: transposed chunks with full 64-row x 256-byte tiles

@@ -165,3 +165,39 @@ def test_pipeline_devices_crc_error(device, monkeypatch):
     with pytest.raises(ValueError) as got:
         arr[...]
     assert str(got.value) == str(want.value)
+
+
+@pytest.mark.parametrize("sharded", [False, True])
+def test_device_store_decodes_where_its_bytes_are(device, monkeypatch, sharded):
+    """devices=[0, 0] over a DeviceStore on GPU 0: every item decodes on the
+    GPU that holds its bytes (parallel.placement) -- no encoded byte is
+    staged device to device (staging.D2D_COPIES unchanged) -- for a device
+    out on that GPU (the single-device read), a host out (decoded there, one
+    copy back) and a strided selection; all exact against the oracle."""
+    import torch
+
+    import zarr_hip
+    from zarr_hip import staging
+
+    monkeypatch.setenv("ZARR_HIP__DEVICES", "0,0")
+    shape, chunks = (128, 96, 64), (32, 32, 32)
+    shards = (64, 96, 64) if sharded else None
+    codecs = [SHARD(chunks, [LE, CRC])] if sharded else [LE, CRC]
+    meta = O.ArrayMeta(shape, shards or chunks, np.dtype("float32"), 0.0, codecs=codecs)
+    host: dict = {}
+    O.write(host, meta, (Ellipsis,), _data(shape, "float32"))
+    store = zarr_hip.DeviceStore.from_host(host, device)
+    arr = zarr_hip.Array.create(store, shape, shards or chunks, "float32", 0.0, codecs=codecs)
+    assert arr.codec_pipeline.devices == (0, 0)
+    before = staging.D2D_COPIES[0]
+    for sel in [(Ellipsis,), (slice(5, 120, 3), slice(None), slice(7, 60))]:
+        want = np.ascontiguousarray(O.read(host, meta, sel))
+        assert np.asarray(arr[sel]).tobytes() == want.tobytes()
+        batch, out_shape = arr.batch_info(sel)
+        hout = np.full(out_shape, -7.0, np.float32)
+        arr.codec_pipeline.read_sync(batch, hout)
+        assert hout.tobytes() == want.tobytes()
+        dout = torch.empty(out_shape, dtype=torch.float32, device=device)
+        arr.codec_pipeline.read_sync(batch, dout)
+        assert dout.cpu().numpy().tobytes() == want.tobytes()
+    assert staging.D2D_COPIES[0] == before

@@ -59,3 +59,77 @@ def test_devices_config():
     p = HipCodecPipeline.from_codecs([BytesCodec()], devices="0,1")
     assert p.devices == (0, 1)
     assert p.evolve_from_array_spec(__import__("zarr_hip").spec.ArraySpec((4,), np.dtype("f4"), 0.0)).devices == (0, 1)
+
+
+class _FakeArena:
+    def __init__(self, index):
+        import torch
+
+        self.device = torch.device("cuda", index)
+
+
+def _dev_store(index):
+    """A DeviceStore on GPU `index` without touching a GPU (placement only
+    reads the store's device)."""
+    from zarr_hip.store import DeviceStore
+
+    st = DeviceStore.__new__(DeviceStore)
+    st.arena = _FakeArena(index)
+    return st
+
+
+class _Path:
+    def __init__(self, store):
+        self.store = store
+
+
+@pytest.mark.parametrize("out_dev", [0, 1, None])
+def test_placement_single_device_store(out_dev):
+    """Every item of one DeviceStore on GPU 0 decodes on GPU 0, whatever the
+    out's device: no encoded bytes move between GPUs (read_multi then moves
+    only decoded bands)."""
+    from zarr_hip.parallel import placement
+
+    batch, _ = _batch((128, 96), (16, 32), (Ellipsis,))
+    st = _dev_store(0)
+    batch = [(_Path(st),) + it[1:] for it in batch]
+    assert placement(batch, out_dev) == {0: list(range(len(batch)))}
+
+
+def test_placement_mixed_sources():
+    """Items on two GPUs stay where their bytes are; host-resident items go
+    with the out's device (or, for a host out, the device holding most)."""
+    from zarr_hip.parallel import placement
+
+    batch, _ = _batch((128, 96), (16, 32), (Ellipsis,))
+    s0, s3 = _dev_store(0), _dev_store(3)
+    srcs = [s0, s3, None, s3, s3, None] * (len(batch) // 6 + 1)
+    batch = [((_Path(s) if s is not None else _Path(None)),) + it[1:] for s, it in zip(srcs, batch)]
+    by = placement(batch, 0)
+    assert sorted(by) == [0, 3]
+    assert all(srcs[j] is s3 for j in by[3])
+    assert all(srcs[j] is not s3 for j in by[0])
+    by_host = placement(batch, None)
+    assert all(srcs[j] is not s0 for j in by_host[3])  # host items joined GPU 3 (most items)
+    host_only = [(_Path(None),) + it[1:] for it in batch]
+    assert placement(host_only, 0) is None
+
+
+def test_item_bands_exclusive_and_interleaved():
+    """Parts whose items form disjoint bands move one band per run; a part
+    interleaved with another moves item by item (None)."""
+    from zarr_hip.parallel import item_bands
+
+    batch, _ = _batch((128, 96), (16, 32), (Ellipsis,))
+    rows = [it[3][0].start // 16 for it in batch]
+    top = [j for j, r in enumerate(rows) if r < 4]
+    bottom = [j for j, r in enumerate(rows) if r >= 4]
+    assert item_bands(batch, [top, bottom], 0) == [[(0, 64)], [(64, 128)]]
+    even = [j for j, r in enumerate(rows) if r % 2 == 0]
+    odd = [j for j, r in enumerate(rows) if r % 2 == 1]
+    assert item_bands(batch, [even, odd], 0) == [[(0, 16), (32, 48), (64, 80), (96, 112)],
+                                                [(16, 32), (48, 64), (80, 96), (112, 128)]]
+    cols = [it[3][1].start // 32 for it in batch]
+    left = [j for j, c in enumerate(cols) if c == 0]
+    rest = [j for j, c in enumerate(cols) if c > 0]
+    assert item_bands(batch, [left, rest], 0) == [None, None]  # both span every row band

@@ -175,21 +175,35 @@ void fill_geom(Geom& g, const zhip_plan& plan) {
     g.drow = plan.drow;
 }
 
+#if ZHIP_TUNING
 uint32_t g_tune_bits = 0;
 int g_tune_blocks = 0;
 int g_tune_arm = 0;
+#endif
 }
 
 extern "C" {
 
+int zhip_tuning_build(void) { return ZHIP_TUNING; }
+
 int zhip_set_tuning(int key, int value) {
     switch (key) {
+#if ZHIP_TUNING
         case ZHIP_TUNE_MAX_GRID: g_tune_max_grid = value; return ZHIP_OK;
         case ZHIP_TUNE_ABLATION: g_tune_bits = (uint32_t)value; return ZHIP_OK;
         case ZHIP_TUNE_BLOCKS: g_tune_blocks = value; return ZHIP_OK;
+        case ZHIP_TUNE_ARM: g_tune_arm = value; return ZHIP_OK;
+#else
+        case ZHIP_TUNE_MAX_GRID:
+        case ZHIP_TUNE_ABLATION:
+        case ZHIP_TUNE_BLOCKS:
+        case ZHIP_TUNE_ARM:
+            if (value == 0) return ZHIP_OK;  // the production setting
+            return set_err(ZHIP_E_UNSUPPORTED, "kernel tuning knobs exist only in the tuning build "
+                                               "(libzarrhip_tune.so, make tune)");
+#endif
         case ZHIP_TUNE_STAGE_STREAMS: zhip_stage_set_streams(value >= 2 ? 2u : 1u); return ZHIP_OK;
         case ZHIP_TUNE_STAGE_COPY: zhip_stage_set_copy(value ? 1u : 0u); return ZHIP_OK;
-        case ZHIP_TUNE_ARM: g_tune_arm = value; return ZHIP_OK;
         default: return set_err(ZHIP_E_INVALID, "unknown tuning key");
     }
 }
@@ -781,6 +795,7 @@ int zhip_decode_mapped(const zhip_plan* plan, const void* src, uint64_t src_size
     std::memcpy(p.fill, plan->fill, sizeof(p.fill));
     p.fast = (decode_flags & ZHIP_DF_FAST_ROWS) ? 1u : 0u;
     p.dv_bank = (decode_flags & ZHIP_DF_BANK1) ? 1u : 0u;
+    p.defer = (decode_flags & ZHIP_DF_DEFER) ? 1u : 0u;
     p.tune = g_tune_bits;
     p.tq = -1;
     p.rows = 0;

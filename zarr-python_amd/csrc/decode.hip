@@ -39,7 +39,9 @@
 
 namespace zhip {
 
+#if ZHIP_TUNING
 int g_tune_max_grid = 0;
+#endif
 
 // Work assignment: unit "positions" q are numbered chunk-major in INCREASING
 // address order (q = c*nseg + nseg-1-sidx) and every workgroup takes one
@@ -492,6 +494,7 @@ KernelFn select_rows_kernel(bool crc, int item, bool swap, int k);  // decode_ro
 KernelFn select_pair_kernel(bool crc, int item, bool swap, int nu);  // decode_rows.hip
 KernelFn select_duo_kernel(bool crc, int item, bool swap);           // decode_rows.hip
 KernelFn select_il_kernel(bool crc, int item, bool swap);            // decode_rows.hip
+#if ZHIP_TUNING
 KernelFn select_il_kernel_lean(bool crc, int item, bool swap);       // decode_rows.hip
 KernelFn select_il_kernel_tuned(bool crc, int item, bool swap);      // decode_rows.hip
 KernelFn select_il_kernel_arm(bool crc, int item, bool swap, int arm);  // decode_rows.hip
@@ -499,11 +502,12 @@ KernelFn select_il_kernel_cf(bool crc, int item, bool swap);         // decode_r
 KernelFn select_il_kernel_regmul(bool crc, int item, bool swap, bool occ6);  // decode_rows.hip
 KernelFn select_xw_kernel(bool crc, int item, bool swap);            // decode_rows.hip
 KernelFn select_ilq_kernel(int item, bool swap, int nq, bool glds);  // decode_rows.hip
-KernelFn select_tile4_kernel(bool crc, int item, bool swap);         // decode_tile.hip
 KernelFn select_tile4f_kernel(int item, bool swap);                  // decode_tile.hip
+#endif
+KernelFn select_tile4_kernel(bool crc, int item, bool swap);         // decode_tile.hip
 KernelFn select_tile4w_kernel(int item, bool swap);                  // decode_tile.hip
-KernelFn select_tilegw_kernel(int item, bool swap);                  // decode_tile.hip
-KernelFn select_tileg_kernel(bool crc, int item, bool swap);         // decode_tile.hip
+KernelFn select_tilegw_kernel(int item, bool swap, bool defer);      // decode_tile.hip
+KernelFn select_tileg_kernel(bool crc, int item, bool swap, bool defer);  // decode_tile.hip
 
 // name of the kernel the last launch_decode chose (zhip_last_kernel: bench
 // labels and tests; the selection depends on layout, plan and tuning bits)
@@ -511,13 +515,15 @@ static const char* g_last_kernel = "";
 
 int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
     if (g_tune_max_grid > 0) max_grid = g_tune_max_grid;
+    // the ablation bits: a compile-time 0 outside the tuning build
+    const uint32_t tune = ZHIP_TUNING ? p.tune : 0u;
     // (the kTunePersist arm never applies to a launch carrying fused index
     // checks of CRC-free inner chunks: only k_decode_lead carries those)
     const bool lead_launch = !(p.lflags & ZHIP_LF_CRC) && p.n_idx != 0;
     if (p.rows && p.rowmap && p.seg == (uint32_t)kWgStride * kDefaultBlocks &&
-        (!(p.tune & kTunePersist) || lead_launch)) {
+        (!(tune & kTunePersist) || lead_launch)) {
         // one workgroup per pair of units, non-persistent (k_decode_pair)
-        const int nu = (p.tune & kTuneSingle) ? 1 : 2;
+        const int nu = (tune & kTuneSingle) ? 1 : 2;
         const bool crc = (p.lflags & ZHIP_LF_CRC) != 0, swap = (p.lflags & ZHIP_LF_SWAP) != 0;
         if (p.nseg == 1u && p.E <= 4u * kWgStride && g_tune_arm != 11) {
             // chunks of <= 16 KiB (sharded or not, with a CRC or not): four per
@@ -551,7 +557,7 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
             const uint32_t lead = (p.n_idx + 7u) & ~7u;
             if ((uint64_t)pairs + lead > 0x7FFFFFFFull) return ZHIP_E_UNSUPPORTED;
             DecodeParams q = p;
-            q.xcd_run = (!(p.tune & kTuneNoXcd) && pairs % 8u == 0u && pairs <= (uint32_t)(max_grid / 8) * 4u)
+            q.xcd_run = (!(tune & kTuneNoXcd) && pairs % 8u == 0u && pairs <= (uint32_t)(max_grid / 8) * 4u)
                             ? pairs / 8u : 0u;
             q.h.xcd_run = q.xcd_run;
             q.h.d_xcd = make_fdiv(q.xcd_run ? q.xcd_run : 1u);
@@ -563,10 +569,11 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
         // eight workgroups (k_decode_il, see decode_rows.hip) -- graph-timed
         // 26.4 vs 27.8 us on the headline; groups of four lose to the pair
         // kernel at C4 (profiles/r03/il/).  kTuneIl / kTuneNoIl force.
-        const bool il = p.il_S != 0 && crc && !(p.tune & (kTuneNoIl | kTuneSkipCrc | kTuneSingle | kTuneDuo)) &&
-                        ((p.tune & kTuneIl) || p.il_S == 8u);
-        const bool xw = p.xw != 0 && crc && (p.tune & kTuneXw) &&
-                        !(p.tune & (kTuneNoXw | kTuneSkipCrc | kTuneSingle | kTuneDuo | kTuneIl));
+        const bool il = p.il_S != 0 && crc && !(tune & (kTuneNoIl | kTuneSkipCrc | kTuneSingle | kTuneDuo)) &&
+                        ((tune & kTuneIl) || p.il_S == 8u);
+#if ZHIP_TUNING
+        const bool xw = p.xw != 0 && crc && (tune & kTuneXw) &&
+                        !(tune & (kTuneNoXw | kTuneSkipCrc | kTuneSingle | kTuneDuo | kTuneIl));
         if (xw) {
             KernelFn xfn = select_xw_kernel(crc, p.g.itemsize, swap);
             if (!xfn) return ZHIP_E_UNSUPPORTED;
@@ -595,15 +602,20 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
             hipLaunchKernelGGL(qfn, dim3(qgrid), dim3(nq * kThreads), 0, stream, p);
             return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
         }
+#endif
         if (il) {
+#if ZHIP_TUNING
             KernelFn ifn = g_tune_arm ? select_il_kernel_arm(crc, p.g.itemsize, swap, g_tune_arm)
-                           : (p.tune & kTuneCfLookup) ? select_il_kernel_cf(crc, p.g.itemsize, swap)
-                           : (p.tune & kTuneIlLean) ? select_il_kernel_lean(crc, p.g.itemsize, swap)
-                           : (p.tune & (kTuneIlRegMul | kTuneIlOcc6))
-                               ? select_il_kernel_regmul(crc, p.g.itemsize, swap, (p.tune & kTuneIlOcc6) != 0)
-                               : (p.tune & (kTuneNoTables | kTuneNoRunEnd | kTuneNoPub | kTuneStamp))
+                           : (tune & kTuneCfLookup) ? select_il_kernel_cf(crc, p.g.itemsize, swap)
+                           : (tune & kTuneIlLean) ? select_il_kernel_lean(crc, p.g.itemsize, swap)
+                           : (tune & (kTuneIlRegMul | kTuneIlOcc6))
+                               ? select_il_kernel_regmul(crc, p.g.itemsize, swap, (tune & kTuneIlOcc6) != 0)
+                               : (tune & (kTuneNoTables | kTuneNoRunEnd | kTuneNoPub | kTuneStamp))
                                    ? select_il_kernel_tuned(crc, p.g.itemsize, swap)
                                    : select_il_kernel(crc, p.g.itemsize, swap);
+#else
+            KernelFn ifn = select_il_kernel(crc, p.g.itemsize, swap);
+#endif
             if (!ifn) return ZHIP_E_UNSUPPORTED;
             const uint32_t igrid = p.n_units > p.n_idx ? p.n_units : p.n_idx;
             if (igrid == 0) return ZHIP_OK;
@@ -611,21 +623,25 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
             hipLaunchKernelGGL(ifn, dim3(igrid), dim3(kThreads), 0, stream, p);
             return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
         }
+#if ZHIP_TUNING
         KernelFn fn = nu != 2 ? nullptr
-                      : (p.tune & kTuneTrailingCrc) ? select_pair_kernel(crc, p.g.itemsize, swap, 3)
-                      : (p.tune & kTuneSplitChain) ? select_pair_kernel(crc, p.g.itemsize, swap, 4)
-                      : (p.tune & kTuneSkipCrc) ? select_pair_kernel(crc, p.g.itemsize, swap, 5)
-                      : (p.tune & (kTunePrio | kTuneDeferB))
+                      : (tune & kTuneTrailingCrc) ? select_pair_kernel(crc, p.g.itemsize, swap, 3)
+                      : (tune & kTuneSplitChain) ? select_pair_kernel(crc, p.g.itemsize, swap, 4)
+                      : (tune & kTuneSkipCrc) ? select_pair_kernel(crc, p.g.itemsize, swap, 5)
+                      : (tune & (kTunePrio | kTuneDeferB))
                           ? select_pair_kernel(crc, p.g.itemsize, swap,
-                                               (p.tune & kTunePrio) && (p.tune & kTuneDeferB) ? 8
-                                               : (p.tune & kTunePrio) ? 6 : 7)
+                                               (tune & kTunePrio) && (tune & kTuneDeferB) ? 8
+                                               : (tune & kTunePrio) ? 6 : 7)
                           : nullptr;
+#else
+        KernelFn fn = nullptr;
+#endif
         if (!fn) fn = select_pair_kernel(crc, p.g.itemsize, swap, nu);
         if (!fn) return ZHIP_E_UNSUPPORTED;
         // chunks of more than 32 units (> 1 MiB): one unit per 256-thread half of
         // a 512-thread workgroup (k_decode_duo; C1 0.55 -> 0.62 of HBM peak,
         // profiles/r02/kernel_arms_ab.jsonl); kTuneDuo forces it
-        if ((p.tune & kTuneDuo) || (p.nseg > 32 && !(p.tune & (kTuneSingle | kTuneSkipCrc)))) {
+        if ((tune & kTuneDuo) || (p.nseg > 32 && !(tune & (kTuneSingle | kTuneSkipCrc)))) {
             KernelFn dfn = select_duo_kernel(crc, p.g.itemsize, swap);
             if (!dfn) return ZHIP_E_UNSUPPORTED;
             const uint32_t duos = (uint32_t)(((uint64_t)p.n_units + 1u) / 2u);
@@ -641,7 +657,7 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
         // one resident wave of workgroups (4 per CU; max_grid = 8 per CU): the
         // workgroups of one XCD take a contiguous eighth of the batch
         DecodeParams q = p;
-        q.xcd_run = (nu == 2 && !(p.tune & kTuneNoXcd) && grid % 8u == 0u &&
+        q.xcd_run = (nu == 2 && !(tune & kTuneNoXcd) && grid % 8u == 0u &&
                      grid <= (uint32_t)(max_grid / 8) * 4u) ? grid / 8u : 0u;
         q.h.xcd_run = q.xcd_run;
         q.h.d_xcd = make_fdiv(q.xcd_run ? q.xcd_run : 1u);
@@ -669,12 +685,17 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
         // four tiles per workgroup, non-persistent (k_decode_tile4, decode_tile.hip)
         // (arm kTuneTile4F: one A_64 chain per thread when the layout's tile step is
         // 256 B, k_decode_tile4f -- exact, measured 0.3-0.4 us slower on C3)
-        const bool f4 = p.t4f_tab != nullptr && (p.lflags & ZHIP_LF_CRC) != 0;
+        const bool f4 = ZHIP_TUNING && p.t4f_tab != nullptr && (p.lflags & ZHIP_LF_CRC) != 0;
         const bool w4 = !f4 && p.t4w_tab != nullptr && (p.lflags & ZHIP_LF_CRC) != 0;
         const bool swp = (p.lflags & ZHIP_LF_SWAP) != 0;
+#if ZHIP_TUNING
         KernelFn fn = f4 ? select_tile4f_kernel(p.g.itemsize, swp)
                       : w4 ? select_tile4w_kernel(p.g.itemsize, swp)
                            : select_tile4_kernel((p.lflags & ZHIP_LF_CRC) != 0, p.g.itemsize, swp);
+#else
+        KernelFn fn = w4 ? select_tile4w_kernel(p.g.itemsize, swp)
+                         : select_tile4_kernel((p.lflags & ZHIP_LF_CRC) != 0, p.g.itemsize, swp);
+#endif
         if (!fn) return ZHIP_E_UNSUPPORTED;
         if (p.n_units == 0) return ZHIP_OK;
         g_last_kernel = f4 ? "k_decode_tile4f" : w4 ? "k_decode_tile4w" : "k_decode_tile4";
@@ -685,9 +706,11 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
         // tiles grouped by four along a stored dim (k_decode_tileg, decode_tile.hip)
         // (k_decode_tilegw when the plan's wave-per-tile chains are selected)
         const bool gw = p.t4w_tab != nullptr && (p.lflags & ZHIP_LF_CRC) != 0;
-        KernelFn fn = gw ? select_tilegw_kernel(p.g.itemsize, (p.lflags & ZHIP_LF_SWAP) != 0)
+        // (arm 2: the returning publication whatever the flags)
+        const bool defer = p.defer != 0 && g_tune_arm != 2;
+        KernelFn fn = gw ? select_tilegw_kernel(p.g.itemsize, (p.lflags & ZHIP_LF_SWAP) != 0, defer)
                          : select_tileg_kernel((p.lflags & ZHIP_LF_CRC) != 0, p.g.itemsize,
-                                               (p.lflags & ZHIP_LF_SWAP) != 0);
+                                               (p.lflags & ZHIP_LF_SWAP) != 0, defer);
         if (!fn) return ZHIP_E_UNSUPPORTED;
         if (p.n_chunks == 0) return ZHIP_OK;
         if ((uint64_t)p.n_chunks * p.n_groups >= (1ull << 31)) return ZHIP_E_UNSUPPORTED;

@@ -1147,6 +1147,7 @@ KernelFn select_pair_kernel(bool crc, int item, bool swap, int nu) {
             default: return nullptr;
         }
     }
+#if ZHIP_TUNING
     if (nu == 5)  // tuning arm (headline item type only): VARIANT 3, no lookups
         return !(crc && item == 4 && !swap) ? nullptr : k_decode_pair<true, 4, false, 2, 8, 3>;
     if (nu >= 6 && nu <= 8) {  // tuning arms (headline item type only): VARIANT 6 / 7 / 8
@@ -1154,8 +1155,10 @@ KernelFn select_pair_kernel(bool crc, int item, bool swap, int nu) {
         return nu == 6 ? k_decode_pair<true, 4, false, 2, 8, 6>
                : nu == 7 ? k_decode_pair<true, 4, false, 2, 8, 7> : k_decode_pair<true, 4, false, 2, 8, 8>;
     }
-    if (nu == 3 || nu == 4) return nullptr;  // retired arms
-    return nu == 1 ? select_pair_nu<1>(crc, item, swap) : select_pair_nu<2>(crc, item, swap);
+    if (nu == 1) return select_pair_nu<1>(crc, item, swap);  // kTuneSingle
+#endif
+    if (nu != 2) return nullptr;
+    return select_pair_nu<2>(crc, item, swap);
 }
 
 // ---------------------------------------------------------------------------
@@ -1541,6 +1544,7 @@ void k_decode_il(const DecodeParams p) {
         for (uint32_t j = g; j < p.n_idx; j += G) verify_index_pair(p, j, t, kix, s_tab, s_red[1], j == g, ipre);
 }
 
+#if ZHIP_TUNING
 KernelFn select_il_kernel_tuned(bool crc, int item, bool swap) {  // runtime timing arms (p.tune)
     return (crc && item == 4 && !swap) ? k_decode_il<true, 4, false, false, false, 0, true> : nullptr;
 }
@@ -1553,6 +1557,8 @@ KernelFn select_il_kernel_arm(bool crc, int item, bool swap, int arm) {  // ZHIP
         default: return k_decode_il<true, 4, false>;  // arms of other kernels: production
     }
 }
+
+#endif
 
 // Deferred verdicts of whole batches (zhip_dv_check): both banks' words of
 // every chunk of every referenced launch folded into its statuses + errflag
@@ -1579,6 +1585,7 @@ int launch_dv_check(const zhip_dv_ref* d_refs, uint32_t n_refs, hipStream_t stre
     return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
 }
 
+#if ZHIP_TUNING
 KernelFn select_il_kernel_lean(bool crc, int item, bool swap) {  // kTuneIlLean (4-byte LE CRC item type only)
     return (crc && item == 4 && !swap) ? k_decode_il<true, 4, false, true> : nullptr;
 }
@@ -1591,6 +1598,8 @@ KernelFn select_il_kernel_regmul(bool crc, int item, bool swap, bool occ6) {  //
     if (!(crc && item == 4 && !swap)) return nullptr;
     return occ6 ? k_decode_il<true, 4, false, false, false, 2> : k_decode_il<true, 4, false, false, false, 1>;
 }
+
+#endif
 
 KernelFn select_il_kernel(bool crc, int item, bool swap) {
     switch (item) {
@@ -1789,6 +1798,7 @@ void k_decode_ilq(const DecodeParams p) {
     }
 }
 
+#if ZHIP_TUNING
 KernelFn select_ilq_kernel(int item, bool swap, int nq, bool glds) {  // CRC chains only
 #define ZHIP_ILQ(I, W) \
     (nq == 4 ? (glds ? k_decode_ilq<I, W, 4, true> : k_decode_ilq<I, W, 4, false>) \
@@ -1800,6 +1810,7 @@ KernelFn select_ilq_kernel(int item, bool swap, int nq, bool glds) {  // CRC cha
     }
 #undef ZHIP_ILQ
 }
+#endif
 
 // ---------------------------------------------------------------------------
 // k_decode_xw: the whole-row decode with the four waves of a workgroup on four
@@ -1944,6 +1955,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))
         for (uint32_t j = g; j < p.n_idx; j += G) verify_index_pair(p, j, t, kix, s_tab, s_red, j == g, ipre);
 }
 
+#if ZHIP_TUNING
 KernelFn select_xw_kernel(bool crc, int item, bool swap) {
     if (!crc) return nullptr;
     switch (item) {
@@ -1954,6 +1966,7 @@ KernelFn select_xw_kernel(bool crc, int item, bool swap) {
         default: return nullptr;
     }
 }
+#endif
 
 KernelFn select_duo_kernel(bool crc, int item, bool swap) {
     switch (item) {
@@ -1969,10 +1982,12 @@ KernelFn select_duo_kernel(bool crc, int item, bool swap) {
 }
 
 KernelFn select_rows_kernel(bool crc, int item, bool swap, int k) {
+#if ZHIP_TUNING
     if (k == 4) {  // 16 KiB units (tuning arm)
         if (crc && item == 4 && !swap) return k_decode_rows<true, 4, false, 4>;
         return nullptr;
     }
+#endif
     if (k != 8) return nullptr;
     switch (item) {
         case 1: return crc ? k_decode_rows<true, 1, false> : k_decode_rows<false, 1, false>;

@@ -822,7 +822,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
 // take k_decode_tileg.  (Taking the previous tile's Horner steps before the
 // barrier, while one wave writes the image, measured the same in
 // k_decode_tile4w.)
-template <int ITEM, bool SWAP>
+// PUB: 2 = deferred verdicts (ZHIP_DF_DEFER, the Python path's choice), 0 =
+// the returning two-level arrival of k_decode_tileg (the C-ABI default: the
+// launch itself sets the chunk's status and the error word).
+template <int ITEM, bool SWAP, int PUB = 2>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_decode_tilegw(
     const DecodeParams p) {
     constexpr int kPer = 16 / ITEM;
@@ -843,7 +846,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     const uint4 tv0 = gt[t], tv1 = gt[t + kThreads], tv2 = gt[t + 2 * kThreads], tv3 = gt[t + 3 * kThreads],
                 tv4 = gt[t + 4 * kThreads], tv5 = gt[t + 5 * kThreads];
     const uint32_t kq = p.t4w_kq[(size_t)grp * kThreads + t];
-    const uint64_t dvprev = dv_prev(p, c, grp == 0, g_tile_zero);
+    uint64_t dvprev = 0;
+    if constexpr (PUB == 2) dvprev = dv_prev(p, c, grp == 0, g_tile_zero);
     const Unit U = resolve_unit(p, c * p.nseg, expected);
     const GroupEnt ge = load_uniform<GroupEnt>(p.gmap + grp);
     const bool ok = U.mode == ZHIP_ST_OK;
@@ -921,18 +925,47 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
         __syncthreads();  // every out-order read of the last tile is done: s_red reuses the image
         if ((t & 63) == 0) s_red[t >> 6] = v;
         __syncthreads();
-        if (t == 0) dv_publish(p, c, grp == 0, s_red[0] ^ s_red[1] ^ s_red[2] ^ s_red[3], stored);
+        if (t == 0 && PUB == 2) {
+            dv_publish(p, c, grp == 0, s_red[0] ^ s_red[1] ^ s_red[2] ^ s_red[3], stored);
+        } else if (t == 0) {  // the returning arrival of k_decode_tileg (V in the same frame)
+            const uint32_t V = s_red[0] ^ s_red[1] ^ s_red[2] ^ s_red[3];
+            uint32_t raw = 0;
+            bool last_one = false;
+            if (gpc <= 16u || p.n_sub) {
+                bool any_ne;
+                last_one = tileg_arrive(p.ws, p.n_chunks, c, grp, gpc, p.n_sub, V, false, raw, any_ne);
+            } else {  // more than 256 groups per chunk: XOR, then count arrivals
+                uint32_t* accw = p.ws + 4ull * c;
+                const uint32_t prev = __hip_atomic_fetch_xor(accw, V, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                asm volatile("s_waitcnt vmcnt(0)" ::"v"(prev) : "memory");
+                const uint32_t tk = __hip_atomic_fetch_add(accw + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (tk + 1u == gpc) {
+                    raw = __hip_atomic_exchange(accw, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(accw + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    last_one = true;
+                }
+            }
+            if (last_one) {
+                const uint32_t computed = ~(raw ^ p.c3);
+                const uint32_t code = computed == stored ? ZHIP_ST_OK : ZHIP_ST_CRC_MISMATCH;
+                zhip_status st = {code, stored, computed, 0u};
+                p.status[c] = st;
+                if (code != ZHIP_ST_OK) atomicOr(p.errflag, 1u << code);
+            }
+        }
     }
     if (grp == 0 && t == 0) {
         if (ok) {
-            zhip_status st = {ZHIP_ST_OK, 0u, 0u, 0u};
-            p.status[c] = st;
+            if constexpr (PUB == 2) {
+                zhip_status st = {ZHIP_ST_OK, 0u, 0u, 0u};
+                p.status[c] = st;
+            }
         } else {
             zhip_status st = {U.mode, 0u, 0u, 0u};
             p.status[c] = st;
             if (U.mode != ZHIP_ST_MISSING) atomicOr(p.errflag, 1u << U.mode);
         }
-        dv_settle(p, c, dvprev);
+        if constexpr (PUB == 2) dv_settle(p, c, dvprev);
     }
 }
 
@@ -1515,28 +1548,39 @@ EncodeFn select_encode_tile4_kernel(bool crc, int item, bool swap) {
     }
 }
 
-KernelFn select_tileg_kernel(bool crc, int item, bool swap) {
-    if (g_tune_arm == 2 && crc && item == 4 && !swap) return k_decode_tileg<true, 4, false, 0>;  // returning arm
+// defer: ZHIP_DF_DEFER (deferred CRC verdicts, PUB 2); otherwise the returning
+// publication (PUB 0), whose launch reports a mismatch itself
+KernelFn select_tileg_kernel(bool crc, int item, bool swap, bool defer) {
+    if (!crc) {
+        switch (item) {
+            case 1: return k_decode_tileg<false, 1, false>;
+            case 2: return swap ? k_decode_tileg<false, 2, true> : k_decode_tileg<false, 2, false>;
+            case 4: return swap ? k_decode_tileg<false, 4, true> : k_decode_tileg<false, 4, false>;
+            case 8: return swap ? k_decode_tileg<false, 8, true> : k_decode_tileg<false, 8, false>;
+            default: return nullptr;
+        }
+    }
+#define ZHIP_TILEG(I, W) (defer ? k_decode_tileg<true, I, W, 2> : k_decode_tileg<true, I, W, 0>)
     switch (item) {
-        case 1: return crc ? k_decode_tileg<true, 1, false> : k_decode_tileg<false, 1, false>;
-        case 2: return crc ? (swap ? k_decode_tileg<true, 2, true> : k_decode_tileg<true, 2, false>)
-                           : (swap ? k_decode_tileg<false, 2, true> : k_decode_tileg<false, 2, false>);
-        case 4: return crc ? (swap ? k_decode_tileg<true, 4, true> : k_decode_tileg<true, 4, false>)
-                           : (swap ? k_decode_tileg<false, 4, true> : k_decode_tileg<false, 4, false>);
-        case 8: return crc ? (swap ? k_decode_tileg<true, 8, true> : k_decode_tileg<true, 8, false>)
-                           : (swap ? k_decode_tileg<false, 8, true> : k_decode_tileg<false, 8, false>);
+        case 1: return ZHIP_TILEG(1, false);
+        case 2: return swap ? ZHIP_TILEG(2, true) : ZHIP_TILEG(2, false);
+        case 4: return swap ? ZHIP_TILEG(4, true) : ZHIP_TILEG(4, false);
+        case 8: return swap ? ZHIP_TILEG(8, true) : ZHIP_TILEG(8, false);
         default: return nullptr;
     }
+#undef ZHIP_TILEG
 }
 
-KernelFn select_tilegw_kernel(int item, bool swap) {  // CRC chains only
+KernelFn select_tilegw_kernel(int item, bool swap, bool defer) {  // CRC chains only
+#define ZHIP_TILEGW(I, W) (defer ? k_decode_tilegw<I, W, 2> : k_decode_tilegw<I, W, 0>)
     switch (item) {
-        case 1: return k_decode_tilegw<1, false>;
-        case 2: return swap ? k_decode_tilegw<2, true> : k_decode_tilegw<2, false>;
-        case 4: return swap ? k_decode_tilegw<4, true> : k_decode_tilegw<4, false>;
-        case 8: return swap ? k_decode_tilegw<8, true> : k_decode_tilegw<8, false>;
+        case 1: return ZHIP_TILEGW(1, false);
+        case 2: return swap ? ZHIP_TILEGW(2, true) : ZHIP_TILEGW(2, false);
+        case 4: return swap ? ZHIP_TILEGW(4, true) : ZHIP_TILEGW(4, false);
+        case 8: return swap ? ZHIP_TILEGW(8, true) : ZHIP_TILEGW(8, false);
         default: return nullptr;
     }
+#undef ZHIP_TILEGW
 }
 
 KernelFn select_tile4w_kernel(int item, bool swap) {  // CRC chains only
@@ -1549,6 +1593,7 @@ KernelFn select_tile4w_kernel(int item, bool swap) {  // CRC chains only
     }
 }
 
+#if ZHIP_TUNING
 KernelFn select_tile4f_kernel(int item, bool swap) {  // CRC chains only
     switch (item) {
         case 1: return k_decode_tile4f<1, false>;
@@ -1558,10 +1603,13 @@ KernelFn select_tile4f_kernel(int item, bool swap) {  // CRC chains only
         default: return nullptr;
     }
 }
+#endif
 
 KernelFn select_tile4_kernel(bool crc, int item, bool swap) {
+#if ZHIP_TUNING
     if (g_tune_arm == 1 && crc && item == 4 && !swap) return k_decode_tile4<true, 4, false, 0>;  // words 16 B apart
     if (g_tune_arm == 2 && crc && item == 4 && !swap) return k_decode_tile4<true, 4, false, 2>;  // deferred arm
+#endif
     switch (item) {
         case 1: return crc ? k_decode_tile4<true, 1, false> : k_decode_tile4<false, 1, false>;
         case 2: return crc ? (swap ? k_decode_tile4<true, 2, true> : k_decode_tile4<true, 2, false>)

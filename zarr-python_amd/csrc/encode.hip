@@ -614,7 +614,9 @@ static EncodeFn pick_encode(int item, bool swap) {
 }
 
 static EncodeFn pick_encode_pair(bool crc, int item, bool swap) {
+#if ZHIP_TUNING
     if (g_tune_arm == 1 && crc && item == 4 && !swap) return k_encode_pair<true, 4, false, true>;  // 11/11/10 tables
+#endif
     switch (item) {
         case 1: return crc ? k_encode_pair<true, 1, false> : k_encode_pair<false, 1, false>;
         case 2: return crc ? (swap ? k_encode_pair<true, 2, true> : k_encode_pair<true, 2, false>)

@@ -143,6 +143,7 @@ struct DecodeParams {
     const uint32_t* il_klane;
     const uint32_t* il_kidx;
     uint32_t dv_bank;  // deferred CRC verdicts: bank this launch publishes into (ZHIP_DF_BANK1)
+    uint32_t defer;    // ZHIP_DF_DEFER: the caller reads deferred verdicts (tileg / tilegw publish so)
     // k_decode_xw: 8 KiB spans per chunk (0: not available), arrival subwords
     // per chunk in the workspace tail (0: one level or xor + count), its A_1024
     // tables, lane constants per (span, lane) and for the fused index check
@@ -235,14 +236,29 @@ constexpr uint32_t kTuneCfLookup = 131072u;  // k_decode_il timing arm: conflict
 constexpr uint32_t kTuneStamp = 1024u;    // k_decode_pair: per-workgroup phase timestamps (zhip_debug_stamps)
 constexpr uint32_t kStampWG = 8192u;      // workgroups stamped per launch
 constexpr uint32_t kStampSlots = 8u;
-extern int g_tune_max_grid;
 }  // namespace zhip
 extern "C" void zhip_stage_set_streams(uint32_t n);  // staging.cpp (ZHIP_TUNE_STAGE_STREAMS)
 extern "C" void zhip_stage_set_copy(uint32_t nt);     // staging.cpp (ZHIP_TUNE_STAGE_COPY)
 namespace zhip {
+// The kernel knobs (zhip_set_tuning ZHIP_TUNE_MAX_GRID / ABLATION / BLOCKS /
+// ARM) and every measurement-arm kernel exist only in the tuning build
+// (make tune -> libzarrhip_tune.so, -DZHIP_TUNING=1; scripts/armbench.py).
+// The shipped library has them as compile-time zeros: no arm is compiled in
+// and no variable of a user's environment can change a launch.
+#ifndef ZHIP_TUNING
+#define ZHIP_TUNING 0
+#endif
+#if ZHIP_TUNING
+extern int g_tune_max_grid;
 extern int g_tune_blocks;
 extern uint32_t g_tune_bits;
 extern int g_tune_arm;  // ZHIP_TUNE_ARM: experimental kernel variant (0 = production)
+#else
+constexpr int g_tune_max_grid = 0;
+constexpr int g_tune_blocks = 0;
+constexpr uint32_t g_tune_bits = 0;
+constexpr int g_tune_arm = 0;
+#endif
 
 struct EncodeParams {
     const uint8_t* arr;   // source array base (device)

@@ -39,6 +39,7 @@ DF_TILE = 2
 DF_ROWS = 4
 DF_TILE_PREFIX = 8
 DF_BANK1 = 16  # deferred CRC verdicts: publish into workspace bank 1, check bank 0
+DF_DEFER = 32  # opt in to deferred CRC verdicts (the Python path reads the verdict words)
 
 PK_TILE4 = 1
 PK_TILE4_ENCODE = 2
@@ -51,8 +52,13 @@ PF_INDEX_CRC = 2
 PF_KEEP_EMPTY = 4
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# ZHIP_LIB: an alternative build of the same library (measurement variants)
-LIB_PATH = os.environ.get("ZHIP_LIB") or os.path.join(_HERE, "_lib", "libzarrhip.so")
+# the shipped library, and the tuning build of the same sources with every
+# measurement arm and kernel knob compiled in (make -C zarr-python_amd tune;
+# scripts/armbench.py, tests/test_gpu_tuning_build.py).  ZHIP_LIB names the
+# library to load explicitly (the tuning build for measurements).
+PRODUCT_LIB_PATH = os.path.join(_HERE, "_lib", "libzarrhip.so")
+TUNING_LIB_PATH = os.path.join(_HERE, "_lib", "libzarrhip_tune.so")
+LIB_PATH = os.environ.get("ZHIP_LIB") or PRODUCT_LIB_PATH
 
 
 class FDiv(ctypes.Structure):
@@ -256,14 +262,16 @@ def lib():
     L.zhip_emulate_chunk_crc_xw.restype = ctypes.c_uint32
     L.zhip_fdiv_eval.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
     L.zhip_fdiv_eval.restype = ctypes.c_uint32
+    L.zhip_tuning_build.restype = ctypes.c_int
     if L.zhip_abi_version() != 1:
         raise NativeError("libzarrhip ABI version mismatch")
-    # ZHIP_TUNE: kernel-variant bits for measurement runs (0 = production)
-    tune = int(os.environ.get("ZHIP_TUNE", "0") or 0)
-    if tune:
-        L.zhip_set_tuning(2, tune)
     _lib = L
     return L
+
+
+def tuning_build() -> bool:
+    """True when the loaded library is the tuning build (arms, knobs)."""
+    return bool(lib().zhip_tuning_build())
 
 
 def check(rc: int, what: str) -> None:

@@ -175,17 +175,33 @@ class GroupProgram:
 
     def gather(self, batch_info, into) -> None:
         """Copy every device's item regions into ``into`` (any device): the
-        optional post-step gather, outside the decode."""
+        optional post-step gather, outside the decode.  A device whose items
+        form bands of the out along its outermost dim that no other device's
+        items touch sends each band in ONE copy (a contiguous range of a C or
+        F out: one peer copy over xGMI); interleaved items go one region each.
+        The copies run asynchronously on the receiving device's stream and
+        are waited for once."""
+        import torch
+
         from .pipeline import normalize_batch
 
         batch = normalize_batch(batch_info)
         self.synchronize()
-        for prog, out, idx in self.parts:
-            for j in idx:
-                osel = tuple(batch[j][3])
+        dim = outer_dim(into.stride(), tuple(into.shape))
+        owner = item_bands(batch, [idx for _, _, idx in self.parts], dim)
+        stream = torch.cuda.current_stream(into.device)
+        with torch.cuda.stream(stream):
+            for (prog, out, idx), spans in zip(self.parts, owner):
                 if out.device == into.device and out.data_ptr() == into.data_ptr():
                     continue
-                into[osel].copy_(out[osel], non_blocking=False)
+                if spans is not None:
+                    for lo, hi in spans:
+                        into.narrow(dim, lo, hi - lo).copy_(out.narrow(dim, lo, hi - lo), non_blocking=True)
+                else:
+                    for j in idx:
+                        osel = tuple(batch[j][3])
+                        into[osel].copy_(out[osel], non_blocking=True)
+        stream.synchronize()
 
 
 # ------------------------------------------- a pipeline over several devices
@@ -225,6 +241,144 @@ def device_bands(batch: list, n_dev: int, dim: int):
     if cur:
         groups.append(cur)
     return [(g[0][0], g[-1][1], [j for k in g for j in bands[k]]) for g in groups]
+
+
+def item_bands(batch: list, parts: list, dim: int) -> list:
+    """Per part (a list of item indices): its items' maximal runs of touching
+    bands [lo, hi) along ``dim`` -- or None for a part whose items are not
+    unit-step slices there or whose runs overlap another part's items (then
+    its regions move one item at a time)."""
+    spans_of = []
+    for idx in parts:
+        iv = []
+        for j in idx:
+            osel = tuple(batch[j][3])
+            s = osel[dim] if dim < len(osel) else None
+            if not isinstance(s, slice) or (s.step or 1) != 1:
+                iv = None
+                break
+            iv.append((int(s.start or 0), int(s.stop)))
+        if iv is None:
+            spans_of.append(None)
+            continue
+        iv.sort()
+        runs: list = []
+        for a, b in iv:
+            if runs and a <= runs[-1][1]:
+                runs[-1][1] = max(runs[-1][1], b)
+            else:
+                runs.append([a, b])
+        spans_of.append([tuple(r) for r in runs])
+    out = []
+    for i, sp in enumerate(spans_of):
+        if sp is None:
+            out.append(None)
+            continue
+        clash = False
+        for k, other in enumerate(spans_of):
+            if k == i:
+                continue
+            if other is None:
+                clash = True  # unknown extents elsewhere: stay per item
+                break
+            for a, b in sp:
+                if any(a < d and c < b for c, d in other):
+                    clash = True
+                    break
+            if clash:
+                break
+        out.append(None if clash else sp)
+    return out
+
+
+def item_device(it) -> int | None:
+    """The GPU whose HBM already holds an item's encoded bytes (a path into a
+    DeviceStore, a getter over a DeviceRef), None for host-resident bytes."""
+    from .store import DeviceRef, DeviceStore
+
+    bg = it[0]
+    st = getattr(bg, "store", None)
+    if isinstance(st, DeviceStore):
+        return int(st.device.index or 0)
+    v = getattr(bg, "value", None)
+    if isinstance(v, DeviceRef):
+        return int(v.arena.device.index or 0)
+    return None
+
+
+def placement(batch: list, out_device: int | None) -> dict | None:
+    """Where each item decodes when some of the batch's bytes are already in
+    HBM: every device-resident item on the GPU that holds it (decoding there
+    moves no encoded bytes between GPUs), host-resident items with the out's
+    device (or the device holding most items).  {device: [item indices]}, or
+    None when every item's bytes are in host memory (then the batch splits
+    into bands over all the pipeline's devices)."""
+    locs = [item_device(it) for it in batch]
+    held = [d for d in locs if d is not None]
+    if not held:
+        return None
+    if out_device is not None and out_device in held:
+        home = out_device
+    else:
+        home = max(set(held), key=held.count)
+    by_dev: dict = {}
+    for j, d in enumerate(locs):
+        by_dev.setdefault(home if d is None else d, []).append(j)
+    return by_dev
+
+
+def _read_placed(sub, batch: list, by_dev: dict, t, h, dim: int) -> tuple:
+    """read_multi for device-resident items: each device decodes the items
+    whose bytes it holds -- into the out itself when the out lives there,
+    else into a slab over its items' band of the out (one copy back when no
+    other device's items touch the band, else one copy per item region)."""
+    import numpy as np
+    import torch
+
+    results: list = [None] * len(batch)
+    devs = list(by_dev)
+    spans = dict(zip(devs, item_bands(batch, [by_dev[d] for d in devs], dim)))
+    shape = tuple(t.shape) if t is not None else h.shape
+
+    def job(d):
+        idx = by_dev[d]
+        items = [batch[j] for j in idx]
+        if t is not None and t.device.index == d:
+            res = sub.read_sync(items, t)
+        else:
+            sp = spans[d]
+            lo, hi = (sp[0][0], sp[-1][1]) if sp else (0, shape[dim])
+            if t is not None:
+                target = t.narrow(dim, lo, hi - lo)
+                slab = _dense_like(target, torch.device("cuda", d))
+            else:
+                target = torch.from_numpy(np.moveaxis(np.moveaxis(h, dim, 0)[lo:hi], 0, dim))
+                slab = torch.empty(tuple(target.shape), dtype=target.dtype, device=torch.device("cuda", d))
+            shifted = [_shift(it, dim, lo) for it in items] if sp else items
+            whole = sp is not None and len(sp) == 1
+            if whole and sum(_cells(it[3]) for it in items) < slab.numel():
+                slab.copy_(target)  # regions no item writes keep their values
+            res = sub.read_sync(shifted, slab)
+            if whole:
+                target.copy_(slab)  # one peer copy (device out) / D2H (host out) of the band
+            else:
+                for it in shifted:
+                    osel = tuple(it[3])
+                    target[osel].copy_(slab[osel])
+            torch.cuda.current_stream(torch.device("cuda", d)).synchronize()
+        for j, r in zip(idx, res):
+            results[j] = r
+
+    _run_on_devices(sub, [(d, (lambda d=d: job(d))) for d in devs])
+    return tuple(results)
+
+
+def _cells(osel) -> int:
+    n = 1
+    for s in osel:
+        if isinstance(s, slice):
+            n *= max(0, -((int(s.start or 0) - int(s.stop)) // (s.step or 1)))
+    return n
 
 
 def _dense_like(band, device):
@@ -281,8 +435,11 @@ def _run_on_devices(pipe, jobs):
 
 
 def read_multi(pipe, batch: list, out, drop_axes: tuple):
-    """HipCodecPipeline.read_sync with ``devices``: the batch's items are
-    split into bands of the out along its outermost dim (the reference's
+    """HipCodecPipeline.read_sync with ``devices``.  Items whose bytes already
+    sit in a GPU's HBM (a DeviceStore) decode on that GPU (``placement``):
+    only decoded bands move, never encoded bytes -- a store on one GPU with
+    the out on the same GPU is the single-device read.  Host-resident items
+    are split into bands of the out along its outermost dim (the reference's
     disjoint-output pool map, codec_pipeline.py:1104-1109, 1169-1171, with a
     GPU per worker); every device decodes its band into a compact slab of its
     own -- the out's own band when the out lives on that device, else a slab
@@ -304,6 +461,12 @@ def read_multi(pipe, batch: list, out, drop_axes: tuple):
     shape = tuple(t.shape) if t is not None else h.shape
     strides = tuple(t.stride()) if t is not None else tuple(x // h.itemsize for x in h.strides)
     dim = outer_dim(strides, shape)
+    # bytes already in HBM decode where they are (no encoded bytes between GPUs)
+    by_dev = placement(batch, t.device.index if t is not None else None)
+    if by_dev is not None:
+        if len(by_dev) == 1 and t is not None and t.device.index in by_dev:
+            return None  # one device holds the bytes and the out: the single-device read
+        return _read_placed(_device_pipes(pipe), batch, by_dev, t, h, dim)
     groups = device_bands(batch, len(pipe.devices), dim)
     if groups is None or len(groups) < 2:
         return None

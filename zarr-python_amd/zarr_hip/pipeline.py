@@ -214,8 +214,10 @@ class DecodeLaunch:
         self.src = src
         self.src_size = src_size
         self.out = out
+        # (DF_DEFER: this path reads the deferred CRC verdict words back with the
+        # error word, results_fast / merge_verdicts, and alternates the banks)
         self.flags = (N.DF_FAST_ROWS if fast else 0) | (N.DF_TILE if tile else 0) | \
-            (N.DF_ROWS if fast and rows else 0)
+            (N.DF_ROWS if fast and rows else 0) | N.DF_DEFER
         self.predict = predict if (fast and rows) else None
         # row map (zhip_rows_map): per (selection, unit, step) destinations for the
         # two-unit row decode; None when the layout does not admit one

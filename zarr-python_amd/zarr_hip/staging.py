@@ -275,6 +275,12 @@ class PendingGroup:
             p.abort()
 
 
+# encoded bytes copied device to device by gather_sources (another GPU's
+# arena): parallel.read_multi decodes device-resident items where they live,
+# and the tests check that it then stages nothing
+D2D_COPIES = [0]
+
+
 def gather_sources(batch: list, device, defer: bool = False, start: bool = True):
     """Resolve every ByteGetter to (offset, length, missing) inside ONE device
     buffer: the shared arena for DeviceStore batches, else a staged copy.
@@ -334,6 +340,7 @@ def gather_sources(batch: list, device, defer: bool = False, start: bool = True)
         for r, off in dev_refs:
             v = r.arena.view(r.offset, r.length) if isinstance(r, DeviceRef) else r
             dev[off: off + v.numel()].copy_(v)
+            D2D_COPIES[0] += 1
 
     if not start:
         return None, lay.top, srcs, [], lambda: stage(lay, device, post=[d2d] if dev_refs else [], defer=True)
