@@ -394,3 +394,42 @@ extern "C" int cb_scatter_geo(const void* src, void* dst, uint64_t cstride, int 
     hipLaunchKernelGGL(fn, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const uint8_t*)src, (uint8_t*)dst, g);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
+
+// Wide workgroups: `threads` (256 / 512 / 1024) lanes per 32 KiB span, K =
+// 8 * 256 / threads blocks per lane (the small-share geometry: one span per
+// workgroup, lane t's blocks at 16 t + k * 16 * threads).
+template <int K>
+__global__ __launch_bounds__(1024) void k_copy_wide(const uint4* __restrict__ src, uint4* __restrict__ dst) {
+    const uint32_t nt = blockDim.x;
+    const uint64_t b0 = (uint64_t)blockIdx.x * 2048ull + threadIdx.x;
+    uint4 v[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const v4u w = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(src) + b0 + (uint64_t)nt * k);
+        v[k] = make_uint4(w.x, w.y, w.z, w.w);
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        v4u w = {v[k].x, v[k].y, v[k].z, v[k].w};
+        __builtin_nontemporal_store(w, reinterpret_cast<v4u*>(dst) + b0 + (uint64_t)nt * k);
+    }
+}
+
+__global__ void k_empty(int* x) {
+    if (x && threadIdx.x == 1024) x[0] = 1;
+}
+
+extern "C" int cb_copy_wide(const void* src, void* dst, uint64_t nbytes, int threads, void* stream) {
+    typedef void (*WFn)(const uint4*, uint4*);
+    WFn fn = threads == 256 ? (WFn)k_copy_wide<8> : threads == 512 ? (WFn)k_copy_wide<4>
+           : threads == 1024 ? (WFn)k_copy_wide<2> : nullptr;
+    if (!fn || nbytes % 32768) return -1;
+    hipLaunchKernelGGL(fn, dim3((uint32_t)(nbytes / 32768)), dim3(threads), 0, (hipStream_t)stream,
+                       (const uint4*)src, (uint4*)dst);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+extern "C" int cb_empty(uint32_t grid, int threads, void* stream) {
+    hipLaunchKernelGGL(k_empty, dim3(grid), dim3(threads), 0, (hipStream_t)stream, (int*)nullptr);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}

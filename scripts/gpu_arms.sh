@@ -5,7 +5,8 @@
 #   CONFIGS   scripts/armbench.py configs (headline share8 share4 c3 c3g c4),
 #             each with ARMS = "name=ablation_bits:ZHIP_TUNE_ARM,..."
 #   ENC_ARMS  scripts/encbench.py arms ("c2:0,c2:1,c3_64:0,...")
-#   STAMPS    optional WORLD values for scripts/stamps.py (tuning build; "1 8")
+#   STAMPS    optional WORLD values for scripts/stamps.py (tuning build; "1 8"),
+#             for each kernel arm of STAMP_ARMS (default "0")
 #   PROF      "1": scripts/prof_uncached.py (SEL full / bench) and
 #             scripts/prof_c5host.py
 #   OUT       output directory under gpurun_out/ (default gpurun_out/arms_run)
@@ -21,12 +22,12 @@ if [ -n "${TESTS:-}" ]; then
   rc=$?; echo "pytest rc=$rc"; tail -1 "$O/pytest.log"
   [ $rc -ne 0 ] && exit $rc
 fi
-for w in ${STAMPS:-}; do  # per-workgroup phase stamps of the headline (WORLD=w: rank 0's share)
-  WORLD=$w TUNE=${STAMP_TUNE:-0} STAMPS_OUT="$O/stamps_w$w.npz" timeout -k 10 300 python scripts/stamps.py \
-    > "$O/stamps_w$w.jsonl" 2> "$O/stamps_w$w.err"
-  rc=$?; echo "stamps w=$w rc=$rc"; cat "$O/stamps_w$w.jsonl"
-  [ $rc -ne 0 ] && { tail -5 "$O/stamps_w$w.err"; exit $rc; }
-done
+for a in ${STAMP_ARMS:-0}; do for w in ${STAMPS:-}; do  # per-workgroup phase stamps (WORLD=w: rank 0's share; ARM=a)
+  WORLD=$w TUNE=${STAMP_TUNE:-0} ARM=$a STAMPS_OUT="$O/stamps_w${w}_a$a.npz" timeout -k 10 300 python scripts/stamps.py \
+    > "$O/stamps_w${w}_a$a.jsonl" 2> "$O/stamps_w${w}_a$a.err"
+  rc=$?; echo "stamps w=$w arm=$a rc=$rc"; cat "$O/stamps_w${w}_a$a.jsonl"
+  [ $rc -ne 0 ] && { tail -5 "$O/stamps_w${w}_a$a.err"; exit $rc; }
+done; done
 for cfg in ${CONFIGS:-}; do
   CONFIG=$cfg ARMS="${ARMS:-prod=0:0}" timeout -k 10 300 python scripts/armbench.py > "$O/arms_$cfg.jsonl" 2> "$O/arms_$cfg.err"
   rc=$?; echo "arms $cfg rc=$rc"; cat "$O/arms_$cfg.jsonl"

@@ -53,13 +53,15 @@ def main():
             progs.append(arr.codec_pipeline.prepare_read(parallel.rank_batch(batch, world, 0), out))
     sh = int(torch.cuda.current_stream(dev).cuda_stream)
     N.lib().zhip_set_tuning(2, 1024 | tune)
+    N.lib().zhip_set_tuning(6, int(os.environ.get("ARM", "0")))  # a kernel arm (k_decode_ilw: 26 / 27)
     for i in range(8):
         progs[i % 4].launch(sh)
     torch.cuda.synchronize(dev)
     N.lib().zhip_set_tuning(2, 0)
+    N.lib().zhip_set_tuning(6, 0)
     for p in progs:
         p.results()
-    il = N.lib().zhip_last_kernel().decode() == "k_decode_il"
+    il = N.lib().zhip_last_kernel().decode().startswith("k_decode_il")
     n_wg = (2048 if (tune & 128 or il) else 1024) // world
     buf = np.zeros(n_wg * 8, np.uint64)
     N.check(N.lib().zhip_debug_stamps(buf.ctypes.data, n_wg), "zhip_debug_stamps")

@@ -1144,6 +1144,120 @@ def test_ilq_arms_exact_and_crc(device, arm, sharded):
 
 
 @pytest.mark.tuning
+@pytest.mark.parametrize("loc", ["end", "start"])
+@pytest.mark.parametrize("sharded", [False, True])
+def test_ilc_arm_exact_and_crc(device, monkeypatch, sharded, loc):
+    """k_decode_ilc (ZHIP_TUNE_ARM 25: CRC tables computed in LDS from 64 basis
+    words, predicted loads issued before the index resolves) decodes exactly,
+    reloads when the prediction misses (misaligned repacked shards), and
+    reports corrupted chunks and indexes with the reference's messages."""
+    import zarr_hip
+    import zarr_hip.pipeline as P
+    from zarr_hip import _native as N
+
+    monkeypatch.setattr(P, "IL_PREDICT", True)
+    shape, chunks = (128, 128, 64), (64, 64, 64)
+    codecs = [SHARD((64, 64, 64), [LE, CRC], loc)] if sharded else [LE, CRC]
+    cshape = (128, 128, 64) if sharded else chunks
+    meta = O.ArrayMeta(shape, cshape, np.dtype("float32"), 1.5, codecs=codecs)
+    host = {}
+    O.write(host, meta, (Ellipsis,), _data(shape, "float32"))
+    if not sharded:
+        host.pop("c/1/0/0")
+    set_tuning(6, 25)
+    try:
+        store = zarr_hip.DeviceStore.from_host(host, device)
+        arr = zarr_hip.Array.create(store, shape, cshape, "float32", 1.5, codecs=codecs)
+        for sel in [(Ellipsis,), (slice(16, 100), slice(0, 128), slice(0, 64))]:
+            prog, out = arr.prepare_read(sel)
+            prog.launch()
+            prog.results()
+            assert N.lib().zhip_last_kernel().decode() == "k_decode_ilc"
+            assert out.cpu().numpy().tobytes() == np.ascontiguousarray(O.read(host, meta, sel)).tobytes()
+        key = "c/0/0/0" if sharded else "c/0/1/0"
+        for at in ([700001, len(host[key]) - 40 if loc == "end" else 20] if sharded else [700001]):
+            _corrupt(store, host, key, at=at)
+            with pytest.raises(ValueError) as want:
+                O.read(host, meta)
+            prog, out = arr.prepare_read((Ellipsis,))
+            prog.launch()
+            with pytest.raises(ValueError) as got:
+                prog.results()
+            assert str(got.value) == str(want.value)
+            _corrupt(store, host, key, at=at)
+            prog.launch()
+            prog.results()
+            assert out.cpu().numpy().tobytes() == O.read(host, meta).tobytes()
+        if sharded:  # prediction wrong for every inner chunk: the kernel reloads
+            mhost = dict(host)
+            for k in list(mhost):
+                if k.startswith("c/"):
+                    mhost[k] = _repack_misaligned(mhost[k], meta.chain.shard, (2, 2, 1))
+            marr = zarr_hip.Array.create(zarr_hip.DeviceStore.from_host(mhost, device), shape, cshape, "float32",
+                                         1.5, codecs=codecs)
+            got = marr[...]
+            assert N.lib().zhip_last_kernel().decode() == "k_decode_ilc"
+            assert got.tobytes() == O.read(host, meta).tobytes()
+    finally:
+        set_tuning(6, 0)
+
+
+ILW_CASES = [  # (shape, chunks, inner chunks or None, dtype, endian)
+    ((128, 128, 64), (64, 64, 64), None, "float32", LE),
+    ((128, 128, 64), (128, 128, 64), (64, 64, 64), "float32", LE),
+    ((64, 96, 64), (64, 96, 64), (32, 32, 64), "int16", BE),     # 128 KiB inner chunks: 4 units
+    ((64, 64, 64), (64, 64, 64), (16, 64, 64), "float64", LE),   # 64 KiB inner chunks
+]
+
+
+@pytest.mark.tuning
+@pytest.mark.parametrize("arm", [26, 27])
+@pytest.mark.parametrize("case", range(len(ILW_CASES)))
+def test_ilw_arms_exact_and_crc(device, arm, case):
+    """k_decode_ilw (one 32 KiB unit per 1024- / 512-lane workgroup, the
+    small-share shape) decodes exactly -- whole array, a partial window, a
+    missing chunk filled -- and reports a corrupted chunk (and, sharded, a
+    corrupted index) with the reference's message."""
+    import zarr_hip
+    from zarr_hip import _native as N
+
+    shape, cshape, inner, dtype, endian = ILW_CASES[case]
+    codecs = [SHARD(inner, [endian, CRC])] if inner else [endian, CRC]
+    meta = O.ArrayMeta(shape, cshape, np.dtype(dtype), 3, codecs=codecs)
+    host = {}
+    O.write(host, meta, (Ellipsis,), _data(shape, dtype))
+    if not inner:
+        host.pop("c/1/0/0")
+    want_kernel = "k_decode_ilw1024" if arm == 26 else "k_decode_ilw512"
+    set_tuning(6, arm)
+    try:
+        store = zarr_hip.DeviceStore.from_host(host, device)
+        arr = zarr_hip.Array.create(store, shape, cshape, dtype, 3, codecs=codecs)
+        for sel in [(Ellipsis,), (slice(5, 60), slice(3, 64), slice(0, 64))]:
+            prog, out = arr.prepare_read(sel)
+            prog.launch()
+            prog.results()
+            assert N.lib().zhip_last_kernel().decode() == want_kernel
+            assert out.cpu().numpy().tobytes() == np.ascontiguousarray(O.read(host, meta, sel)).tobytes()
+        key = "c/0/0/0"
+        for at in ([70001, len(host[key]) - 40] if inner else [70001]):
+            _corrupt(store, host, key, at=at)
+            with pytest.raises(ValueError) as want:
+                O.read(host, meta)
+            prog, out = arr.prepare_read((Ellipsis,))
+            prog.launch()
+            with pytest.raises(ValueError) as got:
+                prog.results()
+            assert str(got.value) == str(want.value)
+            _corrupt(store, host, key, at=at)
+            prog.launch()
+            prog.results()
+            assert out.cpu().numpy().tobytes() == O.read(host, meta).tobytes()
+    finally:
+        set_tuning(6, 0)
+
+
+@pytest.mark.tuning
 @pytest.mark.parametrize("arm", [0, 5])
 @pytest.mark.parametrize("dtype,endian,chunks,shape", TILE4_CASES)
 def test_transpose_tile4w_and_tile4(device, dtype, endian, chunks, shape, arm):

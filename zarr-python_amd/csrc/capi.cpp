@@ -353,9 +353,14 @@ int zhip_plan_upload(zhip_plan* p) {
     // run ends then need no uniform multiply at all
     const size_t n_old = 4096 + kThreads + p->nseg + (size_t)p->nseg * kThreads;
     const size_t n_pair = kPairTabWords + (size_t)p->nseg * kThreads + kThreads;
-    const size_t n_il = p->il_S ? kPairTabWords + (size_t)p->nseg * kThreads + kThreads : 0;
+    const size_t n_il = p->il_S ? kPairTabWords + (size_t)p->nseg * kThreads + kThreads + kIlBasisWords : 0;
     const size_t n_xw = p->xw_P ? kPairTabWords + (size_t)p->xw_P * 64 + kThreads : 0;
-    std::vector<uint32_t> h(n_old + n_pair + n_il + n_xw);
+    // k_decode_ilw regions (NT = 1024, 512)
+    const bool ilw = ZHIP_TUNING && p->kblocks == (uint32_t)kDefaultBlocks && (p->layout.flags & ZHIP_LF_CRC) &&
+                     !(p->layout.flags & ZHIP_LF_NO_WRITE) && p->nseg <= 256u;
+    size_t n_ilw[2] = {0, 0};
+    for (int i = 0; i < 2 && ilw; ++i) n_ilw[i] = kPairTabWords + (size_t)p->nseg * (1024u >> i) + kThreads;
+    std::vector<uint32_t> h(n_old + n_pair + n_il + n_xw + n_ilw[0] + n_ilw[1]);
     build_horner(h.data());
     for (int t = 0; t < kThreads; ++t) h[4096 + t] = xpow8((uint64_t)kWgStride - 16u * t);
     for (uint32_t s = 0; s < p->nseg; ++s) h[4096 + kThreads + s] = xpow8((uint64_t)s * p->seg);
@@ -400,6 +405,15 @@ int zhip_plan_upload(zhip_plan* p) {
         for (int t = 0; t < kThreads; ++t)
             il[kPairTabWords + (size_t)p->nseg * kThreads + t] =
                 gf_mul(h[n_old + kPairTabWords + (size_t)p->nseg * kThreads + t], back);
+        // the tables' bases (they are linear in the index): T1 / T2 / T3 at
+        // single bits, then the four A4 byte tables -- k_decode_ilc builds the
+        // tables in LDS from these 64 words instead of loading 24 KiB
+        uint32_t* bs = il + kPairTabWords + (size_t)p->nseg * kThreads + kThreads;
+        for (int b = 0; b < 11; ++b) bs[b] = il[kPairT1 + (1u << b)];
+        for (int b = 0; b < 11; ++b) bs[11 + b] = il[kPairT2 + (1u << b)];
+        for (int b = 0; b < 10; ++b) bs[22 + b] = il[kPairT3 + (1u << b)];
+        for (int j = 0; j < 4; ++j)
+            for (int b = 0; b < 8; ++b) bs[32 + 8 * j + b] = il[kPairA4 + 256 * j + (1u << b)];
     }
     p->off_xw = 0;
     if (p->xw_P) {
@@ -422,6 +436,35 @@ int zhip_plan_upload(zhip_plan* p) {
         for (int t = 0; t < kThreads; ++t)
             xw[kPairTabWords + (size_t)p->xw_P * 64 + t] =
                 gf_mul(h[n_old + kPairTabWords + (size_t)p->nseg * kThreads + t], fwd);
+    }
+    // k_decode_ilw: lane t of unit r (NT lanes) takes the blocks at 16 t + D k
+    // (D = 16 NT, k < 2048 / NT); its A_D chain leaves every word w at p
+    // multiplied by x^(8 (p_last + D - p)), so the lane constant
+    // x^(8 (4096 (n_steps - 8 r - 7) - 16 t)) c_inv x^(-96) gives the pair
+    // kernel's frame -- factored as F(r) G(t), G(t) = x^(-128 t)
+    size_t at = n_old + n_pair + n_il + n_xw;
+    for (int i = 0; i < 2; ++i) {
+        p->off_ilw[i] = 0;
+        if (!n_ilw[i]) continue;
+        const uint32_t NT = 1024u >> i;
+        const uint64_t D = 16ull * NT;
+        p->off_ilw[i] = at;
+        uint32_t* w = h.data() + at;
+        build_pair_tables(w, D);
+        const uint32_t xm128 = xpow8_inv(16);
+        std::vector<uint32_t> Gt(NT);
+        Gt[0] = kOne;
+        for (uint32_t t = 1; t < NT; ++t) Gt[t] = gf_mul(Gt[t - 1], xm128);
+        const uint64_t n_steps = (uint64_t)p->nseg * kDefaultBlocks;
+        for (uint32_t r = 0; r < p->nseg; ++r) {
+            const uint32_t F = gf_mul(gf_mul(xpow8(4096ull * (n_steps - 8ull * r - 7ull)), p->c_inv), c96);
+            for (uint32_t t = 0; t < NT; ++t) w[kPairTabWords + (size_t)r * NT + t] = gf_mul(F, Gt[t]);
+        }
+        const uint32_t back = xpow8_inv(D - (uint64_t)kWgStride);
+        for (int t = 0; t < kThreads; ++t)
+            w[kPairTabWords + (size_t)p->nseg * NT + t] =
+                gf_mul(h[n_old + kPairTabWords + (size_t)p->nseg * kThreads + t], back);
+        at += n_ilw[i];
     }
     if (p->d_tables) (void)hipFree(p->d_tables);
     p->d_tables = nullptr;
@@ -764,6 +807,7 @@ int zhip_decode_mapped(const zhip_plan* plan, const void* src, uint64_t src_size
         p.il_tab = plan->d_tables + plan->off_il;
         p.il_klane = p.il_tab + kPairTabWords;
         p.il_kidx = p.il_klane + (size_t)plan->nseg * kThreads;
+        p.il_basis = p.il_kidx + kThreads;
     }
     p.xw = (plan->xw_P && (n_index == 0 || plan->idx_E <= (uint32_t)kWgStride)) ? plan->xw_P : 0u;
     if (p.xw) {
@@ -772,6 +816,19 @@ int zhip_decode_mapped(const zhip_plan* plan, const void* src, uint64_t src_size
         p.xw_klane = p.xw_tab + kPairTabWords;
         p.xw_kidx = p.xw_klane + (size_t)plan->xw_P * 64;
     }
+#if ZHIP_TUNING
+    // k_decode_ilw (arms 26: 1024 lanes, 27: 512 lanes per unit)
+    {
+        const int wi = g_tune_arm == 26 ? 0 : g_tune_arm == 27 ? 1 : -1;
+        p.ilw_nt = (wi >= 0 && plan->off_ilw[wi] && (n_index == 0 || plan->idx_E <= (uint32_t)kWgStride))
+                       ? (1024u >> wi) : 0u;
+        if (p.ilw_nt) {
+            p.ilw_tab = plan->d_tables + plan->off_ilw[wi];
+            p.ilw_klane = p.ilw_tab + kPairTabWords;
+            p.ilw_kidx = p.ilw_klane + (size_t)plan->nseg * p.ilw_nt;
+        }
+    }
+#endif
     for (int op = 0; op < 4; ++op) p.hx[op] = plan->hx[op];
     for (int i = 0; i < 32; ++i) p.kq[i] = plan->kq[i];
     p.n_chunks = n_chunks;

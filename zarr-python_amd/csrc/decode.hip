@@ -502,6 +502,8 @@ KernelFn select_il_kernel_cf(bool crc, int item, bool swap);         // decode_r
 KernelFn select_il_kernel_regmul(bool crc, int item, bool swap, bool occ6);  // decode_rows.hip
 KernelFn select_xw_kernel(bool crc, int item, bool swap);            // decode_rows.hip
 KernelFn select_ilq_kernel(int item, bool swap, int nq, bool glds);  // decode_rows.hip
+KernelFn select_ilc_kernel(int item, bool swap);
+KernelFn select_ilw_kernel(int item, bool swap, int nt);                     // decode_rows.hip
 KernelFn select_tile4f_kernel(int item, bool swap);                  // decode_tile.hip
 #endif
 KernelFn select_tile4_kernel(bool crc, int item, bool swap);         // decode_tile.hip
@@ -512,6 +514,33 @@ KernelFn select_tileg_kernel(bool crc, int item, bool swap, bool defer);  // dec
 // name of the kernel the last launch_decode chose (zhip_last_kernel: bench
 // labels and tests; the selection depends on layout, plan and tuning bits)
 static const char* g_last_kernel = "";
+#if ZHIP_TUNING
+// Overhead probes (arms 28-30; results invalid): the launch of a decode-shaped
+// grid with the decode's kernel arguments and nothing else (28), plus the
+// k_decode_il LDS footprint (29), plus the header chain (resolve_unit) of
+// each workgroup's chunk (30).
+template <int MODE>
+__global__ __launch_bounds__(kThreads) void k_probe(const DecodeParams p) {
+    __shared__ uint32_t s_big[MODE >= 1 ? 9216 : 1];
+    const uint32_t g = blockIdx.x;
+    const int t = threadIdx.x;
+    uint32_t v = g;
+    if constexpr (MODE >= 1) {
+        s_big[(t * 37u + g) % 9216u] = g;
+        __syncthreads();
+        v ^= s_big[(t * 41u) % 9216u];
+    }
+    if constexpr (MODE == 2) {
+        const uint32_t c = g / p.nseg;
+        if (c < p.n_chunks) {
+            const Unit U = resolve_unit(p, c * p.nseg, p.g.nbytes + 4u);
+            v ^= (uint32_t)U.out_off ^ (uint32_t)(uintptr_t)U.cp ^ U.mode;
+        }
+    }
+    if (v == 0xFFFFFFFFu && t == 1000) p.errflag[0] = v;  // never: keeps the work live
+}
+#endif
+
 
 int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
     if (g_tune_max_grid > 0) max_grid = g_tune_max_grid;
@@ -534,8 +563,10 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
             // 8 KiB chunks 25.3-25.6 us vs 37.1 with four per workgroup and 30.8
             // with the pair kernel; 4 KiB chunks 37.2 with four, 52.4 with eight,
             // 41.4 with the pair kernel.  Arms 12 / 13 force four / eight.)
-            const bool e8 = g_tune_arm == 13 ||
-                            (g_tune_arm != 12 && p.E > (uint32_t)kWgStride && p.E <= 2u * kWgStride);
+            // (k_decode_lead8 covers at most two steps: arm 13 cannot force it
+            // onto chunks of more than 8 KiB)
+            const bool e8 = p.E <= 2u * kWgStride &&
+                            (g_tune_arm == 13 || (g_tune_arm != 12 && p.E > (uint32_t)kWgStride));
             KernelFn qfn = select_pair_kernel(crc, p.g.itemsize, swap, e8 ? 11 : 10);
             if (!qfn) return ZHIP_E_UNSUPPORTED;
             const uint32_t per = e8 ? 8u : 4u;
@@ -583,6 +614,33 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
             if (grid > 0x7FFFFFFFull) return ZHIP_E_UNSUPPORTED;
             g_last_kernel = "k_decode_xw";
             hipLaunchKernelGGL(xfn, dim3((uint32_t)grid), dim3(kThreads), 0, stream, p);
+            return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
+        }
+        if (g_tune_arm >= 28 && g_tune_arm <= 30) {  // overhead probes
+            const uint32_t pgrid = p.n_units > p.n_idx ? p.n_units : p.n_idx;
+            if (pgrid == 0) return ZHIP_OK;
+            KernelFn pf = g_tune_arm == 28 ? k_probe<0> : g_tune_arm == 29 ? k_probe<1> : k_probe<2>;
+            g_last_kernel = g_tune_arm == 28 ? "k_probe_args" : g_tune_arm == 29 ? "k_probe_lds" : "k_probe_header";
+            hipLaunchKernelGGL(pf, dim3(pgrid), dim3(kThreads), 0, stream, p);
+            return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
+        }
+        if (crc && p.ilw_nt && (g_tune_arm == 26 || g_tune_arm == 27)) {
+            // k_decode_ilw: one 32 KiB unit per workgroup of 1024 / 512 lanes
+            KernelFn wfn = select_ilw_kernel(p.g.itemsize, swap, (int)p.ilw_nt);
+            if (!wfn) return ZHIP_E_UNSUPPORTED;
+            const uint32_t wgrid = p.n_units > p.n_idx ? p.n_units : p.n_idx;
+            if (wgrid == 0) return ZHIP_OK;
+            g_last_kernel = p.ilw_nt == 1024u ? "k_decode_ilw1024" : "k_decode_ilw512";
+            hipLaunchKernelGGL(wfn, dim3(wgrid), dim3(p.ilw_nt), 0, stream, p);
+            return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
+        }
+        if (il && g_tune_arm == 25) {  // k_decode_ilc: tables built in LDS, predicted loads first
+            KernelFn cfn = select_ilc_kernel(p.g.itemsize, swap);
+            if (!cfn) return ZHIP_E_UNSUPPORTED;
+            const uint32_t igrid = p.n_units > p.n_idx ? p.n_units : p.n_idx;
+            if (igrid == 0) return ZHIP_OK;
+            g_last_kernel = "k_decode_ilc";
+            hipLaunchKernelGGL(cfn, dim3(igrid), dim3(kThreads), 0, stream, p);
             return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
         }
         if (il && g_tune_arm >= 20 && g_tune_arm <= 24) {

@@ -1798,6 +1798,340 @@ void k_decode_ilq(const DecodeParams p) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// k_decode_ilc: k_decode_il without a table load and without the header chain
+// in front of its data loads.  The workgroup timeline of k_decode_il
+// (scripts/stamps.py, profiles/r05/b/): start -> data loads issued 1.8 us
+// median (2.7 us for the slowest 5 %: kernel arguments, then the chunk
+// record, then the shard-index entry, dependent scalar round trips under a
+// saturated memory system), -> tables in LDS 1.3 us (24 KiB of L2 reads per
+// workgroup), -> stores and Horner steps 3.1 us, -> run end 0.9 us, -> exit
+// 0.5 us.  Here the data loads go out right after the kernel arguments, at
+// the addresses the default shard packing predicts (zhip_predict; a wrong
+// guess reloads once the index entry arrives, as k_decode_lead), behind only
+// the lane constant (the oldest load, an L2 hit), and the A_(4096 S)
+// 11/11/10 tables and the A4 fold tables are BUILT in LDS while the data is
+// in flight: every table is linear in its index, so entry i is the XOR of the
+// single-bit entries of i's set bits (64 host-built words, scalar loads);
+// thread t writes T1 / T2 entries 4t..4t+3 (+1024), T3 entries 4t..4t+3 and
+// A4 entry t of each byte table: 8 lane masks, ~60 VALU, 5 ds_write_b128 +
+// 4 ds_write_b32 per thread, no vector memory.  The rest -- stores, chains,
+// run end, publication, fused index checks -- is k_decode_il's.
+__device__ __forceinline__ void build_il_tables_lds(uint32_t* s, int t, const uint32_t* gbasis) {
+    struct B64 {
+        uint32_t w[kIlBasisWords];
+    };
+    const B64 B = load_uniform<B64>(gbasis);
+    uint32_t m[8];
+#pragma unroll
+    for (int b = 0; b < 8; ++b) m[b] = 0u - (((uint32_t)t >> b) & 1u);
+    auto lane_part = [&](int off) {
+        uint32_t L = 0;
+#pragma unroll
+        for (int b = 0; b < 8; ++b) L ^= m[b] & B.w[off + b];
+        return L;
+    };
+    {  // T1 (index bits 0..10 of a word): entry 4t + q + 1024 h
+        const uint32_t L = lane_part(2), q1 = B.w[0], q2 = B.w[1], hb = B.w[10];
+        const uint4 lo = make_uint4(L, L ^ q1, L ^ q2, L ^ q1 ^ q2);
+        *reinterpret_cast<uint4*>(s + kPairT1 + 4 * t) = lo;
+        *reinterpret_cast<uint4*>(s + kPairT1 + 1024 + 4 * t) =
+            make_uint4(lo.x ^ hb, lo.y ^ hb, lo.z ^ hb, lo.w ^ hb);
+    }
+    {  // T2 (bits 11..21)
+        const uint32_t L = lane_part(13), q1 = B.w[11], q2 = B.w[12], hb = B.w[21];
+        const uint4 lo = make_uint4(L, L ^ q1, L ^ q2, L ^ q1 ^ q2);
+        *reinterpret_cast<uint4*>(s + kPairT2 + 4 * t) = lo;
+        *reinterpret_cast<uint4*>(s + kPairT2 + 1024 + 4 * t) =
+            make_uint4(lo.x ^ hb, lo.y ^ hb, lo.z ^ hb, lo.w ^ hb);
+    }
+    {  // T3 (bits 22..31): entry 4t + q
+        const uint32_t L = lane_part(24), q1 = B.w[22], q2 = B.w[23];
+        *reinterpret_cast<uint4*>(s + kPairT3 + 4 * t) = make_uint4(L, L ^ q1, L ^ q2, L ^ q1 ^ q2);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) s[kPairA4 + 256 * j + t] = lane_part(32 + 8 * j);  // A4 byte tables
+}
+
+template <int ITEM, bool SWAP>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_decode_ilc(
+    const DecodeParams p) {
+    constexpr int K = kDefaultBlocks;
+    __shared__ uint32_t s_tab[kPairTabWords];
+    __shared__ uint32_t s_mul[12 * kThreads];
+    __shared__ uint32_t s_red[2][kThreads / 64];
+    const int t = threadIdx.x;
+    PairHot h = p.h;
+    pair_hot(h);
+    il_hot(h);
+    const uint32_t G = gridDim.x, g = blockIdx.x;
+    const uint32_t wpc = h.nseg, S = h.il_S;
+    const uint32_t c = fdiv_apply(g, h.d_nseg.m, h.d_nseg.s);
+    const uint32_t r = g - c * wpc;
+    const bool has = c < h.n_chunks;
+    if (!has && g >= h.n_idx) return;
+    const uint32_t expected = p.g.nbytes + 4u;
+    const uint8_t* zero = reinterpret_cast<const uint8_t*>(g_rows_zero);
+    // 1. the lane constants (the oldest loads: waited for alone), then the data
+    const uint32_t kl = load_u32_any(reinterpret_cast<const uint8_t*>(
+        reinterpret_cast<const uint32_t*>(h.il_klane) + (size_t)(has ? r : 0u) * kThreads + t));
+    const uint32_t kix = load_u32_any(reinterpret_cast<const uint8_t*>(reinterpret_cast<const uint32_t*>(h.il_kidx) + t));
+    const uint32_t ls = (uint32_t)__builtin_ctz(S);
+    const uint32_t st0 = ((r >> ls) << ls) * (uint32_t)K + (r & (S - 1u));
+    const int32_t lo_frame = (int32_t)h.E - (int32_t)(h.nseg * h.seg);
+    uint4 A[K];
+    const uint8_t* cpp = zero;
+    if (h.pred) {
+        const uint32_t grp = fdiv_apply(c, h.d_per.m, h.d_per.s);
+        cpp = reinterpret_cast<const uint8_t*>(h.src) + h.pred_base + (uint64_t)grp * h.pred_outer +
+              (uint64_t)(c - grp * h.pred_per) * h.pred_inner;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int32_t base = lo_frame + kWgStride * (int32_t)(st0 + S * (uint32_t)k);
+            A[k] = load_stream16_any(has && base >= 0 ? cpp + base + 16 * t : zero);
+        }
+    }
+    // 2. the tables built in LDS (no memory reads but 64 scalar words), the lane-multiply column
+    build_il_tables_lds(s_tab, t, p.il_basis);
+    lanemul3_init(s_mul, t, kl);
+    // 3. the header chain: verifies the guess (or, unpredicted, addresses the loads)
+    Unit U;
+    if (has) U = resolve_unit(p, c * h.nseg, expected);
+    else {
+        U.c = 0;
+        U.sidx = 0;
+        U.mode = ZHIP_ST_MISSING;
+        U.cp = zero;
+        U.seg_lo = 0;
+        U.sel = 0;
+        U.out_off = 0;
+    }
+    const bool ok = has && U.mode == ZHIP_ST_OK;
+    if (h.pred) {
+        if (ok && U.cp != cpp) {  // a wrong guess: reload from the live index, full drain
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int32_t base = lo_frame + kWgStride * (int32_t)(st0 + S * (uint32_t)k);
+                A[k] = load_stream16_any(base >= 0 ? U.cp + base + 16 * t : zero);
+            }
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int32_t base = lo_frame + kWgStride * (int32_t)(st0 + S * (uint32_t)k);
+            A[k] = load_stream16_any(ok && base >= 0 ? U.cp + base + 16 * t : zero);
+        }
+    }
+    const uint4 ipre = index_prefetch(p, g, g < h.n_idx, t, zero);
+    zhip_rowblk m[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint32_t st = st0 + S * (uint32_t)k;
+        const uint32_t sidx = h.nseg - 1u - st / (uint32_t)K;
+        m[k] = load_uniform<zhip_rowblk>(p.rowmap + ((size_t)U.sel * h.nseg + sidx) * K + (st % (uint32_t)K));
+    }
+    uint32_t stored = 0;
+    if (ok) stored = load_trailer_uniform(U.cp, p.g.nbytes);
+    __syncthreads();
+    if (has) {
+        // 4. stores, each block's Horner step after its store
+        uint8_t* sink = reinterpret_cast<uint8_t*>(g_rows_sink);
+        const uint32_t lane_row = (16u * (uint32_t)t) >> p.row_shift;
+        const uint32_t lane_col = (16u * (uint32_t)t) & ((1u << p.row_shift) - 1u);
+        const int64_t lane_off = (int64_t)lane_row * p.r_oy + (int64_t)lane_col;
+        const bool writes = ok || U.mode == ZHIP_ST_MISSING;
+        uint8_t* const obase = p.out + U.out_off;
+        const uint4 f = make_uint4(p.fill[0], p.fill[1], p.fill[2], p.fill[3]);
+        Acc4 acc = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint32_t lo = m[k].lo, hi = m[k].hi;
+            const bool wr = writes && lane_row - lo < hi - lo;
+            store_nt16(wr ? obase + m[k].rel + lane_off : sink, ok ? swap_block<ITEM, SWAP>(A[k]) : f);
+            if (ok) crc_block4(s_tab, acc, A[k]);
+        }
+        // 5. run end: one chain per workgroup, one publication
+        uint32_t v = ok ? lanemul3(s_mul, t, fold4(s_tab, acc)) : 0u;
+        v = wave_xor(v);
+        if ((t & 63) == 0) s_red[0][t >> 6] = v;
+        __syncthreads();
+        if (ok && t < 64) {
+            const uint32_t V = __builtin_amdgcn_readfirstlane(s_red[0][0] ^ s_red[0][1] ^ s_red[0][2] ^ s_red[0][3]);
+            publish_il(p, c, r, wpc, V, __builtin_amdgcn_readfirstlane(stored), t, kPubLine / 2u);
+        }
+        if (r == 0) unit_status_pair(p, U, true, t);
+    }
+    // 6. fused shard-index checks (one step per lane), the first block prefetched
+    for (uint32_t j = g; j < h.n_idx; j += G) verify_index_pair(p, j, t, kix, s_tab, s_red[1], j == g, ipre);
+}
+
+// ---------------------------------------------------------------------------
+// k_decode_ilw: small shares (below ~2 workgroups per CU: the N = 4 / 8 shares
+// of the strong-scaled headline).  k_decode_il there runs ONE 4-wave
+// workgroup per CU, each lane's eight Horner steps in series with nothing to
+// interleave (stamps at the N = 8 share, profiles/r05/d/: 2.0 us from tables
+// to the last stored block, 0.7 us run end).  Here a 32 KiB unit is taken by
+// NT = 512 or 1024 lanes, 2048 / NT blocks each (lane t: the blocks at 16 t +
+// 16 NT k of the unit), so a CU holds 8 or 16 waves whose chains interleave,
+// under the tables of A_(16 NT); the 4 KiB sub-step of block k is 8 r + t /
+// 256 + (NT / 256) k, so stores, row map and lane offsets are k_decode_il's
+// per sub-step.  Lane constants F(r) G(t) from capi.cpp (off_ilw).
+template <int NT>
+__device__ __forceinline__ void lanemul3_init_w(uint32_t* s_mul, int t, uint32_t k) {
+    const uint32_t k1 = mulx1(k), k2 = mulx1(k1);
+#pragma unroll
+    for (uint32_t v = 0; v < 8; ++v)
+        s_mul[v * NT + t] = ((v & 4u) ? k : 0u) ^ ((v & 2u) ? k1 : 0u) ^ ((v & 1u) ? k2 : 0u);
+#pragma unroll
+    for (uint32_t v = 0; v < 4; ++v) s_mul[(8u + v) * NT + t] = ((v & 2u) ? k : 0u) ^ ((v & 1u) ? k1 : 0u);
+}
+
+template <int NT>
+__device__ __forceinline__ uint32_t lanemul3_w(const uint32_t* s_mul, int t, uint32_t a) {
+    uint32_t m[11];
+#pragma unroll
+    for (int j = 0; j < 10; ++j) m[j] = s_mul[((a >> (3 * j)) & 7u) * NT + t];
+    m[10] = s_mul[(8u + (a >> 30)) * NT + t];
+    uint32_t q = m[0];
+#pragma unroll
+    for (int j = 1; j < 10; ++j) q = (q >> 3) ^ r3(q & 7u) ^ m[j];
+    return (q >> 2) ^ r2(q & 3u) ^ m[10];
+}
+
+template <int ITEM, bool SWAP, int NT>
+__global__ __launch_bounds__(NT) void k_decode_ilw(const DecodeParams p) {
+    constexpr int KW = 2048 / NT;  // blocks per lane
+    constexpr int QW = NT / 256;   // 4 KiB sub-steps per row of lanes
+    constexpr int TV = (kPairTabWords / 4 + NT - 1) / NT;
+    __shared__ uint32_t s_tab[kPairTabWords];
+    __shared__ uint32_t s_mul[12 * NT];
+    __shared__ uint32_t s_red[2][NT / 64];
+    const int t = threadIdx.x;
+    const uint32_t G = gridDim.x, g = blockIdx.x;
+    const uint32_t wpc = p.nseg;
+    const uint32_t c = g / wpc, r = g - c * wpc;
+    const bool has = c < p.n_chunks;
+    if (!has && g >= p.n_idx) return;
+    stamp(p, g, t, 0);
+    const uint32_t expected = p.g.nbytes + 4u;
+    const uint8_t* zero = reinterpret_cast<const uint8_t*>(g_rows_zero);
+    // 1. tables, lane constants, then (header chain) the data
+    uint4 tv[TV];
+    const uint4* gt = reinterpret_cast<const uint4*>(p.ilw_tab);
+#pragma unroll
+    for (int i = 0; i < TV; ++i) {
+        const int ix = t + i * NT;
+        tv[i] = ix < kPairTabWords / 4 ? gt[ix] : make_uint4(0, 0, 0, 0);
+    }
+    const uint32_t kl = load_u32_any(reinterpret_cast<const uint8_t*>(p.ilw_klane + (size_t)(has ? r : 0u) * NT + t));
+    const uint32_t kix = load_u32_any(reinterpret_cast<const uint8_t*>(p.ilw_kidx + (t & (kThreads - 1))));
+    Unit U;
+    if (has) U = resolve_unit(p, c * p.nseg, expected);
+    else {
+        U.c = 0;
+        U.sidx = 0;
+        U.mode = ZHIP_ST_MISSING;
+        U.cp = zero;
+        U.seg_lo = 0;
+        U.sel = 0;
+        U.out_off = 0;
+    }
+    const bool ok = has && U.mode == ZHIP_ST_OK;
+    const int32_t lo_frame = (int32_t)p.E - (int32_t)(p.nseg * p.seg);
+    const uint32_t q = __builtin_amdgcn_readfirstlane((uint32_t)t >> 8);  // wave-uniform
+    const uint32_t l = (uint32_t)t & 255u;
+    const uint4 ipre = index_prefetch(p, g, g < p.n_idx && t < kThreads, t, zero);
+    uint4 A[KW];
+#pragma unroll
+    for (int k = 0; k < KW; ++k) {
+        const int32_t base = lo_frame + kWgStride * (int32_t)(8u * r + q + (uint32_t)(QW * k));
+        A[k] = load_stream16_any(ok && base >= 0 ? U.cp + base + 16 * l : zero);
+    }
+    stamp(p, g, t, 1);
+    zhip_rowblk m[KW];
+    const uint32_t sidx = p.nseg - 1u - r;
+#pragma unroll
+    for (int k = 0; k < KW; ++k)
+        m[k] = load_uniform<zhip_rowblk>(p.rowmap + ((size_t)U.sel * p.nseg + sidx) * kDefaultBlocks + q +
+                                         (uint32_t)(QW * k));
+    uint32_t stored = 0;
+    if (ok) stored = load_trailer_uniform(U.cp, p.g.nbytes);
+    // 2. tables into LDS, the lane-multiply column
+    {
+        uint4* stt = reinterpret_cast<uint4*>(s_tab);
+#pragma unroll
+        for (int i = 0; i < TV; ++i) {
+            const int ix = t + i * NT;
+            if (ix < kPairTabWords / 4) stt[ix] = tv[i];
+        }
+        lanemul3_init_w<NT>(s_mul, t, kl);
+    }
+    __syncthreads();
+    stamp(p, g, t, 2);
+    if (has) {
+        // 3. stores, each block's Horner step after its store
+        uint8_t* sink = reinterpret_cast<uint8_t*>(g_rows_sink);
+        const uint32_t lane_row = (16u * l) >> p.row_shift;
+        const uint32_t lane_col = (16u * l) & ((1u << p.row_shift) - 1u);
+        const int64_t lane_off = (int64_t)lane_row * p.r_oy + (int64_t)lane_col;
+        const bool writes = ok || U.mode == ZHIP_ST_MISSING;
+        uint8_t* const obase = p.out + U.out_off;
+        const uint4 f = make_uint4(p.fill[0], p.fill[1], p.fill[2], p.fill[3]);
+        Acc4 acc = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int k = 0; k < KW; ++k) {
+            const uint32_t lo = m[k].lo, hi = m[k].hi;
+            const bool wr = writes && lane_row - lo < hi - lo;
+            store_nt16(wr ? obase + m[k].rel + lane_off : sink, ok ? swap_block<ITEM, SWAP>(A[k]) : f);
+            if (ok) crc_block4(s_tab, acc, A[k]);
+        }
+        stamp(p, g, t, 3);
+        // 4. run end: one chain per workgroup, one publication
+        uint32_t v = ok ? lanemul3_w<NT>(s_mul, t, fold4(s_tab, acc)) : 0u;
+        v = wave_xor(v);
+        if ((t & 63) == 0) s_red[0][t >> 6] = v;
+        __syncthreads();
+        if (ok && t < 64) {
+            uint32_t x = 0;
+#pragma unroll
+            for (int w = 0; w < NT / 64; ++w) x ^= s_red[0][w];
+            const uint32_t V = __builtin_amdgcn_readfirstlane(x);
+            stamp(p, g, t, 4);
+            publish_il(p, c, r, wpc, V, __builtin_amdgcn_readfirstlane(stored), t, kPubLine / 2u);
+        }
+        if (r == 0) unit_status_pair(p, U, true, t);
+    }
+    stamp(p, g, t, 7);
+    // 5. fused shard-index checks (one step per lane, the first 256 lanes)
+    for (uint32_t j = g; j < p.n_idx; j += G)
+        verify_index_pair(p, j, t, kix, s_tab, s_red[1], j == g, ipre, t < kThreads);
+}
+
+#if ZHIP_TUNING
+KernelFn select_ilw_kernel(int item, bool swap, int nt) {  // CRC chains only
+#define ZHIP_ILW(I, W) (nt == 1024 ? k_decode_ilw<I, W, 1024> : k_decode_ilw<I, W, 512>)
+    switch (item) {
+        case 1: return ZHIP_ILW(1, false);
+        case 2: return swap ? ZHIP_ILW(2, true) : ZHIP_ILW(2, false);
+        case 4: return swap ? ZHIP_ILW(4, true) : ZHIP_ILW(4, false);
+        case 8: return swap ? ZHIP_ILW(8, true) : ZHIP_ILW(8, false);
+        default: return nullptr;
+    }
+#undef ZHIP_ILW
+}
+
+KernelFn select_ilc_kernel(int item, bool swap) {  // CRC chains only
+    switch (item) {
+        case 1: return k_decode_ilc<1, false>;
+        case 2: return swap ? k_decode_ilc<2, true> : k_decode_ilc<2, false>;
+        case 4: return swap ? k_decode_ilc<4, true> : k_decode_ilc<4, false>;
+        case 8: return swap ? k_decode_ilc<8, true> : k_decode_ilc<8, false>;
+        default: return nullptr;
+    }
+}
+#endif
+
 #if ZHIP_TUNING
 KernelFn select_ilq_kernel(int item, bool swap, int nq, bool glds) {  // CRC chains only
 #define ZHIP_ILQ(I, W) \

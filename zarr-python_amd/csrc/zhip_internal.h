@@ -49,6 +49,7 @@ struct GroupEnt {
 // and 10 high bits of a word, then the four byte slices of A4 (x^32).
 constexpr int kPairT1 = 0, kPairT2 = 2048, kPairT3 = 4096, kPairA4 = 5120;
 constexpr int kPairTabWords = 6144;
+constexpr int kIlBasisWords = 64;  // T1 / T2 / T3 bases (11 + 11 + 10, padded to 32), A4 bases (4 x 8)
 
 // What k_decode_lead (and the k_decode_il arm) need before their first vector loads,
 // FIRST in the kernel arguments and read as one scalar batch (pair_hot): the
@@ -142,6 +143,7 @@ struct DecodeParams {
     const uint32_t* il_tab;
     const uint32_t* il_klane;
     const uint32_t* il_kidx;
+    const uint32_t* il_basis;  // kIlBasisWords: the il tables' single-bit entries (k_decode_ilc)
     uint32_t dv_bank;  // deferred CRC verdicts: bank this launch publishes into (ZHIP_DF_BANK1)
     uint32_t defer;    // ZHIP_DF_DEFER: the caller reads deferred verdicts (tileg / tilegw publish so)
     // k_decode_xw: 8 KiB spans per chunk (0: not available), arrival subwords
@@ -151,6 +153,13 @@ struct DecodeParams {
     const uint32_t* xw_tab;
     const uint32_t* xw_klane;
     const uint32_t* xw_kidx;
+    // k_decode_ilw (small shares): ilw_nt lanes per 32 KiB unit (0: not
+    // available), its A_(16 ilw_nt) tables, lane constants per (unit, lane),
+    // the fused index check's lane constants
+    uint32_t ilw_nt;
+    const uint32_t* ilw_tab;
+    const uint32_t* ilw_klane;
+    const uint32_t* ilw_kidx;
     // load-address prediction (zhip_predict; k_decode_pair): payload of chunk c
     // predicted at src + pred_base + (c / pred_per) * pred_outer + (c % pred_per) * pred_inner
     uint32_t pred, pred_per;
@@ -402,4 +411,9 @@ struct zhip_plan {
     // kidx (256)
     uint32_t xw_P, xw_nsub;
     uint64_t off_xw;
+    // k_decode_ilw (decode_rows.hip): one 32 KiB unit per workgroup of NT =
+    // 512 / 1024 lanes (2048 / NT blocks per lane); d_tables continues at
+    // off_ilw[0] (NT = 1024) / off_ilw[1] (NT = 512) with the tables of
+    // A_(16 NT) | klane (nseg x NT) | kidx (256); 0: not built
+    uint64_t off_ilw[2];
 };

@@ -76,9 +76,10 @@ def _dev_key(device) -> int:
 def _pool_take(kind: str, n: int, device, dtype):
     torch = _torch()
     key = (kind, n, _dev_key(device))
-    lst = _BUF_POOL.get(key)
-    if lst:
-        return lst.pop()
+    try:  # (list.pop is atomic: two threads never take the same buffer)
+        return _BUF_POOL.get(key, []).pop()
+    except IndexError:
+        pass
     if kind == "z":
         return torch.zeros(n, dtype=dtype, device=device)
     return torch.empty(n, dtype=dtype, device=device)
@@ -673,6 +674,8 @@ def _config_devices() -> tuple:
 _ZARR_CONFIG: dict = {}
 
 
+IL_PREDICT = os.environ.get("ZARR_HIP_IL_PREDICT", "0") == "1"
+
 # entries of the per-call plan cache (per pipeline instance); 0 disables it
 READ_CACHE_SIZE = int(os.environ.get("ZARR_HIP_READ_CACHE", "16"))
 
@@ -1089,8 +1092,9 @@ class HipCodecPipeline:
             ostr = [int(s) * itemsize for s in out.stride()]
             with torch.cuda.device(device):
                 t = plan_decode(chain, spec, items, ostr, out.data_ptr(), drop_axes, resolved, item_out_extra)
-                # (k_decode_il resolves its own units: no prediction to build)
-                if self.predict_loads and t.rows and not (_kernel_flags(t.layout) & N.PK_IL):
+                # (k_decode_il resolves its own units: no prediction to build;
+                # ZARR_HIP_IL_PREDICT=1 builds one for it too -- measurement arms)
+                if self.predict_loads and t.rows and (IL_PREDICT or not (_kernel_flags(t.layout) & N.PK_IL)):
                     predict_rows(t, chain, spec, size)
                 # fuse the shard-index CRC checks into the data launch
                 # (zhip_decode_indexed: needs the CRC tables, i.e. an inner crc32c, and
