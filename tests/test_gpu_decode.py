@@ -901,10 +901,11 @@ def _il_array(device, fill=0.0, kind="il"):
     return arr, store, host, meta
 
 
-# (kind, ZHIP_TUNE_ARM): k_decode_il's returning publication (production),
-# its deferred-verdict arm, and the deferred verdicts of k_decode_tilegw
+# (kind, ZHIP_TUNE_ARM): k_decode_il's returning publication (arm 33 keeps
+# k_decode_il on this small grid), its deferred-verdict arm, the small-grid
+# production k_decode_ilw512, and the deferred verdicts of k_decode_tilegw
 # (production) and k_decode_tileg (arm 5)
-VERDICT_CASES = [("il", 0), ("il", 2), ("tilegw", 0), ("tileg", 5)]
+VERDICT_CASES = [("il", 33), ("il", 2), ("ilw512", 0), ("tilegw", 0), ("tileg", 5)]
 
 
 @pytest.fixture
@@ -1011,6 +1012,38 @@ def test_deferred_verdict_host_slabs(device):
     arr2 = zarr_hip.Array.create(zarr_hip.MemoryStore(dict(host)), shape, chunks, "float32", 0.0, codecs=[LE, CRC])
     for _ in range(2):
         assert arr2[...].tobytes() == O.read(host, meta).tobytes()
+
+
+@pytest.mark.parametrize("sharded", [False, True])
+def test_il_and_small_grid_kernels(device, sharded):
+    """Production kernel choice for the headline's 1 MiB chunks: k_decode_il
+    above kIlwMaxUnits (512) units, k_decode_ilw512 (512 lanes per unit) at
+    or below; both bit-exact, a corrupted chunk reported with the reference's
+    message."""
+    import zarr_hip
+    from zarr_hip import _native as N
+
+    shape, chunks = (128, 128, 320), (64, 64, 64)  # 20 chunks = 640 units
+    codecs = [SHARD((64, 64, 64), [LE, CRC])] if sharded else [LE, CRC]
+    cshape = (128, 128, 64) if sharded else chunks
+    meta = O.ArrayMeta(shape, cshape, np.dtype("float32"), 0.0, codecs=codecs)
+    host = {}
+    O.write(host, meta, (Ellipsis,), _data(shape, "float32"))
+    store = zarr_hip.DeviceStore.from_host(host, device)
+    arr = zarr_hip.Array.create(store, shape, cshape, "float32", 0.0, codecs=codecs)
+    for sel, kernel in [((Ellipsis,), "k_decode_il"), ((slice(None), slice(None), slice(0, 128)), "k_decode_ilw512")]:
+        prog, out = arr.prepare_read(sel)
+        prog.launch()
+        prog.results()
+        assert N.lib().zhip_last_kernel().decode() == kernel
+        assert out.cpu().numpy().tobytes() == np.ascontiguousarray(O.read(host, meta, sel)).tobytes()
+    _corrupt(store, host, "c/0/0/2" if sharded else "c/1/1/2", at=123457)
+    with pytest.raises(ValueError) as want:
+        O.read(host, meta)
+    for sel in [(Ellipsis,), (slice(None), slice(None), slice(128, 192))]:
+        with pytest.raises(ValueError) as got:
+            arr[sel]
+        assert str(got.value) == str(want.value)
 
 
 @pytest.mark.tuning
@@ -1211,7 +1244,7 @@ ILW_CASES = [  # (shape, chunks, inner chunks or None, dtype, endian)
 
 
 @pytest.mark.tuning
-@pytest.mark.parametrize("arm", [26, 27])
+@pytest.mark.parametrize("arm", [26, 27, 31, 32])
 @pytest.mark.parametrize("case", range(len(ILW_CASES)))
 def test_ilw_arms_exact_and_crc(device, arm, case):
     """k_decode_ilw (one 32 KiB unit per 1024- / 512-lane workgroup, the
@@ -1228,7 +1261,7 @@ def test_ilw_arms_exact_and_crc(device, arm, case):
     O.write(host, meta, (Ellipsis,), _data(shape, dtype))
     if not inner:
         host.pop("c/1/0/0")
-    want_kernel = "k_decode_ilw1024" if arm == 26 else "k_decode_ilw512"
+    want_kernel = {26: "k_decode_ilw1024", 27: "k_decode_ilw512", 31: "k_decode_ilw1024r", 32: "k_decode_ilw512r"}[arm]
     set_tuning(6, arm)
     try:
         store = zarr_hip.DeviceStore.from_host(host, device)

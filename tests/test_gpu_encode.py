@@ -188,6 +188,56 @@ def test_encode_pair_sharded_empty_inner(device):
          [((Ellipsis,), d), ((slice(0, 8),), 0.0), ((slice(2, 30, 3), slice(1, 63)), 5.0)])
 
 
+# ---- k_encode_il: chunks of 8 k units (>= 256 KiB), one unit per workgroup,
+#      steps interleaved in groups of eight; the last arrival of each chunk
+#      writes trailer, status and the non-empty flag (ORed by non-fill waves)
+
+IL_ENC_CASES = [
+    ((64, 64, 128), (32, 64, 32), "float32", [LE, CRC], 0.0),     # 256 KiB chunks: one group of eight
+    ((64, 64, 128), (64, 64, 64), "float32", [BE, CRC], np.nan),  # 1 MiB: the headline's chunk
+    ((64, 128, 64), (64, 64, 32), "int16", [LE, CRC], 0),
+    ((32, 64, 64), (32, 32, 32), "float64", [LE, CRC], 0.0),
+]
+
+
+@pytest.mark.parametrize("case", range(len(IL_ENC_CASES)))
+def test_encode_il(device, case):
+    from zarr_hip import _native as N
+
+    shape, chunks, dtype, codecs, fill = IL_ENC_CASES[case]
+    d = _data(shape, dtype)
+    c0 = tuple(slice(0, c) for c in chunks)
+    d[c0] = fill                                   # one chunk entirely fill: elided
+    c1 = (slice(0, chunks[0]), slice(0, chunks[1]), slice(chunks[2], 2 * chunks[2]))
+    d[c1] = fill                                   # another: fill except one element
+    if np.issubdtype(np.dtype(dtype), np.floating) and not np.isnan(fill):
+        d[chunks[0] - 1, chunks[1] - 1, 2 * chunks[2] - 1] = -0.0   # bitwise != fill: kept
+    else:
+        d[chunks[0] - 1, chunks[1] - 1, 2 * chunks[2] - 1] = 1
+    part = (slice(3, shape[0] - 5), slice(7, shape[1]), slice(1, shape[2] - 9))
+    psh = tuple(s.stop - s.start for s in part)
+    w = [((Ellipsis,), d),
+         (part, _data(psh, dtype, 3)),                                  # merges into every chunk
+         ((slice(0, chunks[0]), slice(0, chunks[1]), slice(shape[2] - chunks[2], shape[2])), fill)]  # back to fill
+    arr, _ = _run(device, shape, chunks, dtype, codecs, fill, w)
+    arr[...] = d
+    assert N.lib().zhip_last_kernel().decode() == "k_encode_il"
+    _run(device, shape, chunks, dtype, codecs, fill, w[:1], write_empty=True)
+
+
+def test_encode_il_sharded(device):
+    from zarr_hip import _native as N
+
+    shape = (64, 64, 128)
+    codecs = [SHARD((32, 64, 32), [LE, CRC])]       # 256 KiB inner chunks
+    d = _data(shape, "float32")
+    d[0:32, :, 32:64] = 0.0
+    arr, _ = _run(device, shape, (64, 64, 64), "float32", codecs, 0.0,
+                  [((Ellipsis,), d), ((slice(5, 60), slice(2, 63), slice(9, 100)), 2.5), ((slice(32, 64),), 0.0)])
+    arr[...] = d
+    assert N.lib().zhip_last_kernel().decode() == "k_encode_il"
+
+
 # ---- k_encode_quad: chunks of <= 16 KiB, four per workgroup (trailer, status
 #      and non-empty flag written by the workgroup that owns the chunk);
 #      ZHIP_TUNE_ARM 11 runs k_encode_pair on the same writes

@@ -355,11 +355,13 @@ int zhip_plan_upload(zhip_plan* p) {
     const size_t n_pair = kPairTabWords + (size_t)p->nseg * kThreads + kThreads;
     const size_t n_il = p->il_S ? kPairTabWords + (size_t)p->nseg * kThreads + kThreads + kIlBasisWords : 0;
     const size_t n_xw = p->xw_P ? kPairTabWords + (size_t)p->xw_P * 64 + kThreads : 0;
-    // k_decode_ilw regions (NT = 1024, 512)
-    const bool ilw = ZHIP_TUNING && p->kblocks == (uint32_t)kDefaultBlocks && (p->layout.flags & ZHIP_LF_CRC) &&
-                     !(p->layout.flags & ZHIP_LF_NO_WRITE) && p->nseg <= 256u;
+    // k_decode_ilw regions (NT = 1024: tuning arms only; 512: the small-grid
+    // form of k_decode_il's layouts)
+    const bool ilw = (p->il_S == 8u || (ZHIP_TUNING && p->kblocks == (uint32_t)kDefaultBlocks &&
+                                        (p->layout.flags & ZHIP_LF_CRC) && !(p->layout.flags & ZHIP_LF_NO_WRITE))) &&
+                     p->nseg <= 256u;
     size_t n_ilw[2] = {0, 0};
-    for (int i = 0; i < 2 && ilw; ++i) n_ilw[i] = kPairTabWords + (size_t)p->nseg * (1024u >> i) + kThreads;
+    for (int i = ZHIP_TUNING ? 0 : 1; i < 2 && ilw; ++i) n_ilw[i] = kPairTabWords + (size_t)p->nseg * (1024u >> i) + kThreads;
     std::vector<uint32_t> h(n_old + n_pair + n_il + n_xw + n_ilw[0] + n_ilw[1]);
     build_horner(h.data());
     for (int t = 0; t < kThreads; ++t) h[4096 + t] = xpow8((uint64_t)kWgStride - 16u * t);
@@ -816,19 +818,22 @@ int zhip_decode_mapped(const zhip_plan* plan, const void* src, uint64_t src_size
         p.xw_klane = p.xw_tab + kPairTabWords;
         p.xw_kidx = p.xw_klane + (size_t)plan->xw_P * 64;
     }
-#if ZHIP_TUNING
-    // k_decode_ilw (arms 26: 1024 lanes, 27: 512 lanes per unit)
+    // k_decode_ilw: 512 lanes per unit for grids of at most kIlwMaxUnits
+    // units (launch_decode; tuning arms 26 / 31 force 1024 lanes, 27 / 32 512)
     {
-        const int wi = g_tune_arm == 26 ? 0 : g_tune_arm == 27 ? 1 : -1;
-        p.ilw_nt = (wi >= 0 && plan->off_ilw[wi] && (n_index == 0 || plan->idx_E <= (uint32_t)kWgStride))
-                       ? (1024u >> wi) : 0u;
+        int wi = (n_index == 0 || plan->idx_E <= (uint32_t)kWgStride) && units <= kIlwMaxUnits ? 1 : -1;
+#if ZHIP_TUNING
+        if (g_tune_arm == 26 || g_tune_arm == 31) wi = 0;
+        else if (g_tune_arm == 27 || g_tune_arm == 32) wi = 1;
+        if (g_tune_arm >= 26 && g_tune_arm <= 32 && !(n_index == 0 || plan->idx_E <= (uint32_t)kWgStride)) wi = -1;
+#endif
+        p.ilw_nt = (wi >= 0 && plan->off_ilw[wi]) ? (1024u >> wi) : 0u;
         if (p.ilw_nt) {
             p.ilw_tab = plan->d_tables + plan->off_ilw[wi];
             p.ilw_klane = p.ilw_tab + kPairTabWords;
             p.ilw_kidx = p.ilw_klane + (size_t)plan->nseg * p.ilw_nt;
         }
     }
-#endif
     for (int op = 0; op < 4; ++op) p.hx[op] = plan->hx[op];
     for (int i = 0; i < 32; ++i) p.kq[i] = plan->kq[i];
     p.n_chunks = n_chunks;
@@ -1059,6 +1064,11 @@ int zhip_encode_mapped(const zhip_plan* plan, const void* arr, void* dst, const 
         p.kpair11 = p.pair_tab + kPairTabWords;
         p.row_shift = (uint32_t)__builtin_ctz(rb);
         p.r_oy = L.out_stride[nd - 2];
+        if (plan->il_S == 8u && (L.flags & ZHIP_LF_CRC)) {  // k_encode_il (launch_encode)
+            p.il_S = plan->il_S;
+            p.il_tab = plan->d_tables + plan->off_il;
+            p.il_klane = p.il_tab + kPairTabWords;
+        }
     }
     int rc = launch_encode(p, static_cast<hipStream_t>(stream), plan->max_grid);
     if (rc == ZHIP_E_UNSUPPORTED) return set_err(rc, "no encode kernel for this layout");

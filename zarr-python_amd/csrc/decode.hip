@@ -494,6 +494,7 @@ KernelFn select_rows_kernel(bool crc, int item, bool swap, int k);  // decode_ro
 KernelFn select_pair_kernel(bool crc, int item, bool swap, int nu);  // decode_rows.hip
 KernelFn select_duo_kernel(bool crc, int item, bool swap);           // decode_rows.hip
 KernelFn select_il_kernel(bool crc, int item, bool swap);            // decode_rows.hip
+KernelFn select_ilw_kernel(int item, bool swap, int nt, bool lmr);   // decode_rows.hip
 #if ZHIP_TUNING
 KernelFn select_il_kernel_lean(bool crc, int item, bool swap);       // decode_rows.hip
 KernelFn select_il_kernel_tuned(bool crc, int item, bool swap);      // decode_rows.hip
@@ -502,8 +503,7 @@ KernelFn select_il_kernel_cf(bool crc, int item, bool swap);         // decode_r
 KernelFn select_il_kernel_regmul(bool crc, int item, bool swap, bool occ6);  // decode_rows.hip
 KernelFn select_xw_kernel(bool crc, int item, bool swap);            // decode_rows.hip
 KernelFn select_ilq_kernel(int item, bool swap, int nq, bool glds);  // decode_rows.hip
-KernelFn select_ilc_kernel(int item, bool swap);
-KernelFn select_ilw_kernel(int item, bool swap, int nt);                     // decode_rows.hip
+KernelFn select_ilc_kernel(int item, bool swap);                     // decode_rows.hip
 KernelFn select_tile4f_kernel(int item, bool swap);                  // decode_tile.hip
 #endif
 KernelFn select_tile4_kernel(bool crc, int item, bool swap);         // decode_tile.hip
@@ -513,7 +513,7 @@ KernelFn select_tileg_kernel(bool crc, int item, bool swap, bool defer);  // dec
 
 // name of the kernel the last launch_decode chose (zhip_last_kernel: bench
 // labels and tests; the selection depends on layout, plan and tuning bits)
-static const char* g_last_kernel = "";
+const char* g_last_kernel = "";
 #if ZHIP_TUNING
 // Overhead probes (arms 28-30; results invalid): the launch of a decode-shaped
 // grid with the decode's kernel arguments and nothing else (28), plus the
@@ -624,13 +624,15 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
             hipLaunchKernelGGL(pf, dim3(pgrid), dim3(kThreads), 0, stream, p);
             return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
         }
-        if (crc && p.ilw_nt && (g_tune_arm == 26 || g_tune_arm == 27)) {
+        if (crc && p.ilw_nt && (g_tune_arm == 26 || g_tune_arm == 27 || g_tune_arm == 31 || g_tune_arm == 32)) {
             // k_decode_ilw: one 32 KiB unit per workgroup of 1024 / 512 lanes
-            KernelFn wfn = select_ilw_kernel(p.g.itemsize, swap, (int)p.ilw_nt);
+            // (31 / 32: the lane multiply in registers)
+            KernelFn wfn = select_ilw_kernel(p.g.itemsize, swap, (int)p.ilw_nt, g_tune_arm >= 31);
             if (!wfn) return ZHIP_E_UNSUPPORTED;
             const uint32_t wgrid = p.n_units > p.n_idx ? p.n_units : p.n_idx;
             if (wgrid == 0) return ZHIP_OK;
-            g_last_kernel = p.ilw_nt == 1024u ? "k_decode_ilw1024" : "k_decode_ilw512";
+            g_last_kernel = p.ilw_nt == 1024u ? (g_tune_arm >= 31 ? "k_decode_ilw1024r" : "k_decode_ilw1024")
+                                              : (g_tune_arm >= 31 ? "k_decode_ilw512r" : "k_decode_ilw512");
             hipLaunchKernelGGL(wfn, dim3(wgrid), dim3(p.ilw_nt), 0, stream, p);
             return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
         }
@@ -661,6 +663,20 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
             return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
         }
 #endif
+        // grids of at most kIlwMaxUnits units (2 per CU: the N = 4 / 8 shares of
+        // the strong-scaled headline): 512 lanes per unit, four blocks per lane
+        // (k_decode_ilw, decode_rows.hip) -- graph-timed 8.8 vs 9.4 us at the
+        // N = 8 share, 10.3 vs 11.0 at N = 4; 14.6 vs 16.5 for k_decode_il at
+        // N = 2 (profiles/r05/f/).  (Tuning build: any arm keeps k_decode_il.)
+        if (il && p.ilw_nt == 512u && p.n_units <= kIlwMaxUnits && g_tune_arm == 0 && (tune & ~kTuneStamp) == 0) {
+            KernelFn wfn = select_ilw_kernel(p.g.itemsize, swap, 512, false);
+            if (!wfn) return ZHIP_E_UNSUPPORTED;
+            const uint32_t wgrid = p.n_units > p.n_idx ? p.n_units : p.n_idx;
+            if (wgrid == 0) return ZHIP_OK;
+            g_last_kernel = "k_decode_ilw512";
+            hipLaunchKernelGGL(wfn, dim3(wgrid), dim3(512), 0, stream, p);
+            return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
+        }
         if (il) {
 #if ZHIP_TUNING
             KernelFn ifn = g_tune_arm ? select_il_kernel_arm(crc, p.g.itemsize, swap, g_tune_arm)

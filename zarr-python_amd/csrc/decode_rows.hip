@@ -467,29 +467,6 @@ __device__ __forceinline__ void crc_block4_cf(const uint32_t* s, Acc4& a, const 
     a.a3 = t11_cf(s, a.a3 ^ v.w, ln);
 }
 
-// The lane's 12-entry window column of k in LDS (12 KiB for 256 lanes; the
-// 4-bit form needs 16), and the multiply over it (windows: zhip_decode_common.h).
-__device__ __forceinline__ void lanemul3_init(uint32_t* s_mul, int t, uint32_t k) {
-    const uint32_t k1 = mulx1(k), k2 = mulx1(k1);
-#pragma unroll
-    for (uint32_t v = 0; v < 8; ++v)
-        s_mul[v * kThreads + t] = ((v & 4u) ? k : 0u) ^ ((v & 2u) ? k1 : 0u) ^ ((v & 1u) ? k2 : 0u);
-#pragma unroll
-    for (uint32_t v = 0; v < 4; ++v) s_mul[(8u + v) * kThreads + t] = ((v & 2u) ? k : 0u) ^ ((v & 1u) ? k1 : 0u);
-}
-
-__device__ __forceinline__ uint32_t lanemul3(const uint32_t* s_mul, int t, uint32_t a) {
-    uint32_t m[11];
-#pragma unroll
-    for (int j = 0; j < 10; ++j) m[j] = s_mul[((a >> (3 * j)) & 7u) * kThreads + t];
-    m[10] = s_mul[(8u + (a >> 30)) * kThreads + t];
-    uint32_t q = m[0];
-#pragma unroll
-    for (int j = 1; j < 10; ++j) q = (q >> 3) ^ r3(q & 7u) ^ m[j];
-    return (q >> 2) ^ r2(q & 3u) ^ m[10];
-}
-
-
 // Shard-index CRC check by one workgroup with the pair tables (verify_index's
 // chain, four accumulators, folded, shifted by kthread11).
 // (`active` false: a second half-workgroup that only joins the barriers)
@@ -1999,13 +1976,15 @@ __device__ __forceinline__ uint32_t lanemul3_w(const uint32_t* s_mul, int t, uin
     return (q >> 2) ^ r2(q & 3u) ^ m[10];
 }
 
-template <int ITEM, bool SWAP, int NT>
+// LMR: the lane multiply in registers (lanemul_reg, VALU) instead of the LDS
+// column: the run end's LDS reads halve.
+template <int ITEM, bool SWAP, int NT, bool LMR = false>
 __global__ __launch_bounds__(NT) void k_decode_ilw(const DecodeParams p) {
     constexpr int KW = 2048 / NT;  // blocks per lane
     constexpr int QW = NT / 256;   // 4 KiB sub-steps per row of lanes
     constexpr int TV = (kPairTabWords / 4 + NT - 1) / NT;
     __shared__ uint32_t s_tab[kPairTabWords];
-    __shared__ uint32_t s_mul[12 * NT];
+    __shared__ uint32_t s_mul[LMR ? 1 : 12 * NT];
     __shared__ uint32_t s_red[2][NT / 64];
     const int t = threadIdx.x;
     const uint32_t G = gridDim.x, g = blockIdx.x;
@@ -2065,7 +2044,7 @@ __global__ __launch_bounds__(NT) void k_decode_ilw(const DecodeParams p) {
             const int ix = t + i * NT;
             if (ix < kPairTabWords / 4) stt[ix] = tv[i];
         }
-        lanemul3_init_w<NT>(s_mul, t, kl);
+        if constexpr (!LMR) lanemul3_init_w<NT>(s_mul, t, kl);
     }
     __syncthreads();
     stamp(p, g, t, 2);
@@ -2088,7 +2067,8 @@ __global__ __launch_bounds__(NT) void k_decode_ilw(const DecodeParams p) {
         }
         stamp(p, g, t, 3);
         // 4. run end: one chain per workgroup, one publication
-        uint32_t v = ok ? lanemul3_w<NT>(s_mul, t, fold4(s_tab, acc)) : 0u;
+        uint32_t v = ok ? (LMR ? lanemul_reg(kl, fold4(s_tab, acc)) : lanemul3_w<NT>(s_mul, t, fold4(s_tab, acc)))
+                        : 0u;
         v = wave_xor(v);
         if ((t & 63) == 0) s_red[0][t >> 6] = v;
         __syncthreads();
@@ -2108,9 +2088,17 @@ __global__ __launch_bounds__(NT) void k_decode_ilw(const DecodeParams p) {
         verify_index_pair(p, j, t, kix, s_tab, s_red[1], j == g, ipre, t < kThreads);
 }
 
+// production: 512 lanes, the LDS lane multiply (small grids, launch_decode);
+// the tuning build adds 1024 lanes and the register multiply
+KernelFn select_ilw_kernel(int item, bool swap, int nt, bool lmr) {  // CRC chains only
 #if ZHIP_TUNING
-KernelFn select_ilw_kernel(int item, bool swap, int nt) {  // CRC chains only
-#define ZHIP_ILW(I, W) (nt == 1024 ? k_decode_ilw<I, W, 1024> : k_decode_ilw<I, W, 512>)
+#define ZHIP_ILW(I, W)                                                                         \
+    (nt == 1024 ? (lmr ? k_decode_ilw<I, W, 1024, true> : k_decode_ilw<I, W, 1024>)            \
+                : (lmr ? k_decode_ilw<I, W, 512, true> : k_decode_ilw<I, W, 512>))
+#else
+    if (nt != 512 || lmr) return nullptr;
+#define ZHIP_ILW(I, W) k_decode_ilw<I, W, 512>
+#endif
     switch (item) {
         case 1: return ZHIP_ILW(1, false);
         case 2: return swap ? ZHIP_ILW(2, true) : ZHIP_ILW(2, false);
@@ -2121,6 +2109,7 @@ KernelFn select_ilw_kernel(int item, bool swap, int nt) {  // CRC chains only
 #undef ZHIP_ILW
 }
 
+#if ZHIP_TUNING
 KernelFn select_ilc_kernel(int item, bool swap) {  // CRC chains only
     switch (item) {
         case 1: return k_decode_ilc<1, false>;

@@ -482,6 +482,126 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
                          (same ? 1u << (sa & 31u) : 0u) | (1u << (sb & 31u)), same ? 2u : 1u, s_red[1], t);
 }
 
+// k_encode_il: k_decode_il in reverse (chunks whose 4 KiB steps tile into
+// groups of eight workgroups: the headline's 1 MiB chunks).  Workgroup r of
+// chunk c gathers the K = 8 steps st0 + 8 k (st0 = (r / 8) 64 + r % 8) of its
+// chunk -- rows from the row map, as k_encode_pair -- tests them against the
+// fill, stores them and carries their CRC through the A_(4096 * 8) 11/11/10
+// tables with k_decode_il's lane constants (the same plan tables: the CRC is
+// over the same stored bytes at the same positions).  One unit per workgroup
+// (2 048 on the headline instead of 1 024 pairs), so 32 workgroups publish
+// per chunk: CRC | arrival bits in the chunk's first 64-bit word (returning
+// xor, as k_decode_il), the non-empty bit in the line's second word -- a wave
+// with a non-fill element ORs it (returning) before its stores, and the
+// workgroup's publication waits for that OR, so the last arrival, which
+// exchanges the word for 0, sees every non-empty wave of the chunk.
+template <int ITEM, bool SWAP>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_encode_il(const EncodeParams p) {
+    constexpr int K = kDefaultBlocks;
+    __shared__ uint32_t s_tab[kPairTabWords];
+    __shared__ uint32_t s_mul[12 * kThreads];
+    __shared__ uint32_t s_red[kThreads / 64];
+    const int t = threadIdx.x;
+    const uint32_t g = blockIdx.x;
+    const uint32_t wpc = p.nseg, S = p.il_S;
+    const uint32_t c = g / wpc, r = g - c * wpc;
+    // 1. tables and the lane constant (the oldest loads), the chunk record and
+    //    the row map (scalar), then the gather loads
+    const uint4* gt = reinterpret_cast<const uint4*>(p.il_tab);
+    const uint4 tv0 = gt[t], tv1 = gt[t + kThreads], tv2 = gt[t + 2 * kThreads], tv3 = gt[t + 3 * kThreads],
+                tv4 = gt[t + 4 * kThreads], tv5 = gt[t + 5 * kThreads];
+    const uint32_t kl = p.il_klane[(size_t)r * kThreads + t];
+    const zhip_chunk ch = load_uniform<zhip_chunk>(p.chunks + c);
+    const uint32_t st0 = (r / S) * S * (uint32_t)K + (r % S);
+    const int32_t lo_frame = (int32_t)p.E - (int32_t)(p.nseg * p.seg);
+    zhip_rowblk m[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint32_t st = st0 + S * (uint32_t)k;
+        const uint32_t sidx = p.nseg - 1u - st / (uint32_t)K;
+        m[k] = load_uniform<zhip_rowblk>(p.rowmap + ((size_t)ch.sel * p.nseg + sidx) * K + (st % (uint32_t)K));
+    }
+    const uint32_t lane_row = (16u * (uint32_t)t) >> p.row_shift;
+    const uint32_t lane_col = (16u * (uint32_t)t) & ((1u << p.row_shift) - 1u);
+    const int64_t lane_off = (int64_t)lane_row * p.r_oy + (int64_t)lane_col;
+    const uint8_t* zero = reinterpret_cast<const uint8_t*>(g_enc_zero);
+    uint4 A[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const bool in = lane_row - m[k].lo < (uint32_t)(m[k].hi - m[k].lo);
+        A[k] = enc_load16(in ? p.arr + ch.out_off + m[k].rel + lane_off : zero);
+    }
+    // 2. tables into LDS, the lane-multiply column
+    {
+        uint4* stt = reinterpret_cast<uint4*>(s_tab);
+        stt[t] = tv0;
+        stt[t + kThreads] = tv1;
+        stt[t + 2 * kThreads] = tv2;
+        stt[t + 3 * kThreads] = tv3;
+        stt[t + 4 * kThreads] = tv4;
+        stt[t + 5 * kThreads] = tv5;
+        lanemul3_init(s_mul, t, kl);
+    }
+    // 3. fill test of the whole unit (chunk_is_empty, chunk_utils.py:74-85;
+    //    outside the selection = fill, _merge_chunk_array), the wave's
+    //    non-empty OR before its stores
+    const uint4 f = make_uint4(p.fill[0], p.fill[1], p.fill[2], p.fill[3]);
+    bool eq = true;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const bool in = lane_row - m[k].lo < (uint32_t)(m[k].hi - m[k].lo);
+        A[k] = in ? A[k] : f;
+        eq = eq && block_eq_fill<ITEM>(A[k], 16u, p);
+    }
+    uint64_t* const w = reinterpret_cast<uint64_t*>(p.ws) + (uint64_t)p.pub_stride * c;
+    uint64_t ne_prev = 0;
+    if (__any(!eq) && (t & 63) == 0)
+        ne_prev = __hip_atomic_fetch_or(w + 1, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();  // tables in LDS
+    // 4. byteswap, store, Horner step per block
+    uint8_t* const cp = p.dst + ch.src;
+    uint8_t* const sink = reinterpret_cast<uint8_t*>(g_enc_sink) + 16 * t;
+    Acc4 acc = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int32_t o = lo_frame + kWgStride * (int32_t)(st0 + S * (uint32_t)k);
+        const uint4 e = swap_block<ITEM, SWAP>(A[k]);
+        enc_store16(o >= 0 ? cp + o + 16 * t : sink, e);
+        if (o >= 0) crc_block4(s_tab, acc, e);
+    }
+    // 5. run end: one chain per workgroup, one publication
+    uint32_t v = wave_xor(lanemul3(s_mul, t, fold4(s_tab, acc)));
+    asm volatile("" ::"v"((uint32_t)ne_prev));  // the wave's non-empty OR has returned
+    if ((t & 63) == 0) s_red[t >> 6] = v;
+    __syncthreads();
+    if (t != 0) return;
+    const uint32_t V = s_red[0] ^ s_red[1] ^ s_red[2] ^ s_red[3];
+    const uint64_t bit = 1ull << r;
+    const uint64_t full = wpc >= 32u ? 0xFFFFFFFFull : ((1ull << wpc) - 1ull);
+    const uint64_t prev = __hip_atomic_fetch_xor(w, (bit << 32) | V, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (((prev >> 32) ^ bit) != full) return;
+    // the last arrival: trailer, status, non-empty flag; both words back to 0
+    const uint64_t ne = __hip_atomic_exchange(w + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(w, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    p.nonempty[c] = ne != 0ull ? 1u : 0u;
+    const uint32_t crc = ~(((uint32_t)prev ^ V) ^ p.c3);  // the lane constants carry c_inv
+    put_le_u32(p.dst + ch.src + p.g.nbytes, crc);         // LE trailer (crc32c_.py:64-68)
+    zhip_status st = {ZHIP_ST_OK, crc, crc, 0u};
+    p.status[c] = st;
+}
+
+using EncodeFn = void (*)(const EncodeParams);
+
+static EncodeFn pick_encode_il(int item, bool swap) {
+    switch (item) {
+        case 1: return k_encode_il<1, false>;
+        case 2: return swap ? k_encode_il<2, true> : k_encode_il<2, false>;
+        case 4: return swap ? k_encode_il<4, true> : k_encode_il<4, false>;
+        case 8: return swap ? k_encode_il<8, true> : k_encode_il<8, false>;
+        default: return nullptr;
+    }
+}
+
 // k_encode_quad: k_encode_pair for chunks of at most 16 KiB (one unit per
 // chunk; the reference example's 64 x 64 int32 inner chunks).  Such a unit's
 // first four steps lie before the chunk start, so the pair kernel gathers and
@@ -584,7 +704,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     }
 }
 
-using EncodeFn = void (*)(const EncodeParams);
 
 template <bool CRC, int ITEM>
 static EncodeFn pick_encode_quad_item(bool swap) {
@@ -670,7 +789,19 @@ int launch_encode(const EncodeParams& p, hipStream_t stream, int max_grid) {
         hipLaunchKernelGGL(fn, dim3((p.n_units + 3u) / 4u), dim3(kThreads), 0, stream, p);
         return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
     }
+    if (p.rowmap && p.seg == (uint32_t)kWgStride * kDefaultBlocks && !(p.tune & kTunePersist) && crc &&
+        p.il_S == 8u && p.nseg <= 32u && g_tune_arm != 34) {
+        // one unit per workgroup, steps interleaved in groups of eight (k_encode_il;
+        // tuning arm 34 keeps k_encode_pair)
+        EncodeFn fn = pick_encode_il(p.g.itemsize, swap);
+        if (!fn) return ZHIP_E_UNSUPPORTED;
+        if (p.n_units == 0) return ZHIP_OK;
+        g_last_kernel = "k_encode_il";
+        hipLaunchKernelGGL(fn, dim3(p.n_units), dim3(kThreads), 0, stream, p);
+        return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
+    }
     if (p.rowmap && p.seg == (uint32_t)kWgStride * kDefaultBlocks && !(p.tune & kTunePersist)) {
+        g_last_kernel = "k_encode_pair";
         EncodeFn fn = pick_encode_pair(crc, p.g.itemsize, swap);
         if (!fn) return ZHIP_E_UNSUPPORTED;
         if (p.n_units == 0) return ZHIP_OK;

@@ -381,6 +381,28 @@ __device__ __forceinline__ uint32_t r2(uint32_t n) {
     return ((n & 1u) ? rbasis(1, 2) : 0u) ^ ((n & 2u) ? rbasis(2, 2) : 0u);
 }
 
+// The lane's 12-entry window column of k in LDS (12 KiB for 256 lanes; the
+// 4-bit form needs 16), and the multiply over it (k_decode_il, k_encode_il).
+__device__ __forceinline__ void lanemul3_init(uint32_t* s_mul, int t, uint32_t k) {
+    const uint32_t k1 = mulx1_u(k), k2 = mulx1_u(k1);
+#pragma unroll
+    for (uint32_t v = 0; v < 8; ++v)
+        s_mul[v * kThreads + t] = ((v & 4u) ? k : 0u) ^ ((v & 2u) ? k1 : 0u) ^ ((v & 1u) ? k2 : 0u);
+#pragma unroll
+    for (uint32_t v = 0; v < 4; ++v) s_mul[(8u + v) * kThreads + t] = ((v & 2u) ? k : 0u) ^ ((v & 1u) ? k1 : 0u);
+}
+
+__device__ __forceinline__ uint32_t lanemul3(const uint32_t* s_mul, int t, uint32_t a) {
+    uint32_t m[11];
+#pragma unroll
+    for (int j = 0; j < 10; ++j) m[j] = s_mul[((a >> (3 * j)) & 7u) * kThreads + t];
+    m[10] = s_mul[(8u + (a >> 30)) * kThreads + t];
+    uint32_t q = m[0];
+#pragma unroll
+    for (int j = 1; j < 10; ++j) q = (q >> 3) ^ r3(q & 7u) ^ m[j];
+    return (q >> 2) ^ r2(q & 3u) ^ m[10];
+}
+
 // The window products selected in registers from k, kx, kx^2 (no LDS column):
 // ~130 VALU instructions once per run end instead of 11 LDS reads
 // (k_decode_il arms LM = 1 / 2, k_decode_tile4f).

@@ -49,6 +49,8 @@ struct GroupEnt {
 // and 10 high bits of a word, then the four byte slices of A4 (x^32).
 constexpr int kPairT1 = 0, kPairT2 = 2048, kPairT3 = 4096, kPairA4 = 5120;
 constexpr int kPairTabWords = 6144;
+extern const char* g_last_kernel;  // zhip_last_kernel: the kernel the last decode / mapped encode launched
+constexpr uint32_t kIlwMaxUnits = 512;  // k_decode_ilw (512 lanes) for grids of at most 2 units per CU
 constexpr int kIlBasisWords = 64;  // T1 / T2 / T3 bases (11 + 11 + 10, padded to 32), A4 bases (4 x 8)
 
 // What k_decode_lead (and the k_decode_il arm) need before their first vector loads,
@@ -317,6 +319,11 @@ struct EncodeParams {
     // 64-bit words between chunks' publication words (k_encode_pair / k_encode_tile4):
     // kPubLine / 2 for CRC layouts (a 128-byte line per chunk), else 2
     uint32_t pub_stride;
+    // k_encode_il: k_decode_il's interleave stride, tables and lane constants
+    // (0: not available for this plan)
+    uint32_t il_S;
+    const uint32_t* il_tab;
+    const uint32_t* il_klane;
 };
 
 struct PackParams {
