@@ -641,7 +641,7 @@ class _EncodeProg:
 
 
 def _encode_bench(device, args, codecs, want, chunks=(64, 64, 64), check=True):
-    """want: "rows" (k_encode_pair), "tile4" (k_encode_tile4) or "tile"
+    """want: "rows" (k_encode_il / k_encode_pair), "tile4" (k_encode_tile4) or "tile"
     (k_encode_tile, the general transposed encode)."""
     import torch
 
@@ -678,13 +678,14 @@ def _encode_bench(device, args, codecs, want, chunks=(64, 64, 64), check=True):
         progs.append(_EncodeProg(el))
         checks.append((store, arr, batch, offs, elen))
     wall, kern = time_programs(progs, max(10, args.steps // 2), 3, device)
+    kname = N.lib().zhip_last_kernel().decode()  # (mapped encodes; before the check's decodes)
     for store, arr, batch, offs, elen in (checks if check else []):  # (check=False: ablation arms)
         for (bg, *_), off in zip(batch, offs):
             store.register(bg.path, off, elen)
         if not torch.equal(arr.get((Ellipsis,)).view(torch.int32), data.view(torch.int32)):
             raise SystemExit("bench encode: decoded store differs from the source")
     src = data.numel() * 4
-    return src, wall, kern
+    return src, wall, kern, kname
 
 
 def encode_c3(device, args):
@@ -692,7 +693,7 @@ def encode_c3(device, args):
     bytes + crc32c into 64 chunks of 64^3 by k_encode_tile4 (four LDS tiles
     per workgroup), timed like the decode and decoded back for the check."""
     codecs = [{"name": "transpose", "configuration": {"order": [2, 1, 0]}}, LE, CRC]
-    src, wall, kern = _encode_bench(device, args, codecs, "tile4")
+    src, wall, kern, _ = _encode_bench(device, args, codecs, "tile4")
     return _entry(src, src + 64 * (1048576 + 4), wall, kern,
                   kernel="k_encode" if args.tune & 65536 else "k_encode_tile4", checked="bytes",
                   note="decoded_GiBps = source bytes encoded per second")
@@ -707,7 +708,7 @@ def encode_c3_general(device, args):
     k_encode at 0.05; --tune 65536 runs the one-group-per-workgroup general
     k_encode_tile instead)."""
     codecs = [{"name": "transpose", "configuration": {"order": [2, 1, 0]}}, LE, CRC]
-    src, wall, kern = _encode_bench(device, args, codecs, "tile", chunks=(128, 128, 128))
+    src, wall, kern, _ = _encode_bench(device, args, codecs, "tile", chunks=(128, 128, 128))
     return _entry(src, src + 8 * (128 ** 3 * 4 + 4), wall, kern,
                   kernel="k_encode_tile" if args.tune & 65536 else "k_encode_tileg", checked="bytes",
                   note="decoded_GiBps = source bytes encoded per second; 128^3 chunks")
@@ -716,13 +717,14 @@ def encode_c3_general(device, args):
 def encode_c2(device, args):
     """Encode side of C2 (a2/a4/a15): the 256^3 f32 device array written as 64
     chunks of 64^3 with bytes+crc32c into a DeviceStore arena -- gather 16-byte
-    rows, empty-chunk check, CRC, trailer -- by k_encode_pair, the launch
-    HipCodecPipeline.write_sync issues for complete chunks.  Timed like the
-    decode (graph replay of K launches); the stored bytes are then decoded back
-    and compared with the source."""
-    src, wall, kern = _encode_bench(device, args, [LE, CRC], "rows")
+    rows, empty-chunk check, CRC, trailer -- by k_encode_il (one 32 KiB unit
+    per workgroup, steps interleaved in groups of eight; k_encode_pair before
+    round 5), the launch HipCodecPipeline.write_sync issues for complete
+    chunks.  Timed like the decode (graph replay of K launches); the stored
+    bytes are then decoded back and compared with the source."""
+    src, wall, kern, kname = _encode_bench(device, args, [LE, CRC], "rows")
     return _entry(src, src + 64 * (1048576 + 4), wall, kern,
-                  kernel="k_encode" if args.tune & 64 else "k_encode_pair", checked="bytes",
+                  kernel="k_encode" if args.tune & 64 else kname, checked="bytes",
                   note="decoded_GiBps = source bytes encoded per second")
 
 

@@ -42,7 +42,7 @@ def main():
         aa, chunks, want, *crc = cfgs[name]  # q16n: no CRC codec
         tail = [bench.LE, bench.CRC] if not crc or crc[0] else [bench.LE]
         N.lib().zhip_set_tuning(6, int(arm or 0))
-        src, wall, kern = bench._encode_bench(dev, args, aa + tail, want, chunks=chunks,
+        src, wall, kern, _ = bench._encode_bench(dev, args, aa + tail, want, chunks=chunks,
                                               check=item not in os.environ.get("NOCHECK", "").split(","))
         N.lib().zhip_set_tuning(6, 0)
         print(json.dumps({"arm": item, "tune": tune, "us_graph": round(wall * 1e6, 2),

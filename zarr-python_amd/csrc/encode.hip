@@ -489,18 +489,21 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
 // fill, stores them and carries their CRC through the A_(4096 * 8) 11/11/10
 // tables with k_decode_il's lane constants (the same plan tables: the CRC is
 // over the same stored bytes at the same positions).  One unit per workgroup
-// (2 048 on the headline instead of 1 024 pairs), so 32 workgroups publish
-// per chunk: CRC | arrival bits in the chunk's first 64-bit word (returning
-// xor, as k_decode_il), the non-empty bit in the line's second word -- a wave
-// with a non-fill element ORs it (returning) before its stores, and the
-// workgroup's publication waits for that OR, so the last arrival, which
-// exchanges the word for 0, sees every non-empty wave of the chunk.
+// (2 048 on the headline instead of 1 024 pairs).  Publication without extra
+// same-address atomics (a non-empty OR per wave doubled the launch): the
+// chunk's workgroups split into halves of at most 16, each half publishing
+// CRC | arrival bits 32..47 | non-empty bits 48..63 in one 64-bit word (the
+// pair kernel's format); the last arrival of a half folds the half's word into
+// the line's third word the same way (bits 32 / 48 + half), and the last of
+// those writes trailer, status and the non-empty flag.  Chunks of at most 16
+// units have one half and no second level.
 template <int ITEM, bool SWAP>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_encode_il(const EncodeParams p) {
     constexpr int K = kDefaultBlocks;
     __shared__ uint32_t s_tab[kPairTabWords];
     __shared__ uint32_t s_mul[12 * kThreads];
     __shared__ uint32_t s_red[kThreads / 64];
+    __shared__ uint32_t s_ne[kThreads / 64];
     const int t = threadIdx.x;
     const uint32_t g = blockIdx.x;
     const uint32_t wpc = p.nseg, S = p.il_S;
@@ -542,50 +545,56 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))
         stt[t + 5 * kThreads] = tv5;
         lanemul3_init(s_mul, t, kl);
     }
-    // 3. fill test of the whole unit (chunk_is_empty, chunk_utils.py:74-85;
-    //    outside the selection = fill, _merge_chunk_array), the wave's
-    //    non-empty OR before its stores
+    __syncthreads();
+    // 3. per block: fill test (chunk_is_empty, chunk_utils.py:74-85; outside
+    //    the selection = fill, _merge_chunk_array), byteswap, store, Horner step
     const uint4 f = make_uint4(p.fill[0], p.fill[1], p.fill[2], p.fill[3]);
-    bool eq = true;
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-        const bool in = lane_row - m[k].lo < (uint32_t)(m[k].hi - m[k].lo);
-        A[k] = in ? A[k] : f;
-        eq = eq && block_eq_fill<ITEM>(A[k], 16u, p);
-    }
-    uint64_t* const w = reinterpret_cast<uint64_t*>(p.ws) + (uint64_t)p.pub_stride * c;
-    uint64_t ne_prev = 0;
-    if (__any(!eq) && (t & 63) == 0)
-        ne_prev = __hip_atomic_fetch_or(w + 1, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();  // tables in LDS
-    // 4. byteswap, store, Horner step per block
     uint8_t* const cp = p.dst + ch.src;
     uint8_t* const sink = reinterpret_cast<uint8_t*>(g_enc_sink) + 16 * t;
     Acc4 acc = {0u, 0u, 0u, 0u};
+    bool eq = true;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         const int32_t o = lo_frame + kWgStride * (int32_t)(st0 + S * (uint32_t)k);
-        const uint4 e = swap_block<ITEM, SWAP>(A[k]);
+        const bool in = lane_row - m[k].lo < (uint32_t)(m[k].hi - m[k].lo);
+        const uint4 v = in ? A[k] : f;
+        eq = eq && block_eq_fill<ITEM>(v, 16u, p);
+        const uint4 e = swap_block<ITEM, SWAP>(v);
         enc_store16(o >= 0 ? cp + o + 16 * t : sink, e);
         if (o >= 0) crc_block4(s_tab, acc, e);
     }
-    // 5. run end: one chain per workgroup, one publication
-    uint32_t v = wave_xor(lanemul3(s_mul, t, fold4(s_tab, acc)));
-    asm volatile("" ::"v"((uint32_t)ne_prev));  // the wave's non-empty OR has returned
-    if ((t & 63) == 0) s_red[t >> 6] = v;
+    // 4. run end: one chain per workgroup, one publication
+    const uint32_t v = wave_xor(lanemul3(s_mul, t, fold4(s_tab, acc)));
+    const bool wave_ne = __any(!eq);
+    if ((t & 63) == 0) {
+        s_red[t >> 6] = v;
+        s_ne[t >> 6] = wave_ne ? 1u : 0u;
+    }
     __syncthreads();
     if (t != 0) return;
     const uint32_t V = s_red[0] ^ s_red[1] ^ s_red[2] ^ s_red[3];
-    const uint64_t bit = 1ull << r;
-    const uint64_t full = wpc >= 32u ? 0xFFFFFFFFull : ((1ull << wpc) - 1ull);
-    const uint64_t prev = __hip_atomic_fetch_xor(w, (bit << 32) | V, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (((prev >> 32) ^ bit) != full) return;
-    // the last arrival: trailer, status, non-empty flag; both words back to 0
-    const uint64_t ne = __hip_atomic_exchange(w + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(w, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    p.nonempty[c] = ne != 0ull ? 1u : 0u;
-    const uint32_t crc = ~(((uint32_t)prev ^ V) ^ p.c3);  // the lane constants carry c_inv
-    put_le_u32(p.dst + ch.src + p.g.nbytes, crc);         // LE trailer (crc32c_.py:64-68)
+    const bool ne = (s_ne[0] | s_ne[1] | s_ne[2] | s_ne[3]) != 0u;
+    uint64_t* const w = reinterpret_cast<uint64_t*>(p.ws) + (uint64_t)p.pub_stride * c;
+    const uint32_t h = r >> 4, b = r & 15u;
+    const uint32_t n_h = h ? wpc - 16u : (wpc < 16u ? wpc : 16u);  // workgroups of this half
+    const uint64_t bit = 1ull << b;
+    const uint64_t word = (bit << 32) | (ne ? bit << 48 : 0ull) | V;
+    const uint64_t prev = __hip_atomic_fetch_xor(w + h, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((((prev ^ word) >> 32) & 0xFFFFull) != (1ull << n_h) - 1ull) return;
+    __hip_atomic_store(w + h, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint64_t all = prev ^ word;  // the half: CRC | arrivals | non-empty bits
+    if (wpc > 16u) {  // second level: the halves into the line's third word
+        const uint64_t hb = 1ull << h;
+        const uint64_t w2 = (hb << 32) | ((all >> 48) ? hb << 48 : 0ull) | (uint32_t)all;
+        const uint64_t p2 = __hip_atomic_fetch_xor(w + 2, w2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((((p2 ^ w2) >> 32) & 0xFFFFull) != 3ull) return;
+        __hip_atomic_store(w + 2, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        all = p2 ^ w2;
+    }
+    // the chunk's last arrival: trailer, status, non-empty flag
+    p.nonempty[c] = (all >> 48) != 0ull ? 1u : 0u;
+    const uint32_t crc = ~((uint32_t)all ^ p.c3);   // the lane constants carry c_inv
+    put_le_u32(p.dst + ch.src + p.g.nbytes, crc);  // LE trailer (crc32c_.py:64-68)
     zhip_status st = {ZHIP_ST_OK, crc, crc, 0u};
     p.status[c] = st;
 }
