@@ -399,9 +399,10 @@ int zhip_decode_mapped(const zhip_plan *plan, const void *src, uint64_t src_size
 int zhip_tuning_build(void);
 int zhip_set_tuning(int key, int value);
 
-/* Name of the decode kernel the last zhip_decode* call on this process
- * launched ("k_decode_il", "k_decode_pair", "k_decode_lead", ...): a
- * diagnostic for labels and tests; not synchronised across threads. */
+/* Name of the kernel the last zhip_decode* (or row-mapped zhip_encode_mapped)
+ * call on this process launched ("k_decode_il", "k_decode_ilw512",
+ * "k_decode_pair", "k_decode_lead", "k_encode_il", ...): a diagnostic for
+ * labels and tests; not synchronised across threads. */
 const char *zhip_last_kernel(void);
 
 /* Diagnostics: with ablation bit 1024 set, k_decode_pair records per-workgroup

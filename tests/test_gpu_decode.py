@@ -1177,13 +1177,16 @@ def test_ilq_arms_exact_and_crc(device, arm, sharded):
 
 
 @pytest.mark.tuning
+@pytest.mark.parametrize("arm", [25, 35])
 @pytest.mark.parametrize("loc", ["end", "start"])
 @pytest.mark.parametrize("sharded", [False, True])
-def test_ilc_arm_exact_and_crc(device, monkeypatch, sharded, loc):
+def test_ilc_arm_exact_and_crc(device, monkeypatch, sharded, loc, arm):
     """k_decode_ilc (ZHIP_TUNE_ARM 25: CRC tables computed in LDS from 64 basis
-    words, predicted loads issued before the index resolves) decodes exactly,
-    reloads when the prediction misses (misaligned repacked shards), and
-    reports corrupted chunks and indexes with the reference's messages."""
+    words, predicted loads issued before the index resolves) and k_decode_ilp
+    (35: the index entry checked after the stores) decode exactly, redo the
+    unit when the prediction misses (misaligned repacked shards, an elided
+    inner chunk), and report corrupted chunks and indexes with the
+    reference's messages."""
     import zarr_hip
     import zarr_hip.pipeline as P
     from zarr_hip import _native as N
@@ -1197,15 +1200,17 @@ def test_ilc_arm_exact_and_crc(device, monkeypatch, sharded, loc):
     O.write(host, meta, (Ellipsis,), _data(shape, "float32"))
     if not sharded:
         host.pop("c/1/0/0")
-    set_tuning(6, 25)
+    kname = "k_decode_ilc" if arm == 25 else "k_decode_ilp"
+    set_tuning(6, arm)
     try:
         store = zarr_hip.DeviceStore.from_host(host, device)
         arr = zarr_hip.Array.create(store, shape, cshape, "float32", 1.5, codecs=codecs)
         for sel in [(Ellipsis,), (slice(16, 100), slice(0, 128), slice(0, 64))]:
             prog, out = arr.prepare_read(sel)
+            assert prog.tables.predict is not None or arm == 25
             prog.launch()
             prog.results()
-            assert N.lib().zhip_last_kernel().decode() == "k_decode_ilc"
+            assert N.lib().zhip_last_kernel().decode() == kname
             assert out.cpu().numpy().tobytes() == np.ascontiguousarray(O.read(host, meta, sel)).tobytes()
         key = "c/0/0/0" if sharded else "c/0/1/0"
         for at in ([700001, len(host[key]) - 40 if loc == "end" else 20] if sharded else [700001]):
@@ -1229,8 +1234,19 @@ def test_ilc_arm_exact_and_crc(device, monkeypatch, sharded, loc):
             marr = zarr_hip.Array.create(zarr_hip.DeviceStore.from_host(mhost, device), shape, cshape, "float32",
                                          1.5, codecs=codecs)
             got = marr[...]
-            assert N.lib().zhip_last_kernel().decode() == "k_decode_ilc"
+            assert N.lib().zhip_last_kernel().decode() == kname
             assert got.tobytes() == O.read(host, meta).tobytes()
+            # an inner chunk entirely fill is elided (the index says missing) and
+            # the chunks after it move: every later guess misses
+            d2 = _data(shape, "float32")
+            d2[0:64, 0:64, :] = 1.5
+            h2 = {}
+            O.write(h2, meta, (Ellipsis,), d2)
+            earr = zarr_hip.Array.create(zarr_hip.DeviceStore.from_host(h2, device), shape, cshape, "float32",
+                                         1.5, codecs=codecs)
+            got = earr[...]  # (no prediction when a blob is shorter than packed: k_decode_il then)
+            assert N.lib().zhip_last_kernel().decode() in (kname, "k_decode_il")
+            assert got.tobytes() == O.read(h2, meta).tobytes()
     finally:
         set_tuning(6, 0)
 

@@ -504,6 +504,7 @@ KernelFn select_il_kernel_regmul(bool crc, int item, bool swap, bool occ6);  // 
 KernelFn select_xw_kernel(bool crc, int item, bool swap);            // decode_rows.hip
 KernelFn select_ilq_kernel(int item, bool swap, int nq, bool glds);  // decode_rows.hip
 KernelFn select_ilc_kernel(int item, bool swap);                     // decode_rows.hip
+KernelFn select_ilp_kernel(int item, bool swap);                     // decode_rows.hip
 KernelFn select_tile4f_kernel(int item, bool swap);                  // decode_tile.hip
 #endif
 KernelFn select_tile4_kernel(bool crc, int item, bool swap);         // decode_tile.hip
@@ -634,6 +635,15 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
             g_last_kernel = p.ilw_nt == 1024u ? (g_tune_arm >= 31 ? "k_decode_ilw1024r" : "k_decode_ilw1024")
                                               : (g_tune_arm >= 31 ? "k_decode_ilw512r" : "k_decode_ilw512");
             hipLaunchKernelGGL(wfn, dim3(wgrid), dim3(p.ilw_nt), 0, stream, p);
+            return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
+        }
+        if (il && g_tune_arm == 35 && p.pred) {  // k_decode_ilp: index entry off the stores' path
+            KernelFn pfn = select_ilp_kernel(p.g.itemsize, swap);
+            if (!pfn) return ZHIP_E_UNSUPPORTED;
+            const uint32_t igrid = p.n_units > p.n_idx ? p.n_units : p.n_idx;
+            if (igrid == 0) return ZHIP_OK;
+            g_last_kernel = "k_decode_ilp";
+            hipLaunchKernelGGL(pfn, dim3(igrid), dim3(kThreads), 0, stream, p);
             return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
         }
         if (il && g_tune_arm == 25) {  // k_decode_ilc: tables built in LDS, predicted loads first

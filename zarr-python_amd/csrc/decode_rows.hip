@@ -1944,6 +1944,165 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))
 }
 
 // ---------------------------------------------------------------------------
+// k_decode_ilp: k_decode_ilc with the shard-index entry OFF the stores' path.
+// k_decode_ilc / the lean prologue issue the data at the predicted address
+// first but still resolve the unit (chunk record -> index entry, a cold HBM
+// read behind the data flood) before storing.  Here the stores need only the
+// chunk record and the row map (small hot tables); the index entry and the
+// predicted trailer are VECTOR loads issued after the data (so waiting for the
+// data never waits for them), checked after the Horner steps: a wrong guess,
+// an index-missing or failing inner chunk redoes the unit on a slow path
+// (drain, reload or fill, restore, re-hash).  launch_decode admits it only
+// with a prediction (zhip_predict).
+template <int ITEM, bool SWAP>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_decode_ilp(
+    const DecodeParams p) {
+    constexpr int K = kDefaultBlocks;
+    __shared__ uint32_t s_tab[kPairTabWords];
+    __shared__ uint32_t s_mul[12 * kThreads];
+    __shared__ uint32_t s_red[2][kThreads / 64];
+    const int t = threadIdx.x;
+    PairHot h = p.h;
+    pair_hot(h);
+    il_hot(h);
+    const uint32_t G = gridDim.x, g = blockIdx.x;
+    const uint32_t wpc = h.nseg, S = h.il_S;
+    const uint32_t c = fdiv_apply(g, h.d_nseg.m, h.d_nseg.s);
+    const uint32_t r = g - c * wpc;
+    const bool has = c < h.n_chunks;
+    if (!has && g >= h.n_idx) return;
+    stamp(p, g, t, 0);
+    const uint32_t expected = p.g.nbytes + 4u;
+    const uint8_t* zero = reinterpret_cast<const uint8_t*>(g_rows_zero);
+    const uint32_t ls = (uint32_t)__builtin_ctz(S);
+    const uint32_t st0 = ((r >> ls) << ls) * (uint32_t)K + (r & (S - 1u));
+    const int32_t lo_frame = (int32_t)h.E - (int32_t)(h.nseg * h.seg);
+    // 1. the data at the predicted address, first
+    const uint32_t grp = fdiv_apply(c, h.d_per.m, h.d_per.s);
+    const uint8_t* const cpp = reinterpret_cast<const uint8_t*>(h.src) + h.pred_base + (uint64_t)grp * h.pred_outer +
+                               (uint64_t)(c - grp * h.pred_per) * h.pred_inner;
+    uint4 A[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int32_t base = lo_frame + kWgStride * (int32_t)(st0 + S * (uint32_t)k);
+        A[k] = load_stream16_any(has && base >= 0 ? cpp + base + 16 * t : zero);
+    }
+    stamp(p, g, t, 1);
+    // 2. the chunk record and the row map (scalar, hot), the lane constants,
+    //    the index entry and the predicted trailer (vector, after the data)
+    zhip_chunk ch = {};
+    if (has) ch = load_uniform<zhip_chunk>(p.chunks + c);
+    const uint32_t kl = load_u32_any(reinterpret_cast<const uint8_t*>(
+        reinterpret_cast<const uint32_t*>(h.il_klane) + (size_t)(has ? r : 0u) * kThreads + t));
+    const uint32_t kix = load_u32_any(reinterpret_cast<const uint8_t*>(reinterpret_cast<const uint32_t*>(h.il_kidx) + t));
+    const bool sharded = (p.lflags & ZHIP_LF_SHARDED) != 0;
+    const bool ch_missing = (ch.flags & ZHIP_CF_MISSING) != 0;
+    const uint64_t ipos = (p.lflags & ZHIP_LF_INDEX_START) ? 0ull : ch.src_len - p.index_size;
+    const uint4 ie = load16_any(has && sharded && !ch_missing ? p.src + ch.src + ipos + 16ull * ch.slot : zero);
+    const uint32_t trp = load_u32_any(has ? cpp + p.g.nbytes : zero);
+    const uint4 ipre = index_prefetch(p, g, g < h.n_idx, t, zero);
+    zhip_rowblk m[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint32_t st = st0 + S * (uint32_t)k;
+        const uint32_t sidx = h.nseg - 1u - st / (uint32_t)K;
+        m[k] = load_uniform<zhip_rowblk>(p.rowmap + ((size_t)ch.sel * h.nseg + sidx) * K + (st % (uint32_t)K));
+    }
+    // 3. tables built in LDS, the lane-multiply column
+    build_il_tables_lds(s_tab, t, p.il_basis);
+    lanemul3_init(s_mul, t, kl);
+    __syncthreads();
+    stamp(p, g, t, 2);
+    uint8_t* sink = reinterpret_cast<uint8_t*>(g_rows_sink);
+    const uint32_t lane_row = (16u * (uint32_t)t) >> p.row_shift;
+    const uint32_t lane_col = (16u * (uint32_t)t) & ((1u << p.row_shift) - 1u);
+    const int64_t lane_off = (int64_t)lane_row * p.r_oy + (int64_t)lane_col;
+    uint8_t* const obase = p.out + ch.out_off;
+    const uint4 f = make_uint4(p.fill[0], p.fill[1], p.fill[2], p.fill[3]);
+    Acc4 acc = {0u, 0u, 0u, 0u};
+    if (has) {
+        // 4. stores and Horner steps of the predicted data (a chunk the chunk
+        //    record marks missing: fill)
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint32_t lo = m[k].lo, hi = m[k].hi;
+            const bool wr = lane_row - lo < hi - lo;
+            store_nt16(wr ? obase + m[k].rel + lane_off : sink, ch_missing ? f : swap_block<ITEM, SWAP>(A[k]));
+            if (!ch_missing) crc_block4(s_tab, acc, A[k]);
+        }
+    }
+    stamp(p, g, t, 3);
+    // 5. the unit as resolve_unit sees it (zhip_decode_common.h), from the
+    //    vector-loaded entry
+    uint32_t mode = ch_missing ? (uint32_t)ZHIP_ST_MISSING : (uint32_t)ZHIP_ST_OK;
+    uint64_t base = ch.src;
+    if (has && !ch_missing) {
+        if (sharded) {
+            const uint64_t off = ((uint64_t)__builtin_amdgcn_readfirstlane(ie.y) << 32) |
+                                 __builtin_amdgcn_readfirstlane(ie.x);
+            const uint64_t len = ((uint64_t)__builtin_amdgcn_readfirstlane(ie.w) << 32) |
+                                 __builtin_amdgcn_readfirstlane(ie.z);
+            if (off == ~0ull && len == ~0ull) mode = ZHIP_ST_MISSING;
+            else if (u64_gt(off, ch.src_len) || u64_gt(len, ch.src_len - off)) mode = ZHIP_ST_INDEX_OOB;
+            else if (len != expected) mode = ZHIP_ST_LENGTH_MISMATCH;
+            else base = ch.src + off;
+        } else if (ch.src_len != expected) {
+            mode = ZHIP_ST_LENGTH_MISMATCH;
+        }
+    }
+    const uint8_t* const cp = p.src + base;
+    const bool ok = has && mode == ZHIP_ST_OK;
+    uint32_t stored = __builtin_amdgcn_readfirstlane(trp);
+    if (has && !ch_missing && !(ok && cp == cpp)) {
+        // a wrong guess, or the index says missing / fails: redo the unit
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the predicted stores are out
+        acc = {0u, 0u, 0u, 0u};
+        if (ok) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int32_t b2 = lo_frame + kWgStride * (int32_t)(st0 + S * (uint32_t)k);
+                A[k] = load_stream16_any(b2 >= 0 ? cp + b2 + 16 * t : zero);
+            }
+            stored = load_trailer_uniform(cp, p.g.nbytes);
+        }
+        const bool fill = mode == ZHIP_ST_MISSING;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint32_t lo = m[k].lo, hi = m[k].hi;
+            const bool wr = (ok || fill) && lane_row - lo < hi - lo;
+            store_nt16(wr ? obase + m[k].rel + lane_off : sink, ok ? swap_block<ITEM, SWAP>(A[k]) : f);
+            if (ok) crc_block4(s_tab, acc, A[k]);
+        }
+    }
+    if (has) {
+        // 6. run end: one chain per workgroup, one publication
+        uint32_t v = ok ? lanemul3(s_mul, t, fold4(s_tab, acc)) : 0u;
+        v = wave_xor(v);
+        if ((t & 63) == 0) s_red[0][t >> 6] = v;
+        __syncthreads();
+        if (ok && t < 64) {
+            const uint32_t V = __builtin_amdgcn_readfirstlane(s_red[0][0] ^ s_red[0][1] ^ s_red[0][2] ^ s_red[0][3]);
+            stamp(p, g, t, 4);
+            publish_il(p, c, r, wpc, V, stored, t, kPubLine / 2u);
+        }
+        if (r == 0) {
+            Unit U;
+            U.c = c;
+            U.sidx = 0;
+            U.mode = mode;
+            U.cp = cp;
+            U.seg_lo = 0;
+            U.sel = ch.sel;
+            U.out_off = ch.out_off;
+            unit_status_pair(p, U, true, t);
+        }
+    }
+    stamp(p, g, t, 7);
+    // 7. fused shard-index checks (one step per lane), the first block prefetched
+    for (uint32_t j = g; j < h.n_idx; j += G) verify_index_pair(p, j, t, kix, s_tab, s_red[1], j == g, ipre);
+}
+
+// ---------------------------------------------------------------------------
 // k_decode_ilw: small shares (below ~2 workgroups per CU: the N = 4 / 8 shares
 // of the strong-scaled headline).  k_decode_il there runs ONE 4-wave
 // workgroup per CU, each lane's eight Horner steps in series with nothing to
@@ -2110,6 +2269,16 @@ KernelFn select_ilw_kernel(int item, bool swap, int nt, bool lmr) {  // CRC chai
 }
 
 #if ZHIP_TUNING
+KernelFn select_ilp_kernel(int item, bool swap) {  // CRC chains only
+    switch (item) {
+        case 1: return k_decode_ilp<1, false>;
+        case 2: return swap ? k_decode_ilp<2, true> : k_decode_ilp<2, false>;
+        case 4: return swap ? k_decode_ilp<4, true> : k_decode_ilp<4, false>;
+        case 8: return swap ? k_decode_ilp<8, true> : k_decode_ilp<8, false>;
+        default: return nullptr;
+    }
+}
+
 KernelFn select_ilc_kernel(int item, bool swap) {  // CRC chains only
     switch (item) {
         case 1: return k_decode_ilc<1, false>;
