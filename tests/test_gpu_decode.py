@@ -1198,7 +1198,7 @@ def test_ilc_arm_exact_and_crc(device, monkeypatch, sharded, loc, arm):
     meta = O.ArrayMeta(shape, cshape, np.dtype("float32"), 1.5, codecs=codecs)
     host = {}
     O.write(host, meta, (Ellipsis,), _data(shape, "float32"))
-    if not sharded:
+    if not sharded and arm == 25:  # (a missing chunk turns the prediction off: k_decode_ilp needs it)
         host.pop("c/1/0/0")
     kname = "k_decode_ilc" if arm == 25 else "k_decode_ilp"
     set_tuning(6, arm)
