@@ -164,3 +164,67 @@ def test_random_host_reads_large(device, tmp_path, seed):
         got = arr[sel]
         assert got.shape == want.shape
         assert got.tobytes() == np.ascontiguousarray(want).tobytes(), (sel, shape, chunks, codecs)
+
+
+def _il_case(seed):
+    """Whole-row chunks of 256 KiB - 1 MiB (steps that tile into groups of eight
+    workgroups): the k_decode_il / k_decode_ilw512 / k_encode_il geometry, with
+    random dtype, endianness, sharding, fill, edge chunks and selections."""
+    rng = np.random.default_rng(9000 + seed)
+    dtype = str(rng.choice(["float32", "int16", "float64", "uint8", "int32"]))
+    it = np.dtype(dtype).itemsize
+    row = int(rng.choice([128, 256, 512]))          # bytes per innermost row
+    c = row // it
+    b = int(rng.choice([32, 64]))                   # rows per plane (a multiple of 4096 / row)
+    chunk_bytes = int(rng.choice([256, 512, 1024])) << 10
+    a = chunk_bytes // (b * row)
+    chunks = (a, b, c)
+    sharded = rng.random() < 0.4
+    per = tuple(int(rng.integers(1, 3)) for _ in range(3)) if sharded else (1, 1, 1)
+    outer = tuple(ch * p for ch, p in zip(chunks, per))
+    shape = tuple(int(o * rng.integers(1, 3) - (0 if rng.random() < 0.6 else rng.integers(1, ch)))
+                  for o, ch in zip(outer, chunks))
+    while int(np.prod(shape)) * it > (24 << 20):  # keep the oracle fast
+        shape = (max(1, shape[0] // 2),) + shape[1:]
+    endian = BE if (it > 1 and rng.random() < 0.3) else LE
+    chain = [endian, CRC]
+    codecs = [SHARD(chunks, chain, str(rng.choice(["end", "start"])))] if sharded else chain
+    fill = float("nan") if (np.dtype(dtype).kind == "f" and rng.random() < 0.3) else (7 if rng.random() < 0.3 else 0)
+    return rng, shape, outer, dtype, codecs, fill
+
+
+@pytest.mark.parametrize("seed", range(int(os.environ.get("ZARR_HIP_FUZZ_IL", "16"))))
+def test_random_il_geometry(device, seed):
+    import zarr_hip
+
+    rng, shape, chunks, dtype, codecs, fill = _il_case(seed)
+    meta = O.ArrayMeta(shape, chunks, np.dtype(dtype), fill, codecs=codecs)
+    host = {}
+    store = zarr_hip.DeviceStore(device) if seed % 2 == 0 else zarr_hip.MemoryStore()
+    arr = zarr_hip.Array.create(store, shape, chunks, dtype, fill, codecs=codecs)
+
+    def check_store():
+        got = {k: bytes(v) for k, v in store.to_dict().items() if not k.endswith("zarr.json")}
+        assert sorted(got) == sorted(host), (shape, chunks, codecs)
+        for k in host:
+            assert got[k] == host[k], (k, shape, chunks, codecs)
+
+    data = _data(shape, dtype, seed)
+    # one chunk-sized region entirely fill (an elided chunk / inner chunk)
+    data[tuple(slice(0, min(s, ch)) for s, ch in zip(shape, (chunks if not isinstance(codecs[0], dict)
+                                                             or codecs[0]["name"] != "sharding_indexed"
+                                                             else codecs[0]["configuration"]["chunk_shape"])))] = fill
+    O.write(host, meta, (Ellipsis,), data)
+    arr[...] = data
+    check_store()
+    sel = _rand_sel(rng, shape)
+    want_shape = O.read(host, meta, sel).shape
+    val = _data(want_shape, dtype, seed + 7) if want_shape else _data((1,), dtype, seed + 7)[0]
+    O.write(host, meta, sel, val)
+    arr[sel] = val
+    check_store()
+    for sel in [(Ellipsis,), _rand_sel(rng, shape), _rand_sel(rng, shape)]:
+        want = O.read(host, meta, sel)
+        got = arr[sel]
+        assert got.shape == want.shape, (sel, shape, chunks, codecs)
+        assert got.tobytes() == np.ascontiguousarray(want).tobytes(), (sel, shape, chunks, codecs)
