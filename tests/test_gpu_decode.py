@@ -426,11 +426,12 @@ def test_transpose_tile4_crc_mismatch(device):
 def test_transpose_tile4f_chain(device, dtype, endian, chunks, shape):
     """The k_decode_tile4f arm (kTuneTile4F, bit 31: the four tiles of a
     workgroup are 1 KiB of every stored row, one A_64 chain per thread) decodes
-    exactly what the oracle wrote; without the bit k_decode_tile4w runs."""
+    exactly what the oracle wrote; without the bit k_decode_tile4w (its
+    two-tile form) runs."""
     from zarr_hip import _native as N
 
     _roundtrip(device, shape, chunks, dtype, [T((2, 1, 0)), endian, CRC])
-    assert N.lib().zhip_last_kernel() == b"k_decode_tile4w"
+    assert N.lib().zhip_last_kernel() == b"k_decode_tile2w"
     set_tuning(2, -(1 << 31))
     try:
         # every case: 256-byte stored rows, one 64-row tile along the transposed dim
@@ -904,8 +905,9 @@ def _il_array(device, fill=0.0, kind="il"):
 # (kind, ZHIP_TUNE_ARM): k_decode_il's returning publication (arm 33 keeps
 # k_decode_il on this small grid), its deferred-verdict arm, the small-grid
 # production k_decode_ilw512, and the deferred verdicts of k_decode_tilegw
+# (production: its two-tile form k_decode_tileg2w; arm 38 keeps four tiles)
 # (production) and k_decode_tileg (arm 5)
-VERDICT_CASES = [("il", 33), ("il", 2), ("ilw512", 0), ("tilegw", 0), ("tileg", 5)]
+VERDICT_CASES = [("il", 33), ("il", 2), ("ilw512", 0), ("tileg2w", 0), ("tilegw", 38), ("tileg", 5)]
 
 
 @pytest.fixture
@@ -1080,7 +1082,7 @@ def test_il_arms_exact_and_crc(device, arm):
 
 
 @pytest.mark.tuning
-@pytest.mark.parametrize("kind", ["tilegw", "tileg"])
+@pytest.mark.parametrize("kind", ["tileg2w", "tilegw", "tileg"])
 def test_c_abi_default_reports_mismatch_each_launch(device, kind):
     """A C caller that does not opt in to deferred verdicts (no ZHIP_DF_DEFER,
     never ZHIP_DF_BANK1) gets the documented zhip_decode contract from the
@@ -1090,7 +1092,7 @@ def test_c_abi_default_reports_mismatch_each_launch(device, kind):
     from zarr_hip import _native as N
 
     arr, store, host, meta = _il_array(device, kind="tileg")
-    set_tuning(6, 5 if kind == "tileg" else 0)
+    set_tuning(6, {"tileg": 5, "tilegw": 38, "tileg2w": 0}[kind])
     try:
         prog, out = arr.prepare_read((Ellipsis,))
         d = prog.data
@@ -1307,18 +1309,19 @@ def test_ilw_arms_exact_and_crc(device, arm, case):
 
 
 @pytest.mark.tuning
-@pytest.mark.parametrize("arm", [0, 5])
+@pytest.mark.parametrize("arm", [0, 5, 37, 38])
 @pytest.mark.parametrize("dtype,endian,chunks,shape", TILE4_CASES)
 def test_transpose_tile4w_and_tile4(device, dtype, endian, chunks, shape, arm):
-    """k_decode_tile4w (production for CRC layouts: a wave per tile, one
-    A_(4 sq) chain per lane) and k_decode_tile4 (ZHIP_TUNE_ARM = 5) decode
-    exactly what the oracle wrote and report a corrupted chunk with the
-    reference's message."""
+    """k_decode_tile4w's two-tile form (production for CRC layouts of at most
+    64 tiles per chunk: two waves per tile, one A_(4 sq) chain per lane),
+    its one- and four-tile forms (ZHIP_TUNE_ARM 37 / 38) and k_decode_tile4
+    (5) decode exactly what the oracle wrote and report a corrupted chunk
+    with the reference's message."""
     import zarr_hip
     from zarr_hip import _native as N
 
     codecs = [T((2, 1, 0)), endian, CRC]
-    kernel = b"k_decode_tile4" if arm else b"k_decode_tile4w"
+    kernel = {0: b"k_decode_tile2w", 5: b"k_decode_tile4", 37: b"k_decode_tile1w", 38: b"k_decode_tile4w"}[arm]
     set_tuning(6, arm)
     try:
         _roundtrip(device, shape, chunks, dtype, codecs)
@@ -1343,20 +1346,20 @@ def test_transpose_tile4w_and_tile4(device, dtype, endian, chunks, shape, arm):
 
 
 @pytest.mark.tuning
-@pytest.mark.parametrize("arm", [0, 5])
+@pytest.mark.parametrize("arm", [0, 5, 38])
 @pytest.mark.parametrize("order", [(2, 1, 0), (1, 2, 0), (0, 2, 1)])
 @pytest.mark.parametrize("dtype,endian", [("float32", LE), ("int16", BE), ("float64", LE), ("uint8", LE)])
 def test_transpose_tilegw_and_tileg(device, order, dtype, endian, arm):
-    """k_decode_tilegw (production for grouped CRC layouts: k_decode_tileg
-    with a wave per tile and one A_(4 sq) chain per lane; partial tiles load
-    zeros) and k_decode_tileg (ZHIP_TUNE_ARM = 5) decode exactly what the
-    oracle wrote, fill missing chunks and report a corrupted chunk with the
-    reference's message."""
+    """k_decode_tilegw's two-tile form (production for grouped CRC layouts:
+    two workgroups per group of four tiles, two waves per tile, one A_(4 sq)
+    chain per lane; partial tiles load zeros), its four-tile form (ZHIP_TUNE_ARM
+    38) and k_decode_tileg (5) decode exactly what the oracle wrote, fill
+    missing chunks and report a corrupted chunk with the reference's message."""
     import zarr_hip
     from zarr_hip import _native as N
 
     codecs = [T(order), endian, CRC]
-    kernel = b"k_decode_tileg" if arm else b"k_decode_tilegw"
+    kernel = {0: b"k_decode_tileg2w", 5: b"k_decode_tileg", 38: b"k_decode_tilegw"}[arm]
     set_tuning(6, arm)
     try:
         _roundtrip(device, (96, 160, 160), (96, 80, 80), dtype, codecs, fill=3, drop=["c/0/1/0"])

@@ -500,7 +500,13 @@ int zhip_plan_upload(zhip_plan* p) {
         // k_decode_tilegw: the same chains for the four tiles of a group
         const bool tgw = p->gd >= 0 && (L.flags & ZHIP_LF_CRC);
         const size_t n_tgw = tgw ? kPairTabWords + (size_t)p->n_groups * kThreads : 0;
-        std::vector<uint32_t> ht(n_base + n_t4 + n_g + n_t4f + n_t4w + n_tgw);
+        // the two-tile form of k_decode_tile4w (at most 32 workgroups per chunk:
+        // the one-word publication): lane constants only
+        const size_t n_t2w = (t4w && T % 2 == 0 && T / 2 <= 32) ? (size_t)(T / 2) * kThreads : 0;
+        const size_t n_t1w = (ZHIP_TUNING && t4w) ? (size_t)T * kThreads : 0;  // one tile per workgroup
+        // the two-tile form of k_decode_tilegw: two workgroups per group of four
+        const size_t n_tg2w = tgw ? (size_t)p->n_groups * 2 * kThreads : 0;
+        std::vector<uint32_t> ht(n_base + n_t4 + n_g + n_t4f + n_t4w + n_tgw + n_t2w + n_t1w + n_tg2w);
         build_horner_stride(ht.data(), 16ull * sq);
         for (int t = 0; t < kThreads; ++t) {
             const uint64_t rel = (uint64_t)(kTileRows + t / 16) * sq + 16u * (t % 16);
@@ -614,6 +620,61 @@ int zhip_plan_upload(zhip_plan* p) {
                     f[kPairTabWords + (size_t)g4 * kThreads + t] = gf_mul(gf_mul(xe, p->c_inv), c96);
                 }
         }
+        p->tile2w_off = 0;
+        if (n_t2w) {
+            // two tiles per workgroup: wave w loads rows 32 (w % 2) + l/16 + 4 m (m < 8)
+            // of tile 2 g + w / 2; the same frame with 8 blocks of stride D = 4 sq
+            p->tile2w_off = n_base + n_t4 + n_g + n_t4f + n_t4w + n_tgw;
+            uint32_t* f = &ht[p->tile2w_off];
+            const uint64_t D = 4ull * sq;
+            const uint32_t c96 = xpow8_inv(12);
+            for (uint32_t g2 = 0; g2 < T / 2; ++g2)
+                for (int t = 0; t < kThreads; ++t) {
+                    const int w = t / 64, l = t % 64;
+                    const int64_t p0 = (int64_t)base[2 * g2 + w / 2] + (int64_t)(32 * (w % 2) + l / 16) * (int64_t)sq +
+                                       16 * (l % 16);
+                    const int64_t e = (int64_t)p->E - p0 + kWgStride - 8 * (int64_t)D;
+                    const uint32_t xe = e >= 0 ? xpow8((uint64_t)e) : xpow8_inv((uint64_t)(-e));
+                    f[(size_t)g2 * kThreads + t] = gf_mul(gf_mul(xe, p->c_inv), c96);
+                }
+        }
+        p->tile1w_off = 0;
+        if (n_t1w) {
+            // one tile per workgroup: wave w loads rows 16 w + l/16 + 4 m (m < 4)
+            p->tile1w_off = n_base + n_t4 + n_g + n_t4f + n_t4w + n_tgw + n_t2w;
+            uint32_t* f = &ht[p->tile1w_off];
+            const uint64_t D = 4ull * sq;
+            const uint32_t c96 = xpow8_inv(12);
+            for (uint32_t ti = 0; ti < T; ++ti)
+                for (int t = 0; t < kThreads; ++t) {
+                    const int w = t / 64, l = t % 64;
+                    const int64_t p0 = (int64_t)base[ti] + (int64_t)(16 * w + l / 16) * (int64_t)sq + 16 * (l % 16);
+                    const int64_t e = (int64_t)p->E - p0 + kWgStride - 4 * (int64_t)D;
+                    const uint32_t xe = e >= 0 ? xpow8((uint64_t)e) : xpow8_inv((uint64_t)(-e));
+                    f[(size_t)ti * kThreads + t] = gf_mul(gf_mul(xe, p->c_inv), c96);
+                }
+        }
+        p->tileg2w_off = 0;
+        if (n_tg2w) {
+            // workgroup 2 g + h of a chunk: tiles 2 h, 2 h + 1 of group g, wave w loading
+            // rows 32 (w % 2) + l/16 + 4 m (m < 8) of tile 2 h + w / 2
+            p->tileg2w_off = n_base + n_t4 + n_g + n_t4f + n_t4w + n_tgw + n_t2w + n_t1w;
+            uint32_t* f = &ht[p->tileg2w_off];
+            const uint64_t D = 4ull * sq;
+            const uint32_t c96 = xpow8_inv(12);
+            const GroupEnt* gm = reinterpret_cast<const GroupEnt*>(&ht[p->g_off_map]);
+            const int64_t gstep = (int64_t)p->sstride[p->gd];
+            for (uint32_t g = 0; g < p->n_groups; ++g)
+                for (uint32_t h = 0; h < 2; ++h)
+                    for (int t = 0; t < kThreads; ++t) {
+                        const int w = t / 64, l = t % 64;
+                        const int64_t p0 = (int64_t)gm[g].tbase + (int64_t)(2 * h + w / 2) * gstep +
+                                           (int64_t)(32 * (w % 2) + l / 16) * (int64_t)sq + 16 * (l % 16);
+                        const int64_t e = (int64_t)p->E - p0 + kWgStride - 8 * (int64_t)D;
+                        const uint32_t xe = e >= 0 ? xpow8((uint64_t)e) : xpow8_inv((uint64_t)(-e));
+                        f[((size_t)g * 2 + h) * kThreads + t] = gf_mul(gf_mul(xe, p->c_inv), c96);
+                    }
+        }
         p->tilegw = tgw ? 1u : 0u;
         p->tilegw_off = n_base + n_t4 + n_g + n_t4f + n_t4w;
         if (tgw) {
@@ -668,8 +729,13 @@ int zhip_plan_info(const zhip_plan* p, uint32_t* units_per_chunk, uint32_t* work
     if (units_per_chunk) *units_per_chunk = p->nseg;
     // + the grouped kernels' / k_decode_xw's arrival subwords
     // (CRC layouts: >= kPubLine, the il / tile4 publication lines)
+    // (k_decode_tilegw's two-tile form: arrival subwords for twice the groups)
+    // (known at plan creation, before the tile tables exist)
+    const bool tg2w = p->gd >= 0 && (p->layout.flags & ZHIP_LF_CRC);
+    const uint32_t n_sub2 = (tg2w && 2 * p->n_groups > 16u && 2 * p->n_groups <= 256u)
+                                ? (2 * p->n_groups + 15u) / 16u : 0u;
     if (workspace_words)
-        *workspace_words = std::max(4 + 2 * std::max(p->n_sub, p->xw_nsub),
+        *workspace_words = std::max(4 + 2 * std::max(std::max(p->n_sub, p->xw_nsub), n_sub2),
                                     (p->layout.flags & ZHIP_LF_CRC) ? kPubLine : 0u);
     return ZHIP_OK;
 }
@@ -921,6 +987,8 @@ int zhip_decode_mapped(const zhip_plan* plan, const void* src, uint64_t src_size
                 // C3 28.9 vs 30.3-30.6 us, profiles/r04/k); arms 1 / 2 / 5: k_decode_tile4
                 p.t4w_tab = plan->d_tile_tables + plan->tile4w_off;
                 p.t4w_kq = p.t4w_tab + kPairTabWords;
+                if (plan->tile2w_off) p.t2w_kq = plan->d_tile_tables + plan->tile2w_off;
+                if (plan->tile1w_off) p.t1w_kq = plan->d_tile_tables + plan->tile1w_off;
             }
         } else if (plan->gd >= 0 && !(g_tune_bits & kTuneTile1) &&
                    L.shape[plan->tq] % (16 / L.itemsize) == 0) {
@@ -935,6 +1003,7 @@ int zhip_decode_mapped(const zhip_plan* plan, const void* src, uint64_t src_size
             if (plan->tilegw && g_tune_arm != 2 && g_tune_arm != 5) {  // a wave per tile, one chain per lane
                 p.t4w_tab = plan->d_tile_tables + plan->tilegw_off;
                 p.t4w_kq = p.t4w_tab + kPairTabWords;
+                if (plan->tileg2w_off) p.t2w_kq = plan->d_tile_tables + plan->tileg2w_off;  // two tiles per workgroup
             }
         }
         const uint64_t tunits = (uint64_t)n_chunks * plan->t_per_chunk;

@@ -509,7 +509,8 @@ KernelFn select_tile4f_kernel(int item, bool swap);                  // decode_t
 #endif
 KernelFn select_tile4_kernel(bool crc, int item, bool swap);         // decode_tile.hip
 KernelFn select_tile4w_kernel(int item, bool swap);                  // decode_tile.hip
-KernelFn select_tilegw_kernel(int item, bool swap, bool defer);      // decode_tile.hip
+KernelFn select_tile2w_kernel(int item, bool swap, int nt);          // decode_tile.hip
+KernelFn select_tilegw_kernel(int item, bool swap, bool defer, int nt);  // decode_tile.hip
 KernelFn select_tileg_kernel(bool crc, int item, bool swap, bool defer);  // decode_tile.hip
 
 // name of the kernel the last launch_decode chose (zhip_last_kernel: bench
@@ -772,6 +773,20 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
         const bool f4 = ZHIP_TUNING && p.t4f_tab != nullptr && (p.lflags & ZHIP_LF_CRC) != 0;
         const bool w4 = !f4 && p.t4w_tab != nullptr && (p.lflags & ZHIP_LF_CRC) != 0;
         const bool swp = (p.lflags & ZHIP_LF_SWAP) != 0;
+        // two tiles per workgroup (2 048 workgroups on C3: two residency rounds
+        // instead of one) -- graph-timed 27.8-27.9 vs 28.4-30.0 us on C3
+        // (profiles/r05/l/); tuning arm 38 keeps four, 37 takes one (46 us)
+        if (w4 && ((p.t2w_kq && g_tune_arm != 38 && g_tune_arm != 37) || (g_tune_arm == 37 && p.t1w_kq))) {
+            const int nt = g_tune_arm == 37 ? 1 : 2;
+            KernelFn fn2 = select_tile2w_kernel(p.g.itemsize, swp, nt);
+            if (!fn2) return ZHIP_E_UNSUPPORTED;
+            if (p.n_units == 0) return ZHIP_OK;
+            DecodeParams q = p;
+            q.t4w_kq = nt == 1 ? p.t1w_kq : p.t2w_kq;
+            g_last_kernel = nt == 1 ? "k_decode_tile1w" : "k_decode_tile2w";
+            hipLaunchKernelGGL(fn2, dim3(p.n_units / (uint32_t)nt), dim3(kThreads), 0, stream, q);
+            return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
+        }
 #if ZHIP_TUNING
         KernelFn fn = f4 ? select_tile4f_kernel(p.g.itemsize, swp)
                       : w4 ? select_tile4w_kernel(p.g.itemsize, swp)
@@ -792,14 +807,20 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
         const bool gw = p.t4w_tab != nullptr && (p.lflags & ZHIP_LF_CRC) != 0;
         // (arm 2: the returning publication whatever the flags)
         const bool defer = p.defer != 0 && g_tune_arm != 2;
-        KernelFn fn = gw ? select_tilegw_kernel(p.g.itemsize, (p.lflags & ZHIP_LF_SWAP) != 0, defer)
+        // two tiles per workgroup where the plan built their constants (as
+        // k_decode_tile4w); tuning arms 38 (deferred) / 2 (returning) keep four
+        const int nt = (gw && p.t2w_kq && g_tune_arm != 38 && g_tune_arm != 2) ? 2 : 4;
+        KernelFn fn = gw ? select_tilegw_kernel(p.g.itemsize, (p.lflags & ZHIP_LF_SWAP) != 0, defer, nt)
                          : select_tileg_kernel((p.lflags & ZHIP_LF_CRC) != 0, p.g.itemsize,
                                                (p.lflags & ZHIP_LF_SWAP) != 0, defer);
         if (!fn) return ZHIP_E_UNSUPPORTED;
         if (p.n_chunks == 0) return ZHIP_OK;
-        if ((uint64_t)p.n_chunks * p.n_groups >= (1ull << 31)) return ZHIP_E_UNSUPPORTED;
-        g_last_kernel = gw ? "k_decode_tilegw" : "k_decode_tileg";
-        hipLaunchKernelGGL(fn, dim3(p.n_chunks * p.n_groups), dim3(kThreads), 0, stream, p);
+        const uint64_t ggrid = (uint64_t)p.n_chunks * p.n_groups * (uint32_t)(4 / nt);
+        if (ggrid >= (1ull << 31)) return ZHIP_E_UNSUPPORTED;
+        DecodeParams q = p;
+        if (nt == 2) q.t4w_kq = p.t2w_kq;
+        g_last_kernel = !gw ? "k_decode_tileg" : nt == 2 ? "k_decode_tileg2w" : "k_decode_tilegw";
+        hipLaunchKernelGGL(fn, dim3((uint32_t)ggrid), dim3(kThreads), 0, stream, q);
         return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
     }
     if (p.tq >= 0) {

@@ -461,39 +461,52 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
 // Production for transposed layouts with a CRC since round 4: C3 28.9 vs
 // 30.3-30.6 us graph-timed (profiles/r04/k/arms_c3.jsonl); ZHIP_TUNE_ARM 5
 // (or 1 / 2, its publication arms) takes k_decode_tile4.
-template <int ITEM, bool SWAP>
+template <int N>
+struct TileMapN {
+    TileEnt e[N];
+};
+
+// NT: tiles per workgroup -- 4 (production) or 2 (arm 36: 2 048 workgroups of
+// 32 KiB on C3, two residency rounds instead of one; two waves per tile, lane
+// l of half h taking rows 32 h + l/16 + 4 m, m < 8: the same A_(4 sq) chain
+// over 8 blocks)
+template <int ITEM, bool SWAP, int NT = kTiles>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_decode_tile4w(
     const DecodeParams p) {
     constexpr int kPer = 16 / ITEM;
     constexpr int kPiecesPerCol = kTileRows / kPer;
-    constexpr int KB = kTileRows / 4;  // blocks per lane
+    constexpr int WPT = kTiles / NT;        // waves per tile
+    constexpr int RPW = kTileRows / WPT;    // tile rows per wave
+    constexpr int KB = RPW / 4;             // blocks per lane
+    constexpr int HS = KB / NT;             // Horner steps per tile iteration
     __shared__ __attribute__((aligned(16))) uint32_t s_mem[kPairTabWords + kTileRows * 64];
     uint32_t* const s_tab = s_mem;
     uint8_t* const s_tile = reinterpret_cast<uint8_t*>(s_mem + kPairTabWords);
     uint32_t* const s_red = s_mem + kPairTabWords;  // after the last out-order pass
     const int t = threadIdx.x;
-    const uint32_t wv = __builtin_amdgcn_readfirstlane((uint32_t)t >> 6);  // this wave's tile
+    const uint32_t wv = __builtin_amdgcn_readfirstlane((uint32_t)t >> 6);
+    const uint32_t tj = wv / WPT, hh = wv % WPT;  // this wave's tile and its row band
     const uint32_t ln = (uint32_t)t & 63u, rg = ln >> 4, cl = 16u * (ln & 15u);
     const uint32_t g = blockIdx.x;
-    const uint32_t gpc = p.t_per_chunk / kTiles;
+    const uint32_t gpc = p.t_per_chunk / NT;
     const uint32_t c = g / gpc;
     const uint32_t grp = g - c * gpc;
     const uint32_t expected = p.g.nbytes + 4u;
-    // 1. tables and the lane constant (L2 hits), the chunk header, 16 data blocks
+    // 1. tables and the lane constant (L2 hits), the chunk header, the data blocks
     const uint4* gt = reinterpret_cast<const uint4*>(p.t4w_tab);
     const uint4 tv0 = gt[t], tv1 = gt[t + kThreads], tv2 = gt[t + 2 * kThreads], tv3 = gt[t + 3 * kThreads],
                 tv4 = gt[t + 4 * kThreads], tv5 = gt[t + 5 * kThreads];
     const uint32_t kq = p.t4w_kq[(size_t)grp * kThreads + t];
     const Unit U = resolve_unit(p, c * p.nseg, expected);
-    const TileMap4 tm = load_uniform<TileMap4>(p.tmap + (size_t)grp * kTiles);
-    const TileEnt mine = load_uniform<TileEnt>(p.tmap + (size_t)grp * kTiles + wv);
+    const TileMapN<NT> tm = load_uniform<TileMapN<NT>>(p.tmap + (size_t)grp * NT);
+    const TileEnt mine = load_uniform<TileEnt>(p.tmap + (size_t)grp * NT + tj);
     const bool ok = U.mode == ZHIP_ST_OK;
     const uint32_t sq = p.sstride[p.tq];
     const uint8_t* zero = reinterpret_cast<const uint8_t*>(g_tile_zero);
     uint4 blk[KB];
 #pragma unroll
     for (int m = 0; m < KB; ++m)
-        blk[m] = load_stream16_a1(ok ? U.cp + mine.tbase + (rg + 4u * (uint32_t)m) * sq + cl : zero);
+        blk[m] = load_stream16_a1(ok ? U.cp + mine.tbase + (hh * RPW + rg + 4u * (uint32_t)m) * sq + cl : zero);
     uint32_t stored = 0;
     if (ok) stored = load_trailer_uniform(U.cp, p.g.nbytes);
     {
@@ -517,12 +530,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     uint8_t* const sink = reinterpret_cast<uint8_t*>(g_tile_sink) + 16 * t;
     Acc4 acc = {0u, 0u, 0u, 0u};
 #pragma unroll
-    for (int j = 0; j < kTiles; ++j) {
+    for (int j = 0; j < NT; ++j) {
         if (j > 0) __syncthreads();  // the previous tile's LDS reads are done
-        if (wv == (uint32_t)j) {
+        if (tj == (uint32_t)j) {
 #pragma unroll
             for (int m = 0; m < KB; ++m)
-                tile_put16<ITEM>(s_tile, rg + 4u * (uint32_t)m, cl, swap_block<ITEM, SWAP>(blk[m]));
+                tile_put16<ITEM>(s_tile, hh * RPW + rg + 4u * (uint32_t)m, cl, swap_block<ITEM, SWAP>(blk[m]));
         }
         __syncthreads();  // tile j (and, first time, the tables) in LDS
 #pragma unroll
@@ -551,7 +564,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
         }
         if (ok) {
 #pragma unroll
-            for (int m = 4 * j; m < 4 * j + 4; ++m) crc_block4(s_tab, acc, blk[m]);
+            for (int m = HS * j; m < HS * j + HS; ++m) crc_block4(s_tab, acc, blk[m]);
         }
     }
     // 3. run end: fold, lane multiply, reduce, publish (returning, the chunk's
@@ -825,29 +838,43 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
 // PUB: 2 = deferred verdicts (ZHIP_DF_DEFER, the Python path's choice), 0 =
 // the returning two-level arrival of k_decode_tileg (the C-ABI default: the
 // launch itself sets the chunk's status and the error word).
-template <int ITEM, bool SWAP, int PUB = 2>
+// NT: tiles per workgroup -- 4, or 2 (two workgroups per group of four, two
+// waves per tile as in k_decode_tile4w's two-tile form; the returning
+// publication then xors and counts per chunk)
+template <int ITEM, bool SWAP, int PUB = 2, int NT = kTiles>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_decode_tilegw(
     const DecodeParams p) {
     constexpr int kPer = 16 / ITEM;
     constexpr int kPiecesPerCol = kTileRows / kPer;
-    constexpr int KB = kTileRows / 4;  // blocks per lane
+    constexpr int WPT = kTiles / NT;        // waves per tile
+    constexpr int RPW = kTileRows / WPT;    // tile rows per wave
+    constexpr int KB = RPW / 4;             // blocks per lane
+    constexpr int HS = KB / NT;             // Horner steps per tile iteration
+    constexpr uint32_t PG = kTiles / NT;    // workgroups per group of four tiles
     __shared__ __attribute__((aligned(16))) uint32_t s_mem[kPairTabWords + kTileRows * 64];
     uint32_t* const s_tab = s_mem;
     uint8_t* const s_tile = reinterpret_cast<uint8_t*>(s_mem + kPairTabWords);
     uint32_t* const s_red = s_mem + kPairTabWords;  // after the last out-order pass
     const int t = threadIdx.x;
     const uint32_t wv = __builtin_amdgcn_readfirstlane((uint32_t)t >> 6);
+    const uint32_t tj = wv / WPT, hh = wv % WPT;  // this wave's tile (of the workgroup's) and row band
     const uint32_t ln = (uint32_t)t & 63u, rg = ln >> 4, cl = 16u * (ln & 15u);
-    const uint32_t gpc = p.n_groups;
+    const uint32_t gpc = p.n_groups * PG;  // workgroups per chunk
     const uint32_t c = blockIdx.x / gpc;
-    const uint32_t grp = blockIdx.x - c * gpc;
+    const uint32_t wg = blockIdx.x - c * gpc;
+    const uint32_t grp = wg / PG, t0 = (wg % PG) * NT;  // the group and its first tile here
     const uint32_t expected = p.g.nbytes + 4u;
     const uint4* gt = reinterpret_cast<const uint4*>(p.t4w_tab);
     const uint4 tv0 = gt[t], tv1 = gt[t + kThreads], tv2 = gt[t + 2 * kThreads], tv3 = gt[t + 3 * kThreads],
                 tv4 = gt[t + 4 * kThreads], tv5 = gt[t + 5 * kThreads];
-    const uint32_t kq = p.t4w_kq[(size_t)grp * kThreads + t];
+    const uint32_t kq = p.t4w_kq[(size_t)wg * kThreads + t];
+    // (the two-tile form always reports in-launch: twice the workgroups per
+    // chunk made the deferred verdicts' one same-address word per chunk the
+    // tail -- 36.8 vs 29.8 us on C3 in 128^3 chunks; its two-level returning
+    // arrival keeps every word at 16 arrivals)
+    constexpr bool kDefer = PUB == 2 && NT == kTiles;
     uint64_t dvprev = 0;
-    if constexpr (PUB == 2) dvprev = dv_prev(p, c, grp == 0, g_tile_zero);
+    if constexpr (kDefer) dvprev = dv_prev(p, c, wg == 0, g_tile_zero);
     const Unit U = resolve_unit(p, c * p.nseg, expected);
     const GroupEnt ge = load_uniform<GroupEnt>(p.gmap + grp);
     const bool ok = U.mode == ZHIP_ST_OK;
@@ -855,11 +882,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     const int32_t rows = ge.rows, cols = ge.cols;
     const uint8_t* zero = reinterpret_cast<const uint8_t*>(g_tile_zero);
     const bool lane_in = (int32_t)cl < cols;
-    const uint8_t* const tb = U.cp + ge.tbase + (size_t)wv * p.g_step_t;
+    const uint8_t* const tb = U.cp + ge.tbase + (size_t)(t0 + tj) * p.g_step_t;
     uint4 blk[KB];
 #pragma unroll
     for (int m = 0; m < KB; ++m) {
-        const uint32_t row = rg + 4u * (uint32_t)m;
+        const uint32_t row = hh * RPW + rg + 4u * (uint32_t)m;
         blk[m] = load_stream16_a1(ok && lane_in && (int32_t)row < rows ? tb + row * sq + cl : zero);
     }
     uint32_t stored = 0;
@@ -882,12 +909,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     uint8_t* const sink = reinterpret_cast<uint8_t*>(g_tile_sink) + 16 * t;
     Acc4 acc = {0u, 0u, 0u, 0u};
 #pragma unroll
-    for (int j = 0; j < kTiles; ++j) {
+    for (int j = 0; j < NT; ++j) {
         if (j > 0) __syncthreads();
-        if (wv == (uint32_t)j) {
+        if (tj == (uint32_t)j) {
 #pragma unroll
             for (int m = 0; m < KB; ++m)
-                tile_put16<ITEM>(s_tile, rg + 4u * (uint32_t)m, cl, swap_block<ITEM, SWAP>(blk[m]));
+                tile_put16<ITEM>(s_tile, hh * RPW + rg + 4u * (uint32_t)m, cl, swap_block<ITEM, SWAP>(blk[m]));
         }
         __syncthreads();
 #pragma unroll
@@ -912,12 +939,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
                 }
             }
             const bool in = writes && (int32_t)(jc * ITEM) < cols && (int32_t)r0 < rows;
-            uint8_t* dst = in ? obase + (int64_t)j * p.g_step_o + (int64_t)jc * ocol + (int64_t)r0 * oq : sink;
+            uint8_t* dst = in ? obase + (int64_t)(t0 + j) * p.g_step_o + (int64_t)jc * ocol + (int64_t)r0 * oq : sink;
             store_nt16(dst, ok ? make_uint4(w[0], w[1], w[2], w[3]) : f);
         }
         if (ok) {
 #pragma unroll
-            for (int m = 4 * j; m < 4 * j + 4; ++m) crc_block4(s_tab, acc, blk[m]);
+            for (int m = HS * j; m < HS * j + HS; ++m) crc_block4(s_tab, acc, blk[m]);
         }
     }
     if (ok) {
@@ -925,15 +952,18 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
         __syncthreads();  // every out-order read of the last tile is done: s_red reuses the image
         if ((t & 63) == 0) s_red[t >> 6] = v;
         __syncthreads();
-        if (t == 0 && PUB == 2) {
-            dv_publish(p, c, grp == 0, s_red[0] ^ s_red[1] ^ s_red[2] ^ s_red[3], stored);
+        if (t == 0 && kDefer) {
+            dv_publish(p, c, wg == 0, s_red[0] ^ s_red[1] ^ s_red[2] ^ s_red[3], stored);
         } else if (t == 0) {  // the returning arrival of k_decode_tileg (V in the same frame)
             const uint32_t V = s_red[0] ^ s_red[1] ^ s_red[2] ^ s_red[3];
             uint32_t raw = 0;
             bool last_one = false;
-            if (gpc <= 16u || p.n_sub) {
+            // subgroups of 16 workgroups (the plan's n_sub for four tiles; for two,
+            // zhip_plan_info sizes the workspace tail for twice as many)
+            const uint32_t nsub = NT == kTiles ? p.n_sub : ((gpc > 16u && gpc <= 256u) ? (gpc + 15u) / 16u : 0u);
+            if (gpc <= 16u || nsub) {
                 bool any_ne;
-                last_one = tileg_arrive(p.ws, p.n_chunks, c, grp, gpc, p.n_sub, V, false, raw, any_ne);
+                last_one = tileg_arrive(p.ws, p.n_chunks, c, wg, gpc, nsub, V, false, raw, any_ne);
             } else {  // more than 256 groups per chunk: XOR, then count arrivals
                 uint32_t* accw = p.ws + 4ull * c;
                 const uint32_t prev = __hip_atomic_fetch_xor(accw, V, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -954,9 +984,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
             }
         }
     }
-    if (grp == 0 && t == 0) {
+    if (wg == 0 && t == 0) {
         if (ok) {
-            if constexpr (PUB == 2) {
+            if constexpr (kDefer) {
                 zhip_status st = {ZHIP_ST_OK, 0u, 0u, 0u};
                 p.status[c] = st;
             }
@@ -965,7 +995,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
             p.status[c] = st;
             if (U.mode != ZHIP_ST_MISSING) atomicOr(p.errflag, 1u << U.mode);
         }
-        if constexpr (PUB == 2) dv_settle(p, c, dvprev);
+        if constexpr (kDefer) dv_settle(p, c, dvprev);
     }
 }
 
@@ -1571,8 +1601,10 @@ KernelFn select_tileg_kernel(bool crc, int item, bool swap, bool defer) {
 #undef ZHIP_TILEG
 }
 
-KernelFn select_tilegw_kernel(int item, bool swap, bool defer) {  // CRC chains only
-#define ZHIP_TILEGW(I, W) (defer ? k_decode_tilegw<I, W, 2> : k_decode_tilegw<I, W, 0>)
+KernelFn select_tilegw_kernel(int item, bool swap, bool defer, int nt) {  // CRC chains only
+#define ZHIP_TILEGW(I, W)                                                                          \
+    (nt == 2 ? (defer ? k_decode_tilegw<I, W, 2, 2> : k_decode_tilegw<I, W, 0, 2>)                 \
+             : (defer ? k_decode_tilegw<I, W, 2> : k_decode_tilegw<I, W, 0>))
     switch (item) {
         case 1: return ZHIP_TILEGW(1, false);
         case 2: return swap ? ZHIP_TILEGW(2, true) : ZHIP_TILEGW(2, false);
@@ -1591,6 +1623,25 @@ KernelFn select_tile4w_kernel(int item, bool swap) {  // CRC chains only
         case 8: return swap ? k_decode_tile4w<8, true> : k_decode_tile4w<8, false>;
         default: return nullptr;
     }
+}
+
+// two tiles per workgroup (production where the plan built its constants);
+// the tuning build adds one tile per workgroup (arm 37)
+KernelFn select_tile2w_kernel(int item, bool swap, int nt) {  // CRC chains only
+#if ZHIP_TUNING
+#define ZHIP_T2W(I, W) (nt == 1 ? k_decode_tile4w<I, W, 1> : k_decode_tile4w<I, W, 2>)
+#else
+    if (nt != 2) return nullptr;
+#define ZHIP_T2W(I, W) k_decode_tile4w<I, W, 2>
+#endif
+    switch (item) {
+        case 1: return ZHIP_T2W(1, false);
+        case 2: return swap ? ZHIP_T2W(2, true) : ZHIP_T2W(2, false);
+        case 4: return swap ? ZHIP_T2W(4, true) : ZHIP_T2W(4, false);
+        case 8: return swap ? ZHIP_T2W(8, true) : ZHIP_T2W(8, false);
+        default: return nullptr;
+    }
+#undef ZHIP_T2W
 }
 
 #if ZHIP_TUNING

@@ -120,6 +120,8 @@ struct DecodeParams {
     // tables, lane constants [T/4 or n_groups][kThreads]
     const uint32_t* t4w_tab;
     const uint32_t* t4w_kq;
+    const uint32_t* t2w_kq;  // k_decode_tile4w with two tiles per workgroup (production when set): lane constants
+    const uint32_t* t1w_kq;  // tuning arm 37 (one tile per workgroup)
     // k_decode_tileg (tileg != 0): group map, step multiply table, steps
     uint32_t tileg;
     const struct GroupEnt* gmap;
@@ -390,6 +392,9 @@ struct zhip_plan {
     // kPairTab* layout | lane constants [T/4][kThreads], at tile4w_off
     uint32_t tile4w;
     uint64_t tile4w_off;
+    uint64_t tile2w_off;  // lane constants [T/2][kThreads] of k_decode_tile4w's two-tile form (0: none)
+    uint64_t tile1w_off;  // tuning builds: lane constants [T][kThreads] of the one-tile form (0: none)
+    uint64_t tileg2w_off; // lane constants [2 n_groups][kThreads] of k_decode_tilegw's two-tile form (0: none)
     // k_decode_tilegw (grouped tile layouts with a CRC): the same for groups
     uint32_t tilegw;
     uint64_t tilegw_off;
