@@ -690,12 +690,13 @@ def _encode_bench(device, args, codecs, want, chunks=(64, 64, 64), check=True):
 
 def encode_c3(device, args):
     """Encode side of C3: the 256^3 f32 array written through transpose(2,1,0) +
-    bytes + crc32c into 64 chunks of 64^3 by k_encode_tile4 (four LDS tiles
-    per workgroup), timed like the decode and decoded back for the check."""
+    bytes + crc32c into 64 chunks of 64^3 by k_encode_tile4 (two LDS tiles per
+    workgroup since round 5, "k_encode_tile2"), timed like the decode and
+    decoded back for the check."""
     codecs = [{"name": "transpose", "configuration": {"order": [2, 1, 0]}}, LE, CRC]
-    src, wall, kern, _ = _encode_bench(device, args, codecs, "tile4")
+    src, wall, kern, kname = _encode_bench(device, args, codecs, "tile4")
     return _entry(src, src + 64 * (1048576 + 4), wall, kern,
-                  kernel="k_encode" if args.tune & 65536 else "k_encode_tile4", checked="bytes",
+                  kernel="k_encode" if args.tune & 65536 else kname, checked="bytes",
                   note="decoded_GiBps = source bytes encoded per second")
 
 

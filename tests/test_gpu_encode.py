@@ -272,12 +272,15 @@ def test_encode_quad_small_chunks(device, arm, shape, chunks, dtype, codecs, fil
 
 # ---- k_encode_tile4: transposed chunks with full 64-row x 256-byte tiles
 
-@pytest.mark.parametrize("dtype,endian,chunks,shape", [
+ENC_TILE4_CASES = [
     ("float32", LE, (64, 64, 64), (128, 128, 64)),
     ("float64", BE, (32, 16, 64), (64, 48, 128)),
     ("int16", LE, (128, 8, 64), (256, 16, 64)),
     ("uint8", LE, (256, 8, 64), (256, 24, 128)),
-])
+]
+
+
+@pytest.mark.parametrize("dtype,endian,chunks,shape", ENC_TILE4_CASES)
 def test_encode_tile4(device, dtype, endian, chunks, shape):
     from zarr_hip import _native as N
     from zarr_hip.planner import _make_layout
@@ -287,12 +290,58 @@ def test_encode_tile4(device, dtype, endian, chunks, shape):
     fill = 0
     sl = tuple(slice(0, c) for c in chunks)  # one chunk entirely fill -> elided
     d[sl] = fill
-    _run(device, shape, chunks, dtype, codecs, fill, [((Ellipsis,), d)])
+    arr, _ = _run(device, shape, chunks, dtype, codecs, fill, [((Ellipsis,), d)])
+    arr[...] = d  # (two tiles per workgroup: the production form for CRC layouts)
+    assert N.lib().zhip_last_kernel() == b"k_encode_tile2"
     # the layout qualifies for the four-tile encode
     st = [chunks[p] for p in (2, 1, 0)]
     it = np.dtype(dtype).itemsize
     L = _make_layout(st, it, [it, shape[2] * it * 999, shape[2] * shape[1] * it], 0, b"\0")
     assert N.Plan(L, upload=False).kernel_flags & N.PK_TILE4_ENCODE
+
+
+@pytest.mark.tuning
+@pytest.mark.parametrize("dtype,endian,chunks,shape", ENC_TILE4_CASES)
+def test_encode_tile4_four_tile_form(device, dtype, endian, chunks, shape):
+    """k_encode_tile4's four-tile form (ZHIP_TUNE_ARM 38) writes the same
+    bytes: elided fill chunk, partial writes merged."""
+    from zarr_hip import _native as N
+
+    codecs = [T((2, 1, 0)), endian, CRC]
+    d = _data(shape, dtype)
+    d[tuple(slice(0, c) for c in chunks)] = 0
+    set_tuning(6, 38)
+    try:
+        arr, _ = _run(device, shape, chunks, dtype, codecs, 0,
+                      [((Ellipsis,), d), ((slice(1, shape[0] - 1), slice(2, shape[1]), slice(0, 33)), 5)])
+        arr[...] = d
+        assert N.lib().zhip_last_kernel() == b"k_encode_tile4"
+    finally:
+        set_tuning(6, 0)
+
+
+@pytest.mark.tuning
+@pytest.mark.parametrize("order", [(2, 1, 0), (1, 2, 0)])
+@pytest.mark.parametrize("dtype,endian", [("float32", LE), ("int16", BE)])
+def test_encode_tileg_four_tile_form(device, order, dtype, endian):
+    """k_encode_tileg (production: four tiles per workgroup) and its two-tile
+    form (ZHIP_TUNE_ARM 36) write byte-identical stores (partial tiles, a
+    fill chunk)."""
+    from zarr_hip import _native as N
+
+    shape, chunks = (96, 160, 160), (96, 80, 80)
+    codecs = [T(order), endian, CRC]
+    d = _data(shape, dtype)
+    d[0:96, 0:80, 0:80] = 0
+    for arm, kname in ((0, b"k_encode_tileg"), (36, b"k_encode_tileg2")):
+        set_tuning(6, arm)
+        try:
+            arr, _ = _run(device, shape, chunks, dtype, codecs, 0,
+                          [((Ellipsis,), d), ((slice(3, 90), slice(5, 150), slice(0, 77)), 7)])
+            arr[...] = d
+            assert N.lib().zhip_last_kernel() == kname
+        finally:
+            set_tuning(6, 0)
 
 
 def test_encode_tile4_nan_fill_merges_and_no_crc(device):

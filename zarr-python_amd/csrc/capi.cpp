@@ -506,7 +506,9 @@ int zhip_plan_upload(zhip_plan* p) {
         const size_t n_t1w = (ZHIP_TUNING && t4w) ? (size_t)T * kThreads : 0;  // one tile per workgroup
         // the two-tile form of k_decode_tilegw: two workgroups per group of four
         const size_t n_tg2w = tgw ? (size_t)p->n_groups * 2 * kThreads : 0;
-        std::vector<uint32_t> ht(n_base + n_t4 + n_g + n_t4f + n_t4w + n_tgw + n_t2w + n_t1w + n_tg2w);
+        // the two-tile form of k_encode_tile4 (CRC, at most 32 workgroups per chunk)
+        const size_t n_t2e = (t4 && (L.flags & ZHIP_LF_CRC) && T % 2 == 0 && T / 2 <= 32) ? (size_t)(T / 2) * kThreads : 0;
+        std::vector<uint32_t> ht(n_base + n_t4 + n_g + n_t4f + n_t4w + n_tgw + n_t2w + n_t1w + n_tg2w + n_t2e);
         build_horner_stride(ht.data(), 16ull * sq);
         for (int t = 0; t < kThreads; ++t) {
             const uint64_t rel = (uint64_t)(kTileRows + t / 16) * sq + 16u * (t % 16);
@@ -674,6 +676,17 @@ int zhip_plan_upload(zhip_plan* p) {
                         const uint32_t xe = e >= 0 ? xpow8((uint64_t)e) : xpow8_inv((uint64_t)(-e));
                         f[((size_t)g * 2 + h) * kThreads + t] = gf_mul(gf_mul(xe, p->c_inv), c96);
                     }
+        }
+        p->tile2e_off = 0;
+        if (n_t2e) {
+            // the four-tile constants' form for groups of two: the state carried
+            // to the group's last tile (tile 2 g + 1), then shifted by its unit constant
+            p->tile2e_off = n_base + n_t4 + n_g + n_t4f + n_t4w + n_tgw + n_t2w + n_t1w + n_tg2w;
+            for (uint32_t g2 = 0; g2 < T / 2; ++g2) {
+                const uint32_t ku = gf_mul(ht[4096 + kThreads + 2 * g2 + 1], p->t_c_inv);
+                for (int t = 0; t < kThreads; ++t)
+                    ht[p->tile2e_off + (size_t)g2 * kThreads + t] = gf_mul(ht[4096 + t], ku);
+            }
         }
         p->tilegw = tgw ? 1u : 0u;
         p->tilegw_off = n_base + n_t4 + n_g + n_t4f + n_t4w;
@@ -1084,6 +1097,7 @@ int zhip_encode_mapped(const zhip_plan* plan, const void* arr, void* dst, const 
         p.horner = plan->d_tile_tables;
         p.tz = plan->d_tile_tables + plan->tile4_off_tz;
         p.kq4 = plan->d_tile_tables + plan->tile4_off_kq;
+        if (plan->tile2e_off) p.kq2 = plan->d_tile_tables + plan->tile2e_off;
         p.tmap = reinterpret_cast<const TileEnt*>(plan->d_tile_tables + plan->tile4_off_map);
         d_rowmap = nullptr;
     } else if ((encode_flags & ZHIP_DF_TILE) && plan->gd >= 0 && plan->d_tile_tables && !(g_tune_bits & kTuneTile1) &&
@@ -1101,6 +1115,7 @@ int zhip_encode_mapped(const zhip_plan* plan, const void* arr, void* dst, const 
         p.n_groups = plan->n_groups;
         p.n_sub = plan->n_sub;
         p.g_step_t = plan->sstride[plan->gd];
+        p.g_z2 = xpow8(2ull * plan->sstride[plan->gd]);
         p.g_step_o = L.out_stride[plan->gd];
         d_rowmap = nullptr;
     } else if ((encode_flags & (ZHIP_DF_TILE | ZHIP_DF_TILE_PREFIX)) && plan->tq >= 0 && plan->d_tile_tables &&

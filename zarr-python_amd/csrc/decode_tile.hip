@@ -1008,7 +1008,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
 // carries CRC | tile-group arrival | tile-group non-empty bits (at most 16
 // workgroups per chunk); the last arrival writes trailer, status and the
 // chunk's non-empty flag.
-template <bool CRC, int ITEM, bool SWAP>
+// NT: tiles per workgroup -- 4, or 2 (twice the workgroups: two residency
+// rounds, as k_decode_tile4w's two-tile form; up to 32 workgroups per chunk
+// publish per half-chunk word with a second level, as k_encode_il)
+template <bool CRC, int ITEM, bool SWAP, int NT = kTiles>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_encode_tile4(
     const EncodeParams p) {
     constexpr int kPer = 16 / ITEM;
@@ -1020,7 +1023,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     __shared__ uint32_t s_ne[kThreads / 64];
     const int t = threadIdx.x;
     const uint32_t g = blockIdx.x;
-    const uint32_t gpc = p.t_per_chunk / kTiles;
+    const uint32_t gpc = p.t_per_chunk / NT;
     const uint32_t c = g / gpc;
     const uint32_t grp = g - c * gpc;
     uint4 tv0, tv1, tv2, tv3, tzv;
@@ -1032,10 +1035,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
         tv2 = gt[t + 2 * kThreads];
         tv3 = gt[t + 3 * kThreads];
         tzv = reinterpret_cast<const uint4*>(p.tz)[t];
-        kq = p.kq4[(size_t)grp * kThreads + t];
+        kq = p.kq4[(size_t)grp * kThreads + t];  // (NT = 2: the two-tile constants, launch_encode)
     }
     const zhip_chunk ch = load_uniform<zhip_chunk>(p.chunks + c);  // src: dst offset, out_off: source offset
-    const TileMap4 tm = load_uniform<TileMap4>(p.tmap + (size_t)grp * kTiles);
+    const TileMapN<NT> tm = load_uniform<TileMapN<NT>>(p.tmap + (size_t)grp * NT);
     const int32_t last = p.g.ndim - 1;
     const int64_t oq = p.g.ostride[p.tq];    // == ITEM (source stride of the out-contiguous dim)
     const int64_t ocol = p.g.ostride[last];  // source stride of the innermost stored dim
@@ -1044,9 +1047,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     const uint32_t sq = p.sstride[p.tq];
     const uint32_t row0 = (uint32_t)t >> 4, col = 16u * (uint32_t)(t & 15);
     // 1. gather every piece of the four tiles
-    uint4 pcs[kTiles][kPasses];
+    uint4 pcs[NT][kPasses];
 #pragma unroll
-    for (int j = 0; j < kTiles; ++j)
+    for (int j = 0; j < NT; ++j)
 #pragma unroll
         for (int k = 0; k < kPasses; ++k) {
             const uint32_t pc = (uint32_t)(k * kThreads + t);
@@ -1065,7 +1068,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     uint32_t S = 0;
     bool eq = true;
 #pragma unroll
-    for (int j = 0; j < kTiles; ++j) {
+    for (int j = 0; j < NT; ++j) {
         if (j > 0) __syncthreads();  // the previous tile's LDS reads are done
         // 2. pieces into the LDS image at their stored (row, column) place
 #pragma unroll
@@ -1115,17 +1118,30 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     if (t != 0) return;
     const uint32_t V = CRC ? (s_red[0] ^ s_red[1] ^ s_red[2] ^ s_red[3]) : 0u;
     const bool ne = (s_ne[0] | s_ne[1] | s_ne[2] | s_ne[3]) != 0u;
-    const uint64_t pb = 1ull << grp;
-    const uint64_t full = (1ull << gpc) - 1ull;
     uint64_t* w = reinterpret_cast<uint64_t*>(p.ws) + (uint64_t)p.pub_stride * c;
-    const uint64_t prev = __hip_atomic_fetch_xor(w, (pb << 32) | (ne ? pb << 48 : 0ull) | V, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-    if ((((prev >> 32) & 0xFFFFull) ^ pb) != full) return;
-    __hip_atomic_store(w, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    p.nonempty[c] = (((prev >> 48) ^ (ne ? pb : 0ull)) != 0ull) ? 1u : 0u;
+    // halves of at most 16 workgroups: CRC | arrival bits 32..47 | non-empty
+    // bits 48..63 per half word, the last of a half folds it into the line's
+    // third word (one half up to 16 workgroups: no second level)
+    const uint32_t h = grp >> 4, b = grp & 15u;
+    const uint32_t n_h = h ? gpc - 16u : (gpc < 16u ? gpc : 16u);
+    const uint64_t pb = 1ull << b;
+    const uint64_t word = (pb << 32) | (ne ? pb << 48 : 0ull) | V;
+    const uint64_t prev = __hip_atomic_fetch_xor(w + h, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((((prev ^ word) >> 32) & 0xFFFFull) != (1ull << n_h) - 1ull) return;
+    __hip_atomic_store(w + h, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint64_t all = prev ^ word;
+    if (gpc > 16u) {
+        const uint64_t hb = 1ull << h;
+        const uint64_t w2 = (hb << 32) | ((all >> 48) ? hb << 48 : 0ull) | (uint32_t)all;
+        const uint64_t p2 = __hip_atomic_fetch_xor(w + 2, w2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((((p2 ^ w2) >> 32) & 0xFFFFull) != 3ull) return;
+        __hip_atomic_store(w + 2, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        all = p2 ^ w2;
+    }
+    p.nonempty[c] = (all >> 48) != 0ull ? 1u : 0u;
     uint32_t crc = 0;
     if constexpr (CRC) {
-        crc = ~(((uint32_t)prev ^ V) ^ p.c3);  // kq4 carries t_c_inv
+        crc = ~((uint32_t)all ^ p.c3);  // kq4 carries t_c_inv
         uint8_t* tr = cp + p.g.nbytes;  // LE trailer (crc32c_.py:64-68)
         tr[0] = (uint8_t)crc;
         tr[1] = (uint8_t)(crc >> 8);
@@ -1386,7 +1402,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
 // line outside the tile), per tile LDS image -> stored blocks -> fill test,
 // byteswap, store, Horner; one lane multiply, one reduction, one XOR + arrival
 // pair per workgroup (any number of groups per chunk).
-template <bool CRC, int ITEM, bool SWAP>
+// NT: tiles per workgroup -- 4, or 2 (two workgroups per group: two
+// residency rounds; the first half's contribution shifted by p.g_z2 to the
+// group's last-tile frame that ge.ku assumes; arrival subwords for twice the
+// workgroups, zhip_plan_info)
+template <bool CRC, int ITEM, bool SWAP, int NT = kTiles>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_encode_tileg(
     const EncodeParams p) {
     constexpr int kPer = 16 / ITEM;
@@ -1397,9 +1417,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     __shared__ uint32_t s_red[kThreads / 64];
     __shared__ uint32_t s_ne[kThreads / 64];
     const int t = threadIdx.x;
-    const uint32_t gpc = p.n_groups;
+    constexpr uint32_t PG = kTiles / NT;  // workgroups per group of four tiles
+    const uint32_t gpc = p.n_groups * PG;   // workgroups per chunk
     const uint32_t c = blockIdx.x / gpc;
-    const uint32_t grp = blockIdx.x - c * gpc;
+    const uint32_t wg = blockIdx.x - c * gpc;
+    const uint32_t grp = wg / PG, t0 = (wg % PG) * NT;  // the group and its first tile here
     uint4 tv0, tv1, tv2, tv3, tzv;
     uint32_t kth = 0;
     if constexpr (CRC) {
@@ -1421,17 +1443,18 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     uint8_t* const cp = p.dst + ch.src + ge.tbase;
     const int32_t rows = ge.rows, cols = ge.cols;
     const uint8_t* zero = reinterpret_cast<const uint8_t*>(g_tile_zero);
-    // 1. every load of the four tiles (pieces outside the tile read a dummy line)
-    uint4 pcs[kTiles][kPasses];
+    // 1. every load of the workgroup's tiles (pieces outside the tile read a dummy line)
+    uint4 pcs[NT][kPasses];
 #pragma unroll
-    for (int j = 0; j < kTiles; ++j)
+    for (int j = 0; j < NT; ++j)
 #pragma unroll
         for (int k = 0; k < kPasses; ++k) {
             const int32_t pc = k * kThreads + t;
             const int32_t jc = pc / kPiecesPerCol;
             const int32_t r0 = (pc % kPiecesPerCol) * kPer;
             const bool in = jc * ITEM < cols && r0 < rows;  // rows % kPer == 0 (zhip_encode_mapped)
-            pcs[j][k] = load_stream16_a1(in ? abase + (int64_t)j * p.g_step_o + (int64_t)jc * ocol + (int64_t)r0 * oq
+            pcs[j][k] = load_stream16_a1(in ? abase + (int64_t)(t0 + j) * p.g_step_o + (int64_t)jc * ocol +
+                                                  (int64_t)r0 * oq
                                         : zero);
         }
     if constexpr (CRC) {
@@ -1446,7 +1469,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     uint32_t S = 0;
     bool eq = true;
 #pragma unroll
-    for (int j = 0; j < kTiles; ++j) {
+    for (int j = 0; j < NT; ++j) {
         if (j > 0) __syncthreads();  // the previous tile's LDS reads are done
         // 2. pieces into the LDS image at their stored (row, column) place
 #pragma unroll
@@ -1481,7 +1504,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
                 const uint4 v = tile_get16<ITEM>(s_tile, row, col);
                 eq = eq && block_eq_fill_e<ITEM>(v, p);
                 e = swap_block<ITEM, SWAP>(v);
-                store_nt16_a1(cp + (size_t)j * p.g_step_t + row * sq + col, e);
+                store_nt16_a1(cp + (size_t)(t0 + j) * p.g_step_t + row * sq + col, e);
             }
             if constexpr (CRC)
                 acc = tab_apply(s_tab, acc ^ e.x) ^ tab_apply(s_tab + 1024, e.y) ^ tab_apply(s_tab + 2048, e.z) ^
@@ -1503,10 +1526,15 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     const bool ne = (s_ne[0] | s_ne[1] | s_ne[2] | s_ne[3]) != 0u;
     uint8_t* const chunk = p.dst + ch.src;
     uint32_t raw = 0;
-    const uint32_t V = CRC ? gf_mul(s_red[0] ^ s_red[1] ^ s_red[2] ^ s_red[3], ge.ku) : 0u;
-    if (gpc <= 16u || p.n_sub) {
+    uint32_t V = 0;
+    if constexpr (CRC) {
+        const uint32_t ku = (NT == 2 && t0 == 0) ? gf_mul(ge.ku, p.g_z2) : ge.ku;
+        V = gf_mul(s_red[0] ^ s_red[1] ^ s_red[2] ^ s_red[3], ku);
+    }
+    const uint32_t nsub = NT == kTiles ? p.n_sub : ((gpc > 16u && gpc <= 256u) ? (gpc + 15u) / 16u : 0u);
+    if (gpc <= 16u || nsub) {
         bool any_ne = false;
-        if (!tileg_arrive(p.ws, p.n_chunks, c, grp, gpc, p.n_sub, V, ne, raw, any_ne)) return;
+        if (!tileg_arrive(p.ws, p.n_chunks, c, wg, gpc, nsub, V, ne, raw, any_ne)) return;
         p.nonempty[c] = any_ne ? 1u : 0u;
     } else {  // more than 256 groups per chunk: arrival count | non-empty count word
         uint32_t* accw = p.ws + 4ull * c;
@@ -1539,7 +1567,17 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
 using KernelFn = void (*)(const DecodeParams);
 using EncodeFn = void (*)(const EncodeParams);
 
-EncodeFn select_encode_tileg_kernel(bool crc, int item, bool swap) {
+EncodeFn select_encode_tileg_kernel(bool crc, int item, bool swap, int nt) {
+    if (nt == 2) {  // CRC layouts only
+        if (!crc) return nullptr;
+        switch (item) {
+            case 1: return k_encode_tileg<true, 1, false, 2>;
+            case 2: return swap ? k_encode_tileg<true, 2, true, 2> : k_encode_tileg<true, 2, false, 2>;
+            case 4: return swap ? k_encode_tileg<true, 4, true, 2> : k_encode_tileg<true, 4, false, 2>;
+            case 8: return swap ? k_encode_tileg<true, 8, true, 2> : k_encode_tileg<true, 8, false, 2>;
+            default: return nullptr;
+        }
+    }
     switch (item) {
         case 1: return crc ? k_encode_tileg<true, 1, false> : k_encode_tileg<false, 1, false>;
         case 2: return crc ? (swap ? k_encode_tileg<true, 2, true> : k_encode_tileg<true, 2, false>)
@@ -1565,7 +1603,18 @@ EncodeFn select_encode_tile_kernel(bool crc, int item, bool swap) {
     }
 }
 
-EncodeFn select_encode_tile4_kernel(bool crc, int item, bool swap) {
+// nt = 2: the two-tile form (CRC layouts whose plan built its constants)
+EncodeFn select_encode_tile4_kernel(bool crc, int item, bool swap, int nt) {
+    if (nt == 2) {
+        if (!crc) return nullptr;
+        switch (item) {
+            case 1: return k_encode_tile4<true, 1, false, 2>;
+            case 2: return swap ? k_encode_tile4<true, 2, true, 2> : k_encode_tile4<true, 2, false, 2>;
+            case 4: return swap ? k_encode_tile4<true, 4, true, 2> : k_encode_tile4<true, 4, false, 2>;
+            case 8: return swap ? k_encode_tile4<true, 8, true, 2> : k_encode_tile4<true, 8, false, 2>;
+            default: return nullptr;
+        }
+    }
     switch (item) {
         case 1: return crc ? k_encode_tile4<true, 1, false> : k_encode_tile4<false, 1, false>;
         case 2: return crc ? (swap ? k_encode_tile4<true, 2, true> : k_encode_tile4<true, 2, false>)

@@ -757,27 +757,38 @@ static EncodeFn pick_encode_pair(bool crc, int item, bool swap) {
     }
 }
 
-EncodeFn select_encode_tile4_kernel(bool crc, int item, bool swap);  // decode_tile.hip
+EncodeFn select_encode_tile4_kernel(bool crc, int item, bool swap, int nt);  // decode_tile.hip
 EncodeFn select_encode_tile_kernel(bool crc, int item, bool swap);   // decode_tile.hip
-EncodeFn select_encode_tileg_kernel(bool crc, int item, bool swap);  // decode_tile.hip
+EncodeFn select_encode_tileg_kernel(bool crc, int item, bool swap, int nt);  // decode_tile.hip
 
 int launch_encode(const EncodeParams& p, hipStream_t stream, int max_grid) {
     const bool crc = (p.lflags & ZHIP_LF_CRC) != 0;
     const bool swap = (p.lflags & ZHIP_LF_SWAP) != 0;
     if (p.tile4) {  // transposed layouts with full tiles (k_encode_tile4)
-        EncodeFn fn = select_encode_tile4_kernel(crc, p.g.itemsize, swap);
+        // two tiles per workgroup where the plan built their constants (tuning
+        // arm 38 keeps four)
+        const int nt = (crc && p.kq2 && g_tune_arm != 38) ? 2 : 4;
+        EncodeFn fn = select_encode_tile4_kernel(crc, p.g.itemsize, swap, nt);
         if (!fn) return ZHIP_E_UNSUPPORTED;
         if (p.n_chunks == 0) return ZHIP_OK;
-        hipLaunchKernelGGL(fn, dim3(p.n_chunks * (p.t_per_chunk / 4u)), dim3(kThreads), 0, stream, p);
+        EncodeParams q = p;
+        if (nt == 2) q.kq4 = p.kq2;
+        g_last_kernel = nt == 2 ? "k_encode_tile2" : "k_encode_tile4";
+        hipLaunchKernelGGL(fn, dim3(p.n_chunks * (p.t_per_chunk / (uint32_t)nt)), dim3(kThreads), 0, stream, q);
         return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
     }
     if (p.tile == 2) {  // full selections, tiles grouped by four at a uniform step (k_encode_tileg)
-        EncodeFn fn = select_encode_tileg_kernel(crc, p.g.itemsize, swap);
+        // (tuning arm 36: two workgroups per group, two tiles each -- C3 in 128^3
+        // chunks 33.1-34.1 vs 32.8-33.6 us graph-timed, no gain, profiles/r05/p/)
+        const int nt = (crc && g_tune_arm == 36) ? 2 : 4;
+        EncodeFn fn = select_encode_tileg_kernel(crc, p.g.itemsize, swap, nt);
         if (!fn) return ZHIP_E_UNSUPPORTED;
         if (p.n_chunks == 0) return ZHIP_OK;
-        if ((uint64_t)p.n_chunks * p.n_groups >= (1ull << 31) || p.n_groups >= 65536u) return ZHIP_E_UNSUPPORTED;
+        const uint64_t grid = (uint64_t)p.n_chunks * p.n_groups * (uint32_t)(4 / nt);
+        if (grid >= (1ull << 31) || p.n_groups >= 65536u) return ZHIP_E_UNSUPPORTED;
         // (the last arrival of each chunk writes its non-empty flag)
-        hipLaunchKernelGGL(fn, dim3(p.n_chunks * p.n_groups), dim3(kThreads), 0, stream, p);
+        g_last_kernel = nt == 2 ? "k_encode_tileg2" : "k_encode_tileg";
+        hipLaunchKernelGGL(fn, dim3((uint32_t)grid), dim3(kThreads), 0, stream, p);
         return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
     }
     if (p.tile) {  // other transposed layouts / prefix selections (k_encode_tile)

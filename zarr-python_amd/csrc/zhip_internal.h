@@ -307,6 +307,7 @@ struct EncodeParams {
     uint32_t sstride[ZHIP_MAX_DIMS];
     const uint32_t* tz;
     const uint32_t* kq4;
+    const uint32_t* kq2;  // k_encode_tile4's two-tile form: lane constants [T/2][kThreads] (null: four tiles)
     const struct TileEnt* tmap;
     // k_encode_tile (ZHIP_DF_TILE / ZHIP_DF_TILE_PREFIX, not tile4): one tile
     // per workgroup; horner / kthread / kunit / c_inv are the tile tables then
@@ -316,6 +317,7 @@ struct EncodeParams {
     const struct GroupEnt* gmap;
     const uint32_t* gtz;
     uint32_t n_groups, g_step_t, n_sub;
+    uint32_t g_z2;  // k_encode_tileg's two-tile form: x^(8 * 2 g_step_t), the first half's shift to ku's frame
     int64_t g_step_o;
     uint32_t xcd_run;     // k_encode_pair: pairs per XCD-contiguous run (0: dispatch order)
     // 64-bit words between chunks' publication words (k_encode_pair / k_encode_tile4):
@@ -395,6 +397,7 @@ struct zhip_plan {
     uint64_t tile2w_off;  // lane constants [T/2][kThreads] of k_decode_tile4w's two-tile form (0: none)
     uint64_t tile1w_off;  // tuning builds: lane constants [T][kThreads] of the one-tile form (0: none)
     uint64_t tileg2w_off; // lane constants [2 n_groups][kThreads] of k_decode_tilegw's two-tile form (0: none)
+    uint64_t tile2e_off;  // lane constants [T/2][kThreads] of k_encode_tile4's two-tile form (0: none)
     // k_decode_tilegw (grouped tile layouts with a CRC): the same for groups
     uint32_t tilegw;
     uint64_t tilegw_off;
