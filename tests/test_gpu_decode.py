@@ -1345,6 +1345,91 @@ def test_transpose_tile4w_and_tile4(device, dtype, endian, chunks, shape, arm):
         set_tuning(6, 0)
 
 
+def test_transpose_tile4w_many_workgroups_per_chunk(device):
+    """k_decode_tile4w with more than 32 workgroups per chunk (256 tiles of a
+    128 x 64 x 256 int16 chunk: 64 groups of four) reports through subwords
+    of 16 arrivals: exact, a missing chunk filled, a corrupted chunk reported
+    with the reference's message on every launch of one program."""
+    import zarr_hip
+    from zarr_hip import _native as N
+
+    shape, chunks, dtype = (128, 128, 256), (128, 64, 256), "int16"
+    codecs = [T((2, 1, 0)), BE, CRC]
+    _roundtrip(device, shape, chunks, dtype, codecs, fill=3, drop=["c/0/1/0"])
+    assert N.lib().zhip_last_kernel() == b"k_decode_tile4w"
+    meta = O.ArrayMeta(shape, chunks, np.dtype(dtype), 0, codecs=codecs)
+    host = {}
+    O.write(host, meta, (Ellipsis,), _data(shape, dtype))
+    bad = bytearray(host["c/0/1/0"])
+    bad[12345] ^= 0x01
+    host["c/0/1/0"] = bytes(bad)
+    with pytest.raises(ValueError) as want:
+        O.read(host, meta)
+    arr = zarr_hip.Array.create(zarr_hip.DeviceStore.from_host(host, device), shape, chunks, dtype, 0,
+                                codecs=codecs)
+    prog, out = arr.prepare_read((Ellipsis,))
+    for _ in range(3):
+        prog.launch()
+        with pytest.raises(ValueError) as got:
+            prog.results()
+        assert str(got.value) == str(want.value)
+
+
+TILEP_CASES = [  # full tiles that k_decode_tile4 declines: consecutive tile pairs (k_decode_tilep)
+    ("float32", LE, (128, 128, 128), (128, 128, 256), (2, 1, 0)),   # C3 in 128^3 chunks
+    ("int16", BE, (256, 32, 64), (256, 64, 128), (2, 1, 0)),        # (uniform groups: the tile4 plan's pairs)
+    ("float64", LE, (64, 128, 64), (128, 128, 64), (1, 2, 0)),
+]
+
+
+@pytest.mark.tuning
+@pytest.mark.parametrize("dtype,endian,chunks,shape,order", TILEP_CASES)
+def test_transpose_tile_pairs(device, dtype, endian, chunks, shape, order):
+    """Transposed CRC layouts whose tiles are full but whose natural groups of
+    four sit at two steps (k_decode_tile4 declines): one workgroup per pair of
+    consecutive tiles (the two column blocks of a row band), two waves per
+    tile, subword arrival past 32 workgroups per chunk (ZHIP_TUNE_ARM 39) --
+    exact, a missing chunk filled, a corrupted chunk reported with the
+    reference's message."""
+
+    codecs = [T(order), endian, CRC]
+    set_tuning(6, 39)  # (tuning arm: the grouped kernels are the production choice)
+    try:
+        _tile_pairs_case(device, dtype, endian, chunks, shape, order, codecs)
+    finally:
+        set_tuning(6, 0)
+
+
+def _tile_pairs_case(device, dtype, endian, chunks, shape, order, codecs):
+    import zarr_hip
+    from zarr_hip import _native as N
+
+    grid = [sh // ch for sh, ch in zip(shape, chunks)]
+    key = "c/" + "/".join(str(int(x)) for x in np.unravel_index(1, grid))
+    _roundtrip(device, shape, chunks, dtype, codecs, fill=3, drop=[key])
+    # (where the natural groups of four are uniform, tile4's plan takes the same pairs: k_decode_tile2w)
+    assert N.lib().zhip_last_kernel() in (b"k_decode_tilep", b"k_decode_tile2w")
+    meta = O.ArrayMeta(shape, chunks, np.dtype(dtype), 0, codecs=codecs)
+    host = {}
+    O.write(host, meta, (Ellipsis,), _data(shape, dtype))
+    bad = bytearray(host[key])
+    bad[len(bad) // 3 + 7] ^= 0x08
+    host[key] = bytes(bad)
+    with pytest.raises(ValueError) as want:
+        O.read(host, meta)
+    arr = zarr_hip.Array.create(zarr_hip.DeviceStore.from_host(host, device), shape, chunks, dtype, 0,
+                                codecs=codecs)
+    with pytest.raises(ValueError) as got:
+        arr[...]
+    assert str(got.value) == str(want.value)
+    # repeated launches of one program: the arrival words reset themselves
+    prog, out = arr.prepare_read((Ellipsis,))
+    for _ in range(3):
+        prog.launch()
+        with pytest.raises(ValueError):
+            prog.results()
+
+
 @pytest.mark.tuning
 @pytest.mark.parametrize("arm", [0, 5, 38])
 @pytest.mark.parametrize("order", [(2, 1, 0), (1, 2, 0), (0, 2, 1)])

@@ -328,6 +328,9 @@ int zhip_plan_create(const zhip_layout* layout, zhip_plan** out) {
                 if (base[ti] != base[ti & ~3u] + (uint64_t)(ti & 3u) * step) t4 = false;
             p->tile4 = t4 ? 1u : 0u;
             p->tile4_step = step;
+            // k_decode_tile4w over consecutive tile pairs where tile4 declines
+            p->tile2 = (!t4 && (L.flags & ZHIP_LF_CRC) && (L.shape[p->tq] % kTileRows) == 0 &&
+                        (p->row_bytes % kTileCols) == 0 && T % 2 == 0 && T >= 2 && T / 2 <= 65535u) ? 1u : 0u;
             // k_encode_tileg: the innermost other stored dim with shape % 4 == 0
             for (int d = L.ndim - 2; d >= 0 && p->gd < 0; --d)
                 if (d != p->tq && L.shape[d] % 4 == 0) p->gd = d;
@@ -508,7 +511,10 @@ int zhip_plan_upload(zhip_plan* p) {
         const size_t n_tg2w = tgw ? (size_t)p->n_groups * 2 * kThreads : 0;
         // the two-tile form of k_encode_tile4 (CRC, at most 32 workgroups per chunk)
         const size_t n_t2e = (t4 && (L.flags & ZHIP_LF_CRC) && T % 2 == 0 && T / 2 <= 32) ? (size_t)(T / 2) * kThreads : 0;
-        std::vector<uint32_t> ht(n_base + n_t4 + n_g + n_t4f + n_t4w + n_tgw + n_t2w + n_t1w + n_tg2w + n_t2e);
+        // (tuning builds: the tile-pair decode, arm 39 -- 29.8-30.0 vs 29.2-29.4 us
+        // for the grouped kernel on C3 in 128^3 chunks, profiles/r05/q/)
+        const size_t n_t2 = (ZHIP_TUNING && p->tile2) ? kPairTabWords + (size_t)T * 4 + (size_t)(T / 2) * kThreads : 0;
+        std::vector<uint32_t> ht(n_base + n_t4 + n_g + n_t4f + n_t4w + n_tgw + n_t2w + n_t1w + n_tg2w + n_t2e + n_t2);
         build_horner_stride(ht.data(), 16ull * sq);
         for (int t = 0; t < kThreads; ++t) {
             const uint64_t rel = (uint64_t)(kTileRows + t / 16) * sq + 16u * (t % 16);
@@ -688,6 +694,44 @@ int zhip_plan_upload(zhip_plan* p) {
                     ht[p->tile2e_off + (size_t)g2 * kThreads + t] = gf_mul(ht[4096 + t], ku);
             }
         }
+        p->tile2_off = 0;
+        if (n_t2) {
+            p->tile2_off = n_base + n_t4 + n_g + n_t4f + n_t4w + n_tgw + n_t2w + n_t1w + n_tg2w + n_t2e;
+            uint32_t* f = &ht[p->tile2_off];
+            const uint64_t D = 4ull * sq;
+            build_pair_tables(f, D);
+            // tile map (as tile4's): stored base, out offset relative to the chunk's out_off
+            for (uint32_t ti = 0; ti < T; ++ti) {
+                uint32_t r = ti;
+                const uint32_t cb = r % p->n_cb;
+                r /= p->n_cb;
+                const uint32_t qb = r % p->n_qb;
+                r /= p->n_qb;
+                int64_t o = (int64_t)qb * kTileRows * L.out_stride[p->tq] +
+                            (int64_t)cb * (kTileCols / L.itemsize) * L.out_stride[L.ndim - 1];
+                for (int d = L.ndim - 2; d >= 0; --d) {
+                    if (d == p->tq) continue;
+                    o += (int64_t)(r % (uint32_t)L.shape[d]) * L.out_stride[d];
+                    r /= (uint32_t)L.shape[d];
+                }
+                uint32_t* e = &f[kPairTabWords + 4ull * ti];
+                e[0] = (uint32_t)base[ti];
+                e[1] = 0;
+                std::memcpy(e + 2, &o, sizeof(o));
+            }
+            // lane constants: wave w of pair g loads rows 32 (w % 2) + l/16 + 4 m (m < 8) of tile 2 g + w / 2
+            const uint32_t c96 = xpow8_inv(12);
+            uint32_t* kc = f + kPairTabWords + (size_t)T * 4;
+            for (uint32_t g2 = 0; g2 < T / 2; ++g2)
+                for (int t = 0; t < kThreads; ++t) {
+                    const int w = t / 64, l = t % 64;
+                    const int64_t p0 = (int64_t)base[2 * g2 + w / 2] + (int64_t)(32 * (w % 2) + l / 16) * (int64_t)sq +
+                                       16 * (l % 16);
+                    const int64_t e = (int64_t)p->E - p0 + kWgStride - 8 * (int64_t)D;
+                    const uint32_t xe = e >= 0 ? xpow8((uint64_t)e) : xpow8_inv((uint64_t)(-e));
+                    kc[(size_t)g2 * kThreads + t] = gf_mul(gf_mul(xe, p->c_inv), c96);
+                }
+        }
         p->tilegw = tgw ? 1u : 0u;
         p->tilegw_off = n_base + n_t4 + n_g + n_t4f + n_t4w;
         if (tgw) {
@@ -745,8 +789,14 @@ int zhip_plan_info(const zhip_plan* p, uint32_t* units_per_chunk, uint32_t* work
     // (k_decode_tilegw's two-tile form: arrival subwords for twice the groups)
     // (known at plan creation, before the tile tables exist)
     const bool tg2w = p->gd >= 0 && (p->layout.flags & ZHIP_LF_CRC);
-    const uint32_t n_sub2 = (tg2w && 2 * p->n_groups > 16u && 2 * p->n_groups <= 256u)
-                                ? (2 * p->n_groups + 15u) / 16u : 0u;
+    uint32_t n_sub2 = (tg2w && 2 * p->n_groups > 16u && 2 * p->n_groups <= 256u)
+                          ? (2 * p->n_groups + 15u) / 16u : 0u;
+    // (the tile-pair decode, tuning builds: subwords of 16 for 33..256 workgroups per chunk)
+    const uint32_t wpc2 = (ZHIP_TUNING && p->tile2) ? p->t_per_chunk / 2u : 0u;
+    if (wpc2 > 32u && wpc2 <= 256u) n_sub2 = std::max(n_sub2, (wpc2 + 15u) / 16u);
+    // (k_decode_tile4w, four tiles per workgroup: the same subwords past 32 workgroups per chunk)
+    const uint32_t wpc4 = (p->tile4 && (p->layout.flags & ZHIP_LF_CRC)) ? p->t_per_chunk / 4u : 0u;
+    if (wpc4 > 32u && wpc4 <= 256u) n_sub2 = std::max(n_sub2, (wpc4 + 15u) / 16u);
     if (workspace_words)
         *workspace_words = std::max(4 + 2 * std::max(std::max(p->n_sub, p->xw_nsub), n_sub2),
                                     (p->layout.flags & ZHIP_LF_CRC) ? kPubLine : 0u);
@@ -1003,6 +1053,13 @@ int zhip_decode_mapped(const zhip_plan* plan, const void* src, uint64_t src_size
                 if (plan->tile2w_off) p.t2w_kq = plan->d_tile_tables + plan->tile2w_off;
                 if (plan->tile1w_off) p.t1w_kq = plan->d_tile_tables + plan->tile1w_off;
             }
+        } else if (plan->tile2 && plan->tile2_off && !(g_tune_bits & kTuneTile1) && g_tune_arm == 39) {
+            // consecutive tile pairs (k_decode_tile4w<2>) where tile4 declines
+            // (tuning arm 39; the grouped kernels are faster)
+            p.tile2 = 1;
+            p.t4w_tab = plan->d_tile_tables + plan->tile2_off;
+            p.tmap = reinterpret_cast<const TileEnt*>(p.t4w_tab + kPairTabWords);
+            p.t4w_kq = p.t4w_tab + kPairTabWords + (size_t)plan->t_per_chunk * 4;
         } else if (plan->gd >= 0 && !(g_tune_bits & kTuneTile1) &&
                    L.shape[plan->tq] % (16 / L.itemsize) == 0) {
             // k_decode_tileg: tiles grouped by four along gd, whole out pieces

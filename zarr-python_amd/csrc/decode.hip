@@ -801,6 +801,17 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
         hipLaunchKernelGGL(fn, dim3(p.n_units / 4u), dim3(kThreads), 0, stream, p);
         return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
     }
+    if (p.tq >= 0 && p.tile2) {
+        // consecutive tile pairs (k_decode_tile4w<2>, decode_tile.hip): 128^3
+        // chunks' two 256-byte column blocks of one row band per workgroup
+        KernelFn fn = select_tile2w_kernel(p.g.itemsize, (p.lflags & ZHIP_LF_SWAP) != 0, 2);
+        if (!fn) return ZHIP_E_UNSUPPORTED;
+        if (p.n_units == 0) return ZHIP_OK;
+        if (p.n_units / 2u >= (1u << 31)) return ZHIP_E_UNSUPPORTED;
+        g_last_kernel = "k_decode_tilep";
+        hipLaunchKernelGGL(fn, dim3(p.n_units / 2u), dim3(kThreads), 0, stream, p);
+        return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
+    }
     if (p.tq >= 0 && p.tileg) {
         // tiles grouped by four along a stored dim (k_decode_tileg, decode_tile.hip)
         // (k_decode_tilegw when the plan's wave-per-tile chains are selected)

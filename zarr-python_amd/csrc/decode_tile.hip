@@ -461,6 +461,42 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
 // Production for transposed layouts with a CRC since round 4: C3 28.9 vs
 // 30.3-30.6 us graph-timed (profiles/r04/k/arms_c3.jsonl); ZHIP_TUNE_ARM 5
 // (or 1 / 2, its publication arms) takes k_decode_tile4.
+// Arrival of one workgroup of a grouped tile kernel (k_decode_tileg /
+// k_encode_tileg) with its CRC contribution v and non-empty bit: 64-bit words
+// CRC (low 32) | arrival bits (32..47) | non-empty bits (48..63), one relaxed
+// XOR per level.  Up to 16 groups per chunk the chunk word is the only level;
+// up to 256 the groups first meet in words of 16 (the workspace tail after the
+// 4 words per chunk), whose completing arrival carries the subgroup's XOR on
+// to the chunk word.  True for the arrival completing the chunk, with the
+// XOR of every contribution and whether any group was non-empty.
+__device__ __forceinline__ bool tileg_arrive(uint32_t* ws, uint32_t n_chunks, uint32_t c, uint32_t grp,
+                                             uint32_t gpc, uint32_t n_sub, uint32_t v, bool ne, uint32_t& raw,
+                                             bool& any_ne) {
+    if (n_sub) {
+        const uint32_t sg = grp >> 4;
+        const uint32_t in_sg = min(16u, gpc - (sg << 4));
+        uint64_t* sw = reinterpret_cast<uint64_t*>(ws + 4ull * n_chunks) + (uint64_t)c * n_sub + sg;
+        const uint64_t b = 1ull << (grp & 15u);
+        const uint64_t prev = __hip_atomic_fetch_xor(sw, (b << 32) | (ne ? b << 48 : 0ull) | v, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+        if ((((prev >> 32) & 0xFFFFull) ^ b) != (1ull << in_sg) - 1ull) return false;
+        __hip_atomic_store(sw, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        v ^= (uint32_t)prev;
+        ne = ne || ((prev >> 48) & 0xFFFFull) != 0ull;
+        grp = sg;
+        gpc = n_sub;
+    }
+    uint64_t* cw = reinterpret_cast<uint64_t*>(ws) + 2ull * c;
+    const uint64_t b = 1ull << grp;
+    const uint64_t prev = __hip_atomic_fetch_xor(cw, (b << 32) | (ne ? b << 48 : 0ull) | v, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+    if ((((prev >> 32) & 0xFFFFull) ^ b) != (1ull << gpc) - 1ull) return false;
+    __hip_atomic_store(cw, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    raw = (uint32_t)prev ^ v;
+    any_ne = ne || ((prev >> 48) & 0xFFFFull) != 0ull;
+    return true;
+}
+
 template <int N>
 struct TileMapN {
     TileEnt e[N];
@@ -590,7 +626,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
                         raw = (uint32_t)prev ^ V;
                         last_arrival = 1;
                     }
-                } else {  // more than 32 workgroups per chunk: xor, then count arrivals
+                } else if (gpc <= 256u) {  // subwords of 16 workgroups (tile pairs of large chunks)
+                    bool any_ne;
+                    last_arrival = tileg_arrive(p.ws, p.n_chunks, c, grp, gpc, (gpc + 15u) / 16u, V, false, raw,
+                                                any_ne) ? 1u : 0u;
+                } else {  // more than 256 workgroups per chunk: xor, then count arrivals
                     uint32_t* accw = p.ws + 4ull * c;
                     const uint32_t prev = __hip_atomic_fetch_xor(accw, V, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     asm volatile("s_waitcnt vmcnt(0)" ::"v"(prev) : "memory");
@@ -617,42 +657,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
         p.status[c] = st;
         if (U.mode != ZHIP_ST_MISSING) atomicOr(p.errflag, 1u << U.mode);
     }
-}
-
-// Arrival of one workgroup of a grouped tile kernel (k_decode_tileg /
-// k_encode_tileg) with its CRC contribution v and non-empty bit: 64-bit words
-// CRC (low 32) | arrival bits (32..47) | non-empty bits (48..63), one relaxed
-// XOR per level.  Up to 16 groups per chunk the chunk word is the only level;
-// up to 256 the groups first meet in words of 16 (the workspace tail after the
-// 4 words per chunk), whose completing arrival carries the subgroup's XOR on
-// to the chunk word.  True for the arrival completing the chunk, with the
-// XOR of every contribution and whether any group was non-empty.
-__device__ __forceinline__ bool tileg_arrive(uint32_t* ws, uint32_t n_chunks, uint32_t c, uint32_t grp,
-                                             uint32_t gpc, uint32_t n_sub, uint32_t v, bool ne, uint32_t& raw,
-                                             bool& any_ne) {
-    if (n_sub) {
-        const uint32_t sg = grp >> 4;
-        const uint32_t in_sg = min(16u, gpc - (sg << 4));
-        uint64_t* sw = reinterpret_cast<uint64_t*>(ws + 4ull * n_chunks) + (uint64_t)c * n_sub + sg;
-        const uint64_t b = 1ull << (grp & 15u);
-        const uint64_t prev = __hip_atomic_fetch_xor(sw, (b << 32) | (ne ? b << 48 : 0ull) | v, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT);
-        if ((((prev >> 32) & 0xFFFFull) ^ b) != (1ull << in_sg) - 1ull) return false;
-        __hip_atomic_store(sw, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        v ^= (uint32_t)prev;
-        ne = ne || ((prev >> 48) & 0xFFFFull) != 0ull;
-        grp = sg;
-        gpc = n_sub;
-    }
-    uint64_t* cw = reinterpret_cast<uint64_t*>(ws) + 2ull * c;
-    const uint64_t b = 1ull << grp;
-    const uint64_t prev = __hip_atomic_fetch_xor(cw, (b << 32) | (ne ? b << 48 : 0ull) | v, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-    if ((((prev >> 32) & 0xFFFFull) ^ b) != (1ull << gpc) - 1ull) return false;
-    __hip_atomic_store(cw, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    raw = (uint32_t)prev ^ v;
-    any_ne = ne || ((prev >> 48) & 0xFFFFull) != 0ull;
-    return true;
 }
 
 // k_decode_tileg: k_decode_tile4 for the transposed layouts it declines

@@ -110,6 +110,7 @@ struct DecodeParams {
     zhip_fdiv d_qb, d_cb;
     // k_decode_tile4 (tile4 != 0): see zhip_plan
     uint32_t tile4;
+    uint32_t tile2;  // k_decode_tile4w's two-tile form over consecutive tile pairs (plans without tile4)
     const uint32_t* tz;
     const uint32_t* kq4;
     const struct TileEnt* tmap;
@@ -398,6 +399,13 @@ struct zhip_plan {
     uint64_t tile1w_off;  // tuning builds: lane constants [T][kThreads] of the one-tile form (0: none)
     uint64_t tileg2w_off; // lane constants [2 n_groups][kThreads] of k_decode_tilegw's two-tile form (0: none)
     uint64_t tile2e_off;  // lane constants [T/2][kThreads] of k_encode_tile4's two-tile form (0: none)
+    // full-tile layouts that tile4 declines (e.g. 128^3 chunks: the four tiles
+    // of a natural group at two steps) but whose consecutive tile pairs are the
+    // two column blocks of one row band: k_decode_tile4w<2> over pairs (2 k,
+    // 2 k + 1), tuning arm 39; d_tile_tables at tile2_off (tuning builds): A_(4 sq)
+    // pair tables | tile map (T TileEnt) | lane constants [T/2][kThreads]
+    uint32_t tile2;
+    uint64_t tile2_off;
     // k_decode_tilegw (grouped tile layouts with a CRC): the same for groups
     uint32_t tilegw;
     uint64_t tilegw_off;
