@@ -1431,7 +1431,7 @@ def _tile_pairs_case(device, dtype, endian, chunks, shape, order, codecs):
 
 
 @pytest.mark.tuning
-@pytest.mark.parametrize("arm", [0, 5, 38])
+@pytest.mark.parametrize("arm", [0, 5, 38, 40])
 @pytest.mark.parametrize("order", [(2, 1, 0), (1, 2, 0), (0, 2, 1)])
 @pytest.mark.parametrize("dtype,endian", [("float32", LE), ("int16", BE), ("float64", LE), ("uint8", LE)])
 def test_transpose_tilegw_and_tileg(device, order, dtype, endian, arm):
@@ -1444,7 +1444,7 @@ def test_transpose_tilegw_and_tileg(device, order, dtype, endian, arm):
     from zarr_hip import _native as N
 
     codecs = [T(order), endian, CRC]
-    kernel = {0: b"k_decode_tileg2w", 5: b"k_decode_tileg", 38: b"k_decode_tilegw"}[arm]
+    kernel = {0: b"k_decode_tileg2w", 5: b"k_decode_tileg", 38: b"k_decode_tilegw", 40: b"k_decode_tileglt"}[arm]
     set_tuning(6, arm)
     try:
         _roundtrip(device, (96, 160, 160), (96, 80, 80), dtype, codecs, fill=3, drop=["c/0/1/0"])

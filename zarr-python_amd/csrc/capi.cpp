@@ -514,7 +514,9 @@ int zhip_plan_upload(zhip_plan* p) {
         // (tuning builds: the tile-pair decode, arm 39 -- 29.8-30.0 vs 29.2-29.4 us
         // for the grouped kernel on C3 in 128^3 chunks, profiles/r05/q/)
         const size_t n_t2 = (ZHIP_TUNING && p->tile2) ? kPairTabWords + (size_t)T * 4 + (size_t)(T / 2) * kThreads : 0;
-        std::vector<uint32_t> ht(n_base + n_t4 + n_g + n_t4f + n_t4w + n_tgw + n_t2w + n_t1w + n_tg2w + n_t2e + n_t2);
+        const size_t n_tgl = (ZHIP_TUNING && tgw) ? (size_t)p->n_groups * kThreads : 0;  // lane-tile form, arm 40
+        std::vector<uint32_t> ht(n_base + n_t4 + n_g + n_t4f + n_t4w + n_tgw + n_t2w + n_t1w + n_tg2w + n_t2e + n_t2 +
+                                 n_tgl);
         build_horner_stride(ht.data(), 16ull * sq);
         for (int t = 0; t < kThreads; ++t) {
             const uint64_t rel = (uint64_t)(kTileRows + t / 16) * sq + 16u * (t % 16);
@@ -730,6 +732,25 @@ int zhip_plan_upload(zhip_plan* p) {
                     const int64_t e = (int64_t)p->E - p0 + kWgStride - 8 * (int64_t)D;
                     const uint32_t xe = e >= 0 ? xpow8((uint64_t)e) : xpow8_inv((uint64_t)(-e));
                     kc[(size_t)g2 * kThreads + t] = gf_mul(gf_mul(xe, p->c_inv), c96);
+                }
+        }
+        p->tilegl_off = 0;
+        if (n_tgl) {
+            // lane l of wave w: rows w + 4 m (m < 16) of tile l / 16 at column block l % 16
+            p->tilegl_off = n_base + n_t4 + n_g + n_t4f + n_t4w + n_tgw + n_t2w + n_t1w + n_tg2w + n_t2e + n_t2;
+            uint32_t* f = &ht[p->tilegl_off];
+            const uint64_t D = 4ull * sq;
+            const uint32_t c96 = xpow8_inv(12);
+            const GroupEnt* gm = reinterpret_cast<const GroupEnt*>(&ht[p->g_off_map]);
+            const int64_t gstep = (int64_t)p->sstride[p->gd];
+            for (uint32_t g = 0; g < p->n_groups; ++g)
+                for (int t = 0; t < kThreads; ++t) {
+                    const int w = t / 64, l = t % 64;
+                    const int64_t p0 = (int64_t)gm[g].tbase + (int64_t)(l / 16) * gstep + (int64_t)w * (int64_t)sq +
+                                       16 * (l % 16);
+                    const int64_t e = (int64_t)p->E - p0 + kWgStride - 16 * (int64_t)D;
+                    const uint32_t xe = e >= 0 ? xpow8((uint64_t)e) : xpow8_inv((uint64_t)(-e));
+                    f[(size_t)g * kThreads + t] = gf_mul(gf_mul(xe, p->c_inv), c96);
                 }
         }
         p->tilegw = tgw ? 1u : 0u;
@@ -1074,6 +1095,7 @@ int zhip_decode_mapped(const zhip_plan* plan, const void* src, uint64_t src_size
                 p.t4w_tab = plan->d_tile_tables + plan->tilegw_off;
                 p.t4w_kq = p.t4w_tab + kPairTabWords;
                 if (plan->tileg2w_off) p.t2w_kq = plan->d_tile_tables + plan->tileg2w_off;  // two tiles per workgroup
+                if (plan->tilegl_off) p.tglt_kq = plan->d_tile_tables + plan->tilegl_off;    // (arm 40)
             }
         }
         const uint64_t tunits = (uint64_t)n_chunks * plan->t_per_chunk;

@@ -820,17 +820,22 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
         const bool defer = p.defer != 0 && g_tune_arm != 2;
         // two tiles per workgroup where the plan built their constants (as
         // k_decode_tile4w); tuning arms 38 (deferred) / 2 (returning) keep four
-        const int nt = (gw && p.t2w_kq && g_tune_arm != 38 && g_tune_arm != 2) ? 2 : 4;
+        int nt = (gw && p.t2w_kq && g_tune_arm != 38 && g_tune_arm != 2 && g_tune_arm != 40) ? 2 : 4;
+#if ZHIP_TUNING
+        if (gw && g_tune_arm == 40 && p.tglt_kq) nt = 5;  // four tiles, lanes pick the tile
+#endif
         KernelFn fn = gw ? select_tilegw_kernel(p.g.itemsize, (p.lflags & ZHIP_LF_SWAP) != 0, defer, nt)
                          : select_tileg_kernel((p.lflags & ZHIP_LF_CRC) != 0, p.g.itemsize,
                                                (p.lflags & ZHIP_LF_SWAP) != 0, defer);
         if (!fn) return ZHIP_E_UNSUPPORTED;
         if (p.n_chunks == 0) return ZHIP_OK;
-        const uint64_t ggrid = (uint64_t)p.n_chunks * p.n_groups * (uint32_t)(4 / nt);
+        const uint64_t ggrid = (uint64_t)p.n_chunks * p.n_groups * (uint32_t)(nt == 2 ? 2 : 1);
         if (ggrid >= (1ull << 31)) return ZHIP_E_UNSUPPORTED;
         DecodeParams q = p;
         if (nt == 2) q.t4w_kq = p.t2w_kq;
-        g_last_kernel = !gw ? "k_decode_tileg" : nt == 2 ? "k_decode_tileg2w" : "k_decode_tilegw";
+        if (nt == 5) q.t4w_kq = p.tglt_kq;
+        g_last_kernel = !gw ? "k_decode_tileg" : nt == 2 ? "k_decode_tileg2w" : nt == 5 ? "k_decode_tileglt"
+                                                                                      : "k_decode_tilegw";
         hipLaunchKernelGGL(fn, dim3((uint32_t)ggrid), dim3(kThreads), 0, stream, q);
         return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
     }

@@ -845,9 +845,17 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
 // NT: tiles per workgroup -- 4, or 2 (two workgroups per group of four, two
 // waves per tile as in k_decode_tile4w's two-tile form; the returning
 // publication then xors and counts per chunk)
-template <int ITEM, bool SWAP, int PUB = 2, int NT = kTiles>
+// LT (four tiles, tuning arm 40): lanes, not waves, pick the tile -- lane l of
+// wave w loads rows w + 4 m of tile l / 16 (column block l % 16), so one load
+// instruction reads one row of all four tiles (four 256-byte pieces one
+// group step apart) instead of four rows of one tile (a stored-row stride
+// apart: 64 KiB in 128^3 chunks); the chain is the same A_(4 sq) one, the lane
+// constants swap the roles of w and l / 16, and in tile iteration j the 16
+// lanes of every wave that hold tile j write the image.
+template <int ITEM, bool SWAP, int PUB = 2, int NT = kTiles, bool LT = false>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_decode_tilegw(
     const DecodeParams p) {
+    static_assert(!LT || NT == kTiles, "lane-tile mapping: four tiles per workgroup");
     constexpr int kPer = 16 / ITEM;
     constexpr int kPiecesPerCol = kTileRows / kPer;
     constexpr int WPT = kTiles / NT;        // waves per tile
@@ -861,8 +869,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     uint32_t* const s_red = s_mem + kPairTabWords;  // after the last out-order pass
     const int t = threadIdx.x;
     const uint32_t wv = __builtin_amdgcn_readfirstlane((uint32_t)t >> 6);
-    const uint32_t tj = wv / WPT, hh = wv % WPT;  // this wave's tile (of the workgroup's) and row band
-    const uint32_t ln = (uint32_t)t & 63u, rg = ln >> 4, cl = 16u * (ln & 15u);
+    const uint32_t ln = (uint32_t)t & 63u, cl = 16u * (ln & 15u);
+    // the lane's tile (of the workgroup's), row band and first row
+    const uint32_t tj = LT ? (ln >> 4) : wv / WPT, hh = LT ? 0u : wv % WPT;
+    const uint32_t rg = LT ? wv : (ln >> 4);
     const uint32_t gpc = p.n_groups * PG;  // workgroups per chunk
     const uint32_t c = blockIdx.x / gpc;
     const uint32_t wg = blockIdx.x - c * gpc;
@@ -1655,9 +1665,16 @@ KernelFn select_tileg_kernel(bool crc, int item, bool swap, bool defer) {
 }
 
 KernelFn select_tilegw_kernel(int item, bool swap, bool defer, int nt) {  // CRC chains only
+#if ZHIP_TUNING
+#define ZHIP_TILEGW(I, W)                                                                          \
+    (nt == 2 ? (defer ? k_decode_tilegw<I, W, 2, 2> : k_decode_tilegw<I, W, 0, 2>)                 \
+     : nt == 5 ? (defer ? k_decode_tilegw<I, W, 2, 4, true> : k_decode_tilegw<I, W, 0, 4, true>)   \
+             : (defer ? k_decode_tilegw<I, W, 2> : k_decode_tilegw<I, W, 0>))
+#else
 #define ZHIP_TILEGW(I, W)                                                                          \
     (nt == 2 ? (defer ? k_decode_tilegw<I, W, 2, 2> : k_decode_tilegw<I, W, 0, 2>)                 \
              : (defer ? k_decode_tilegw<I, W, 2> : k_decode_tilegw<I, W, 0>))
+#endif
     switch (item) {
         case 1: return ZHIP_TILEGW(1, false);
         case 2: return swap ? ZHIP_TILEGW(2, true) : ZHIP_TILEGW(2, false);

@@ -123,6 +123,7 @@ struct DecodeParams {
     const uint32_t* t4w_kq;
     const uint32_t* t2w_kq;  // k_decode_tile4w with two tiles per workgroup (production when set): lane constants
     const uint32_t* t1w_kq;  // tuning arm 37 (one tile per workgroup)
+    const uint32_t* tglt_kq; // tuning arm 40 (k_decode_tilegw, lanes pick the tile): lane constants
     // k_decode_tileg (tileg != 0): group map, step multiply table, steps
     uint32_t tileg;
     const struct GroupEnt* gmap;
@@ -398,6 +399,7 @@ struct zhip_plan {
     uint64_t tile2w_off;  // lane constants [T/2][kThreads] of k_decode_tile4w's two-tile form (0: none)
     uint64_t tile1w_off;  // tuning builds: lane constants [T][kThreads] of the one-tile form (0: none)
     uint64_t tileg2w_off; // lane constants [2 n_groups][kThreads] of k_decode_tilegw's two-tile form (0: none)
+    uint64_t tilegl_off;  // tuning builds: lane constants [n_groups][kThreads] of its lane-tile form (0: none)
     uint64_t tile2e_off;  // lane constants [T/2][kThreads] of k_encode_tile4's two-tile form (0: none)
     // full-tile layouts that tile4 declines (e.g. 128^3 chunks: the four tiles
     // of a natural group at two steps) but whose consecutive tile pairs are the
