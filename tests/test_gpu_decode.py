@@ -1262,6 +1262,16 @@ ILW_CASES = [  # (shape, chunks, inner chunks or None, dtype, endian)
 
 
 @pytest.mark.tuning
+@pytest.mark.parametrize("case", [0, 1, 3])
+def test_ilh_arm_exact_and_crc(device, case):
+    """k_decode_ilh (ZHIP_TUNE_ARM 41: 16 KiB per workgroup, the pair tables'
+    A_4096 chain, two-level arrival past 32 workgroups per chunk) decodes
+    exactly and reports corrupted chunks and indexes with the reference's
+    messages."""
+    _ilw_case(device, 41, case)
+
+
+@pytest.mark.tuning
 @pytest.mark.parametrize("arm", [26, 27, 31, 32])
 @pytest.mark.parametrize("case", range(len(ILW_CASES)))
 def test_ilw_arms_exact_and_crc(device, arm, case):
@@ -1269,6 +1279,10 @@ def test_ilw_arms_exact_and_crc(device, arm, case):
     small-share shape) decodes exactly -- whole array, a partial window, a
     missing chunk filled -- and reports a corrupted chunk (and, sharded, a
     corrupted index) with the reference's message."""
+    _ilw_case(device, arm, case)
+
+
+def _ilw_case(device, arm, case):
     import zarr_hip
     from zarr_hip import _native as N
 
@@ -1279,7 +1293,8 @@ def test_ilw_arms_exact_and_crc(device, arm, case):
     O.write(host, meta, (Ellipsis,), _data(shape, dtype))
     if not inner:
         host.pop("c/1/0/0")
-    want_kernel = {26: "k_decode_ilw1024", 27: "k_decode_ilw512", 31: "k_decode_ilw1024r", 32: "k_decode_ilw512r"}[arm]
+    want_kernel = {26: "k_decode_ilw1024", 27: "k_decode_ilw512", 31: "k_decode_ilw1024r", 32: "k_decode_ilw512r",
+                   41: "k_decode_ilh"}[arm]
     set_tuning(6, arm)
     try:
         store = zarr_hip.DeviceStore.from_host(host, device)

@@ -365,7 +365,8 @@ int zhip_plan_upload(zhip_plan* p) {
                      p->nseg <= 256u;
     size_t n_ilw[2] = {0, 0};
     for (int i = ZHIP_TUNING ? 0 : 1; i < 2 && ilw; ++i) n_ilw[i] = kPairTabWords + (size_t)p->nseg * (1024u >> i) + kThreads;
-    std::vector<uint32_t> h(n_old + n_pair + n_il + n_xw + n_ilw[0] + n_ilw[1]);
+    const size_t n_ilh = (ZHIP_TUNING && p->il_S == 8u && 2 * p->nseg <= 64u) ? (size_t)2 * p->nseg * kThreads : 0;
+    std::vector<uint32_t> h(n_old + n_pair + n_il + n_xw + n_ilw[0] + n_ilw[1] + n_ilh);
     build_horner(h.data());
     for (int t = 0; t < kThreads; ++t) h[4096 + t] = xpow8((uint64_t)kWgStride - 16u * t);
     for (uint32_t s = 0; s < p->nseg; ++s) h[4096 + kThreads + s] = xpow8((uint64_t)s * p->seg);
@@ -470,6 +471,22 @@ int zhip_plan_upload(zhip_plan* p) {
             w[kPairTabWords + (size_t)p->nseg * NT + t] =
                 gf_mul(h[n_old + kPairTabWords + (size_t)p->nseg * kThreads + t], back);
         at += n_ilw[i];
+    }
+    // k_decode_ilh (tuning arm 41): lane t of half unit u = 2 r + h takes the
+    // sub-steps 8 r + 4 h + k (k < 4) at 16 t through A_4096; the constant
+    // x^(8 (4096 (n_steps - st0 - 3) - 16 t)) c_inv x^(-96), st0 = 8 r + 4 h
+    p->off_ilh = 0;
+    if (n_ilh) {
+        p->off_ilh = at;
+        const int64_t n_steps = (int64_t)p->nseg * kDefaultBlocks;
+        for (uint32_t uu = 0; uu < 2 * p->nseg; ++uu)
+            for (int t = 0; t < kThreads; ++t) {
+                const int64_t st0 = 8 * (int64_t)(uu >> 1) + 4 * (int64_t)(uu & 1u);
+                const int64_t e = (int64_t)kWgStride * (n_steps - st0 - 3) - 16 * t;
+                const uint32_t xe = e >= 0 ? xpow8((uint64_t)e) : xpow8_inv((uint64_t)(-e));
+                h[at + (size_t)uu * kThreads + t] = gf_mul(gf_mul(xe, p->c_inv), c96);
+            }
+        at += n_ilh;
     }
     if (p->d_tables) (void)hipFree(p->d_tables);
     p->d_tables = nullptr;
@@ -984,6 +1001,7 @@ int zhip_decode_mapped(const zhip_plan* plan, const void* src, uint64_t src_size
             p.ilw_kidx = p.ilw_klane + (size_t)plan->nseg * p.ilw_nt;
         }
     }
+    if (plan->off_ilh) p.ilh_klane = plan->d_tables + plan->off_ilh;
     for (int op = 0; op < 4; ++op) p.hx[op] = plan->hx[op];
     for (int i = 0; i < 32; ++i) p.kq[i] = plan->kq[i];
     p.n_chunks = n_chunks;

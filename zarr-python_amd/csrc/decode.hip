@@ -505,6 +505,7 @@ KernelFn select_xw_kernel(bool crc, int item, bool swap);            // decode_r
 KernelFn select_ilq_kernel(int item, bool swap, int nq, bool glds);  // decode_rows.hip
 KernelFn select_ilc_kernel(int item, bool swap);                     // decode_rows.hip
 KernelFn select_ilp_kernel(int item, bool swap);                     // decode_rows.hip
+KernelFn select_ilh_kernel(int item, bool swap);                     // decode_rows.hip
 KernelFn select_tile4f_kernel(int item, bool swap);                  // decode_tile.hip
 #endif
 KernelFn select_tile4_kernel(bool crc, int item, bool swap);         // decode_tile.hip
@@ -636,6 +637,16 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
             g_last_kernel = p.ilw_nt == 1024u ? (g_tune_arm >= 31 ? "k_decode_ilw1024r" : "k_decode_ilw1024")
                                               : (g_tune_arm >= 31 ? "k_decode_ilw512r" : "k_decode_ilw512");
             hipLaunchKernelGGL(wfn, dim3(wgrid), dim3(p.ilw_nt), 0, stream, p);
+            return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
+        }
+        if (il && g_tune_arm == 41 && p.ilh_klane) {  // k_decode_ilh: 16 KiB per workgroup
+            KernelFn hfn = select_ilh_kernel(p.g.itemsize, swap);
+            if (!hfn) return ZHIP_E_UNSUPPORTED;
+            const uint32_t hunits = 2u * p.n_units;
+            const uint32_t hgrid = hunits > p.n_idx ? hunits : p.n_idx;
+            if (hgrid == 0) return ZHIP_OK;
+            g_last_kernel = "k_decode_ilh";
+            hipLaunchKernelGGL(hfn, dim3(hgrid), dim3(kThreads), 0, stream, p);
             return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
         }
         if (il && g_tune_arm == 35 && p.pred) {  // k_decode_ilp: index entry off the stores' path

@@ -2103,6 +2103,140 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))
 }
 
 // ---------------------------------------------------------------------------
+// k_decode_ilh (tuning arm 41): half units -- 16 KiB per workgroup (4 096 on
+// the headline: four residency rounds instead of two, the change that gave
+// the transposes 1.6 us), lane t taking the four 4 KiB sub-steps 8 r + 4 h + k
+// of its segment's half h at 16 t: one chain through the pair kernel's
+// A_4096 tables, lane constants per (half unit, lane) from capi.cpp; up to
+// 64 workgroups per chunk publish per 32-workgroup word with a second level.
+template <int ITEM, bool SWAP>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_decode_ilh(
+    const DecodeParams p) {
+    constexpr int KW = 4;
+    __shared__ uint32_t s_tab[kPairTabWords];
+    __shared__ uint32_t s_mul[12 * kThreads];
+    __shared__ uint32_t s_red[2][kThreads / 64];
+    const int t = threadIdx.x;
+    const uint32_t G = gridDim.x, g = blockIdx.x;
+    const uint32_t wpc = 2u * p.nseg;
+    const uint32_t c = g / wpc, u = g - c * wpc, r = u >> 1, hh = u & 1u;
+    const bool has = c < p.n_chunks;
+    if (!has && g >= p.n_idx) return;
+    const uint32_t expected = p.g.nbytes + 4u;
+    const uint8_t* zero = reinterpret_cast<const uint8_t*>(g_rows_zero);
+    const uint4* gt = reinterpret_cast<const uint4*>(p.pair_tab);
+    const uint4 tv0 = gt[t], tv1 = gt[t + kThreads], tv2 = gt[t + 2 * kThreads], tv3 = gt[t + 3 * kThreads],
+                tv4 = gt[t + 4 * kThreads], tv5 = gt[t + 5 * kThreads];
+    const uint32_t kl = load_u32_any(reinterpret_cast<const uint8_t*>(p.ilh_klane + (size_t)(has ? u : 0u) * kThreads + t));
+    const uint32_t kix = load_u32_any(reinterpret_cast<const uint8_t*>(p.kthread11 + t));
+    Unit U;
+    if (has) U = resolve_unit(p, c * p.nseg, expected);
+    else {
+        U.c = 0;
+        U.sidx = 0;
+        U.mode = ZHIP_ST_MISSING;
+        U.cp = zero;
+        U.seg_lo = 0;
+        U.sel = 0;
+        U.out_off = 0;
+    }
+    const bool ok = has && U.mode == ZHIP_ST_OK;
+    const int32_t lo_frame = (int32_t)p.E - (int32_t)(p.nseg * p.seg);
+    const uint4 ipre = index_prefetch(p, g, g < p.n_idx, t, zero);
+    uint4 A[KW];
+#pragma unroll
+    for (int k = 0; k < KW; ++k) {
+        const int32_t base = lo_frame + kWgStride * (int32_t)(8u * r + 4u * hh + (uint32_t)k);
+        A[k] = load_stream16_any(ok && base >= 0 ? U.cp + base + 16 * t : zero);
+    }
+    zhip_rowblk m[KW];
+    const uint32_t sidx = p.nseg - 1u - r;
+#pragma unroll
+    for (int k = 0; k < KW; ++k)
+        m[k] = load_uniform<zhip_rowblk>(p.rowmap + ((size_t)U.sel * p.nseg + sidx) * kDefaultBlocks + 4u * hh +
+                                         (uint32_t)k);
+    uint32_t stored = 0;
+    if (ok) stored = load_trailer_uniform(U.cp, p.g.nbytes);
+    {
+        uint4* stt = reinterpret_cast<uint4*>(s_tab);
+        stt[t] = tv0;
+        stt[t + kThreads] = tv1;
+        stt[t + 2 * kThreads] = tv2;
+        stt[t + 3 * kThreads] = tv3;
+        stt[t + 4 * kThreads] = tv4;
+        stt[t + 5 * kThreads] = tv5;
+        lanemul3_init(s_mul, t, kl);
+    }
+    __syncthreads();
+    if (has) {
+        uint8_t* sink = reinterpret_cast<uint8_t*>(g_rows_sink);
+        const uint32_t lane_row = (16u * (uint32_t)t) >> p.row_shift;
+        const uint32_t lane_col = (16u * (uint32_t)t) & ((1u << p.row_shift) - 1u);
+        const int64_t lane_off = (int64_t)lane_row * p.r_oy + (int64_t)lane_col;
+        const bool writes = ok || U.mode == ZHIP_ST_MISSING;
+        uint8_t* const obase = p.out + U.out_off;
+        const uint4 f = make_uint4(p.fill[0], p.fill[1], p.fill[2], p.fill[3]);
+        Acc4 acc = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int k = 0; k < KW; ++k) {
+            const uint32_t lo = m[k].lo, hi = m[k].hi;
+            const bool wr = writes && lane_row - lo < hi - lo;
+            store_nt16(wr ? obase + m[k].rel + lane_off : sink, ok ? swap_block<ITEM, SWAP>(A[k]) : f);
+            if (ok) crc_block4(s_tab, acc, A[k]);
+        }
+        uint32_t v = ok ? lanemul3(s_mul, t, fold4(s_tab, acc)) : 0u;
+        v = wave_xor(v);
+        if ((t & 63) == 0) s_red[0][t >> 6] = v;
+        __syncthreads();
+        if (ok && t < 64) {
+            const uint32_t V = __builtin_amdgcn_readfirstlane(s_red[0][0] ^ s_red[0][1] ^ s_red[0][2] ^ s_red[0][3]);
+            const uint32_t st = __builtin_amdgcn_readfirstlane(stored);
+            if (wpc <= 32u) {
+                publish_il(p, c, u, wpc, V, st, t, kPubLine / 2u);
+            } else {  // words of 32 arrivals, then the line's third word
+                uint64_t* const w = reinterpret_cast<uint64_t*>(p.ws) + (uint64_t)(kPubLine / 2u) * c;
+                const uint32_t h2 = u >> 5;
+                const uint32_t n_h = h2 ? wpc - 32u : 32u;
+                const uint64_t bit = 1ull << (u & 31u);
+                uint64_t prev = 0;
+                if (t == 0) prev = __hip_atomic_fetch_xor(w + h2, (bit << 32) | V, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)prev);
+                const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(prev >> 32));
+                const uint64_t fullh = n_h >= 32u ? 0xFFFFFFFFull : ((1ull << n_h) - 1ull);
+                if ((uint64_t)(hi ^ (uint32_t)bit) == fullh) {
+                    if (t == 0) __hip_atomic_store(w + h2, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const uint32_t Vh = lo ^ V;
+                    const uint64_t hb = 1ull << h2;
+                    uint64_t p2 = 0;
+                    if (t == 0) p2 = __hip_atomic_fetch_xor(w + 2, (hb << 32) | Vh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const uint32_t lo2 = __builtin_amdgcn_readfirstlane((uint32_t)p2);
+                    const uint32_t hi2 = __builtin_amdgcn_readfirstlane((uint32_t)(p2 >> 32));
+                    if ((hi2 ^ (uint32_t)hb) == 3u) {
+                        if (t == 0) __hip_atomic_store(w + 2, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        finalize_uniform(p, c, st, lo2 ^ Vh, t, true);
+                    }
+                }
+            }
+        }
+        if (u == 0) unit_status_pair(p, U, true, t);
+    }
+    // fused shard-index checks under the pair tables (A_4096: the pair kernel's kthread11)
+    for (uint32_t j = g; j < p.n_idx; j += G) verify_index_pair(p, j, t, kix, s_tab, s_red[1], j == g, ipre);
+}
+
+#if ZHIP_TUNING
+KernelFn select_ilh_kernel(int item, bool swap) {  // CRC chains only
+    switch (item) {
+        case 1: return k_decode_ilh<1, false>;
+        case 2: return swap ? k_decode_ilh<2, true> : k_decode_ilh<2, false>;
+        case 4: return swap ? k_decode_ilh<4, true> : k_decode_ilh<4, false>;
+        case 8: return swap ? k_decode_ilh<8, true> : k_decode_ilh<8, false>;
+        default: return nullptr;
+    }
+}
+#endif
+
+// ---------------------------------------------------------------------------
 // k_decode_ilw: small shares (below ~2 workgroups per CU: the N = 4 / 8 shares
 // of the strong-scaled headline).  k_decode_il there runs ONE 4-wave
 // workgroup per CU, each lane's eight Horner steps in series with nothing to

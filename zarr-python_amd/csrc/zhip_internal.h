@@ -163,6 +163,7 @@ struct DecodeParams {
     // available), its A_(16 ilw_nt) tables, lane constants per (unit, lane),
     // the fused index check's lane constants
     uint32_t ilw_nt;
+    const uint32_t* ilh_klane;  // tuning arm 41 (k_decode_ilh, 16 KiB per workgroup): lane constants [2 nseg][kThreads]
     const uint32_t* ilw_tab;
     const uint32_t* ilw_klane;
     const uint32_t* ilw_kidx;
@@ -441,4 +442,5 @@ struct zhip_plan {
     // off_ilw[0] (NT = 1024) / off_ilw[1] (NT = 512) with the tables of
     // A_(16 NT) | klane (nseg x NT) | kidx (256); 0: not built
     uint64_t off_ilw[2];
+    uint64_t off_ilh;  // tuning builds: k_decode_ilh's lane constants [2 nseg][kThreads] (0: none)
 };
