@@ -1272,7 +1272,7 @@ def test_ilh_arm_exact_and_crc(device, case):
 
 
 @pytest.mark.tuning
-@pytest.mark.parametrize("arm", [26, 27, 31, 32])
+@pytest.mark.parametrize("arm", [26, 27, 31, 32, 42])
 @pytest.mark.parametrize("case", range(len(ILW_CASES)))
 def test_ilw_arms_exact_and_crc(device, arm, case):
     """k_decode_ilw (one 32 KiB unit per 1024- / 512-lane workgroup, the
@@ -1294,7 +1294,7 @@ def _ilw_case(device, arm, case):
     if not inner:
         host.pop("c/1/0/0")
     want_kernel = {26: "k_decode_ilw1024", 27: "k_decode_ilw512", 31: "k_decode_ilw1024r", 32: "k_decode_ilw512r",
-                   41: "k_decode_ilh"}[arm]
+                   41: "k_decode_ilh", 42: "k_decode_ilw512m"}[arm]
     set_tuning(6, arm)
     try:
         store = zarr_hip.DeviceStore.from_host(host, device)

@@ -991,8 +991,9 @@ int zhip_decode_mapped(const zhip_plan* plan, const void* src, uint64_t src_size
         int wi = (n_index == 0 || plan->idx_E <= (uint32_t)kWgStride) && units <= kIlwMaxUnits ? 1 : -1;
 #if ZHIP_TUNING
         if (g_tune_arm == 26 || g_tune_arm == 31) wi = 0;
-        else if (g_tune_arm == 27 || g_tune_arm == 32) wi = 1;
-        if (g_tune_arm >= 26 && g_tune_arm <= 32 && !(n_index == 0 || plan->idx_E <= (uint32_t)kWgStride)) wi = -1;
+        else if (g_tune_arm == 27 || g_tune_arm == 32 || g_tune_arm == 42) wi = 1;
+        if (((g_tune_arm >= 26 && g_tune_arm <= 32) || g_tune_arm == 42) &&
+            !(n_index == 0 || plan->idx_E <= (uint32_t)kWgStride)) wi = -1;
 #endif
         p.ilw_nt = (wi >= 0 && plan->off_ilw[wi]) ? (1024u >> wi) : 0u;
         if (p.ilw_nt) {

@@ -2270,8 +2270,10 @@ __device__ __forceinline__ uint32_t lanemul3_w(const uint32_t* s_mul, int t, uin
 }
 
 // LMR: the lane multiply in registers (lanemul_reg, VALU) instead of the LDS
-// column: the run end's LDS reads halve.
-template <int ITEM, bool SWAP, int NT, bool LMR = false>
+// column: the run end's LDS reads halve.  MIX (tuning arm 42): the waves of
+// the second 256 lanes multiply in registers, the first through the LDS
+// column, so the run end's lookups and VALU work overlap.
+template <int ITEM, bool SWAP, int NT, bool LMR = false, bool MIX = false>
 __global__ __launch_bounds__(NT) void k_decode_ilw(const DecodeParams p) {
     constexpr int KW = 2048 / NT;  // blocks per lane
     constexpr int QW = NT / 256;   // 4 KiB sub-steps per row of lanes
@@ -2337,7 +2339,9 @@ __global__ __launch_bounds__(NT) void k_decode_ilw(const DecodeParams p) {
             const int ix = t + i * NT;
             if (ix < kPairTabWords / 4) stt[ix] = tv[i];
         }
-        if constexpr (!LMR) lanemul3_init_w<NT>(s_mul, t, kl);
+        if constexpr (!LMR) {
+            if (!MIX || t < kThreads) lanemul3_init_w<NT>(s_mul, t, kl);
+        }
     }
     __syncthreads();
     stamp(p, g, t, 2);
@@ -2360,8 +2364,12 @@ __global__ __launch_bounds__(NT) void k_decode_ilw(const DecodeParams p) {
         }
         stamp(p, g, t, 3);
         // 4. run end: one chain per workgroup, one publication
-        uint32_t v = ok ? (LMR ? lanemul_reg(kl, fold4(s_tab, acc)) : lanemul3_w<NT>(s_mul, t, fold4(s_tab, acc)))
-                        : 0u;
+        uint32_t v = 0;
+        if (ok) {
+            const uint32_t fo = fold4(s_tab, acc);
+            if (LMR || (MIX && t >= kThreads)) v = lanemul_reg(kl, fo);  // (wave-uniform choice)
+            else v = lanemul3_w<NT>(s_mul, t, fo);
+        }
         v = wave_xor(v);
         if ((t & 63) == 0) s_red[0][t >> 6] = v;
         __syncthreads();
@@ -2387,6 +2395,7 @@ KernelFn select_ilw_kernel(int item, bool swap, int nt, bool lmr) {  // CRC chai
 #if ZHIP_TUNING
 #define ZHIP_ILW(I, W)                                                                         \
     (nt == 1024 ? (lmr ? k_decode_ilw<I, W, 1024, true> : k_decode_ilw<I, W, 1024>)            \
+     : nt == 513 ? k_decode_ilw<I, W, 512, false, true>                                         \
                 : (lmr ? k_decode_ilw<I, W, 512, true> : k_decode_ilw<I, W, 512>))
 #else
     if (nt != 512 || lmr) return nullptr;
