@@ -13,6 +13,7 @@ rocprofv3 --pmc pass over this process attributes every counter to one arm.
             1 nt loads+stores, 2 nt loads, 3 nt stores), 4 replicas at 64 MiB,
             1 at 4 GiB
   TUNE      zhip_set_tuning(2, TUNE) ablation bits for hl / c2 / c4
+  KARM      zhip_set_tuning(6, KARM) kernel arm (loads the tuning build)
   REPS      launches (default 40; 8 for c4 / 4 GiB copies)
 
 Prints one JSON line: arm, median / min event-timed microseconds per launch,
@@ -28,6 +29,9 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "zarr-python_amd"))
+
+if os.environ.get("KARM"):  # kernel arms exist only in the tuning build
+    os.environ.setdefault("ZHIP_LIB", os.path.join(ROOT, "zarr-python_amd", "zarr_hip", "_lib", "libzarrhip_tune.so"))
 
 import bench  # noqa: E402
 import workloads as W  # noqa: E402
@@ -75,6 +79,8 @@ def main():
             alg += n_shards * ((n_inner // n_shards) * 16 + 4)
         del data
         N.lib().zhip_set_tuning(2, tune)
+        if os.environ.get("KARM"):
+            N.check(N.lib().zhip_set_tuning(6, int(os.environ["KARM"])), "zhip_set_tuning")
         launch = lambda i: progs[i % R][0].launch(sh)  # noqa: E731
     elif arm == "copy":
         cb = ctypes.CDLL(os.path.join(ROOT, "scripts", "copybench", "libcopybench.so"))

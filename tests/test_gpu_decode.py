@@ -1282,7 +1282,18 @@ def test_ilw_arms_exact_and_crc(device, arm, case):
     _ilw_case(device, arm, case)
 
 
-def _ilw_case(device, arm, case):
+@pytest.mark.tuning
+@pytest.mark.parametrize("arm", [43, 44])
+@pytest.mark.parametrize("case", [0, 1])
+def test_affine_destination_arms(device, arm, case):
+    """k_decode_il / k_decode_ilw512 with the K destinations from the plan's
+    two-level affine form of the whole-chunk row map (tuning arms 43 / 44, the
+    row-map loads gone) decode whole-chunk selections exactly, fill a missing
+    chunk and report corrupted chunks with the reference's message."""
+    _ilw_case(device, arm, case, whole=True)
+
+
+def _ilw_case(device, arm, case, whole=False):
     import zarr_hip
     from zarr_hip import _native as N
 
@@ -1294,12 +1305,13 @@ def _ilw_case(device, arm, case):
     if not inner:
         host.pop("c/1/0/0")
     want_kernel = {26: "k_decode_ilw1024", 27: "k_decode_ilw512", 31: "k_decode_ilw1024r", 32: "k_decode_ilw512r",
-                   41: "k_decode_ilh", 42: "k_decode_ilw512m"}[arm]
+                   41: "k_decode_ilh", 42: "k_decode_ilw512m", 43: "k_decode_ila", 44: "k_decode_ilw512a"}[arm]
     set_tuning(6, arm)
     try:
         store = zarr_hip.DeviceStore.from_host(host, device)
         arr = zarr_hip.Array.create(store, shape, cshape, dtype, 3, codecs=codecs)
-        for sel in [(Ellipsis,), (slice(5, 60), slice(3, 64), slice(0, 64))]:
+        # (whole: the affine arms take whole-chunk selections only)
+        for sel in [(Ellipsis,)] + ([] if whole else [(slice(5, 60), slice(3, 64), slice(0, 64))]):
             prog, out = arr.prepare_read(sel)
             prog.launch()
             prog.results()

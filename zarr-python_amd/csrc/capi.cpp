@@ -232,6 +232,8 @@ int zhip_device_count(void) {
     return n;
 }
 
+static void plan_affine(zhip_plan* p);
+
 int zhip_plan_create(const zhip_layout* layout, zhip_plan** out) {
     std::call_once(g_once, init_tables);
     if (!layout || !out) return set_err(ZHIP_E_INVALID, "null argument");
@@ -341,6 +343,7 @@ int zhip_plan_create(const zhip_layout* layout, zhip_plan** out) {
             }
         }
     }
+    plan_affine(p);
     *out = p;
     return ZHIP_OK;
 }
@@ -876,25 +879,94 @@ uint64_t zhip_rows_map_len(const zhip_plan* plan, uint32_t n_sels) {
 // The destination arithmetic of the row decode (per step: row R of the
 // chunk's flattened leading dims, its place in dims 0..ndim-2 and in the
 // selection), evaluated once per (selection, unit, step) on the host.
+// Entry of the row map for the step whose first output byte is base_o
+// (>= 0) of the chunk: 0 ok (e set, possibly empty), 1 offset beyond 32 bits.
+static int rows_entry(const zhip_layout& L, uint32_t shift, const zhip_sel& sel, int64_t base_o, zhip_rowblk& e) {
+    const int nd = L.ndim, nd2 = nd - 2;
+    const int64_t rps = (int64_t)kWgStride >> shift;  // rows per step
+    const int64_t sy = L.shape[nd - 2];
+    const int64_t oy = L.out_stride[nd - 2];
+    const int64_t sy0 = sel.start[nd2], cy = sel.count[nd2];
+    e.rel = 0;
+    e.lo = e.hi = 0;
+    const int64_t R = base_o >> shift;
+    int64_t r = R / sy;
+    const int64_t y0 = R - r * sy;
+    int64_t dst = (y0 - sy0) * oy;
+    bool ok = true;
+    for (int d = nd2 - 1; d >= 0; --d) {
+        const int64_t qd = d > 0 ? r / L.shape[d] : 0;
+        const int64_t rel = r - qd * L.shape[d] - sel.start[d];
+        r = qd;
+        ok = ok && rel >= 0 && rel < sel.count[d];
+        dst += rel * L.out_stride[d];
+    }
+    const int64_t lo = std::min(std::max(sy0 - y0, (int64_t)0), rps);
+    const int64_t hi = std::min(std::max(sy0 - y0 + cy, (int64_t)0), rps);
+    if (!ok || hi <= lo) return 0;
+    if (dst < INT32_MIN || dst > INT32_MAX) return 1;
+    e.rel = (int32_t)dst;
+    e.lo = (uint16_t)lo;
+    e.hi = (uint16_t)hi;
+    return 0;
+}
+
+static bool rows_layout(const zhip_plan* plan) {  // zhip_rows_map's admission
+    const zhip_layout& L = plan->layout;
+    const uint32_t rb = plan->row_bytes;
+    const int nd = L.ndim;
+    return !(nd < 2 || rb < 16 || rb > (uint32_t)kWgStride || (rb & (rb - 1)) != 0 ||
+             (uint32_t)L.shape[nd - 2] % ((uint32_t)kWgStride / rb) != 0 ||
+             plan->seg != (uint32_t)kWgStride * kDefaultBlocks);
+}
+
+// The whole-chunk selection's row map in two-level affine form (tuning arms
+// 43 / 44): rel(st) = (st >> sh) B + (st & (2^sh - 1)) C + D with every row
+// of every step written, st = (base_o - lo_frame) / 4 KiB; only chunks that
+// end on a unit boundary (lo_frame 0).  aff_ok = 0 when no shift fits.
+static void plan_affine(zhip_plan* p) {
+    p->aff_ok = 0;
+    if (!rows_layout(p) || p->E != p->nseg * p->seg || p->nseg == 0) return;
+    const zhip_layout& L = p->layout;
+    const uint32_t shift = (uint32_t)__builtin_ctz(p->row_bytes);
+    const uint16_t rps = (uint16_t)((uint32_t)kWgStride >> shift);
+    zhip_sel full{};
+    for (int d = 0; d < L.ndim; ++d) full.count[d] = (int32_t)L.shape[d];
+    const uint32_t n_st = p->nseg * (uint32_t)kDefaultBlocks;
+    std::vector<int32_t> rel(n_st);
+    for (uint32_t st = 0; st < n_st; ++st) {
+        zhip_rowblk e;
+        if (rows_entry(L, shift, full, (int64_t)kWgStride * st, e) || e.lo != 0 || e.hi != rps) return;
+        rel[st] = e.rel;
+    }
+    for (uint32_t sh = 0; sh <= 12; ++sh) {
+        const uint32_t mask = (1u << sh) - 1u;
+        const int64_t D = rel[0];
+        const int64_t C = (sh > 0 && n_st > 1) ? (int64_t)rel[1] - D : 0;
+        const int64_t B = ((1u << sh) < n_st) ? (int64_t)rel[1u << sh] - D : 0;
+        bool fit = true;
+        for (uint32_t st = 0; st < n_st && fit; ++st)
+            fit = (int64_t)(st >> sh) * B + (int64_t)(st & mask) * C + D == rel[st];
+        if (fit && B >= INT32_MIN && B <= INT32_MAX && C >= INT32_MIN && C <= INT32_MAX) {
+            p->aff_ok = 1;
+            p->aff_sh = sh;
+            p->aff_B = (int32_t)B;
+            p->aff_C = (int32_t)C;
+            p->aff_D = (int32_t)D;
+            return;
+        }
+    }
+}
+
 int zhip_rows_map(const zhip_plan* plan, const zhip_sel* h_sels, uint32_t n_sels, zhip_rowblk* h_map,
                   uint64_t map_len) {
     if (!plan) return set_err(ZHIP_E_INVALID, "null plan");
     if (n_sels && (!h_sels || !h_map)) return set_err(ZHIP_E_INVALID, "null host pointer");
     if (map_len < zhip_rows_map_len(plan, n_sels)) return set_err(ZHIP_E_INVALID, "row map too short");
+    if (!rows_layout(plan)) return set_err(ZHIP_E_UNSUPPORTED, "not a whole-row layout with 32 KiB units");
     const zhip_layout& L = plan->layout;
-    const uint32_t rb = plan->row_bytes;
-    const int nd = L.ndim;
-    if (nd < 2 || rb < 16 || rb > (uint32_t)kWgStride || (rb & (rb - 1)) != 0 ||
-        (uint32_t)L.shape[nd - 2] % ((uint32_t)kWgStride / rb) != 0 || plan->seg != (uint32_t)kWgStride * kDefaultBlocks)
-        return set_err(ZHIP_E_UNSUPPORTED, "not a whole-row layout with 32 KiB units");
-    const uint32_t shift = (uint32_t)__builtin_ctz(rb);
-    const int64_t rps = (int64_t)kWgStride >> shift;  // rows per step
-    const int64_t sy = L.shape[nd - 2];
-    const int64_t oy = L.out_stride[nd - 2];
-    const int nd2 = nd - 2;
+    const uint32_t shift = (uint32_t)__builtin_ctz(plan->row_bytes);
     for (uint32_t s = 0; s < n_sels; ++s) {
-        const zhip_sel& sel = h_sels[s];
-        const int64_t sy0 = sel.start[nd2], cy = sel.count[nd2];
         for (uint32_t u = 0; u < plan->nseg; ++u) {
             const int64_t seg_lo = (int64_t)(int32_t)plan->E - (int64_t)(u + 1) * plan->seg;
             for (int k = 0; k < kDefaultBlocks; ++k) {
@@ -903,26 +975,8 @@ int zhip_rows_map(const zhip_plan* plan, const zhip_sel* h_sels, uint32_t n_sels
                 e.lo = e.hi = 0;
                 const int64_t base_o = seg_lo + (int64_t)kWgStride * k;
                 if (base_o < 0) continue;  // before the chunk start: nothing written
-                const int64_t R = base_o >> shift;
-                int64_t r = R / sy;
-                const int64_t y0 = R - r * sy;
-                int64_t dst = (y0 - sy0) * oy;
-                bool ok = true;
-                for (int d = nd2 - 1; d >= 0; --d) {
-                    const int64_t qd = d > 0 ? r / L.shape[d] : 0;
-                    const int64_t rel = r - qd * L.shape[d] - sel.start[d];
-                    r = qd;
-                    ok = ok && rel >= 0 && rel < sel.count[d];
-                    dst += rel * L.out_stride[d];
-                }
-                const int64_t lo = std::min(std::max(sy0 - y0, (int64_t)0), rps);
-                const int64_t hi = std::min(std::max(sy0 - y0 + cy, (int64_t)0), rps);
-                if (!ok || hi <= lo) continue;
-                if (dst < INT32_MIN || dst > INT32_MAX)
+                if (rows_entry(L, shift, h_sels[s], base_o, e))
                     return set_err(ZHIP_E_UNSUPPORTED, "row offset does not fit 32 bits");
-                e.rel = (int32_t)dst;
-                e.lo = (uint16_t)lo;
-                e.hi = (uint16_t)hi;
             }
         }
     }
@@ -1003,6 +1057,14 @@ int zhip_decode_mapped(const zhip_plan* plan, const void* src, uint64_t src_size
         }
     }
     if (plan->off_ilh) p.ilh_klane = plan->d_tables + plan->off_ilh;
+    p.aff_ok = plan->aff_ok;
+    if (plan->aff_ok) {
+        p.aff_sh = plan->aff_sh;
+        p.aff_mask = (1u << plan->aff_sh) - 1u;
+        p.aff_B = plan->aff_B;
+        p.aff_C = plan->aff_C;
+        p.aff_D = plan->aff_D;
+    }
     for (int op = 0; op < 4; ++op) p.hx[op] = plan->hx[op];
     for (int i = 0; i < 32; ++i) p.kq[i] = plan->kq[i];
     p.n_chunks = n_chunks;

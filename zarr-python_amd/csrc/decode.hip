@@ -628,15 +628,18 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
             return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
         }
         if (crc && p.ilw_nt && (g_tune_arm == 26 || g_tune_arm == 27 || g_tune_arm == 31 || g_tune_arm == 32 ||
-                                g_tune_arm == 42)) {
+                                g_tune_arm == 42 || (g_tune_arm == 44 && p.aff_ok && p.ilw_nt == 512u))) {
             // k_decode_ilw: one 32 KiB unit per workgroup of 1024 / 512 lanes
-            // (31 / 32: the lane multiply in registers; 42: half in registers)
-            KernelFn wfn = g_tune_arm == 42 ? select_ilw_kernel(p.g.itemsize, swap, 513, false)
-                                            : select_ilw_kernel(p.g.itemsize, swap, (int)p.ilw_nt, g_tune_arm >= 31);
+            // (31 / 32: the lane multiply in registers; 42: half in registers;
+            // 44: affine destinations, whole-chunk selections only)
+            KernelFn wfn = g_tune_arm == 42   ? select_ilw_kernel(p.g.itemsize, swap, 513, false)
+                           : g_tune_arm == 44 ? select_ilw_kernel(p.g.itemsize, swap, 514, false)
+                                              : select_ilw_kernel(p.g.itemsize, swap, (int)p.ilw_nt, g_tune_arm >= 31);
             if (!wfn) return ZHIP_E_UNSUPPORTED;
             const uint32_t wgrid = p.n_units > p.n_idx ? p.n_units : p.n_idx;
             if (wgrid == 0) return ZHIP_OK;
-            g_last_kernel = g_tune_arm == 42 ? "k_decode_ilw512m"
+            g_last_kernel = g_tune_arm == 42   ? "k_decode_ilw512m"
+                            : g_tune_arm == 44 ? "k_decode_ilw512a"
                             : p.ilw_nt == 1024u ? (g_tune_arm >= 31 ? "k_decode_ilw1024r" : "k_decode_ilw1024")
                                                 : (g_tune_arm >= 31 ? "k_decode_ilw512r" : "k_decode_ilw512");
             hipLaunchKernelGGL(wfn, dim3(wgrid), dim3(p.ilw_nt), 0, stream, p);
@@ -715,10 +718,13 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
 #else
             KernelFn ifn = select_il_kernel(crc, p.g.itemsize, swap);
 #endif
+#if ZHIP_TUNING
+            if (g_tune_arm == 43 && !p.aff_ok) ifn = select_il_kernel(crc, p.g.itemsize, swap);
+#endif
             if (!ifn) return ZHIP_E_UNSUPPORTED;
             const uint32_t igrid = p.n_units > p.n_idx ? p.n_units : p.n_idx;
             if (igrid == 0) return ZHIP_OK;
-            g_last_kernel = "k_decode_il";
+            g_last_kernel = (ZHIP_TUNING && g_tune_arm == 43 && p.aff_ok) ? "k_decode_ila" : "k_decode_il";
             hipLaunchKernelGGL(ifn, dim3(igrid), dim3(kThreads), 0, stream, p);
             return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
         }

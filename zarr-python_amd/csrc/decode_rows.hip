@@ -1279,6 +1279,16 @@ __device__ __forceinline__ void publish_il(const DecodeParams& p, uint32_t c, ui
     }
 }
 
+// the whole-chunk row map's entry for step st from its two-level affine form
+// (tuning arms 43 / 44; zhip_plan aff_*): every row of the step, one offset
+__device__ __forceinline__ zhip_rowblk aff_rowblk(const DecodeParams& p, uint32_t st) {
+    zhip_rowblk e;
+    e.rel = (int32_t)(st >> p.aff_sh) * p.aff_B + (int32_t)(st & p.aff_mask) * p.aff_C + p.aff_D;
+    e.lo = 0;
+    e.hi = (uint16_t)((uint32_t)kWgStride >> p.row_shift);
+    return e;
+}
+
 // LEAN (tuning arm kTuneIlLean): the PairHot batch, then tables, constants
 // and -- at the addresses the default shard packing predicts (zhip_predict) --
 // the data loads, all before the header chain (chunk record -> index entry)
@@ -1306,8 +1316,12 @@ __device__ __forceinline__ void publish_il(const DecodeParams& p, uint32_t c, ui
 //   Graph-timed on one box (profiles/r04/c/arms_*.jsonl), headline / N = 8
 //   share: 3: 26.01 / 9.45 us, 0: 26.22 / 9.62, 2: 26.38 / 10.14, no
 //   publication at all 25.48 / 9.17.
+// AFF (tuning arm 43): the K destinations from the plan's two-level affine
+//   form of the whole-chunk row map (zhip_plan aff_*: rel = (st >> sh) B +
+//   (st & (2^sh - 1)) C + D, every row of the step) in scalar registers
+//   instead of K scalar loads of the map; whole-chunk selections only.
 template <bool CRC, int ITEM, bool SWAP, bool LEAN = false, bool CF = false, int LM = 0, bool TUNE = false,
-          int PUB = 3>
+          int PUB = 3, bool AFF = false>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(LM == 2 ? 6 : 4, LM == 2 ? 6 : 4)))
 void k_decode_il(const DecodeParams p) {
     constexpr int K = kDefaultBlocks;
@@ -1447,8 +1461,12 @@ void k_decode_il(const DecodeParams p) {
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         const uint32_t st = st0 + S * (uint32_t)k;
-        const uint32_t sidx = p.nseg - 1u - st / (uint32_t)K;
-        m[k] = load_uniform<zhip_rowblk>(p.rowmap + ((size_t)U.sel * p.nseg + sidx) * K + (st % (uint32_t)K));
+        if constexpr (AFF) {
+            m[k] = aff_rowblk(p, st);
+        } else {
+            const uint32_t sidx = p.nseg - 1u - st / (uint32_t)K;
+            m[k] = load_uniform<zhip_rowblk>(p.rowmap + ((size_t)U.sel * p.nseg + sidx) * K + (st % (uint32_t)K));
+        }
     }
     uint32_t stored = 0;
     if (CRC && ok) stored = load_trailer_uniform(U.cp, p.g.nbytes);
@@ -1531,6 +1549,7 @@ KernelFn select_il_kernel_arm(bool crc, int item, bool swap, int arm) {  // ZHIP
     switch (arm) {
         case 1: return k_decode_il<true, 4, false, false, false, 0, false, 0>;  // round 3: words 16 B apart
         case 2: return k_decode_il<true, 4, false, false, false, 0, false, 2>;  // deferred verdicts
+        case 43: return k_decode_il<true, 4, false, false, false, 0, false, 3, true>;  // affine destinations
         default: return k_decode_il<true, 4, false>;  // arms of other kernels: production
     }
 }
@@ -2273,7 +2292,7 @@ __device__ __forceinline__ uint32_t lanemul3_w(const uint32_t* s_mul, int t, uin
 // column: the run end's LDS reads halve.  MIX (tuning arm 42): the waves of
 // the second 256 lanes multiply in registers, the first through the LDS
 // column, so the run end's lookups and VALU work overlap.
-template <int ITEM, bool SWAP, int NT, bool LMR = false, bool MIX = false>
+template <int ITEM, bool SWAP, int NT, bool LMR = false, bool MIX = false, bool AFF = false>
 __global__ __launch_bounds__(NT) void k_decode_ilw(const DecodeParams p) {
     constexpr int KW = 2048 / NT;  // blocks per lane
     constexpr int QW = NT / 256;   // 4 KiB sub-steps per row of lanes
@@ -2326,9 +2345,14 @@ __global__ __launch_bounds__(NT) void k_decode_ilw(const DecodeParams p) {
     zhip_rowblk m[KW];
     const uint32_t sidx = p.nseg - 1u - r;
 #pragma unroll
-    for (int k = 0; k < KW; ++k)
-        m[k] = load_uniform<zhip_rowblk>(p.rowmap + ((size_t)U.sel * p.nseg + sidx) * kDefaultBlocks + q +
-                                         (uint32_t)(QW * k));
+    for (int k = 0; k < KW; ++k) {
+        if constexpr (AFF) {  // tuning arm 44 (k_decode_il's AFF)
+            m[k] = aff_rowblk(p, 8u * r + q + (uint32_t)(QW * k));
+        } else {
+            m[k] = load_uniform<zhip_rowblk>(p.rowmap + ((size_t)U.sel * p.nseg + sidx) * kDefaultBlocks + q +
+                                             (uint32_t)(QW * k));
+        }
+    }
     uint32_t stored = 0;
     if (ok) stored = load_trailer_uniform(U.cp, p.g.nbytes);
     // 2. tables into LDS, the lane-multiply column
@@ -2396,6 +2420,7 @@ KernelFn select_ilw_kernel(int item, bool swap, int nt, bool lmr) {  // CRC chai
 #define ZHIP_ILW(I, W)                                                                         \
     (nt == 1024 ? (lmr ? k_decode_ilw<I, W, 1024, true> : k_decode_ilw<I, W, 1024>)            \
      : nt == 513 ? k_decode_ilw<I, W, 512, false, true>                                         \
+     : nt == 514 ? k_decode_ilw<I, W, 512, false, false, true>                                  \
                 : (lmr ? k_decode_ilw<I, W, 512, true> : k_decode_ilw<I, W, 512>))
 #else
     if (nt != 512 || lmr) return nullptr;

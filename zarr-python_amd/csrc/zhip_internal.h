@@ -167,6 +167,10 @@ struct DecodeParams {
     const uint32_t* ilw_tab;
     const uint32_t* ilw_klane;
     const uint32_t* ilw_kidx;
+    // tuning arms 43 / 44: the whole-chunk row map as rel(st) = (st >> aff_sh)
+    // aff_B + (st & aff_mask) aff_C + aff_D (zhip_plan aff_*)
+    uint32_t aff_ok, aff_sh, aff_mask;
+    int32_t aff_B, aff_C, aff_D;
     // load-address prediction (zhip_predict; k_decode_pair): payload of chunk c
     // predicted at src + pred_base + (c / pred_per) * pred_outer + (c % pred_per) * pred_inner
     uint32_t pred, pred_per;
@@ -409,6 +413,10 @@ struct zhip_plan {
     // pair tables | tile map (T TileEnt) | lane constants [T/2][kThreads]
     uint32_t tile2;
     uint64_t tile2_off;
+    // the whole-chunk row map of a whole-row layout in two-level affine form
+    // (plan_affine; tuning arms 43 / 44): aff_ok, shift, B, C, D
+    uint32_t aff_ok, aff_sh;
+    int32_t aff_B, aff_C, aff_D;
     // k_decode_tilegw (grouped tile layouts with a CRC): the same for groups
     uint32_t tilegw;
     uint64_t tilegw_off;
