@@ -1282,15 +1282,49 @@ def test_ilw_arms_exact_and_crc(device, arm, case):
     _ilw_case(device, arm, case)
 
 
+@pytest.mark.parametrize("shape,cshape,inner,kname", [
+    ((256, 256, 128), (64, 64, 64), None, "k_decode_il"),                     # 1 024 units
+    ((128, 128, 64), (128, 128, 64), (64, 64, 64), "k_decode_ilw512"),        # 128 units, sharded
+])
+def test_whole_chunk_reads_compute_destinations(device, shape, cshape, inner, kname):
+    """Whole-chunk reads launch with ZHIP_DF_WHOLE: k_decode_il /
+    k_decode_ilw512 take each step's destination from the plan's affine form
+    of the whole-chunk row map, not from the map -- exact with the map zeroed
+    on the device (a map-driven launch would write nothing); a partial
+    window keeps the map."""
+    import zarr_hip
+    from zarr_hip import _native as N
+
+    codecs = [SHARD(inner, [LE, CRC])] if inner else [LE, CRC]
+    meta = O.ArrayMeta(shape, cshape, np.dtype("float32"), 1.5, codecs=codecs)
+    host = {}
+    O.write(host, meta, (Ellipsis,), _data(shape, "float32"))
+    if not inner:
+        host.pop("c/1/0/1")  # a missing chunk: filled through the same destinations
+    store = zarr_hip.DeviceStore.from_host(host, device)
+    arr = zarr_hip.Array.create(store, shape, cshape, "float32", 1.5, codecs=codecs)
+    prog, out = arr.prepare_read((Ellipsis,))
+    assert prog.data.flags & N.DF_WHOLE
+    prog.data.d_rowmap.zero_()
+    prog.launch()
+    prog.results()
+    assert N.lib().zhip_last_kernel().decode() == kname
+    assert out.cpu().numpy().tobytes() == O.read(host, meta).tobytes()
+    win = (slice(5, 60), slice(3, 64), slice(0, 64))
+    prog, out = arr.prepare_read(win)
+    assert not prog.data.flags & N.DF_WHOLE
+    prog.launch()
+    prog.results()
+    assert out.cpu().numpy().tobytes() == np.ascontiguousarray(O.read(host, meta, win)).tobytes()
+
+
 @pytest.mark.tuning
-@pytest.mark.parametrize("arm", [43, 44])
 @pytest.mark.parametrize("case", [0, 1])
-def test_affine_destination_arms(device, arm, case):
-    """k_decode_il / k_decode_ilw512 with the K destinations from the plan's
-    two-level affine form of the whole-chunk row map (tuning arms 43 / 44, the
-    row-map loads gone) decode whole-chunk selections exactly, fill a missing
-    chunk and report corrupted chunks with the reference's message."""
-    _ilw_case(device, arm, case, whole=True)
+def test_row_map_arm_exact_and_crc(device, case):
+    """Tuning arm 45 keeps the row-map loads for whole-chunk launches (the A/B
+    reference of ZHIP_DF_WHOLE): exact, missing chunks filled, corrupted
+    chunks and indexes reported with the reference's message."""
+    _ilw_case(device, 45, case, whole=True)
 
 
 def _ilw_case(device, arm, case, whole=False):
@@ -1305,7 +1339,7 @@ def _ilw_case(device, arm, case, whole=False):
     if not inner:
         host.pop("c/1/0/0")
     want_kernel = {26: "k_decode_ilw1024", 27: "k_decode_ilw512", 31: "k_decode_ilw1024r", 32: "k_decode_ilw512r",
-                   41: "k_decode_ilh", 42: "k_decode_ilw512m", 43: "k_decode_ila", 44: "k_decode_ilw512a"}[arm]
+                   41: "k_decode_ilh", 42: "k_decode_ilw512m", 45: "k_decode_il"}[arm]
     set_tuning(6, arm)
     try:
         store = zarr_hip.DeviceStore.from_host(host, device)

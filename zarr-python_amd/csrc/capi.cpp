@@ -920,8 +920,8 @@ static bool rows_layout(const zhip_plan* plan) {  // zhip_rows_map's admission
              plan->seg != (uint32_t)kWgStride * kDefaultBlocks);
 }
 
-// The whole-chunk selection's row map in two-level affine form (tuning arms
-// 43 / 44): rel(st) = (st >> sh) B + (st & (2^sh - 1)) C + D with every row
+// The whole-chunk selection's row map in two-level affine form (ZHIP_DF_WHOLE
+// launches): rel(st) = (st >> sh) B + (st & (2^sh - 1)) C + D with every row
 // of every step written, st = (base_o - lo_frame) / 4 KiB; only chunks that
 // end on a unit boundary (lo_frame 0).  aff_ok = 0 when no shift fits.
 static void plan_affine(zhip_plan* p) {
@@ -956,6 +956,17 @@ static void plan_affine(zhip_plan* p) {
             return;
         }
     }
+}
+
+extern "C++" {
+template <class P>
+static void set_affine(P& p, const zhip_plan* plan) {  // DecodeParams / EncodeParams
+    p.aff_sh = plan->aff_sh;
+    p.aff_mask = (1u << plan->aff_sh) - 1u;
+    p.aff_B = plan->aff_B;
+    p.aff_C = plan->aff_C;
+    p.aff_D = plan->aff_D;
+}
 }
 
 int zhip_rows_map(const zhip_plan* plan, const zhip_sel* h_sels, uint32_t n_sels, zhip_rowblk* h_map,
@@ -1057,14 +1068,12 @@ int zhip_decode_mapped(const zhip_plan* plan, const void* src, uint64_t src_size
         }
     }
     if (plan->off_ilh) p.ilh_klane = plan->d_tables + plan->off_ilh;
-    p.aff_ok = plan->aff_ok;
-    if (plan->aff_ok) {
-        p.aff_sh = plan->aff_sh;
-        p.aff_mask = (1u << plan->aff_sh) - 1u;
-        p.aff_B = plan->aff_B;
-        p.aff_C = plan->aff_C;
-        p.aff_D = plan->aff_D;
-    }
+    // whole-chunk selections (ZHIP_DF_WHOLE, with a row map) of a plan whose
+    // whole-chunk row map is affine: the row kernels compute destinations
+    // (tuning arm 45 keeps the map loads: the A/B reference)
+    p.aff_ok = (decode_flags & ZHIP_DF_WHOLE) && (decode_flags & ZHIP_DF_ROWS) && d_rowmap && plan->aff_ok &&
+               !(ZHIP_TUNING && g_tune_arm == 45);
+    if (p.aff_ok) set_affine(p, plan);
     for (int op = 0; op < 4; ++op) p.hx[op] = plan->hx[op];
     for (int i = 0; i < 32; ++i) p.kq[i] = plan->kq[i];
     p.n_chunks = n_chunks;
@@ -1312,6 +1321,10 @@ int zhip_encode_mapped(const zhip_plan* plan, const void* arr, void* dst, const 
             p.il_S = plan->il_S;
             p.il_tab = plan->d_tables + plan->off_il;
             p.il_klane = p.il_tab + kPairTabWords;
+            // whole-chunk selections: destinations computed (ZHIP_DF_WHOLE, as the decode)
+            p.aff_ok = (encode_flags & ZHIP_DF_WHOLE) && plan->aff_ok &&
+                       !(ZHIP_TUNING && g_tune_arm == 45);
+            if (p.aff_ok) set_affine(p, plan);
         }
     }
     int rc = launch_encode(p, static_cast<hipStream_t>(stream), plan->max_grid);

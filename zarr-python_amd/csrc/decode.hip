@@ -493,8 +493,8 @@ static KernelFn select_tile_kernel(bool crc, int item, bool swap) {
 KernelFn select_rows_kernel(bool crc, int item, bool swap, int k);  // decode_rows.hip
 KernelFn select_pair_kernel(bool crc, int item, bool swap, int nu);  // decode_rows.hip
 KernelFn select_duo_kernel(bool crc, int item, bool swap);           // decode_rows.hip
-KernelFn select_il_kernel(bool crc, int item, bool swap);            // decode_rows.hip
-KernelFn select_ilw_kernel(int item, bool swap, int nt, bool lmr);   // decode_rows.hip
+KernelFn select_il_kernel(bool crc, int item, bool swap, bool aff);  // decode_rows.hip
+KernelFn select_ilw_kernel(int item, bool swap, int nt, bool lmr, bool aff);  // decode_rows.hip
 #if ZHIP_TUNING
 KernelFn select_il_kernel_lean(bool crc, int item, bool swap);       // decode_rows.hip
 KernelFn select_il_kernel_tuned(bool crc, int item, bool swap);      // decode_rows.hip
@@ -628,18 +628,16 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
             return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
         }
         if (crc && p.ilw_nt && (g_tune_arm == 26 || g_tune_arm == 27 || g_tune_arm == 31 || g_tune_arm == 32 ||
-                                g_tune_arm == 42 || (g_tune_arm == 44 && p.aff_ok && p.ilw_nt == 512u))) {
+                                g_tune_arm == 42)) {
             // k_decode_ilw: one 32 KiB unit per workgroup of 1024 / 512 lanes
-            // (31 / 32: the lane multiply in registers; 42: half in registers;
-            // 44: affine destinations, whole-chunk selections only)
-            KernelFn wfn = g_tune_arm == 42   ? select_ilw_kernel(p.g.itemsize, swap, 513, false)
-                           : g_tune_arm == 44 ? select_ilw_kernel(p.g.itemsize, swap, 514, false)
-                                              : select_ilw_kernel(p.g.itemsize, swap, (int)p.ilw_nt, g_tune_arm >= 31);
+            // (31 / 32: the lane multiply in registers; 42: half in registers)
+            KernelFn wfn = g_tune_arm == 42
+                               ? select_ilw_kernel(p.g.itemsize, swap, 513, false, false)
+                               : select_ilw_kernel(p.g.itemsize, swap, (int)p.ilw_nt, g_tune_arm >= 31, p.aff_ok != 0);
             if (!wfn) return ZHIP_E_UNSUPPORTED;
             const uint32_t wgrid = p.n_units > p.n_idx ? p.n_units : p.n_idx;
             if (wgrid == 0) return ZHIP_OK;
-            g_last_kernel = g_tune_arm == 42   ? "k_decode_ilw512m"
-                            : g_tune_arm == 44 ? "k_decode_ilw512a"
+            g_last_kernel = g_tune_arm == 42 ? "k_decode_ilw512m"
                             : p.ilw_nt == 1024u ? (g_tune_arm >= 31 ? "k_decode_ilw1024r" : "k_decode_ilw1024")
                                                 : (g_tune_arm >= 31 ? "k_decode_ilw512r" : "k_decode_ilw512");
             hipLaunchKernelGGL(wfn, dim3(wgrid), dim3(p.ilw_nt), 0, stream, p);
@@ -697,7 +695,7 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
         // N = 8 share, 10.3 vs 11.0 at N = 4; 14.6 vs 16.5 for k_decode_il at
         // N = 2 (profiles/r05/f/).  (Tuning build: any arm keeps k_decode_il.)
         if (il && p.ilw_nt == 512u && p.n_units <= kIlwMaxUnits && g_tune_arm == 0 && (tune & ~kTuneStamp) == 0) {
-            KernelFn wfn = select_ilw_kernel(p.g.itemsize, swap, 512, false);
+            KernelFn wfn = select_ilw_kernel(p.g.itemsize, swap, 512, false, p.aff_ok != 0);
             if (!wfn) return ZHIP_E_UNSUPPORTED;
             const uint32_t wgrid = p.n_units > p.n_idx ? p.n_units : p.n_idx;
             if (wgrid == 0) return ZHIP_OK;
@@ -714,17 +712,14 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
                                ? select_il_kernel_regmul(crc, p.g.itemsize, swap, (tune & kTuneIlOcc6) != 0)
                                : (tune & (kTuneNoTables | kTuneNoRunEnd | kTuneNoPub | kTuneStamp))
                                    ? select_il_kernel_tuned(crc, p.g.itemsize, swap)
-                                   : select_il_kernel(crc, p.g.itemsize, swap);
+                                   : select_il_kernel(crc, p.g.itemsize, swap, p.aff_ok != 0);
 #else
-            KernelFn ifn = select_il_kernel(crc, p.g.itemsize, swap);
-#endif
-#if ZHIP_TUNING
-            if (g_tune_arm == 43 && !p.aff_ok) ifn = select_il_kernel(crc, p.g.itemsize, swap);
+            KernelFn ifn = select_il_kernel(crc, p.g.itemsize, swap, p.aff_ok != 0);
 #endif
             if (!ifn) return ZHIP_E_UNSUPPORTED;
             const uint32_t igrid = p.n_units > p.n_idx ? p.n_units : p.n_idx;
             if (igrid == 0) return ZHIP_OK;
-            g_last_kernel = (ZHIP_TUNING && g_tune_arm == 43 && p.aff_ok) ? "k_decode_ila" : "k_decode_il";
+            g_last_kernel = "k_decode_il";
             hipLaunchKernelGGL(ifn, dim3(igrid), dim3(kThreads), 0, stream, p);
             return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
         }

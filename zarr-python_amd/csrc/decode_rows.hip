@@ -1279,16 +1279,6 @@ __device__ __forceinline__ void publish_il(const DecodeParams& p, uint32_t c, ui
     }
 }
 
-// the whole-chunk row map's entry for step st from its two-level affine form
-// (tuning arms 43 / 44; zhip_plan aff_*): every row of the step, one offset
-__device__ __forceinline__ zhip_rowblk aff_rowblk(const DecodeParams& p, uint32_t st) {
-    zhip_rowblk e;
-    e.rel = (int32_t)(st >> p.aff_sh) * p.aff_B + (int32_t)(st & p.aff_mask) * p.aff_C + p.aff_D;
-    e.lo = 0;
-    e.hi = (uint16_t)((uint32_t)kWgStride >> p.row_shift);
-    return e;
-}
-
 // LEAN (tuning arm kTuneIlLean): the PairHot batch, then tables, constants
 // and -- at the addresses the default shard packing predicts (zhip_predict) --
 // the data loads, all before the header chain (chunk record -> index entry)
@@ -1316,10 +1306,11 @@ __device__ __forceinline__ zhip_rowblk aff_rowblk(const DecodeParams& p, uint32_
 //   Graph-timed on one box (profiles/r04/c/arms_*.jsonl), headline / N = 8
 //   share: 3: 26.01 / 9.45 us, 0: 26.22 / 9.62, 2: 26.38 / 10.14, no
 //   publication at all 25.48 / 9.17.
-// AFF (tuning arm 43): the K destinations from the plan's two-level affine
-//   form of the whole-chunk row map (zhip_plan aff_*: rel = (st >> sh) B +
-//   (st & (2^sh - 1)) C + D, every row of the step) in scalar registers
-//   instead of K scalar loads of the map; whole-chunk selections only.
+// AFF (production for ZHIP_DF_WHOLE launches of plans with aff_ok): the K
+//   destinations from the plan's two-level affine form of the whole-chunk row
+//   map (aff_rowblk) in scalar registers instead of K scalar loads of the map:
+//   graph-timed 26.06 vs 26.38 us on the headline, SALU instructions 3.61 M ->
+//   2.80 M per launch (profiles/r05/w/).
 template <bool CRC, int ITEM, bool SWAP, bool LEAN = false, bool CF = false, int LM = 0, bool TUNE = false,
           int PUB = 3, bool AFF = false>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(LM == 2 ? 6 : 4, LM == 2 ? 6 : 4)))
@@ -1549,7 +1540,6 @@ KernelFn select_il_kernel_arm(bool crc, int item, bool swap, int arm) {  // ZHIP
     switch (arm) {
         case 1: return k_decode_il<true, 4, false, false, false, 0, false, 0>;  // round 3: words 16 B apart
         case 2: return k_decode_il<true, 4, false, false, false, 0, false, 2>;  // deferred verdicts
-        case 43: return k_decode_il<true, 4, false, false, false, 0, false, 3, true>;  // affine destinations
         default: return k_decode_il<true, 4, false>;  // arms of other kernels: production
     }
 }
@@ -1597,17 +1587,19 @@ KernelFn select_il_kernel_regmul(bool crc, int item, bool swap, bool occ6) {  //
 
 #endif
 
-KernelFn select_il_kernel(bool crc, int item, bool swap) {
+KernelFn select_il_kernel(bool crc, int item, bool swap, bool aff) {  // aff: ZHIP_DF_WHOLE (CRC chains)
+#define ZHIP_IL(I, W) (aff ? k_decode_il<true, I, W, false, false, 0, false, 3, true> : k_decode_il<true, I, W>)
     switch (item) {
-        case 1: return crc ? k_decode_il<true, 1, false> : k_decode_il<false, 1, false>;
-        case 2: return crc ? (swap ? k_decode_il<true, 2, true> : k_decode_il<true, 2, false>)
+        case 1: return crc ? ZHIP_IL(1, false) : k_decode_il<false, 1, false>;
+        case 2: return crc ? (swap ? ZHIP_IL(2, true) : ZHIP_IL(2, false))
                            : (swap ? k_decode_il<false, 2, true> : k_decode_il<false, 2, false>);
-        case 4: return crc ? (swap ? k_decode_il<true, 4, true> : k_decode_il<true, 4, false>)
+        case 4: return crc ? (swap ? ZHIP_IL(4, true) : ZHIP_IL(4, false))
                            : (swap ? k_decode_il<false, 4, true> : k_decode_il<false, 4, false>);
-        case 8: return crc ? (swap ? k_decode_il<true, 8, true> : k_decode_il<true, 8, false>)
+        case 8: return crc ? (swap ? ZHIP_IL(8, true) : ZHIP_IL(8, false))
                            : (swap ? k_decode_il<false, 8, true> : k_decode_il<false, 8, false>);
         default: return nullptr;
     }
+#undef ZHIP_IL
 }
 
 // ---------------------------------------------------------------------------
@@ -2346,7 +2338,7 @@ __global__ __launch_bounds__(NT) void k_decode_ilw(const DecodeParams p) {
     const uint32_t sidx = p.nseg - 1u - r;
 #pragma unroll
     for (int k = 0; k < KW; ++k) {
-        if constexpr (AFF) {  // tuning arm 44 (k_decode_il's AFF)
+        if constexpr (AFF) {  // (k_decode_il's AFF)
             m[k] = aff_rowblk(p, 8u * r + q + (uint32_t)(QW * k));
         } else {
             m[k] = load_uniform<zhip_rowblk>(p.rowmap + ((size_t)U.sel * p.nseg + sidx) * kDefaultBlocks + q +
@@ -2413,18 +2405,20 @@ __global__ __launch_bounds__(NT) void k_decode_ilw(const DecodeParams p) {
         verify_index_pair(p, j, t, kix, s_tab, s_red[1], j == g, ipre, t < kThreads);
 }
 
-// production: 512 lanes, the LDS lane multiply (small grids, launch_decode);
-// the tuning build adds 1024 lanes and the register multiply
-KernelFn select_ilw_kernel(int item, bool swap, int nt, bool lmr) {  // CRC chains only
+// production: 512 lanes, the LDS lane multiply (small grids, launch_decode),
+// the AFF form for ZHIP_DF_WHOLE launches; the tuning build adds 1024 lanes
+// and the register multiply (513: half the waves, arm 42)
+KernelFn select_ilw_kernel(int item, bool swap, int nt, bool lmr, bool aff) {  // CRC chains only
 #if ZHIP_TUNING
 #define ZHIP_ILW(I, W)                                                                         \
     (nt == 1024 ? (lmr ? k_decode_ilw<I, W, 1024, true> : k_decode_ilw<I, W, 1024>)            \
      : nt == 513 ? k_decode_ilw<I, W, 512, false, true>                                         \
-     : nt == 514 ? k_decode_ilw<I, W, 512, false, false, true>                                  \
-                : (lmr ? k_decode_ilw<I, W, 512, true> : k_decode_ilw<I, W, 512>))
+     : lmr       ? k_decode_ilw<I, W, 512, true>                                                \
+     : aff       ? k_decode_ilw<I, W, 512, false, false, true>                                  \
+                 : k_decode_ilw<I, W, 512>)
 #else
     if (nt != 512 || lmr) return nullptr;
-#define ZHIP_ILW(I, W) k_decode_ilw<I, W, 512>
+#define ZHIP_ILW(I, W) (aff ? k_decode_ilw<I, W, 512, false, false, true> : k_decode_ilw<I, W, 512>)
 #endif
     switch (item) {
         case 1: return ZHIP_ILW(1, false);

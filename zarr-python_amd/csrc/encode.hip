@@ -497,7 +497,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
 // the line's third word the same way (bits 32 / 48 + half), and the last of
 // those writes trailer, status and the non-empty flag.  Chunks of at most 16
 // units have one half and no second level.
-template <int ITEM, bool SWAP>
+// AFF: ZHIP_DF_WHOLE launches of plans with aff_ok take the destinations from
+// aff_rowblk instead of the row map (k_decode_il's AFF).
+template <int ITEM, bool SWAP, bool AFF = false>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_encode_il(const EncodeParams p) {
     constexpr int K = kDefaultBlocks;
     __shared__ uint32_t s_tab[kPairTabWords];
@@ -521,8 +523,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         const uint32_t st = st0 + S * (uint32_t)k;
-        const uint32_t sidx = p.nseg - 1u - st / (uint32_t)K;
-        m[k] = load_uniform<zhip_rowblk>(p.rowmap + ((size_t)ch.sel * p.nseg + sidx) * K + (st % (uint32_t)K));
+        if constexpr (AFF) {
+            m[k] = aff_rowblk(p, st);
+        } else {
+            const uint32_t sidx = p.nseg - 1u - st / (uint32_t)K;
+            m[k] = load_uniform<zhip_rowblk>(p.rowmap + ((size_t)ch.sel * p.nseg + sidx) * K + (st % (uint32_t)K));
+        }
     }
     const uint32_t lane_row = (16u * (uint32_t)t) >> p.row_shift;
     const uint32_t lane_col = (16u * (uint32_t)t) & ((1u << p.row_shift) - 1u);
@@ -601,14 +607,16 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))
 
 using EncodeFn = void (*)(const EncodeParams);
 
-static EncodeFn pick_encode_il(int item, bool swap) {
+static EncodeFn pick_encode_il(int item, bool swap, bool aff) {
+#define ZHIP_EIL(I, W) (aff ? k_encode_il<I, W, true> : k_encode_il<I, W>)
     switch (item) {
-        case 1: return k_encode_il<1, false>;
-        case 2: return swap ? k_encode_il<2, true> : k_encode_il<2, false>;
-        case 4: return swap ? k_encode_il<4, true> : k_encode_il<4, false>;
-        case 8: return swap ? k_encode_il<8, true> : k_encode_il<8, false>;
+        case 1: return ZHIP_EIL(1, false);
+        case 2: return swap ? ZHIP_EIL(2, true) : ZHIP_EIL(2, false);
+        case 4: return swap ? ZHIP_EIL(4, true) : ZHIP_EIL(4, false);
+        case 8: return swap ? ZHIP_EIL(8, true) : ZHIP_EIL(8, false);
         default: return nullptr;
     }
+#undef ZHIP_EIL
 }
 
 // k_encode_quad: k_encode_pair for chunks of at most 16 KiB (one unit per
@@ -813,7 +821,7 @@ int launch_encode(const EncodeParams& p, hipStream_t stream, int max_grid) {
         p.il_S == 8u && p.nseg <= 32u && g_tune_arm != 34) {
         // one unit per workgroup, steps interleaved in groups of eight (k_encode_il;
         // tuning arm 34 keeps k_encode_pair)
-        EncodeFn fn = pick_encode_il(p.g.itemsize, swap);
+        EncodeFn fn = pick_encode_il(p.g.itemsize, swap, p.aff_ok != 0);
         if (!fn) return ZHIP_E_UNSUPPORTED;
         if (p.n_units == 0) return ZHIP_OK;
         g_last_kernel = "k_encode_il";

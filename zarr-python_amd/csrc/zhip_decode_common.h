@@ -225,6 +225,19 @@ __device__ __forceinline__ uint32_t load_trailer_uniform(const uint8_t* cp, uint
     return (uint32_t)((((uint64_t)w.y << 32) | w.x) >> sh);
 }
 
+// The whole-chunk row map's entry for step st (ZHIP_DF_WHOLE launches, plans
+// with aff_ok): rel = (st >> aff_sh) B + (st & aff_mask) C + D, every row of
+// the step (zhip_plan aff_*, plan_affine in capi.cpp).  DecodeParams or
+// EncodeParams.
+template <class P>
+__device__ __forceinline__ zhip_rowblk aff_rowblk(const P& p, uint32_t st) {
+    zhip_rowblk e;
+    e.rel = (int32_t)(st >> p.aff_sh) * p.aff_B + (int32_t)(st & p.aff_mask) * p.aff_C + p.aff_D;
+    e.lo = 0;
+    e.hi = (uint16_t)((uint32_t)kWgStride >> p.row_shift);
+    return e;
+}
+
 __device__ __forceinline__ uint32_t load_trailer(const uint8_t* cp, uint32_t n) {
     const uint8_t* tr = cp + n;
     return (uint32_t)tr[0] | ((uint32_t)tr[1] << 8) | ((uint32_t)tr[2] << 16) | ((uint32_t)tr[3] << 24);

@@ -167,8 +167,9 @@ struct DecodeParams {
     const uint32_t* ilw_tab;
     const uint32_t* ilw_klane;
     const uint32_t* ilw_kidx;
-    // tuning arms 43 / 44: the whole-chunk row map as rel(st) = (st >> aff_sh)
-    // aff_B + (st & aff_mask) aff_C + aff_D (zhip_plan aff_*)
+    // ZHIP_DF_WHOLE launches of a plan with aff_ok: the row map of the whole
+    // chunk as rel(st) = (st >> aff_sh) aff_B + (st & aff_mask) aff_C + aff_D
+    // (zhip_plan aff_*); k_decode_il / k_decode_ilw take their AFF form
     uint32_t aff_ok, aff_sh, aff_mask;
     int32_t aff_B, aff_C, aff_D;
     // load-address prediction (zhip_predict; k_decode_pair): payload of chunk c
@@ -335,6 +336,9 @@ struct EncodeParams {
     uint32_t il_S;
     const uint32_t* il_tab;
     const uint32_t* il_klane;
+    // ZHIP_DF_WHOLE (k_encode_il's AFF form): DecodeParams' aff_* fields
+    uint32_t aff_ok, aff_sh, aff_mask;
+    int32_t aff_B, aff_C, aff_D;
 };
 
 struct PackParams {
@@ -414,7 +418,7 @@ struct zhip_plan {
     uint32_t tile2;
     uint64_t tile2_off;
     // the whole-chunk row map of a whole-row layout in two-level affine form
-    // (plan_affine; tuning arms 43 / 44): aff_ok, shift, B, C, D
+    // (plan_affine; ZHIP_DF_WHOLE launches): aff_ok, shift, B, C, D
     uint32_t aff_ok, aff_sh;
     int32_t aff_B, aff_C, aff_D;
     // k_decode_tilegw (grouped tile layouts with a CRC): the same for groups

@@ -40,6 +40,7 @@ DF_ROWS = 4
 DF_TILE_PREFIX = 8
 DF_BANK1 = 16  # deferred CRC verdicts: publish into workspace bank 1, check bank 0
 DF_DEFER = 32  # opt in to deferred CRC verdicts (the Python path reads the verdict words)
+DF_WHOLE = 64  # every selection is its chunk's whole region: affine row destinations (zarrhip.h)
 
 PK_TILE4 = 1
 PK_TILE4_ENCODE = 2

@@ -193,6 +193,19 @@ def _rows_map_host(plan, sels: np.ndarray):
     return host
 
 
+def _whole_sels(layout: N.Layout, sels: np.ndarray) -> bool:
+    """Every selection of the (deduplicated) table is its chunk's whole
+    region -- start 0, count = chunk shape, unit steps -- so a row-map launch
+    may take ZHIP_DF_WHOLE (destinations computed from the plan's affine form
+    of the whole-chunk map instead of loaded from the map)."""
+    if len(sels) != 1:
+        return False
+    nd = layout.ndim
+    s = sels[0]
+    shape = np.array(layout.shape[:nd])
+    return bool((s["start"][:nd] == 0).all() and (s["count"][:nd] == shape).all() and (s["step"][:nd] == 1).all())
+
+
 def _rows_map(plan, sels: np.ndarray, device):
     """_rows_map_host, uploaded."""
     host = _rows_map_host(plan, sels)
@@ -223,6 +236,8 @@ class DecodeLaunch:
         # row map (zhip_rows_map): per (selection, unit, step) destinations for the
         # two-unit row decode; None when the layout does not admit one
         rowmap = _rows_map_host(self.plan, sels) if fast and rows else None
+        if rowmap is not None and _whole_sels(layout, sels):
+            self.flags |= N.DF_WHOLE
         # every table in one host -> device copy; statuses and workspaces in
         # one zeroed buffer.  The launches take plain addresses (p_*); the d_*
         # tensor views are built on demand (result checks, tests, tools).

@@ -61,7 +61,7 @@ class EncodeLaunch:
 
     def __init__(self, layout: N.Layout, chunks: np.ndarray, sels: np.ndarray, arr, dst, fast: bool,
                  device, rows: bool = False, tile: bool = False, tile_prefix: bool = False):
-        from .pipeline import _rows_map, get_plan
+        from .pipeline import _rows_map, _whole_sels, get_plan
 
         torch = _torch()
         self.plan = get_plan(layout)
@@ -78,6 +78,8 @@ class EncodeLaunch:
         self.flags = N.DF_FAST_ROWS if fast else 0
         # whole-row batches encode in k_encode_pair through the row map
         self.d_rowmap = _rows_map(self.plan, sels, device) if fast and rows else None
+        if self.d_rowmap is not None and _whole_sels(layout, sels):
+            self.flags |= N.DF_WHOLE  # whole chunks: destinations from the plan (zarrhip.h)
         # transposed layouts: k_encode_tile4 (full selections, full tiles, <= 64
         # tiles per chunk: the library decides) or k_encode_tile (any tiling,
         # prefix-box selections of edge chunks)
