@@ -188,8 +188,9 @@ int zhip_plan_kernel_flags(const zhip_plan *plan, uint32_t *flags);
 #define ZHIP_DF_DEFER 32u     /* opt in to deferred CRC verdicts (below).  Without it
                                  every decode reports a chunk's CRC mismatch in its own
                                  launch (d_status + d_errflag), as zhip_decode documents */
-#define ZHIP_DF_WHOLE 64u     /* with a row map (zhip_decode_mapped with ZHIP_DF_ROWS,
-                                 zhip_encode_mapped): the caller states that every
+#define ZHIP_DF_WHOLE 64u     /* with a row map (zhip_decode_mapped with ZHIP_DF_ROWS;
+                                 accepted by zhip_encode_mapped, whose kernels keep the
+                                 map): the caller states that every
                                  selection of d_sels is its chunk's whole region (start 0,
                                  count = shape, unit steps).  Where the plan's whole-chunk
                                  row map is two-level affine in the step (zhip_plan_info

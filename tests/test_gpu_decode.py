@@ -1339,7 +1339,7 @@ def _ilw_case(device, arm, case, whole=False):
     if not inner:
         host.pop("c/1/0/0")
     want_kernel = {26: "k_decode_ilw1024", 27: "k_decode_ilw512", 31: "k_decode_ilw1024r", 32: "k_decode_ilw512r",
-                   41: "k_decode_ilh", 42: "k_decode_ilw512m", 45: "k_decode_il"}[arm]
+                   41: "k_decode_ilh", 42: "k_decode_ilw512m", 45: "k_decode_ilw512"}[arm]
     set_tuning(6, arm)
     try:
         store = zarr_hip.DeviceStore.from_host(host, device)

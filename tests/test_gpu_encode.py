@@ -225,6 +225,28 @@ def test_encode_il(device, case):
     _run(device, shape, chunks, dtype, codecs, fill, w[:1], write_empty=True)
 
 
+@pytest.mark.tuning
+@pytest.mark.parametrize("case", [0, 1])
+def test_encode_il_affine_arm(device, case):
+    """Tuning arm 46: k_encode_il takes whole-chunk writes' destinations from
+    the plan's affine form of the row map (ZHIP_DF_WHOLE) instead of the map:
+    stores byte-identical with the oracle, partial writes (the map) between."""
+    from zarr_hip import _native as N
+
+    shape, chunks, dtype, codecs, fill = IL_ENC_CASES[case]
+    d = _data(shape, dtype)
+    part = (slice(3, shape[0] - 5), slice(7, shape[1]), slice(1, shape[2] - 9))
+    psh = tuple(s.stop - s.start for s in part)
+    set_tuning(6, 46)
+    try:
+        arr, _ = _run(device, shape, chunks, dtype, codecs, fill,
+                      [((Ellipsis,), d), (part, _data(psh, dtype, 3)), ((Ellipsis,), d)])
+        arr[...] = d
+        assert N.lib().zhip_last_kernel().decode() == "k_encode_il"
+    finally:
+        set_tuning(6, 0)
+
+
 def test_encode_il_sharded(device):
     from zarr_hip import _native as N
 

@@ -694,7 +694,8 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
         // (k_decode_ilw, decode_rows.hip) -- graph-timed 8.8 vs 9.4 us at the
         // N = 8 share, 10.3 vs 11.0 at N = 4; 14.6 vs 16.5 for k_decode_il at
         // N = 2 (profiles/r05/f/).  (Tuning build: any arm keeps k_decode_il.)
-        if (il && p.ilw_nt == 512u && p.n_units <= kIlwMaxUnits && g_tune_arm == 0 && (tune & ~kTuneStamp) == 0) {
+        if (il && p.ilw_nt == 512u && p.n_units <= kIlwMaxUnits && (g_tune_arm == 0 || g_tune_arm == 45) &&
+            (tune & ~kTuneStamp) == 0) {
             KernelFn wfn = select_ilw_kernel(p.g.itemsize, swap, 512, false, p.aff_ok != 0);
             if (!wfn) return ZHIP_E_UNSUPPORTED;
             const uint32_t wgrid = p.n_units > p.n_idx ? p.n_units : p.n_idx;

@@ -497,8 +497,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
 // the line's third word the same way (bits 32 / 48 + half), and the last of
 // those writes trailer, status and the non-empty flag.  Chunks of at most 16
 // units have one half and no second level.
-// AFF: ZHIP_DF_WHOLE launches of plans with aff_ok take the destinations from
-// aff_rowblk instead of the row map (k_decode_il's AFF).
+// AFF (tuning arm 46): ZHIP_DF_WHOLE launches of plans with aff_ok take the
+// destinations from aff_rowblk instead of the row map (k_decode_il's AFF);
+// graph-timed 0.5 us slower on the C2 encode, not adopted.
 template <int ITEM, bool SWAP, bool AFF = false>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_encode_il(const EncodeParams p) {
     constexpr int K = kDefaultBlocks;
@@ -608,7 +609,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))
 using EncodeFn = void (*)(const EncodeParams);
 
 static EncodeFn pick_encode_il(int item, bool swap, bool aff) {
-#define ZHIP_EIL(I, W) (aff ? k_encode_il<I, W, true> : k_encode_il<I, W>)
+#if ZHIP_TUNING
+#define ZHIP_EIL(I, W) (aff ? k_encode_il<I, W, true> : k_encode_il<I, W>)  // (arm 46)
+#else
+#define ZHIP_EIL(I, W) k_encode_il<I, W>
+#endif
     switch (item) {
         case 1: return ZHIP_EIL(1, false);
         case 2: return swap ? ZHIP_EIL(2, true) : ZHIP_EIL(2, false);
