@@ -1282,30 +1282,35 @@ def test_ilw_arms_exact_and_crc(device, arm, case):
     _ilw_case(device, arm, case)
 
 
-@pytest.mark.parametrize("shape,cshape,inner,kname", [
-    ((256, 256, 128), (64, 64, 64), None, "k_decode_il"),                     # 1 024 units
-    ((128, 128, 64), (128, 128, 64), (64, 64, 64), "k_decode_ilw512"),        # 128 units, sharded
+@pytest.mark.parametrize("shape,cshape,inner,dtype,endian,kname,affine", [
+    ((256, 256, 128), (64, 64, 64), None, "float32", LE, "k_decode_il", True),                 # 1 024 units
+    ((128, 128, 64), (128, 128, 64), (64, 64, 64), "float32", LE, "k_decode_ilw512", True),    # sharded
+    ((64, 128, 128), (32, 64, 64), None, "int16", BE, "k_decode_ilw512", True),                # 128-byte rows
+    # three 4 KiB steps per z plane: no power-of-two split, the launch keeps the map
+    ((128, 96, 64), (64, 48, 64), None, "float32", LE, "k_decode_ilw512", False),
 ])
-def test_whole_chunk_reads_compute_destinations(device, shape, cshape, inner, kname):
+def test_whole_chunk_reads_compute_destinations(device, shape, cshape, inner, dtype, endian, kname, affine):
     """Whole-chunk reads launch with ZHIP_DF_WHOLE: k_decode_il /
     k_decode_ilw512 take each step's destination from the plan's affine form
     of the whole-chunk row map, not from the map -- exact with the map zeroed
-    on the device (a map-driven launch would write nothing); a partial
-    window keeps the map."""
+    on the device (a map-driven launch would write nothing); a layout whose
+    map has no two-level affine form keeps the map under the same flag; a
+    partial window never sets it."""
     import zarr_hip
     from zarr_hip import _native as N
 
-    codecs = [SHARD(inner, [LE, CRC])] if inner else [LE, CRC]
-    meta = O.ArrayMeta(shape, cshape, np.dtype("float32"), 1.5, codecs=codecs)
+    codecs = [SHARD(inner, [endian, CRC])] if inner else [endian, CRC]
+    meta = O.ArrayMeta(shape, cshape, np.dtype(dtype), 3, codecs=codecs)
     host = {}
-    O.write(host, meta, (Ellipsis,), _data(shape, "float32"))
-    if not inner:
-        host.pop("c/1/0/1")  # a missing chunk: filled through the same destinations
+    O.write(host, meta, (Ellipsis,), _data(shape, dtype))
+    if not inner:  # a missing chunk: filled through the same destinations
+        host.pop(sorted(k for k in host if k.startswith("c/"))[-1])
     store = zarr_hip.DeviceStore.from_host(host, device)
-    arr = zarr_hip.Array.create(store, shape, cshape, "float32", 1.5, codecs=codecs)
+    arr = zarr_hip.Array.create(store, shape, cshape, dtype, 3, codecs=codecs)
     prog, out = arr.prepare_read((Ellipsis,))
     assert prog.data.flags & N.DF_WHOLE
-    prog.data.d_rowmap.zero_()
+    if affine:
+        prog.data.d_rowmap.zero_()
     prog.launch()
     prog.results()
     assert N.lib().zhip_last_kernel().decode() == kname
