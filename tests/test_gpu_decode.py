@@ -1497,7 +1497,39 @@ def _tile_pairs_case(device, dtype, endian, chunks, shape, order, codecs):
 
 
 @pytest.mark.tuning
-@pytest.mark.parametrize("arm", [0, 5, 38, 40])
+@pytest.mark.parametrize("arm", [0, 47])
+def test_transpose_tileg_128_chunks_arrivals(device, arm):
+    """C3's 128^3-chunk geometry (256 workgroups per chunk in the two-tile
+    form: 16 arrival subwords and a second level): the returning publication
+    with its words packed (production) and on lines of their own (tuning arm
+    47) decodes exactly, fills a missing chunk and reports a corrupted one."""
+    import zarr_hip
+    from zarr_hip import _native as N
+
+    codecs = [T((2, 1, 0)), LE, CRC]
+    kernel = {0: b"k_decode_tileg2w", 47: b"k_decode_tileg2ws"}[arm]
+    set_tuning(6, arm)
+    try:
+        arr, host, meta = _roundtrip(device, (128, 256, 256), (128, 128, 128), "float32", codecs, fill=3,
+                                     drop=["c/0/1/0"])
+        assert N.lib().zhip_last_kernel() == kernel
+        bad = bytearray(host["c/0/0/1"])
+        bad[len(bad) // 3 + 5] ^= 0x40
+        host["c/0/0/1"] = bytes(bad)
+        with pytest.raises(ValueError) as want:
+            O.read(host, meta)
+        arr = zarr_hip.Array.create(zarr_hip.DeviceStore.from_host(host, device), (128, 256, 256),
+                                    (128, 128, 128), "float32", 3, codecs=codecs)
+        with pytest.raises(ValueError) as got:
+            arr[...]
+        assert str(got.value) == str(want.value)
+        assert N.lib().zhip_last_kernel() == kernel
+    finally:
+        set_tuning(6, 0)
+
+
+@pytest.mark.tuning
+@pytest.mark.parametrize("arm", [0, 5, 38, 40, 47])
 @pytest.mark.parametrize("order", [(2, 1, 0), (1, 2, 0), (0, 2, 1)])
 @pytest.mark.parametrize("dtype,endian", [("float32", LE), ("int16", BE), ("float64", LE), ("uint8", LE)])
 def test_transpose_tilegw_and_tileg(device, order, dtype, endian, arm):
@@ -1510,7 +1542,8 @@ def test_transpose_tilegw_and_tileg(device, order, dtype, endian, arm):
     from zarr_hip import _native as N
 
     codecs = [T(order), endian, CRC]
-    kernel = {0: b"k_decode_tileg2w", 5: b"k_decode_tileg", 38: b"k_decode_tilegw", 40: b"k_decode_tileglt"}[arm]
+    kernel = {0: b"k_decode_tileg2w", 5: b"k_decode_tileg", 38: b"k_decode_tilegw", 40: b"k_decode_tileglt",
+              47: b"k_decode_tileg2ws"}[arm]
     set_tuning(6, arm)
     try:
         _roundtrip(device, (96, 160, 160), (96, 80, 80), dtype, codecs, fill=3, drop=["c/0/1/0"])

@@ -838,9 +838,12 @@ int zhip_plan_info(const zhip_plan* p, uint32_t* units_per_chunk, uint32_t* work
     // (k_decode_tile4w, four tiles per workgroup: the same subwords past 32 workgroups per chunk)
     const uint32_t wpc4 = (p->tile4 && (p->layout.flags & ZHIP_LF_CRC)) ? p->t_per_chunk / 4u : 0u;
     if (wpc4 > 32u && wpc4 <= 256u) n_sub2 = std::max(n_sub2, (wpc4 + 15u) / 16u);
-    if (workspace_words)
-        *workspace_words = std::max(4 + 2 * std::max(std::max(p->n_sub, p->xw_nsub), n_sub2),
-                                    (p->layout.flags & ZHIP_LF_CRC) ? kPubLine : 0u);
+    uint32_t w = std::max(4 + 2 * std::max(std::max(p->n_sub, p->xw_nsub), n_sub2),
+                          (p->layout.flags & ZHIP_LF_CRC) ? kPubLine : 0u);
+    // (tuning arm 47: the grouped kernels' arrival words on lines of their own)
+    if (ZHIP_TUNING && p->gd >= 0 && (p->layout.flags & ZHIP_LF_CRC))
+        w = std::max(w, kPubLine * (1u + std::max(p->n_sub, n_sub2)));
+    if (workspace_words) *workspace_words = w;
     return ZHIP_OK;
 }
 

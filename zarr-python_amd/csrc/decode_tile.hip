@@ -469,13 +469,19 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
 // 4 words per chunk), whose completing arrival carries the subgroup's XOR on
 // to the chunk word.  True for the arrival completing the chunk, with the
 // XOR of every contribution and whether any group was non-empty.
+// SPR (tuning arm 47): every subword and the chunk's word on a 128-byte line
+// of its own (chunk lines at ws + 32 c, subword lines after all chunk lines;
+// zhip_plan_info sizes the tuning build's workspace for it), so a chunk's
+// arrivals do not meet on one line.
+template <bool SPR = false>
 __device__ __forceinline__ bool tileg_arrive(uint32_t* ws, uint32_t n_chunks, uint32_t c, uint32_t grp,
                                              uint32_t gpc, uint32_t n_sub, uint32_t v, bool ne, uint32_t& raw,
                                              bool& any_ne) {
     if (n_sub) {
         const uint32_t sg = grp >> 4;
         const uint32_t in_sg = min(16u, gpc - (sg << 4));
-        uint64_t* sw = reinterpret_cast<uint64_t*>(ws + 4ull * n_chunks) + (uint64_t)c * n_sub + sg;
+        uint64_t* sw = SPR ? reinterpret_cast<uint64_t*>(ws + 32ull * n_chunks) + ((uint64_t)c * n_sub + sg) * 16u
+                           : reinterpret_cast<uint64_t*>(ws + 4ull * n_chunks) + (uint64_t)c * n_sub + sg;
         const uint64_t b = 1ull << (grp & 15u);
         const uint64_t prev = __hip_atomic_fetch_xor(sw, (b << 32) | (ne ? b << 48 : 0ull) | v, __ATOMIC_RELAXED,
                                                      __HIP_MEMORY_SCOPE_AGENT);
@@ -486,7 +492,7 @@ __device__ __forceinline__ bool tileg_arrive(uint32_t* ws, uint32_t n_chunks, ui
         grp = sg;
         gpc = n_sub;
     }
-    uint64_t* cw = reinterpret_cast<uint64_t*>(ws) + 2ull * c;
+    uint64_t* cw = reinterpret_cast<uint64_t*>(ws) + (SPR ? 16ull : 2ull) * c;
     const uint64_t b = 1ull << grp;
     const uint64_t prev = __hip_atomic_fetch_xor(cw, (b << 32) | (ne ? b << 48 : 0ull) | v, __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_AGENT);
@@ -852,7 +858,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
 // apart: 64 KiB in 128^3 chunks); the chain is the same A_(4 sq) one, the lane
 // constants swap the roles of w and l / 16, and in tile iteration j the 16
 // lanes of every wave that hold tile j write the image.
-template <int ITEM, bool SWAP, int PUB = 2, int NT = kTiles, bool LT = false>
+template <int ITEM, bool SWAP, int PUB = 2, int NT = kTiles, bool LT = false, bool SPR = false>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_decode_tilegw(
     const DecodeParams p) {
     static_assert(!LT || NT == kTiles, "lane-tile mapping: four tiles per workgroup");
@@ -977,7 +983,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
             const uint32_t nsub = NT == kTiles ? p.n_sub : ((gpc > 16u && gpc <= 256u) ? (gpc + 15u) / 16u : 0u);
             if (gpc <= 16u || nsub) {
                 bool any_ne;
-                last_one = tileg_arrive(p.ws, p.n_chunks, c, wg, gpc, nsub, V, false, raw, any_ne);
+                last_one = tileg_arrive<SPR>(p.ws, p.n_chunks, c, wg, gpc, nsub, V, false, raw, any_ne);
             } else {  // more than 256 groups per chunk: XOR, then count arrivals
                 uint32_t* accw = p.ws + 4ull * c;
                 const uint32_t prev = __hip_atomic_fetch_xor(accw, V, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1420,7 +1426,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
 // residency rounds; the first half's contribution shifted by p.g_z2 to the
 // group's last-tile frame that ge.ku assumes; arrival subwords for twice the
 // workgroups, zhip_plan_info)
-template <bool CRC, int ITEM, bool SWAP, int NT = kTiles>
+template <bool CRC, int ITEM, bool SWAP, int NT = kTiles, bool SPR = false>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_encode_tileg(
     const EncodeParams p) {
     constexpr int kPer = 16 / ITEM;
@@ -1548,7 +1554,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     const uint32_t nsub = NT == kTiles ? p.n_sub : ((gpc > 16u && gpc <= 256u) ? (gpc + 15u) / 16u : 0u);
     if (gpc <= 16u || nsub) {
         bool any_ne = false;
-        if (!tileg_arrive(p.ws, p.n_chunks, c, wg, gpc, nsub, V, ne, raw, any_ne)) return;
+        if (!tileg_arrive<SPR>(p.ws, p.n_chunks, c, wg, gpc, nsub, V, ne, raw, any_ne)) return;
         p.nonempty[c] = any_ne ? 1u : 0u;
     } else {  // more than 256 groups per chunk: arrival count | non-empty count word
         uint32_t* accw = p.ws + 4ull * c;
@@ -1582,6 +1588,18 @@ using KernelFn = void (*)(const DecodeParams);
 using EncodeFn = void (*)(const EncodeParams);
 
 EncodeFn select_encode_tileg_kernel(bool crc, int item, bool swap, int nt) {
+#if ZHIP_TUNING
+    if (nt == 6) {  // arm 47: four tiles, arrival words on lines of their own (CRC layouts)
+        if (!crc) return nullptr;
+        switch (item) {
+            case 1: return k_encode_tileg<true, 1, false, 4, true>;
+            case 2: return swap ? k_encode_tileg<true, 2, true, 4, true> : k_encode_tileg<true, 2, false, 4, true>;
+            case 4: return swap ? k_encode_tileg<true, 4, true, 4, true> : k_encode_tileg<true, 4, false, 4, true>;
+            case 8: return swap ? k_encode_tileg<true, 8, true, 4, true> : k_encode_tileg<true, 8, false, 4, true>;
+            default: return nullptr;
+        }
+    }
+#endif
     if (nt == 2) {  // CRC layouts only
         if (!crc) return nullptr;
         switch (item) {
@@ -1669,6 +1687,7 @@ KernelFn select_tilegw_kernel(int item, bool swap, bool defer, int nt) {  // CRC
 #define ZHIP_TILEGW(I, W)                                                                          \
     (nt == 2 ? (defer ? k_decode_tilegw<I, W, 2, 2> : k_decode_tilegw<I, W, 0, 2>)                 \
      : nt == 5 ? (defer ? k_decode_tilegw<I, W, 2, 4, true> : k_decode_tilegw<I, W, 0, 4, true>)   \
+     : nt == 6 ? k_decode_tilegw<I, W, 0, 2, false, true>                                           \
              : (defer ? k_decode_tilegw<I, W, 2> : k_decode_tilegw<I, W, 0>))
 #else
 #define ZHIP_TILEGW(I, W)                                                                          \
