@@ -1497,17 +1497,17 @@ def _tile_pairs_case(device, dtype, endian, chunks, shape, order, codecs):
 
 
 @pytest.mark.tuning
-@pytest.mark.parametrize("arm", [0, 47])
+@pytest.mark.parametrize("arm", [0, 48])
 def test_transpose_tileg_128_chunks_arrivals(device, arm):
     """C3's 128^3-chunk geometry (256 workgroups per chunk in the two-tile
     form: 16 arrival subwords and a second level): the returning publication
-    with its words packed (production) and on lines of their own (tuning arm
-    47) decodes exactly, fills a missing chunk and reports a corrupted one."""
+    with its words on lines of their own (production) and packed (tuning arm
+    48) decodes exactly, fills a missing chunk and reports a corrupted one."""
     import zarr_hip
     from zarr_hip import _native as N
 
     codecs = [T((2, 1, 0)), LE, CRC]
-    kernel = {0: b"k_decode_tileg2w", 47: b"k_decode_tileg2ws"}[arm]
+    kernel = {0: b"k_decode_tileg2w", 48: b"k_decode_tileg2wp"}[arm]
     set_tuning(6, arm)
     try:
         arr, host, meta = _roundtrip(device, (128, 256, 256), (128, 128, 128), "float32", codecs, fill=3,
@@ -1529,7 +1529,7 @@ def test_transpose_tileg_128_chunks_arrivals(device, arm):
 
 
 @pytest.mark.tuning
-@pytest.mark.parametrize("arm", [0, 5, 38, 40, 47])
+@pytest.mark.parametrize("arm", [0, 5, 38, 40, 48])
 @pytest.mark.parametrize("order", [(2, 1, 0), (1, 2, 0), (0, 2, 1)])
 @pytest.mark.parametrize("dtype,endian", [("float32", LE), ("int16", BE), ("float64", LE), ("uint8", LE)])
 def test_transpose_tilegw_and_tileg(device, order, dtype, endian, arm):
@@ -1543,7 +1543,7 @@ def test_transpose_tilegw_and_tileg(device, order, dtype, endian, arm):
 
     codecs = [T(order), endian, CRC]
     kernel = {0: b"k_decode_tileg2w", 5: b"k_decode_tileg", 38: b"k_decode_tilegw", 40: b"k_decode_tileglt",
-              47: b"k_decode_tileg2ws"}[arm]
+              48: b"k_decode_tileg2wp"}[arm]
     set_tuning(6, arm)
     try:
         _roundtrip(device, (96, 160, 160), (96, 80, 80), dtype, codecs, fill=3, drop=["c/0/1/0"])

@@ -840,9 +840,9 @@ int zhip_plan_info(const zhip_plan* p, uint32_t* units_per_chunk, uint32_t* work
     if (wpc4 > 32u && wpc4 <= 256u) n_sub2 = std::max(n_sub2, (wpc4 + 15u) / 16u);
     uint32_t w = std::max(4 + 2 * std::max(std::max(p->n_sub, p->xw_nsub), n_sub2),
                           (p->layout.flags & ZHIP_LF_CRC) ? kPubLine : 0u);
-    // (tuning arm 47: the grouped kernels' arrival words on lines of their own)
-    if (ZHIP_TUNING && p->gd >= 0 && (p->layout.flags & ZHIP_LF_CRC))
-        w = std::max(w, kPubLine * (1u + std::max(p->n_sub, n_sub2)));
+    // (k_decode_tilegw's two-tile form, tuning arm 47's k_encode_tileg: the
+    // arrival words on 128-byte lines of their own, tileg_arrive SPR)
+    if (tg2w) w = std::max(w, kPubLine * (1u + (ZHIP_TUNING ? std::max(p->n_sub, n_sub2) : n_sub2)));
     if (workspace_words) *workspace_words = w;
     return ZHIP_OK;
 }

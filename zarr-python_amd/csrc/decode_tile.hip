@@ -469,10 +469,13 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
 // 4 words per chunk), whose completing arrival carries the subgroup's XOR on
 // to the chunk word.  True for the arrival completing the chunk, with the
 // XOR of every contribution and whether any group was non-empty.
-// SPR (tuning arm 47): every subword and the chunk's word on a 128-byte line
-// of its own (chunk lines at ws + 32 c, subword lines after all chunk lines;
-// zhip_plan_info sizes the tuning build's workspace for it), so a chunk's
-// arrivals do not meet on one line.
+// SPR: every subword and the chunk's word on a 128-byte line of its own
+// (chunk lines at ws + 32 c, subword lines after all chunk lines;
+// zhip_plan_info sizes the workspace for it), so a chunk's arrivals do not
+// meet on one line: production for k_decode_tilegw's two-tile form -- C3 in
+// 128^3 chunks, 256 arrivals per chunk, 28.94 / 29.00 vs 29.57 / 29.28 us
+// graph-timed (profiles/r05/aa/; tuning arm 48 keeps the packed words); in
+// k_encode_tileg (128 arrivals per chunk) neutral, tuning arm 47.
 template <bool SPR = false>
 __device__ __forceinline__ bool tileg_arrive(uint32_t* ws, uint32_t n_chunks, uint32_t c, uint32_t grp,
                                              uint32_t gpc, uint32_t n_sub, uint32_t v, bool ne, uint32_t& raw,
@@ -1684,14 +1687,17 @@ KernelFn select_tileg_kernel(bool crc, int item, bool swap, bool defer) {
 
 KernelFn select_tilegw_kernel(int item, bool swap, bool defer, int nt) {  // CRC chains only
 #if ZHIP_TUNING
+// (nt 2: the two-tile form, always the returning publication on spread lines;
+// tuning: 6 the same on packed words, 5 lanes pick the tile)
+#if ZHIP_TUNING
 #define ZHIP_TILEGW(I, W)                                                                          \
-    (nt == 2 ? (defer ? k_decode_tilegw<I, W, 2, 2> : k_decode_tilegw<I, W, 0, 2>)                 \
+    (nt == 2 ? k_decode_tilegw<I, W, 0, 2, false, true>                                             \
      : nt == 5 ? (defer ? k_decode_tilegw<I, W, 2, 4, true> : k_decode_tilegw<I, W, 0, 4, true>)   \
-     : nt == 6 ? k_decode_tilegw<I, W, 0, 2, false, true>                                           \
+     : nt == 6 ? k_decode_tilegw<I, W, 0, 2>                                                        \
              : (defer ? k_decode_tilegw<I, W, 2> : k_decode_tilegw<I, W, 0>))
 #else
 #define ZHIP_TILEGW(I, W)                                                                          \
-    (nt == 2 ? (defer ? k_decode_tilegw<I, W, 2, 2> : k_decode_tilegw<I, W, 0, 2>)                 \
+    (nt == 2 ? k_decode_tilegw<I, W, 0, 2, false, true>                                             \
              : (defer ? k_decode_tilegw<I, W, 2> : k_decode_tilegw<I, W, 0>))
 #endif
     switch (item) {
