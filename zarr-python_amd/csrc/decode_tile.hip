@@ -1686,7 +1686,6 @@ KernelFn select_tileg_kernel(bool crc, int item, bool swap, bool defer) {
 }
 
 KernelFn select_tilegw_kernel(int item, bool swap, bool defer, int nt) {  // CRC chains only
-#if ZHIP_TUNING
 // (nt 2: the two-tile form, always the returning publication on spread lines;
 // tuning: 6 the same on packed words, 5 lanes pick the tile)
 #if ZHIP_TUNING
