@@ -1324,12 +1324,46 @@ def test_whole_chunk_reads_compute_destinations(device, shape, cshape, inner, dt
 
 
 @pytest.mark.tuning
+@pytest.mark.parametrize("arm", [45, 49])
 @pytest.mark.parametrize("case", [0, 1])
-def test_row_map_arm_exact_and_crc(device, case):
+def test_row_map_arm_exact_and_crc(device, arm, case):
     """Tuning arm 45 keeps the row-map loads for whole-chunk launches (the A/B
-    reference of ZHIP_DF_WHOLE): exact, missing chunks filled, corrupted
-    chunks and indexes reported with the reference's message."""
-    _ilw_case(device, 45, case, whole=True)
+    reference of ZHIP_DF_WHOLE); arm 49 publishes through two subwords of 16
+    on lines of their own: exact, missing chunks filled, corrupted chunks and
+    indexes reported with the reference's message."""
+    _ilw_case(device, arm, case, whole=True)
+
+
+@pytest.mark.tuning
+def test_il_split_publication_arm(device):
+    """Tuning arm 49 on k_decode_il (1 024 units, whole-chunk reads): the
+    split publication decodes exactly and reports a corrupted chunk."""
+    import zarr_hip
+    from zarr_hip import _native as N
+
+    shape, cshape = (256, 256, 128), (64, 64, 64)
+    codecs = [LE, CRC]
+    meta = O.ArrayMeta(shape, cshape, np.dtype("float32"), 0, codecs=codecs)
+    host = {}
+    O.write(host, meta, (Ellipsis,), _data(shape, "float32"))
+    set_tuning(6, 49)
+    try:
+        arr = zarr_hip.Array.create(zarr_hip.DeviceStore.from_host(host, device), shape, cshape, "float32", 0,
+                                    codecs=codecs)
+        assert arr[...].tobytes() == O.read(host, meta).tobytes()
+        assert N.lib().zhip_last_kernel().decode() == "k_decode_il"
+        bad = bytearray(host["c/1/2/1"])
+        bad[70001] ^= 0x10
+        host["c/1/2/1"] = bytes(bad)
+        with pytest.raises(ValueError) as want:
+            O.read(host, meta)
+        arr = zarr_hip.Array.create(zarr_hip.DeviceStore.from_host(host, device), shape, cshape, "float32", 0,
+                                    codecs=codecs)
+        with pytest.raises(ValueError) as got:
+            arr[...]
+        assert str(got.value) == str(want.value)
+    finally:
+        set_tuning(6, 0)
 
 
 def _ilw_case(device, arm, case, whole=False):
@@ -1344,7 +1378,8 @@ def _ilw_case(device, arm, case, whole=False):
     if not inner:
         host.pop("c/1/0/0")
     want_kernel = {26: "k_decode_ilw1024", 27: "k_decode_ilw512", 31: "k_decode_ilw1024r", 32: "k_decode_ilw512r",
-                   41: "k_decode_ilh", 42: "k_decode_ilw512m", 45: "k_decode_ilw512"}[arm]
+                   41: "k_decode_ilh", 42: "k_decode_ilw512m", 45: "k_decode_ilw512",
+                   49: "k_decode_ilw512"}[arm]
     set_tuning(6, arm)
     try:
         store = zarr_hip.DeviceStore.from_host(host, device)
@@ -1375,7 +1410,7 @@ def _ilw_case(device, arm, case, whole=False):
 
 
 @pytest.mark.tuning
-@pytest.mark.parametrize("arm", [0, 5, 37, 38])
+@pytest.mark.parametrize("arm", [0, 5, 37, 38, 49])
 @pytest.mark.parametrize("dtype,endian,chunks,shape", TILE4_CASES)
 def test_transpose_tile4w_and_tile4(device, dtype, endian, chunks, shape, arm):
     """k_decode_tile4w's two-tile form (production for CRC layouts of at most
@@ -1387,7 +1422,8 @@ def test_transpose_tile4w_and_tile4(device, dtype, endian, chunks, shape, arm):
     from zarr_hip import _native as N
 
     codecs = [T((2, 1, 0)), endian, CRC]
-    kernel = {0: b"k_decode_tile2w", 5: b"k_decode_tile4", 37: b"k_decode_tile1w", 38: b"k_decode_tile4w"}[arm]
+    kernel = {0: b"k_decode_tile2w", 5: b"k_decode_tile4", 37: b"k_decode_tile1w", 38: b"k_decode_tile4w",
+              49: b"k_decode_tile2ws"}[arm]
     set_tuning(6, arm)
     try:
         _roundtrip(device, shape, chunks, dtype, codecs)

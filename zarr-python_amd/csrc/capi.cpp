@@ -843,6 +843,9 @@ int zhip_plan_info(const zhip_plan* p, uint32_t* units_per_chunk, uint32_t* work
     // (k_decode_tilegw's two-tile form, tuning arm 47's k_encode_tileg: the
     // arrival words on 128-byte lines of their own, tileg_arrive SPR)
     if (tg2w) w = std::max(w, kPubLine * (1u + (ZHIP_TUNING ? std::max(p->n_sub, n_sub2) : n_sub2)));
+    // (tuning arm 49: k_decode_il / k_decode_ilw / two-tile k_decode_tile4w publish
+    // through two subwords on lines of their own)
+    if (ZHIP_TUNING && (p->layout.flags & ZHIP_LF_CRC) && (p->il_S || p->tile4)) w = std::max(w, 3u * kPubLine);
     if (workspace_words) *workspace_words = w;
     return ZHIP_OK;
 }

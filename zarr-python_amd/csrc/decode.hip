@@ -694,9 +694,10 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
         // (k_decode_ilw, decode_rows.hip) -- graph-timed 8.8 vs 9.4 us at the
         // N = 8 share, 10.3 vs 11.0 at N = 4; 14.6 vs 16.5 for k_decode_il at
         // N = 2 (profiles/r05/f/).  (Tuning build: any arm keeps k_decode_il.)
-        if (il && p.ilw_nt == 512u && p.n_units <= kIlwMaxUnits && (g_tune_arm == 0 || g_tune_arm == 45) &&
-            (tune & ~kTuneStamp) == 0) {
-            KernelFn wfn = select_ilw_kernel(p.g.itemsize, swap, 512, false, p.aff_ok != 0);
+        if (il && p.ilw_nt == 512u && p.n_units <= kIlwMaxUnits &&
+            (g_tune_arm == 0 || g_tune_arm == 45 || (g_tune_arm == 49 && p.aff_ok)) && (tune & ~kTuneStamp) == 0) {
+            // (tuning arm 49: the split publication, whole-chunk reads)
+            KernelFn wfn = select_ilw_kernel(p.g.itemsize, swap, g_tune_arm == 49 ? 515 : 512, false, p.aff_ok != 0);
             if (!wfn) return ZHIP_E_UNSUPPORTED;
             const uint32_t wgrid = p.n_units > p.n_idx ? p.n_units : p.n_idx;
             if (wgrid == 0) return ZHIP_OK;
@@ -707,7 +708,8 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
         if (il) {
 #if ZHIP_TUNING
             // (arms 1 / 2 are k_decode_il's own; every other arm keeps production here)
-            KernelFn ifn = (g_tune_arm == 1 || g_tune_arm == 2) ? select_il_kernel_arm(crc, p.g.itemsize, swap, g_tune_arm)
+            KernelFn ifn = (g_tune_arm == 1 || g_tune_arm == 2 || (g_tune_arm == 49 && p.aff_ok))
+                               ? select_il_kernel_arm(crc, p.g.itemsize, swap, g_tune_arm)
                            : (tune & kTuneCfLookup) ? select_il_kernel_cf(crc, p.g.itemsize, swap)
                            : (tune & kTuneIlLean) ? select_il_kernel_lean(crc, p.g.itemsize, swap)
                            : (tune & (kTuneIlRegMul | kTuneIlOcc6))
@@ -795,12 +797,13 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
         // (profiles/r05/l/); tuning arm 38 keeps four, 37 takes one (46 us)
         if (w4 && ((p.t2w_kq && g_tune_arm != 38 && g_tune_arm != 37) || (g_tune_arm == 37 && p.t1w_kq))) {
             const int nt = g_tune_arm == 37 ? 1 : 2;
-            KernelFn fn2 = select_tile2w_kernel(p.g.itemsize, swp, nt);
+            // (tuning arm 49: the split publication of 17..32 workgroups per chunk)
+            KernelFn fn2 = select_tile2w_kernel(p.g.itemsize, swp, (nt == 2 && g_tune_arm == 49) ? 3 : nt);
             if (!fn2) return ZHIP_E_UNSUPPORTED;
             if (p.n_units == 0) return ZHIP_OK;
             DecodeParams q = p;
             q.t4w_kq = nt == 1 ? p.t1w_kq : p.t2w_kq;
-            g_last_kernel = nt == 1 ? "k_decode_tile1w" : "k_decode_tile2w";
+            g_last_kernel = nt == 1 ? "k_decode_tile1w" : g_tune_arm == 49 ? "k_decode_tile2ws" : "k_decode_tile2w";
             hipLaunchKernelGGL(fn2, dim3(p.n_units / (uint32_t)nt), dim3(kThreads), 0, stream, q);
             return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
         }

@@ -1279,6 +1279,20 @@ __device__ __forceinline__ void publish_il(const DecodeParams& p, uint32_t c, ui
     }
 }
 
+// publish_il through two subwords of 16 arrivals on lines of their own and a
+// second level on the chunk's line (tileg_arrive SPR; 17..32 workgroups per
+// chunk; tuning arm 49): 16 returning atomics per line instead of 32 on one
+// word, one more round trip for the two subwords' last arrivals.
+__device__ __forceinline__ void publish_il_split(const DecodeParams& p, uint32_t c, uint32_t r, uint32_t wpc,
+                                                 uint32_t V, uint32_t stored, int t) {
+    uint32_t raw = 0, last = 0;
+    if (t == 0) {
+        bool any_ne;
+        last = tileg_arrive<true>(p.ws, p.n_chunks, c, r, wpc, (wpc + 15u) / 16u, V, false, raw, any_ne) ? 1u : 0u;
+    }
+    if (__builtin_amdgcn_readfirstlane(last)) finalize_uniform(p, c, stored, __builtin_amdgcn_readfirstlane(raw), t, true);
+}
+
 // LEAN (tuning arm kTuneIlLean): the PairHot batch, then tables, constants
 // and -- at the addresses the default shard packing predicts (zhip_predict) --
 // the data loads, all before the header chain (chunk record -> index entry)
@@ -1512,6 +1526,11 @@ void k_decode_il(const DecodeParams p) {
                     if (t == 0) dv_publish(p, c, r == 0, V, __builtin_amdgcn_readfirstlane(stored));
                 } else if constexpr (PUB == 3) {  // the chunk's word alone in its line
                     publish_il(p, c, r, wpc, V, __builtin_amdgcn_readfirstlane(stored), t, kPubLine / 2u);
+                } else if constexpr (PUB == 4) {  // two subwords of 16 (tuning arm 49)
+                    if (wpc > 16u && wpc <= 32u)
+                        publish_il_split(p, c, r, wpc, V, __builtin_amdgcn_readfirstlane(stored), t);
+                    else
+                        publish_il(p, c, r, wpc, V, __builtin_amdgcn_readfirstlane(stored), t, kPubLine / 2u);
                 } else {
                     publish_il(p, c, r, wpc, V, __builtin_amdgcn_readfirstlane(stored), t);
                 }
@@ -1540,6 +1559,7 @@ KernelFn select_il_kernel_arm(bool crc, int item, bool swap, int arm) {  // ZHIP
     switch (arm) {
         case 1: return k_decode_il<true, 4, false, false, false, 0, false, 0>;  // round 3: words 16 B apart
         case 2: return k_decode_il<true, 4, false, false, false, 0, false, 2>;  // deferred verdicts
+        case 49: return k_decode_il<true, 4, false, false, false, 0, false, 4, true>;  // split publication (AFF)
         default: return k_decode_il<true, 4, false>;  // arms of other kernels: production
     }
 }
@@ -2284,7 +2304,7 @@ __device__ __forceinline__ uint32_t lanemul3_w(const uint32_t* s_mul, int t, uin
 // column: the run end's LDS reads halve.  MIX (tuning arm 42): the waves of
 // the second 256 lanes multiply in registers, the first through the LDS
 // column, so the run end's lookups and VALU work overlap.
-template <int ITEM, bool SWAP, int NT, bool LMR = false, bool MIX = false, bool AFF = false>
+template <int ITEM, bool SWAP, int NT, bool LMR = false, bool MIX = false, bool AFF = false, bool SPL = false>
 __global__ __launch_bounds__(NT) void k_decode_ilw(const DecodeParams p) {
     constexpr int KW = 2048 / NT;  // blocks per lane
     constexpr int QW = NT / 256;   // 4 KiB sub-steps per row of lanes
@@ -2395,7 +2415,10 @@ __global__ __launch_bounds__(NT) void k_decode_ilw(const DecodeParams p) {
             for (int w = 0; w < NT / 64; ++w) x ^= s_red[0][w];
             const uint32_t V = __builtin_amdgcn_readfirstlane(x);
             stamp(p, g, t, 4);
-            publish_il(p, c, r, wpc, V, __builtin_amdgcn_readfirstlane(stored), t, kPubLine / 2u);
+            if (SPL && wpc > 16u && wpc <= 32u)  // (tuning arm 49)
+                publish_il_split(p, c, r, wpc, V, __builtin_amdgcn_readfirstlane(stored), t);
+            else
+                publish_il(p, c, r, wpc, V, __builtin_amdgcn_readfirstlane(stored), t, kPubLine / 2u);
         }
         if (r == 0) unit_status_pair(p, U, true, t);
     }
@@ -2413,6 +2436,7 @@ KernelFn select_ilw_kernel(int item, bool swap, int nt, bool lmr, bool aff) {  /
 #define ZHIP_ILW(I, W)                                                                         \
     (nt == 1024 ? (lmr ? k_decode_ilw<I, W, 1024, true> : k_decode_ilw<I, W, 1024>)            \
      : nt == 513 ? k_decode_ilw<I, W, 512, false, true>                                         \
+     : nt == 515 ? k_decode_ilw<I, W, 512, false, false, true, true>                            \
      : lmr       ? k_decode_ilw<I, W, 512, true>                                                \
      : aff       ? k_decode_ilw<I, W, 512, false, false, true>                                  \
                  : k_decode_ilw<I, W, 512>)

@@ -461,50 +461,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
 // Production for transposed layouts with a CRC since round 4: C3 28.9 vs
 // 30.3-30.6 us graph-timed (profiles/r04/k/arms_c3.jsonl); ZHIP_TUNE_ARM 5
 // (or 1 / 2, its publication arms) takes k_decode_tile4.
-// Arrival of one workgroup of a grouped tile kernel (k_decode_tileg /
-// k_encode_tileg) with its CRC contribution v and non-empty bit: 64-bit words
-// CRC (low 32) | arrival bits (32..47) | non-empty bits (48..63), one relaxed
-// XOR per level.  Up to 16 groups per chunk the chunk word is the only level;
-// up to 256 the groups first meet in words of 16 (the workspace tail after the
-// 4 words per chunk), whose completing arrival carries the subgroup's XOR on
-// to the chunk word.  True for the arrival completing the chunk, with the
-// XOR of every contribution and whether any group was non-empty.
-// SPR: every subword and the chunk's word on a 128-byte line of its own
-// (chunk lines at ws + 32 c, subword lines after all chunk lines;
-// zhip_plan_info sizes the workspace for it), so a chunk's arrivals do not
-// meet on one line: production for k_decode_tilegw's two-tile form -- C3 in
-// 128^3 chunks, 256 arrivals per chunk, 28.94 / 29.00 vs 29.57 / 29.28 us
-// graph-timed (profiles/r05/aa/; tuning arm 48 keeps the packed words); in
-// k_encode_tileg (128 arrivals per chunk) neutral, tuning arm 47.
-template <bool SPR = false>
-__device__ __forceinline__ bool tileg_arrive(uint32_t* ws, uint32_t n_chunks, uint32_t c, uint32_t grp,
-                                             uint32_t gpc, uint32_t n_sub, uint32_t v, bool ne, uint32_t& raw,
-                                             bool& any_ne) {
-    if (n_sub) {
-        const uint32_t sg = grp >> 4;
-        const uint32_t in_sg = min(16u, gpc - (sg << 4));
-        uint64_t* sw = SPR ? reinterpret_cast<uint64_t*>(ws + 32ull * n_chunks) + ((uint64_t)c * n_sub + sg) * 16u
-                           : reinterpret_cast<uint64_t*>(ws + 4ull * n_chunks) + (uint64_t)c * n_sub + sg;
-        const uint64_t b = 1ull << (grp & 15u);
-        const uint64_t prev = __hip_atomic_fetch_xor(sw, (b << 32) | (ne ? b << 48 : 0ull) | v, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT);
-        if ((((prev >> 32) & 0xFFFFull) ^ b) != (1ull << in_sg) - 1ull) return false;
-        __hip_atomic_store(sw, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        v ^= (uint32_t)prev;
-        ne = ne || ((prev >> 48) & 0xFFFFull) != 0ull;
-        grp = sg;
-        gpc = n_sub;
-    }
-    uint64_t* cw = reinterpret_cast<uint64_t*>(ws) + (SPR ? 16ull : 2ull) * c;
-    const uint64_t b = 1ull << grp;
-    const uint64_t prev = __hip_atomic_fetch_xor(cw, (b << 32) | (ne ? b << 48 : 0ull) | v, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-    if ((((prev >> 32) & 0xFFFFull) ^ b) != (1ull << gpc) - 1ull) return false;
-    __hip_atomic_store(cw, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    raw = (uint32_t)prev ^ v;
-    any_ne = ne || ((prev >> 48) & 0xFFFFull) != 0ull;
-    return true;
-}
+// (tileg_arrive: zhip_decode_common.h)
 
 template <int N>
 struct TileMapN {
@@ -515,7 +472,10 @@ struct TileMapN {
 // 32 KiB on C3, two residency rounds instead of one; two waves per tile, lane
 // l of half h taking rows 32 h + l/16 + 4 m, m < 8: the same A_(4 sq) chain
 // over 8 blocks)
-template <int ITEM, bool SWAP, int NT = kTiles>
+// SPL (tuning arm 49): chunks of 17..32 workgroups publish through two
+// subwords of 16 on lines of their own and a second level (tileg_arrive SPR)
+// instead of 32 arrivals on the chunk's one word.
+template <int ITEM, bool SWAP, int NT = kTiles, bool SPL = false>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_decode_tile4w(
     const DecodeParams p) {
     constexpr int kPer = 16 / ITEM;
@@ -624,7 +584,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
             const uint32_t V = __builtin_amdgcn_readfirstlane(s_red[0] ^ s_red[1] ^ s_red[2] ^ s_red[3]);
             uint32_t raw = 0, last_arrival = 0;
             if (t == 0) {
-                if (gpc <= 32) {
+                if (SPL && gpc > 16u && gpc <= 32u) {
+                    bool any_ne;
+                    last_arrival = tileg_arrive<true>(p.ws, p.n_chunks, c, grp, gpc, 2u, V, false, raw, any_ne) ? 1u : 0u;
+                } else if (gpc <= 32) {
                     const uint64_t full = gpc == 32 ? 0xFFFFFFFFull : ((1ull << gpc) - 1ull);
                     const uint64_t bits = 1ull << grp;
                     uint64_t* w = reinterpret_cast<uint64_t*>(p.ws) + (uint64_t)(kPubLine / 2u) * c;
@@ -1723,7 +1686,8 @@ KernelFn select_tile4w_kernel(int item, bool swap) {  // CRC chains only
 // the tuning build adds one tile per workgroup (arm 37)
 KernelFn select_tile2w_kernel(int item, bool swap, int nt) {  // CRC chains only
 #if ZHIP_TUNING
-#define ZHIP_T2W(I, W) (nt == 1 ? k_decode_tile4w<I, W, 1> : k_decode_tile4w<I, W, 2>)
+#define ZHIP_T2W(I, W) \
+    (nt == 1 ? k_decode_tile4w<I, W, 1> : nt == 3 ? k_decode_tile4w<I, W, 2, true> : k_decode_tile4w<I, W, 2>)
 #else
     if (nt != 2) return nullptr;
 #define ZHIP_T2W(I, W) k_decode_tile4w<I, W, 2>

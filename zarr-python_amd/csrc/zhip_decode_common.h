@@ -431,4 +431,49 @@ __device__ __forceinline__ uint32_t lanemul_reg(uint32_t k, uint32_t a) {
     return (q >> 2) ^ r2(q & 3u) ^ (k & (0u - ((w >> 1) & 1u))) ^ (k1 & (0u - (w & 1u)));
 }
 
+// Arrival of one workgroup of a grouped tile kernel (k_decode_tileg /
+// k_encode_tileg) with its CRC contribution v and non-empty bit: 64-bit words
+// CRC (low 32) | arrival bits (32..47) | non-empty bits (48..63), one relaxed
+// XOR per level.  Up to 16 groups per chunk the chunk word is the only level;
+// up to 256 the groups first meet in words of 16 (the workspace tail after the
+// 4 words per chunk), whose completing arrival carries the subgroup's XOR on
+// to the chunk word.  True for the arrival completing the chunk, with the
+// XOR of every contribution and whether any group was non-empty.
+// SPR: every subword and the chunk's word on a 128-byte line of its own
+// (chunk lines at ws + 32 c, subword lines after all chunk lines;
+// zhip_plan_info sizes the workspace for it), so a chunk's arrivals do not
+// meet on one line: production for k_decode_tilegw's two-tile form -- C3 in
+// 128^3 chunks, 256 arrivals per chunk, 28.94 / 29.00 vs 29.57 / 29.28 us
+// graph-timed (profiles/r05/aa/; tuning arm 48 keeps the packed words); in
+// k_encode_tileg (128 arrivals per chunk) neutral, tuning arm 47.
+template <bool SPR = false>
+__device__ __forceinline__ bool tileg_arrive(uint32_t* ws, uint32_t n_chunks, uint32_t c, uint32_t grp,
+                                             uint32_t gpc, uint32_t n_sub, uint32_t v, bool ne, uint32_t& raw,
+                                             bool& any_ne) {
+    if (n_sub) {
+        const uint32_t sg = grp >> 4;
+        const uint32_t in_sg = min(16u, gpc - (sg << 4));
+        uint64_t* sw = SPR ? reinterpret_cast<uint64_t*>(ws + 32ull * n_chunks) + ((uint64_t)c * n_sub + sg) * 16u
+                           : reinterpret_cast<uint64_t*>(ws + 4ull * n_chunks) + (uint64_t)c * n_sub + sg;
+        const uint64_t b = 1ull << (grp & 15u);
+        const uint64_t prev = __hip_atomic_fetch_xor(sw, (b << 32) | (ne ? b << 48 : 0ull) | v, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+        if ((((prev >> 32) & 0xFFFFull) ^ b) != (1ull << in_sg) - 1ull) return false;
+        __hip_atomic_store(sw, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        v ^= (uint32_t)prev;
+        ne = ne || ((prev >> 48) & 0xFFFFull) != 0ull;
+        grp = sg;
+        gpc = n_sub;
+    }
+    uint64_t* cw = reinterpret_cast<uint64_t*>(ws) + (SPR ? 16ull : 2ull) * c;
+    const uint64_t b = 1ull << grp;
+    const uint64_t prev = __hip_atomic_fetch_xor(cw, (b << 32) | (ne ? b << 48 : 0ull) | v, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+    if ((((prev >> 32) & 0xFFFFull) ^ b) != (1ull << gpc) - 1ull) return false;
+    __hip_atomic_store(cw, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    raw = (uint32_t)prev ^ v;
+    any_ne = ne || ((prev >> 48) & 0xFFFFull) != 0ull;
+    return true;
+}
+
 }  // namespace zhip
