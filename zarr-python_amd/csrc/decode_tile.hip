@@ -1555,15 +1555,17 @@ using EncodeFn = void (*)(const EncodeParams);
 
 EncodeFn select_encode_tileg_kernel(bool crc, int item, bool swap, int nt) {
 #if ZHIP_TUNING
-    if (nt == 6) {  // arm 47: four tiles, arrival words on lines of their own (CRC layouts)
+    if (nt == 6 || nt == 7) {  // arms 47 / 50: four / two tiles, arrival words on lines of their own
         if (!crc) return nullptr;
+#define ZHIP_ETG(I, W) (nt == 6 ? k_encode_tileg<true, I, W, 4, true> : k_encode_tileg<true, I, W, 2, true>)
         switch (item) {
-            case 1: return k_encode_tileg<true, 1, false, 4, true>;
-            case 2: return swap ? k_encode_tileg<true, 2, true, 4, true> : k_encode_tileg<true, 2, false, 4, true>;
-            case 4: return swap ? k_encode_tileg<true, 4, true, 4, true> : k_encode_tileg<true, 4, false, 4, true>;
-            case 8: return swap ? k_encode_tileg<true, 8, true, 4, true> : k_encode_tileg<true, 8, false, 4, true>;
+            case 1: return ZHIP_ETG(1, false);
+            case 2: return swap ? ZHIP_ETG(2, true) : ZHIP_ETG(2, false);
+            case 4: return swap ? ZHIP_ETG(4, true) : ZHIP_ETG(4, false);
+            case 8: return swap ? ZHIP_ETG(8, true) : ZHIP_ETG(8, false);
             default: return nullptr;
         }
+#undef ZHIP_ETG
     }
 #endif
     if (nt == 2) {  // CRC layouts only
