@@ -34,7 +34,9 @@ def main():
             "c2": ([], (64, 64, 64), "rows"),
             # 16 KiB chunks (the reference example's chunk size): k_encode_quad, arm 11 k_encode_pair
             "q16": ([], (1, 64, 64), "rows"), "q16n": ([], (1, 64, 64), "rows", False),
-            "c2n": ([], (64, 64, 64), "rows", False)}
+            "c2n": ([], (64, 64, 64), "rows", False),
+            # the transposed encodes without a CRC (what the transpose alone costs)
+            "c3_64n": (tr, (64, 64, 64), "tile4", False), "c3_128n": (tr, (128, 128, 128), "tile", False)}
     # ARMS: comma list of config[:arm] (arm = zhip_set_tuning(ARM), e.g. c2:1);
     # NOCHECK: the same items for ablation arms whose output is not a valid store
     for item in os.environ.get("ARMS", "c3_64,c3_128").split(","):
