@@ -846,6 +846,8 @@ int zhip_plan_info(const zhip_plan* p, uint32_t* units_per_chunk, uint32_t* work
     // (tuning arm 49: k_decode_il / k_decode_ilw / two-tile k_decode_tile4w publish
     // through two subwords on lines of their own)
     if (ZHIP_TUNING && (p->layout.flags & ZHIP_LF_CRC) && (p->il_S || p->tile4)) w = std::max(w, 3u * kPubLine);
+    // (tuning arm 39, tile pairs past 32 workgroups per chunk: spread subwords)
+    if (wpc2 > 32u && wpc2 <= 256u) w = std::max(w, kPubLine * (1u + (wpc2 + 15u) / 16u));
     if (workspace_words) *workspace_words = w;
     return ZHIP_OK;
 }

@@ -598,9 +598,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
                         raw = (uint32_t)prev ^ V;
                         last_arrival = 1;
                     }
-                } else if (gpc <= 256u) {  // subwords of 16 workgroups (tile pairs of large chunks)
+                } else if (gpc <= 256u) {  // subwords of 16 workgroups (tile pairs of large chunks;
+                    // two tiles: on lines of their own, as k_decode_tilegw's two-tile form)
                     bool any_ne;
-                    last_arrival = tileg_arrive(p.ws, p.n_chunks, c, grp, gpc, (gpc + 15u) / 16u, V, false, raw,
+                    last_arrival = tileg_arrive<NT == 2>(p.ws, p.n_chunks, c, grp, gpc, (gpc + 15u) / 16u, V, false, raw,
                                                 any_ne) ? 1u : 0u;
                 } else {  // more than 256 workgroups per chunk: xor, then count arrivals
                     uint32_t* accw = p.ws + 4ull * c;
