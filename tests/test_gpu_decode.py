@@ -1335,9 +1335,11 @@ def test_row_map_arm_exact_and_crc(device, arm, case):
 
 
 @pytest.mark.tuning
-def test_il_split_publication_arm(device):
-    """Tuning arm 49 on k_decode_il (1 024 units, whole-chunk reads): the
-    split publication decodes exactly and reports a corrupted chunk."""
+@pytest.mark.parametrize("arm", [49, 51, 52, 53, 54, 55, 56])
+def test_il_split_publication_arm(device, arm):
+    """Tuning arms on k_decode_il (1 024 units, whole-chunk reads): 49, the
+    split publication, and 51-53, wave priority at the run end / load issue /
+    both, decode exactly and report a corrupted chunk."""
     import zarr_hip
     from zarr_hip import _native as N
 
@@ -1346,7 +1348,7 @@ def test_il_split_publication_arm(device):
     meta = O.ArrayMeta(shape, cshape, np.dtype("float32"), 0, codecs=codecs)
     host = {}
     O.write(host, meta, (Ellipsis,), _data(shape, "float32"))
-    set_tuning(6, 49)
+    set_tuning(6, arm)
     try:
         arr = zarr_hip.Array.create(zarr_hip.DeviceStore.from_host(host, device), shape, cshape, "float32", 0,
                                     codecs=codecs)

@@ -1325,11 +1325,19 @@ __device__ __forceinline__ void publish_il_split(const DecodeParams& p, uint32_t
 //   map (aff_rowblk) in scalar registers instead of K scalar loads of the map:
 //   graph-timed 26.06 vs 26.38 us on the headline, SALU instructions 3.61 M ->
 //   2.80 M per launch (profiles/r05/w/).
+// PRIO (tuning arms 51-53): wave issue priority (s_setprio 3) -- bit 0: from
+//   the run end on (a finishing workgroup frees its CU slot sooner), bit 1:
+//   until the data loads are issued (a starting workgroup's loads go out ahead
+//   of its neighbours' Horner steps), bit 2: until the tables are in LDS
+//   (production for the AFF launches: graph-timed 25.78-25.98 vs 25.97-26.09
+//   us median in four interleaved pairs, profiles/r05/ag/; arm 56 keeps 0);
+//   0 = the other instantiations.
 template <bool CRC, int ITEM, bool SWAP, bool LEAN = false, bool CF = false, int LM = 0, bool TUNE = false,
-          int PUB = 3, bool AFF = false>
+          int PUB = 3, bool AFF = false, int PRIO = 0>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(LM == 2 ? 6 : 4, LM == 2 ? 6 : 4)))
 void k_decode_il(const DecodeParams p) {
     constexpr int K = kDefaultBlocks;
+    if constexpr ((PRIO & 6) != 0) __builtin_amdgcn_s_setprio(3);
     __shared__ uint32_t s_tab[CRC ? kPairTabWords : 1];
     __shared__ uint32_t s_mul[CRC && LM == 0 ? 12 * kThreads : 1];
     __shared__ uint32_t s_red[2][kThreads / 64];
@@ -1460,6 +1468,7 @@ void k_decode_il(const DecodeParams p) {
     }
     if constexpr (TUNE) stamp(p, g, t, 1);
     }
+    if constexpr ((PRIO & 2) != 0) __builtin_amdgcn_s_setprio(0);
     const uint32_t S = p.il_S, wpc = p.nseg;
     // destinations of the K steps (scalar loads, consumed at the stores)
     zhip_rowblk m[K];
@@ -1486,6 +1495,7 @@ void k_decode_il(const DecodeParams p) {
         stt[t + 5 * kThreads] = tv5;
         if constexpr (LM == 0) lanemul3_init(s_mul, t, kl);
         __syncthreads();
+        if constexpr ((PRIO & 4) != 0) __builtin_amdgcn_s_setprio(0);
         if constexpr (TUNE) stamp(p, g, t, 2);
     }
     if (has) {
@@ -1510,6 +1520,7 @@ void k_decode_il(const DecodeParams p) {
             }
         }
         // 4. run end: one chain per workgroup, one publication
+        if constexpr ((PRIO & 1) != 0) __builtin_amdgcn_s_setprio(3);
         if constexpr (TUNE) stamp(p, g, t, 3);
         if constexpr (CRC) {
             uint32_t v = ok ? ((TUNE && (p.tune & kTuneNoRunEnd)) ? acc.a0 ^ acc.a1 ^ acc.a2 ^ acc.a3  // timing arm
@@ -1560,6 +1571,12 @@ KernelFn select_il_kernel_arm(bool crc, int item, bool swap, int arm) {  // ZHIP
         case 1: return k_decode_il<true, 4, false, false, false, 0, false, 0>;  // round 3: words 16 B apart
         case 2: return k_decode_il<true, 4, false, false, false, 0, false, 2>;  // deferred verdicts
         case 49: return k_decode_il<true, 4, false, false, false, 0, false, 4, true>;  // split publication (AFF)
+        case 51: return k_decode_il<true, 4, false, false, false, 0, false, 3, true, 1>;  // priority: run end (AFF)
+        case 52: return k_decode_il<true, 4, false, false, false, 0, false, 3, true, 2>;  // priority: load issue (AFF)
+        case 53: return k_decode_il<true, 4, false, false, false, 0, false, 3, true, 3>;  // priority: both (AFF)
+        case 54: return k_decode_il<true, 4, false, false, false, 0, false, 3, true, 4>;  // priority: to the tables (AFF; production)
+        case 56: return k_decode_il<true, 4, false, false, false, 0, false, 3, true, 0>;  // no priority (AFF; round-5 production)
+        case 55: return k_decode_il<true, 4, false, false, false, 0, false, 3, true, 5>;  // 54 + run end (AFF)
         default: return k_decode_il<true, 4, false>;  // arms of other kernels: production
     }
 }
@@ -1608,7 +1625,7 @@ KernelFn select_il_kernel_regmul(bool crc, int item, bool swap, bool occ6) {  //
 #endif
 
 KernelFn select_il_kernel(bool crc, int item, bool swap, bool aff) {  // aff: ZHIP_DF_WHOLE (CRC chains)
-#define ZHIP_IL(I, W) (aff ? k_decode_il<true, I, W, false, false, 0, false, 3, true> : k_decode_il<true, I, W>)
+#define ZHIP_IL(I, W) (aff ? k_decode_il<true, I, W, false, false, 0, false, 3, true, 4> : k_decode_il<true, I, W>)
     switch (item) {
         case 1: return crc ? ZHIP_IL(1, false) : k_decode_il<false, 1, false>;
         case 2: return crc ? (swap ? ZHIP_IL(2, true) : ZHIP_IL(2, false))
