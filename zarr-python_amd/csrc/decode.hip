@@ -708,7 +708,7 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
         if (il) {
 #if ZHIP_TUNING
             // (arms 1 / 2 are k_decode_il's own; every other arm keeps production here)
-            KernelFn ifn = (g_tune_arm == 1 || g_tune_arm == 2 || ((g_tune_arm == 49 || (g_tune_arm >= 51 && g_tune_arm <= 56)) && p.aff_ok))
+            KernelFn ifn = (g_tune_arm == 1 || g_tune_arm == 2 || ((g_tune_arm == 49 || (g_tune_arm >= 51 && g_tune_arm <= 57)) && p.aff_ok))
                                ? select_il_kernel_arm(crc, p.g.itemsize, swap, g_tune_arm)
                            : (tune & kTuneCfLookup) ? select_il_kernel_cf(crc, p.g.itemsize, swap)
                            : (tune & kTuneIlLean) ? select_il_kernel_lean(crc, p.g.itemsize, swap)
