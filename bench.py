@@ -1079,6 +1079,167 @@ def cpu_baseline(data_np, shape, chunks, shards, budget_s=12.0):
                               "cores": 1, "sample": f"{n1} full decodes in {n1 * dt1:.1f}s"}}
 
 
+def _pool_rate(fn, tasks, nbytes, budget_s, cores):
+    """Time full passes of fn over tasks on a thread pool of min(cores, tasks)
+    workers and of 1 worker (FusedCodecPipeline.read_sync's per-item pool map,
+    codec_pipeline.py:1095-1172, at the pool size _resolve_max_workers gives on
+    this box's share and single-threaded); returns the port's line."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    res = {}
+    for label, workers, share in (("w", min(cores, len(tasks)), 0.6), ("w1", 1, 0.4)):
+        with ThreadPoolExecutor(max_workers=workers) as pool:
+            list(pool.map(fn, tasks))  # warm-up
+            n, t0 = 0, time.perf_counter()
+            while True:
+                list(pool.map(fn, tasks))
+                n += 1
+                if time.perf_counter() - t0 > budget_s * share:
+                    break
+            dt = (time.perf_counter() - t0) / n
+        res[label] = (workers, dt, n)
+    (w, dt, n), (_, dt1, n1) = res["w"], res["w1"]
+    return {"value": round(nbytes / dt / GIB, 3), "unit": "GiB/s", "cores": w, "kind": "port",
+            "passes": n, "single_worker": {"value": round(nbytes / dt1 / GIB, 3), "unit": "GiB/s", "cores": 1,
+                                           "passes": n1}}
+
+
+def cpu_config_ports(budget_s=4.0) -> dict:
+    """The CPU restatement (oracle port, test infrastructure) of the reference's
+    read path for every BASELINE config line beside the headline, timed on this
+    host at 1 worker and at the box's share of cores -- reported baselines, not
+    targets.  Each reads a bounded sample of its config's workload and says
+    which:
+
+    * c2_unsharded_256 / c3_transpose_210: the whole 256^3 f32 array, one pool
+      task per 1 MiB chunk: CRC-32C verify (SSE4.2, as google_crc32c;
+      crc32c_.py:34-50) -> bytes view (bytes.py:97-120) -> [TransposeCodec
+      decode: the (2,1,0) permutation, transpose.py:113-118] -> scatter
+      (chunk_utils.py:88-214);
+    * c4_sharded_1024: 32 of its 512 shards (a 512 x 512 x 256 region, 128^3
+      shards of 32^3 inner chunks), one task per shard: index CRC, then every
+      inner chunk's CRC and scatter (sharding.py:1222-1309);
+    * c5_partial_2048: 16 of its 512 shards (512 x 512 x 1024 int16, 256^3
+      shards of 64^3 inner chunks) with ceil(10 %) of their inner chunks drawn
+      as bench c5 draws them (workloads.partial_selection, seed 1), one task per
+      selected inner chunk as the GPU batch has it: the shard index by suffix
+      read + its CRC, the inner chunk's byte range + CRC, scatter."""
+    from oracle import oracle as O
+
+    lib = O._load_lib()
+    cores = box_cores()
+
+    def crc_ok(u8):
+        return np.uint32(lib.oracle_crc32c(u8.ctypes.data, u8.size - 4)).tobytes() == u8[-4:].tobytes()
+
+    def crc_blob(a):
+        return np.frombuffer(bytes(O.crc32c_encode(np.ascontiguousarray(a).view(np.uint8).reshape(-1))), np.uint8)
+
+    out = {}
+    # c2 / c3: unsharded 64^3 chunks of the 256^3 array
+    shape, chunks = (256, 256, 256), (64, 64, 64)
+    data = W.synthetic(shape, seed=0)
+    grid = list(np.ndindex(*[s // c for s, c in zip(shape, chunks)]))
+    sls = {c: tuple(slice(i * k, (i + 1) * k) for i, k in zip(c, chunks)) for c in grid}
+    for name, perm in (("c2_unsharded_256", None), ("c3_transpose_210", (2, 1, 0))):
+        store = {c: crc_blob(data[sls[c]] if perm is None else data[sls[c]].transpose(perm)) for c in grid}
+        res = np.empty(shape, np.float32)
+
+        def read_chunk(c, store=store, res=res, perm=perm):
+            raw = store[c]
+            if not crc_ok(raw):
+                raise ValueError("checksum")
+            a = raw[:-4].view(np.float32)
+            res[sls[c]] = a.reshape(chunks) if perm is None else a.reshape(tuple(chunks[p] for p in perm)).transpose(perm)
+
+        line = _pool_rate(read_chunk, grid, data.nbytes, budget_s, cores)
+        assert res.tobytes() == data.tobytes()
+        line["sample"] = f"the whole 256^3 f32 array: 64 chunks of 64^3 (+crc){'' if perm is None else ', transpose (2,1,0)'}"
+        out[name] = line
+    del data
+    # c4: 32 shards of 128^3 (32^3 inner chunks, bytes + crc32c, index at end)
+    out["c4_sharded_1024"] = _sharded_port(lib, crc_ok, crc_blob, (512, 512, 256), (128, 128, 128),
+                                           (32, 32, 32), np.float32, None, budget_s, cores)
+    out["c4_sharded_1024"]["sample"] = ("32 of the 512 shards (512 x 512 x 256 f32, 128^3 shards of 32^3 "
+                                        "inner chunks + crc), one task per shard")
+    # c5: 16 shards of 256^3 int16, the 10 % inner-chunk selection
+    out["c5_partial_2048"] = _sharded_port(lib, crc_ok, crc_blob, (512, 512, 1024), (256, 256, 256),
+                                           (64, 64, 64), np.int16, 0.1, budget_s, cores)
+    out["c5_partial_2048"]["sample"] = ("16 of the 512 shards (512 x 512 x 1024 int16, 256^3 shards of 64^3 "
+                                        "inner chunks + crc), 10 % of their inner chunks (seed 1), one task "
+                                        "per selected inner chunk: index suffix + CRC, chunk range + CRC")
+    return out
+
+
+def _sharded_port(lib, crc_ok, crc_blob, shape, shards, inner, dtype, frac, budget_s, cores):
+    """_decode_partial_sync restated (sharding.py:1222-1309) over a sample
+    region: frac None = every inner chunk of each shard per task (one task per
+    shard), else one task per selected inner chunk."""
+    rng = np.random.default_rng(0)
+    if np.dtype(dtype).kind == "f":
+        data = rng.standard_normal(shape, dtype=np.float32)
+    else:
+        data = rng.integers(-2 ** 15, 2 ** 15, shape, dtype=np.int16)
+    cps = tuple(s // c for s, c in zip(shards, inner))
+    n_inner = int(np.prod(cps))
+    isz = n_inner * 16 + 4
+    sgrid = list(np.ndindex(*[s // c for s, c in zip(shape, shards)]))
+    store = {}
+    for sc in sgrid:
+        shard = data[tuple(slice(i * k, (i + 1) * k) for i, k in zip(sc, shards))]
+        parts, index, top = [], [], 0
+        for ic in np.ndindex(*cps):
+            enc = crc_blob(shard[tuple(slice(i * k, (i + 1) * k) for i, k in zip(ic, inner))])
+            index.append((top, enc.size))
+            parts.append(enc.tobytes())
+            top += enc.size
+        idx = np.array(index, "<u8").reshape(-1).view(np.uint8)
+        store[sc] = np.frombuffer(b"".join(parts) + crc_blob(idx).tobytes(), np.uint8)
+    res = np.zeros(shape, dtype)
+
+    def index_of(blob):
+        ib = blob[-isz:]
+        if not crc_ok(ib):
+            raise ValueError("index checksum")
+        return ib[:-4].view("<u8").reshape(n_inner, 2)
+
+    def put(blob, idx, sc, ic):
+        slot = int(np.ravel_multi_index(ic, cps))
+        o, n = int(idx[slot, 0]), int(idx[slot, 1])
+        raw = blob[o:o + n]
+        if not crc_ok(raw):
+            raise ValueError("checksum")
+        reg = tuple(slice(s * k + i * c, s * k + (i + 1) * c) for s, k, i, c in zip(sc, shards, ic, inner))
+        res[reg] = raw[:-4].view(dtype).reshape(inner)
+
+    if frac is None:
+        def task(sc):
+            blob = store[sc]
+            idx = index_of(blob)
+            for ic in np.ndindex(*cps):
+                put(blob, idx, sc, ic)
+        tasks, nbytes = sgrid, data.nbytes
+    else:
+        igrid = tuple(s // c for s, c in zip(shape, inner))
+        coords = W.partial_selection(igrid, frac, 1)
+
+        def task(co):
+            sc = tuple(int(c) // k for c, k in zip(co, cps))
+            ic = tuple(int(c) % k for c, k in zip(co, cps))
+            blob = store[sc]
+            put(blob, index_of(blob), sc, ic)
+        tasks = [tuple(c) for c in coords]
+        nbytes = len(tasks) * int(np.prod(inner)) * np.dtype(dtype).itemsize
+    line = _pool_rate(task, tasks, nbytes, budget_s, cores)
+    if frac is None:
+        assert res.tobytes() == data.tobytes()
+    else:
+        for co in tasks[:8]:
+            reg = tuple(slice(c * k, (c + 1) * k) for c, k in zip(co, inner))
+            assert res[reg].tobytes() == data[reg].tobytes()
+    return line
+
+
 def lib_sha16() -> str | None:
     """sha256[:16] of the kernel library this process loads."""
     import hashlib
@@ -1214,6 +1375,10 @@ def main():
     ap.add_argument("--eager", action="store_true",
                     help="time one host launch per step instead of a hipGraph replay")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--extra-only", action="store_true",
+                    help="profiling runs (rocprofv3 per config line): the extra configs only, no headline")
+    ap.add_argument("--extra-cpu", default="cpu",
+                    help="'cpu': time the CPU port of every config line too (N=1, rank 0); '' to skip")
     ap.add_argument("--extra", default="c1,c2,c3,c4,c5,enc,e2e,call,cpp",
                     help="extra configs (subset of c1,c2,c3,c4,c5,enc,e2e,call,cpp, or ''); c4/c5 run "
                          "partitioned at every N, the others at N=1")
@@ -1234,8 +1399,13 @@ def main():
 
         if not N.tuning_build():
             raise SystemExit("--tune needs the tuning build (make -C zarr-python_amd tune; "
-                             "ZHIP_LIB=zarr-python_amd/zarr_hip/_lib/libzarrhip_tune.so)")
+                             "ZARR_HIP_ALLOW_LIB_OVERRIDE=1 ZHIP_LIB=zarr-python_amd/zarr_hip/_lib/libzarrhip_tune.so)")
         N.check(N.lib().zhip_set_tuning(2, args.tune), "zhip_set_tuning")
+    if args.extra_only:  # rocprofv3 runs of the config lines (profiles/r06/final/)
+        res = {"extra": extra_configs(ctx, args), "lib_sha16": lib_sha16(), "steps": args.steps}
+        if ctx.rank == 0:
+            print(json.dumps(res), flush=True)
+        return
     log(f"[bench] building {args.replicas} replicas of the headline batch on {device} "
         f"(rank {ctx.rank} of {ctx.world})")
     plist, decoded, encoded = headline(ctx, args, weak=True)
@@ -1324,6 +1494,11 @@ def main():
         g = W.HEADLINE
         res["cpu_baseline"] = cpu_baseline(synthetic(g["shape"], seed=0), g["shape"], g["inner"],
                                            g["shards"], args.cpu_budget)
+        if args.extra and "cpu" in args.extra_cpu:
+            log("[bench] cpu ports of the config lines")
+            for name, port in cpu_config_ports(args.cpu_budget / 3).items():
+                if name in res.get("extra", {}):
+                    res["extra"][name]["cpu_port"] = port
     if ctx.rank == 0:
         print(json.dumps(res), flush=True)
     if ctx.distributed:

@@ -196,7 +196,10 @@ int zhip_plan_kernel_flags(const zhip_plan *plan, uint32_t *flags);
                                  row map is two-level affine in the step (zhip_plan_info
                                  reports it), the row kernels then compute each step's
                                  destination instead of loading it from the map; the map
-                                 is still required and used otherwise */
+                                 is still required and used otherwise.  The statement is
+                                 checked, not trusted: each workgroup reads its chunk's
+                                 selection record and keeps the map for any selection that
+                                 is not whole, so a wrong flag costs speed, never placement */
 
 /* Deferred CRC verdicts (opt-in: ZHIP_DF_DEFER).  With the flag,
  * k_decode_tileg / k_decode_tilegw (the transposing decodes of chunks

@@ -18,6 +18,7 @@ output is compared with the source (the graph must decode exactly)."""
 import json
 import os
 # kernel arms and knobs exist only in the tuning build (make -C zarr-python_amd tune)
+os.environ.setdefault("ZARR_HIP_ALLOW_LIB_OVERRIDE", "1")
 os.environ.setdefault("ZHIP_LIB", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                                "zarr-python_amd", "zarr_hip", "_lib", "libzarrhip_tune.so"))
 import sys

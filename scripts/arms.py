@@ -31,6 +31,7 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "zarr-python_amd"))
 
 if os.environ.get("KARM"):  # kernel arms exist only in the tuning build
+    os.environ.setdefault("ZARR_HIP_ALLOW_LIB_OVERRIDE", "1")
     os.environ.setdefault("ZHIP_LIB", os.path.join(ROOT, "zarr-python_amd", "zarr_hip", "_lib", "libzarrhip_tune.so"))
 
 import bench  # noqa: E402

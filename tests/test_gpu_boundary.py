@@ -246,6 +246,25 @@ def test_decode_encode_64_chunks_one_launch(device, codecs):
     assert eb2[0].to_bytes() == eb and eb2[1].to_bytes() == enc[2].to_bytes()
 
 
+def test_decode_encode_keep_each_items_prototype(device):
+    """Specs that differ only in prototype (a host prototype and none: this
+    package's device buffers) share one decode / encode group, yet each result
+    comes back as ITS item's buffer type (advisor round 5: the group's first
+    spec used to wrap every result)."""
+    from zarr_hip.buffer import Buffer, NDBuffer
+
+    meta, spec, pipe = _setup((16, 16), (16, 16), [LE, CRC])
+    spec_dev = Z.ArraySpec((16, 16), Z.ZDType("float32"), np.float32(0), Z.ArrayConfig(), None)
+    a, b = _data((16, 16), seed=1), _data((16, 16), seed=2)
+    enc = pipe.encode_sync([(NDBuffer(a), spec), (NDBuffer(b), spec_dev)])
+    assert isinstance(enc[0], Z.Buffer) and isinstance(enc[1], Buffer)
+    assert enc[0].to_bytes() == bytes(O.chain_encode(a, O.Chain.from_json([LE, CRC]), meta.spec()))
+    dec = pipe.decode_sync([(enc[0], spec_dev), (enc[1], spec)])
+    assert isinstance(dec[0], NDBuffer) and isinstance(dec[1], Z.NDBuffer)
+    assert dec[0].as_numpy_array().tobytes() == a.tobytes()
+    assert dec[1].as_numpy_array().tobytes() == b.tobytes()
+
+
 def test_rocm_buffer_prototype(device):
     from zarr_hip.buffer import Buffer, NDBuffer, buffer_prototype
 

@@ -904,10 +904,11 @@ def _il_array(device, fill=0.0, kind="il"):
 
 # (kind, ZHIP_TUNE_ARM): k_decode_il's returning publication (arm 33 keeps
 # k_decode_il on this small grid), its deferred-verdict arm, the small-grid
-# production k_decode_ilw512, and the deferred verdicts of k_decode_tilegw
+# production k_decode_ilh (look-back finalizer) and the round-5 one
+# k_decode_ilw512 (arm 61), and the deferred verdicts of k_decode_tilegw
 # (production: its two-tile form k_decode_tileg2w; arm 38 keeps four tiles)
 # (production) and k_decode_tileg (arm 5)
-VERDICT_CASES = [("il", 33), ("il", 2), ("ilw512", 0), ("tileg2w", 0), ("tilegw", 38), ("tileg", 5)]
+VERDICT_CASES = [("il", 33), ("il", 2), ("ilh", 0), ("ilw512", 61), ("tileg2w", 0), ("tilegw", 38), ("tileg", 5)]
 
 
 @pytest.fixture
@@ -1019,9 +1020,9 @@ def test_deferred_verdict_host_slabs(device):
 @pytest.mark.parametrize("sharded", [False, True])
 def test_il_and_small_grid_kernels(device, sharded):
     """Production kernel choice for the headline's 1 MiB chunks: k_decode_il
-    above kIlwMaxUnits (512) units, k_decode_ilw512 (512 lanes per unit) at
-    or below; both bit-exact, a corrupted chunk reported with the reference's
-    message."""
+    above kIlwMaxUnits (512) units, k_decode_ilh (16 KiB half units, the
+    look-back finalizer) at or below; both bit-exact, a corrupted chunk
+    reported with the reference's message."""
     import zarr_hip
     from zarr_hip import _native as N
 
@@ -1033,7 +1034,7 @@ def test_il_and_small_grid_kernels(device, sharded):
     O.write(host, meta, (Ellipsis,), _data(shape, "float32"))
     store = zarr_hip.DeviceStore.from_host(host, device)
     arr = zarr_hip.Array.create(store, shape, cshape, "float32", 0.0, codecs=codecs)
-    for sel, kernel in [((Ellipsis,), "k_decode_il"), ((slice(None), slice(None), slice(0, 128)), "k_decode_ilw512")]:
+    for sel, kernel in [((Ellipsis,), "k_decode_il"), ((slice(None), slice(None), slice(0, 128)), "k_decode_ilh")]:
         prog, out = arr.prepare_read(sel)
         prog.launch()
         prog.results()
@@ -1262,13 +1263,15 @@ ILW_CASES = [  # (shape, chunks, inner chunks or None, dtype, endian)
 
 
 @pytest.mark.tuning
+@pytest.mark.parametrize("arm", [41, 59, 60])
 @pytest.mark.parametrize("case", [0, 1, 3])
-def test_ilh_arm_exact_and_crc(device, case):
-    """k_decode_ilh (ZHIP_TUNE_ARM 41: 16 KiB per workgroup, the pair tables'
-    A_4096 chain, two-level arrival past 32 workgroups per chunk) decodes
-    exactly and reports corrupted chunks and indexes with the reference's
-    messages."""
-    _ilw_case(device, 41, case)
+def test_ilh_arm_exact_and_crc(device, arm, case):
+    """k_decode_ilh (16 KiB per workgroup, the pair tables' A_4096 chain):
+    ZHIP_TUNE_ARM 41 with the returning two-level arrival past 32 workgroups
+    per chunk, 59 with the look-back finalizer (two words of arrivals), 60 the
+    production form (look-back, AFF destinations for whole reads) -- exact,
+    corrupted chunks and indexes reported with the reference's messages."""
+    _ilw_case(device, arm, case)
 
 
 @pytest.mark.tuning
@@ -1284,14 +1287,14 @@ def test_ilw_arms_exact_and_crc(device, arm, case):
 
 @pytest.mark.parametrize("shape,cshape,inner,dtype,endian,kname,affine", [
     ((256, 256, 128), (64, 64, 64), None, "float32", LE, "k_decode_il", True),                 # 1 024 units
-    ((128, 128, 64), (128, 128, 64), (64, 64, 64), "float32", LE, "k_decode_ilw512", True),    # sharded
-    ((64, 128, 128), (32, 64, 64), None, "int16", BE, "k_decode_ilw512", True),                # 128-byte rows
+    ((128, 128, 64), (128, 128, 64), (64, 64, 64), "float32", LE, "k_decode_ilh", True),       # sharded
+    ((64, 128, 128), (32, 64, 64), None, "int16", BE, "k_decode_ilh", True),                   # 128-byte rows
     # three 4 KiB steps per z plane: no power-of-two split, the launch keeps the map
-    ((128, 96, 64), (64, 48, 64), None, "float32", LE, "k_decode_ilw512", False),
+    ((128, 96, 64), (64, 48, 64), None, "float32", LE, "k_decode_ilh", False),
 ])
 def test_whole_chunk_reads_compute_destinations(device, shape, cshape, inner, dtype, endian, kname, affine):
     """Whole-chunk reads launch with ZHIP_DF_WHOLE: k_decode_il /
-    k_decode_ilw512 take each step's destination from the plan's affine form
+    k_decode_ilh take each step's destination from the plan's affine form
     of the whole-chunk row map, not from the map -- exact with the map zeroed
     on the device (a map-driven launch would write nothing); a layout whose
     map has no two-level affine form keeps the map under the same flag; a
@@ -1323,8 +1326,51 @@ def test_whole_chunk_reads_compute_destinations(device, shape, cshape, inner, dt
     assert out.cpu().numpy().tobytes() == np.ascontiguousarray(O.read(host, meta, win)).tobytes()
 
 
+@pytest.mark.parametrize("win,kname", [
+    ((slice(5, 60), slice(3, 64), slice(0, 64)), "k_decode_ilh"),             # one chunk, partial
+    ((slice(5, 250), slice(3, 256), slice(0, 128)), "k_decode_il"),           # 32 chunks, edges partial
+    ((slice(0, 256), slice(0, 256), slice(0, 128, 2)), "k_decode_il"),        # every chunk, strided
+])
+def test_df_whole_is_checked_not_trusted(device, win, kname):
+    """ZHIP_DF_WHOLE set by a C caller on PARTIAL selections (the flag the
+    Python path sets only for whole-chunk reads): the kernels read each
+    chunk's selection record and keep the row map wherever it is not whole,
+    so the read stays exact and nothing is written outside the selection --
+    the out sits between two 1 MiB guard bands of a sentinel that must come
+    back untouched (advisor round 5; chunk_utils.py:88-214 semantics)."""
+    import torch
+
+    import zarr_hip
+    from zarr_hip import _native as N
+
+    shape, cshape = (256, 256, 128), (64, 64, 64)
+    codecs = [LE, CRC]
+    meta = O.ArrayMeta(shape, cshape, np.dtype("float32"), 3, codecs=codecs)
+    host = {}
+    O.write(host, meta, (Ellipsis,), _data(shape, "float32"))
+    arr = zarr_hip.Array.create(zarr_hip.DeviceStore.from_host(host, device), shape, cshape, "float32", 3,
+                                codecs=codecs)
+    prog, out = arr.prepare_read(win)
+    if prog.data.p_rowmap is None:
+        pytest.skip("this window does not take the row-map launch")
+    assert not prog.data.flags & N.DF_WHOLE
+    guard = (1 << 20) // 4
+    big = torch.full((out.numel() + 2 * guard,), -7.25, dtype=torch.float32, device=device)
+    view = big[guard: guard + out.numel()].view(out.shape)
+    assert view.is_contiguous() and out.is_contiguous()
+    prog.retarget(view)
+    prog.data.flags |= N.DF_WHOLE  # the false promise
+    prog.launch()
+    prog.results()
+    assert N.lib().zhip_last_kernel().decode() == kname
+    want = np.ascontiguousarray(O.read(host, meta, win))
+    assert view.cpu().numpy().tobytes() == want.tobytes()
+    g = big.cpu().numpy()
+    assert (g[:guard] == -7.25).all() and (g[guard + out.numel():] == -7.25).all()
+
+
 @pytest.mark.tuning
-@pytest.mark.parametrize("arm", [45, 49])
+@pytest.mark.parametrize("arm", [45, 49, 61])
 @pytest.mark.parametrize("case", [0, 1])
 def test_row_map_arm_exact_and_crc(device, arm, case):
     """Tuning arm 45 keeps the row-map loads for whole-chunk launches (the A/B
@@ -1335,7 +1381,7 @@ def test_row_map_arm_exact_and_crc(device, arm, case):
 
 
 @pytest.mark.tuning
-@pytest.mark.parametrize("arm", [49, 51, 52, 53, 54, 55, 56, 57])
+@pytest.mark.parametrize("arm", [49, 51, 52, 53, 54, 55, 56, 57, 58])
 def test_il_split_publication_arm(device, arm):
     """Tuning arms on k_decode_il (1 024 units, whole-chunk reads): 49, the
     split publication, and 51-53, wave priority at the run end / load issue /
@@ -1368,6 +1414,77 @@ def test_il_split_publication_arm(device, arm):
         set_tuning(6, 0)
 
 
+LB_CASES = {  # arm -> (shape, kernel, positions per chunk, byte offset of position p in a chunk)
+    # k_decode_il: workgroup r takes steps 64 (r / 8) + r % 8 + 8 k (S = 8)
+    58: ((256, 256, 128), "k_decode_il", 32, lambda p: 4096 * (64 * (p // 8) + p % 8) + 2000),
+    # k_decode_ilw512 (the N = 8 share's shape): unit r takes steps 8 r .. 8 r + 7
+    "58w": ((128, 128, 128), "k_decode_ilw512", 32, lambda p: 4096 * 8 * p + 2000),
+    # k_decode_ilh: half unit u takes steps 8 (u / 2) + 4 (u % 2) .. + 3
+    59: ((256, 256, 128), "k_decode_ilh", 64, lambda p: 4096 * 4 * p + 2000),
+}
+
+
+@pytest.mark.tuning
+@pytest.mark.parametrize("case", [58, "58w", 59])
+def test_lookback_finalizer_every_position(device, case):
+    """The look-back finalizer (tuning arms 58 / 59: every workgroup but the
+    chunk's last publishes by a non-returning xor and retires, the last one
+    polls and compares): a corrupted byte in EACH workgroup position of a chunk
+    -- the finalizer's own and every non-finalizer's -- sets that chunk's
+    CRC_MISMATCH status and the error word and raises the reference's message
+    (crc32c_.py:34-50), while the other chunks stay OK; the restored bytes then
+    read exactly (the self-resetting words hold nothing stale)."""
+    import zarr_hip
+    from zarr_hip import _native as N
+    from zarr_hip.pipeline import STATUS_DT
+
+    arm = 58 if case == "58w" else case
+    shape, kname, npos, off = LB_CASES[case]
+    cshape = (64, 64, 64)
+    codecs = [LE, CRC]
+    meta = O.ArrayMeta(shape, cshape, np.dtype("float32"), 0, codecs=codecs)
+    host = {}
+    O.write(host, meta, (Ellipsis,), _data(shape, "float32"))
+    keys = sorted(k for k in host if k.startswith("c/"))
+    nc = len(keys)
+    set_tuning(6, arm)
+    try:
+        store = zarr_hip.DeviceStore.from_host(host, device)
+        arr = zarr_hip.Array.create(store, shape, cshape, "float32", 0, codecs=codecs)
+        prog, out = arr.prepare_read((Ellipsis,))
+        prog.launch()
+        prog.results()
+        assert N.lib().zhip_last_kernel().decode() == kname
+        assert out.cpu().numpy().tobytes() == O.read(host, meta).tobytes()
+        d = prog.data
+        assert d.n == nc
+        for rnd in range((npos + nc - 1) // nc):
+            hit = {}
+            for i, key in enumerate(keys):
+                p = rnd * nc + i
+                if p < npos:
+                    _corrupt(store, host, key, at=off(p))
+                    hit[key] = p
+            with pytest.raises(ValueError) as want:
+                O.read(host, meta)
+            d.reset_errflag()
+            prog.launch()
+            st = d.d_status[: d.n * 4].cpu().numpy().view(STATUS_DT)
+            assert d.errflag() & (1 << N.ST_CRC_MISMATCH)
+            assert (st["code"] == N.ST_CRC_MISMATCH).sum() == len(hit), (rnd, sorted(hit.values()))
+            with pytest.raises(ValueError) as got:
+                prog.results()
+            assert str(got.value) == str(want.value)
+            for key, p in hit.items():
+                _corrupt(store, host, key, at=off(p))
+            for _ in range(2):
+                prog.launch()
+                prog.results()
+            assert out.cpu().numpy().tobytes() == O.read(host, meta).tobytes()
+    finally:
+        set_tuning(6, 0)
+
+
 def _ilw_case(device, arm, case, whole=False):
     import zarr_hip
     from zarr_hip import _native as N
@@ -1381,7 +1498,7 @@ def _ilw_case(device, arm, case, whole=False):
         host.pop("c/1/0/0")
     want_kernel = {26: "k_decode_ilw1024", 27: "k_decode_ilw512", 31: "k_decode_ilw1024r", 32: "k_decode_ilw512r",
                    41: "k_decode_ilh", 42: "k_decode_ilw512m", 45: "k_decode_ilw512",
-                   49: "k_decode_ilw512"}[arm]
+                   49: "k_decode_ilw512", 59: "k_decode_ilh", 60: "k_decode_ilh", 61: "k_decode_ilw512"}[arm]
     set_tuning(6, arm)
     try:
         store = zarr_hip.DeviceStore.from_host(host, device)

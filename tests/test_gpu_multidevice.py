@@ -65,6 +65,35 @@ def test_device_group_matches_oracle(device, kind, sharded, n_dev):
         assert into.cpu().numpy().tobytes() == want.tobytes()
 
 
+@pytest.mark.parametrize("keep", [lambda j: j % 3 != 1, lambda j: j < 5, lambda j: j >= 12])
+def test_gather_partial_batch_keeps_unselected_regions(device, keep):
+    """gather of a batch that does not tile the devices' bands (a subset of
+    the chunks) into a pre-filled `into`: only the items' regions change, the
+    rest keeps its sentinel (the per-device outs hold garbage there: a band
+    copy would overwrite it -- advisor round 5)."""
+    import torch
+
+    from zarr_hip.parallel import DeviceGroup
+
+    shape = (128, 96, 64)
+    arr, host, meta = _arr(device, "device", shape, (32, 32, 32), [LE, CRC])
+    batch, out_shape = arr.batch_info((Ellipsis,))
+    sub = [it for j, it in enumerate(batch) if keep(j)]
+    want = np.full(out_shape, -5.0, np.float32)
+    full = O.read(host, meta)
+    for it in sub:
+        osel = tuple(it[3])
+        want[osel] = full[osel]
+    for n_dev in (2, 3):
+        grp = DeviceGroup([0] * n_dev)
+        prog = grp.prepare_read(arr.codec_pipeline, sub, out_shape, "float32")
+        prog.launch()
+        prog.results()
+        into = torch.full(out_shape, -5.0, dtype=torch.float32, device=device)
+        prog.gather(sub, into)
+        assert into.cpu().numpy().tobytes() == want.tobytes()
+
+
 def test_device_group_crc_error_surfaces(device):
     """A corrupted chunk on any device raises the reference's message."""
     import zarr_hip

@@ -181,3 +181,44 @@ def test_read_sync_with_zarr_per_chunk_specs(device):
         csel, osel, comp) for co, csel, osel, comp in rows]
     pipe.write_sync(wb, torch.from_numpy(data).to(device))
     assert {k: bytes(v) for k, v in store2.to_dict().items()} == host
+
+
+@pytest.mark.parametrize("codecs", [[LE, CRC], [BE]])
+def test_many_distinct_edges_one_synchronisation(codecs, device):
+    """A 1-D rectilinear grid of 64 distinct edge lengths (1, 2, ..., 64: an
+    RLE-free [[1, 2, 3, ...]] grid, chunk_grids.py:167-293) read whole and
+    strided into a device out: 64 spec groups, one plan and one launch each,
+    launched back to back, and ONE host synchronisation for the whole batch
+    (pipeline.SYNCS); bit-exact with the oracle.  A corrupted chunk still
+    raises the reference's message from that single readback."""
+    import zarr_hip
+    from zarr_hip import pipeline as P
+
+    edges = list(range(1, 65))
+    n = sum(edges)
+    store = zarr_hip.DeviceStore(device)
+    arr = zarr_hip.Array.create(store, (n,), (edges,), "float32", -2.0, codecs=codecs)
+    data = _data((n,), "float32")
+    arr[...] = data
+    meta = O.ArrayMeta((n,), (edges,), np.dtype("float32"), -2.0, codecs=codecs)
+    host = _check(arr, store, meta, data, [])
+    for sel in [(Ellipsis,), (slice(3, n - 5, 3),), (slice(100, 900),)]:
+        groups = len({id(it[1]) for it in arr.batch_info(sel)[0]})
+        assert groups == 64 or sel != (Ellipsis,)
+        arr.get(sel)  # warm: plans and pooled buffers exist
+        l0, s0 = P.LAUNCHES[0], P.SYNCS[0]
+        got = arr.get(sel)
+        assert P.SYNCS[0] - s0 == 1, (sel, P.SYNCS[0] - s0)
+        assert P.LAUNCHES[0] - l0 == groups
+        want = np.ascontiguousarray(O.read(host, meta, sel))
+        assert got.cpu().numpy().tobytes() == want.tobytes()
+    if CRC in codecs:
+        bad = bytearray(host["c/40"])
+        bad[17] ^= 0x04
+        host["c/40"] = bytes(bad)
+        store.set_sync("c/40", bytes(bad))
+        with pytest.raises(ValueError) as want:
+            O.read(host, meta)
+        with pytest.raises(ValueError) as got:
+            arr.get((Ellipsis,))
+        assert str(got.value) == str(want.value)

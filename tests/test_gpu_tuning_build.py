@@ -40,7 +40,7 @@ def test_tuning_arms_in_tuning_build(device):
     logdir = os.path.join(ROOT, "gpurun_out")
     os.makedirs(logdir, exist_ok=True)
     log = os.path.join(logdir, "tuning_tests.log")
-    env = dict(os.environ, ZHIP_LIB=lib)
+    env = dict(os.environ, ZHIP_LIB=lib, ZARR_HIP_ALLOW_LIB_OVERRIDE="1")
     with open(log, "w") as fh:  # streamed to a file: progress stays visible
         r = subprocess.run([sys.executable, "-u", "-m", "pytest", "tests", "-m", "gpu and tuning", "-x", "-v",
                             "-p", "no:cacheprovider", "--timeout", "300", "--timeout-method", "thread"],

@@ -209,3 +209,17 @@ def test_oracle_rectilinear_roundtrip():
     assert len(store["c/0/0"]) == 10 * 50 * 8 + 4
     np.testing.assert_array_equal(O.read(store, meta), data)
     np.testing.assert_array_equal(O.read(store, meta, (slice(5, 66, 3), slice(40, 60))), data[5:66:3, 40:60])
+
+
+def test_array_chunks_raises_for_rectilinear():
+    """Array.chunks is defined for regular grids only; a rectilinear grid
+    raises NotImplementedError (src/zarr/core/array.py:849-862), where it
+    used to return the internal placeholder (1,) * ndim (advisor round 5)."""
+    import zarr_hip
+
+    store = zarr_hip.MemoryStore()
+    arr = zarr_hip.Array.create(store, (30, 30), ([10, 20], [20, 10]), "float32", 0.0)
+    with pytest.raises(NotImplementedError):
+        arr.chunks
+    reg = zarr_hip.Array.create(zarr_hip.MemoryStore(), (30, 30), (10, 10), "float32", 0.0)
+    assert reg.chunks == (10, 10)

@@ -13,6 +13,7 @@ import pytest
 from oracle import oracle as O
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "zarr-python_amd")
 
 
 def _header_functions():
@@ -249,3 +250,55 @@ def test_emulated_xw_crc_matches_oracle(n):
     L.flags = N.LF_CRC
     plan = N.Plan(L, upload=False)
     assert plan.emulate_chunk_crc(data, pair="xw") == O.crc32c(data)
+
+
+def _import_native(env_extra):
+    """Import zarr_hip._native (and load the library) in a fresh interpreter
+    with `env_extra` added; returns (returncode, stderr)."""
+    import subprocess
+    import sys
+
+    env = {k: v for k, v in os.environ.items() if k not in ("ZHIP_LIB", "ZARR_HIP_ALLOW_LIB_OVERRIDE")}
+    env.update(env_extra)
+    code = ("import sys; sys.path.insert(0, %r); from zarr_hip import _native as N; "
+            "N.lib(); print('tuning', N.tuning_build())" % PKG)
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    return r.returncode, r.stdout + r.stderr
+
+
+def test_lib_override_needs_explicit_opt_in():
+    """ZHIP_LIB alone (a stray variable in a user's environment) raises at
+    import instead of swapping the shipped library for the tuning build; with
+    ZARR_HIP_ALLOW_LIB_OVERRIDE=1 the named library loads."""
+    from zarr_hip import _native as N
+
+    if not os.path.exists(N.TUNING_LIB_PATH):
+        pytest.skip("tuning build absent (make -C zarr-python_amd tune)")
+    rc, out = _import_native({"ZHIP_LIB": N.TUNING_LIB_PATH})
+    assert rc != 0 and "ZARR_HIP_ALLOW_LIB_OVERRIDE" in out and "ImportError" in out, out
+    rc, out = _import_native({"ZHIP_LIB": N.TUNING_LIB_PATH, "ZARR_HIP_ALLOW_LIB_OVERRIDE": "1"})
+    assert rc == 0 and "tuning True" in out, out
+    rc, out = _import_native({})
+    assert rc == 0 and "tuning False" in out, out
+
+
+def test_tuning_build_refused_in_product_path(tmp_path):
+    """A tuning build loaded through the opt-in path check alone is still
+    refused when the opt-in is absent: copied over (or symlinked as) the
+    product name, lib() raises NativeError."""
+    import shutil
+
+    from zarr_hip import _native as N
+
+    if not os.path.exists(N.TUNING_LIB_PATH):
+        pytest.skip("tuning build absent (make -C zarr-python_amd tune)")
+    pkg = tmp_path / "zarr_hip"
+    shutil.copytree(os.path.join(PKG, "zarr_hip"), pkg, ignore=shutil.ignore_patterns("*.so", "__pycache__"))
+    shutil.copy(N.TUNING_LIB_PATH, pkg / "_lib" / "libzarrhip.so")
+    import subprocess
+    import sys
+
+    env = {k: v for k, v in os.environ.items() if k not in ("ZHIP_LIB", "ZARR_HIP_ALLOW_LIB_OVERRIDE")}
+    code = "import sys; sys.path.insert(0, %r); from zarr_hip import _native as N; N.lib()" % str(tmp_path)
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and "tuning build" in r.stderr, r.stderr

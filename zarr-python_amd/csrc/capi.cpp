@@ -368,7 +368,7 @@ int zhip_plan_upload(zhip_plan* p) {
                      p->nseg <= 256u;
     size_t n_ilw[2] = {0, 0};
     for (int i = ZHIP_TUNING ? 0 : 1; i < 2 && ilw; ++i) n_ilw[i] = kPairTabWords + (size_t)p->nseg * (1024u >> i) + kThreads;
-    const size_t n_ilh = (ZHIP_TUNING && p->il_S == 8u && 2 * p->nseg <= 64u) ? (size_t)2 * p->nseg * kThreads : 0;
+    const size_t n_ilh = (ilw && p->il_S == 8u && 2 * p->nseg <= 64u) ? (size_t)2 * p->nseg * kThreads : 0;
     std::vector<uint32_t> h(n_old + n_pair + n_il + n_xw + n_ilw[0] + n_ilw[1] + n_ilh);
     build_horner(h.data());
     for (int t = 0; t < kThreads; ++t) h[4096 + t] = xpow8((uint64_t)kWgStride - 16u * t);
@@ -475,7 +475,7 @@ int zhip_plan_upload(zhip_plan* p) {
                 gf_mul(h[n_old + kPairTabWords + (size_t)p->nseg * kThreads + t], back);
         at += n_ilw[i];
     }
-    // k_decode_ilh (tuning arm 41): lane t of half unit u = 2 r + h takes the
+    // k_decode_ilh (small launches; tuning arm 41): lane t of half unit u = 2 r + h takes the
     // sub-steps 8 r + 4 h + k (k < 4) at 16 t through A_4096; the constant
     // x^(8 (4096 (n_steps - st0 - 3) - 16 t)) c_inv x^(-96), st0 = 8 r + 4 h
     p->off_ilh = 0;

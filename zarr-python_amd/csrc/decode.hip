@@ -495,6 +495,7 @@ KernelFn select_pair_kernel(bool crc, int item, bool swap, int nu);  // decode_r
 KernelFn select_duo_kernel(bool crc, int item, bool swap);           // decode_rows.hip
 KernelFn select_il_kernel(bool crc, int item, bool swap, bool aff);  // decode_rows.hip
 KernelFn select_ilw_kernel(int item, bool swap, int nt, bool lmr, bool aff);  // decode_rows.hip
+KernelFn select_ilh_kernel(int item, bool swap, bool lb, bool aff);  // decode_rows.hip
 #if ZHIP_TUNING
 KernelFn select_il_kernel_lean(bool crc, int item, bool swap);       // decode_rows.hip
 KernelFn select_il_kernel_tuned(bool crc, int item, bool swap);      // decode_rows.hip
@@ -505,7 +506,6 @@ KernelFn select_xw_kernel(bool crc, int item, bool swap);            // decode_r
 KernelFn select_ilq_kernel(int item, bool swap, int nq, bool glds);  // decode_rows.hip
 KernelFn select_ilc_kernel(int item, bool swap);                     // decode_rows.hip
 KernelFn select_ilp_kernel(int item, bool swap);                     // decode_rows.hip
-KernelFn select_ilh_kernel(int item, bool swap);                     // decode_rows.hip
 KernelFn select_tile4f_kernel(int item, bool swap);                  // decode_tile.hip
 #endif
 KernelFn select_tile4_kernel(bool crc, int item, bool swap);         // decode_tile.hip
@@ -546,6 +546,10 @@ __global__ __launch_bounds__(kThreads) void k_probe(const DecodeParams p) {
 
 
 int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
+    // the look-back finalizer (publish_lb) waits only while fewer chunks than
+    // CUs are in the launch (max_grid arrives as CUs * 8)
+    const bool lb_ok = p.n_chunks < (uint32_t)(max_grid / 8);
+    (void)lb_ok;
     if (g_tune_max_grid > 0) max_grid = g_tune_max_grid;
     // the ablation bits: a compile-time 0 outside the tuning build
     const uint32_t tune = ZHIP_TUNING ? p.tune : 0u;
@@ -643,8 +647,9 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
             hipLaunchKernelGGL(wfn, dim3(wgrid), dim3(p.ilw_nt), 0, stream, p);
             return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
         }
-        if (il && g_tune_arm == 41 && p.ilh_klane) {  // k_decode_ilh: 16 KiB per workgroup
-            KernelFn hfn = select_ilh_kernel(p.g.itemsize, swap);
+        if (il && (g_tune_arm == 41 || g_tune_arm == 59) && p.ilh_klane) {  // k_decode_ilh: 16 KiB per workgroup
+            // (59: with the look-back finalizer, at most 64 half units per chunk)
+            KernelFn hfn = select_ilh_kernel(p.g.itemsize, swap, g_tune_arm == 59 && lb_ok && p.nseg <= 32u, false);
             if (!hfn) return ZHIP_E_UNSUPPORTED;
             const uint32_t hunits = 2u * p.n_units;
             const uint32_t hgrid = hunits > p.n_idx ? hunits : p.n_idx;
@@ -690,14 +695,33 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
         }
 #endif
         // grids of at most kIlwMaxUnits units (2 per CU: the N = 4 / 8 shares of
-        // the strong-scaled headline): 512 lanes per unit, four blocks per lane
-        // (k_decode_ilw, decode_rows.hip) -- graph-timed 8.8 vs 9.4 us at the
-        // N = 8 share, 10.3 vs 11.0 at N = 4; 14.6 vs 16.5 for k_decode_il at
-        // N = 2 (profiles/r05/f/).  (Tuning build: any arm keeps k_decode_il.)
+        // the strong-scaled headline) with fewer chunks than CUs: half units of
+        // 16 KiB (k_decode_ilh, two workgroups per unit) publishing through the
+        // look-back finalizer -- graph-timed 8.39 vs 9.77 us (k_decode_ilw512)
+        // at the N = 8 share, 10.73 vs 11.03 at N = 4 (profiles/r06/a/).
+        // (Tuning build: arm 0 only; arm 58 / 49 keep k_decode_ilw512.)
+        if (il && p.ilh_klane && p.n_units <= kIlwMaxUnits && lb_ok && p.nseg <= 32u &&
+            (g_tune_arm == 0 || g_tune_arm == 60) && (tune & ~kTuneStamp) == 0) {
+            KernelFn hfn = select_ilh_kernel(p.g.itemsize, swap, true, p.aff_ok != 0);
+            if (!hfn) return ZHIP_E_UNSUPPORTED;
+            const uint32_t hunits = 2u * p.n_units;
+            const uint32_t hgrid = hunits > p.n_idx ? hunits : p.n_idx;
+            if (hgrid == 0) return ZHIP_OK;
+            g_last_kernel = "k_decode_ilh";
+            hipLaunchKernelGGL(hfn, dim3(hgrid), dim3(kThreads), 0, stream, p);
+            return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
+        }
+        // otherwise 512 lanes per unit, four blocks per lane (k_decode_ilw,
+        // decode_rows.hip) -- graph-timed 8.8 vs 9.4 us at the N = 8 share, 10.3
+        // vs 11.0 at N = 4; 14.6 vs 16.5 for k_decode_il at N = 2
+        // (profiles/r05/f/).  (Tuning build: any arm keeps k_decode_il.)
         if (il && p.ilw_nt == 512u && p.n_units <= kIlwMaxUnits &&
-            (g_tune_arm == 0 || g_tune_arm == 45 || (g_tune_arm == 49 && p.aff_ok)) && (tune & ~kTuneStamp) == 0) {
-            // (tuning arm 49: the split publication, whole-chunk reads)
-            KernelFn wfn = select_ilw_kernel(p.g.itemsize, swap, g_tune_arm == 49 ? 515 : 512, false, p.aff_ok != 0);
+            (g_tune_arm == 0 || g_tune_arm == 45 || g_tune_arm == 61 || ((g_tune_arm == 49 || g_tune_arm == 58) && p.aff_ok)) &&
+            (tune & ~kTuneStamp) == 0) {
+            // (tuning arms, whole-chunk reads: 49 the split publication, 58 the
+            // look-back finalizer)
+            const int nt = g_tune_arm == 49 ? 515 : (g_tune_arm == 58 && lb_ok && p.nseg <= 64u) ? 516 : 512;
+            KernelFn wfn = select_ilw_kernel(p.g.itemsize, swap, nt, false, p.aff_ok != 0);
             if (!wfn) return ZHIP_E_UNSUPPORTED;
             const uint32_t wgrid = p.n_units > p.n_idx ? p.n_units : p.n_idx;
             if (wgrid == 0) return ZHIP_OK;
@@ -708,7 +732,10 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
         if (il) {
 #if ZHIP_TUNING
             // (arms 1 / 2 are k_decode_il's own; every other arm keeps production here)
-            KernelFn ifn = (g_tune_arm == 1 || g_tune_arm == 2 || ((g_tune_arm == 49 || (g_tune_arm >= 51 && g_tune_arm <= 57)) && p.aff_ok))
+            // (58: the look-back finalizer, while fewer chunks than CUs)
+            KernelFn ifn = (g_tune_arm == 1 || g_tune_arm == 2 ||
+                            ((g_tune_arm == 49 || (g_tune_arm >= 51 && g_tune_arm <= 57) ||
+                              (g_tune_arm == 58 && lb_ok && p.nseg <= 32u)) && p.aff_ok))
                                ? select_il_kernel_arm(crc, p.g.itemsize, swap, g_tune_arm)
                            : (tune & kTuneCfLookup) ? select_il_kernel_cf(crc, p.g.itemsize, swap)
                            : (tune & kTuneIlLean) ? select_il_kernel_lean(crc, p.g.itemsize, swap)

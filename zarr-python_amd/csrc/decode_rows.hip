@@ -1293,6 +1293,52 @@ __device__ __forceinline__ void publish_il_split(const DecodeParams& p, uint32_t
     if (__builtin_amdgcn_readfirstlane(last)) finalize_uniform(p, c, stored, __builtin_amdgcn_readfirstlane(raw), t, true);
 }
 
+// publish_lb: the look-back finalizer (round 6; PUB = 5, at most 64
+// workgroups per chunk).  Workgroups r < wpc - 1 publish (bit r << 32) | V
+// with a NON-returning agent-scope xor into word r / 32 of the chunk's line
+// and retire at once; the chunk's highest-index workgroup r = wpc - 1 polls
+// the words (one lane, relaxed agent loads, s_sleep between polls) until every
+// other arrival bit is set, resets them and finalizes.  Forward progress: the
+// only waiting workgroups are the finalizers, one per chunk, and they wait
+// only on workgroups that never wait; the host takes this form only when
+// n_chunks < CUs (launch_decode), so the finalizers can never hold every
+// resident slot whatever the dispatch order.  (CPU-side protocol checks:
+// tests/test_gpu_decode.py, a corrupted unit in every position.)
+__device__ __forceinline__ void publish_lb(const DecodeParams& p, uint32_t c, uint32_t r, uint32_t wpc, uint32_t V,
+                                           uint32_t stored, int t, uint32_t wstride) {
+    uint64_t* const w = reinterpret_cast<uint64_t*>(p.ws) + (uint64_t)wstride * c;
+    if (r + 1u < wpc) {
+        if (t == 0)
+            (void)__hip_atomic_fetch_xor(w + (r >> 5), ((1ull << (r & 31u)) << 32) | V, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
+    // arrival bits expected in word 0 / word 1 (the finalizer's own excluded)
+    const uint32_t n0 = wpc < 32u ? wpc : 32u, n1 = wpc - n0;
+    const uint32_t e0 = n1 ? 0xFFFFFFFFu : (uint32_t)((1ull << (n0 - 1u)) - 1ull);
+    const uint32_t e1 = n1 ? (uint32_t)((1ull << (n1 - 1u)) - 1ull) : 0u;
+    uint32_t lo = 0;
+    if (t == 0) {
+        uint64_t a = 0, b = 0;
+        for (;;) {
+            a = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((uint32_t)(a >> 32) == e0) break;
+            __builtin_amdgcn_s_sleep(1);
+        }
+        if (n1) {
+            for (;;) {
+                b = __hip_atomic_load(w + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if ((uint32_t)(b >> 32) == e1) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+            __hip_atomic_store(w + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __hip_atomic_store(w, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        lo = (uint32_t)a ^ (uint32_t)b;
+    }
+    finalize_uniform(p, c, stored, __builtin_amdgcn_readfirstlane(lo) ^ V, t, true);
+}
+
 // LEAN (tuning arm kTuneIlLean): the PairHot batch, then tables, constants
 // and -- at the addresses the default shard packing predicts (zhip_predict) --
 // the data loads, all before the header chain (chunk record -> index entry)
@@ -1478,12 +1524,14 @@ void k_decode_il(const DecodeParams p) {
     const uint32_t S = p.il_S, wpc = p.nseg;
     // destinations of the K steps (scalar loads, consumed at the stores)
     zhip_rowblk m[K];
+    // (AFF: only for a chunk whose selection record is whole, sel_whole)
+    if (AFF && (!has || sel_whole(p, U.sel))) {
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-        const uint32_t st = st0 + S * (uint32_t)k;
-        if constexpr (AFF) {
-            m[k] = aff_rowblk(p, st);
-        } else {
+        for (int k = 0; k < K; ++k) m[k] = aff_rowblk(p, st0 + S * (uint32_t)k);
+    } else {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint32_t st = st0 + S * (uint32_t)k;
             const uint32_t sidx = p.nseg - 1u - st / (uint32_t)K;
             m[k] = load_uniform<zhip_rowblk>(p.rowmap + ((size_t)U.sel * p.nseg + sidx) * K + (st % (uint32_t)K));
         }
@@ -1543,6 +1591,8 @@ void k_decode_il(const DecodeParams p) {
                     if (t == 0) dv_publish(p, c, r == 0, V, __builtin_amdgcn_readfirstlane(stored));
                 } else if constexpr (PUB == 3) {  // the chunk's word alone in its line
                     publish_il(p, c, r, wpc, V, __builtin_amdgcn_readfirstlane(stored), t, kPubLine / 2u);
+                } else if constexpr (PUB == 5) {  // look-back finalizer (arm 58)
+                    publish_lb(p, c, r, wpc, V, __builtin_amdgcn_readfirstlane(stored), t, kPubLine / 2u);
                 } else if constexpr (PUB == 4) {  // two subwords of 16 (tuning arm 49)
                     if (wpc > 16u && wpc <= 32u)
                         publish_il_split(p, c, r, wpc, V, __builtin_amdgcn_readfirstlane(stored), t);
@@ -1584,6 +1634,7 @@ KernelFn select_il_kernel_arm(bool crc, int item, bool swap, int arm) {  // ZHIP
         case 56: return k_decode_il<true, 4, false, false, false, 0, false, 3, true, 0>;  // no priority (AFF; round-5 production)
         case 57: return k_decode_il<true, 4, false, false, false, 0, false, 3, true, 12>;  // 54 + XCD eighths (AFF)
         case 55: return k_decode_il<true, 4, false, false, false, 0, false, 3, true, 5>;  // 54 + run end (AFF)
+        case 58: return k_decode_il<true, 4, false, false, false, 0, false, 5, true, 4>;  // 54 + look-back finalizer (AFF)
         default: return k_decode_il<true, 4, false>;  // arms of other kernels: production
     }
 }
@@ -2158,13 +2209,14 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))
 }
 
 // ---------------------------------------------------------------------------
-// k_decode_ilh (tuning arm 41): half units -- 16 KiB per workgroup (4 096 on
+// k_decode_ilh (production for small launches since round 6, with LB; tuning
+// arm 41 without it): half units -- 16 KiB per workgroup (4 096 on
 // the headline: four residency rounds instead of two, the change that gave
 // the transposes 1.6 us), lane t taking the four 4 KiB sub-steps 8 r + 4 h + k
 // of its segment's half h at 16 t: one chain through the pair kernel's
 // A_4096 tables, lane constants per (half unit, lane) from capi.cpp; up to
 // 64 workgroups per chunk publish per 32-workgroup word with a second level.
-template <int ITEM, bool SWAP>
+template <int ITEM, bool SWAP, bool LB = false, bool AFF = false>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_decode_ilh(
     const DecodeParams p) {
     constexpr int KW = 4;
@@ -2206,10 +2258,15 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))
     }
     zhip_rowblk m[KW];
     const uint32_t sidx = p.nseg - 1u - r;
+    if (AFF && (!has || sel_whole(p, U.sel))) {  // (k_decode_il's AFF, checked by sel_whole)
 #pragma unroll
-    for (int k = 0; k < KW; ++k)
-        m[k] = load_uniform<zhip_rowblk>(p.rowmap + ((size_t)U.sel * p.nseg + sidx) * kDefaultBlocks + 4u * hh +
-                                         (uint32_t)k);
+        for (int k = 0; k < KW; ++k) m[k] = aff_rowblk(p, 8u * r + 4u * hh + (uint32_t)k);
+    } else {
+#pragma unroll
+        for (int k = 0; k < KW; ++k)
+            m[k] = load_uniform<zhip_rowblk>(p.rowmap + ((size_t)U.sel * p.nseg + sidx) * kDefaultBlocks +
+                                             4u * hh + (uint32_t)k);
+    }
     uint32_t stored = 0;
     if (ok) stored = load_trailer_uniform(U.cp, p.g.nbytes);
     {
@@ -2246,7 +2303,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))
         if (ok && t < 64) {
             const uint32_t V = __builtin_amdgcn_readfirstlane(s_red[0][0] ^ s_red[0][1] ^ s_red[0][2] ^ s_red[0][3]);
             const uint32_t st = __builtin_amdgcn_readfirstlane(stored);
-            if (wpc <= 32u) {
+            if (LB && wpc <= 64u) {  // look-back finalizer (tuning arm 59)
+                publish_lb(p, c, u, wpc, V, st, t, kPubLine / 2u);
+            } else if (wpc <= 32u) {
                 publish_il(p, c, u, wpc, V, st, t, kPubLine / 2u);
             } else {  // words of 32 arrivals, then the line's third word
                 uint64_t* const w = reinterpret_cast<uint64_t*>(p.ws) + (uint64_t)(kPubLine / 2u) * c;
@@ -2279,17 +2338,26 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))
     for (uint32_t j = g; j < p.n_idx; j += G) verify_index_pair(p, j, t, kix, s_tab, s_red[1], j == g, ipre);
 }
 
+// production (round 6) for launches of at most kIlwMaxUnits units while
+// fewer chunks than CUs are in flight: LB (the look-back finalizer) with the
+// AFF form for ZHIP_DF_WHOLE launches; the tuning build adds the returning
+// publication (arm 41) and LB without AFF (arm 59)
+KernelFn select_ilh_kernel(int item, bool swap, bool lb, bool aff) {  // CRC chains only
 #if ZHIP_TUNING
-KernelFn select_ilh_kernel(int item, bool swap) {  // CRC chains only
+#define ZHIP_ILH(I, W) (!lb ? k_decode_ilh<I, W> : aff ? k_decode_ilh<I, W, true, true> : k_decode_ilh<I, W, true>)
+#else
+    if (!lb) return nullptr;
+#define ZHIP_ILH(I, W) (aff ? k_decode_ilh<I, W, true, true> : k_decode_ilh<I, W, true>)
+#endif
     switch (item) {
-        case 1: return k_decode_ilh<1, false>;
-        case 2: return swap ? k_decode_ilh<2, true> : k_decode_ilh<2, false>;
-        case 4: return swap ? k_decode_ilh<4, true> : k_decode_ilh<4, false>;
-        case 8: return swap ? k_decode_ilh<8, true> : k_decode_ilh<8, false>;
+        case 1: return ZHIP_ILH(1, false);
+        case 2: return swap ? ZHIP_ILH(2, true) : ZHIP_ILH(2, false);
+        case 4: return swap ? ZHIP_ILH(4, true) : ZHIP_ILH(4, false);
+        case 8: return swap ? ZHIP_ILH(8, true) : ZHIP_ILH(8, false);
         default: return nullptr;
     }
+#undef ZHIP_ILH
 }
-#endif
 
 // ---------------------------------------------------------------------------
 // k_decode_ilw: small shares (below ~2 workgroups per CU: the N = 4 / 8 shares
@@ -2328,7 +2396,8 @@ __device__ __forceinline__ uint32_t lanemul3_w(const uint32_t* s_mul, int t, uin
 // column: the run end's LDS reads halve.  MIX (tuning arm 42): the waves of
 // the second 256 lanes multiply in registers, the first through the LDS
 // column, so the run end's lookups and VALU work overlap.
-template <int ITEM, bool SWAP, int NT, bool LMR = false, bool MIX = false, bool AFF = false, bool SPL = false>
+template <int ITEM, bool SWAP, int NT, bool LMR = false, bool MIX = false, bool AFF = false, bool SPL = false,
+          bool LB = false>
 __global__ __launch_bounds__(NT) void k_decode_ilw(const DecodeParams p) {
     constexpr int KW = 2048 / NT;  // blocks per lane
     constexpr int QW = NT / 256;   // 4 KiB sub-steps per row of lanes
@@ -2380,14 +2449,14 @@ __global__ __launch_bounds__(NT) void k_decode_ilw(const DecodeParams p) {
     stamp(p, g, t, 1);
     zhip_rowblk m[KW];
     const uint32_t sidx = p.nseg - 1u - r;
+    if (AFF && (!has || sel_whole(p, U.sel))) {  // (k_decode_il's AFF, checked by sel_whole)
 #pragma unroll
-    for (int k = 0; k < KW; ++k) {
-        if constexpr (AFF) {  // (k_decode_il's AFF)
-            m[k] = aff_rowblk(p, 8u * r + q + (uint32_t)(QW * k));
-        } else {
+        for (int k = 0; k < KW; ++k) m[k] = aff_rowblk(p, 8u * r + q + (uint32_t)(QW * k));
+    } else {
+#pragma unroll
+        for (int k = 0; k < KW; ++k)
             m[k] = load_uniform<zhip_rowblk>(p.rowmap + ((size_t)U.sel * p.nseg + sidx) * kDefaultBlocks + q +
                                              (uint32_t)(QW * k));
-        }
     }
     uint32_t stored = 0;
     if (ok) stored = load_trailer_uniform(U.cp, p.g.nbytes);
@@ -2441,6 +2510,8 @@ __global__ __launch_bounds__(NT) void k_decode_ilw(const DecodeParams p) {
             stamp(p, g, t, 4);
             if (SPL && wpc > 16u && wpc <= 32u)  // (tuning arm 49)
                 publish_il_split(p, c, r, wpc, V, __builtin_amdgcn_readfirstlane(stored), t);
+            else if (LB && wpc <= 64u)  // look-back finalizer (tuning arm 58)
+                publish_lb(p, c, r, wpc, V, __builtin_amdgcn_readfirstlane(stored), t, kPubLine / 2u);
             else
                 publish_il(p, c, r, wpc, V, __builtin_amdgcn_readfirstlane(stored), t, kPubLine / 2u);
         }
@@ -2461,6 +2532,7 @@ KernelFn select_ilw_kernel(int item, bool swap, int nt, bool lmr, bool aff) {  /
     (nt == 1024 ? (lmr ? k_decode_ilw<I, W, 1024, true> : k_decode_ilw<I, W, 1024>)            \
      : nt == 513 ? k_decode_ilw<I, W, 512, false, true>                                         \
      : nt == 515 ? k_decode_ilw<I, W, 512, false, false, true, true>                            \
+     : nt == 516 ? k_decode_ilw<I, W, 512, false, false, true, false, true>                     \
      : lmr       ? k_decode_ilw<I, W, 512, true>                                                \
      : aff       ? k_decode_ilw<I, W, 512, false, false, true>                                  \
                  : k_decode_ilw<I, W, 512>)

@@ -521,12 +521,13 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))
     const uint32_t st0 = (r / S) * S * (uint32_t)K + (r % S);
     const int32_t lo_frame = (int32_t)p.E - (int32_t)(p.nseg * p.seg);
     zhip_rowblk m[K];
+    if (AFF && sel_whole(p, ch.sel)) {  // (checked, not trusted: sel_whole)
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-        const uint32_t st = st0 + S * (uint32_t)k;
-        if constexpr (AFF) {
-            m[k] = aff_rowblk(p, st);
-        } else {
+        for (int k = 0; k < K; ++k) m[k] = aff_rowblk(p, st0 + S * (uint32_t)k);
+    } else {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint32_t st = st0 + S * (uint32_t)k;
             const uint32_t sidx = p.nseg - 1u - st / (uint32_t)K;
             m[k] = load_uniform<zhip_rowblk>(p.rowmap + ((size_t)ch.sel * p.nseg + sidx) * K + (st % (uint32_t)K));
         }

@@ -238,6 +238,27 @@ __device__ __forceinline__ zhip_rowblk aff_rowblk(const P& p, uint32_t st) {
     return e;
 }
 
+// ZHIP_DF_WHOLE is checked in the kernel, not trusted (round 6): the
+// selection record of the unit's chunk must be the whole chunk -- start 0,
+// count = shape, step 1 in every dimension (chunk_utils.py:88-214,
+// is_complete_chunk) -- before a launch computes destinations instead of
+// loading them from the row map.  Scalar loads (3 x 32 bytes) issued beside
+// the data loads; a C caller's partial selection under the flag falls back to
+// the map, so nothing lands outside its selection.
+template <class P>
+__device__ __forceinline__ bool sel_whole(const P& p, uint32_t sel) {
+    struct S3 {
+        int32_t v[3 * ZHIP_MAX_DIMS];
+    };
+    const S3 s = load_uniform<S3>(p.sels + sel);
+    bool w = true;
+#pragma unroll
+    for (int d = 0; d < ZHIP_MAX_DIMS; ++d)
+        if (d < p.g.ndim)
+            w = w && s.v[d] == 0 && s.v[ZHIP_MAX_DIMS + d] == p.g.shape[d] && s.v[2 * ZHIP_MAX_DIMS + d] == 1;
+    return w;
+}
+
 __device__ __forceinline__ uint32_t load_trailer(const uint8_t* cp, uint32_t n) {
     const uint8_t* tr = cp + n;
     return (uint32_t)tr[0] | ((uint32_t)tr[1] << 8) | ((uint32_t)tr[2] << 16) | ((uint32_t)tr[3] << 24);

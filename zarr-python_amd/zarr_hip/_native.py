@@ -55,11 +55,24 @@ PF_KEEP_EMPTY = 4
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # the shipped library, and the tuning build of the same sources with every
 # measurement arm and kernel knob compiled in (make -C zarr-python_amd tune;
-# scripts/armbench.py, tests/test_gpu_tuning_build.py).  ZHIP_LIB names the
-# library to load explicitly (the tuning build for measurements).
+# scripts/armbench.py, tests/test_gpu_tuning_build.py).  ZHIP_LIB names
+# another library to load, and is honoured only together with the explicit
+# opt-in ZARR_HIP_ALLOW_LIB_OVERRIDE=1 (the measurement scripts set both): a
+# stray ZHIP_LIB in a user's environment raises here instead of silently
+# swapping the kernels, and lib() refuses a tuning build without the opt-in.
 PRODUCT_LIB_PATH = os.path.join(_HERE, "_lib", "libzarrhip.so")
 TUNING_LIB_PATH = os.path.join(_HERE, "_lib", "libzarrhip_tune.so")
-LIB_PATH = os.environ.get("ZHIP_LIB") or PRODUCT_LIB_PATH
+OVERRIDE_OPT_IN = "ZARR_HIP_ALLOW_LIB_OVERRIDE"
+
+
+def _override_allowed() -> bool:
+    return os.environ.get(OVERRIDE_OPT_IN) == "1"
+
+
+if os.environ.get("ZHIP_LIB") and not _override_allowed():
+    raise ImportError(f"ZHIP_LIB={os.environ['ZHIP_LIB']!r} is set without {OVERRIDE_OPT_IN}=1: refusing to load a "
+                      "library other than the shipped libzarrhip.so (unset ZHIP_LIB, or opt in explicitly)")
+LIB_PATH = (os.environ.get("ZHIP_LIB") if _override_allowed() else None) or PRODUCT_LIB_PATH
 
 
 class FDiv(ctypes.Structure):
@@ -266,6 +279,9 @@ def lib():
     L.zhip_tuning_build.restype = ctypes.c_int
     if L.zhip_abi_version() != 1:
         raise NativeError("libzarrhip ABI version mismatch")
+    if L.zhip_tuning_build() and not _override_allowed():
+        raise NativeError(f"{LIB_PATH} is the tuning build (measurement arms compiled in): it loads only with "
+                          f"{OVERRIDE_OPT_IN}=1")
     _lib = L
     return L
 

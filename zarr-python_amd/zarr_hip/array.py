@@ -200,6 +200,12 @@ class Array:
 
     @property
     def chunks(self):
+        """The chunk shape; only defined for regular chunk grids -- a
+        rectilinear grid raises NotImplementedError, as the reference's
+        Array.chunks does (src/zarr/core/array.py:849-862, 2024-2036)."""
+        if not self.metadata.is_regular:
+            raise NotImplementedError("chunks is only defined for arrays using a regular chunk grid; "
+                                      "this array uses a rectilinear chunk grid")
         return self.metadata.chunk_shape
 
     def _key(self, coords) -> str:

@@ -177,8 +177,10 @@ class GroupProgram:
         """Copy every device's item regions into ``into`` (any device): the
         optional post-step gather, outside the decode.  A device whose items
         form bands of the out along its outermost dim that no other device's
-        items touch sends each band in ONE copy (a contiguous range of a C or
-        F out: one peer copy over xGMI); interleaved items go one region each.
+        items touch, and tile those bands completely, sends each band in ONE
+        copy (a contiguous range of a C or F out: one peer copy over xGMI);
+        otherwise its items go one region each, so regions of `into` that no
+        item selects are left alone.
         The copies run asynchronously on the receiving device's stream and
         are waited for once."""
         import torch
@@ -194,6 +196,10 @@ class GroupProgram:
             for (prog, out, idx), spans in zip(self.parts, owner):
                 if out.device == into.device and out.data_ptr() == into.data_ptr():
                     continue
+                if spans is not None:  # one copy per band only where the part's items tile it
+                    band = sum(into.narrow(dim, lo, hi - lo).numel() for lo, hi in spans)
+                    if sum(_cells(tuple(batch[j][3])) for j in idx) != band:
+                        spans = None  # (regions no item writes hold garbage in the part's out)
                 if spans is not None:
                     for lo, hi in spans:
                         into.narrow(dim, lo, hi - lo).copy_(out.narrow(dim, lo, hi - lo), non_blocking=True)

@@ -367,6 +367,7 @@ class DecodeLaunch:
         nonzero verdict word w of bank b is a mismatch with stored trailer s_b,
         computed w ^ s_b (zarrhip.h); such words are cleared, so the next
         launch starts clean."""
+        SYNCS[0] += 1
         st = self.d_status[: self.n * 4].cpu().numpy().view(STATUS_DT).copy()
         if self._ranges:  # range launches: chunk first + c's words at first * wsw + 4 c
             wsw = self.ws_words
@@ -396,9 +397,11 @@ class DecodeLaunch:
         return True
 
     def index_statuses(self) -> np.ndarray:
+        SYNCS[0] += 1
         return self.d_idx_status[: self.n_idx * 4].cpu().numpy().view(STATUS_DT)
 
     def errflag(self) -> int:
+        SYNCS[0] += 1
         return int(self.d_err[0].item())
 
     def reset_errflag(self):
@@ -456,18 +459,18 @@ class DecodeProgram:
         shards), so the GetResults are prebuilt."""
         w = getattr(self, "_err_ranges", None)
         if w is None:
-            import ctypes
+            w = self._err_ranges = _RangeSet(self.wait_ranges())
+        return self.results_from_words(w.wait(self.data.device))
 
-            rngs = [self.data.verdict_range]
-            if self.index is not None:
-                rngs.append((self.index.p_err, 4))
-            n = len(rngs)
-            host = np.zeros(sum(r[1] for r in rngs) // 4, np.uint32)
-            w = self._err_ranges = ((ctypes.c_void_p * n)(*[r[0] for r in rngs]),
-                                    (ctypes.c_uint64 * n)(*[r[1] for r in rngs]), n, host)
-        host = w[3]
-        N.check(N.lib().zhip_wait_ranges(w[0], w[1], w[2], host.ctypes.data, _stream_handle(self.data.device)),
-                "zhip_wait_ranges")
+    def wait_ranges(self) -> list:
+        """The device ranges results_fast reads back: (pointer, bytes)."""
+        rngs = [self.data.verdict_range]
+        if self.index is not None:
+            rngs.append((self.index.p_err, 4))
+        return rngs
+
+    def results_from_words(self, host: np.ndarray) -> tuple[GetResult, ...]:
+        """results_fast's verdict on the host copy of wait_ranges()."""
         nv = self.data.verdict_range[1] // 4
         err = int(host[0]) | (int(host[nv]) if self.index is not None else 0)
         dv = host[64:nv]
@@ -579,12 +582,52 @@ class ProgramGroup:
         return self._merge([p.results() for p in self.programs])
 
     def results_fast(self) -> tuple[GetResult, ...]:
-        return self._merge([p.results_fast() for p in self.programs])
+        """Every group's error word and verdict words come back in ONE
+        synchronisation (one zhip_wait_ranges over all the programs' ranges);
+        the status tables are read only for a group that reports an error."""
+        progs = self.programs
+        if not all(isinstance(p, DecodeProgram) for p in progs):
+            return self._merge([p.results_fast() for p in progs])
+        w = getattr(self, "_err_ranges", None)
+        if w is None:
+            per = [p.wait_ranges() for p in progs]
+            w = self._err_ranges = (_RangeSet([r for rs in per for r in rs]),
+                                    [sum(r[1] for r in rs) // 4 for rs in per])
+        host = w[0].wait(progs[0].data.device)
+        res, pos = [], 0
+        for p, n in zip(progs, w[1]):
+            res.append(p.results_from_words(host[pos: pos + n]))
+            pos += n
+        return self._merge(res)
 
 
 # host-side count of decode launches issued (DecodeLaunch.launch /
 # launch_range): tests check that a batch costs one launch per spec group
 LAUNCHES = [0]
+# host-side count of the read path's blocking device-to-host readbacks
+# (_RangeSet.wait, status tables, error words): tests check that a batch of
+# several spec groups costs ONE synchronisation
+SYNCS = [0]
+
+
+class _RangeSet:
+    """Device ranges (pointer, bytes) read back by ONE zhip_wait_ranges: the
+    stream's work drains, then every range lands in one host array (uint32)."""
+
+    def __init__(self, rngs: list):
+        import ctypes
+
+        n = len(rngs)
+        self.ptrs = (ctypes.c_void_p * n)(*[r[0] for r in rngs])
+        self.lens = (ctypes.c_uint64 * n)(*[r[1] for r in rngs])
+        self.n = n
+        self.host = np.zeros(sum(r[1] for r in rngs) // 4, np.uint32)
+
+    def wait(self, device) -> np.ndarray:
+        SYNCS[0] += 1
+        N.check(N.lib().zhip_wait_ranges(self.ptrs, self.lens, self.n, self.host.ctypes.data,
+                                         _stream_handle(device)), "zhip_wait_ranges")
+        return self.host
 
 
 def _dv_refs(launches: list, device):
@@ -1196,15 +1239,25 @@ class HipCodecPipeline:
         return res
 
     def _read_groups(self, batch, groups, out, drop_axes) -> tuple[GetResult, ...]:
-        """read_sync of a batch whose items carry different chunk specs: each
-        spec group is read on its own (its own plan, tables and launch) into
-        the same device out, whose regions the groups split between them; a
-        host out is copied back once, after the last group."""
+        """read_sync of a batch whose items carry different chunk specs
+        (rectilinear grids: zarr hands one spec per item, array.py:5469-5486):
+        one plan and one launch per spec group into the same device out, whose
+        regions the groups split between them, every group launched back to
+        back on one stream, then ONE synchronisation for all their error and
+        verdict words (ProgramGroup.results_fast); a host out is copied back
+        once, after the last group.  Several devices keep one read per group."""
         dev_out, host_out = _resolve_out(out, batch, drop_axes)
-        res: list = [None] * len(batch)
-        for idx in groups:
-            for i, r in zip(idx, self.read_sync([batch[i] for i in idx], dev_out, drop_axes)):
-                res[i] = r
+        if len(self.devices) > 1:
+            res: list = [None] * len(batch)
+            for idx in groups:
+                for i, r in zip(idx, self.read_sync([batch[i] for i in idx], dev_out, drop_axes)):
+                    res[i] = r
+        else:
+            prog = self.prepare_read(batch, dev_out, drop_axes, pooled=True)
+            prog.launch()
+            res = prog.results_fast()
+            if prog.clean:  # nothing raised or flagged: the pooled buffers are zero again
+                prog.release()
         if host_out is not None:
             from .buffer import copy_to_host
 
@@ -1453,9 +1506,10 @@ class HipCodecPipeline:
         items = list(chunk_bytes_and_specs)
         res: list = [None] * len(items)
         groups: dict = {}
+        own: dict = {}  # each result is wrapped with its item's own spec (prototype included)
         for i, (raw, spec) in enumerate(items):
             if raw is not None:
-                spec = coerce_spec(spec)
+                spec = own[i] = coerce_spec(spec)
                 groups.setdefault(_spec_key(spec), (spec, []))[1].append(i)
         for spec, idx in groups.values():
             raws = []
@@ -1474,7 +1528,7 @@ class HipCodecPipeline:
                 for i, raw in zip(idx, raws):
                     out = torch.empty((), dtype=torch_dtype(spec.dtype), device=dev)
                     self.read_sync([(_Raw(raw), spec, (), (), True)], out)
-                    res[i] = _as_nd_buffer(out, spec)
+                    res[i] = _as_nd_buffer(out, own[i])
                 continue
             s0 = spec.shape[0]
             out = torch.empty((len(idx) * s0,) + tuple(spec.shape[1:]), dtype=torch_dtype(spec.dtype), device=dev)
@@ -1482,7 +1536,7 @@ class HipCodecPipeline:
                      for j, raw in enumerate(raws)]
             self.read_sync(batch, out)
             for j, i in enumerate(idx):
-                res[i] = _as_nd_buffer(out[j * s0:(j + 1) * s0], spec)
+                res[i] = _as_nd_buffer(out[j * s0:(j + 1) * s0], own[i])
         return res
 
     async def decode(self, chunk_bytes_and_specs: Iterable) -> list:
@@ -1503,9 +1557,10 @@ class HipCodecPipeline:
         items = list(chunk_arrays_and_specs)
         res: list = [None] * len(items)
         groups: dict = {}
+        own: dict = {}  # each result is wrapped with its item's own spec (prototype included)
         for i, (arr, spec) in enumerate(items):
             if arr is not None:
-                spec = coerce_spec(spec)
+                spec = own[i] = coerce_spec(spec)
                 groups.setdefault(_spec_key(spec), (spec, []))[1].append(i)
         for spec, idx in groups.values():
             full = tuple(slice(0, s, 1) for s in spec.shape)
@@ -1516,7 +1571,7 @@ class HipCodecPipeline:
                 for i, v in zip(idx, vals):
                     sink = _CollectSetter()
                     self._write_sync([(sink, spec, (), (), True)], v, partial_encode=False)
-                    res[i] = None if sink.value is None else _as_buffer(sink.value, spec)
+                    res[i] = None if sink.value is None else _as_buffer(sink.value, own[i])
                 continue
             s0 = spec.shape[0]
             stacked = torch.cat([_value_tensor(v, spec.dtype, dev).reshape(spec.shape) for v in vals], 0)
@@ -1525,7 +1580,7 @@ class HipCodecPipeline:
                      for j, sink in enumerate(sinks)]
             self._write_sync(batch, stacked, partial_encode=False)
             for i, sink in zip(idx, sinks):
-                res[i] = None if sink.value is None else _as_buffer(sink.value, spec)
+                res[i] = None if sink.value is None else _as_buffer(sink.value, own[i])
         return res
 
     async def encode(self, chunk_arrays_and_specs: Iterable) -> list:
