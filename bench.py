@@ -54,7 +54,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # of this same command (scripts/gpu_pmc.sh -> scripts/pmc_summary.py); counters
 # cannot be read from inside the timed process, so the value is labelled with
 # the file it comes from
-TRAFFIC_JSON = os.path.join("profiles", "r05", "pmc_traffic.json")
+TRAFFIC_JSON = os.path.join("profiles", "r06", "pmc_traffic.json")
 LIB_SO = os.path.join("zarr-python_amd", "zarr_hip", "_lib", "libzarrhip.so")
 GIB = float(1 << 30)
 LE, CRC = W.LE, W.CRC

@@ -872,6 +872,8 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
 #if ZHIP_TUNING
         if (gw && g_tune_arm == 40 && p.tglt_kq) nt = nsel = 5;  // four tiles, lanes pick the tile
         if (nt == 2 && g_tune_arm == 48) nsel = 6;  // the arrival words packed (round-4 layout)
+        // the look-back finalizer (fewer chunks than CUs; the spread subwords)
+        if (nt == 2 && g_tune_arm == 62 && lb_ok && p.n_groups <= 128u) nsel = 7;
 #endif
         KernelFn fn = gw ? select_tilegw_kernel(p.g.itemsize, (p.lflags & ZHIP_LF_SWAP) != 0, defer, nsel)
                          : select_tileg_kernel((p.lflags & ZHIP_LF_CRC) != 0, p.g.itemsize,
@@ -883,7 +885,8 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
         DecodeParams q = p;
         if (nt == 2) q.t4w_kq = p.t2w_kq;
         if (nt == 5) q.t4w_kq = p.tglt_kq;
-        g_last_kernel = !gw ? "k_decode_tileg" : nsel == 6 ? "k_decode_tileg2wp" : nt == 2 ? "k_decode_tileg2w"
+        g_last_kernel = !gw ? "k_decode_tileg" : nsel == 6 ? "k_decode_tileg2wp" : nsel == 7 ? "k_decode_tileg2w_lb"
+                                           : nt == 2 ? "k_decode_tileg2w"
                                            : nt == 5 ? "k_decode_tileglt"
                                                                                       : "k_decode_tilegw";
         hipLaunchKernelGGL(fn, dim3((uint32_t)ggrid), dim3(kThreads), 0, stream, q);

@@ -825,7 +825,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
 // apart: 64 KiB in 128^3 chunks); the chain is the same A_(4 sq) one, the lane
 // constants swap the roles of w and l / 16, and in tile iteration j the 16
 // lanes of every wave that hold tile j write the image.
-template <int ITEM, bool SWAP, int PUB = 2, int NT = kTiles, bool LT = false, bool SPR = false>
+// LB (tuning arm 62): the returning arrival replaced by tileg_arrive_lb (the
+//   chunk's last workgroup polls, the others retire after a non-returning xor)
+template <int ITEM, bool SWAP, int PUB = 2, int NT = kTiles, bool LT = false, bool SPR = false, bool LB = false>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_decode_tilegw(
     const DecodeParams p) {
     static_assert(!LT || NT == kTiles, "lane-tile mapping: four tiles per workgroup");
@@ -948,7 +950,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
             // subgroups of 16 workgroups (the plan's n_sub for four tiles; for two,
             // zhip_plan_info sizes the workspace tail for twice as many)
             const uint32_t nsub = NT == kTiles ? p.n_sub : ((gpc > 16u && gpc <= 256u) ? (gpc + 15u) / 16u : 0u);
-            if (gpc <= 16u || nsub) {
+            if (LB && (gpc <= 16u || nsub)) {
+                bool any_ne;
+                last_one = tileg_arrive_lb(p.ws, p.n_chunks, c, wg, gpc, nsub, V, false, raw, any_ne);
+            } else if (gpc <= 16u || nsub) {
                 bool any_ne;
                 last_one = tileg_arrive<SPR>(p.ws, p.n_chunks, c, wg, gpc, nsub, V, false, raw, any_ne);
             } else {  // more than 256 groups per chunk: XOR, then count arrivals
@@ -1393,7 +1398,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
 // residency rounds; the first half's contribution shifted by p.g_z2 to the
 // group's last-tile frame that ge.ku assumes; arrival subwords for twice the
 // workgroups, zhip_plan_info)
-template <bool CRC, int ITEM, bool SWAP, int NT = kTiles, bool SPR = false>
+// LB (tuning arm 63): tileg_arrive_lb instead of the returning arrival
+template <bool CRC, int ITEM, bool SWAP, int NT = kTiles, bool SPR = false, bool LB = false>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_encode_tileg(
     const EncodeParams p) {
     constexpr int kPer = 16 / ITEM;
@@ -1521,7 +1527,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     const uint32_t nsub = NT == kTiles ? p.n_sub : ((gpc > 16u && gpc <= 256u) ? (gpc + 15u) / 16u : 0u);
     if (gpc <= 16u || nsub) {
         bool any_ne = false;
-        if (!tileg_arrive<SPR>(p.ws, p.n_chunks, c, wg, gpc, nsub, V, ne, raw, any_ne)) return;
+        if (LB) {
+            if (!tileg_arrive_lb(p.ws, p.n_chunks, c, wg, gpc, nsub, V, ne, raw, any_ne)) return;
+        } else if (!tileg_arrive<SPR>(p.ws, p.n_chunks, c, wg, gpc, nsub, V, ne, raw, any_ne)) {
+            return;
+        }
         p.nonempty[c] = any_ne ? 1u : 0u;
     } else {  // more than 256 groups per chunk: arrival count | non-empty count word
         uint32_t* accw = p.ws + 4ull * c;
@@ -1556,9 +1566,12 @@ using EncodeFn = void (*)(const EncodeParams);
 
 EncodeFn select_encode_tileg_kernel(bool crc, int item, bool swap, int nt) {
 #if ZHIP_TUNING
-    if (nt == 6 || nt == 7) {  // arms 47 / 50: four / two tiles, arrival words on lines of their own
+    if (nt == 6 || nt == 7 || nt == 8) {  // arms 47 / 50: four / two tiles, arrival words on lines of
+        // their own; arm 63 (8): four tiles, the look-back finalizer
         if (!crc) return nullptr;
-#define ZHIP_ETG(I, W) (nt == 6 ? k_encode_tileg<true, I, W, 4, true> : k_encode_tileg<true, I, W, 2, true>)
+#define ZHIP_ETG(I, W)                                                                                      \
+    (nt == 6 ? k_encode_tileg<true, I, W, 4, true> : nt == 8 ? k_encode_tileg<true, I, W, 4, true, true>    \
+             : k_encode_tileg<true, I, W, 2, true>)
         switch (item) {
             case 1: return ZHIP_ETG(1, false);
             case 2: return swap ? ZHIP_ETG(2, true) : ZHIP_ETG(2, false);
@@ -1657,6 +1670,7 @@ KernelFn select_tilegw_kernel(int item, bool swap, bool defer, int nt) {  // CRC
 #if ZHIP_TUNING
 #define ZHIP_TILEGW(I, W)                                                                          \
     (nt == 2 ? k_decode_tilegw<I, W, 0, 2, false, true>                                             \
+     : nt == 7 ? k_decode_tilegw<I, W, 0, 2, false, true, true>                                     \
      : nt == 5 ? (defer ? k_decode_tilegw<I, W, 2, 4, true> : k_decode_tilegw<I, W, 0, 4, true>)   \
      : nt == 6 ? k_decode_tilegw<I, W, 0, 2>                                                        \
              : (defer ? k_decode_tilegw<I, W, 2> : k_decode_tilegw<I, W, 0>))

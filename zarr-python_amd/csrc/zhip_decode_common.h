@@ -497,4 +497,48 @@ __device__ __forceinline__ bool tileg_arrive(uint32_t* ws, uint32_t n_chunks, ui
     return true;
 }
 
+// tileg_arrive with the look-back finalizer (round 6; tuning arms 62 / 63):
+// the subwords of 16 arrivals on lines of their own (tileg_arrive SPR's
+// layout; one word of up to 16 when n_sub is 0).  Every workgroup but the
+// chunk's last (grp = gpc - 1) xors its bit | non-empty bit | v with a
+// NON-returning atomic and returns false; the last one polls every subword
+// (one lane, relaxed agent loads) until all the other arrivals are in, resets
+// them and returns true with the chunk's raw sum and non-empty flag.  The
+// caller takes it only while fewer chunks than CUs are in the launch (the
+// finalizers then never hold every slot; publish_lb, decode_rows.hip).
+__device__ __forceinline__ bool tileg_arrive_lb(uint32_t* ws, uint32_t n_chunks, uint32_t c, uint32_t grp,
+                                                uint32_t gpc, uint32_t n_sub, uint32_t v, bool ne, uint32_t& raw,
+                                                bool& any_ne) {
+    const uint32_t nsw = n_sub ? n_sub : 1u;
+    uint64_t* const base = n_sub ? reinterpret_cast<uint64_t*>(ws + 32ull * n_chunks) + (uint64_t)c * n_sub * 16u
+                                 : reinterpret_cast<uint64_t*>(ws) + 16ull * c;
+    const uint32_t sg = n_sub ? grp >> 4 : 0u;
+    const uint64_t b = 1ull << (n_sub ? (grp & 15u) : grp);
+    if (grp + 1u < gpc) {
+        (void)__hip_atomic_fetch_xor(base + 16ull * sg, (b << 32) | (ne ? b << 48 : 0ull) | v, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+        return false;
+    }
+    uint32_t acc = v;
+    bool nn = ne;
+    for (uint32_t s = 0; s < nsw; ++s) {
+        const uint32_t in_s = n_sub ? min(16u, gpc - 16u * s) : gpc;
+        uint64_t expect = (1ull << in_s) - 1ull;
+        if (s == sg) expect ^= b;
+        uint64_t* const w = base + 16ull * s;
+        uint64_t cur;
+        for (;;) {
+            cur = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (((cur >> 32) & 0xFFFFull) == expect) break;
+            __builtin_amdgcn_s_sleep(1);
+        }
+        __hip_atomic_store(w, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        acc ^= (uint32_t)cur;
+        nn = nn || ((cur >> 48) & 0xFFFFull) != 0ull;
+    }
+    raw = acc;
+    any_ne = nn;
+    return true;
+}
+
 }  // namespace zhip
