@@ -27,11 +27,11 @@ if [ "${SKIP_PMC:-0}" != "1" ]; then
 fi
 timeout -k 10 700 python -u bench.py > "$O/bench.json" 2> "$O/bench.err"
 rc=$?; echo "bench rc=$rc"; tail -c 300 "$O/bench.json"; echo; [ $rc -ne 0 ] && { tail -20 "$O/bench.err"; exit $rc; }
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof/hl" -o hl -- python bench.py --steps 50 --extra "" \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof/hl" -o hl -- python bench.py --steps 50 --extra "" \
   --no-cpu-baseline > "$O/prof/hl.json" 2> "$O/prof/hl.err"
 rc=$?; echo "rocprof hl rc=$rc"; [ $rc -ne 0 ] && { tail -20 "$O/prof/hl.err"; exit $rc; }
 for x in ${RUNS:-c1 c2 c3 c4 c5 enc cpp}; do
-  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$O/prof/$x" -o $x -- python bench.py --extra-only \
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof/$x" -o $x -- python bench.py --extra-only \
     --extra $x --steps 20 > "$O/prof/$x.json" 2> "$O/prof/$x.err"
   rc=$?; echo "rocprof $x rc=$rc"; [ $rc -ne 0 ] && { tail -20 "$O/prof/$x.err"; exit $rc; }
 done

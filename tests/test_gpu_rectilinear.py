@@ -189,8 +189,11 @@ def test_many_distinct_edges_one_synchronisation(codecs, device):
     RLE-free [[1, 2, 3, ...]] grid, chunk_grids.py:167-293) read whole and
     strided into a device out: 64 spec groups, one plan and one launch each,
     launched back to back, and ONE host synchronisation for the whole batch
-    (pipeline.SYNCS); bit-exact with the oracle.  A corrupted chunk still
-    raises the reference's message from that single readback."""
+    (pipeline.SYNCS); bit-exact with the oracle.  Writes (whole, and a strided
+    scalar write whose edge chunks merge with their stored bytes) encode every
+    group before ONE readback of their checks and non-empty flags; stores
+    byte-identical.  A corrupted chunk still raises the reference's message
+    from that single readback."""
     import zarr_hip
     from zarr_hip import pipeline as P
 
@@ -212,6 +215,14 @@ def test_many_distinct_edges_one_synchronisation(codecs, device):
         assert P.LAUNCHES[0] - l0 == groups
         want = np.ascontiguousarray(O.read(host, meta, sel))
         assert got.cpu().numpy().tobytes() == want.tobytes()
+    # writes: every group's merge reads and encodes first, one readback
+    for sel, val in [((Ellipsis,), _data((n,), "float32", seed=5)), ((slice(7, 1500, 2),), np.float32(2.5))]:
+        s0 = P.SYNCS[0]
+        arr[sel] = val
+        assert P.SYNCS[0] - s0 == 1, (sel, P.SYNCS[0] - s0)
+        O.write(host, meta, sel, val)
+        got = {k: bytes(v) for k, v in store.to_dict().items() if not k.endswith("zarr.json")}
+        assert got == host
     if CRC in codecs:
         bad = bytearray(host["c/40"])
         bad[17] ^= 0x04

@@ -735,7 +735,8 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
             // (58: the look-back finalizer, while fewer chunks than CUs)
             KernelFn ifn = (g_tune_arm == 1 || g_tune_arm == 2 ||
                             ((g_tune_arm == 49 || (g_tune_arm >= 51 && g_tune_arm <= 57) ||
-                              (g_tune_arm == 58 && lb_ok && p.nseg <= 32u)) && p.aff_ok))
+                              (g_tune_arm == 58 && lb_ok && p.nseg <= 32u) ||
+                              g_tune_arm == 64 || g_tune_arm == 65) && p.aff_ok))
                                ? select_il_kernel_arm(crc, p.g.itemsize, swap, g_tune_arm)
                            : (tune & kTuneCfLookup) ? select_il_kernel_cf(crc, p.g.itemsize, swap)
                            : (tune & kTuneIlLean) ? select_il_kernel_lean(crc, p.g.itemsize, swap)

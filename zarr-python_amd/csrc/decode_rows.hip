@@ -1378,8 +1378,13 @@ __device__ __forceinline__ void publish_lb(const DecodeParams& p, uint32_t c, ui
 //   (production for the AFF launches: graph-timed 25.78-25.98 vs 25.97-26.09
 //   us median in four interleaved pairs, profiles/r05/ag/; arm 56 keeps 0);
 //   0 = the other instantiations.
+// STW (tuning arms 64 / 65, outs below 2 GiB): the stores through a buffer
+//   descriptor on the chunk's out base, unselected rows dropped by the range
+//   check instead of written to the sink; 1 = write-through (sc1: no dirty
+//   lines left in L2 at the kernel's end), 2 = nontemporal (the production
+//   policy, isolating the store form)
 template <bool CRC, int ITEM, bool SWAP, bool LEAN = false, bool CF = false, int LM = 0, bool TUNE = false,
-          int PUB = 3, bool AFF = false, int PRIO = 0>
+          int PUB = 3, bool AFF = false, int PRIO = 0, int STW = 0>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(LM == 2 ? 6 : 4, LM == 2 ? 6 : 4)))
 void k_decode_il(const DecodeParams p) {
     constexpr int K = kDefaultBlocks;
@@ -1562,10 +1567,22 @@ void k_decode_il(const DecodeParams p) {
         uint8_t* const obase = p.out + U.out_off;
         const uint4 f = make_uint4(p.fill[0], p.fill[1], p.fill[2], p.fill[3]);
         Acc4 acc = {0u, 0u, 0u, 0u};
+#if ZHIP_TUNING
+        __amdgpu_buffer_rsrc_t ors;
+        if constexpr (STW != 0) ors = __builtin_amdgcn_make_buffer_rsrc(obase, (short)0, 0x7FFFFFF0, 0x00020000);
+#endif
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const uint32_t lo = m[k].lo, hi = m[k].hi;
             const bool wr = writes && lane_row - lo < hi - lo;
+#if ZHIP_TUNING
+            if constexpr (STW != 0) {
+                const uint4 v = ok ? swap_block<ITEM, SWAP>(A[k]) : f;
+                zhip_v4u w = {v.x, v.y, v.z, v.w};
+                __builtin_amdgcn_raw_buffer_store_b128(w, ors, wr ? (int)(m[k].rel + lane_off) : 0x7FFFFFF0, 0,
+                                                       STW == 1 ? 16 : 2);
+            } else
+#endif
             store_nt16(wr ? obase + m[k].rel + lane_off : sink, ok ? swap_block<ITEM, SWAP>(A[k]) : f);
             if constexpr (CF) {  // timing arm: the lookups at lane-owned banks (results invalid)
                 if (CRC && ok) crc_block4_cf(s_tab, acc, A[k], (uint32_t)t & 31u);
@@ -1635,6 +1652,8 @@ KernelFn select_il_kernel_arm(bool crc, int item, bool swap, int arm) {  // ZHIP
         case 57: return k_decode_il<true, 4, false, false, false, 0, false, 3, true, 12>;  // 54 + XCD eighths (AFF)
         case 55: return k_decode_il<true, 4, false, false, false, 0, false, 3, true, 5>;  // 54 + run end (AFF)
         case 58: return k_decode_il<true, 4, false, false, false, 0, false, 5, true, 4>;  // 54 + look-back finalizer (AFF)
+        case 64: return k_decode_il<true, 4, false, false, false, 0, false, 3, true, 4, 1>;  // 54 + write-through stores
+        case 65: return k_decode_il<true, 4, false, false, false, 0, false, 3, true, 4, 2>;  // 54 + buffer nt stores
         default: return k_decode_il<true, 4, false>;  // arms of other kernels: production
     }
 }

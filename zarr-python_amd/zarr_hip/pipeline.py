@@ -1436,8 +1436,27 @@ class HipCodecPipeline:
             return
         value = _resolve_value(value)
         groups = spec_groups(batch)
-        if groups is not None:  # chunks of different specs (rectilinear grids): one write per spec
-            for idx in groups:
+        if groups is not None:  # chunks of different specs (rectilinear grids)
+            if self._plain_unsharded():
+                # every group's merge reads and encodes launched first, then ONE
+                # readback of all their checks and non-empty flags, then the commits
+                from .writer import ChunkWriter, PendingWrites
+
+                from .writer import _value_tensor
+
+                device = _write_device(batch, value)
+                pend = PendingWrites()
+                with torch.cuda.device(device):
+                    if not isinstance(value, torch.Tensor) or not value.is_cuda:  # one upload for all groups
+                        value = _value_tensor(value, batch[0][1].dtype, device)
+                    for idx in groups:
+                        sub = [batch[i] for i in idx]
+                        spec = sub[0][1]
+                        ChunkWriter(self.codecs, spec, spec.shape, device).write(
+                            sub, value, self.codecs, drop_axes, partial_encode=partial_encode, pending=pend)
+                    pend.finish(device)
+                return
+            for idx in groups:  # one write per spec
                 self._write_sync([batch[i] for i in idx], value, drop_axes, partial_encode)
             return
         if len(self.devices) > 1:  # items split over several GPUs (parallel.write_multi)
@@ -1461,13 +1480,16 @@ class HipCodecPipeline:
             # not the partial-encode path (codec_pipeline.py:1212)
             return pipe._write_sync(batch_s, value_s, drop_axes, partial_encode=False)
         spec: ArraySpec = batch[0][1]
-        device = value.device if isinstance(value, torch.Tensor) and value.is_cuda else None
-        if device is None:
-            st = getattr(batch[0][0], "store", None)
-            device = getattr(st, "device", None) or torch.device("cuda", torch.cuda.current_device())
+        device = _write_device(batch, value)
         with torch.cuda.device(device):
             w = ChunkWriter(self.codecs, spec, None or spec.shape, device)
             w.write(batch, value, self.codecs, drop_axes, partial_encode=partial_encode)
+
+    def _plain_unsharded(self) -> bool:
+        """One device, no sharding codec, no host stage, no nesting: the
+        chain ChunkWriter encodes unsharded (the two-phase mixed-spec write)."""
+        return (len(self.devices) <= 1 and self._nested() is None and self._host_split() is None
+                and not isinstance(self.array_bytes_codec, ShardingCodec))
 
     def _host_write(self, batch, value, drop_axes, partial_encode, hs) -> None:
         """Writes through a host stage: the GPU encodes the fixed-size chain;
@@ -1758,6 +1780,16 @@ def _slab_groups(batch: list, dev_out, min_bytes: int = 8 << 20, max_groups: int
     if cur:
         groups.append((lo * row_bytes, keys[-1][1] * row_bytes, cur))
     return groups if len(groups) >= 2 else None
+
+
+def _write_device(batch, value):
+    """The device a write encodes on: the value's, else the first item's
+    store's, else the current one."""
+    torch = _torch()
+    if isinstance(value, torch.Tensor) and value.is_cuda:
+        return value.device
+    st = getattr(batch[0][0], "store", None)
+    return getattr(st, "device", None) or torch.device("cuda", torch.cuda.current_device())
 
 
 def _resolve_value(value):

@@ -103,7 +103,49 @@ class EncodeLaunch:
                                            s), "zhip_encode_mapped")
 
     def nonempty(self) -> np.ndarray:
+        from . import pipeline as P
+
+        P.SYNCS[0] += 1
         return self.d_nonempty[: self.n].cpu().numpy().astype(bool)
+
+
+class PendingWrites:
+    """Encodes launched but not yet committed (a batch of several chunk specs,
+    pipeline._write_sync): every group's merge reads, encodes and flag words
+    are queued first, then ONE zhip_wait_ranges brings back all the groups'
+    decode error / verdict words and non-empty flags, errors raise before
+    anything is stored, and each group's results are committed."""
+
+    def __init__(self):
+        self.items = []  # (dest, setters, [(EncodeLaunch, idx)], elen, keep_all, prototype, [DecodeProgram])
+
+    def finish(self, device) -> None:
+        from .pipeline import _RangeSet
+
+        rngs, shape = [], []
+        for dest, setters, launches, elen, keep, proto, checks in self.items:
+            for prog in checks:
+                r = prog.wait_ranges()
+                rngs += r
+                shape.append(("check", sum(x[1] for x in r) // 4))
+            for l, _ in launches:
+                rngs.append((l.d_nonempty.data_ptr(), 4 * l.n))
+                shape.append(("ne", l.n))
+        host = _RangeSet(rngs).wait(device).copy() if rngs else np.zeros(0, np.uint32)
+        pos, k = 0, 0
+        for dest, setters, launches, elen, keep, proto, checks in self.items:
+            for prog in checks:
+                n = shape[k][1]
+                prog.results_from_words(host[pos: pos + n])  # raises like the reference
+                pos += n
+                k += 1
+            ne = np.zeros(len(setters), bool)
+            for l, idx in launches:
+                ne[idx] = host[pos: pos + l.n] != 0
+                pos += l.n
+                k += 1
+            dest.finish(setters, [elen if (keep or ne[i]) else 0 for i in range(len(setters))], proto)
+        self.items = []
 
 
 def _value_tensor(value, dtype, device):
@@ -203,7 +245,10 @@ class ChunkWriter:
         self.array_shape = tuple(array_shape)
         self.device = device
 
-    def write(self, batch, value, codecs, drop_axes=(), partial_encode: bool = True) -> None:
+    def write(self, batch, value, codecs, drop_axes=(), partial_encode: bool = True,
+              pending: "PendingWrites | None" = None) -> None:
+        """pending (unsharded chains): queue the merge read's check and the
+        encode's commit on it instead of synchronising here."""
         from .pipeline import HipCodecPipeline, _Raw
 
         torch = _torch()
@@ -234,6 +279,7 @@ class ChunkWriter:
         # temporary (absent -> fill), then the merge on the device
         temp = None
         present = None
+        prog = None  # the merge read, when its check is left to `pending`
         if partial_items:
             pipe = HipCodecPipeline.from_codecs(codecs).evolve_from_array_spec(spec)
             temp = torch.empty((len(partial_items),) + tuple(chunk_shape),
@@ -244,7 +290,9 @@ class ChunkWriter:
             stride0 = temp.stride(0) * temp.element_size()
             prog = pipe.prepare_read(rb, temp[0], (), np.arange(len(rb), dtype=np.int64) * stride0)
             prog.launch()
-            prog.results()
+            if pending is None or sharded_partial or self.chain.shard is not None:
+                prog.results()
+                prog = None
             if sharded_partial:
                 # per (item, inner slot): the inner chunk exists in the stored shard
                 st = prog.data.statuses()
@@ -260,9 +308,10 @@ class ChunkWriter:
         if self.chain.shard is not None:
             return self._encode_shards(complete_items, partial_items, v, temp, present,
                                        sharded_partial)
-        self._encode_chunks(complete_items, partial_items, v, temp)
+        self._encode_chunks(complete_items, partial_items, v, temp, pending,
+                            [prog] if partial_items and prog is not None else [])
 
-    def _encode_chunks(self, complete_items, partial_items, v, temp):
+    def _encode_chunks(self, complete_items, partial_items, v, temp, pending=None, checks=()):
         spec = self.spec
         chain = self.chain
         itemsize = spec.dtype.itemsize
@@ -298,6 +347,10 @@ class ChunkWriter:
                 l.launch()
         finally:
             dest.release_lock()
+        if pending is not None:  # committed by PendingWrites.finish after one readback
+            pending.items.append((dest, setters, launches, elen, spec.config.write_empty_chunks, spec.prototype,
+                                  list(checks)))
+            return
         nonempty = np.zeros(len(setters), bool)
         for l, idx in launches:
             nonempty[idx] = l.nonempty()
