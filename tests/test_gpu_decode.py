@@ -1529,7 +1529,7 @@ def _ilw_case(device, arm, case, whole=False):
 
 
 @pytest.mark.tuning
-@pytest.mark.parametrize("arm", [0, 5, 37, 38, 49])
+@pytest.mark.parametrize("arm", [0, 5, 37, 38, 49, 67])
 @pytest.mark.parametrize("dtype,endian,chunks,shape", TILE4_CASES)
 def test_transpose_tile4w_and_tile4(device, dtype, endian, chunks, shape, arm):
     """k_decode_tile4w's two-tile form (production for CRC layouts of at most
@@ -1542,7 +1542,7 @@ def test_transpose_tile4w_and_tile4(device, dtype, endian, chunks, shape, arm):
 
     codecs = [T((2, 1, 0)), endian, CRC]
     kernel = {0: b"k_decode_tile2w", 5: b"k_decode_tile4", 37: b"k_decode_tile1w", 38: b"k_decode_tile4w",
-              49: b"k_decode_tile2ws"}[arm]
+              49: b"k_decode_tile2ws", 67: b"k_decode_tile2w_bt"}[arm]
     set_tuning(6, arm)
     try:
         _roundtrip(device, shape, chunks, dtype, codecs)
@@ -1652,7 +1652,7 @@ def _tile_pairs_case(device, dtype, endian, chunks, shape, order, codecs):
 
 
 @pytest.mark.tuning
-@pytest.mark.parametrize("arm", [0, 48, 62])
+@pytest.mark.parametrize("arm", [0, 48, 62, 66])
 def test_transpose_tileg_128_chunks_arrivals(device, arm):
     """C3's 128^3-chunk geometry (256 workgroups per chunk in the two-tile
     form: 16 arrival subwords and a second level): the returning publication
@@ -1662,7 +1662,8 @@ def test_transpose_tileg_128_chunks_arrivals(device, arm):
     from zarr_hip import _native as N
 
     codecs = [T((2, 1, 0)), LE, CRC]
-    kernel = {0: b"k_decode_tileg2w", 48: b"k_decode_tileg2wp", 62: b"k_decode_tileg2w_lb"}[arm]
+    kernel = {0: b"k_decode_tileg2w", 48: b"k_decode_tileg2wp", 62: b"k_decode_tileg2w_lb",
+              66: b"k_decode_tileg2w_bt"}[arm]
     set_tuning(6, arm)
     try:
         arr, host, meta = _roundtrip(device, (128, 256, 256), (128, 128, 128), "float32", codecs, fill=3,
@@ -1684,7 +1685,7 @@ def test_transpose_tileg_128_chunks_arrivals(device, arm):
 
 
 @pytest.mark.tuning
-@pytest.mark.parametrize("arm", [0, 5, 38, 40, 48, 62])
+@pytest.mark.parametrize("arm", [0, 5, 38, 40, 48, 62, 66])
 @pytest.mark.parametrize("order", [(2, 1, 0), (1, 2, 0), (0, 2, 1)])
 @pytest.mark.parametrize("dtype,endian", [("float32", LE), ("int16", BE), ("float64", LE), ("uint8", LE)])
 def test_transpose_tilegw_and_tileg(device, order, dtype, endian, arm):
@@ -1698,7 +1699,7 @@ def test_transpose_tilegw_and_tileg(device, order, dtype, endian, arm):
 
     codecs = [T(order), endian, CRC]
     kernel = {0: b"k_decode_tileg2w", 5: b"k_decode_tileg", 38: b"k_decode_tilegw", 40: b"k_decode_tileglt",
-              48: b"k_decode_tileg2wp", 62: b"k_decode_tileg2w_lb"}[arm]
+              48: b"k_decode_tileg2wp", 62: b"k_decode_tileg2w_lb", 66: b"k_decode_tileg2w_bt"}[arm]
     set_tuning(6, arm)
     try:
         # (arm 62 takes the look-back form only up to 128 groups per chunk)

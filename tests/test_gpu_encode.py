@@ -356,7 +356,7 @@ def test_encode_tileg_four_tile_form(device, order, dtype, endian):
     d = _data(shape, dtype)
     d[0:96, 0:80, 0:80] = 0
     for arm, kname in ((0, b"k_encode_tileg"), (36, b"k_encode_tileg2"), (47, b"k_encode_tilegs"),
-                       (50, b"k_encode_tileg2s"), (63, b"k_encode_tileg_lb")):
+                       (50, b"k_encode_tileg2s"), (63, b"k_encode_tileg_lb"), (68, b"k_encode_tileg_a4")):
         set_tuning(6, arm)
         try:
             arr, _ = _run(device, shape, chunks, dtype, codecs, 0,

@@ -535,8 +535,11 @@ int zhip_plan_upload(zhip_plan* p) {
         // for the grouped kernel on C3 in 128^3 chunks, profiles/r05/q/)
         const size_t n_t2 = (ZHIP_TUNING && p->tile2) ? kPairTabWords + (size_t)T * 4 + (size_t)(T / 2) * kThreads : 0;
         const size_t n_tgl = (ZHIP_TUNING && tgw) ? (size_t)p->n_groups * kThreads : 0;  // lane-tile form, arm 40
+        // (tuning arms 66 / 67: A_(4 sq) as byte tables for the chains of the
+        // two-tile forms)
+        const size_t n_tbt = (ZHIP_TUNING && (t4w || tgw)) ? (size_t)kByteTabWords : 0;
         std::vector<uint32_t> ht(n_base + n_t4 + n_g + n_t4f + n_t4w + n_tgw + n_t2w + n_t1w + n_tg2w + n_t2e + n_t2 +
-                                 n_tgl);
+                                 n_tgl + n_tbt);
         build_horner_stride(ht.data(), 16ull * sq);
         for (int t = 0; t < kThreads; ++t) {
             const uint64_t rel = (uint64_t)(kTileRows + t / 16) * sq + 16u * (t % 16);
@@ -771,6 +774,17 @@ int zhip_plan_upload(zhip_plan* p) {
                     const int64_t e = (int64_t)p->E - p0 + kWgStride - 16 * (int64_t)D;
                     const uint32_t xe = e >= 0 ? xpow8((uint64_t)e) : xpow8_inv((uint64_t)(-e));
                     f[(size_t)g * kThreads + t] = gf_mul(gf_mul(xe, p->c_inv), c96);
+                }
+        }
+        p->tilebt_off = 0;
+        if (n_tbt) {
+            p->tilebt_off = n_base + n_t4 + n_g + n_t4f + n_t4w + n_tgw + n_t2w + n_t1w + n_tg2w + n_t2e + n_t2 + n_tgl;
+            uint32_t* f = &ht[p->tilebt_off];
+            const uint32_t x = xpow8(4ull * sq), x4 = xpow8(4);
+            for (int sl = 0; sl < 4; ++sl)
+                for (uint32_t b = 0; b < 256; ++b) {
+                    f[sl * 256 + b] = gf_mul(x, b << (8 * sl));
+                    f[1024 + sl * 256 + b] = gf_mul(x4, b << (8 * sl));
                 }
         }
         p->tilegw = tgw ? 1u : 0u;
@@ -1169,6 +1183,7 @@ int zhip_decode_mapped(const zhip_plan* plan, const void* src, uint64_t src_size
                 // C3 28.9 vs 30.3-30.6 us, profiles/r04/k); arms 1 / 2 / 5: k_decode_tile4
                 p.t4w_tab = plan->d_tile_tables + plan->tile4w_off;
                 p.t4w_kq = p.t4w_tab + kPairTabWords;
+                if (plan->tilebt_off) p.tbt_tab = plan->d_tile_tables + plan->tilebt_off;
                 if (plan->tile2w_off) p.t2w_kq = plan->d_tile_tables + plan->tile2w_off;
                 if (plan->tile1w_off) p.t1w_kq = plan->d_tile_tables + plan->tile1w_off;
             }
@@ -1194,6 +1209,7 @@ int zhip_decode_mapped(const zhip_plan* plan, const void* src, uint64_t src_size
                 p.t4w_kq = p.t4w_tab + kPairTabWords;
                 if (plan->tileg2w_off) p.t2w_kq = plan->d_tile_tables + plan->tileg2w_off;  // two tiles per workgroup
                 if (plan->tilegl_off) p.tglt_kq = plan->d_tile_tables + plan->tilegl_off;    // (arm 40)
+                if (plan->tilebt_off) p.tbt_tab = plan->d_tile_tables + plan->tilebt_off;    // (arm 66)
             }
         }
         const uint64_t tunits = (uint64_t)n_chunks * plan->t_per_chunk;
@@ -1294,6 +1310,8 @@ int zhip_encode_mapped(const zhip_plan* plan, const void* arr, void* dst, const 
         p.g_step_t = plan->sstride[plan->gd];
         p.g_z2 = xpow8(2ull * plan->sstride[plan->gd]);
         p.g_step_o = L.out_stride[plan->gd];
+        if (plan->tilebt_off) p.g_a4 = plan->d_tile_tables + plan->tilebt_off + 1024;  // (arm 68)
+        p.g_c96 = xpow8_inv(12);
         d_rowmap = nullptr;
     } else if ((encode_flags & (ZHIP_DF_TILE | ZHIP_DF_TILE_PREFIX)) && plan->tq >= 0 && plan->d_tile_tables &&
                (plan->t_per_chunk + 3u) / 4u < 65536u) {

@@ -826,12 +826,16 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
         if (w4 && ((p.t2w_kq && g_tune_arm != 38 && g_tune_arm != 37) || (g_tune_arm == 37 && p.t1w_kq))) {
             const int nt = g_tune_arm == 37 ? 1 : 2;
             // (tuning arm 49: the split publication of 17..32 workgroups per chunk)
-            KernelFn fn2 = select_tile2w_kernel(p.g.itemsize, swp, (nt == 2 && g_tune_arm == 49) ? 3 : nt);
+            // (tuning arm 67: the byte-table chains, where the plan built them)
+            KernelFn fn2 = select_tile2w_kernel(p.g.itemsize, swp,
+                                                (nt == 2 && g_tune_arm == 49) ? 3
+                                                : (nt == 2 && g_tune_arm == 67 && p.tbt_tab) ? 4 : nt);
             if (!fn2) return ZHIP_E_UNSUPPORTED;
             if (p.n_units == 0) return ZHIP_OK;
             DecodeParams q = p;
             q.t4w_kq = nt == 1 ? p.t1w_kq : p.t2w_kq;
-            g_last_kernel = nt == 1 ? "k_decode_tile1w" : g_tune_arm == 49 ? "k_decode_tile2ws" : "k_decode_tile2w";
+            g_last_kernel = nt == 1 ? "k_decode_tile1w" : g_tune_arm == 49 ? "k_decode_tile2ws"
+                            : (g_tune_arm == 67 && p.tbt_tab) ? "k_decode_tile2w_bt" : "k_decode_tile2w";
             hipLaunchKernelGGL(fn2, dim3(p.n_units / (uint32_t)nt), dim3(kThreads), 0, stream, q);
             return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
         }
@@ -875,6 +879,7 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
         if (nt == 2 && g_tune_arm == 48) nsel = 6;  // the arrival words packed (round-4 layout)
         // the look-back finalizer (fewer chunks than CUs; the spread subwords)
         if (nt == 2 && g_tune_arm == 62 && lb_ok && p.n_groups <= 128u) nsel = 7;
+        if (nt == 2 && g_tune_arm == 66 && p.tbt_tab) nsel = 8;  // the byte-table chains
 #endif
         KernelFn fn = gw ? select_tilegw_kernel(p.g.itemsize, (p.lflags & ZHIP_LF_SWAP) != 0, defer, nsel)
                          : select_tileg_kernel((p.lflags & ZHIP_LF_CRC) != 0, p.g.itemsize,
@@ -887,6 +892,7 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
         if (nt == 2) q.t4w_kq = p.t2w_kq;
         if (nt == 5) q.t4w_kq = p.tglt_kq;
         g_last_kernel = !gw ? "k_decode_tileg" : nsel == 6 ? "k_decode_tileg2wp" : nsel == 7 ? "k_decode_tileg2w_lb"
+                                           : nsel == 8 ? "k_decode_tileg2w_bt"
                                            : nt == 2 ? "k_decode_tileg2w"
                                            : nt == 5 ? "k_decode_tileglt"
                                                                                       : "k_decode_tilegw";

@@ -475,7 +475,9 @@ struct TileMapN {
 // SPL (tuning arm 49): chunks of 17..32 workgroups publish through two
 // subwords of 16 on lines of their own and a second level (tileg_arrive SPR)
 // instead of 32 arrivals on the chunk's one word.
-template <int ITEM, bool SWAP, int NT = kTiles, bool SPL = false>
+// BT (tuning arm 67): the chain through byte tables (crc_block4_t): 24 KiB of
+// LDS per workgroup instead of 40, six resident per CU instead of four
+template <int ITEM, bool SWAP, int NT = kTiles, bool SPL = false, bool BT = false>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_decode_tile4w(
     const DecodeParams p) {
     constexpr int kPer = 16 / ITEM;
@@ -484,10 +486,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     constexpr int RPW = kTileRows / WPT;    // tile rows per wave
     constexpr int KB = RPW / 4;             // blocks per lane
     constexpr int HS = KB / NT;             // Horner steps per tile iteration
-    __shared__ __attribute__((aligned(16))) uint32_t s_mem[kPairTabWords + kTileRows * 64];
+    constexpr int TW = BT ? kByteTabWords : kPairTabWords;  // table words
+    __shared__ __attribute__((aligned(16))) uint32_t s_mem[TW + kTileRows * 64];
     uint32_t* const s_tab = s_mem;
-    uint8_t* const s_tile = reinterpret_cast<uint8_t*>(s_mem + kPairTabWords);
-    uint32_t* const s_red = s_mem + kPairTabWords;  // after the last out-order pass
+    uint8_t* const s_tile = reinterpret_cast<uint8_t*>(s_mem + TW);
+    uint32_t* const s_red = s_mem + TW;  // after the last out-order pass
     const int t = threadIdx.x;
     const uint32_t wv = __builtin_amdgcn_readfirstlane((uint32_t)t >> 6);
     const uint32_t tj = wv / WPT, hh = wv % WPT;  // this wave's tile and its row band
@@ -498,9 +501,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     const uint32_t grp = g - c * gpc;
     const uint32_t expected = p.g.nbytes + 4u;
     // 1. tables and the lane constant (L2 hits), the chunk header, the data blocks
-    const uint4* gt = reinterpret_cast<const uint4*>(p.t4w_tab);
-    const uint4 tv0 = gt[t], tv1 = gt[t + kThreads], tv2 = gt[t + 2 * kThreads], tv3 = gt[t + 3 * kThreads],
-                tv4 = gt[t + 4 * kThreads], tv5 = gt[t + 5 * kThreads];
+    constexpr int TV = TW / 4 / kThreads;  // uint4 table pieces per thread
+    const uint4* gt = reinterpret_cast<const uint4*>(BT ? p.tbt_tab : p.t4w_tab);
+    uint4 tv[TV];
+#pragma unroll
+    for (int i = 0; i < TV; ++i) tv[i] = gt[t + i * kThreads];
     const uint32_t kq = p.t4w_kq[(size_t)grp * kThreads + t];
     const Unit U = resolve_unit(p, c * p.nseg, expected);
     const TileMapN<NT> tm = load_uniform<TileMapN<NT>>(p.tmap + (size_t)grp * NT);
@@ -516,12 +521,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     if (ok) stored = load_trailer_uniform(U.cp, p.g.nbytes);
     {
         uint4* st = reinterpret_cast<uint4*>(s_tab);
-        st[t] = tv0;
-        st[t + kThreads] = tv1;
-        st[t + 2 * kThreads] = tv2;
-        st[t + 3 * kThreads] = tv3;
-        st[t + 4 * kThreads] = tv4;
-        st[t + 5 * kThreads] = tv5;
+#pragma unroll
+        for (int i = 0; i < TV; ++i) st[t + i * kThreads] = tv[i];
     }
     // 2. per tile: wave j writes tile j into LDS in stored order, every wave
     //    reads it back in out order and stores 16-byte pieces, then takes four
@@ -569,14 +570,14 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
         }
         if (ok) {
 #pragma unroll
-            for (int m = HS * j; m < HS * j + HS; ++m) crc_block4(s_tab, acc, blk[m]);
+            for (int m = HS * j; m < HS * j + HS; ++m) crc_block4_t<BT>(s_tab, acc, blk[m]);
         }
     }
     // 3. run end: fold, lane multiply, reduce, publish (returning, the chunk's
     //    word alone in its 128-byte line); the arrival completing the chunk
     //    compares with the trailer
     if (ok) {
-        const uint32_t v = wave_xor(lanemul_reg(kq, fold4(s_tab, acc)));
+        const uint32_t v = wave_xor(lanemul_reg(kq, fold4_t<BT>(s_tab, acc)));
         __syncthreads();  // every out-order read of the last tile is done: s_red reuses the image
         if ((t & 63) == 0) s_red[t >> 6] = v;
         __syncthreads();
@@ -827,7 +828,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
 // lanes of every wave that hold tile j write the image.
 // LB (tuning arm 62): the returning arrival replaced by tileg_arrive_lb (the
 //   chunk's last workgroup polls, the others retire after a non-returning xor)
-template <int ITEM, bool SWAP, int PUB = 2, int NT = kTiles, bool LT = false, bool SPR = false, bool LB = false>
+// BT (tuning arm 66): the chain through byte tables (crc_block4_t), 24 KiB of
+//   LDS instead of 40
+template <int ITEM, bool SWAP, int PUB = 2, int NT = kTiles, bool LT = false, bool SPR = false, bool LB = false,
+          bool BT = false>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_decode_tilegw(
     const DecodeParams p) {
     static_assert(!LT || NT == kTiles, "lane-tile mapping: four tiles per workgroup");
@@ -838,10 +842,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     constexpr int KB = RPW / 4;             // blocks per lane
     constexpr int HS = KB / NT;             // Horner steps per tile iteration
     constexpr uint32_t PG = kTiles / NT;    // workgroups per group of four tiles
-    __shared__ __attribute__((aligned(16))) uint32_t s_mem[kPairTabWords + kTileRows * 64];
+    constexpr int TW = BT ? kByteTabWords : kPairTabWords;  // table words
+    __shared__ __attribute__((aligned(16))) uint32_t s_mem[TW + kTileRows * 64];
     uint32_t* const s_tab = s_mem;
-    uint8_t* const s_tile = reinterpret_cast<uint8_t*>(s_mem + kPairTabWords);
-    uint32_t* const s_red = s_mem + kPairTabWords;  // after the last out-order pass
+    uint8_t* const s_tile = reinterpret_cast<uint8_t*>(s_mem + TW);
+    uint32_t* const s_red = s_mem + TW;  // after the last out-order pass
     const int t = threadIdx.x;
     const uint32_t wv = __builtin_amdgcn_readfirstlane((uint32_t)t >> 6);
     const uint32_t ln = (uint32_t)t & 63u, cl = 16u * (ln & 15u);
@@ -853,9 +858,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     const uint32_t wg = blockIdx.x - c * gpc;
     const uint32_t grp = wg / PG, t0 = (wg % PG) * NT;  // the group and its first tile here
     const uint32_t expected = p.g.nbytes + 4u;
-    const uint4* gt = reinterpret_cast<const uint4*>(p.t4w_tab);
-    const uint4 tv0 = gt[t], tv1 = gt[t + kThreads], tv2 = gt[t + 2 * kThreads], tv3 = gt[t + 3 * kThreads],
-                tv4 = gt[t + 4 * kThreads], tv5 = gt[t + 5 * kThreads];
+    constexpr int TV = TW / 4 / kThreads;  // uint4 table pieces per thread
+    const uint4* gt = reinterpret_cast<const uint4*>(BT ? p.tbt_tab : p.t4w_tab);
+    uint4 tv[TV];
+#pragma unroll
+    for (int i = 0; i < TV; ++i) tv[i] = gt[t + i * kThreads];
     const uint32_t kq = p.t4w_kq[(size_t)wg * kThreads + t];
     // (the two-tile form always reports in-launch: twice the workgroups per
     // chunk made the deferred verdicts' one same-address word per chunk the
@@ -882,12 +889,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     if (ok) stored = load_trailer_uniform(U.cp, p.g.nbytes);
     {
         uint4* st = reinterpret_cast<uint4*>(s_tab);
-        st[t] = tv0;
-        st[t + kThreads] = tv1;
-        st[t + 2 * kThreads] = tv2;
-        st[t + 3 * kThreads] = tv3;
-        st[t + 4 * kThreads] = tv4;
-        st[t + 5 * kThreads] = tv5;
+#pragma unroll
+        for (int i = 0; i < TV; ++i) st[t + i * kThreads] = tv[i];
     }
     const bool writes = ok || U.mode == ZHIP_ST_MISSING;
     const uint4 f = make_uint4(p.fill[0], p.fill[1], p.fill[2], p.fill[3]);
@@ -933,11 +936,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
         }
         if (ok) {
 #pragma unroll
-            for (int m = HS * j; m < HS * j + HS; ++m) crc_block4(s_tab, acc, blk[m]);
+            for (int m = HS * j; m < HS * j + HS; ++m) crc_block4_t<BT>(s_tab, acc, blk[m]);
         }
     }
     if (ok) {
-        const uint32_t v = wave_xor(lanemul_reg(kq, fold4(s_tab, acc)));
+        const uint32_t v = wave_xor(lanemul_reg(kq, fold4_t<BT>(s_tab, acc)));
         __syncthreads();  // every out-order read of the last tile is done: s_red reuses the image
         if ((t & 63) == 0) s_red[t >> 6] = v;
         __syncthreads();
@@ -1399,12 +1402,18 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
 // group's last-tile frame that ge.ku assumes; arrival subwords for twice the
 // workgroups, zhip_plan_info)
 // LB (tuning arm 63): tileg_arrive_lb instead of the returning arrival
-template <bool CRC, int ITEM, bool SWAP, int NT = kTiles, bool SPR = false, bool LB = false>
+// A4C (tuning arm 68): four word accumulators per lane through the ONE
+//   operator A_(16 sq) (the first of the four byte-table operators) instead of
+//   one accumulator through four, folded per tile by the A4 tables
+//   (fold4_t: the state x^96 times the single accumulator's, undone by g_c96
+//   in the lane multiply): 16 + 4 lookups per tile more, 8 KiB of tables
+//   instead of 16 -- 28 KiB of LDS, five workgroups per CU instead of four
+template <bool CRC, int ITEM, bool SWAP, int NT = kTiles, bool SPR = false, bool LB = false, bool A4C = false>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_encode_tileg(
     const EncodeParams p) {
     constexpr int kPer = 16 / ITEM;
     constexpr int kPiecesPerCol = kTileRows / kPer;
-    __shared__ uint32_t s_tab[CRC ? 16 * 256 : 1];
+    __shared__ uint32_t s_tab[CRC ? (A4C ? 2048 : 16 * 256) : 1];
     __shared__ uint32_t s_tz[CRC ? 1024 : 1];
     __shared__ __attribute__((aligned(16))) uint8_t s_tile[kTileRows * 256];
     __shared__ uint32_t s_red[kThreads / 64];
@@ -1420,9 +1429,13 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     if constexpr (CRC) {
         const uint4* gt = reinterpret_cast<const uint4*>(p.horner);
         tv0 = gt[t];
-        tv1 = gt[t + kThreads];
-        tv2 = gt[t + 2 * kThreads];
-        tv3 = gt[t + 3 * kThreads];
+        if constexpr (A4C) {
+            tv1 = reinterpret_cast<const uint4*>(p.g_a4)[t];
+        } else {
+            tv1 = gt[t + kThreads];
+            tv2 = gt[t + 2 * kThreads];
+            tv3 = gt[t + 3 * kThreads];
+        }
         tzv = reinterpret_cast<const uint4*>(p.gtz)[t];
         kth = p.kthread[t];
     }
@@ -1454,8 +1467,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
         uint4* st = reinterpret_cast<uint4*>(s_tab);
         st[t] = tv0;
         st[t + kThreads] = tv1;
-        st[t + 2 * kThreads] = tv2;
-        st[t + 3 * kThreads] = tv3;
+        if constexpr (!A4C) {
+            st[t + 2 * kThreads] = tv2;
+            st[t + 3 * kThreads] = tv3;
+        }
         reinterpret_cast<uint4*>(s_tz)[t] = tzv;
     }
     const uint32_t row0 = (uint32_t)t >> 4, col = 16u * (uint32_t)(t & 15);
@@ -1489,6 +1504,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
         // 3. stored-order blocks inside the tile: fill test, byteswap, store,
         //    Horner steps (blocks outside the tile count as zeros)
         uint32_t acc = 0;
+        Acc4 a4 = {0u, 0u, 0u, 0u};
 #pragma unroll
         for (int k = 0; k < kPasses; ++k) {
             const uint32_t row = 16u * k + row0;
@@ -1499,15 +1515,19 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
                 e = swap_block<ITEM, SWAP>(v);
                 store_nt16_a1(cp + (size_t)(t0 + j) * p.g_step_t + row * sq + col, e);
             }
-            if constexpr (CRC)
+            if constexpr (CRC && A4C) {
+                crc_block4_t<true>(s_tab, a4, e);
+            } else if constexpr (CRC) {
                 acc = tab_apply(s_tab, acc ^ e.x) ^ tab_apply(s_tab + 1024, e.y) ^ tab_apply(s_tab + 2048, e.z) ^
                       tab_apply(s_tab + 3072, e.w);
+            }
         }
+        if constexpr (CRC && A4C) acc = fold4_t<true>(s_tab, a4);  // x^96 times the single accumulator
         if constexpr (CRC) S = (j == 0 ? 0u : tab_apply(s_tz, S)) ^ acc;
     }
     // 4. run end: lane shift, reduction, the group's tile / chunk-end shift
     uint32_t v = 0;
-    if constexpr (CRC) v = wave_xor(gf_mul(S, kth));
+    if constexpr (CRC) v = wave_xor(gf_mul(S, A4C ? gf_mul(kth, p.g_c96) : kth));
     const bool wne = __any(!eq);
     if ((t & 63) == 0) {
         s_red[t >> 6] = v;
@@ -1566,12 +1586,13 @@ using EncodeFn = void (*)(const EncodeParams);
 
 EncodeFn select_encode_tileg_kernel(bool crc, int item, bool swap, int nt) {
 #if ZHIP_TUNING
-    if (nt == 6 || nt == 7 || nt == 8) {  // arms 47 / 50: four / two tiles, arrival words on lines of
-        // their own; arm 63 (8): four tiles, the look-back finalizer
+    if (nt == 6 || nt == 7 || nt == 8 || nt == 9) {  // arms 47 / 50: four / two tiles, arrival words on
+        // lines of their own; arm 63 (8): four tiles, the look-back finalizer; arm 68 (9): four
+        // accumulators through one byte-table operator
         if (!crc) return nullptr;
 #define ZHIP_ETG(I, W)                                                                                      \
     (nt == 6 ? k_encode_tileg<true, I, W, 4, true> : nt == 8 ? k_encode_tileg<true, I, W, 4, true, true>    \
-             : k_encode_tileg<true, I, W, 2, true>)
+     : nt == 9 ? k_encode_tileg<true, I, W, 4, false, false, true> : k_encode_tileg<true, I, W, 2, true>)
         switch (item) {
             case 1: return ZHIP_ETG(1, false);
             case 2: return swap ? ZHIP_ETG(2, true) : ZHIP_ETG(2, false);
@@ -1671,6 +1692,7 @@ KernelFn select_tilegw_kernel(int item, bool swap, bool defer, int nt) {  // CRC
 #define ZHIP_TILEGW(I, W)                                                                          \
     (nt == 2 ? k_decode_tilegw<I, W, 0, 2, false, true>                                             \
      : nt == 7 ? k_decode_tilegw<I, W, 0, 2, false, true, true>                                     \
+     : nt == 8 ? k_decode_tilegw<I, W, 0, 2, false, true, false, true>                              \
      : nt == 5 ? (defer ? k_decode_tilegw<I, W, 2, 4, true> : k_decode_tilegw<I, W, 0, 4, true>)   \
      : nt == 6 ? k_decode_tilegw<I, W, 0, 2>                                                        \
              : (defer ? k_decode_tilegw<I, W, 2> : k_decode_tilegw<I, W, 0>))
@@ -1703,8 +1725,9 @@ KernelFn select_tile4w_kernel(int item, bool swap) {  // CRC chains only
 // the tuning build adds one tile per workgroup (arm 37)
 KernelFn select_tile2w_kernel(int item, bool swap, int nt) {  // CRC chains only
 #if ZHIP_TUNING
-#define ZHIP_T2W(I, W) \
-    (nt == 1 ? k_decode_tile4w<I, W, 1> : nt == 3 ? k_decode_tile4w<I, W, 2, true> : k_decode_tile4w<I, W, 2>)
+#define ZHIP_T2W(I, W)                                                                                  \
+    (nt == 1 ? k_decode_tile4w<I, W, 1> : nt == 3 ? k_decode_tile4w<I, W, 2, true>                       \
+     : nt == 4 ? k_decode_tile4w<I, W, 2, false, true> : k_decode_tile4w<I, W, 2>)
 #else
     if (nt != 2) return nullptr;
 #define ZHIP_T2W(I, W) k_decode_tile4w<I, W, 2>

@@ -800,7 +800,10 @@ int launch_encode(const EncodeParams& p, hipStream_t stream, int max_grid) {
         // (tuning arm 63: four tiles, the look-back finalizer, while fewer chunks than CUs)
         const bool lb = ZHIP_TUNING && crc && g_tune_arm == 63 && p.n_chunks < (uint32_t)(max_grid / 8) &&
                         (p.n_groups <= 16u || p.n_sub);
-        EncodeFn fn = select_encode_tileg_kernel(crc, p.g.itemsize, swap, lb ? 8 : spr ? (nt == 4 ? 6 : 7) : nt);
+        // (tuning arm 68: four accumulators through one byte-table operator)
+        const bool a4c = ZHIP_TUNING && crc && g_tune_arm == 68 && p.g_a4 != nullptr;
+        EncodeFn fn = select_encode_tileg_kernel(crc, p.g.itemsize, swap,
+                                                 a4c ? 9 : lb ? 8 : spr ? (nt == 4 ? 6 : 7) : nt);
         if (!fn) return ZHIP_E_UNSUPPORTED;
         if (p.n_chunks == 0) return ZHIP_OK;
         const uint64_t grid = (uint64_t)p.n_chunks * p.n_groups * (uint32_t)(4 / nt);
@@ -808,6 +811,7 @@ int launch_encode(const EncodeParams& p, hipStream_t stream, int max_grid) {
         // (the last arrival of each chunk writes its non-empty flag)
         g_last_kernel = nt == 2 ? (spr ? "k_encode_tileg2s" : "k_encode_tileg2") : spr ? "k_encode_tilegs" : "k_encode_tileg";
         if (lb) g_last_kernel = "k_encode_tileg_lb";
+        if (a4c) g_last_kernel = "k_encode_tileg_a4";
         hipLaunchKernelGGL(fn, dim3((uint32_t)grid), dim3(kThreads), 0, stream, p);
         return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
     }

@@ -49,6 +49,9 @@ struct GroupEnt {
 // and 10 high bits of a word, then the four byte slices of A4 (x^32).
 constexpr int kPairT1 = 0, kPairT2 = 2048, kPairT3 = 4096, kPairA4 = 5120;
 constexpr int kPairTabWords = 6144;
+// the byte-table form of the same operator (tuning arms 66 / 67: k_decode_tile4w
+// / k_decode_tilegw): A_D's four 256-entry byte tables, then the A4 fold tables
+constexpr int kByteTabWords = 2048;
 extern const char* g_last_kernel;  // zhip_last_kernel: the kernel the last decode / mapped encode launched
 constexpr uint32_t kIlwMaxUnits = 512;  // k_decode_ilw (512 lanes) for grids of at most 2 units per CU
 constexpr int kIlBasisWords = 64;  // T1 / T2 / T3 bases (11 + 11 + 10, padded to 32), A4 bases (4 x 8)
@@ -124,6 +127,7 @@ struct DecodeParams {
     const uint32_t* t2w_kq;  // k_decode_tile4w with two tiles per workgroup (production when set): lane constants
     const uint32_t* t1w_kq;  // tuning arm 37 (one tile per workgroup)
     const uint32_t* tglt_kq; // tuning arm 40 (k_decode_tilegw, lanes pick the tile): lane constants
+    const uint32_t* tbt_tab; // tuning arms 66 / 67: A_(4 sq) as byte tables + A4 (kByteTabWords)
     // k_decode_tileg (tileg != 0): group map, step multiply table, steps
     uint32_t tileg;
     const struct GroupEnt* gmap;
@@ -326,6 +330,10 @@ struct EncodeParams {
     const uint32_t* gtz;
     uint32_t n_groups, g_step_t, n_sub;
     uint32_t g_z2;  // k_encode_tileg's two-tile form: x^(8 * 2 g_step_t), the first half's shift to ku's frame
+    // tuning arm 68 (k_encode_tileg, four accumulators through one byte-table
+    // operator): the A4 fold tables and x^(-96), the folded state's frame
+    const uint32_t* g_a4;
+    uint32_t g_c96;
     int64_t g_step_o;
     uint32_t xcd_run;     // k_encode_pair: pairs per XCD-contiguous run (0: dispatch order)
     // 64-bit words between chunks' publication words (k_encode_pair / k_encode_tile4):
@@ -409,6 +417,7 @@ struct zhip_plan {
     uint64_t tile1w_off;  // tuning builds: lane constants [T][kThreads] of the one-tile form (0: none)
     uint64_t tileg2w_off; // lane constants [2 n_groups][kThreads] of k_decode_tilegw's two-tile form (0: none)
     uint64_t tilegl_off;  // tuning builds: lane constants [n_groups][kThreads] of its lane-tile form (0: none)
+    uint64_t tilebt_off;  // tuning builds: A_(4 sq) byte tables + A4 (kByteTabWords) for arms 66 / 67 (0: none)
     uint64_t tile2e_off;  // lane constants [T/2][kThreads] of k_encode_tile4's two-tile form (0: none)
     // full-tile layouts that tile4 declines (e.g. 128^3 chunks: the four tiles
     // of a natural group at two steps) but whose consecutive tile pairs are the
