@@ -279,7 +279,7 @@ class ChunkWriter:
         # temporary (absent -> fill), then the merge on the device
         temp = None
         present = None
-        prog = None  # the merge read, when its check is left to `pending`
+        deferred = None  # the merge read, when its check is left to `pending`
         if partial_items:
             pipe = HipCodecPipeline.from_codecs(codecs).evolve_from_array_spec(spec)
             temp = torch.empty((len(partial_items),) + tuple(chunk_shape),
@@ -292,7 +292,8 @@ class ChunkWriter:
             prog.launch()
             if pending is None or sharded_partial or self.chain.shard is not None:
                 prog.results()
-                prog = None
+            else:
+                deferred = prog
             if sharded_partial:
                 # per (item, inner slot): the inner chunk exists in the stored shard
                 st = prog.data.statuses()
@@ -309,7 +310,7 @@ class ChunkWriter:
             return self._encode_shards(complete_items, partial_items, v, temp, present,
                                        sharded_partial)
         self._encode_chunks(complete_items, partial_items, v, temp, pending,
-                            [prog] if partial_items and prog is not None else [])
+                            [deferred] if deferred is not None else [])
 
     def _encode_chunks(self, complete_items, partial_items, v, temp, pending=None, checks=()):
         spec = self.spec
