@@ -501,11 +501,17 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     const uint32_t grp = g - c * gpc;
     const uint32_t expected = p.g.nbytes + 4u;
     // 1. tables and the lane constant (L2 hits), the chunk header, the data blocks
-    constexpr int TV = TW / 4 / kThreads;  // uint4 table pieces per thread
+    // (six uint4 table pieces per thread, two for the byte tables; named
+    // registers -- an indexed array of them was placed in scratch)
     const uint4* gt = reinterpret_cast<const uint4*>(BT ? p.tbt_tab : p.t4w_tab);
-    uint4 tv[TV];
-#pragma unroll
-    for (int i = 0; i < TV; ++i) tv[i] = gt[t + i * kThreads];
+    const uint4 tv0 = gt[t], tv1 = gt[t + kThreads];
+    uint4 tv2, tv3, tv4, tv5;
+    if constexpr (!BT) {
+        tv2 = gt[t + 2 * kThreads];
+        tv3 = gt[t + 3 * kThreads];
+        tv4 = gt[t + 4 * kThreads];
+        tv5 = gt[t + 5 * kThreads];
+    }
     const uint32_t kq = p.t4w_kq[(size_t)grp * kThreads + t];
     const Unit U = resolve_unit(p, c * p.nseg, expected);
     const TileMapN<NT> tm = load_uniform<TileMapN<NT>>(p.tmap + (size_t)grp * NT);
@@ -521,8 +527,14 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     if (ok) stored = load_trailer_uniform(U.cp, p.g.nbytes);
     {
         uint4* st = reinterpret_cast<uint4*>(s_tab);
-#pragma unroll
-        for (int i = 0; i < TV; ++i) st[t + i * kThreads] = tv[i];
+        st[t] = tv0;
+        st[t + kThreads] = tv1;
+        if constexpr (!BT) {
+            st[t + 2 * kThreads] = tv2;
+            st[t + 3 * kThreads] = tv3;
+            st[t + 4 * kThreads] = tv4;
+            st[t + 5 * kThreads] = tv5;
+        }
     }
     // 2. per tile: wave j writes tile j into LDS in stored order, every wave
     //    reads it back in out order and stores 16-byte pieces, then takes four
@@ -858,11 +870,17 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     const uint32_t wg = blockIdx.x - c * gpc;
     const uint32_t grp = wg / PG, t0 = (wg % PG) * NT;  // the group and its first tile here
     const uint32_t expected = p.g.nbytes + 4u;
-    constexpr int TV = TW / 4 / kThreads;  // uint4 table pieces per thread
+    // (six uint4 table pieces per thread, two for the byte tables; named
+    // registers -- an indexed array of them was placed in scratch)
     const uint4* gt = reinterpret_cast<const uint4*>(BT ? p.tbt_tab : p.t4w_tab);
-    uint4 tv[TV];
-#pragma unroll
-    for (int i = 0; i < TV; ++i) tv[i] = gt[t + i * kThreads];
+    const uint4 tv0 = gt[t], tv1 = gt[t + kThreads];
+    uint4 tv2, tv3, tv4, tv5;
+    if constexpr (!BT) {
+        tv2 = gt[t + 2 * kThreads];
+        tv3 = gt[t + 3 * kThreads];
+        tv4 = gt[t + 4 * kThreads];
+        tv5 = gt[t + 5 * kThreads];
+    }
     const uint32_t kq = p.t4w_kq[(size_t)wg * kThreads + t];
     // (the two-tile form always reports in-launch: twice the workgroups per
     // chunk made the deferred verdicts' one same-address word per chunk the
@@ -889,8 +907,14 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     if (ok) stored = load_trailer_uniform(U.cp, p.g.nbytes);
     {
         uint4* st = reinterpret_cast<uint4*>(s_tab);
-#pragma unroll
-        for (int i = 0; i < TV; ++i) st[t + i * kThreads] = tv[i];
+        st[t] = tv0;
+        st[t + kThreads] = tv1;
+        if constexpr (!BT) {
+            st[t + 2 * kThreads] = tv2;
+            st[t + 3 * kThreads] = tv3;
+            st[t + 4 * kThreads] = tv4;
+            st[t + 5 * kThreads] = tv5;
+        }
     }
     const bool writes = ok || U.mode == ZHIP_ST_MISSING;
     const uint4 f = make_uint4(p.fill[0], p.fill[1], p.fill[2], p.fill[3]);
