@@ -369,7 +369,12 @@ int zhip_plan_upload(zhip_plan* p) {
     size_t n_ilw[2] = {0, 0};
     for (int i = ZHIP_TUNING ? 0 : 1; i < 2 && ilw; ++i) n_ilw[i] = kPairTabWords + (size_t)p->nseg * (1024u >> i) + kThreads;
     const size_t n_ilh = (ilw && p->il_S == 8u && 2 * p->nseg <= 64u) ? (size_t)2 * p->nseg * kThreads : 0;
-    std::vector<uint32_t> h(n_old + n_pair + n_il + n_xw + n_ilw[0] + n_ilw[1] + n_ilh);
+    // (tuning arms 69 / 70: k_decode_il with groups of 16 / 32 workgroups -- the
+    // same tables and constants for interleave strides S = 16 / 32)
+    size_t n_ils[2] = {0, 0};
+    for (int i = 0; i < 2 && ZHIP_TUNING && p->il_S == 8u; ++i)
+        if (((uint64_t)p->nseg * kDefaultBlocks) % ((16u << i) * (uint64_t)kDefaultBlocks) == 0) n_ils[i] = n_il;
+    std::vector<uint32_t> h(n_old + n_pair + n_il + n_xw + n_ilw[0] + n_ilw[1] + n_ilh + n_ils[0] + n_ils[1]);
     build_horner(h.data());
     for (int t = 0; t < kThreads; ++t) h[4096 + t] = xpow8((uint64_t)kWgStride - 16u * t);
     for (uint32_t s = 0; s < p->nseg; ++s) h[4096 + kThreads + s] = xpow8((uint64_t)s * p->seg);
@@ -387,19 +392,16 @@ int zhip_plan_upload(zhip_plan* p) {
         h[n_old + kPairTabWords + i] = gf_mul(h[4096 + kThreads + p->nseg + i], c96);
     for (int t = 0; t < kThreads; ++t)
         h[n_old + kPairTabWords + (size_t)p->nseg * kThreads + t] = gf_mul(h[4096 + t], c96);
-    p->off_il = 0;
-    if (p->il_S) {
-        // k_decode_il: workgroup r of a chunk (group r / S, offset r % S) takes
-        // steps st_k = (r / S) S 8 + r % S + S k; lane t's chain over them (stride
-        // D = 4096 S) leaves word w of step st_0 multiplied by x^(8 D 8), so the
-        // lane constant x^(8 (E - p_0 + 4096 - 8 D)) c_inv x^(-96) gives every
-        // word at p the pair kernel's x^(8 (E - p + 4096)) c_inv (p_0 = E -
-        // 4096 (n_steps - st_0) + 16 t); exponents may be negative
-        p->off_il = n_old + n_pair;
-        uint32_t* il = h.data() + p->off_il;
-        const uint64_t D = (uint64_t)kWgStride * p->il_S;
+    // k_decode_il: workgroup r of a chunk (group r / S, offset r % S) takes
+    // steps st_k = (r / S) S 8 + r % S + S k; lane t's chain over them (stride
+    // D = 4096 S) leaves word w of step st_0 multiplied by x^(8 D 8), so the
+    // lane constant x^(8 (E - p_0 + 4096 - 8 D)) c_inv x^(-96) gives every
+    // word at p the pair kernel's x^(8 (E - p + 4096)) c_inv (p_0 = E -
+    // 4096 (n_steps - st_0) + 16 t); exponents may be negative
+    auto build_il = [&](uint32_t* il, uint32_t il_S) {
+        const uint64_t D = (uint64_t)kWgStride * il_S;
         build_pair_tables(il, D);
-        const int64_t n_steps = (int64_t)p->nseg * kDefaultBlocks, K = kDefaultBlocks, S = p->il_S;
+        const int64_t n_steps = (int64_t)p->nseg * kDefaultBlocks, K = kDefaultBlocks, S = il_S;
         for (uint32_t r = 0; r < p->nseg; ++r) {
             const int64_t st0 = (int64_t)(r / S) * S * K + (int64_t)(r % S);
             for (int t = 0; t < kThreads; ++t) {
@@ -423,6 +425,11 @@ int zhip_plan_upload(zhip_plan* p) {
         for (int b = 0; b < 10; ++b) bs[22 + b] = il[kPairT3 + (1u << b)];
         for (int j = 0; j < 4; ++j)
             for (int b = 0; b < 8; ++b) bs[32 + 8 * j + b] = il[kPairA4 + 256 * j + (1u << b)];
+    };
+    p->off_il = 0;
+    if (p->il_S) {
+        p->off_il = n_old + n_pair;
+        build_il(h.data() + p->off_il, p->il_S);
     }
     p->off_xw = 0;
     if (p->xw_P) {
@@ -490,6 +497,13 @@ int zhip_plan_upload(zhip_plan* p) {
                 h[at + (size_t)uu * kThreads + t] = gf_mul(gf_mul(xe, p->c_inv), c96);
             }
         at += n_ilh;
+    }
+    for (int i = 0; i < 2; ++i) {  // (tuning arms 69 / 70)
+        p->off_il_s[i] = 0;
+        if (!n_ils[i]) continue;
+        p->off_il_s[i] = at;
+        build_il(h.data() + at, 16u << i);
+        at += n_ils[i];
     }
     if (p->d_tables) (void)hipFree(p->d_tables);
     p->d_tables = nullptr;
@@ -1059,6 +1073,16 @@ int zhip_decode_mapped(const zhip_plan* plan, const void* src, uint64_t src_size
     p.kthread11 = p.kpair11 + (size_t)plan->nseg * kThreads;
     // k_decode_il needs its tables, and a fused index check of one step per lane
     p.il_S = (plan->il_S && (n_index == 0 || plan->idx_E <= (uint32_t)kWgStride)) ? plan->il_S : 0u;
+#if ZHIP_TUNING
+    if (p.il_S && (g_tune_arm == 69 || g_tune_arm == 70) && plan->off_il_s[g_tune_arm - 69]) {
+        // groups of 16 / 32 workgroups: the plan's second / third table set
+        p.il_S = 16u << (g_tune_arm - 69);
+        p.il_tab = plan->d_tables + plan->off_il_s[g_tune_arm - 69];
+        p.il_klane = p.il_tab + kPairTabWords;
+        p.il_kidx = p.il_klane + (size_t)plan->nseg * kThreads;
+        p.il_basis = p.il_kidx + kThreads;
+    } else
+#endif
     if (p.il_S) {
         p.il_tab = plan->d_tables + plan->off_il;
         p.il_klane = p.il_tab + kPairTabWords;

@@ -463,5 +463,6 @@ struct zhip_plan {
     // off_ilw[0] (NT = 1024) / off_ilw[1] (NT = 512) with the tables of
     // A_(16 NT) | klane (nseg x NT) | kidx (256); 0: not built
     uint64_t off_ilw[2];
-    uint64_t off_ilh;  // tuning builds: k_decode_ilh's lane constants [2 nseg][kThreads] (0: none)
+    uint64_t off_ilh;
+    uint64_t off_il_s[2];  // tuning builds: k_decode_il's tables for S = 16 / 32 (arms 69 / 70; 0: none)  // tuning builds: k_decode_ilh's lane constants [2 nseg][kThreads] (0: none)
 };
