@@ -1381,7 +1381,7 @@ def test_row_map_arm_exact_and_crc(device, arm, case):
 
 
 @pytest.mark.tuning
-@pytest.mark.parametrize("arm", [49, 51, 52, 53, 54, 55, 56, 57, 58, 64, 65, 69, 70])
+@pytest.mark.parametrize("arm", [49, 51, 52, 53, 54, 55, 56, 57, 58, 64, 65, 69, 70, 71])
 def test_il_split_publication_arm(device, arm):
     """Tuning arms on k_decode_il (1 024 units, whole-chunk reads): 49, the
     split publication, and 51-53, wave priority at the run end / load issue /

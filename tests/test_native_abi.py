@@ -210,12 +210,14 @@ def test_host_copy_pool(n):
         assert dst.tobytes() == src.tobytes()
 
 
-@pytest.mark.parametrize("n", [65536, 126976, 131072, 196608, 1048576, 2 ** 21, 4100, 65552])
+@pytest.mark.parametrize("n", [65536, 126976, 131072, 196608, 524288, 1048576, 2 ** 21, 3 * 2 ** 20, 4100, 65552])
 def test_emulated_interleaved_crc_matches_oracle(n):
     """k_decode_il's decomposition (a workgroup's eight 4 KiB steps at a stride
     of S steps, A_(4096 S) tables, per-workgroup lane constants with negative
-    shifts where the stride outruns the chunk end) reproduces crc32c; layouts
-    whose step count no group of S x 8 steps tiles have no interleaved form."""
+    shifts where the stride outruns the chunk end) reproduces crc32c, with the
+    interleave the decode takes (the widest of S = 32 / 16 / 8 that tiles the
+    steps: 1 MiB chunks S = 32, 512 KiB S = 16); layouts whose step count no
+    group of S x 8 steps tiles have no interleaved form."""
     from zarr_hip import _native as N
 
     rng = np.random.default_rng(n)

@@ -369,10 +369,14 @@ int zhip_plan_upload(zhip_plan* p) {
     size_t n_ilw[2] = {0, 0};
     for (int i = ZHIP_TUNING ? 0 : 1; i < 2 && ilw; ++i) n_ilw[i] = kPairTabWords + (size_t)p->nseg * (1024u >> i) + kThreads;
     const size_t n_ilh = (ilw && p->il_S == 8u && 2 * p->nseg <= 64u) ? (size_t)2 * p->nseg * kThreads : 0;
-    // (tuning arms 69 / 70: k_decode_il with groups of 16 / 32 workgroups -- the
-    // same tables and constants for interleave strides S = 16 / 32)
+    // k_decode_il's wider interleave (round 6): groups of 16 / 32 workgroups, the
+    // same tables and constants for strides S = 16 / 32 where the chunk's steps
+    // tile them (the decode takes the widest, il_decode_S; k_encode_il keeps
+    // S = 8; tuning arms 69 / 70 / 71 force 16 / 32 / 8).  Graph-timed on the
+    // headline: S = 32 25.49 / 25.33 us vs 25.76 / 25.76 for S = 8 in two
+    // interleaved pairs (profiles/r06/f/)
     size_t n_ils[2] = {0, 0};
-    for (int i = 0; i < 2 && ZHIP_TUNING && p->il_S == 8u; ++i)
+    for (int i = 0; i < 2 && p->il_S == 8u; ++i)
         if (((uint64_t)p->nseg * kDefaultBlocks) % ((16u << i) * (uint64_t)kDefaultBlocks) == 0) n_ils[i] = n_il;
     std::vector<uint32_t> h(n_old + n_pair + n_il + n_xw + n_ilw[0] + n_ilw[1] + n_ilh + n_ils[0] + n_ils[1]);
     build_horner(h.data());
@@ -498,7 +502,7 @@ int zhip_plan_upload(zhip_plan* p) {
             }
         at += n_ilh;
     }
-    for (int i = 0; i < 2; ++i) {  // (tuning arms 69 / 70)
+    for (int i = 0; i < 2; ++i) {  // S = 16 / 32
         p->off_il_s[i] = 0;
         if (!n_ils[i]) continue;
         p->off_il_s[i] = at;
@@ -1073,17 +1077,21 @@ int zhip_decode_mapped(const zhip_plan* plan, const void* src, uint64_t src_size
     p.kthread11 = p.kpair11 + (size_t)plan->nseg * kThreads;
     // k_decode_il needs its tables, and a fused index check of one step per lane
     p.il_S = (plan->il_S && (n_index == 0 || plan->idx_E <= (uint32_t)kWgStride)) ? plan->il_S : 0u;
+    // the widest interleave the plan built (S = 32, else 16, else 8); tuning
+    // arms 69 / 70 / 71 force 16 / 32 / 8
+    int si = plan->off_il_s[1] ? 1 : plan->off_il_s[0] ? 0 : -1;
 #if ZHIP_TUNING
-    if (p.il_S && (g_tune_arm == 69 || g_tune_arm == 70) && plan->off_il_s[g_tune_arm - 69]) {
-        // groups of 16 / 32 workgroups: the plan's second / third table set
-        p.il_S = 16u << (g_tune_arm - 69);
-        p.il_tab = plan->d_tables + plan->off_il_s[g_tune_arm - 69];
+    if (g_tune_arm == 69) si = plan->off_il_s[0] ? 0 : -1;
+    if (g_tune_arm == 70) si = plan->off_il_s[1] ? 1 : -1;
+    if (g_tune_arm == 71) si = -1;
+#endif
+    if (p.il_S && si >= 0) {  // groups of 16 / 32 workgroups: the plan's second / third table set
+        p.il_S = 16u << si;
+        p.il_tab = plan->d_tables + plan->off_il_s[si];
         p.il_klane = p.il_tab + kPairTabWords;
         p.il_kidx = p.il_klane + (size_t)plan->nseg * kThreads;
         p.il_basis = p.il_kidx + kThreads;
-    } else
-#endif
-    if (p.il_S) {
+    } else if (p.il_S) {
         p.il_tab = plan->d_tables + plan->off_il;
         p.il_klane = p.il_tab + kPairTabWords;
         p.il_kidx = p.il_klane + (size_t)plan->nseg * kThreads;
@@ -1532,7 +1540,12 @@ uint32_t zhip_emulate_chunk_crc_pair(const zhip_plan* plan, const uint8_t* data)
 uint32_t zhip_emulate_chunk_crc_il(const zhip_plan* plan, const uint8_t* data) {
     std::call_once(g_once, init_tables);
     if (!plan || !plan->il_S) return 0xFFFFFFFFu;
-    const uint32_t S = plan->il_S, K = kDefaultBlocks;
+    // the interleave the decode launches take (zhip_decode_mapped): the widest
+    // that tiles the chunk's steps (the rule zhip_plan_upload builds tables by)
+    uint32_t S = plan->il_S;
+    const uint64_t n_st = (uint64_t)plan->nseg * kDefaultBlocks;
+    if (S == 8u) S = n_st % (32ull * kDefaultBlocks) == 0 ? 32u : n_st % (16ull * kDefaultBlocks) == 0 ? 16u : 8u;
+    const uint32_t K = kDefaultBlocks;
     std::vector<uint32_t> tab(kPairTabWords);
     build_pair_tables(tab.data(), (uint64_t)kWgStride * S);
     const uint32_t* T = tab.data();

@@ -608,7 +608,7 @@ int launch_decode(const DecodeParams& p, hipStream_t stream, int max_grid) {
         // 26.4 vs 27.8 us on the headline; groups of four lose to the pair
         // kernel at C4 (profiles/r03/il/).  kTuneIl / kTuneNoIl force.
         const bool il = p.il_S != 0 && crc && !(tune & (kTuneNoIl | kTuneSkipCrc | kTuneSingle | kTuneDuo)) &&
-                        ((tune & kTuneIl) || p.il_S == 8u || (ZHIP_TUNING && p.il_S >= 16u));
+                        ((tune & kTuneIl) || p.il_S >= 8u);
 #if ZHIP_TUNING
         const bool xw = p.xw != 0 && crc && (tune & kTuneXw) &&
                         !(tune & (kTuneNoXw | kTuneSkipCrc | kTuneSingle | kTuneDuo | kTuneIl));
