@@ -1376,8 +1376,12 @@ int zhip_encode_mapped(const zhip_plan* plan, const void* arr, void* dst, const 
         p.row_shift = (uint32_t)__builtin_ctz(rb);
         p.r_oy = L.out_stride[nd - 2];
         if (plan->il_S == 8u && (L.flags & ZHIP_LF_CRC)) {  // k_encode_il (launch_encode)
-            p.il_S = plan->il_S;
-            p.il_tab = plan->d_tables + plan->off_il;
+            // the decode's widest interleave (S = 32 / 16 where the steps tile
+            // it; tuning arm 73 keeps S = 8)
+            int si = plan->off_il_s[1] ? 1 : plan->off_il_s[0] ? 0 : -1;
+            if (ZHIP_TUNING && g_tune_arm == 73) si = -1;
+            p.il_S = si >= 0 ? 16u << si : plan->il_S;
+            p.il_tab = plan->d_tables + (si >= 0 ? plan->off_il_s[si] : plan->off_il);
             p.il_klane = p.il_tab + kPairTabWords;
             // whole-chunk selections: destinations computed (ZHIP_DF_WHOLE, as the
             // decode) only in tuning arm 46 -- graph-timed 29.1 vs 28.6 us on the

@@ -834,7 +834,7 @@ int launch_encode(const EncodeParams& p, hipStream_t stream, int max_grid) {
         return hipGetLastError() == hipSuccess ? ZHIP_OK : ZHIP_E_HIP;
     }
     if (p.rowmap && p.seg == (uint32_t)kWgStride * kDefaultBlocks && !(p.tune & kTunePersist) && crc &&
-        p.il_S == 8u && p.nseg <= 32u && g_tune_arm != 34) {
+        p.il_S >= 8u && p.nseg <= 32u && g_tune_arm != 34) {
         // one unit per workgroup, steps interleaved in groups of eight (k_encode_il;
         // tuning arm 34 keeps k_encode_pair)
         EncodeFn fn = pick_encode_il(p.g.itemsize, swap, p.aff_ok != 0);
