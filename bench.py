@@ -353,7 +353,7 @@ def extra_configs(ctx, args):
     if "c5" in args.extra:
         out["c5_partial_2048"] = c5_partial(ctx, args)
         torch.cuda.empty_cache()
-        if single:
+        if single and not getattr(args, "no_host_legs", False):
             out["c5_host_coalesced"] = c5_host(ctx, args)
             torch.cuda.empty_cache()
     if single and "enc" in args.extra:
@@ -759,12 +759,12 @@ def c1_plumbing(device, args):
     wall, kern = time_programs([p for p, _ in progs], max(10, args.steps // 2), 3, device)
     dec = n * 4
     t_rt = []
-    for _ in range(5):
+    for _ in range(0 if getattr(args, "no_host_legs", False) else 5):
         t0 = time.perf_counter()
         harr[...]
         t_rt.append(time.perf_counter() - t0)
     return _entry(dec, dec + 10 * ck * 4, wall, kern, checked="bytes",
-                  host_roundtrip_GiBps=round(dec / float(np.median(t_rt)) / GIB, 2),
+                  host_roundtrip_GiBps=round(dec / float(np.median(t_rt)) / GIB, 2) if t_rt else None,
                   note="device decode of 1-D chunks viewed as whole 512-byte rows (planner._split_1d; 128 units per chunk); host_roundtrip = MemoryStore -> HBM -> numpy")
 
 
@@ -933,6 +933,8 @@ def cpp_example(device, args):
     torch.cuda.empty_cache()
     # 2. host stores, full write + full read (the example's measure())
     host = {}
+    if getattr(args, "no_host_legs", False):
+        return res
     with tempfile.TemporaryDirectory() as tmp:
         for kind in ("memory", "local"):
             for label, codecs, src in (("uncompressed", [LE], plain), ("gzip6", [LE, W.GZIP6], noisy)):
@@ -1377,6 +1379,9 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--extra-only", action="store_true",
                     help="profiling runs (rocprofv3 per config line): the extra configs only, no headline")
+    ap.add_argument("--no-host-legs", action="store_true",
+                    help="profiling runs: skip the host-store legs (c5_host, the example's host reads, C1's host "
+                         "round trip), whose launches share kernels with the device-resident lines")
     ap.add_argument("--extra-cpu", default="cpu",
                     help="'cpu': time the CPU port of every config line too (N=1, rank 0); '' to skip")
     ap.add_argument("--extra", default="c1,c2,c3,c4,c5,enc,e2e,call,cpp",

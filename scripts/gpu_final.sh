@@ -32,7 +32,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/pr
 rc=$?; echo "rocprof hl rc=$rc"; [ $rc -ne 0 ] && { tail -20 "$O/prof/hl.err"; exit $rc; }
 for x in ${RUNS:-c1 c2 c3 c4 c5 enc cpp}; do
   timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof/$x" -o $x -- python bench.py --extra-only \
-    --extra $x --steps 20 > "$O/prof/$x.json" 2> "$O/prof/$x.err"
+    --extra $x --steps 20 --no-host-legs > "$O/prof/$x.json" 2> "$O/prof/$x.err"
   rc=$?; echo "rocprof $x rc=$rc"; [ $rc -ne 0 ] && { tail -20 "$O/prof/$x.err"; exit $rc; }
 done
 python scripts/rocprof_table.py "$O/bench.json" "$O/prof" "$O/frac_table.json" || exit $?
