@@ -231,6 +231,17 @@ def time_programs(progs, steps, warmup, device, ctx=None):
     return wall_max / steps, min(float(np.median(kern)), span / steps)
 
 
+def _short_steps(args) -> int:
+    """Timed launches for the device-only lines whose launch is tens of
+    microseconds (C1, C2, C3, the encodes, the example array): at least 50, so
+    the graph span per launch is not swayed by one slow first replay (the
+    rocprof traces show single launches up to 1.3x the median)."""
+    return max(50, args.steps)
+
+
+SHORT_WARMUP = 10
+
+
 def _last_kernel() -> str:
     from zarr_hip import _native as N
 
@@ -259,7 +270,7 @@ def extra_configs(ctx, args):
 
     device = ctx.device
     out = {}
-    steps = max(10, args.steps // 2)
+    steps = _short_steps(args)
     single = ctx.world == 1
     # the host-memory legs first: after the 4-16 GiB legs below the same reads
     # measured up to 2x slower in one process (caching-allocator and host
@@ -285,7 +296,7 @@ def extra_configs(ctx, args):
         progs[0][0].results()
         if not torch.equal(progs[0][1].view(torch.int32), data.view(torch.int32)):
             raise SystemExit("bench c2: decoded bytes differ from the source")
-        wall, kern = time_programs([p for p, _ in progs], steps, 3, device)
+        wall, kern = time_programs([p for p, _ in progs], steps, SHORT_WARMUP, device)
         dec = data.numel() * 4
         out["c2_unsharded_256"] = _entry(dec, dec + 64 * (1048576 + 4), wall, kern, checked="bytes")
         del progs
@@ -302,7 +313,7 @@ def extra_configs(ctx, args):
         if not torch.equal(progs[0][1].view(torch.int32), data.view(torch.int32)):
             raise SystemExit("bench sharded default chain: decoded bytes differ from the source")
         fused = progs[0][0].index is None and progs[0][0].data.n_idx == 8
-        wall, kern = time_programs([p for p, _ in progs], steps, 3, device)
+        wall, kern = time_programs([p for p, _ in progs], steps, SHORT_WARMUP, device)
         out["sharded_default_chain_256"] = _entry(
             dec, dec + 64 * 1048576 + 8 * (8 * 16 + 4), wall, kern, checked="bytes",
             kernel=_last_kernel() + (" (index checks in 8 leading workgroups)" if fused
@@ -324,7 +335,7 @@ def extra_configs(ctx, args):
         from zarr_hip import _native as N
         tile4 = bool(N.Plan(progs[0][0].tables.layout, upload=False).kernel_flags & N.PK_TILE4) and \
             not (args.tune & 65536)
-        wall, kern = time_programs([p for p, _ in progs], steps, 3, device)
+        wall, kern = time_programs([p for p, _ in progs], steps, SHORT_WARMUP, device)
         dec = data.numel() * 4
         out["c3_transpose_210"] = _entry(dec, dec + 64 * (1048576 + 4), wall, kern, checked="bytes",
                                          tile4_eligible=tile4)
@@ -341,7 +352,7 @@ def extra_configs(ctx, args):
         if not torch.equal(progs[0][1].view(torch.int32), data.view(torch.int32)):
             raise SystemExit("bench c3 (128^3 chunks): decoded bytes differ from the source")
         kf = N.Plan(progs[0][0].tables.layout, upload=False).kernel_flags
-        wall, kern = time_programs([p for p, _ in progs], steps, 3, device)
+        wall, kern = time_programs([p for p, _ in progs], steps, SHORT_WARMUP, device)
         out["c3_transpose_210_chunks128"] = _entry(
             dec, dec + 8 * (128 ** 3 * 4 + 4), wall, kern, checked="bytes",
             tileg_eligible=bool(kf & N.PK_TILEG),
@@ -487,7 +498,7 @@ def c4_partitioned(ctx, args):
             check_regions(out, data, mine, "c4")
         progs.append(prog)
     del data
-    wall, kern = time_programs(progs, 6, 2, ctx.device, ctx)
+    wall, kern = time_programs(progs, 10, 3, ctx.device, ctx)
     my_dec = mine_n * 128 ** 3 * 4
     dec = ctx.sum(my_dec)
     my_alg = my_dec + mine_n * blob
@@ -536,7 +547,7 @@ def c5_partial(ctx, args):
     prog.results()
     check_regions(out, data, batch, "c5")
     del data
-    wall, kern = time_programs([prog], max(10, args.steps // 2), 3, ctx.device, ctx)
+    wall, kern = time_programs([prog], max(20, args.steps // 2), 5, ctx.device, ctx)
     n_sel = len(batch)
     touched = len({it[0].path for it in batch})
     my_dec = n_sel * 64 ** 3 * 2
@@ -677,7 +688,7 @@ def _encode_bench(device, args, codecs, want, chunks=(64, 64, 64), check=True):
             assert t4 == (want == "tile4"), f"expected the {want} encode"
         progs.append(_EncodeProg(el))
         checks.append((store, arr, batch, offs, elen))
-    wall, kern = time_programs(progs, max(10, args.steps // 2), 3, device)
+    wall, kern = time_programs(progs, _short_steps(args), SHORT_WARMUP, device)
     kname = N.lib().zhip_last_kernel().decode()  # (mapped encodes; before the check's decodes)
     for store, arr, batch, offs, elen in (checks if check else []):  # (check=False: ablation arms)
         for (bg, *_), off in zip(batch, offs):
@@ -756,7 +767,7 @@ def c1_plumbing(device, args):
     progs[0][0].results()
     if progs[0][1].cpu().numpy().tobytes() != a.tobytes():
         raise SystemExit("bench c1: device decode differs from the source")
-    wall, kern = time_programs([p for p, _ in progs], max(10, args.steps // 2), 3, device)
+    wall, kern = time_programs([p for p, _ in progs], _short_steps(args), SHORT_WARMUP, device)
     dec = n * 4
     t_rt = []
     for _ in range(0 if getattr(args, "no_host_legs", False) else 5):
@@ -925,7 +936,7 @@ def cpp_example(device, args):
     progs[0][0].results()
     if not torch.equal(progs[0][1], data):
         raise SystemExit("bench cpp_example: decoded bytes differ from the source")
-    wall, kern = time_programs([p for p, _ in progs], max(10, args.steps // 2), 3, device)
+    wall, kern = time_programs([p for p, _ in progs], _short_steps(args), SHORT_WARMUP, device)
     alg = 2 * dec + 16 * (256 * 16 + 4)
     res["device_uncompressed"] = _entry(dec, alg, wall, kern, checked="bytes",
                                         note=f"{n_inner} inner chunks of 16 KiB + 16 index CRCs per launch")
