@@ -193,7 +193,10 @@ def _il_case(seed):
     return rng, shape, outer, dtype, codecs, fill
 
 
-@pytest.mark.parametrize("seed", range(int(os.environ.get("ZARR_HIP_FUZZ_IL", "16"))))
+_IL_FIRST = int(os.environ.get("ZARR_HIP_FUZZ_IL_FIRST", "0"))
+
+
+@pytest.mark.parametrize("seed", range(_IL_FIRST, _IL_FIRST + int(os.environ.get("ZARR_HIP_FUZZ_IL", "16"))))
 def test_random_il_geometry(device, seed):
     import zarr_hip
 
@@ -228,3 +231,105 @@ def test_random_il_geometry(device, seed):
         got = arr[sel]
         assert got.shape == want.shape, (sel, shape, chunks, codecs)
         assert got.tobytes() == np.ascontiguousarray(want).tobytes(), (sel, shape, chunks, codecs)
+
+
+def _edges(rng, extent_unit, max_edges, max_mult):
+    """A varying dimension: 1..max_edges edges, each a multiple of extent_unit."""
+    return [int(extent_unit * rng.integers(1, max_mult + 1)) for _ in range(int(rng.integers(1, max_edges + 1)))]
+
+
+def _rect_case(seed):
+    """Rectilinear chunk grids (row n3): per dimension either a regular chunk or
+    a list of edges (RLE-free, lengths repeating or not), the extent ending
+    inside the last edge (an overhanging last chunk) or on it; optionally
+    sharded (rectilinear shards whose edges are multiples of a regular inner
+    chunk, sharding.py:567-593), with a random chain (transpose, endianness,
+    crc32c) and fill."""
+    rng = np.random.default_rng(13000 + seed)
+    nd = int(rng.choice([1, 2, 2, 3]))
+    dtype = str(rng.choice(DTYPES))
+    sharded = rng.random() < 0.35
+    inner = tuple(int(rng.integers(2, 7)) for _ in range(nd)) if sharded else None
+    grid, shape = [], []
+    for d in range(nd):
+        unit = inner[d] if sharded else 1
+        if rng.random() < 0.25:  # a regular dimension
+            c = unit * int(rng.integers(1, 4 if sharded else 13))
+            grid.append(c)
+            shape.append(int(rng.integers(1, 3 * c + 1)))
+        else:
+            e = _edges(rng, unit, 4 if sharded else 6, 3 if sharded else 12)
+            grid.append(e)
+            lo = sum(e[:-1])
+            shape.append(int(rng.integers(lo + 1, lo + e[-1] + 1)))
+    endian = BE if (rng.random() < 0.3 and np.dtype(dtype).itemsize > 1) else LE
+    chain = []
+    if nd >= 2 and rng.random() < 0.3:
+        chain.append(T(tuple(int(x) for x in rng.permutation(nd))))
+    chain.append(endian)
+    if rng.random() < 0.7:
+        chain.append(CRC)
+    fill = 0
+    if np.dtype(dtype).kind == "f" and rng.random() < 0.3:
+        fill = float("nan")
+    elif rng.random() < 0.3:
+        fill = 7
+    return rng, tuple(shape), tuple(grid), inner, dtype, chain, fill
+
+
+@pytest.mark.parametrize("seed", range(int(os.environ.get("ZARR_HIP_FUZZ_RECT_FIRST", "0")),
+                                       int(os.environ.get("ZARR_HIP_FUZZ_RECT_FIRST", "0")) +
+                                       int(os.environ.get("ZARR_HIP_FUZZ_RECT", "64"))))
+def test_random_rectilinear_grid(device, seed):
+    """Seeded rectilinear parity: whole write, an array and a scalar write into
+    random selections, whole and random reads; store bytes after every write and
+    every read compared with the oracle.  A read from a device store is one
+    host synchronisation whatever the number of spec groups (pipeline.SYNCS)."""
+    import zarr_hip
+    from zarr_hip import pipeline as P
+
+    rng, shape, grid, inner, dtype, chain, fill = _rect_case(seed)
+    loc = str(rng.choice(["end", "start"]))
+    codecs = chain if inner is None else [SHARD(inner, chain, loc)]
+    meta = O.ArrayMeta(shape, grid, np.dtype(dtype), fill, codecs=codecs)
+    host = {}
+    dev = seed % 2 == 0
+    store = zarr_hip.DeviceStore(device) if dev else zarr_hip.MemoryStore()
+    if inner is None:
+        arr = zarr_hip.Array.create(store, shape, grid, dtype, fill, codecs=chain)
+    else:
+        arr = zarr_hip.Array.create(store, shape, inner, dtype, fill, codecs=chain, shards=grid, index_location=loc)
+
+    def check_store(what):
+        got = {k: bytes(v) for k, v in store.to_dict().items() if not k.endswith("zarr.json")}
+        assert sorted(got) == sorted(host), (what, shape, grid, inner, codecs)
+        for k in host:
+            assert got[k] == host[k], (what, k, shape, grid, inner, codecs)
+
+    data = _data(shape, dtype, seed)
+    O.write(host, meta, (Ellipsis,), data)
+    arr[...] = data
+    check_store("whole")
+    sel = _rand_sel(rng, shape)
+    want_shape = O.read(host, meta, sel).shape
+    val = _data(want_shape, dtype, seed + 7) if want_shape else _data((1,), dtype, seed + 7)[0]
+    O.write(host, meta, sel, val)
+    arr[sel] = val
+    check_store(("array", sel))
+    sel = _rand_sel(rng, shape)
+    sval = _data((1,), dtype, seed + 11)[0]
+    O.write(host, meta, sel, sval)
+    arr[sel] = sval
+    check_store(("scalar", sel))
+    for sel in [(Ellipsis,), _rand_sel(rng, shape), _rand_sel(rng, shape)]:
+        want = O.read(host, meta, sel)
+        got = arr[sel]
+        assert got.shape == want.shape, (sel, shape, grid, inner, codecs)
+        want = np.ascontiguousarray(want)
+        assert got.tobytes() == want.tobytes(), (sel, shape, grid, inner, codecs)
+        if dev:
+            arr.get(sel)  # plans and pooled buffers exist
+            s0 = P.SYNCS[0]
+            g = arr.get(sel)
+            assert P.SYNCS[0] - s0 == 1, (sel, P.SYNCS[0] - s0, shape, grid)
+            assert g.cpu().numpy().tobytes() == want.tobytes(), (sel, shape, grid, inner, codecs)
