@@ -5,6 +5,8 @@ its own out.  On the one-GPU box the list is [0, 0] (two workers on one card,
 the same code path as eight GPUs of a node); the union of the devices' regions
 and the gathered out are compared with the CPU oracle bit for bit."""
 
+import os
+
 import numpy as np
 import pytest
 
@@ -230,3 +232,58 @@ def test_device_store_decodes_where_its_bytes_are(device, monkeypatch, sharded):
         arr.codec_pipeline.read_sync(batch, dout)
         assert dout.cpu().numpy().tobytes() == want.tobytes()
     assert staging.D2D_COPIES[0] == before
+
+
+@pytest.mark.parametrize("seed", range(int(os.environ.get("ZARR_HIP_FUZZ_MULTI", "24"))))
+def test_random_device_list(device, monkeypatch, seed):
+    """Seeded parity of the device-list pipeline (devices [0, 0] or [0, 0, 0]):
+    the regular and rectilinear fuzz geometries (test_gpu_fuzz._case /
+    _rect_case: sharding, transposes, endianness, crc32c, edge chunks), a whole
+    write and a random write, then random reads through arr[sel] and through
+    read_sync into pre-filled host and device outs; stores and reads compared
+    with the oracle."""
+    import torch
+
+    import zarr_hip
+    from test_gpu_fuzz import _case, _rand_sel, _rect_case
+
+    monkeypatch.setenv("ZARR_HIP__DEVICES", "0,0" if seed % 2 == 0 else "0,0,0")
+    if seed % 3 == 2:
+        rng, shape, grid, inner, dtype, chain, fill = _rect_case(seed)
+        loc = str(rng.choice(["end", "start"]))
+        codecs = chain if inner is None else [SHARD(inner, chain, loc)]
+        meta = O.ArrayMeta(shape, grid, np.dtype(dtype), fill, codecs=codecs)
+        kw = {"codecs": chain} if inner is None else {"codecs": chain, "shards": grid, "index_location": loc}
+        chunks = grid if inner is None else inner
+    else:
+        rng, shape, chunks, dtype, codecs, fill = _case(seed)
+        meta = O.ArrayMeta(shape, chunks, np.dtype(dtype), fill, codecs=codecs)
+        kw = {"codecs": codecs}
+    store = zarr_hip.DeviceStore(device) if seed % 4 < 2 else zarr_hip.MemoryStore()
+    arr = zarr_hip.Array.create(store, shape, chunks, dtype, fill, **kw)
+    assert len(arr.codec_pipeline.devices) in (2, 3)
+    host: dict = {}
+    data = _data(shape, dtype, seed)
+    sel = _rand_sel(rng, shape)
+    wshape = O.read({}, meta, sel).shape
+    val = _data(wshape, dtype, seed + 3) if wshape else _data((1,), dtype, seed + 3)[0]
+    for s, v in [((Ellipsis,), data), (sel, val)]:
+        O.write(host, meta, s, v)
+        arr[s] = v
+        got = {k: bytes(b) for k, b in store.to_dict().items() if not k.endswith("zarr.json")}
+        assert got == host, (s, shape, chunks, codecs)
+    for sel in [(Ellipsis,), _rand_sel(rng, shape), _rand_sel(rng, shape)]:
+        want = O.read(host, meta, sel)
+        got = arr[sel]
+        assert got.shape == want.shape, (sel, shape, chunks, codecs)
+        want = np.ascontiguousarray(want)
+        assert got.tobytes() == want.tobytes(), (sel, shape, chunks, codecs)
+        batch, out_shape = arr.batch_info(sel)
+        if not batch or not out_shape:
+            continue
+        hout = np.full(out_shape, 3, np.dtype(dtype))
+        arr.codec_pipeline.read_sync(batch, hout)
+        assert hout.tobytes() == want.tobytes(), (sel, shape, chunks, codecs)
+        dout = torch.from_numpy(np.full(out_shape, 3, np.dtype(dtype))).to(device)
+        arr.codec_pipeline.read_sync(batch, dout)
+        assert dout.cpu().numpy().tobytes() == want.tobytes(), (sel, shape, chunks, codecs)

@@ -46,6 +46,11 @@ def test_outer_dim_and_unsplittable():
     assert device_bands(batch, 2, 1) is None  # no such out dim
     one, _ = _batch((16, 64), (16, 16), (Ellipsis,))
     assert len(device_bands(one, 4, 0)) == 1  # one band: nothing to split
+    # a scalar selection: a 0-d out has no dim to band along (found by the
+    # device-list fuzz, tests/test_gpu_multidevice.py::test_random_device_list)
+    assert outer_dim((), ()) == 0
+    scalar, shape = _batch((64, 64), (16, 16), (5, 7))
+    assert shape == () and device_bands(scalar, 2, outer_dim((), shape)) is None
 
 
 def test_devices_config():

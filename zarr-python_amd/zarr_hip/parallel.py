@@ -214,7 +214,10 @@ class GroupProgram:
 def outer_dim(strides, shape) -> int:
     """The out dim with the largest stride among dims longer than 1 (dim 0 of
     a C-order array, the last of an F-order one): bands along it are
-    contiguous byte ranges of the out."""
+    contiguous byte ranges of the out.  0 for a 0-d out (a scalar selection):
+    device_bands / item_bands find no slice there, so nothing is banded."""
+    if not shape:
+        return 0
     dims = [d for d in range(len(shape)) if shape[d] > 1] or [0]
     return max(dims, key=lambda d: abs(int(strides[d])))
 
@@ -465,6 +468,8 @@ def read_multi(pipe, batch: list, out, drop_axes: tuple):
     if t is None and h is None:
         return None
     shape = tuple(t.shape) if t is not None else h.shape
+    if not shape:  # a 0-d out (every index an integer): one element, one device
+        return None
     strides = tuple(t.stride()) if t is not None else tuple(x // h.itemsize for x in h.strides)
     dim = outer_dim(strides, shape)
     # bytes already in HBM decode where they are (no encoded bytes between GPUs)
