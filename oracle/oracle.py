@@ -428,6 +428,26 @@ def shard_decode(blob: np.ndarray, sh: ShardSpec, shard_spec: Spec) -> np.ndarra
     return out
 
 
+def shard_decode_partial(blob: np.ndarray, sh: ShardSpec, shard_spec: Spec, selection: tuple) -> np.ndarray:
+    """ShardingCodec._decode_partial_sync (sharding.py:1222-1309): the shard
+    index (its CRC checked) and only the inner chunks `selection` touches are
+    decoded -- a corrupted inner chunk outside the selection is never read.
+    Returns a shard-shaped array whose touched inner chunks hold their data
+    (the rest fill: never selected)."""
+    cps = _cps(shard_spec, sh)
+    inner_spec = Spec(sh.chunk_shape, shard_spec.dtype, shard_spec.fill_value,
+                      shard_spec.write_empty_chunks, shard_spec.order)
+    touched = {c for c, *_ in basic_indexer(selection, shard_spec.shape, sh.chunk_shape)[0]}
+    chunks = shard_reader(blob, sh, cps)
+    out = np.full(shard_spec.shape, shard_spec.fill_value, dtype=shard_spec.dtype)
+    for coords in sorted(touched):
+        raw = chunks[coords]
+        if raw is not None:
+            sel = tuple(slice(c * s, (c + 1) * s) for c, s in zip(coords, sh.chunk_shape))
+            out[sel] = chain_decode(raw, sh.inner, inner_spec)
+    return out
+
+
 def shard_encode(shard_array: np.ndarray, sh: ShardSpec, shard_spec: Spec) -> np.ndarray | None:
     """ShardingCodec._encode_sync + _build_shard_layout + _assemble_shard
     (sharding.py:716-772, 887-950)."""
@@ -751,18 +771,24 @@ class ArrayMeta:
 
 
 def read(store: dict, meta: ArrayMeta, selection: Any = Ellipsis) -> np.ndarray:
-    """Array._get_selection + FusedCodecPipeline.read_sync (per-chunk decode & scatter)."""
+    """Array._get_selection + FusedCodecPipeline.read_sync (per-chunk decode &
+    scatter; a sharding codec with no array->array / bytes->bytes codec around
+    it takes the partial-decode path, codec_pipeline.py:1136-1150, 143-166)."""
     grid = meta.chunk_shape if meta.regular else meta.dims()
     projections, out_shape = basic_indexer(selection if isinstance(selection, tuple)
                                            else (selection,), meta.shape, grid)
     out = np.empty(out_shape, dtype=meta.dtype)
     chain = meta.chain
+    partial = chain.shard is not None and not chain.aa and not chain.bb
     for coords, csel, osel, _ in projections:
         raw = store.get(meta.chunk_key(coords))
         if raw is None:
             out[osel] = meta.fill_value  # scatter_chunk(None, ...) (chunk_utils.py:106-108)
             continue
-        chunk = chain_decode(_as_u8(raw), chain, meta.chunk_spec(coords))
+        if partial:
+            chunk = shard_decode_partial(_as_u8(raw), chain.shard, meta.chunk_spec(coords), csel)
+        else:
+            chunk = chain_decode(_as_u8(raw), chain, meta.chunk_spec(coords))
         out[osel] = chunk[csel]
     return out
 

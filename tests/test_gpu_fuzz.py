@@ -333,3 +333,49 @@ def test_random_rectilinear_grid(device, seed):
             g = arr.get(sel)
             assert P.SYNCS[0] - s0 == 1, (sel, P.SYNCS[0] - s0, shape, grid)
             assert g.cpu().numpy().tobytes() == want.tobytes(), (sel, shape, grid, inner, codecs)
+
+
+@pytest.mark.parametrize("seed", range(int(os.environ.get("ZARR_HIP_FUZZ_CORRUPT", "48"))))
+def test_random_single_bit_corruption(device, seed):
+    """One flipped bit in one stored object (an inner chunk, its CRC trailer,
+    a shard index or its CRC), geometries of test_random_roundtrip (odd seeds:
+    the il geometries): a whole read and a random read raise the oracle's
+    exception with its exact message (crc32c_.py:46-49; sharding.py's index
+    check), or -- for chains without a CRC -- return the same corrupted bytes;
+    once the object is restored the same reads are exact again (nothing left
+    dirty by the failed launch: pooled buffers, arrival words, cached plans)."""
+    import zarr_hip
+
+    if seed % 2:
+        rng, shape, chunks, dtype, codecs, fill = _il_case(seed)
+    else:
+        rng, shape, chunks, dtype, codecs, fill = _case(seed)
+    meta = O.ArrayMeta(shape, chunks, np.dtype(dtype), fill, codecs=codecs)
+    store = zarr_hip.DeviceStore(device) if seed % 4 < 2 else zarr_hip.MemoryStore()
+    arr = zarr_hip.Array.create(store, shape, chunks, dtype, fill, codecs=codecs)
+    data = _data(shape, dtype, seed)
+    host: dict = {}
+    O.write(host, meta, (Ellipsis,), data)
+    arr[...] = data
+    if not host:
+        pytest.skip("every chunk is fill: nothing stored")
+    r = np.random.default_rng(7000 + seed)
+    key = sorted(host)[int(r.integers(len(host)))]
+    good = host[key]
+    bad = bytearray(good)
+    bad[int(r.integers(len(bad)))] ^= 1 << int(r.integers(8))
+    sels = [(Ellipsis,), _rand_sel(rng, shape)]
+
+    def outcome(fn):
+        try:
+            return ("ok", np.ascontiguousarray(fn()).tobytes())
+        except Exception as e:  # noqa: BLE001 -- compared type and message
+            return (type(e).__name__, str(e))
+
+    for stored in (bytes(bad), good):
+        host[key] = stored
+        store.set_sync(key, stored)
+        for sel in sels:
+            want = outcome(lambda: O.read(host, meta, sel))
+            got = outcome(lambda: arr[sel])
+            assert got == want, (key, sel, shape, chunks, codecs, got[0], want[0])
