@@ -379,3 +379,65 @@ def test_random_single_bit_corruption(device, seed):
             want = outcome(lambda: O.read(host, meta, sel))
             got = outcome(lambda: arr[sel])
             assert got == want, (key, sel, shape, chunks, codecs, got[0], want[0])
+
+
+@pytest.mark.parametrize("seed", range(int(os.environ.get("ZARR_HIP_FUZZ_CORRUPT_W", "48"))))
+def test_random_corruption_then_write(device, seed):
+    """One flipped bit in one stored object, then a random write (array or
+    scalar) over it: a write that must merge with the corrupted bytes raises
+    the oracle's exception and message (merge_and_encode_chunk decodes the
+    existing chunk, chunk_utils.py:115-190; a partial shard write decodes only
+    the touched, partially written inner chunks and carries the others' bytes
+    over verbatim, sharding.py:774-885); any other write leaves a store
+    byte-identical with the oracle's, corrupted object included, and the
+    whole read afterwards has the oracle's outcome."""
+    import zarr_hip
+
+    if seed % 2:
+        rng, shape, chunks, dtype, codecs, fill = _il_case(seed)
+    else:
+        rng, shape, chunks, dtype, codecs, fill = _case(seed)
+    meta = O.ArrayMeta(shape, chunks, np.dtype(dtype), fill, codecs=codecs)
+    store = zarr_hip.DeviceStore(device) if seed % 4 < 2 else zarr_hip.MemoryStore()
+    arr = zarr_hip.Array.create(store, shape, chunks, dtype, fill, codecs=codecs)
+    data = _data(shape, dtype, seed)
+    host: dict = {}
+    O.write(host, meta, (Ellipsis,), data)
+    arr[...] = data
+    if not host:
+        pytest.skip("every chunk is fill: nothing stored")
+    r = np.random.default_rng(9100 + seed)
+    key = sorted(host)[int(r.integers(len(host)))]
+    bad = bytearray(host[key])
+    bad[int(r.integers(len(bad)))] ^= 1 << int(r.integers(8))
+    host[key] = bytes(bad)
+    store.set_sync(key, bytes(bad))
+    sel = _rand_sel(rng, shape)
+    if r.random() < 0.5:
+        val = np.array(3, dtype=dtype)[()]
+    else:
+        shp = O.read({}, meta, sel).shape
+        val = _data(shp, dtype, seed + 5) if shp else _data((1,), dtype, seed + 5)[0]
+
+    def outcome(fn):
+        try:
+            fn()
+            return ("ok", "")
+        except Exception as e:  # noqa: BLE001 -- compared type and message
+            return (type(e).__name__, str(e))
+
+    want = outcome(lambda: O.write(host, meta, sel, val))
+    got = outcome(lambda: arr.__setitem__(sel, val))
+    assert got == want, (key, sel, shape, chunks, codecs)
+    if want[0] != "ok":
+        return  # (which other chunks a failed write stored is not specified)
+    stored = {k: bytes(v) for k, v in store.to_dict().items() if not k.endswith("zarr.json")}
+    assert stored == host, (key, sel, shape, chunks, codecs)
+
+    def read_outcome(fn):
+        try:
+            return ("ok", np.ascontiguousarray(fn()).tobytes())
+        except Exception as e:  # noqa: BLE001
+            return (type(e).__name__, str(e))
+
+    assert read_outcome(lambda: arr[...]) == read_outcome(lambda: O.read(host, meta)), (key, sel)

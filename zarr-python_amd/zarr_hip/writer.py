@@ -290,13 +290,14 @@ class ChunkWriter:
             stride0 = temp.stride(0) * temp.element_size()
             prog = pipe.prepare_read(rb, temp[0], (), np.arange(len(rb), dtype=np.int64) * stride0)
             prog.launch()
-            if pending is None or sharded_partial or self.chain.shard is not None:
+            if sharded_partial:
+                st, repairs = self._check_partial_merge(prog, partial_items, chunk_shape)
+            elif pending is None or self.chain.shard is not None:
                 prog.results()
             else:
                 deferred = prog
             if sharded_partial:
                 # per (item, inner slot): the inner chunk exists in the stored shard
-                st = prog.data.statuses()
                 n_inner = int(np.prod(self.chain.shard.chunks_per_shard(chunk_shape)))
                 present = np.zeros((len(partial_items), n_inner), bool)
                 ch = prog.tables.chunks
@@ -308,9 +309,63 @@ class ChunkWriter:
                 temp[i][tuple(csel)] = v[tuple(osel)] if v.dim() else v
         if self.chain.shard is not None:
             return self._encode_shards(complete_items, partial_items, v, temp, present,
-                                       sharded_partial)
+                                       sharded_partial, repairs if sharded_partial and partial_items else (),
+                                       raws if partial_items else None)
         self._encode_chunks(complete_items, partial_items, v, temp, pending,
                             [deferred] if deferred is not None else [])
+
+    def _check_partial_merge(self, prog, partial_items, shard_shape):
+        """The merge read of a partial shard write, checked as
+        ShardingCodec._encode_partial_sync (sharding.py:774-885) checks it: the
+        stored shard index is parsed (its CRC verified), and only the inner
+        chunks the write touches but does not cover whole are decoded (their
+        CRCs verified, merge_and_encode_chunk).  An inner chunk that fails its
+        check raises the reference's message only then; a touched, completely
+        overwritten one is replaced by the value; an untouched one is carried
+        over as stored -- its bytes copied verbatim into the new shard
+        (returned as repairs: (partial item, inner slot)).  Returns (the
+        chunk statuses, repairs)."""
+        from .pipeline import crc_error_message
+
+        st = prog.data.statuses()  # (consumes the deferred CRC verdicts)
+        ist = prog.index.statuses() if prog.index is not None else (
+            prog.data.index_statuses() if prog.data.n_idx else None)
+        if ist is not None:
+            badi = np.nonzero(ist["code"] != N.ST_OK)[0]
+            if len(badi):
+                r = ist[badi[0]]
+                raise ValueError(crc_error_message(int(r["stored"]), int(r["computed"])))
+        codes = st["code"]
+        bad = np.nonzero((codes != N.ST_OK) & (codes != N.ST_MISSING))[0]
+        repairs: list = []
+        if not len(bad):
+            return st, repairs
+        sh = self.chain.shard
+        cps = sh.chunks_per_shard(shard_shape)
+        cstr = np.array([int(np.prod(cps[d + 1:])) for d in range(len(cps))], np.int64)
+        item_of = prog.tables.item_of_chunk
+        slot_of = prog.tables.chunks["slot"].astype(np.int64)
+        touched: dict = {}
+        errors = []
+        for j in bad:
+            i = int(item_of[j])
+            if i not in touched:
+                pr = basic_projections(tuple(partial_items[i][2]), tuple(shard_shape), tuple(sh.chunk_shape))
+                touched[i] = dict(zip(((pr.coords * cstr[None, :]).sum(axis=1)).tolist(), pr.complete.tolist()))
+            s = int(slot_of[j])
+            if s not in touched[i]:
+                repairs.append((i, s))
+            elif not touched[i][s]:
+                errors.append((i, s, j))
+        if errors:
+            _, _, j = min(errors)  # the first shard of the batch, the first inner chunk of its indexer
+            r = st[j]
+            if r["code"] == N.ST_CRC_MISMATCH:
+                raise ValueError(crc_error_message(int(r["stored"]), int(r["computed"])))
+            if r["code"] == N.ST_INDEX_OOB:
+                raise ValueError("shard index entry points outside the shard blob")
+            raise ValueError("encoded chunk length does not match the fixed-size codec chain")
+        return st, repairs
 
     def _encode_chunks(self, complete_items, partial_items, v, temp, pending=None, checks=()):
         spec = self.spec
@@ -359,7 +414,8 @@ class ChunkWriter:
         lengths = [elen if (keep_all or nonempty[i]) else 0 for i in range(len(setters))]
         dest.finish(setters, lengths, spec.prototype)
 
-    def _encode_shards(self, complete_items, partial_items, v, temp, present, partial_encode):
+    def _encode_shards(self, complete_items, partial_items, v, temp, present, partial_encode,
+                       repairs=(), raws=None):
         torch = _torch()
         spec = self.spec
         chain = self.chain
@@ -447,6 +503,20 @@ class ChunkWriter:
                                              self.device, t.rows, t.tile, t.tile_prefix))
             for l in launches:
                 l.launch()
+            # untouched inner chunks that failed their check keep their stored
+            # bytes (the reference carries them over without decoding them)
+            if repairs:
+                from .nested import _host_bytes
+
+                base = len(complete_items)
+                for i, s in repairs:
+                    raw = _host_bytes(raws[i])
+                    ib = raw[:index_size] if sh.index_location == "start" else raw[len(raw) - index_size:]
+                    off, ln = (int(x) for x in np.frombuffer(ib[: 16 * n_inner].tobytes(), "<u8").reshape(n_inner, 2)[s])
+                    if ln != elen:
+                        raise ValueError("encoded chunk length does not match the fixed-size codec chain")
+                    at = int(offs[base + i]) + data_start + int(rank_of_slot[s]) * elen
+                    dest.buf[at: at + elen].copy_(torch.from_numpy(np.array(raw[off: off + ln], np.uint8)).to(dest.buf.device))
             # pack: one workgroup per shard over all launches' inner chunks
             nonempty = torch.cat([l.d_nonempty[: l.n] for l in launches])
             pflags = (N.PF_INDEX_START if sh.index_location == "start" else 0) | \
