@@ -58,6 +58,8 @@ def normalize_selection(selection, shape: tuple[int, ...]) -> tuple:
                 raise IndexError(f"index out of bounds for dimension with length {n}")
             out.append(i)
         elif isinstance(s, slice):
+            if s.step == 0:  # slice.indices raises first (indexing.py:408)
+                raise ValueError("slice step cannot be zero")
             if s.step is not None and s.step < 1:
                 raise IndexError("only slices with step >= 1 are supported.")
             out.append(slice(*s.indices(n)))
