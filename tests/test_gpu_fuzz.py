@@ -441,3 +441,56 @@ def test_random_corruption_then_write(device, seed):
             return (type(e).__name__, str(e))
 
     assert read_outcome(lambda: arr[...]) == read_outcome(lambda: O.read(host, meta)), (key, sel)
+
+
+def _with_gzip(rng, codecs):
+    """A gzip (numcodecs.GZip restated by the oracle, mtime 0) inserted after the
+    bytes codec -- before or after a crc32c -- of the chain, or of the shard's
+    inner chain, or (sharded, 1 in 4) around the whole sharding codec."""
+    gz = {"name": "gzip", "configuration": {"level": int(rng.integers(1, 10))}}
+    if codecs and codecs[0].get("name") == "sharding_indexed":
+        if rng.random() < 0.25:
+            return codecs + [gz]
+        inner = list(codecs[0]["configuration"]["codecs"])
+        cfg = dict(codecs[0]["configuration"], codecs=_with_gzip(rng, inner))
+        return [dict(codecs[0], configuration=cfg)]
+    pos = next(i for i, c in enumerate(codecs) if c.get("name") == "bytes") + 1
+    pos += int(rng.integers(0, len(codecs) - pos + 1))
+    return codecs[:pos] + [gz] + codecs[pos:]
+
+
+@pytest.mark.parametrize("seed", range(int(os.environ.get("ZARR_HIP_FUZZ_GZ", "24"))))
+def test_random_compressed_roundtrip(device, seed):
+    """test_random_roundtrip's geometries with a compressor in the chain: the
+    host stage (gzip) beside the GPU chain, whole and random writes, whole and
+    random reads, stores byte-identical with the oracle's."""
+    import zarr_hip
+
+    rng, shape, chunks, dtype, codecs, fill = _case(seed)
+    codecs = _with_gzip(rng, codecs)
+    meta = O.ArrayMeta(shape, chunks, np.dtype(dtype), fill, codecs=codecs)
+    store = zarr_hip.DeviceStore(device) if seed % 2 == 0 else zarr_hip.MemoryStore()
+    arr = zarr_hip.Array.create(store, shape, chunks, dtype, fill, codecs=codecs)
+    host: dict = {}
+
+    def check_store(what):
+        got = {k: bytes(v) for k, v in store.to_dict().items() if not k.endswith("zarr.json")}
+        assert sorted(got) == sorted(host), (what, shape, chunks, codecs)
+        for k in host:
+            assert got[k] == host[k], (what, k, shape, chunks, codecs)
+
+    data = _data(shape, dtype, seed)
+    O.write(host, meta, (Ellipsis,), data)
+    arr[...] = data
+    check_store("whole")
+    sel = _rand_sel(rng, shape)
+    wshape = O.read(host, meta, sel).shape
+    val = _data(wshape, dtype, seed + 7) if wshape else _data((1,), dtype, seed + 7)[0]
+    O.write(host, meta, sel, val)
+    arr[sel] = val
+    check_store(("array", sel))
+    for sel in [(Ellipsis,), _rand_sel(rng, shape), _rand_sel(rng, shape)]:
+        want = O.read(host, meta, sel)
+        got = arr[sel]
+        assert got.shape == want.shape, (sel, shape, chunks, codecs)
+        assert got.tobytes() == np.ascontiguousarray(want).tobytes(), (sel, shape, chunks, codecs)
