@@ -489,8 +489,92 @@ def test_random_compressed_roundtrip(device, seed):
     O.write(host, meta, sel, val)
     arr[sel] = val
     check_store(("array", sel))
+    sel = (Ellipsis,) if rng.random() < 0.3 else _rand_sel(rng, shape)  # (whole: every chunk emptied)
+    sval = np.array(fill if rng.random() < 0.5 else 3, dtype=dtype)[()]
+    O.write(host, meta, sel, sval)
+    arr[sel] = sval
+    check_store(("scalar", sel))
     for sel in [(Ellipsis,), _rand_sel(rng, shape), _rand_sel(rng, shape)]:
         want = O.read(host, meta, sel)
         got = arr[sel]
         assert got.shape == want.shape, (sel, shape, chunks, codecs)
         assert got.tobytes() == np.ascontiguousarray(want).tobytes(), (sel, shape, chunks, codecs)
+
+
+def _nested_case(seed):
+    """Nested sharding (suite:308-320 generalised): inner chunks c2, inner
+    shards c1 = k1 * c2 whose codec is itself sharding_indexed, outer shards
+    c0 = k0 * c1; random chain, index locations, dtype, fill, edge shards."""
+    rng = np.random.default_rng(17000 + seed)
+    nd = int(rng.choice([1, 2, 2, 3]))
+    dtype = str(rng.choice(DTYPES))
+    c2 = tuple(int(rng.integers(2, 6)) for _ in range(nd))
+    c1 = tuple(c * int(rng.integers(1, 4)) for c in c2)
+    c0 = tuple(c * int(rng.integers(1, 4)) for c in c1)
+    shape = tuple(int(rng.integers(1, int(2.5 * c) + 2)) for c in c0)
+    endian = BE if (rng.random() < 0.3 and np.dtype(dtype).itemsize > 1) else LE
+    chain = [endian] + ([CRC] if rng.random() < 0.7 else [])
+    inner_shard = SHARD(c2, chain, str(rng.choice(["end", "start"])))
+    codecs = [SHARD(c1, [inner_shard], str(rng.choice(["end", "start"])))]
+    fill = float("nan") if (np.dtype(dtype).kind == "f" and rng.random() < 0.3) else (7 if rng.random() < 0.3 else 0)
+    return rng, shape, c0, dtype, codecs, fill
+
+
+@pytest.mark.parametrize("seed", range(int(os.environ.get("ZARR_HIP_FUZZ_NESTED", "24"))))
+def test_random_nested_sharding(device, seed):
+    """Whole, array and scalar writes, whole and random reads of nested-sharded
+    arrays (the outer level routed on the host, zarr_hip/nested.py; the inner
+    shards on the GPU), stores and reads compared with the oracle."""
+    import zarr_hip
+
+    rng, shape, chunks, dtype, codecs, fill = _nested_case(seed)
+    meta = O.ArrayMeta(shape, chunks, np.dtype(dtype), fill, codecs=codecs)
+    store = zarr_hip.DeviceStore(device) if seed % 2 == 0 else zarr_hip.MemoryStore()
+    arr = zarr_hip.Array.create(store, shape, chunks, dtype, fill, codecs=codecs)
+    host: dict = {}
+
+    def check_store(what):
+        got = {k: bytes(v) for k, v in store.to_dict().items() if not k.endswith("zarr.json")}
+        assert sorted(got) == sorted(host), (what, shape, chunks, codecs)
+        for k in host:
+            assert got[k] == host[k], (what, k, shape, chunks, codecs)
+
+    data = _data(shape, dtype, seed)
+    O.write(host, meta, (Ellipsis,), data)
+    arr[...] = data
+    check_store("whole")
+    sel = _rand_sel(rng, shape)
+    wshape = O.read(host, meta, sel).shape
+    val = _data(wshape, dtype, seed + 7) if wshape else _data((1,), dtype, seed + 7)[0]
+    O.write(host, meta, sel, val)
+    arr[sel] = val
+    check_store(("array", sel))
+    sel = _rand_sel(rng, shape)
+    sval = np.array(fill if rng.random() < 0.5 else 3, dtype=dtype)[()]
+    O.write(host, meta, sel, sval)
+    arr[sel] = sval
+    check_store(("scalar", sel))
+    for sel in [(Ellipsis,), _rand_sel(rng, shape), _rand_sel(rng, shape)]:
+        want = O.read(host, meta, sel)
+        got = arr[sel]
+        assert got.shape == want.shape, (sel, shape, chunks, codecs)
+        assert got.tobytes() == np.ascontiguousarray(want).tobytes(), (sel, shape, chunks, codecs)
+
+
+@pytest.mark.parametrize("kind", ["device", "memory"])
+def test_nested_whole_fill_write_deletes_shards(kind, device):
+    """A complete write of the fill value over nested-sharded data (found by
+    test_random_nested_sharding): every outer shard is deleted, as the
+    reference deletes an empty shard (sharding.py:882-883) -- it was left
+    holding the old bytes, so a read returned the old data instead of fill."""
+    import zarr_hip
+
+    inner = SHARD((4, 4), [LE, CRC])
+    codecs = [SHARD((8, 8), [inner])]
+    store = zarr_hip.DeviceStore(device) if kind == "device" else zarr_hip.MemoryStore()
+    arr = zarr_hip.Array.create(store, (32, 16), (16, 16), "float32", 0.0, codecs=codecs)
+    arr[...] = _data((32, 16), "float32", 1)
+    assert len([k for k in store.to_dict() if not k.endswith("zarr.json")]) == 2
+    arr[...] = np.float32(0.0)
+    assert [k for k in store.to_dict() if not k.endswith("zarr.json")] == []
+    assert not np.asarray(arr[...]).any()

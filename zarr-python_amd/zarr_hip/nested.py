@@ -192,15 +192,17 @@ def write_sync(pipe, outer: ShardingCodec, batch: list, value, drop_axes: tuple 
             io = _Cell(parts[cell])
             touched[cell] = io
             items.append((io, spec_in, c_csel, _compose(tuple(osel), c_osel), c_complete))
-        plans.append((bg, sp, cps, tr, parts, touched, old is not None))
+        plans.append((bg, sp, cps, tr, parts, touched))
     if items:
         inner.write_sync(items, value, drop_axes)
-    for bg, sp, cps, tr, parts, touched, existed in plans:
+    for bg, sp, cps, tr, parts, touched in plans:
         for cell, io in touched.items():
             parts[cell] = None if io.value is None else np.frombuffer(io.value, np.uint8)
         if all(p is None for p in parts):
-            if existed:
-                bg.delete_sync()
+            # deleted whether or not it was read first: a complete write (not
+            # read) of nothing but empty inner shards replaces whatever the key
+            # held (sharding.py:882-883 deletes unconditionally)
+            bg.delete_sync()
             continue
         order = subchunk_order(tuple(cps), outer.subchunk_write_order)
         strides = np.array([int(np.prod(cps[d + 1:])) for d in range(len(cps))], np.int64)
