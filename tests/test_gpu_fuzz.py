@@ -578,3 +578,45 @@ def test_nested_whole_fill_write_deletes_shards(kind, device):
     arr[...] = np.float32(0.0)
     assert [k for k in store.to_dict() if not k.endswith("zarr.json")] == []
     assert not np.asarray(arr[...]).any()
+
+
+@pytest.mark.parametrize("seed", range(int(os.environ.get("ZARR_HIP_FUZZ_STORES", "24"))))
+def test_random_roundtrip_file_and_pinned_stores(device, tmp_path, seed):
+    """test_random_roundtrip's geometries on the two other stores: LocalStore
+    (files: pread into pinned windows, writes as files) and PinnedMemoryStore
+    (page-locked arena: DMA straight from it, writes into it); whole, array and
+    scalar writes, whole and random reads, stores and reads as the oracle's."""
+    import zarr_hip
+
+    rng, shape, chunks, dtype, codecs, fill = _case(seed)
+    meta = O.ArrayMeta(shape, chunks, np.dtype(dtype), fill, codecs=codecs)
+    store = zarr_hip.LocalStore(str(tmp_path)) if seed % 2 == 0 else zarr_hip.PinnedMemoryStore()
+    arr = zarr_hip.Array.create(store, shape, chunks, dtype, fill, codecs=codecs)
+    host: dict = {}
+
+    def check_store(what):
+        got = {k: bytes(v) for k, v in store.to_dict().items() if not k.endswith("zarr.json")}
+        assert sorted(got) == sorted(host), (what, shape, chunks, codecs)
+        for k in host:
+            assert got[k] == host[k], (what, k, shape, chunks, codecs)
+
+    data = _data(shape, dtype, seed)
+    O.write(host, meta, (Ellipsis,), data)
+    arr[...] = data
+    check_store("whole")
+    sel = _rand_sel(rng, shape)
+    wshape = O.read(host, meta, sel).shape
+    val = _data(wshape, dtype, seed + 7) if wshape else _data((1,), dtype, seed + 7)[0]
+    O.write(host, meta, sel, val)
+    arr[sel] = val
+    check_store(("array", sel))
+    sel = (Ellipsis,) if rng.random() < 0.3 else _rand_sel(rng, shape)
+    sval = np.array(fill if rng.random() < 0.5 else 3, dtype=dtype)[()]
+    O.write(host, meta, sel, sval)
+    arr[sel] = sval
+    check_store(("scalar", sel))
+    for sel in [(Ellipsis,), _rand_sel(rng, shape), _rand_sel(rng, shape)]:
+        want = O.read(host, meta, sel)
+        got = arr[sel]
+        assert got.shape == want.shape, (sel, shape, chunks, codecs)
+        assert got.tobytes() == np.ascontiguousarray(want).tobytes(), (sel, shape, chunks, codecs)
