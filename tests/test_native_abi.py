@@ -304,3 +304,32 @@ def test_tuning_build_refused_in_product_path(tmp_path):
     code = "import sys; sys.path.insert(0, %r); from zarr_hip import _native as N; N.lib()" % str(tmp_path)
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode != 0 and "tuning build" in r.stderr, r.stderr
+
+
+def test_non_basic_selections_refused_by_name():
+    """zarr's orthogonal / coordinate / mask indexers hand integer arrays or
+    masks: the pipeline refuses them with NotImplementedError naming the
+    reason (BasicIndexer selections), not a TypeError from
+    the planner; slices and integers (numpy ones included) pass."""
+    import numpy as np
+
+    from zarr_hip.pipeline import normalize_batch
+    from zarr_hip.spec import ArraySpec
+
+    class Spec:  # a foreign (zarr-like) spec object: takes the coercing path
+        def __init__(self, s):
+            self.s = s
+
+    spec = ArraySpec((4, 4), np.dtype("float32"), 0.0)
+    import zarr_hip.pipeline as P
+
+    orig = P.coerce_spec
+    P.coerce_spec = lambda s: s.s
+    try:
+        ok = normalize_batch([(None, Spec(spec), (slice(0, 4, 1), np.int64(2)), (slice(0, 4, 1),), False)])
+        assert ok[0][1] is spec
+        for bad in (np.array([0, 2]), [1, 3], np.array([True, False, True, False])):
+            with pytest.raises(NotImplementedError, match="BasicIndexer"):
+                normalize_batch([(None, Spec(spec), (slice(0, 4, 1), bad), (slice(0, 4, 1), slice(0, 2, 1)), False)])
+    finally:
+        P.coerce_spec = orig

@@ -1619,11 +1619,27 @@ def normalize_batch(batch_info: Iterable) -> list:
     seen: dict = {}  # one coerced spec per caller spec object (a regular grid shares one)
     for it in items:
         it = tuple(it)
+        _check_basic(it[2])
+        _check_basic(it[3])
         sp = seen.get(id(it[1]))
         if sp is None:
             sp = seen[id(it[1])] = coerce_spec(it[1])
         out.append((it[0], sp) + it[2:])
     return out
+
+
+def _check_basic(selection) -> None:
+    """The GPU path takes BasicIndexer selections (SURVEY §8 a16,
+    indexing.py:571-621): per dim a slice or an integer.  zarr's orthogonal,
+    coordinate and mask indexers (OrthogonalIndexer, CoordinateIndexer,
+    MaskIndexer: indexing.py:902-1046, 1171-1400) hand integer arrays or
+    boolean masks; those are refused here, by name, instead of failing
+    somewhere in the planner."""
+    for s in selection:
+        if not isinstance(s, (slice, int, np.integer)):
+            raise NotImplementedError(
+                "only BasicIndexer selections (slices and integers) are on the GPU path; got "
+                f"{type(s).__name__} (zarr's orthogonal / coordinate / mask selections are not)")
 
 
 def _spec_key(spec: ArraySpec) -> tuple:
