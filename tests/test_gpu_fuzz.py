@@ -620,3 +620,62 @@ def test_random_roundtrip_file_and_pinned_stores(device, tmp_path, seed):
         got = arr[sel]
         assert got.shape == want.shape, (sel, shape, chunks, codecs)
         assert got.tobytes() == np.ascontiguousarray(want).tobytes(), (sel, shape, chunks, codecs)
+
+
+@pytest.mark.parametrize("seed", range(int(os.environ.get("ZARR_HIP_FUZZ_VIEWS", "24"))))
+def test_read_sync_into_views(device, seed):
+    """read_sync straight into caller outs that are views: an offset window of
+    a larger tensor, a stepped view, a transposed (F-order-like) view, and a
+    numpy host view; the regions the batch selects equal the oracle's and every
+    other byte of the underlying buffer is untouched -- or the read is refused
+    with an error, never silently misplaced."""
+    import torch
+
+    import zarr_hip
+
+    rng, shape, chunks, dtype, codecs, fill = _case(seed)
+    meta = O.ArrayMeta(shape, chunks, np.dtype(dtype), fill, codecs=codecs)
+    store = zarr_hip.DeviceStore(device) if seed % 2 == 0 else zarr_hip.MemoryStore()
+    arr = zarr_hip.Array.create(store, shape, chunks, dtype, fill, codecs=codecs)
+    host: dict = {}
+    data = _data(shape, dtype, seed)
+    O.write(host, meta, (Ellipsis,), data)
+    arr[...] = data
+    sel = _rand_sel(rng, shape) if rng.random() < 0.6 else (Ellipsis,)
+    batch, out_shape = arr.batch_info(sel)
+    if not out_shape or not batch:
+        pytest.skip("scalar selection")
+    want = np.ascontiguousarray(O.read(host, meta, sel))
+    tdt = torch.from_numpy(np.zeros(1, dtype)).dtype
+    sentinel = np.array(5, dtype)
+    nd = len(out_shape)
+    kind = ["window", "stepped", "transposed", "host_window"][seed % 4]
+    if kind == "transposed":
+        base = torch.full(tuple(reversed(out_shape)), 5, dtype=tdt, device=device)
+        view = base.permute(*reversed(range(nd)))
+    else:
+        big = tuple(n * (2 if (kind == "stepped" and d == 0) else 1) + 3 for d, n in enumerate(out_shape))
+        base_np = np.full(big, sentinel)
+        base = base_np if kind == "host_window" else torch.from_numpy(base_np).to(device)
+        if kind == "stepped":
+            view = base[tuple(slice(1, 1 + 2 * n, 2) if d == 0 else slice(2, 2 + n) for d, n in enumerate(out_shape))]
+        else:
+            view = base[tuple(slice(2, 2 + n) for n in out_shape)]
+    try:
+        arr.codec_pipeline.read_sync(batch, view)
+    except (NotImplementedError, ValueError):
+        return  # refused: acceptable, as long as nothing was written (checked below)
+    else:
+        got = view.cpu().numpy() if isinstance(view, torch.Tensor) else view
+        assert np.ascontiguousarray(got).tobytes() == want.tobytes(), (kind, sel, shape, chunks, codecs)
+    finally:
+        b = base.cpu().numpy() if isinstance(base, torch.Tensor) else base
+        mask = np.ones(b.shape, bool)
+        if kind == "transposed":
+            mask[...] = False
+        elif kind == "stepped":
+            mask[tuple(slice(1, 1 + 2 * n, 2) if d == 0 else slice(2, 2 + n) for d, n in enumerate(out_shape))] = False
+        else:
+            mask[tuple(slice(2, 2 + n) for n in out_shape)] = False
+        outside = b[mask]
+        assert (outside.view(np.uint8) == np.full(outside.shape, sentinel).view(np.uint8)).all(), (kind, sel)
