@@ -679,3 +679,47 @@ def test_read_sync_into_views(device, seed):
             mask[tuple(slice(2, 2 + n) for n in out_shape)] = False
         outside = b[mask]
         assert (outside.view(np.uint8) == np.full(outside.shape, sentinel).view(np.uint8)).all(), (kind, sel)
+
+
+@pytest.mark.parametrize("seed", range(int(os.environ.get("ZARR_HIP_FUZZ_VIEWS", "24"))))
+def test_write_from_views(device, seed):
+    """Array writes whose value is a view: an offset window, a stepped view
+    and a transposed view of a larger array, as numpy (host) or torch (device)
+    -- the encode reads the value through its strides; stores equal the
+    oracle's (which is given the same values, contiguous)."""
+    import torch
+
+    import zarr_hip
+
+    rng, shape, chunks, dtype, codecs, fill = _case(seed)
+    meta = O.ArrayMeta(shape, chunks, np.dtype(dtype), fill, codecs=codecs)
+    store = zarr_hip.DeviceStore(device) if seed % 2 == 0 else zarr_hip.MemoryStore()
+    arr = zarr_hip.Array.create(store, shape, chunks, dtype, fill, codecs=codecs)
+    host: dict = {}
+    for sel in [(Ellipsis,), _rand_sel(rng, shape)]:
+        vshape = O.read(host, meta, sel).shape
+        if not vshape:
+            continue
+        nd = len(vshape)
+        src = _data((2 * max(vshape) + 3,) * nd, dtype, seed + len(host))  # every view fits
+        kind = ["window", "stepped", "transposed"][int(rng.integers(0, 3))]
+        if kind == "window":
+            v = src[tuple(slice(1, 1 + n) for n in vshape)]
+        elif kind == "stepped":
+            v = src[tuple(slice(0, 2 * n, 2) for n in vshape)]
+        else:
+            t = np.ascontiguousarray(src[tuple(slice(0, n) for n in reversed(vshape))])
+            v = t.transpose(tuple(reversed(range(nd))))
+        assert v.shape == vshape
+        val = torch.from_numpy(np.ascontiguousarray(src)).to(device) if rng.random() < 0.5 else None
+        if val is not None:  # the same view taken of a device tensor
+            if kind == "window":
+                val = val[tuple(slice(1, 1 + n) for n in vshape)]
+            elif kind == "stepped":
+                val = val[tuple(slice(0, 2 * n, 2) for n in vshape)]
+            else:
+                val = torch.from_numpy(np.ascontiguousarray(t)).to(device).permute(*reversed(range(nd)))
+        O.write(host, meta, sel, np.ascontiguousarray(v))
+        arr[sel] = v if val is None else val
+        got = {k: bytes(b) for k, b in store.to_dict().items() if not k.endswith("zarr.json")}
+        assert got == host, (kind, sel, shape, chunks, codecs, val is not None)
