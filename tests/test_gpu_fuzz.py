@@ -723,3 +723,46 @@ def test_write_from_views(device, seed):
         arr[sel] = v if val is None else val
         got = {k: bytes(b) for k, b in store.to_dict().items() if not k.endswith("zarr.json")}
         assert got == host, (kind, sel, shape, chunks, codecs, val is not None)
+
+
+@pytest.mark.parametrize("kind", ["device", "memory"])
+@pytest.mark.parametrize("codecs_name", ["plain", "crc", "sharded"])
+def test_empty_and_degenerate_shapes(kind, codecs_name, device):
+    """Degenerate cases the reference handles: a zero-length dimension (no
+    chunk exists; reads return empty arrays, writes store nothing), empty
+    selections (arr[3:3], a step past the end), a one-element array, chunks
+    larger than the array; stores and reads as the oracle's / numpy's."""
+    import zarr_hip
+
+    chains = {"plain": [LE], "crc": [LE, CRC]}
+    for shape, chunks in [((0, 5), (4, 4)), ((1,), (1,)), ((3, 2), (8, 8)), ((5, 0, 2), (2, 2, 2))]:
+        if codecs_name == "sharded":
+            inner = tuple(max(1, c // 2) for c in chunks)
+            codecs = [SHARD(inner, [LE, CRC])]
+        else:
+            codecs = chains[codecs_name]
+        meta = O.ArrayMeta(shape, chunks, np.dtype("float32"), 1.5, codecs=codecs)
+        store = zarr_hip.DeviceStore(device) if kind == "device" else zarr_hip.MemoryStore()
+        arr = zarr_hip.Array.create(store, shape, chunks, "float32", 1.5, codecs=codecs)
+        host: dict = {}
+        data = _data(shape, "float32", 3)
+        O.write(host, meta, (Ellipsis,), data)
+        arr[...] = data
+        got = {k: bytes(v) for k, v in store.to_dict().items() if not k.endswith("zarr.json")}
+        assert got == host, (shape, chunks, codecs)
+        full = O.read(host, meta)
+        assert np.asarray(arr[...]).shape == full.shape
+        assert np.asarray(arr[...]).tobytes() == full.tobytes()
+        nd = len(shape)
+        for sel in [(slice(3, 3),) + (slice(None),) * (nd - 1), (slice(shape[0] + 5, None),) + (slice(None),) * (nd - 1),
+                    (slice(0, shape[0], 7),) + (slice(None),) * (nd - 1)]:
+            want = full[sel]
+            g = arr[sel]
+            assert g.shape == want.shape, (shape, sel)
+            assert np.ascontiguousarray(g).tobytes() == np.ascontiguousarray(want).tobytes(), (shape, sel)
+            if want.size:
+                continue
+            arr[sel] = np.zeros(want.shape, np.float32)  # an empty write stores nothing
+            O.write(host, meta, sel, np.zeros(want.shape, np.float32))
+            got = {k: bytes(v) for k, v in store.to_dict().items() if not k.endswith("zarr.json")}
+            assert got == host, (shape, sel)
