@@ -766,3 +766,75 @@ def test_empty_and_degenerate_shapes(kind, codecs_name, device):
             O.write(host, meta, sel, np.zeros(want.shape, np.float32))
             got = {k: bytes(v) for k, v in store.to_dict().items() if not k.endswith("zarr.json")}
             assert got == host, (shape, sel)
+
+
+@pytest.mark.parametrize("seed", range(int(os.environ.get("ZARR_HIP_FUZZ_TSHARD", "24"))))
+def test_random_transpose_around_shards(device, seed):
+    """A transpose OUTSIDE the sharding codec ([transpose, sharding_indexed]):
+    the sharding codec is no longer alone, so the reference reads and writes
+    whole shards (no partial decode / encode, codec_pipeline.py:143-166); whole,
+    array and scalar writes and random reads against the oracle."""
+    import zarr_hip
+
+    rng = np.random.default_rng(23000 + seed)
+    nd = int(rng.choice([2, 3]))
+    dtype = str(rng.choice(DTYPES))
+    inner = tuple(int(rng.integers(2, 7)) for _ in range(nd))
+    chunks = tuple(i * int(rng.integers(1, 4)) for i in inner)
+    perm = tuple(int(x) for x in rng.permutation(nd))
+    # ShardingCodec.validate checks the inner chunk against the array's own
+    # (untransposed) chunk edges (sharding.py:567-595), while the codec then
+    # tiles the transposed shard: a valid inner edge divides both
+    import math
+
+    if seed % 2 == 0:
+        inner_t = tuple(math.gcd(chunks[d], chunks[perm[d]]) for d in range(nd))
+    else:
+        inner_t = tuple(int(rng.integers(1, 7)) for _ in range(nd))
+        bad = [d for d in range(nd) if chunks[d] % inner_t[d]]
+        if bad:  # the reference refuses it at validation, and so must we, with its message
+            d = bad[0]
+            with pytest.raises(ValueError) as e:
+                zarr_hip.Array.create(zarr_hip.MemoryStore(), tuple(2 * c for c in chunks), chunks, dtype, 0,
+                                      codecs=[T(perm), SHARD(inner_t, [LE])])
+            assert str(e.value) == (f"Chunk edge length {chunks[d]} in dimension {d} is not divisible by the "
+                                    f"shard's inner chunk size {inner_t[d]}.")
+            return
+        if any(chunks[perm[d]] % inner_t[d] for d in range(nd)):
+            pytest.skip("valid for ShardingCodec.validate, not a tiling of the transposed shard")
+    shape = tuple(int(rng.integers(1, 3 * c + 2)) for c in chunks)
+    endian = BE if (rng.random() < 0.3 and np.dtype(dtype).itemsize > 1) else LE
+    codecs = [T(perm), SHARD(inner_t, [endian] + ([CRC] if rng.random() < 0.7 else []),
+                             str(rng.choice(["end", "start"])))]
+    fill = float("nan") if (np.dtype(dtype).kind == "f" and rng.random() < 0.3) else (7 if rng.random() < 0.3 else 0)
+    meta = O.ArrayMeta(shape, chunks, np.dtype(dtype), fill, codecs=codecs)
+    store = zarr_hip.DeviceStore(device) if seed % 2 == 0 else zarr_hip.MemoryStore()
+    arr = zarr_hip.Array.create(store, shape, chunks, dtype, fill, codecs=codecs)
+    host: dict = {}
+
+    def check_store(what):
+        got = {k: bytes(v) for k, v in store.to_dict().items() if not k.endswith("zarr.json")}
+        assert sorted(got) == sorted(host), (what, shape, chunks, codecs)
+        for k in host:
+            assert got[k] == host[k], (what, k, shape, chunks, codecs)
+
+    data = _data(shape, dtype, seed)
+    O.write(host, meta, (Ellipsis,), data)
+    arr[...] = data
+    check_store("whole")
+    sel = _rand_sel(rng, shape)
+    wshape = O.read(host, meta, sel).shape
+    val = _data(wshape, dtype, seed + 7) if wshape else _data((1,), dtype, seed + 7)[0]
+    O.write(host, meta, sel, val)
+    arr[sel] = val
+    check_store(("array", sel))
+    sel = _rand_sel(rng, shape)
+    sval = np.array(fill if rng.random() < 0.5 else 3, dtype=dtype)[()]
+    O.write(host, meta, sel, sval)
+    arr[sel] = sval
+    check_store(("scalar", sel))
+    for sel in [(Ellipsis,), _rand_sel(rng, shape), _rand_sel(rng, shape)]:
+        want = O.read(host, meta, sel)
+        got = arr[sel]
+        assert got.shape == want.shape, (sel, shape, chunks, codecs)
+        assert got.tobytes() == np.ascontiguousarray(want).tobytes(), (sel, shape, chunks, codecs)
