@@ -889,10 +889,13 @@ class HipCodecPipeline:
 
     @classmethod
     def from_codecs(cls, codecs: Iterable, *, batch_size: int | None = None,
-                    devices=None) -> "HipCodecPipeline":
+                    devices=None, warn: bool = True) -> "HipCodecPipeline":
+        """warn=False: the package's own internal pipelines over an array's
+        codecs (the writer's merge read) skip the advisory zarr already gave
+        when the array was made."""
         codecs = tuple(codecs)
         cl = tuple(parse_codecs(codecs))
-        if any(isinstance(c, ShardingCodec) for c in cl) and len(cl) > 1:
+        if warn and any(isinstance(c, ShardingCodec) for c in cl) and len(cl) > 1:
             # codecs_from_list's advisory (codec_pipeline.py:859-883)
             warnings.warn("Combining a `sharding_indexed` codec disables partial reads and writes, which "
                           "may lead to inefficient performance.", UserWarning, stacklevel=2)

@@ -281,11 +281,7 @@ class ChunkWriter:
         present = None
         deferred = None  # the merge read, when its check is left to `pending`
         if partial_items:
-            import warnings
-
-            with warnings.catch_warnings():  # (codecs_from_list's warning was given when the array was made)
-                warnings.simplefilter("ignore", UserWarning)
-                pipe = HipCodecPipeline.from_codecs(codecs).evolve_from_array_spec(spec)
+            pipe = HipCodecPipeline.from_codecs(codecs, warn=False).evolve_from_array_spec(spec)
             temp = torch.empty((len(partial_items),) + tuple(chunk_shape),
                                dtype=torch_dtype(spec.dtype), device=self.device)
             full = tuple(slice(0, s, 1) for s in chunk_shape)
