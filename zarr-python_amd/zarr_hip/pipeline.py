@@ -80,7 +80,7 @@ def _pool_take(kind: str, n: int, device, dtype):
         return _BUF_POOL.get(key, []).pop()
     except IndexError:
         pass
-    if kind == "z":
+    if kind.startswith("z"):
         return torch.zeros(n, dtype=dtype, device=device)
     return torch.empty(n, dtype=dtype, device=device)
 
@@ -265,7 +265,15 @@ class DecodeLaunch:
         # error word and the chunks' deferred-verdict words (the first 4 words
         # per chunk of the workspace, zarrhip.h) are one contiguous range, read
         # back with one copy after a launch
-        z = _pool_take("z", nw + 64 + nws + ni, device, torch.int32) if pooled else \
+        # pooled per region split, not per total size: after a clean launch the
+        # workspace is zero again (self-resetting) but the statuses are not, so
+        # a buffer may only go to a launch whose statuses and workspace sit at
+        # the same offsets -- there every status is rewritten, as on any
+        # relaunch of one program (a split-blind pool handed one program's
+        # statuses to another as verdict words: a false CRC mismatch, found by
+        # the rectilinear fuzz, tests/test_gpu_fuzz.py)
+        self._zkind = f"z:{nw}:{nws}:{ni}"
+        z = _pool_take(self._zkind, nw + 64 + nws + ni, device, torch.int32) if pooled else \
             torch.zeros(nw + 64 + nws + ni, dtype=torch.int32, device=device)
         self._z = z
         self._zl = (nw, nws, ni)
@@ -360,7 +368,7 @@ class DecodeLaunch:
             self._bufs = None
             if tb is not None:
                 _pool_give("t", tb)
-            _pool_give("z", z)
+            _pool_give(self._zkind, z)
 
     def statuses(self) -> np.ndarray:
         """Per-chunk statuses with the deferred CRC verdicts merged in: a
